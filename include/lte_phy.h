@@ -1,0 +1,143 @@
+/*
+ * lte_phy.h -- C ABI of liblte_hip.so, the gfx950 (MI355X) LTE PHY link engine.
+ *
+ * The reference (Darioxavierl/OFDM-LTE) is pure Python/NumPy and has no FFI;
+ * its drop-in boundary is the Python class API (ofdm_module.py:32-207,
+ * core/ofdm_core.py:42-2486).  This header is the native boundary underneath
+ * the Python mirror of that API (ofdm-lte_amd/lte_phy/): plain C, plain
+ * pointers and sizes, no torch or C++ types.  Each entry point names the
+ * reference function(s) whose work it replaces.
+ *
+ * Conventions: every function returns LTE_OK (0) or a negative LTE_E* code;
+ * lte_strerror() / lte_last_error() describe it.  Host buffers are owned by
+ * the caller; device memory is owned by the library (one plan = one device
+ * workspace).  All calls are synchronous at return.  One plan per thread.
+ */
+#ifndef LTE_PHY_H
+#define LTE_PHY_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  LTE_OK = 0,
+  LTE_EINVAL = -1,  /* bad argument (mirrors the reference's ValueError)      */
+  LTE_EHIP = -2,    /* HIP runtime / launch failure                             */
+  LTE_ENOMEM = -3,  /* device allocation failed                                 */
+  LTE_ENODEV = -4,  /* no gfx950 device                                         */
+  LTE_EUNSUP = -5   /* configuration outside what the GPU path implements       */
+};
+
+/* Chain kinds: which reference simulate_* method a plan runs. */
+enum {
+  LTE_CHAIN_UNCODED = 0, /* OFDMSimulator.simulate_siso      core/ofdm_core.py:660-737   */
+  LTE_CHAIN_CODED = 1,   /* OFDMSimulator.simulate_siso_coded core/ofdm_core.py:925-1338 */
+  LTE_CHAIN_SIMO = 2     /* OFDMSimulator.simulate_simo (MRC) core/ofdm_core.py:1536-1679 */
+};
+enum { LTE_CH_AWGN = 0, LTE_CH_RAYLEIGH = 1 }; /* core/channel.py:10-245 */
+
+#define LTE_MAX_PATHS 16
+
+/* Plan descriptor.  Numerology follows LTEConfig (config.py:101-130); the
+ * resource grid (guards, DC, pilot every 6th SC) is derived from N, Nc exactly
+ * as LTEResourceGrid (core/resource_mapper.py:57-93). */
+typedef struct {
+  int32_t N, Nc, cp_len;   /* FFT size, useful SCs, CP samples                   */
+  int32_t bps;             /* 2 / 4 / 6  (QPSK / 16-QAM / 64-QAM)                */
+  int32_t n_sym;           /* OFDM symbols per frame (uncoded/SIMO); coded: 0=auto */
+  int32_t chain;           /* LTE_CHAIN_*                                        */
+  int32_t channel;         /* LTE_CH_*                                           */
+  int32_t num_rx;          /* 1 for SISO, >=1 for SIMO                           */
+  int32_t n_paths;         /* Rayleigh taps                                      */
+  int32_t delays[LTE_MAX_PATHS]; /* integer sample delays round(tau*fs)          */
+  double gains[LTE_MAX_PATHS];   /* linear amplitudes as RayleighChannel holds them */
+  double fD;               /* max Doppler (Hz); 0 -> static taps                 */
+  double fs;               /* sample rate (Hz)                                   */
+  int32_t n_bits;          /* payload bits per frame (uncoded) / TB size (coded) */
+  int32_t turbo_iters;     /* coded: decoder iterations (reference passes 8)     */
+  int32_t max_frames;      /* workspace capacity (frames per lte_run call)       */
+  int32_t cell_id;         /* pilot PN seed (PilotPattern cell_id), normally 0   */
+} lte_plan_desc;
+
+typedef struct lte_plan lte_plan;
+
+/* Per-call arguments of lte_run.  Frame b (0 <= b < n_frames) is one
+ * independent (SNR, trial) unit.  Randomness: Philox4x32-10 keyed by
+ * (seed, frame_id, stream, index); any non-NULL inject pointer replaces the
+ * corresponding Philox draws (ref-compat mode: the host supplies the numbers
+ * the reference's global NumPy RNG would draw).  *_stride = elements between
+ * consecutive frames (0 = the same data broadcast to every frame). */
+typedef struct {
+  int32_t n_frames;
+  const float *snr_db;         /* host [n_frames]                                  */
+  const int32_t *snr_index;    /* host [n_frames] row in counts (NULL -> 0)        */
+  int32_t n_snr;               /* rows of counts                                   */
+  uint64_t seed;
+  const uint64_t *frame_ids;   /* host [n_frames] (NULL -> frame_id0 + b)          */
+  uint64_t frame_id0;
+  /* injection (host, optional) */
+  const uint8_t *bits; int64_t bits_stride;     /* [.][n_bits] values 0/1          */
+  const double *phases; int64_t phases_stride;  /* [.][num_rx][n_paths][16] rad    */
+  const double *noise; int64_t noise_stride;    /* [.][num_rx][2][L] unit normals  */
+  /* outputs */
+  uint64_t *counts;            /* host [n_snr][4] += {bit_err, bits, blk_err, blks} */
+  uint32_t *frame_errors;      /* host [n_frames] optional                         */
+  uint8_t *frame_crc_ok;       /* host [n_frames] optional (coded)                 */
+  /* captures (host, optional; used by the single-call Python API) */
+  float *cap_signal_tx;        /* [n_frames][L] complex64                           */
+  float *cap_signal_rx;        /* [n_frames][num_rx][L] complex64 (noisy)           */
+  float *cap_data_syms;        /* [n_frames][n_sym*Nd] complex64 (ZF or MRC output) */
+  float *cap_H;                /* [n_frames][num_rx][n_grp][N] complex64            */
+  float *cap_pilot_stats;      /* [n_frames][num_rx][n_grp][2] float (P, noise)     */
+  uint8_t *cap_bits_rx;        /* [n_frames][n_bits]                                */
+  float *cap_llr;              /* [n_frames][n_sym*Nd*bps] (coded, RE order)        */
+  float *cap_noise_power;      /* [n_frames][num_rx]                                */
+} lte_run_args;
+
+/* Library / device. */
+const char *lte_strerror(int code);
+const char *lte_last_error(void);
+int lte_device_init(int device);            /* select + check gfx950 */
+int lte_version(void);
+
+/* Plans. */
+int lte_plan_create(const lte_plan_desc *desc, lte_plan **out);
+int lte_plan_destroy(lte_plan *plan);
+/* Geometry derived by the plan: [L, n_sym, Nd, Np, n_grp, n_cb, coded_bits, n_re_bits] */
+int lte_plan_info(const lte_plan *plan, int64_t *info8);
+/* Run the full chain (TX -> channel -> RX (-> turbo)) for one batch of frames. */
+int lte_run(lte_plan *plan, const lte_run_args *args);
+/* Per-kernel device time accumulated by lte_run while timing is on (HIP events
+ * on the plan's stream).  names: comma-separated kernel names; ms/launches per
+ * kernel in the same order.  n_max entries. */
+int lte_timing_enable(lte_plan *plan, int on);
+int lte_timing_read(lte_plan *plan, char *names, int names_len, double *ms, int64_t *launches, int n_max);
+int lte_timing_reset(lte_plan *plan);
+
+/* ---- stage entry points (parity tests; host in/out, same device kernels) ---- */
+/* IFFT*sqrt(N) / FFT/sqrt(N): core/modulator.py:242 / core/lte_receiver.py:487 */
+int lte_fft_host(int N, int inverse, int64_t batch, const float *in, float *out);
+/* Pilots: PilotPattern.generate_pilots core/resource_mapper.py:137-152 (MT19937 seed(cell_id) + choice([1,-1])) */
+int lte_pilots(int cell_id, int n, double *out_re_im);
+/* Soft demap: _calculate_llrs_* core/ofdm_core.py:791-923 (bps 2/4/6) */
+int lte_llr_host(int bps, int64_t n, const float *syms, const float *noise_var, float *llr);
+/* Hard decision: QAMModulator.symbols_to_bits core/modulator.py:90-112 */
+int lte_hard_host(int bps, int64_t n, const float *syms, uint8_t *bits);
+/* Turbo encode: turbo_encode core/channel_coding/turbo_encoder.py:214-313 */
+int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t *bits, uint8_t *out /*[ncb][3K+12]*/);
+/* Turbo decode: turbo_decode core/channel_coding/turbo_decoder.py:338-450 */
+int lte_turbo_decode_host(int K, int iters, int64_t ncb, const float *llr /*[ncb][3K+12]*/, uint8_t *bits);
+/* One max-log BCJR pass, a-posteriori output: LogMAPDecoder.decode turbo_decoder.py:181-278 */
+int lte_bcjr_host(int K, int64_t ncb, const float *ls, const float *lp, const float *la, float *app);
+/* CRC: _calculate_crc core/channel_coding/crc.py:89-134 (MSB-first, zero init) */
+int lte_crc_host(int64_t n, const uint8_t *bits, uint32_t poly, int len, uint32_t *crc);
+/* Rate dematching map: rate_dematching_turbo core/channel_coding/rate_matching.py:374-489
+ * src[j] = index into the E rate-matched LLRs feeding output j of [3K+12], -1 = zero. */
+int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t *src);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LTE_PHY_H */

@@ -1,0 +1,1123 @@
+// C ABI of liblte_hip.so (include/lte_phy.h): plan construction (all index /
+// permutation tables are built here, natively, once per configuration),
+// device workspace ownership, and orchestration of the kernel chain on the
+// plan's HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lte_common.h"
+#include "lte_internal.h"
+
+using namespace lte;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(LTE_EHIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+#define LCHK(expr)                                                                           \
+  do {                                                                                       \
+    int _e = (expr);                                                                         \
+    if (_e != 0) return fail(LTE_EHIP, std::string(#expr ": ") + hipGetErrorString((hipError_t)_e)); \
+  } while (0)
+
+// ------------------------------------------------------------------ MT19937
+// NumPy legacy RandomState: seed(s) = init_genrand(s); choice([1,-1], n) =
+// randint(0, 2, n) = (next_uint32 & 1) per draw (masked bounded ints).
+struct MT19937 {
+  uint32_t mt[624];
+  int idx;
+  explicit MT19937(uint32_t s) {
+    mt[0] = s;
+    for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    idx = 624;
+  }
+  uint32_t next() {
+    if (idx >= 624) {
+      for (int i = 0; i < 624; ++i) {
+        const uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+        mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      idx = 0;
+    }
+    uint32_t y = mt[idx++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+};
+
+// QPP table (3GPP TS 36.212 Table 5.1.3-3; turbo_encoder.py:34-73)
+const int QPP_TAB[][3] = {
+    {40, 3, 10}, {48, 7, 12}, {56, 19, 42}, {64, 7, 16}, {72, 7, 18}, {80, 11, 20}, {88, 5, 22}, {96, 11, 24},
+    {104, 7, 26}, {112, 41, 84}, {120, 103, 90}, {128, 15, 32}, {136, 9, 34}, {144, 17, 108}, {152, 9, 38},
+    {160, 21, 120}, {168, 101, 84}, {176, 21, 44}, {184, 57, 46}, {192, 23, 48}, {200, 13, 50}, {208, 27, 52},
+    {216, 11, 36}, {224, 27, 56}, {232, 85, 58}, {240, 29, 60}, {248, 33, 62}, {256, 15, 32}, {264, 17, 198},
+    {272, 33, 68}, {280, 103, 210}, {288, 19, 36}, {296, 19, 74}, {304, 37, 76}, {312, 19, 78}, {320, 21, 120},
+    {328, 21, 82}, {336, 115, 84}, {344, 193, 86}, {352, 21, 44}, {360, 133, 90}, {368, 81, 46}, {376, 45, 94},
+    {384, 23, 48}, {392, 243, 98}, {400, 151, 40}, {408, 155, 102}, {416, 25, 52}, {424, 51, 106}, {432, 47, 72},
+    {440, 91, 110}, {448, 29, 168}, {456, 29, 114}, {464, 247, 58}, {472, 29, 118}, {480, 89, 180},
+    {488, 91, 122}, {496, 157, 62}, {504, 55, 84}, {512, 31, 64}, {528, 17, 66}, {544, 35, 68}, {560, 227, 420},
+    {576, 65, 96}, {592, 19, 74}, {608, 37, 76}, {624, 41, 234}, {640, 39, 80}, {656, 185, 82}, {672, 43, 252},
+    {688, 21, 86}, {704, 155, 44}, {720, 79, 120}, {736, 139, 92}, {752, 23, 94}, {768, 217, 48}, {784, 25, 98},
+    {800, 17, 80}, {816, 127, 102}, {832, 25, 52}, {848, 239, 106}, {864, 17, 48}, {880, 137, 110},
+    {896, 215, 112}, {912, 29, 114}, {928, 15, 58}, {944, 147, 118}, {960, 29, 60}, {976, 59, 122},
+    {992, 65, 124}, {1008, 55, 84}, {1024, 31, 64}, {1056, 17, 66}, {1088, 171, 204}, {1120, 67, 140},
+    {1152, 35, 72}, {1184, 19, 74}, {1216, 39, 76}, {1248, 19, 78}, {1280, 199, 240}, {1312, 21, 82},
+    {1344, 211, 252}, {1376, 21, 86}, {1408, 43, 88}, {1440, 149, 60}, {1472, 45, 92}, {1504, 49, 846},
+    {1536, 71, 48}, {1568, 13, 28}, {1600, 17, 80}, {1632, 25, 102}, {1664, 183, 104}, {1696, 55, 954},
+    {1728, 127, 96}, {1760, 27, 110}, {1792, 29, 112}, {1824, 29, 114}, {1856, 57, 116}, {1888, 45, 354},
+    {1920, 31, 120}, {1952, 59, 610}, {1984, 185, 124}, {2016, 113, 420}, {2048, 31, 64}, {2112, 17, 66},
+    {2176, 171, 136}, {2240, 209, 420}, {2304, 253, 216}, {2368, 367, 444}, {2432, 265, 456}, {2496, 181, 468},
+    {2560, 39, 80}, {2624, 27, 164}, {2688, 127, 504}, {2752, 143, 172}, {2816, 43, 88}, {2880, 29, 300},
+    {2944, 45, 92}, {3008, 157, 188}, {3072, 47, 96}, {3136, 13, 28}, {3200, 111, 240}, {3264, 443, 204},
+    {3328, 51, 104}, {3392, 51, 212}, {3456, 451, 192}, {3520, 257, 220}, {3584, 57, 336}, {3648, 313, 228},
+    {3712, 271, 232}, {3776, 179, 236}, {3840, 331, 120}, {3904, 363, 244}, {3968, 375, 248}, {4032, 127, 168},
+    {4096, 31, 64}, {4160, 33, 130}, {4224, 43, 264}, {4288, 33, 134}, {4352, 477, 408}, {4416, 35, 138},
+    {4480, 233, 280}, {4544, 357, 142}, {4608, 337, 480}, {4672, 37, 146}, {4736, 71, 444}, {4800, 71, 120},
+    {4864, 37, 152}, {4928, 39, 462}, {4992, 127, 234}, {5056, 39, 158}, {5120, 39, 80}, {5184, 31, 96},
+    {5248, 113, 902}, {5312, 41, 166}, {5376, 251, 336}, {5440, 43, 170}, {5504, 21, 86}, {5568, 43, 174},
+    {5632, 45, 176}, {5696, 45, 178}, {5760, 161, 120}, {5824, 89, 182}, {5888, 323, 184}, {5952, 47, 186},
+    {6016, 23, 94}, {6080, 47, 190}, {6144, 263, 480}};
+const int N_QPP = sizeof(QPP_TAB) / sizeof(QPP_TAB[0]);
+
+bool qpp_lookup(int K, int* f1, int* f2) {
+  for (int i = 0; i < N_QPP; ++i)
+    if (QPP_TAB[i][0] == K) { *f1 = QPP_TAB[i][1]; *f2 = QPP_TAB[i][2]; return true; }
+  return false;
+}
+
+int find_interleaver_size(int n) {  // segmentation.py:53-71
+  for (int i = 0; i < N_QPP; ++i)
+    if (QPP_TAB[i][0] >= n) return QPP_TAB[i][0];
+  return -1;
+}
+
+// segment_code_blocks (segmentation.py:74-263) as a table of CB slots.
+bool segmentation_plan(int B, std::vector<CbInfo>& out) {
+  const int Z = 6144;
+  out.clear();
+  if (B <= Z) {
+    const int K = find_interleaver_size(B);
+    if (K < 0) return false;
+    CbInfo c{K, K - B, B, 0, 0, 0, 0, 3 * K + 12};
+    qpp_lookup(K, &c.f1, &c.f2);
+    out.push_back(c);
+    return true;
+  }
+  const int L = 24;
+  const int C = (B + (Z - L) - 1) / (Z - L);
+  const int Bp = B + C * L;
+  const int Kp = find_interleaver_size((Bp + C - 1) / C);
+  if (Kp < 0) return false;
+  int ki = 0;
+  while (QPP_TAB[ki][0] != Kp) ++ki;
+  const int Km = ki > 0 ? QPP_TAB[ki - 1][0] : Kp;
+  const int dK = Kp - Km;
+  const int Cm = dK > 0 ? (C * Kp - Bp) / dK : 0;
+  int rem = B, off = 0;
+  for (int r = 0; r < C; ++r) {
+    const int K = r < Cm ? Km : Kp;
+    const int avail = K - L;
+    const int info = (r == C - 1) ? rem : std::min(avail, rem / (C - r));
+    rem -= info;
+    CbInfo c{K, (K - L) - info, info, off, 1, 0, 0, 3 * K + 12};
+    qpp_lookup(K, &c.f1, &c.f2);
+    out.push_back(c);
+    off += info;
+  }
+  return true;
+}
+
+const int SBI_P[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+                       1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
+
+// sub_block_interleaver index map (rate_matching.py:25-94): v[i] = d[perm[i]]
+std::vector<int> subblock_perm(int n) {
+  const int R = (n + 31) / 32;
+  std::vector<int> p;
+  p.reserve(n);
+  for (int row = 0; row < R; ++row)
+    for (int j = 0; j < 32; ++j) {
+      const int idx = SBI_P[j] * R + row;
+      if (idx < n) p.push_back(idx);
+    }
+  return p;
+}
+
+// Where coded bit i of CB (K, rv) comes from: stream (0/1/2) and index in that
+// stream, or stream -1 (padding of v1/v2).  rate_matching.py:249-297.
+struct RmSrc { int stream, idx; };
+void rm_source(int K, int rv, int E, std::vector<RmSrc>& out) {
+  const int ml = K + 6, Ncb = 3 * ml;
+  const int starts[4] = {0, Ncb / 4, Ncb / 2, 3 * Ncb / 4};
+  const int st = starts[rv & 3];
+  const std::vector<int> p0 = subblock_perm(K + 6), p1 = subblock_perm(K + 3);
+  out.resize(E);
+  for (int i = 0; i < E; ++i) {
+    const int c = (st + i) % Ncb;
+    const int s = c % 3, v = c / 3;
+    if (s == 0) out[i] = {0, p0[v]};
+    else if (v < K + 3) out[i] = {s, p1[v]};
+    else out[i] = {-1, 0};
+  }
+}
+
+// ------------------------------------------------------------------ buffers
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int alloc(size_t count) {
+    if (count <= n && p) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (count == 0) return 0;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) return -1;
+    n = count;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+int ilog2(int n) {
+  int l = 0;
+  while ((1 << l) < n) ++l;
+  return l;
+}
+
+struct GridHost {
+  int N, Nc, cp, Nd, Np;
+  std::vector<int32_t> data, pilot, seg;
+  std::vector<float> inv_gap;
+};
+
+// LTEResourceGrid._init_subcarrier_types (resource_mapper.py:57-93)
+GridHost make_grid(int N, int Nc, int cp) {
+  GridHost g;
+  g.N = N; g.Nc = Nc; g.cp = cp;
+  const int gl = (N - Nc) / 2, gr = N - Nc - gl, dc = N / 2;
+  for (int k = 0; k < N; ++k) {
+    if (k < gl || k >= N - gr) continue;
+    if (k == dc) continue;
+    if (((k - gl) % 6) == 3) g.pilot.push_back(k);
+    else g.data.push_back(k);
+  }
+  g.Nd = (int)g.data.size();
+  g.Np = (int)g.pilot.size();
+  g.seg.assign(N, -1);
+  int s = -1;
+  for (int k = 0; k < N; ++k) {
+    while (s + 1 < g.Np && g.pilot[s + 1] <= k) ++s;
+    g.seg[k] = s;
+  }
+  g.inv_gap.assign(std::max(g.Np, 1), 0.f);
+  for (int i = 0; i + 1 < g.Np; ++i) g.inv_gap[i] = (float)(1.0 * (1.0 / (g.pilot[i + 1] - g.pilot[i])));
+  return g;
+}
+
+std::vector<float2> make_constellation(int bps) {  // modulator.py:28-59
+  std::vector<float2> c;
+  if (bps == 2) {
+    const double s = 1.0 / std::sqrt(2.0);
+    c = {make_float2(s, s), make_float2(s, -s), make_float2(-s, s), make_float2(-s, -s)};
+    return c;
+  }
+  const int nl = 1 << (bps / 2);
+  const double sc = bps == 4 ? std::sqrt(10.0) : std::sqrt(42.0);
+  for (int i = 0; i < nl; ++i)
+    for (int q = 0; q < nl; ++q)
+      c.push_back(make_float2((float)((2 * i - (nl - 1)) / sc), (float)((2 * q - (nl - 1)) / sc)));
+  return c;
+}
+
+std::vector<float2> make_twiddles(int N) {
+  std::vector<float2> t(N);
+  for (int k = 0; k < N; ++k) {
+    const double a = -2.0 * M_PI * (double)k / (double)N;
+    t[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  return t;
+}
+
+void make_pilots(int cell, int n, std::vector<double>& re_im) {
+  MT19937 mt((uint32_t)cell);
+  re_im.resize(2 * (size_t)n);
+  const double v = 1.0 / std::sqrt(2.0);
+  for (int i = 0; i < n; ++i) {
+    const double s = (mt.next() & 1u) ? -1.0 : 1.0;
+    re_im[2 * i] = v * s;
+    re_im[2 * i + 1] = v * s;
+  }
+}
+
+struct TableSet {  // device copies of the static grid tables for one N
+  DBuf<int32_t> data, pilot, seg;
+  DBuf<float> inv_gap;
+  DBuf<float2> pilots, tw, constel;
+  void release() {
+    data.release(); pilot.release(); seg.release(); inv_gap.release(); pilots.release(); tw.release();
+    constel.release();
+  }
+};
+
+template <class T>
+int upload(DBuf<T>& d, const std::vector<T>& h) {
+  if (d.alloc(std::max<size_t>(h.size(), 1))) return -1;
+  if (!h.empty() && hipMemcpy(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  return 0;
+}
+
+const char* KNAMES[] = {"payload", "encode", "ofdm_tx", "fading", "channel", "rx_chest", "rx_data",
+                        "dematch", "turbo",   "crc_count", "accumulate", "capture"};
+enum { KN_PAYLOAD, KN_ENCODE, KN_OFDM_TX, KN_FADING, KN_CHANNEL, KN_RX_CHEST, KN_RX_DATA, KN_DEMATCH, KN_TURBO,
+       KN_CRC, KN_ACC, KN_CAP, KN_COUNT };
+
+}  // namespace
+
+// ------------------------------------------------------------------ capture kernel
+namespace lte {
+__global__ void k_cap_rx(int L, int num_rx, int B, const float2* __restrict__ y, int64_t y_rx_stride,
+                         int64_t y_frame_stride, const float* __restrict__ npow, const uint64_t* __restrict__ fid,
+                         uint64_t seed, const float* __restrict__ inj_z, int64_t inj_stride, float2* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int rx = blockIdx.y, b = blockIdx.z;
+  if (n >= L) return;
+  const float sigma = sqrtf(npow[(size_t)b * num_rx + rx] * 0.5f);
+  float2 z;
+  if (inj_z) {
+    const float* zf = inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * L;
+    z = make_float2(zf[n], zf[L + n]);
+  } else {
+    const u32x4 r = rng4(seed, fid[b], RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)(n >> 1));
+    z = (n & 1) ? box_muller(r.z, r.w) : box_muller(r.x, r.y);
+  }
+  const float2 v = y[b * y_frame_stride + rx * y_rx_stride + n];
+  out[((size_t)b * num_rx + rx) * L + n] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+}
+}  // namespace lte
+
+struct lte_plan {
+  lte_plan_desc d;
+  int L, n_sym, Nd, Np, n_grp, nblk, PW, C = 0, KWmax = 0, EW = 0, enc_words = 0;
+  int coded_len = 0, n_re_bits = 0;
+  int log2N;
+  GridHost gh;
+  TableSet tabs;
+  Grid grid;
+  hipStream_t stream = nullptr;
+  std::vector<CbInfo> cbs;
+  std::vector<float> gains_f;
+  // device
+  DBuf<CbInfo> cbi;
+  DBuf<int32_t> tx_map, rx_map, delays;
+  DBuf<float> gains;
+  DBuf<uint32_t> pw, cbw, enc, inj_bits;
+  DBuf<float2> x, y, coef, H, capbuf;
+  DBuf<float> phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
+  DBuf<uint32_t> frame_err, frame_crc;
+  DBuf<int32_t> snr_idx;
+  DBuf<uint64_t> fid;
+  DBuf<unsigned long long> counts;
+  DBuf<uint8_t> cap_bits;
+  std::vector<DBuf<float>> blk, ckpt;
+  std::vector<DBuf<uint32_t>> decb;
+  DBuf<float*> blk_ptrs;
+  DBuf<int64_t> rows_dev;
+  DBuf<uint32_t*> dec_ptrs;
+  DBuf<int> kw_dev;
+  // timing
+  bool timing = false;
+  double kms[KN_COUNT] = {0};
+  int64_t klaunch[KN_COUNT] = {0};
+  std::vector<hipEvent_t> evpool;
+  std::vector<std::pair<int, int>> evuse;  // (kernel id, first event index)
+};
+
+namespace {
+
+struct Timer {  // brackets one launch with events when timing is on
+  lte_plan* p;
+  int id, e0;
+  Timer(lte_plan* pl, int kid) : p(pl), id(kid), e0(-1) {
+    if (!p->timing) return;
+    e0 = (int)p->evuse.size() * 2;
+    if ((int)p->evpool.size() < e0 + 2) {
+      hipEvent_t a, b;
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      p->evpool.push_back(a);
+      p->evpool.push_back(b);
+    }
+    (void)hipEventRecord(p->evpool[e0], p->stream);
+  }
+  ~Timer() {
+    if (e0 < 0) return;
+    (void)hipEventRecord(p->evpool[e0 + 1], p->stream);
+    p->evuse.push_back({id, e0});
+  }
+};
+
+void collect_timing(lte_plan* p) {
+  for (auto& u : p->evuse) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p->evpool[u.second], p->evpool[u.second + 1]) == hipSuccess) {
+      p->kms[u.first] += ms;
+      p->klaunch[u.first] += 1;
+    }
+  }
+  p->evuse.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+int lte_version(void) { return 1; }
+
+const char* lte_last_error(void) { return g_err.c_str(); }
+
+const char* lte_strerror(int code) {
+  switch (code) {
+    case LTE_OK: return "ok";
+    case LTE_EINVAL: return "invalid argument";
+    case LTE_EHIP: return "HIP runtime error";
+    case LTE_ENOMEM: return "device out of memory";
+    case LTE_ENODEV: return "no gfx950 device";
+    case LTE_EUNSUP: return "unsupported configuration";
+    default: return "unknown error";
+  }
+}
+
+int lte_device_init(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(LTE_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(LTE_EINVAL, "device index out of range");
+  HIPCHK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(LTE_ENODEV, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
+  return LTE_OK;
+}
+
+int lte_pilots(int cell_id, int n, double* out) {
+  if (n < 0 || !out) return fail(LTE_EINVAL, "bad pilot request");
+  std::vector<double> v;
+  make_pilots(cell_id, n, v);
+  std::memcpy(out, v.data(), v.size() * sizeof(double));
+  return LTE_OK;
+}
+
+int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t* src) {
+  int f1, f2;
+  if (!qpp_lookup(K, &f1, &f2)) return fail(LTE_EINVAL, "Invalid interleaver size K=" + std::to_string(K));
+  if (E <= 0 || !src) return fail(LTE_EINVAL, "bad E");
+  std::vector<RmSrc> rs;
+  rm_source(K, rv_idx, E, rs);
+  const int n = 3 * K + 12;
+  for (int j = 0; j < n; ++j) src[j] = -1;
+  for (int i = 0; i < E; ++i) {
+    const RmSrc s = rs[i];
+    if (s.stream < 0) continue;
+    int j;
+    if (s.stream == 0) {
+      if (s.idx < K) j = 3 * s.idx;
+      else if (s.idx < K + 3) j = 3 * K + (s.idx - K);
+      else j = 3 * K + 6 + (s.idx - K - 3);
+    } else if (s.stream == 1) {
+      j = s.idx < K ? 3 * s.idx + 1 : 3 * K + 3 + (s.idx - K);
+    } else {
+      j = s.idx < K ? 3 * s.idx + 2 : 3 * K + 9 + (s.idx - K);
+    }
+    if (src[j] >= 0) return fail(LTE_EUNSUP, "rate-dematch repetition (E > N_cb) not supported by the map form");
+    src[j] = i;
+  }
+  return LTE_OK;
+}
+
+static int plan_tables(lte_plan* p) {
+  const lte_plan_desc& d = p->d;
+  p->gh = make_grid(d.N, d.Nc, d.cp_len);
+  p->Nd = p->gh.Nd;
+  p->Np = p->gh.Np;
+  p->log2N = ilog2(d.N);
+  std::vector<double> pr;
+  make_pilots(d.cell_id, p->Np, pr);
+  std::vector<float2> pil(p->Np);
+  for (int i = 0; i < p->Np; ++i) pil[i] = make_float2((float)pr[2 * i], (float)pr[2 * i + 1]);
+  if (upload(p->tabs.data, p->gh.data) || upload(p->tabs.pilot, p->gh.pilot) || upload(p->tabs.seg, p->gh.seg) ||
+      upload(p->tabs.inv_gap, p->gh.inv_gap) || upload(p->tabs.pilots, pil) ||
+      upload(p->tabs.tw, make_twiddles(d.N)) || upload(p->tabs.constel, make_constellation(d.bps)))
+    return fail(LTE_ENOMEM, "table upload failed");
+  return LTE_OK;
+}
+
+static int plan_coded_maps(lte_plan* p) {
+  const lte_plan_desc& d = p->d;
+  if (!segmentation_plan(d.n_bits + 24, p->cbs)) return fail(LTE_EINVAL, "No valid interleaver size");
+  p->C = (int)p->cbs.size();
+  int Kmax = 0;
+  std::vector<int> Eoff(p->C + 1, 0);
+  for (int r = 0; r < p->C; ++r) {
+    Kmax = std::max(Kmax, p->cbs[r].K);
+    Eoff[r + 1] = Eoff[r] + p->cbs[r].E;
+  }
+  p->coded_len = Eoff[p->C];
+  p->KWmax = (Kmax + 31) / 32 + 1;
+  p->EW = (Kmax + 6 + 31) / 32;
+  p->enc_words = p->C * 3 * p->EW;
+  const int bps = d.bps, Nd = p->Nd;
+  const int ncs_tx = (p->coded_len + bps - 1) / bps;  // bits_to_symbols pads (modulator.py:74-75)
+  const int rows = (ncs_tx + Nd - 1) / Nd;
+  p->n_sym = rows;
+  const int ncs_rx = p->coded_len / bps;               // ofdm_core.py:1140
+  const int rows_rx = (ncs_rx + Nd - 1) / Nd;
+  const int n_re = p->n_sym * Nd;
+  p->n_re_bits = n_re * bps;
+  std::vector<std::vector<RmSrc>> rs(p->C);
+  for (int r = 0; r < p->C; ++r) rm_source(p->cbs[r].K, 0, p->cbs[r].E, rs[r]);
+  auto locate = [&](int e, int& r, int& i) {
+    r = 0;
+    while (e >= Eoff[r + 1]) ++r;
+    i = e - Eoff[r];
+  };
+  std::vector<int32_t> txm(p->n_re_bits), rxm(p->n_re_bits);
+  for (int re = 0; re < n_re; ++re) {
+    // TX: interleaved position re <- padded coded symbol q (ofdm_core.py:1046-1060)
+    const int c = re / rows, rr = re % rows;
+    const int q = rr * Nd + c;
+    for (int m = 0; m < bps; ++m) {
+      int32_t v;
+      if (q >= ncs_tx) v = -2;
+      else {
+        const int e = q * bps + m;
+        if (e >= p->coded_len) v = -1;
+        else {
+          int r, i;
+          locate(e, r, i);
+          const RmSrc s = rs[r][i];
+          v = s.stream < 0 ? -1 : ((r * 3 + s.stream) * p->EW) * 32 + s.idx;
+        }
+      }
+      txm[(size_t)re * bps + m] = v;
+    }
+    // RX: de-interleave (ofdm_core.py:1176-1197) then rate dematch rows
+    int32_t base = -1;
+    int qr = -1;
+    if (re < rows_rx * Nd) {
+      const int c2 = re / rows_rx, r2 = re % rows_rx;
+      qr = r2 * Nd + c2;
+      if (qr >= ncs_rx) qr = -1;
+    }
+    for (int m = 0; m < bps; ++m) {
+      int32_t v = -1;
+      if (qr >= 0) {
+        const int e = qr * bps + m;
+        if (e < p->coded_len) {
+          int r, i;
+          locate(e, r, i);
+          const int K = p->cbs[r].K;
+          const RmSrc s = rs[r][i];
+          int row = -1;
+          if (s.stream == 0) row = s.idx < K + 3 ? s.idx : 3 * K + 9 + (s.idx - K - 3);
+          else if (s.stream == 1) row = K + 3 + s.idx;
+          else if (s.stream == 2) row = 2 * K + 6 + s.idx;
+          if (row >= 0) v = (r << 24) | row;
+        }
+      }
+      rxm[(size_t)re * bps + m] = v;
+      (void)base;
+    }
+  }
+  for (int r = 0; r < p->C; ++r)
+    if (p->cbs[r].E > 3 * (p->cbs[r].K + 6)) return fail(LTE_EUNSUP, "rate-matching repetition not supported");
+  if (upload(p->tx_map, txm) || upload(p->rx_map, rxm) || upload(p->cbi, p->cbs))
+    return fail(LTE_ENOMEM, "map upload failed");
+  return LTE_OK;
+}
+
+static int plan_alloc(lte_plan* p) {
+  const lte_plan_desc& d = p->d;
+  const size_t B = (size_t)d.max_frames;
+  const int G = (int)((B + 63) / 64);
+  const int rx = d.num_rx;
+  const bool ray = d.channel == LTE_CH_RAYLEIGH;
+  const bool coded = d.chain == LTE_CHAIN_CODED;
+  bool bad = false;
+  bad |= p->pw.alloc(B * p->PW) != 0;
+  bad |= p->x.alloc(B * p->L) != 0;
+  if (ray) {
+    bad |= p->y.alloc(B * rx * p->L) != 0;
+    bad |= p->phases.alloc(std::max<size_t>(B * rx * d.n_paths * 16, 1)) != 0;
+    bad |= p->coef.alloc(std::max<size_t>(B * rx * d.n_paths, 1)) != 0;
+  }
+  bad |= p->pow_part.alloc(B * rx * p->nblk) != 0;
+  bad |= p->H.alloc(B * rx * p->n_grp * d.N) != 0;
+  bad |= p->pstats.alloc(B * rx * p->n_grp * 2) != 0;
+  bad |= p->npow.alloc(B * rx) != 0;
+  bad |= p->snr_lin.alloc(B) != 0;
+  bad |= p->snr_idx.alloc(B) != 0;
+  bad |= p->fid.alloc(B) != 0;
+  bad |= p->frame_err.alloc(B) != 0;
+  bad |= p->frame_crc.alloc(B) != 0;
+  if (coded) {
+    bad |= p->cbw.alloc(B * p->C * p->KWmax) != 0;
+    bad |= p->enc.alloc(B * p->enc_words) != 0;
+    bad |= p->llr.alloc(B * p->n_re_bits) != 0;
+    p->blk.resize(p->C);
+    p->ckpt.resize(p->C);
+    p->decb.resize(p->C);
+    std::vector<float*> bp(p->C);
+    std::vector<int64_t> rows(p->C);
+    std::vector<uint32_t*> dp(p->C);
+    std::vector<int> kw(p->C);
+    for (int r = 0; r < p->C; ++r) {
+      const int K = p->cbs[r].K;
+      rows[r] = turbo_rows(K);
+      bad |= p->blk[r].alloc((size_t)G * rows[r] * 64) != 0;
+      bad |= p->ckpt[r].alloc((size_t)G * turbo_nwin(K) * 8 * 64) != 0;
+      kw[r] = turbo_kw(K);
+      bad |= p->decb[r].alloc((size_t)G * kw[r] * 64) != 0;
+      if (!bad) HIPCHK(hipMemset(p->blk[r].p, 0, p->blk[r].n * sizeof(float)));
+      bp[r] = p->blk[r].p;
+      dp[r] = p->decb[r].p;
+    }
+    if (!bad) bad |= upload(p->blk_ptrs, bp) || upload(p->rows_dev, rows) || upload(p->dec_ptrs, dp) ||
+                     upload(p->kw_dev, kw);
+  }
+  if (bad) return fail(LTE_ENOMEM, "device workspace allocation failed (max_frames too large?)");
+  return LTE_OK;
+}
+
+int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
+  if (!desc || !out) return fail(LTE_EINVAL, "null argument");
+  const lte_plan_desc& d = *desc;
+  if (d.N < 128 || d.N > 2048 || (d.N & (d.N - 1))) return fail(LTE_EUNSUP, "N must be a power of two in [128, 2048]");
+  if (d.Nc <= 0 || d.Nc >= d.N || d.cp_len < 0 || d.cp_len > d.N) return fail(LTE_EINVAL, "bad Nc / cp_len");
+  if (d.bps != 2 && d.bps != 4 && d.bps != 6) return fail(LTE_EINVAL, "Unsupported modulation");
+  if (d.chain < 0 || d.chain > 2) return fail(LTE_EINVAL, "bad chain");
+  if (d.channel != LTE_CH_AWGN && d.channel != LTE_CH_RAYLEIGH) return fail(LTE_EINVAL, "Tipo de canal desconocido");
+  if (d.num_rx < 1 || d.num_rx > 16) return fail(LTE_EINVAL, "num_rx must be >= 1");
+  if (d.chain != LTE_CHAIN_SIMO && d.num_rx != 1) return fail(LTE_EINVAL, "SISO chains need num_rx == 1");
+  if (d.channel == LTE_CH_RAYLEIGH && (d.n_paths < 1 || d.n_paths > LTE_MAX_PATHS))
+    return fail(LTE_EINVAL, "bad n_paths");
+  if (d.max_frames < 1) return fail(LTE_EINVAL, "max_frames must be >= 1");
+  if (d.n_bits < 1) return fail(LTE_EINVAL, "Bits array cannot be empty");
+  lte_plan* p = new lte_plan();
+  p->d = d;
+  if (d.chain == LTE_CHAIN_CODED && d.turbo_iters < 0) { delete p; return fail(LTE_EINVAL, "bad turbo_iters"); }
+  int rc = plan_tables(p);
+  if (rc) { delete p; return rc; }
+  // Nd < N/2 is assumed by k_rx_data (4 data REs per thread)
+  if (p->Nd * 2 >= d.N) { delete p; return fail(LTE_EUNSUP, "Nd >= N/2 not supported"); }
+  if (d.chain == LTE_CHAIN_CODED) {
+    rc = plan_coded_maps(p);
+    if (rc) { p->tabs.release(); delete p; return rc; }
+    p->PW = (d.n_bits + 24 + 31) / 32 + 1;
+  } else {
+    if (d.n_sym < 1) { delete p; return fail(LTE_EINVAL, "n_sym must be >= 1"); }
+    p->n_sym = d.n_sym;
+    if ((int64_t)d.n_bits > (int64_t)p->n_sym * p->Nd * d.bps) { delete p; return fail(LTE_EINVAL, "n_bits exceeds frame capacity"); }
+    p->PW = (p->n_sym * p->Nd * d.bps + 31) / 32 + 1;
+  }
+  p->L = p->n_sym * (d.N + d.cp_len);
+  p->n_grp = (p->n_sym + 13) / 14;
+  p->nblk = (p->L + 255) / 256;
+  p->grid = Grid{d.N, p->log2N, d.Nc, d.cp_len, p->Nd, p->Np, d.bps, p->n_sym, p->L, p->n_grp,
+                 p->tabs.data.p, p->tabs.pilot.p, p->tabs.pilots.p, p->tabs.seg.p, p->tabs.inv_gap.p,
+                 p->tabs.tw.p, p->tabs.constel.p,
+                 (float)(d.bps == 2 ? std::sqrt(2.0) : d.bps == 4 ? std::sqrt(10.0) : std::sqrt(42.0))};
+  if (d.channel == LTE_CH_RAYLEIGH) {
+    std::vector<int32_t> dl(d.delays, d.delays + d.n_paths);
+    p->gains_f.assign(d.n_paths, 0.f);
+    for (int i = 0; i < d.n_paths; ++i) {
+      if (dl[i] < 0) { delete p; return fail(LTE_EINVAL, "negative delay"); }
+      p->gains_f[i] = (float)d.gains[i];
+    }
+    if (upload(p->delays, dl) || upload(p->gains, p->gains_f)) { delete p; return fail(LTE_ENOMEM, "upload"); }
+  }
+  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete p;
+    return fail(LTE_EHIP, "stream creation failed");
+  }
+  rc = plan_alloc(p);
+  if (rc) { lte_plan_destroy(p); return rc; }
+  if (p->counts.alloc(4 * 64)) { lte_plan_destroy(p); return fail(LTE_ENOMEM, "counts"); }
+  *out = p;
+  return LTE_OK;
+}
+
+int lte_plan_destroy(lte_plan* p) {
+  if (!p) return LTE_OK;
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  p->tabs.release();
+  p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release(); p->gains.release();
+  p->pw.release(); p->cbw.release(); p->enc.release(); p->inj_bits.release();
+  p->x.release(); p->y.release(); p->coef.release(); p->H.release(); p->capbuf.release();
+  p->phases.release(); p->pow_part.release(); p->pstats.release(); p->npow.release(); p->llr.release();
+  p->snr_lin.release(); p->inj_ph.release(); p->inj_z.release();
+  p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->fid.release(); p->counts.release();
+  p->cap_bits.release();
+  for (auto& b : p->blk) b.release();
+  for (auto& b : p->ckpt) b.release();
+  for (auto& b : p->decb) b.release();
+  p->blk_ptrs.release(); p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
+  for (auto e : p->evpool) (void)hipEventDestroy(e);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+  return LTE_OK;
+}
+
+int lte_plan_info(const lte_plan* p, int64_t* info) {
+  if (!p || !info) return fail(LTE_EINVAL, "null argument");
+  info[0] = p->L; info[1] = p->n_sym; info[2] = p->Nd; info[3] = p->Np;
+  info[4] = p->n_grp; info[5] = p->C; info[6] = p->coded_len; info[7] = p->n_re_bits;
+  return LTE_OK;
+}
+
+int lte_timing_enable(lte_plan* p, int on) {
+  if (!p) return fail(LTE_EINVAL, "null plan");
+  p->timing = on != 0;
+  return LTE_OK;
+}
+
+int lte_timing_reset(lte_plan* p) {
+  if (!p) return fail(LTE_EINVAL, "null plan");
+  for (int i = 0; i < KN_COUNT; ++i) { p->kms[i] = 0; p->klaunch[i] = 0; }
+  return LTE_OK;
+}
+
+int lte_timing_read(lte_plan* p, char* names, int names_len, double* ms, int64_t* launches, int n_max) {
+  if (!p) return fail(LTE_EINVAL, "null plan");
+  std::string s;
+  for (int i = 0; i < KN_COUNT; ++i) {
+    if (i) s += ",";
+    s += KNAMES[i];
+    if (i < n_max) {
+      if (ms) ms[i] = p->kms[i];
+      if (launches) launches[i] = p->klaunch[i];
+    }
+  }
+  if (names && names_len > 0) {
+    std::strncpy(names, s.c_str(), names_len - 1);
+    names[names_len - 1] = 0;
+  }
+  return KN_COUNT;
+}
+
+static void pack_bits(const uint8_t* bits, int n, uint32_t* w, int nw) {
+  std::memset(w, 0, sizeof(uint32_t) * nw);
+  for (int i = 0; i < n; ++i)
+    if (bits[i] & 1) w[i >> 5] |= 1u << (31 - (i & 31));
+}
+
+int lte_run(lte_plan* p, const lte_run_args* a) {
+  if (!p || !a) return fail(LTE_EINVAL, "null argument");
+  const lte_plan_desc& d = p->d;
+  const int B = a->n_frames;
+  if (B < 1 || B > d.max_frames) return fail(LTE_EINVAL, "n_frames out of range (1..max_frames)");
+  if (!a->snr_db) return fail(LTE_EINVAL, "snr_db required");
+  const int n_snr = std::max(1, a->n_snr);
+  const bool coded = d.chain == LTE_CHAIN_CODED, ray = d.channel == LTE_CH_RAYLEIGH;
+  const int rx = d.num_rx;
+  hipStream_t s = p->stream;
+  if (p->counts.alloc((size_t)4 * n_snr)) return fail(LTE_ENOMEM, "counts");
+  // per-frame parameters
+  std::vector<float> sl(B);
+  std::vector<int32_t> si(B, 0);
+  std::vector<uint64_t> fid(B);
+  for (int b = 0; b < B; ++b) {
+    sl[b] = (float)std::pow(10.0, (double)a->snr_db[b] / 10.0);
+    if (a->snr_index) {
+      si[b] = a->snr_index[b];
+      if (si[b] < 0 || si[b] >= n_snr) return fail(LTE_EINVAL, "snr_index out of range");
+    }
+    fid[b] = a->frame_ids ? a->frame_ids[b] : a->frame_id0 + (uint64_t)b;
+  }
+  HIPCHK(hipMemcpyAsync(p->snr_lin.p, sl.data(), B * sizeof(float), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(p->snr_idx.p, si.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(p->fid.p, fid.data(), B * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  // injection
+  const uint32_t* inj_bits = nullptr;
+  int64_t inj_bits_stride = 0;
+  std::vector<uint32_t> hb;
+  if (a->bits) {
+    const int nf = a->bits_stride ? B : 1;
+    const int nwd = (d.n_bits + 31) / 32;
+    hb.assign((size_t)nf * nwd, 0);
+    for (int f = 0; f < nf; ++f) pack_bits(a->bits + (size_t)f * a->bits_stride, d.n_bits, &hb[(size_t)f * nwd], nwd);
+    if (p->inj_bits.alloc(hb.size())) return fail(LTE_ENOMEM, "inj bits");
+    HIPCHK(hipMemcpyAsync(p->inj_bits.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, s));
+    inj_bits = p->inj_bits.p;
+    inj_bits_stride = a->bits_stride ? nwd : 0;
+  }
+  const float* inj_ph = nullptr;
+  int64_t inj_ph_stride = 0;
+  std::vector<float> hph;
+  if (a->phases && ray) {
+    const int nf = a->phases_stride ? B : 1;
+    const size_t per = (size_t)rx * d.n_paths * 16;
+    hph.resize(nf * per);
+    for (int f = 0; f < nf; ++f)
+      for (size_t i = 0; i < per; ++i) hph[f * per + i] = (float)a->phases[(size_t)f * a->phases_stride + i];
+    if (p->inj_ph.alloc(hph.size())) return fail(LTE_ENOMEM, "inj phases");
+    HIPCHK(hipMemcpyAsync(p->inj_ph.p, hph.data(), hph.size() * 4, hipMemcpyHostToDevice, s));
+    inj_ph = p->inj_ph.p;
+    inj_ph_stride = a->phases_stride ? (int64_t)per : 0;
+  }
+  const float* inj_z = nullptr;
+  int64_t inj_z_stride = 0;
+  std::vector<float> hz;
+  if (a->noise) {
+    const int nf = a->noise_stride ? B : 1;
+    const size_t per = (size_t)rx * 2 * p->L;
+    hz.resize(nf * per);
+    for (int f = 0; f < nf; ++f)
+      for (size_t i = 0; i < per; ++i) hz[f * per + i] = (float)a->noise[(size_t)f * a->noise_stride + i];
+    if (p->inj_z.alloc(hz.size())) return fail(LTE_ENOMEM, "inj noise");
+    HIPCHK(hipMemcpyAsync(p->inj_z.p, hz.data(), hz.size() * 4, hipMemcpyHostToDevice, s));
+    inj_z = p->inj_z.p;
+    inj_z_stride = a->noise_stride ? (int64_t)per : 0;
+  }
+  HIPCHK(hipMemsetAsync(p->counts.p, 0, 4 * n_snr * sizeof(unsigned long long), s));
+  HIPCHK(hipMemsetAsync(p->frame_err.p, 0, B * sizeof(uint32_t), s));
+  const Grid& g = p->grid;
+  p->evuse.clear();
+  {
+    Timer t(p, KN_PAYLOAD);
+    LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
+  }
+  if (coded) {
+    Timer t(p, KN_ENCODE);
+    LCHK(launch_encode(s, p->pw.p, p->PW, p->cbw.p, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
+  }
+  {
+    Timer t(p, KN_OFDM_TX);
+    LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B));
+  }
+  const float2* ysrc = ray ? p->y.p : p->x.p;
+  const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
+  if (ray) {
+    Timer t(p, KN_FADING);
+    LCHK(launch_fading(s, B, rx, d.n_paths, p->gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, p->phases.p,
+                       p->coef.p));
+  }
+  {
+    Timer t(p, KN_CHANNEL);
+    LCHK(launch_channel(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
+                        p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, p->nblk));
+  }
+  {
+    Timer t(p, KN_RX_CHEST);
+    LCHK(launch_rx_chest(s, g, B, rx, ysrc, yrs, yfs, p->pow_part.p, p->nblk, p->snr_lin.p, p->fid.p, a->seed,
+                         inj_z, inj_z_stride, p->H.p, p->pstats.p, p->npow.p));
+  }
+  float2* cap_syms_dev = nullptr;
+  uint8_t* cap_bits_dev = nullptr;
+  if (a->cap_data_syms) {
+    if (p->capbuf.alloc((size_t)B * p->n_sym * p->Nd)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = p->capbuf.p;
+  }
+  if (a->cap_bits_rx) {
+    if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
+    cap_bits_dev = p->cap_bits.p;
+  }
+  {
+    Timer t(p, KN_RX_DATA);
+    LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, p->H.p, p->npow.p, p->snr_lin.p,
+                        p->fid.p, a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p, p->llr.p,
+                        cap_syms_dev, coded ? nullptr : cap_bits_dev));
+  }
+  if (coded) {
+    {
+      Timer t(p, KN_DEMATCH);
+      LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
+    }
+    const int G = (B + 63) / 64;
+    for (int r = 0; r < p->C; ++r) {
+      Timer t(p, KN_TURBO);
+      const CbInfo& c = p->cbs[r];
+      LCHK(launch_turbo(s, p->blk[r].p, p->ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, d.turbo_iters, G, TM_DEC1));
+    }
+    {
+      Timer t(p, KN_CRC);
+      LCHK(launch_crc_count(s, p->cbi.p, p->C, p->dec_ptrs.p, p->kw_dev.p, B, p->pw.p, p->PW, d.n_bits,
+                            p->frame_err.p, p->frame_crc.p, cap_bits_dev));
+    }
+  }
+  {
+    Timer t(p, KN_ACC);
+    LCHK(launch_accumulate(s, B, coded ? 1 : 0, d.n_bits, p->snr_idx.p, p->frame_err.p, p->frame_crc.p,
+                           p->counts.p));
+  }
+  // results
+  std::vector<unsigned long long> hc((size_t)4 * n_snr);
+  HIPCHK(hipMemcpyAsync(hc.data(), p->counts.p, hc.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  if (a->frame_errors)
+    HIPCHK(hipMemcpyAsync(a->frame_errors, p->frame_err.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  std::vector<uint32_t> crc;
+  if (a->frame_crc_ok && coded) {
+    crc.resize(B);
+    HIPCHK(hipMemcpyAsync(crc.data(), p->frame_crc.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
+  if (a->cap_signal_tx)
+    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, p->x.p, (size_t)B * p->L * sizeof(float2), hipMemcpyDeviceToHost, s));
+  if (a->cap_signal_rx) {
+    DBuf<float2> tmp;
+    if (tmp.alloc((size_t)B * rx * p->L)) return fail(LTE_ENOMEM, "capture");
+    {
+      Timer t(p, KN_CAP);
+      hipLaunchKernelGGL(k_cap_rx, dim3((p->L + 255) / 256, rx, B), dim3(256), 0, s, p->L, rx, B, ysrc, yrs, yfs,
+                         p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p);
+      LCHK((int)hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * rx * p->L * sizeof(float2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    tmp.release();
+  }
+  if (a->cap_data_syms)
+    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->n_sym * p->Nd * sizeof(float2),
+                          hipMemcpyDeviceToHost, s));
+  if (a->cap_H)
+    HIPCHK(hipMemcpyAsync(a->cap_H, p->H.p, (size_t)B * rx * p->n_grp * d.N * sizeof(float2), hipMemcpyDeviceToHost, s));
+  if (a->cap_pilot_stats)
+    HIPCHK(hipMemcpyAsync(a->cap_pilot_stats, p->pstats.p, (size_t)B * rx * p->n_grp * 2 * sizeof(float),
+                          hipMemcpyDeviceToHost, s));
+  if (a->cap_bits_rx)
+    HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
+  if (a->cap_llr && coded)
+    HIPCHK(hipMemcpyAsync(a->cap_llr, p->llr.p, (size_t)B * p->n_re_bits * sizeof(float), hipMemcpyDeviceToHost, s));
+  if (a->cap_noise_power)
+    HIPCHK(hipMemcpyAsync(a->cap_noise_power, p->npow.p, (size_t)B * rx * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (p->timing) collect_timing(p);
+  if (a->counts)
+    for (size_t i = 0; i < hc.size(); ++i) a->counts[i] += hc[i];
+  if (a->frame_crc_ok && coded)
+    for (int b = 0; b < B; ++b) a->frame_crc_ok[b] = (uint8_t)crc[b];
+  return LTE_OK;
+}
+
+// ------------------------------------------------------------------ stage entry points
+static int stage_grid(int N, TableSet& t, Grid& g) {
+  const std::vector<float2> tw = make_twiddles(N);
+  if (upload(t.tw, tw)) return -1;
+  g = Grid{};
+  g.N = N;
+  g.log2N = ilog2(N);
+  g.tw = t.tw.p;
+  return 0;
+}
+
+int lte_fft_host(int N, int inverse, int64_t batch, const float* in, float* out) {
+  if (N < 8 || N > 2048 || (N & (N - 1)) || batch < 0 || (!in && batch) || (!out && batch))
+    return fail(LTE_EINVAL, "bad fft arguments");
+  if (batch == 0) return LTE_OK;
+  if (N < 64) return fail(LTE_EUNSUP, "N < 64");
+  TableSet t;
+  Grid g;
+  if (stage_grid(N, t, g)) return fail(LTE_ENOMEM, "tables");
+  DBuf<float2> di, dout;
+  if (di.alloc(batch * N) || dout.alloc(batch * N)) { t.release(); return fail(LTE_ENOMEM, "fft buffers"); }
+  int rc = LTE_OK;
+  if (hipMemcpy(di.p, in, batch * N * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+      launch_fft(nullptr, g, inverse, batch, di.p, dout.p) != 0 || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, dout.p, batch * N * sizeof(float2), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, "fft failed");
+  di.release(); dout.release(); t.release();
+  return rc;
+}
+
+int lte_llr_host(int bps, int64_t n, const float* syms, const float* nv, float* llr) {
+  if ((bps != 2 && bps != 4 && bps != 6) || n < 0) return fail(LTE_EINVAL, "bad llr arguments");
+  if (n == 0) return LTE_OK;
+  DBuf<float2> ds;
+  DBuf<float> dn, dl;
+  if (ds.alloc(n) || dn.alloc(n) || dl.alloc(n * bps)) return fail(LTE_ENOMEM, "llr buffers");
+  int rc = LTE_OK;
+  if (hipMemcpy(ds.p, syms, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dn.p, nv, n * 4, hipMemcpyHostToDevice) != hipSuccess || launch_llr(nullptr, bps, n, ds.p, dn.p, dl.p) ||
+      hipMemcpy(llr, dl.p, n * bps * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, "llr failed");
+  ds.release(); dn.release(); dl.release();
+  return rc;
+}
+
+int lte_hard_host(int bps, int64_t n, const float* syms, uint8_t* bits) {
+  if ((bps != 2 && bps != 4 && bps != 6) || n < 0) return fail(LTE_EINVAL, "bad hard arguments");
+  if (n == 0) return LTE_OK;
+  DBuf<float2> ds;
+  DBuf<uint8_t> db;
+  if (ds.alloc(n) || db.alloc(n * bps)) return fail(LTE_ENOMEM, "buffers");
+  int rc = LTE_OK;
+  if (hipMemcpy(ds.p, syms, n * 8, hipMemcpyHostToDevice) != hipSuccess || launch_hard(nullptr, bps, n, ds.p, db.p) ||
+      hipMemcpy(bits, db.p, n * bps, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, "hard failed");
+  ds.release(); db.release();
+  return rc;
+}
+
+int lte_crc_host(int64_t n, const uint8_t* bits, uint32_t poly, int len, uint32_t* crc) {
+  if (n < 0 || !crc || (n && !bits)) return fail(LTE_EINVAL, "bad crc arguments");
+  if (poly != 0x1864CFBu || len != 24) return fail(LTE_EUNSUP, "only CRC-24A runs on the device path");
+  const int nw = (int)((n + 24 + 31) / 32) + 1;
+  std::vector<uint32_t> w(nw, 0);
+  pack_bits(bits, (int)n, w.data(), nw);
+  DBuf<uint32_t> dpw, dinj;
+  DBuf<uint64_t> dfid;
+  if (dpw.alloc(nw) || dinj.alloc(nw) || dfid.alloc(1)) return fail(LTE_ENOMEM, "buffers");
+  int rc = LTE_OK;
+  std::vector<uint32_t> o(nw);
+  if (hipMemcpy(dinj.p, w.data(), nw * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(dfid.p, 0, 8) != hipSuccess ||
+      launch_payload(nullptr, dpw.p, nw, (int)n, 1, dfid.p, 0, 1, dinj.p, 0) ||
+      hipMemcpy(o.data(), dpw.p, nw * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, "crc failed");
+  if (rc == LTE_OK) {
+    uint32_t v = 0;
+    for (int t = 0; t < 24; ++t) {
+      const int64_t q = n + t;
+      v = (v << 1) | ((o[q >> 5] >> (31 - (q & 31))) & 1u);
+    }
+    *crc = v;
+  }
+  dpw.release(); dinj.release(); dfid.release();
+  return rc;
+}
+
+int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out) {
+  int f1, f2;
+  if (!qpp_lookup(K, &f1, &f2)) return fail(LTE_EINVAL, "Invalid code block size K=" + std::to_string(K));
+  if (ncb < 0 || (ncb && (!bits || !out))) return fail(LTE_EINVAL, "bad arguments");
+  if (ncb == 0) return LTE_OK;
+  const int PW = (K + 31) / 32 + 1, KW = PW, EW = (K + 6 + 31) / 32;
+  std::vector<uint32_t> w((size_t)ncb * PW);
+  for (int64_t c = 0; c < ncb; ++c) pack_bits(bits + c * K, K, &w[c * PW], PW);
+  CbInfo ci{K, 0, K, 0, 0, f1, f2, 3 * K + 12};
+  DBuf<uint32_t> dpw, dcb, denc;
+  DBuf<CbInfo> dci;
+  std::vector<CbInfo> vci{ci};
+  if (dpw.alloc(w.size()) || dcb.alloc((size_t)ncb * KW) || denc.alloc((size_t)ncb * 3 * EW) || upload(dci, vci))
+    return fail(LTE_ENOMEM, "buffers");
+  std::vector<uint32_t> e((size_t)ncb * 3 * EW);
+  int rc = LTE_OK;
+  if (hipMemcpy(dpw.p, w.data(), w.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_encode(nullptr, dpw.p, PW, dcb.p, KW, denc.p, EW, dci.p, 1, (int)ncb) ||
+      hipMemcpy(e.data(), denc.p, e.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, "encode failed");
+  if (rc == LTE_OK) {
+    for (int64_t c = 0; c < ncb; ++c) {
+      const uint32_t* d0 = &e[c * 3 * EW];
+      const uint32_t* d1 = d0 + EW;
+      const uint32_t* d2 = d1 + EW;
+      auto gb = [](const uint32_t* w, int i) -> uint8_t { return (w[i >> 5] >> (31 - (i & 31))) & 1u; };
+      uint8_t* o = out + c * (3 * K + 12);
+      for (int k = 0; k < K; ++k) { o[3 * k] = gb(d0, k); o[3 * k + 1] = gb(d1, k); o[3 * k + 2] = gb(d2, k); }
+      for (int t = 0; t < 3; ++t) {
+        o[3 * K + t] = gb(d0, K + t);
+        o[3 * K + 3 + t] = gb(d1, K + t);
+        o[3 * K + 6 + t] = gb(d0, K + 3 + t);
+        o[3 * K + 9 + t] = gb(d2, K + t);
+      }
+    }
+  }
+  dpw.release(); dcb.release(); denc.release(); dci.release();
+  return rc;
+}
+
+// Host-side layout conversion [ncb][3K+12] -> decoder rows, shared by the two
+// turbo entry points.
+static int turbo_host_run(int K, int iters, int64_t ncb, const float* llr, const float* ls, const float* lp,
+                          const float* la, int mode, uint8_t* bits, float* app) {
+  int f1, f2;
+  if (!qpp_lookup(K, &f1, &f2)) return fail(LTE_EINVAL, "Invalid interleaver size K=" + std::to_string(K));
+  if (ncb < 0) return fail(LTE_EINVAL, "bad ncb");
+  if (ncb == 0) return LTE_OK;
+  const int G = (int)((ncb + 63) / 64);
+  const int64_t rows = turbo_rows(K);
+  std::vector<float> h((size_t)G * rows * 64, 0.f);
+  auto at = [&](int64_t c, int64_t row) -> float& { return h[((c / 64) * rows + row) * 64 + (c % 64)]; };
+  for (int64_t c = 0; c < ncb; ++c) {
+    if (mode == TM_APP) {
+      const float* s = ls + c * (K + 3);
+      const float* q = lp + c * (K + 3);
+      const float* A = la + c * (K + 3);
+      for (int k = 0; k < K + 3; ++k) { at(c, k) = s[k]; at(c, K + 3 + k) = q[k]; }
+      for (int k = 0; k < K; ++k) at(c, 3 * K + 12 + k) = A[k];
+    } else {
+      const float* l = llr + c * (3 * K + 12);
+      for (int k = 0; k < K; ++k) {
+        at(c, k) = l[3 * k];
+        at(c, K + 3 + k) = l[3 * k + 1];
+        at(c, 2 * K + 6 + k) = l[3 * k + 2];
+      }
+      for (int t = 0; t < 3; ++t) {
+        at(c, K + t) = l[3 * K + t];
+        at(c, 2 * K + 3 + t) = l[3 * K + 3 + t];
+        at(c, 3 * K + 9 + t) = l[3 * K + 6 + t];
+        at(c, 3 * K + 6 + t) = l[3 * K + 9 + t];
+      }
+    }
+  }
+  DBuf<float> db, dck;
+  DBuf<uint32_t> dbits;
+  const int KW = turbo_kw(K);
+  if (db.alloc(h.size()) || dck.alloc((size_t)G * turbo_nwin(K) * 8 * 64) || dbits.alloc((size_t)G * KW * 64))
+    return fail(LTE_ENOMEM, "turbo buffers");
+  int rc = LTE_OK;
+  std::vector<uint32_t> hb((size_t)G * KW * 64);
+  if (hipMemcpy(db.p, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_turbo(nullptr, db.p, dck.p, dbits.p, K, f1, f2, iters, G, mode) || hipDeviceSynchronize() != hipSuccess)
+    rc = fail(LTE_EHIP, std::string("turbo failed: ") + hipGetErrorString(hipGetLastError()));
+  if (rc == LTE_OK) {
+    if (mode == TM_APP) {
+      if (hipMemcpy(h.data(), db.p, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(LTE_EHIP, "copy");
+      for (int64_t c = 0; c < ncb && rc == LTE_OK; ++c)
+        for (int k = 0; k < K; ++k) app[c * K + k] = at(c, 3 * K + 12 + k);
+    } else {
+      if (hipMemcpy(hb.data(), dbits.p, hb.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(LTE_EHIP, "copy");
+      for (int64_t c = 0; c < ncb && rc == LTE_OK; ++c)
+        for (int k = 0; k < K; ++k) {
+          const uint32_t w = hb[((c / 64) * KW + (k >> 5)) * 64 + (c % 64)];
+          bits[c * K + k] = (w >> (31 - (k & 31))) & 1u;
+        }
+    }
+  }
+  db.release(); dck.release(); dbits.release();
+  return rc;
+}
+
+int lte_turbo_decode_host(int K, int iters, int64_t ncb, const float* llr, uint8_t* bits) {
+  if (iters < 0 || (ncb > 0 && (!llr || !bits))) return fail(LTE_EINVAL, "bad arguments");
+  return turbo_host_run(K, iters, ncb, llr, nullptr, nullptr, nullptr, TM_DEC1, bits, nullptr);
+}
+
+int lte_bcjr_host(int K, int64_t ncb, const float* ls, const float* lp, const float* la, float* app) {
+  if (ncb > 0 && (!ls || !lp || !la || !app)) return fail(LTE_EINVAL, "bad arguments");
+  return turbo_host_run(K, 0, ncb, nullptr, ls, lp, la, TM_APP, nullptr, app);
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// Internal (non-ABI) declarations shared by the kernel TUs and the C-ABI TU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/lte_phy.h"
+
+namespace lte {
+
+// Per code-block-slot description (one entry per CB index r of a frame).
+struct CbInfo {
+  int K, F, info, off, crc;   // segmentation.py:74-263
+  int f1, f2;                 // QPP (turbo_encoder.py:34-73)
+  int E;                      // rate-matched length
+};
+
+struct Grid {                 // device pointers + numerology for one plan
+  int N, log2N, Nc, cp, Nd, Np, bps, n_sym, L, n_grp;
+  const int32_t* data_idx;    // [Nd]
+  const int32_t* pilot_idx;   // [Np]
+  const float2* pilots;       // [Np]
+  const int32_t* seg;         // [N]  left pilot of the interpolation segment
+  const float* inv_gap;       // [Np] 1/(p_{i+1}-p_i)
+  const float2* tw;           // [N]
+  const float2* constel;      // [M]
+  float qscale;               // sqrt(2) / sqrt(10) / sqrt(42)
+};
+
+// launchers (return hipError_t as int)
+int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, const uint64_t* fid,
+                   uint64_t seed, int B, const uint32_t* inj, int64_t inj_stride);
+int launch_encode(hipStream_t s, const uint32_t* pw, int PW, uint32_t* cbw, int KWmax, uint32_t* enc,
+                  int EW, const CbInfo* cbi_dev, int C, int B);
+int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
+                   int enc_words, const int32_t* tx_map, float2* x, int B);
+int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* gains_dev, const uint64_t* fid,
+                  uint64_t seed, const float* inj_ph, int64_t inj_stride, float* phases, float2* coef);
+int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
+                   const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
+                   const float2* coef, const float2* x, float2* y, float* pow_part, int nblk);
+int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float2* y, int64_t y_rx_stride,
+                    int64_t y_frame_stride, const float* pow_part, int nblk, const float* snr_lin,
+                    const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride,
+                    float2* H, float* pstats, float* npow_out);
+int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, int num_rx,
+                   const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
+                   const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
+                   const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
+                   uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits);
+int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
+                   const int64_t* rows, int C);
+int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
+                 int G, int mode);
+int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
+                     const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
+                     uint8_t* cap_bits);
+int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, const int32_t* snr_idx,
+                      const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts);
+int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);
+int launch_llr(hipStream_t s, int bps, int64_t n, const float2* syms, const float* nv, float* llr);
+int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* bits);
+
+// turbo modes
+enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_FINAL = 2, TM_APP = 3 };
+// turbo geometry: rows of one (r, group) block = 4K+12:
+//   [0,K+3) LS (sys + sys1 tail) | [K+3,2K+6) LP1 | [2K+6,3K+9) LP2 | [3K+9,3K+12) LS2T | [3K+12,4K+12) LE
+__host__ __device__ inline int64_t turbo_rows(int K) { return 4LL * K + 12; }
+__host__ __device__ inline int turbo_nwin(int K) { return K / 8 + 1; }
+__host__ __device__ inline int turbo_kw(int K) { return (K + 31) / 32; }
+
+}  // namespace lte

@@ -1,0 +1,596 @@
+// Front-end kernels of the LTE link chain for gfx950: payload/CRC, OFDM TX
+// (QAM map + resource map + IFFT + CP), multipath Rayleigh + AWGN channel,
+// RX (CP removal + FFT, CRS LS estimation + interpolation, ZF / MRC, hard
+// decision or soft demap).  All HBM-bound: every kernel streams its frame
+// data once, coalesced, with per-symbol FFTs staged in LDS.
+#include "lte_common.h"
+#include "lte_internal.h"
+
+namespace lte {
+
+constexpr int WG = 256;
+
+// ---------------------------------------------------------------------------
+// Payload bits (+ CRC-24A, crc.py:212-233) : one lane per frame.
+__device__ __forceinline__ uint32_t crc24_entry(uint32_t i, uint32_t poly) {
+  uint32_t r = i << 16;
+  for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? ((r << 1) ^ poly) : (r << 1);
+  return r & 0xFFFFFFu;
+}
+
+__global__ __launch_bounds__(WG) void k_payload(uint32_t* __restrict__ pw, int PW, int n_bits, int crc,
+                                                const uint64_t* __restrict__ fid, uint64_t seed, int B,
+                                                const uint32_t* __restrict__ inj, int64_t inj_stride) {
+  __shared__ uint32_t T[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_entry(i, 0x864CFBu);
+  __syncthreads();
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  uint32_t* w = pw + (size_t)b * PW;
+  const int nwd = (n_bits + 31) >> 5;
+  u32x4 rv{0, 0, 0, 0};
+  uint32_t c = 0;
+  for (int i = 0; i < PW; ++i) {
+    uint32_t v = 0;
+    if (i < nwd) {
+      if (inj) {
+        v = inj[(size_t)b * inj_stride + i];
+      } else {
+        if ((i & 3) == 0) rv = rng4(seed, fid[b], RNG_STREAM_BITS, (uint32_t)(i >> 2));
+        const int q = i & 3;
+        v = q == 0 ? rv.x : q == 1 ? rv.y : q == 2 ? rv.z : rv.w;
+      }
+      const int rem = n_bits - 32 * i;
+      if (rem < 32) v &= ~(0xFFFFFFFFu >> rem);
+      if (crc) {
+        const int dbits = min(32, rem);
+        int k = 0;
+        for (; k + 8 <= dbits; k += 8) c = ((c << 8) & 0xFFFFFFu) ^ T[((c >> 16) ^ (v >> (24 - k))) & 0xFFu];
+        for (; k < dbits; ++k) {
+          const uint32_t msb = (c >> 23) & 1u;
+          c = (c << 1) & 0xFFFFFFu;
+          if (msb ^ ((v >> (31 - k)) & 1u)) c ^= 0x864CFBu;
+        }
+      }
+    }
+    w[i] = v;
+  }
+  if (crc) {  // append the 24 CRC bits MSB-first at [n_bits, n_bits+24)
+    for (int t = 0; t < 24; ++t) {
+      const int p = n_bits + t;
+      if ((c >> (23 - t)) & 1u) w[p >> 5] |= 1u << (31 - (p & 31));
+    }
+  }
+}
+
+int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, const uint64_t* fid, uint64_t seed,
+                   int B, const uint32_t* inj, int64_t inj_stride) {
+  hipLaunchKernelGGL(k_payload, dim3((B + WG - 1) / WG), dim3(WG), 0, s, pw, PW, n_bits, crc, fid, seed, B, inj,
+                     inj_stride);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// OFDM TX: one slot = one OFDM symbol; 2048/N slots per 256-thread block.
+// QAMModulator.bits_to_symbols (modulator.py:61-88) / coded RE mapping via
+// tx_map (rate_match_turbo + T/F interleaver, rate_matching.py:193-297,
+// ofdm_core.py:1040-1099), ResourceMapper.map_symbols (resource_mapper.py:
+// 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
+__global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, int coded, const uint32_t* __restrict__ pw, int PW,
+                                                const uint32_t* __restrict__ enc, int enc_words,
+                                                const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B) {
+  extern __shared__ float2 sm[];
+  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int64_t gs = (int64_t)blockIdx.x * spw + slot;
+  const int b = (int)(gs / g.n_sym), l = (int)(gs % g.n_sym);
+  const bool active = slot < spw && b < B;
+  float2* buf = sm + slot * N;
+  if (active) {
+    for (int k = tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  if (active) {
+    const uint32_t* fb = pw + (size_t)b * PW;
+    const uint32_t* fe = enc + (size_t)b * enc_words;
+    for (int j = tid; j < g.Nd; j += T) {
+      const int64_t t0 = ((int64_t)l * g.Nd + j) * g.bps;
+      int idx = 0;
+      bool zero = false;
+      for (int m = 0; m < g.bps; ++m) {
+        uint32_t bit;
+        if (coded) {
+          const int src = tx_map[t0 + m];
+          if (src == -2) { zero = true; bit = 0; }
+          else bit = src >= 0 ? getbit(fe, src) : 0u;
+        } else {
+          bit = getbit(fb, t0 + m);
+        }
+        idx = (idx << 1) | (int)bit;
+      }
+      buf[g.data_idx[j]] = zero ? make_float2(0.f, 0.f) : g.constel[idx];
+    }
+    for (int p = tid; p < g.Np; p += T) buf[g.pilot_idx[p]] = g.pilots[p];
+  }
+  __syncthreads();
+  fft_lds<true>(buf, N, g.log2N, g.tw, tid, active);
+  if (active) {
+    const float sc = rsqrtf((float)N);
+    float2* xo = x + (size_t)b * g.L + (size_t)l * (N + g.cp);
+    for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
+    for (int k = tid; k < g.cp; k += T) xo[k] = cscale(buf[N - g.cp + k], sc);
+  }
+}
+
+int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
+                   int enc_words, const int32_t* tx_map, float2* x, int B) {
+  const int spw = WG / (g.N >> 3);
+  const int64_t total = (int64_t)B * g.n_sym;
+  const int blocks = (int)((total + spw - 1) / spw);
+  hipLaunchKernelGGL(k_ofdm_tx, dim3(blocks), dim3(WG), spw * g.N * sizeof(float2), s, g, coded, pw, PW, enc,
+                     enc_words, tx_map, x, B);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Fading taps: RayleighChannel.jakes_fading phases (rayleighchannel.py:20-42).
+// One thread per (frame, rx, path): 16 phases phi_m (Philox or injected) and
+// the static coefficient g_p * sqrt(2/16) * sum_m exp(j phi_m) used when fD=0.
+__global__ __launch_bounds__(WG) void k_fading(int B, int num_rx, int n_paths, const float* __restrict__ gains,
+                                               const uint64_t* __restrict__ fid, uint64_t seed,
+                                               const float* __restrict__ inj, int64_t inj_stride,
+                                               float* __restrict__ phases, float2* __restrict__ coef) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = num_rx * n_paths;
+  if (i >= B * per) return;
+  const int b = i / per, rp = i % per, rx = rp / n_paths, p = rp % n_paths;
+  float* ph = phases + (size_t)i * 16;
+  float sr = 0.f, si = 0.f;
+  for (int m = 0; m < 16; ++m) {
+    float v;
+    if (inj) {
+      v = inj[(size_t)b * inj_stride + (size_t)rp * 16 + m];
+    } else {
+      const u32x4 r = rng4(seed, fid[b], RNG_STREAM_FADE + (uint32_t)rx * 64u + (uint32_t)p, (uint32_t)(m >> 2));
+      const int q = m & 3;
+      const uint32_t u = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+      v = 6.2831853071795864f * ((u >> 8) * (1.0f / 16777216.0f));
+    }
+    ph[m] = v;
+    float s, c;
+    sincosf(v, &s, &c);
+    sr += c;
+    si += s;
+  }
+  const float k = sqrtf(2.0f / 16.0f) * gains[p];
+  coef[i] = make_float2(sr * k, si * k);
+}
+
+int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* gains_dev, const uint64_t* fid,
+                  uint64_t seed, const float* inj_ph, int64_t inj_stride, float* phases, float2* coef) {
+  const int n = B * num_rx * n_paths;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_fading, dim3((n + WG - 1) / WG), dim3(WG), 0, s, B, num_rx, n_paths, gains_dev, fid, seed,
+                     inj_ph, inj_stride, phases, coef);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Channel: y[n] = sum_p g_p h_p[n] x[n - d_p] (RayleighChannel.filter,
+// rayleighchannel.py:44-58: stream-level delay with zero prefix, Q4) and the
+// per-block partial sums of |y|^2 for the measured-power SNR (channel.py:
+// 217-224, Q5).  AWGN: only the power of x.  grid (nblk, num_rx, B).
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  }
+  return t;
+}
+
+__global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh, int n_paths,
+                                                const int32_t* __restrict__ delays, const float* __restrict__ gains,
+                                                float fD, float fs, const float* __restrict__ phases,
+                                                const float2* __restrict__ coef, const float2* __restrict__ x,
+                                                float2* __restrict__ y, float* __restrict__ pow_part, int nblk) {
+  __shared__ float red[WG / 64];
+  const int n = blockIdx.x * WG + threadIdx.x;
+  const int rx = blockIdx.y, b = blockIdx.z;
+  const float2* xf = x + (size_t)b * L;
+  float2 v = make_float2(0.f, 0.f);
+  if (n < L) {
+    if (!rayleigh) {
+      v = xf[n];
+    } else {
+      const size_t cb = ((size_t)b * num_rx + rx) * n_paths;
+      for (int p = 0; p < n_paths; ++p) {
+        const int src = n - delays[p];
+        if (src < 0) continue;
+        float2 c;
+        if (fD == 0.0f) {
+          c = coef[cb + p];
+        } else {  // jakes_fading with t = n / fs
+          const float* ph = phases + (cb + p) * 16;
+          float sr = 0.f, si = 0.f;
+          const float t = (float)n / fs;
+          for (int m = 0; m < 16; ++m) {
+            const float al = 6.2831853071795864f * (float)(m + 1) / 16.0f;
+            const float arg = 6.2831853071795864f * fD * cosf(al) * t + ph[m];
+            float s, cc;
+            sincosf(arg, &s, &cc);
+            sr += cc;
+            si += s;
+          }
+          const float k = sqrtf(2.0f / 16.0f) * gains[p];
+          c = make_float2(sr * k, si * k);
+        }
+        v = cadd(v, cmul(c, xf[src]));
+      }
+      y[((size_t)b * num_rx + rx) * L + n] = v;
+    }
+  }
+  const float t = block_sum(v.x * v.x + v.y * v.y, red);
+  if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blockIdx.x] = t;
+}
+
+int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
+                   const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
+                   const float2* coef, const float2* x, float2* y, float* pow_part, int nblk) {
+  hipLaunchKernelGGL(k_channel, dim3(nblk, num_rx, B), dim3(WG), 0, s, g.L, num_rx, rayleigh, n_paths, delays_dev,
+                     gains_dev, fD, fs, phases, coef, x, y, pow_part, nblk);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// RX helpers
+__device__ __forceinline__ float frame_power(const float* pp, int nblk, int L) {
+  float t = 0.f;
+  for (int i = 0; i < nblk; ++i) t += pp[i];
+  return t / (float)L;
+}
+
+// Load one OFDM symbol (CP removed) of (frame, rx) into LDS adding AWGN:
+// noise = sigma * z, sigma = sqrt(P/SNR/2) (channel.py:52-60).
+__device__ __forceinline__ void load_symbol_noisy(float2* buf, const float2* __restrict__ yf, int N, int cp, int l,
+                                                  float sigma, uint64_t seed, uint64_t frame, int rx,
+                                                  const float* __restrict__ zf /*inj: [2][L] or null*/, int L,
+                                                  int tid, int T) {
+  const int off = l * (N + cp) + cp;
+  for (int k = tid; k < N; k += T) {
+    const int n = off + k;
+    float2 z;
+    if (zf) {
+      z = make_float2(zf[n], zf[L + n]);
+    } else {
+      const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)(n >> 1));
+      z = (n & 1) ? box_muller(r.z, r.w) : box_muller(r.x, r.y);
+    }
+    const float2 v = yf[n];
+    buf[k] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Channel estimation: one slot per (frame, rx, 14-symbol group) on the group's
+// first symbol (LTEReceiver._estimate_channel_periodic lte_receiver.py:360-411,
+// LTEChannelEstimator.estimate_channel :40-96, _interpolate_channel :98-133).
+__global__ __launch_bounds__(WG) void k_rx_chest(Grid g, int B, int num_rx, const float2* __restrict__ y,
+                                                 int64_t y_rx_stride, int64_t y_frame_stride,
+                                                 const float* __restrict__ pow_part, int nblk,
+                                                 const float* __restrict__ snr_lin, const uint64_t* __restrict__ fid,
+                                                 uint64_t seed, const float* __restrict__ inj_z, int64_t inj_stride,
+                                                 float2* __restrict__ H, float* __restrict__ pstats,
+                                                 float* __restrict__ npow_out) {
+  extern __shared__ float2 sm[];
+  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int64_t gs = (int64_t)blockIdx.x * spw + slot;
+  const int per = num_rx * g.n_grp;
+  const int b = (int)(gs / per), rr = (int)(gs % per), rx = rr / g.n_grp, grp = rr % g.n_grp;
+  const bool active = slot < spw && b < B;
+  float2* buf = sm + slot * N;
+  float2* hp = sm + spw * N + slot * g.Np;
+  float npow = 0.f;
+  if (active) {
+    const float P = frame_power(pow_part + ((size_t)b * num_rx + rx) * nblk, nblk, g.L);
+    npow = P / snr_lin[b];
+    const float sigma = sqrtf(npow * 0.5f);
+    const float* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+    load_symbol_noisy(buf, y + b * y_frame_stride + rx * y_rx_stride, N, g.cp, grp * 14, sigma, seed, fid[b], rx,
+                      zf, g.L, tid, T);
+  }
+  __syncthreads();
+  fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
+  if (active) {
+    const float sc = rsqrtf((float)N);
+    for (int p = tid; p < g.Np; p += T) {
+      const float2 Y = cscale(buf[g.pilot_idx[p]], sc);
+      hp[p] = cdiv(Y, g.pilots[p]);
+      buf[g.pilot_idx[p]] = Y;  // keep scaled pilots for the SNR stats
+    }
+  }
+  __syncthreads();
+  if (active) {
+    float2* Hf = H + (((size_t)b * num_rx + rx) * g.n_grp + grp) * N;
+    for (int k = tid; k < N; k += T) {
+      const int sidx = g.seg[k];
+      float2 h;
+      if (sidx < 0) h = hp[0];
+      else if (sidx >= g.Np - 1) h = hp[g.Np - 1];
+      else {
+        const float2 v0 = hp[sidx], v1 = hp[sidx + 1];
+        const float fk = (float)(k - g.pilot_idx[sidx]);
+        const float ig = g.inv_gap[sidx];
+        h = make_float2(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+      }
+      Hf[k] = h;
+    }
+    if (tid == 0) {
+      float pp = 0.f, en = 0.f;
+      for (int p = 0; p < g.Np; ++p) {
+        const float2 Y = buf[g.pilot_idx[p]], X = g.pilots[p];
+        pp += Y.x * Y.x + Y.y * Y.y;
+        const float2 d = csub(Y, X);
+        en += d.x * d.x + d.y * d.y;
+      }
+      float* st = pstats + (((size_t)b * num_rx + rx) * g.n_grp + grp) * 2;
+      st[0] = pp / g.Np;
+      st[1] = en / g.Np;
+      if (grp == 0) npow_out[(size_t)b * num_rx + rx] = npow;
+    }
+  }
+}
+
+int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float2* y, int64_t y_rx_stride,
+                    int64_t y_frame_stride, const float* pow_part, int nblk, const float* snr_lin,
+                    const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride, float2* H,
+                    float* pstats, float* npow_out) {
+  const int spw = WG / (g.N >> 3);
+  const int64_t total = (int64_t)B * num_rx * g.n_grp;
+  const int blocks = (int)((total + spw - 1) / spw);
+  const size_t shm = (size_t)spw * (g.N + g.Np) * sizeof(float2);
+  hipLaunchKernelGGL(k_rx_chest, dim3(blocks), dim3(WG), shm, s, g, B, num_rx, y, y_rx_stride, y_frame_stride,
+                     pow_part, nblk, snr_lin, fid, seed, inj_z, inj_stride, H, pstats, npow_out);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Hard decision / soft demap.  Natural-binary QAM, I-level-major index
+// (modulator.py:28-59, Q9): bits = [I-level bits | Q-level bits], MSB first.
+__device__ __forceinline__ int level_idx(float v, float scale, int nl) {
+  // nearest of the nl levels (2i-(nl-1))/scale, ties -> lower level (argmin
+  // returns the first index, modulator.py:106)
+  const float t = (v * scale + (float)(nl - 1)) * 0.5f;
+  int i = (int)ceilf(t - 0.5f);
+  return i < 0 ? 0 : (i > nl - 1 ? nl - 1 : i);
+}
+
+__device__ __forceinline__ int hard_index(float2 y, int bps, float scale) {
+  if (bps == 2) return (y.x < 0.f ? 2 : 0) | (y.y < 0.f ? 1 : 0);  // [1+1j,1-1j,-1+1j,-1-1j]
+  const int nl = 1 << (bps >> 1);
+  return (level_idx(y.x, scale, nl) << (bps >> 1)) | level_idx(y.y, scale, nl);
+}
+
+// max-log LLRs (core/ofdm_core.py:791-923): QPSK 2*sqrt(2)*y/nv (no clip);
+// 16/64-QAM (min_{b=1} d^2 - min_{b=0} d^2)/(2 nv) clipped to +-10.  The
+// natural-binary map makes the metric separable per axis.
+__device__ __forceinline__ void llr_axis(float v, float scale, int nbits, float inv2nv, float* out) {
+  const int nl = 1 << nbits;
+  float m0[3] = {3.4e38f, 3.4e38f, 3.4e38f}, m1[3] = {3.4e38f, 3.4e38f, 3.4e38f};
+  for (int i = 0; i < nl; ++i) {
+    const float lv = (float)(2 * i - (nl - 1)) / scale;
+    const float d = (v - lv) * (v - lv);
+    for (int bb = 0; bb < nbits; ++bb) {
+      if ((i >> (nbits - 1 - bb)) & 1) m1[bb] = fminf(m1[bb], d);
+      else m0[bb] = fminf(m0[bb], d);
+    }
+  }
+  for (int bb = 0; bb < nbits; ++bb) out[bb] = fminf(10.f, fmaxf(-10.f, (m1[bb] - m0[bb]) * inv2nv));
+}
+
+__device__ __forceinline__ void soft_demap(float2 y, float nv, int bps, float scale, float* out) {
+  if (bps == 2) {
+    const float k = (2.0f / nv) * 1.41421356237309515f;
+    out[0] = (2.0f / nv) * y.x * 1.41421356237309515f;
+    out[1] = (2.0f / nv) * y.y * 1.41421356237309515f;
+    (void)k;
+    return;
+  }
+  const float inv2nv = 1.0f / (2.0f * nv);
+  llr_axis(y.x, scale, bps >> 1, inv2nv, out);
+  llr_axis(y.y, scale, bps >> 1, inv2nv, out + (bps >> 1));
+}
+
+// ---------------------------------------------------------------------------
+// Data path: one slot per (frame, OFDM symbol).  Per RX: CP-remove + noise +
+// FFT/sqrt(N) (lte_receiver.py:444-491); then
+//  UNCODED: ZF Y/(H+1e-6) (lte_receiver.py:154-180) -> hard bits -> bit errors
+//  CODED:   ZF -> sigma2_eff (ofdm_core.py:1224-1243) -> LLRs (RE order)
+//  SIMO:    MRC sum conj(H_i)Y_i / (sum|H_i|^2 + 1e-10) (ofdm_core.py:1405-1534)
+__global__ __launch_bounds__(WG) void k_rx_data(Grid g, int chain, int rayleigh, int B, int num_rx,
+                                                const float2* __restrict__ y, int64_t y_rx_stride,
+                                                int64_t y_frame_stride, const float2* __restrict__ H,
+                                                const float* __restrict__ npow, const float* __restrict__ snr_lin,
+                                                const uint64_t* __restrict__ fid, uint64_t seed,
+                                                const float* __restrict__ inj_z, int64_t inj_stride,
+                                                const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                uint32_t* __restrict__ frame_err, float* __restrict__ llr,
+                                                float2* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+  extern __shared__ float2 sm[];
+  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int64_t gs = (int64_t)blockIdx.x * spw + slot;
+  const int b = (int)(gs / g.n_sym), l = (int)(gs % g.n_sym);
+  const bool active = slot < spw && b < B;
+  float2* buf = sm + slot * N;
+  const int grp = l / 14;
+  const float sc = rsqrtf((float)N);
+  constexpr int QM = 4;  // data REs per thread (Nd < N/2 for every LTE profile)
+  float2 num[QM];
+  float den[QM];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) { num[q] = make_float2(0.f, 0.f); den[q] = 0.f; }
+  for (int rx = 0; rx < num_rx; ++rx) {
+    if (active) {
+      const float sigma = sqrtf(npow[(size_t)b * num_rx + rx] * 0.5f);
+      const float* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+      load_symbol_noisy(buf, y + b * y_frame_stride + rx * y_rx_stride, N, g.cp, l, sigma, seed, fid[b], rx, zf,
+                        g.L, tid, T);
+    }
+    __syncthreads();
+    fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
+    if (active) {
+      const float2* Hf = H + (((size_t)b * num_rx + rx) * g.n_grp + grp) * N;
+#pragma unroll
+      for (int q = 0; q < QM; ++q) {
+        const int j = tid + q * T;
+        if (j < g.Nd) {
+          const int k = g.data_idx[j];
+          const float2 Y = cscale(buf[k], sc), h = Hf[k];
+          if (chain == LTE_CHAIN_SIMO) {
+            num[q] = cadd(num[q], cmulc(Y, h));
+            den[q] += h.x * h.x + h.y * h.y;
+          } else {
+            num[q] = cdiv(Y, make_float2(h.x + 1e-6f, h.y));
+            den[q] = h.x * h.x + h.y * h.y;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!active) return;
+  const float* const unused = nullptr;
+  (void)unused;
+  uint32_t errs = 0;
+  const uint32_t* fb = pw + (size_t)b * PW;
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int j = tid + q * T;
+    if (j >= g.Nd) continue;
+    const int64_t re = (int64_t)l * g.Nd + j;
+    float2 z = num[q];
+    if (chain == LTE_CHAIN_SIMO) z = make_float2(z.x / (den[q] + 1e-10f), z.y / (den[q] + 1e-10f));
+    if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + re] = z;
+    if (chain == LTE_CHAIN_CODED) {
+      const float s2 = 1.0f / snr_lin[b];
+      float nv = s2;
+      if (rayleigh) nv = fmaxf(s2 / fminf(fmaxf(den[q], 1e-6f), 1e6f), s2 * 0.25f);
+      float o[6];
+      soft_demap(z, nv, g.bps, g.qscale, o);
+      float* lo = llr + ((size_t)b * g.n_sym * g.Nd + re) * g.bps;
+      for (int m = 0; m < g.bps; ++m) lo[m] = o[m];
+    } else {
+      const int idx = hard_index(z, g.bps, g.qscale);
+      for (int m = 0; m < g.bps; ++m) {
+        const int64_t pbit = re * g.bps + m;
+        if (pbit < n_bits) {
+          const uint32_t bit = (idx >> (g.bps - 1 - m)) & 1;
+          errs += bit ^ getbit(fb, pbit);
+          if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
+        }
+      }
+    }
+  }
+  if (chain != LTE_CHAIN_CODED && errs) atomicAdd(frame_err + b, errs);
+}
+
+int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, int num_rx, const float2* y,
+                   int64_t y_rx_stride, int64_t y_frame_stride, const float2* H, const float* npow,
+                   const float* snr_lin, const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride,
+                   const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, float* llr, float2* cap_syms,
+                   uint8_t* cap_bits) {
+  const int spw = WG / (g.N >> 3);
+  const int64_t total = (int64_t)B * g.n_sym;
+  const int blocks = (int)((total + spw - 1) / spw);
+  hipLaunchKernelGGL(k_rx_data, dim3(blocks), dim3(WG), spw * g.N * sizeof(float2), s, g, chain, rayleigh, B,
+                     num_rx, y, y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW,
+                     n_bits, frame_err, llr, cap_syms, cap_bits);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+__global__ void k_accumulate(int B, int coded, int n_bits, const int32_t* __restrict__ snr_idx,
+                             const uint32_t* __restrict__ frame_err, const uint32_t* __restrict__ frame_crc,
+                             unsigned long long* __restrict__ counts) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int s = snr_idx[b];
+  const uint32_t e = frame_err[b];
+  const uint32_t blk = coded ? (frame_crc[b] ? 0u : 1u) : (e ? 1u : 0u);
+  atomicAdd(counts + 4 * s + 0, (unsigned long long)e);
+  atomicAdd(counts + 4 * s + 1, (unsigned long long)n_bits);
+  atomicAdd(counts + 4 * s + 2, (unsigned long long)blk);
+  atomicAdd(counts + 4 * s + 3, 1ull);
+}
+
+int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, const int32_t* snr_idx,
+                      const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts) {
+  hipLaunchKernelGGL(k_accumulate, dim3((B + WG - 1) / WG), dim3(WG), 0, s, B, coded, n_bits, snr_idx, frame_err,
+                     frame_crc, counts);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Stage kernels for the parity entry points.
+__global__ __launch_bounds__(WG) void k_fft_batch(Grid g, int inverse, int64_t batch, const float2* __restrict__ in,
+                                                  float2* __restrict__ out) {
+  extern __shared__ float2 sm[];
+  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int64_t i = (int64_t)blockIdx.x * spw + slot;
+  const bool active = slot < spw && i < batch;
+  float2* buf = sm + slot * N;
+  if (active)
+    for (int k = tid; k < N; k += T) buf[k] = in[i * N + k];
+  __syncthreads();
+  if (inverse) fft_lds<true>(buf, N, g.log2N, g.tw, tid, active);
+  else fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
+  if (active) {
+    const float sc = rsqrtf((float)N);
+    for (int k = tid; k < N; k += T) out[i * N + k] = cscale(buf[k], sc);
+  }
+}
+
+int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out) {
+  const int spw = WG / (g.N >> 3);
+  const int blocks = (int)((batch + spw - 1) / spw);
+  hipLaunchKernelGGL(k_fft_batch, dim3(blocks), dim3(WG), spw * g.N * sizeof(float2), s, g, inverse, batch, in, out);
+  return (int)hipGetLastError();
+}
+
+__device__ __forceinline__ float qam_scale(int bps) {
+  return bps == 2 ? 1.41421356237309515f : (bps == 4 ? 3.16227766016837952f : 6.48074069840786023f);
+}
+
+__global__ void k_llr(int bps, int64_t n, const float2* __restrict__ syms, const float* __restrict__ nv,
+                      float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float o[6];
+  soft_demap(syms[i], nv[i], bps, qam_scale(bps), o);
+  for (int m = 0; m < bps; ++m) out[i * bps + m] = o[m];
+}
+
+int launch_llr(hipStream_t s, int bps, int64_t n, const float2* syms, const float* nv, float* llr) {
+  hipLaunchKernelGGL(k_llr, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, bps, n, syms, nv, llr);
+  return (int)hipGetLastError();
+}
+
+__global__ void k_hard(int bps, int64_t n, const float2* __restrict__ syms, uint8_t* __restrict__ bits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int idx = hard_index(syms[i], bps, qam_scale(bps));
+  for (int m = 0; m < bps; ++m) bits[i * bps + m] = (idx >> (bps - 1 - m)) & 1;
+}
+
+int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* bits) {
+  hipLaunchKernelGGL(k_hard, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, bps, n, syms, bits);
+  return (int)hipGetLastError();
+}
+
+}  // namespace lte

@@ -1,0 +1,490 @@
+// Turbo decoder (max-log BCJR, 8-state RSC) for gfx950.
+//
+// Replaces turbo_decode / LogMAPDecoder (core/channel_coding/turbo_decoder.py:
+// 118-450).  Design:
+//  * one lane = one code block; a wave = 64 code blocks of the same K taken
+//    from 64 consecutive frames.  All state (8 alpha/beta metrics, window of
+//    recomputed alphas) lives in VGPRs -> no cross-lane traffic at all.
+//  * batch-innermost layout [row][64 lanes] per (CB slot r, frame group g):
+//    every load/store of a step is one 256-B coalesced row; the QPP index
+//    pi(k) is wave-uniform (computed incrementally on the scalar unit) so the
+//    interleaved accesses of decoder 2 are coalesced rows too.
+//  * full-length recursion exactly as the reference (no sliding-window
+//    approximation): the forward pass stores alpha checkpoints every 8 steps,
+//    the backward pass recomputes each 8-step window from its checkpoint.
+//  * metrics are normalised to state 0 every step (max-log is shift
+//    invariant, so decisions equal the unnormalised float64 reference up to
+//    rounding).
+#include "lte_common.h"
+#include "lte_internal.h"
+
+namespace lte {
+
+// gamma for (fb, par, u); c = {g(0,0,0), g(0,0,1), g(0,1,0), g(0,1,1)}.  The
+// other four are exact negations (turbo_decoder.py:305-333 sums +/-L/2 terms).
+__device__ __forceinline__ float gsel(const float c[4], int fb, int par, int u) {
+  return fb == 0 ? c[par * 2 + u] : -c[(1 - par) * 2 + (1 - u)];
+}
+
+__device__ __forceinline__ void gam(float ls, float lp, float la, float c[4]) {
+  const float hs = 0.5f * ls, hp = 0.5f * lp, ha = 0.5f * la;
+  const float sp = hs + hp, sm = hs - hp;
+  c[0] = sp + ha;
+  c[1] = sp - ha;
+  c[2] = sm + ha;
+  c[3] = sm - ha;
+}
+
+// forward recursion (turbo_decoder.py:227-235) + normalisation.
+// State s = 4*s0 + 2*s1 + s2; next = 4*fb + 2*s0 + s1, fb = u^s1^s2,
+// par = fb^s0^s2.  Predecessors of ns=(f,a,b): (a,b,0) with u=f^b, par=f^a and
+// (a,b,1) with u=f^b^1, par=f^a^1.
+__device__ __forceinline__ void fwd(const float a[8], const float c[4], float o[8]) {
+#pragma unroll
+  for (int ns = 0; ns < 8; ++ns) {
+    const int f = ns >> 2, s0 = (ns >> 1) & 1, s1 = ns & 1;
+    const float v0 = a[4 * s0 + 2 * s1] + gsel(c, f, f ^ s0, f ^ s1);
+    const float v1 = a[4 * s0 + 2 * s1 + 1] + gsel(c, f, f ^ s0 ^ 1, f ^ s1 ^ 1);
+    o[ns] = fmaxf(v0, v1);
+  }
+  const float n0 = o[0];
+  o[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; ++s) o[s] -= n0;
+}
+
+// backward branch terms (turbo_decoder.py:238-245): t0[s] = beta[next(s,0)] +
+// g(s,0), t1[s] = beta[next(s,1)] + g(s,1) = beta[next(s,0)^4] - g(s,0).
+__device__ __forceinline__ void bterms(const float b[8], const float c[4], float t0[8], float t1[8]) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int s0 = s >> 2, s1 = (s >> 1) & 1, s2 = s & 1;
+    const int fb = s1 ^ s2, par = fb ^ s0 ^ s2, ns = 4 * fb + 2 * s0 + s1;
+    const float g = gsel(c, fb, par, 0);
+    t0[s] = b[ns] + g;
+    t1[s] = b[ns ^ 4] - g;
+  }
+}
+
+__device__ __forceinline__ void bnext(const float t0[8], const float t1[8], float b[8]) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) b[s] = fmaxf(t0[s], t1[s]);
+  const float n0 = b[0];
+  b[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; ++s) b[s] -= n0;
+}
+
+// a-posteriori LLR (turbo_decoder.py:250-266)
+__device__ __forceinline__ float llr_app(const float a[8], const float t0[8], const float t1[8]) {
+  float m0 = a[0] + t0[0], m1 = a[0] + t1[0];
+#pragma unroll
+  for (int s = 1; s < 8; ++s) {
+    m0 = fmaxf(m0, a[s] + t0[s]);
+    m1 = fmaxf(m1, a[s] + t1[s]);
+  }
+  return m0 - m1;
+}
+
+__device__ __forceinline__ int modadd(int a, int b, int K) { a += b; return a >= K ? a - K : a; }
+__device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 0 ? a + K : a; }
+
+constexpr int RS = 64;  // row stride (floats): 64 lanes
+
+// Buffer-resource row accessor: the 128-bit descriptor (SGPRs) covers one
+// wave's block; a row is addressed by a scalar byte offset (soffset) and the
+// lane by one shared 32-bit VGPR (voffset = 4*lane).  T8/T20 of the CDNA
+// guide: no per-load 64-bit vector addresses, no waterfall loops.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* pu = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pu, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+template <class T>
+struct RowPtr {
+  __amdgpu_buffer_rsrc_t r;
+  int row0;   // first row of this sub-array inside the block
+  int voff;   // 4 * lane
+  __device__ __forceinline__ T ld(int row) const {
+    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(r, voff, (row0 + row) * (RS * 4), 0);
+    if constexpr (sizeof(T) == 4 && (T)0.5f == 0.5f) return __uint_as_float(v);
+    else return (T)v;
+  }
+  __device__ __forceinline__ void st(int row, T v) const {
+    uint32_t u;
+    if constexpr ((T)0.5f == 0.5f) u = __float_as_uint(v);
+    else u = (uint32_t)v;
+    __builtin_amdgcn_raw_buffer_store_b32(u, r, voff, (row0 + row) * (RS * 4), 0);
+  }
+};
+
+// One half-iteration (one constituent decoder pass) for the code block of this lane.
+// All pointers are wave-uniform (scalar) bases; `lane` is the only per-lane
+// offset, so every access is a global load/store with an SGPR base + one
+// shared VGPR offset (no per-load 64-bit vector addresses).
+template <int MODE>
+__device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck,
+                                          uint32_t* __restrict__ wbout, int lane, int K, int f1, int f2,
+                                          bool first) {
+  const int vo = lane * 4;
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * 4));
+  const RowPtr<float> LS{rb, 0, vo};
+  const RowPtr<float> LP{rb, ((MODE == TM_DEC2) ? 2 : 1) * (K + 3), vo};
+  const RowPtr<float> LS2T{rb, 3 * K + 9, vo};
+  const RowPtr<float> LE{rb, 3 * K + 12, vo};
+  const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * 8 * RS * 4)), 0, vo};
+  const RowPtr<uint32_t> bout{make_rsrc(wbout, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
+  const int nfull = K >> 3;
+  const int tf2 = (2 * f2) % K;
+  const bool use_la = !first;
+
+  // ---------------- forward pass: alpha, checkpoint every 8 steps
+  float a[8];
+  a[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; ++s) a[s] = LTE_NEG_BIG;
+  int pi = 0, d = (f1 + f2) % K;
+#pragma unroll 1
+  for (int w = 0; w < nfull; ++w) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ck.st(w * 8 + s, a[s]);
+    float ls[8], lp[8], la[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = w * 8 + j;
+      const int p = (MODE == TM_DEC2) ? pi : k;
+      ls[j] = LS.ld(p);
+      lp[j] = LP.ld(k);
+      la[j] = use_la ? LE.ld(p) : 0.0f;
+      if (MODE == TM_DEC2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float c[4], o[8];
+      gam(ls[j], lp[j], la[j], c);
+      fwd(a, c, o);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) a[s] = o[s];
+    }
+  }
+
+  // ---------------- backward pass
+  float b[8];
+  b[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; ++s) b[s] = LTE_NEG_BIG;
+  // trellis-termination steps k = K+2, K+1, K (only beta is needed there)
+#pragma unroll
+  for (int j = 2; j >= 0; --j) {
+    const int k = K + j;
+    const float ls = (MODE == TM_DEC2) ? LS2T.ld(j) : LS.ld(k);
+    const float lp = LP.ld(k);
+    float c[4], t0[8], t1[8];
+    gam(ls, lp, 0.0f, c);
+    bterms(b, c, t0, t1);
+    bnext(t0, t1, b);
+  }
+  // pi/d are now at k = K; step back to the start of the last full window
+  if (MODE == TM_DEC2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+  }
+  uint32_t acc = 0;
+#pragma unroll 1
+  for (int w = nfull - 1; w >= 0; --w) {
+    float A[8][8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) A[0][s] = ck.ld(w * 8 + s);
+    float ls[8], lp[8], la[8];
+    int pl[8];
+    int pp = pi, dd = d;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = w * 8 + j;
+      const int p = (MODE == TM_DEC2) ? pp : k;
+      pl[j] = p;
+      ls[j] = LS.ld(p);
+      lp[j] = LP.ld(k);
+      la[j] = use_la ? LE.ld(p) : 0.0f;
+      if (MODE == TM_DEC2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      float c[4];
+      gam(ls[j], lp[j], la[j], c);
+      fwd(A[j], c, A[j + 1]);
+    }
+#pragma unroll
+    for (int j = 7; j >= 0; --j) {
+      const int k = w * 8 + j;
+      float c[4], t0[8], t1[8];
+      gam(ls[j], lp[j], la[j], c);
+      bterms(b, c, t0, t1);
+      const float L = llr_app(A[j], t0, t1);
+      if (MODE == TM_DEC1) {
+        LE.st(k, (L - la[j]) - ls[j]);
+      } else if (MODE == TM_DEC2) {
+        LE.st(pl[j], (L - la[j]) - ls[j]);
+      } else if (MODE == TM_APP) {
+        LE.st(k, L);
+      } else {  // TM_FINAL: hard decision (L < 0) packed MSB-first
+        acc |= (L < 0.0f ? 1u : 0u) << (31 - (k & 31));
+        if ((k & 31) == 0) {
+          bout.st(k >> 5, acc);
+          acc = 0;
+        }
+      }
+      bnext(t0, t1, b);
+    }
+    if (MODE == TM_DEC2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+    }
+  }
+}
+
+// grid: ceil(G/4) blocks of 256 threads; wave = one group of 64 code blocks.
+__global__ __launch_bounds__(256) void k_turbo(float* __restrict__ blk, float* __restrict__ ckpt,
+                                               uint32_t* __restrict__ bits, int K, int f1, int f2,
+                                               int iters, int G, int mode) {
+  const int g = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= G) return;
+  float* base = blk + (size_t)g * turbo_rows(K) * RS;
+  float* ck = ckpt + (size_t)g * (turbo_nwin(K) * 8) * RS;
+  uint32_t* bo = bits + (size_t)g * turbo_kw(K) * RS;
+  if (mode == TM_APP) {
+    half_pass<TM_APP>(base, ck, bo, lane, K, f1, f2, false);
+    return;
+  }
+  for (int it = 0; it < iters; ++it) {
+    half_pass<TM_DEC1>(base, ck, bo, lane, K, f1, f2, it == 0);
+    half_pass<TM_DEC2>(base, ck, bo, lane, K, f1, f2, false);
+  }
+  half_pass<TM_FINAL>(base, ck, bo, lane, K, f1, f2, iters == 0);
+}
+
+int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
+                 int G, int mode) {
+  if (G <= 0) return 0;
+  hipLaunchKernelGGL(k_turbo, dim3((G + 3) / 4), dim3(256), 0, s, blk, ckpt, bits, K, f1, f2, iters, G, mode);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// RX rate-dematch + transpose into the decoder layout.
+// Replaces rate_dematching_turbo (rate_matching.py:374-489) composed with the
+// T/F de-interleaver (core/ofdm_core.py:1174-1207): rx_map[t] gives, for LLR t
+// of a frame in RE order, the destination (r<<24 | row) or -1.  A block loads
+// a [64 frames][256 t] tile (coalesced rows), then every wave writes whole
+// 256-B decoder rows.
+constexpr int DM_CH = 256;
+__global__ __launch_bounds__(256) void k_dematch(const float* __restrict__ llr, int T, int B,
+                                                 const int32_t* __restrict__ rx_map,
+                                                 float* const* __restrict__ blk, const int64_t* __restrict__ rows) {
+  __shared__ float tile[64][DM_CH + 1];
+  const int g = blockIdx.y;
+  const int t0 = blockIdx.x * DM_CH;
+  for (int idx = threadIdx.x; idx < 64 * DM_CH; idx += 256) {
+    const int f = idx / DM_CH, c = idx % DM_CH;
+    const int b = g * 64 + f, t = t0 + c;
+    tile[f][c] = (b < B && t < T) ? llr[(size_t)b * T + t] : 0.0f;
+  }
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, f = threadIdx.x & 63;
+  for (int c = wv; c < DM_CH; c += 4) {
+    const int t = t0 + c;
+    if (t >= T) break;
+    const int m = rx_map[t];
+    if (m < 0) continue;
+    const int r = m >> 24, row = m & 0xFFFFFF;
+    blk[r][((size_t)g * rows[r] + row) * RS + f] = tile[f][c];
+  }
+}
+
+int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
+                   const int64_t* rows, int C) {
+  (void)C;
+  const int G = (B + 63) / 64;
+  hipLaunchKernelGGL(k_dematch, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B, rx_map, blk, rows);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// TX: CB construction (segmentation.py:212-247 + CRC-24B crc.py:162-184) and
+// turbo encoding (turbo_encoder.py:137-313).  One lane = one (CB slot, frame).
+struct BitWriter {
+  uint32_t* p;
+  uint32_t acc;
+  int n;
+  __device__ void put(uint32_t bit) {
+    acc = (acc << 1) | bit;
+    if (++n == 32) { *p++ = acc; acc = 0; n = 0; }
+  }
+  __device__ void flush() {
+    if (n) { *p = acc << (32 - n); }
+  }
+};
+
+__global__ __launch_bounds__(256) void k_encode(const uint32_t* __restrict__ pw, int PW, uint32_t* __restrict__ cbw,
+                                                int KWmax, uint32_t* __restrict__ enc, int EW,
+                                                const CbInfo* __restrict__ cbi, int C, int B) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= C * B) return;
+  const int r = gid / B, b = gid % B;
+  const CbInfo ci = cbi[r];
+  const int K = ci.K;
+  const uint32_t* tb = pw + (size_t)b * PW;
+  uint32_t* cw = cbw + ((size_t)b * C + r) * KWmax;
+  uint32_t* e = enc + ((size_t)b * C + r) * 3 * EW;
+  BitWriter w0{e, 0, 0}, w1{e + EW, 0, 0}, w2{e + 2 * EW, 0, 0}, wc{cw, 0, 0};
+  const int Kd = ci.crc ? K - 24 : K;
+  uint32_t crc = 0, s0 = 0, s1 = 0, s2 = 0;
+  for (int p = 0; p < K; ++p) {
+    uint32_t bit;
+    if (p < ci.F) bit = 0;
+    else if (p < ci.F + ci.info) bit = getbit(tb, (int64_t)ci.off + p - ci.F);
+    else bit = (crc >> (23 - (p - Kd))) & 1u;
+    if (ci.crc && p < Kd) {
+      const uint32_t msb = (crc >> 23) & 1u;
+      crc = (crc << 1) & 0xFFFFFFu;
+      if (msb ^ bit) crc ^= 0x800063u;  // CRC-24B (0x1800063)
+    }
+    wc.put(bit);
+    const uint32_t fb = bit ^ s1 ^ s2;
+    w0.put(fb);                 // "systematic" = feedback bit (Q13)
+    w1.put(fb ^ s0 ^ s2);
+    s2 = s1; s1 = s0; s0 = fb;
+  }
+  wc.flush();
+  for (int t = 0; t < 3; ++t) {  // trellis termination, encoder 1
+    const uint32_t tail = s1 ^ s2, fb = tail ^ s1 ^ s2;
+    w0.put(fb);
+    w1.put(fb ^ s0 ^ s2);
+    s2 = s1; s1 = s0; s0 = fb;
+  }
+  w1.flush();
+  // encoder 2 on the QPP-interleaved block
+  s0 = s1 = s2 = 0;
+  int pi = 0, d = (ci.f1 + ci.f2) % K;
+  const int tf2 = (2 * ci.f2) % K;
+  for (int i = 0; i < K; ++i) {
+    const uint32_t bit = getbit(cw, pi);
+    const uint32_t fb = bit ^ s1 ^ s2;
+    w2.put(fb ^ s0 ^ s2);
+    s2 = s1; s1 = s0; s0 = fb;
+    pi += d; if (pi >= K) pi -= K;
+    d += tf2; if (d >= K) d -= K;
+  }
+  for (int t = 0; t < 3; ++t) {
+    const uint32_t tail = s1 ^ s2, fb = tail ^ s1 ^ s2;
+    w0.put(fb);                 // sys2 tail -> d0[K+3..K+5]
+    w2.put(fb ^ s0 ^ s2);
+    s2 = s1; s1 = s0; s0 = fb;
+  }
+  w0.flush();
+  w2.flush();
+}
+
+int launch_encode(hipStream_t s, const uint32_t* pw, int PW, uint32_t* cbw, int KWmax, uint32_t* enc, int EW,
+                  const CbInfo* cbi_dev, int C, int B) {
+  const int n = C * B;
+  hipLaunchKernelGGL(k_encode, dim3((n + 255) / 256), dim3(256), 0, s, pw, PW, cbw, KWmax, enc, EW, cbi_dev, C, B);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// CRC-24A / desegmentation / bit-error count.  One lane per frame; lanes of a
+// wave are 64 consecutive frames = one decoder group, so the decoded-word
+// reads are coalesced rows.  Replaces desegment_code_blocks
+// (segmentation.py:266-359), check_crc24a (crc.py:277-307) and the BER count
+// (core/ofdm_core.py:1304-1311).
+__device__ __forceinline__ uint32_t crc24_table_entry(uint32_t i, uint32_t poly) {
+  uint32_t r = i << 16;
+  for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? ((r << 1) ^ poly) : (r << 1);
+  return r & 0xFFFFFFu;
+}
+
+// 32 bits starting at bit position p of an MSB-first stream whose words are
+// strided by `st` elements.
+__device__ __forceinline__ uint32_t get32s(const uint32_t* w, int64_t st, int64_t p, int64_t nwords) {
+  const int64_t i = p >> 5;
+  const int o = (int)(p & 31);
+  const uint32_t a = w[i * st];
+  if (o == 0) return a;
+  const uint32_t b = (i + 1 < nwords) ? w[(i + 1) * st] : 0u;
+  return (a << o) | (b >> (32 - o));
+}
+
+__global__ __launch_bounds__(256) void k_crc_count(const CbInfo* __restrict__ cbi, int C,
+                                                   uint32_t* const* __restrict__ dec, const int* __restrict__ KW,
+                                                   int B, const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                   uint32_t* __restrict__ frame_err, uint32_t* __restrict__ frame_crc,
+                                                   uint8_t* __restrict__ cap_bits) {
+  __shared__ uint32_t T[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_table_entry(i, 0x864CFBu);
+  __syncthreads();
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int g = b >> 6, lane = b & 63;
+  const uint32_t* tx = pw + (size_t)b * PW;
+  const int Btb = n_bits + 24;
+  const int nw = (Btb + 31) >> 5;
+  uint32_t crc = 0, err = 0, rx_crc = 0;
+  int r = 0;
+  for (int w = 0; w < nw; ++w) {
+    // assemble TB word w (bits 32w .. 32w+31) from the decoded code blocks
+    uint32_t word = 0;
+    int got = 0;
+    const int want = min(32, Btb - 32 * w);
+    while (got < want) {
+      const int j = 32 * w + got;  // TB position
+      while (j >= cbi[r].off + cbi[r].info) ++r;
+      const CbInfo ci = cbi[r];
+      const int avail = min(want - got, ci.off + ci.info - j);
+      const int64_t pcb = (int64_t)ci.F + (j - ci.off);
+      const uint32_t* base = dec[r] + (size_t)g * KW[r] * 64 + lane;
+      const uint32_t v = get32s(base, 64, pcb, KW[r]);
+      const uint32_t m = avail >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> avail);
+      word |= (v & m) >> got;
+      got += avail;
+    }
+    // CRC over data bits [0, n_bits), byte-wise table (MSB-first)
+    const int dbits = min(32, max(0, n_bits - 32 * w));
+    int k = 0;
+    for (; k + 8 <= dbits; k += 8) {
+      const uint32_t byte = (word >> (24 - k)) & 0xFFu;
+      crc = ((crc << 8) & 0xFFFFFFu) ^ T[((crc >> 16) ^ byte) & 0xFFu];
+    }
+    for (; k < dbits; ++k) {
+      const uint32_t bit = (word >> (31 - k)) & 1u;
+      const uint32_t msb = (crc >> 23) & 1u;
+      crc = (crc << 1) & 0xFFFFFFu;
+      if (msb ^ bit) crc ^= 0x864CFBu;
+    }
+    // received CRC bits [n_bits, n_bits+24)
+    for (int q = max(0, n_bits - 32 * w); q < want; ++q) rx_crc = (rx_crc << 1) | ((word >> (31 - q)) & 1u);
+    if (dbits > 0) {
+      const uint32_t m = dbits >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> dbits);
+      err += __popc((word ^ tx[w]) & m);
+    }
+    if (cap_bits) {
+      for (int q = 0; q < dbits; ++q) cap_bits[(size_t)b * n_bits + 32 * w + q] = (word >> (31 - q)) & 1u;
+    }
+  }
+  frame_err[b] = err;
+  frame_crc[b] = (crc == rx_crc) ? 1u : 0u;
+}
+
+int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
+                     const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
+                     uint8_t* cap_bits) {
+  hipLaunchKernelGGL(k_crc_count, dim3((B + 255) / 256), dim3(256), 0, s, cbi_dev, C, dec, KW, B, pw, PW, n_bits,
+                     frame_err, frame_crc, cap_bits);
+  return (int)hipGetLastError();
+}
+
+}  // namespace lte

@@ -1,0 +1,204 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  Never linked into, called by, or shipped
+ * with the product path (ofdm-lte_amd/).  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg load it, as the checker / CPU baseline.
+ *
+ * Plain-C restatement (float64, same operation order) of the serial loops of
+ * the reference's channel-coding chain, so that the oracle is bit-exact with
+ * the reference while being fast enough to time as a CPU baseline:
+ *
+ *   or_crc            <- core/channel_coding/crc.py:89-134   (_calculate_crc,
+ *                        MSB-first long division == zero-init LFSR)
+ *   or_rsc_encode     <- core/channel_coding/turbo_encoder.py:137-211
+ *   or_bcjr_maxlog    <- core/channel_coding/turbo_decoder.py:181-335
+ *                        (LogMAPDecoder.decode + _compute_gamma, USE_MAX_LOG_MAP)
+ *   or_turbo_decode   <- core/channel_coding/turbo_decoder.py:338-450
+ *
+ * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off: no FMA contraction,
+ * so every add/sub rounds exactly like the NumPy float64 reference).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* crc.py:89-134. poly includes the x^len term (0x1864CFB for CRC-24A). */
+uint32_t or_crc(const uint8_t *bits, int64_t n, uint32_t poly, int len)
+{
+    const uint32_t mask = (len >= 32) ? 0xFFFFFFFFu : ((1u << len) - 1u);
+    const uint32_t p = poly & mask;
+    uint32_t reg = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        uint32_t msb = (reg >> (len - 1)) & 1u;
+        reg = (reg << 1) & mask;
+        if (msb ^ (bits[i] & 1u)) reg ^= p;
+    }
+    return reg;
+}
+
+/* turbo_encoder.py:137-211 — "systematic" output is the feedback bit a_k. */
+void or_rsc_encode(const uint8_t *in, int K, uint8_t *sys, uint8_t *par)
+{
+    uint8_t s0 = 0, s1 = 0, s2 = 0;
+    for (int k = 0; k < K; ++k) {
+        uint8_t fb = (in[k] + s1 + s2) & 1;
+        sys[k] = fb;
+        par[k] = (fb + s0 + s2) & 1;
+        s2 = s1; s1 = s0; s0 = fb;
+    }
+    for (int t = 0; t < 3; ++t) {
+        uint8_t tail = (s1 + s2) & 1;
+        uint8_t fb = (tail + s1 + s2) & 1;
+        sys[K + t] = fb;
+        par[K + t] = (fb + s0 + s2) & 1;
+        s2 = s1; s1 = s0; s0 = fb;
+    }
+}
+
+/* Trellis of turbo_decoder.py:137-179: state = (s0<<2)|(s1<<1)|s2. */
+static int NS[8][2], OS[8][2], OP[8][2];
+static int trellis_ready = 0;
+static void build_trellis(void)
+{
+    if (trellis_ready) return;
+    for (int st = 0; st < 8; ++st) {
+        int s0 = (st >> 2) & 1, s1 = (st >> 1) & 1, s2 = st & 1;
+        for (int u = 0; u < 2; ++u) {
+            int fb = (u + s1 + s2) % 2;
+            NS[st][u] = (fb << 2) | (s0 << 1) | s1;
+            OS[st][u] = fb;
+            OP[st][u] = (fb + s0 + s2) % 2;
+        }
+    }
+    trellis_ready = 1;
+}
+
+/* Python's builtin max(a, b): keeps a unless b > a. */
+static inline double pymax(double a, double b) { return (b > a) ? b : a; }
+
+/*
+ * LogMAPDecoder.decode (turbo_decoder.py:181-278) with max_star = max.
+ * n = K_extended (data + 3 tail steps).  Writes the a-posteriori LLR.
+ * Scratch: alpha/beta (n+1)*8, gamma n*16 doubles.
+ */
+void or_bcjr_maxlog(const double *Ls, const double *Lp, const double *La,
+                    int n, double *Lapp, double *scratch)
+{
+    build_trellis();
+    double *alpha = scratch;
+    double *beta = alpha + (size_t)(n + 1) * 8;
+    double *gamma = beta + (size_t)(n + 1) * 8;
+    for (int i = 0; i < (n + 1) * 8; ++i) { alpha[i] = -INFINITY; beta[i] = -INFINITY; }
+    alpha[0] = 0.0;
+    beta[(size_t)n * 8 + 0] = 0.0;
+    /* _compute_gamma :280-335 : (sys + par) + apr, each = +/- L / 2.0 */
+    for (int k = 0; k < n; ++k) {
+        for (int st = 0; st < 8; ++st) {
+            for (int u = 0; u < 2; ++u) {
+                double sm = OS[st][u] == 0 ? Ls[k] / 2.0 : -Ls[k] / 2.0;
+                double pm = OP[st][u] == 0 ? Lp[k] / 2.0 : -Lp[k] / 2.0;
+                double am = u == 0 ? La[k] / 2.0 : -La[k] / 2.0;
+                gamma[(size_t)k * 16 + st * 2 + u] = sm + pm + am;
+            }
+        }
+    }
+    /* forward :227-235 */
+    for (int k = 0; k < n; ++k) {
+        for (int ns = 0; ns < 8; ++ns) {
+            double mv = -INFINITY;
+            for (int ps = 0; ps < 8; ++ps)
+                for (int u = 0; u < 2; ++u)
+                    if (NS[ps][u] == ns)
+                        mv = pymax(mv, alpha[(size_t)k * 8 + ps] + gamma[(size_t)k * 16 + ps * 2 + u]);
+            alpha[(size_t)(k + 1) * 8 + ns] = mv;
+        }
+    }
+    /* backward :238-245 */
+    for (int k = n - 1; k >= 0; --k) {
+        for (int ps = 0; ps < 8; ++ps) {
+            double mv = -INFINITY;
+            for (int u = 0; u < 2; ++u) {
+                int ns = NS[ps][u];
+                mv = pymax(mv, beta[(size_t)(k + 1) * 8 + ns] + gamma[(size_t)k * 16 + ps * 2 + u]);
+            }
+            beta[(size_t)k * 8 + ps] = mv;
+        }
+    }
+    /* LLR :250-265 */
+    for (int k = 0; k < n; ++k) {
+        double l0 = -INFINITY, l1 = -INFINITY;
+        for (int st = 0; st < 8; ++st) {
+            for (int u = 0; u < 2; ++u) {
+                int ns = NS[st][u];
+                double v = alpha[(size_t)k * 8 + st] + gamma[(size_t)k * 16 + st * 2 + u] +
+                           beta[(size_t)(k + 1) * 8 + ns];
+                if (u == 0) l0 = pymax(l0, v); else l1 = pymax(l1, v);
+            }
+        }
+        Lapp[k] = l0 - l1;
+    }
+}
+
+size_t or_bcjr_scratch_doubles(int n) { return (size_t)(n + 1) * 16 + (size_t)n * 16; }
+
+/*
+ * turbo_decode (turbo_decoder.py:338-450).  llr = [3K+12] rate-dematched LLRs,
+ * perm = QPP pi(i) (turbo_encoder.py:76-102).  out = K hard bits.
+ * If ext_trace != NULL it receives the decoder-2 output (extrinsic_2to1,
+ * natural order, K values) of every iteration: [iters][K].
+ */
+void or_turbo_decode(const double *llr, int K, int iters, const int32_t *perm,
+                     uint8_t *out, double *ext_trace)
+{
+    const int n = K + 3;
+    double *ls1 = (double *)malloc(sizeof(double) * n);
+    double *lp1 = (double *)malloc(sizeof(double) * n);
+    double *ls2 = (double *)malloc(sizeof(double) * n);
+    double *lp2 = (double *)malloc(sizeof(double) * n);
+    double *la = (double *)malloc(sizeof(double) * n);
+    double *lapp = (double *)malloc(sizeof(double) * n);
+    double *e12 = (double *)calloc(K, sizeof(double));
+    double *e21 = (double *)calloc(K, sizeof(double));
+    double *scr = (double *)malloc(sizeof(double) * or_bcjr_scratch_doubles(n));
+    for (int k = 0; k < K; ++k) {
+        ls1[k] = llr[3 * k];
+        lp1[k] = llr[3 * k + 1];
+        lp2[k] = llr[3 * k + 2];
+    }
+    for (int t = 0; t < 3; ++t) {
+        ls1[K + t] = llr[3 * K + t];
+        lp1[K + t] = llr[3 * K + 3 + t];
+        ls2[K + t] = llr[3 * K + 6 + t];
+        lp2[K + t] = llr[3 * K + 9 + t];
+    }
+    /* llr_systematic_interleaved = qpp_interleave(llr_systematic[:K]) :424 */
+    for (int k = 0; k < K; ++k) ls2[k] = ls1[perm[k]];
+    for (int it = 0; it < iters; ++it) {
+        for (int k = 0; k < K; ++k) la[k] = e21[k];
+        la[K] = la[K + 1] = la[K + 2] = 0.0;
+        or_bcjr_maxlog(ls1, lp1, la, n, lapp, scr);
+        /* extrinsic = lapp - la - ls :270 */
+        for (int k = 0; k < K; ++k) e12[k] = lapp[k] - la[k] - ls1[k];
+        for (int k = 0; k < K; ++k) la[k] = e12[perm[k]];
+        la[K] = la[K + 1] = la[K + 2] = 0.0;
+        or_bcjr_maxlog(ls2, lp2, la, n, lapp, scr);
+        /* qpp_deinterleave: out[perm[i]] = in[i] */
+        for (int k = 0; k < K; ++k) e21[perm[k]] = lapp[k] - la[k] - ls2[k];
+        if (ext_trace) memcpy(ext_trace + (size_t)it * K, e21, sizeof(double) * K);
+    }
+    for (int k = 0; k < K; ++k) la[k] = e21[k];
+    la[K] = la[K + 1] = la[K + 2] = 0.0;
+    or_bcjr_maxlog(ls1, lp1, la, n, lapp, scr);
+    for (int k = 0; k < K; ++k) out[k] = lapp[k] < 0.0 ? 1 : 0;
+    free(ls1); free(lp1); free(ls2); free(lp2); free(la); free(lapp);
+    free(e12); free(e21); free(scr);
+}
+
+/* Batched convenience wrapper: ncb code blocks of equal K. */
+void or_turbo_decode_batch(const double *llr, int ncb, int K, int iters,
+                           const int32_t *perm, uint8_t *out)
+{
+    for (int c = 0; c < ncb; ++c)
+        or_turbo_decode(llr + (size_t)c * (3 * K + 12), K, iters, perm,
+                        out + (size_t)c * K, NULL);
+}

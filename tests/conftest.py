@@ -1,0 +1,51 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, 'ofdm-lte_amd')
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, 'tests', 'golden', 'golden.npz')
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (gfx950) GPU; runs the HIP path')
+
+
+def _gpu_present():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if _gpu_present() or os.environ.get('LTE_REQUIRE_GPU'):
+        return
+    skip = pytest.mark.skip(reason='no GPU in this container (run with -m gpu on an MI355X)')
+    for it in items:
+        if 'gpu' in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture(scope='session')
+def golden():
+    return np.load(GOLDEN, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def oracle():
+    from oracle import lte_oracle
+    lte_oracle.lib()
+    return lte_oracle
+
+
+def unpack(a, n=None):
+    b = np.unpackbits(np.asarray(a, dtype=np.uint8))
+    return b if n is None else b[:n]

@@ -1,0 +1,177 @@
+"""Headline benchmark: LTE subframes/s through the full coded chain
+(config 2: 20 MHz, 64-QAM, Rayleigh ITU Pedestrian-A, turbo max-log-MAP x8,
+TB 27 760 bits = 5 code blocks = 14 OFDM symbols), BER sweep SNR 0:2:30 dB.
+
+One step = one batch of `--frames` subframes per GPU pushed TX -> channel ->
+RX + turbo; all inputs (Philox bits / fading / noise) are generated on the
+device.  N>1: one process per GPU (torch.distributed, RCCL); frames are
+partitioned by global frame id (weak scaling, no data-path collective); the
+only collective is the SUM of the BER counters (and MAX of the step time).
+
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, 'ofdm-lte_amd')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "LTE subframes/sec (20 MHz, 64-QAM, Rayleigh+turbo) at 1/2/4/8 GPU; BER match"
+SNRS = np.arange(0, 31, 2, dtype=np.float64)
+TB = 27760
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_baseline(seconds=15.0):
+    """Time the oracle (float64 CPU restatement: NumPy front end + C turbo
+    decoder, bit-exact with the reference) on this host, one core, on a bounded
+    sample of the same workload (config-2 coded subframes cycling over SNRs)."""
+    from oracle import lte_oracle as O
+    O.lib()
+    num = O.Numerology(bandwidth=20.0, modulation='64-QAM')
+    L = 14 * (num.N + num.cp)
+    rs = np.random.RandomState(1234)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        bits = rs.randint(0, 2, TB)
+        d = [{'phases': [2 * np.pi * rs.rand(16) for _ in range(4)], 'z_re': rs.randn(L), 'z_im': rs.randn(L)}]
+        O.simulate_siso_coded(num, bits, float(SNRS[n % len(SNRS)]), 'rayleigh_mp', draws=d)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {'value': n / el, 'unit': 'subframes/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{n} config-2 coded subframes (TB {TB}, 8 it.) over SNR 0:2:30 dB, '
+                      f'{el:.1f} s on 1 host core (oracle: NumPy + C, float64)'}
+
+
+def load_traffic():
+    """HBM bytes per turbo launch from the committed rocprofv3 --pmc summary."""
+    p = os.path.join(ROOT, 'profiles', 'pmc_turbo_traffic.json')
+    if os.path.exists(p):
+        try:
+            return json.load(open(p))
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--frames', type=int, default=16384, help='subframes per step per GPU')
+    ap.add_argument('--iters', type=int, default=8)
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--no-cpu', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(local)
+
+    import lte_phy
+    from lte_phy import _capi as C
+    C.device_init(local)
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=20.0, modulation='64-QAM'),
+                                channel_type='rayleigh_mp', itu_profile='Pedestrian_A')
+    F = int(args.frames)
+    plan = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=F, iters=args.iters)
+    S = len(SNRS)
+    counts = np.zeros((S, 4), dtype=np.uint64)
+
+    def step(k):
+        ids = (np.uint64(k * world + rank) * np.uint64(F) + np.arange(F, dtype=np.uint64))
+        si = (ids % np.uint64(S)).astype(np.int32)
+        r = plan.run(SNRS[si], snr_index=si, n_snr=S, seed=0x5EED, frame_ids=ids)
+        return r['counts']
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for w in range(args.warmup):
+        step(10_000 + w)
+    plan.timing_reset()
+    plan.timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        counts += step(k)
+    barrier()
+    el = time.perf_counter() - t0
+    plan.timing(False)
+    tim = plan.timing_read()
+
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        c = torch.tensor(counts.astype(np.int64), device='cuda')
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        counts = c.cpu().numpy().astype(np.uint64)
+
+    total = F * args.steps * world
+    value = total / el
+    # dominant kernel: turbo decoder.  Algorithmic bytes per launch (SURVEY §8d
+    # per-CB figure x CBs per launch): its compulsory input = the rate-dematched
+    # f32 LLRs (3K+12 per CB) + output = K decoded bits per CB.
+    t_ms, t_n = tim.get('turbo', (0.0, 0))
+    from lte_phy.channel_coding import segmentation_sizes
+    cb_K = segmentation_sizes(TB + 24)
+    Fp = ((F + 63) // 64) * 64
+    alg_bytes_total = sum(Fp * ((3 * K + 12) * 4 + K / 8) for K in cb_K) * args.steps
+    avg_launch_ms = t_ms / max(t_n, 1)
+    alg_per_launch = alg_bytes_total / max(t_n, 1)
+    achieved = alg_per_launch / (avg_launch_ms * 1e-3) / 1e9 if t_n else 0.0
+    traffic = load_traffic()
+    roof = {'bound': 'hbm', 'kernel': 'k_turbo', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
+            'traffic': (traffic or {}).get('bytes_per_launch'),
+            'avg_launch_ms': round(avg_launch_ms, 3), 'launches': t_n,
+            'alg_bytes_per_launch': int(alg_per_launch),
+            'turbo_share_of_step': round(t_ms / (el * 1e3 / world) if el > 0 else 0, 3),
+            'kernel_ms': {k: round(v[0], 2) for k, v in tim.items() if v[1]}}
+    ber = (counts[:, 0] / np.maximum(counts[:, 1], 1)).tolist()
+    bler = (counts[:, 2] / np.maximum(counts[:, 3], 1)).tolist()
+    out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'subframes/s', 'n_gpus': world,
+           'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el * 1e3 / args.steps, 3),
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+           'data': 'synthetic (Philox4x32-10 payload bits, Jakes phases and AWGN generated on the GPU)',
+           'config': {'workload': 'config 2: SISO 20 MHz (N=2048) 64-QAM, Rayleigh ITU Pedestrian-A, '
+                                  'turbo max-log-MAP 8 it., TB 27760 (5 CBs, 14 OFDM symbols), SNR 0:2:30 dB',
+                      'frames_per_step_per_gpu': F, 'global_batch': F * world, 'parallelism': f'dp{world}',
+                      'snr_db': SNRS.tolist()},
+           'roofline': roof,
+           'ber': [float(f'{b:.4e}') for b in ber], 'bler': [float(f'{b:.4e}') for b in bler]}
+    if rank == 0:
+        if world == 1 and not args.no_cpu:
+            out['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
+        else:
+            out['cpu_baseline'] = None
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

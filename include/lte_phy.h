@@ -39,6 +39,7 @@ enum {
 enum { LTE_CH_AWGN = 0, LTE_CH_RAYLEIGH = 1 }; /* core/channel.py:10-245 */
 
 #define LTE_MAX_PATHS 16
+enum { LTE_STAGE_TX = 1, LTE_STAGE_CHANNEL = 2, LTE_STAGE_RX = 4, LTE_STAGE_ALL = 7 };
 
 /* Plan descriptor.  Numerology follows LTEConfig (config.py:101-130); the
  * resource grid (guards, DC, pilot every 6th SC) is derived from N, Nc exactly
@@ -85,6 +86,11 @@ typedef struct {
   uint64_t *counts;            /* host [n_snr][4] += {bit_err, bits, blk_err, blks} */
   uint32_t *frame_errors;      /* host [n_frames] optional                         */
   uint8_t *frame_crc_ok;       /* host [n_frames] optional (coded)                 */
+  /* stage selection (LTE_STAGE_* bitmask, 0 = all).  Without LTE_STAGE_TX the
+   * time-domain TX signal comes from in_signal; without LTE_STAGE_CHANNEL,
+   * in_signal is taken as the already-received signal (no fading, no noise). */
+  int32_t stages;
+  const float *in_signal; int64_t in_signal_stride; /* [.][L] complex64 */
   /* captures (host, optional; used by the single-call Python API) */
   float *cap_signal_tx;        /* [n_frames][L] complex64                           */
   float *cap_signal_rx;        /* [n_frames][num_rx][L] complex64 (noisy)           */
@@ -94,6 +100,7 @@ typedef struct {
   uint8_t *cap_bits_rx;        /* [n_frames][n_bits]                                */
   float *cap_llr;              /* [n_frames][n_sym*Nd*bps] (coded, RE order)        */
   float *cap_noise_power;      /* [n_frames][num_rx]                                */
+  float *cap_tx_syms;          /* [n_frames][n_sym*Nd] complex64 TX data REs        */
 } lte_run_args;
 
 /* Library / device. */
@@ -133,6 +140,14 @@ int lte_turbo_decode_host(int K, int iters, int64_t ncb, const float *llr /*[ncb
 int lte_bcjr_host(int K, int64_t ncb, const float *ls, const float *lp, const float *la, float *app);
 /* CRC: _calculate_crc core/channel_coding/crc.py:89-134 (MSB-first, zero init) */
 int lte_crc_host(int64_t n, const uint8_t *bits, uint32_t poly, int len, uint32_t *crc);
+/* Channel on an arbitrary-length stream: ChannelSimulator.transmit (core/channel.py:
+ * 334-345) = RayleighChannel.filter (rayleighchannel.py:44-58) + measured-power
+ * AWGN (channel.py:34-68, 203-234).  x [L] complex64 -> y [num_rx][L] complex64.
+ * phases [num_rx][n_paths][16] (NULL -> Philox(seed)), noise [num_rx][2][L]
+ * unit normals (NULL -> Philox(seed)). */
+int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int32_t *delays, const double *gains,
+                     double fD, double fs, double snr_db, uint64_t seed, const float *x, const double *phases,
+                     const double *noise, float *y, float *noise_power);
 /* Rate dematching map: rate_dematching_turbo core/channel_coding/rate_matching.py:374-489
  * src[j] = index into the E rate-matched LLRs feeding output j of [3K+12], -1 = zero. */
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t *src);

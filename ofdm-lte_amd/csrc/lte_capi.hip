@@ -302,8 +302,9 @@ namespace lte {
 __global__ void k_cap_rx(int L, int num_rx, int B, const float2* __restrict__ y, int64_t y_rx_stride,
                          int64_t y_frame_stride, const float* __restrict__ npow, const uint64_t* __restrict__ fid,
                          uint64_t seed, const float* __restrict__ inj_z, int64_t inj_stride, float2* __restrict__ out) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  const int rx = blockIdx.y, b = blockIdx.z;
+  const int nb = (L + 255) / 256;
+  const int n = (blockIdx.x % nb) * blockDim.x + threadIdx.x;
+  const int rx = blockIdx.y, b = blockIdx.x / nb;
   if (n >= L) return;
   const float sigma = sqrtf(npow[(size_t)b * num_rx + rx] * 0.5f);
   float2 z;
@@ -335,7 +336,7 @@ struct lte_plan {
   DBuf<int32_t> tx_map, rx_map, delays;
   DBuf<float> gains;
   DBuf<uint32_t> pw, cbw, enc, inj_bits;
-  DBuf<float2> x, y, coef, H, capbuf;
+  DBuf<float2> x, y, coef, H, capbuf, captx;
   DBuf<float> phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
   DBuf<uint32_t> frame_err, frame_crc;
   DBuf<int32_t> snr_idx;
@@ -429,6 +430,69 @@ int lte_pilots(int cell_id, int n, double* out) {
   make_pilots(cell_id, n, v);
   std::memcpy(out, v.data(), v.size() * sizeof(double));
   return LTE_OK;
+}
+
+int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int32_t* delays, const double* gains,
+                     double fD, double fs, double snr_db, uint64_t seed, const float* x, const double* phases,
+                     const double* noise, float* y, float* noise_power) {
+  if (L < 1 || L > (1LL << 30) || num_rx < 1 || !x || !y) return fail(LTE_EINVAL, "bad channel arguments");
+  const bool ray = channel == LTE_CH_RAYLEIGH;
+  if (!ray && channel != LTE_CH_AWGN) return fail(LTE_EINVAL, "Tipo de canal desconocido");
+  if (ray && (n_paths < 1 || n_paths > LTE_MAX_PATHS || !delays || !gains)) return fail(LTE_EINVAL, "bad paths");
+  Grid g{};
+  g.L = (int)L;
+  const int nblk = (int)((L + 255) / 256);
+  DBuf<float2> dx, dy, dcoef, dout;
+  DBuf<float> dph, dpp, dsl, dnp, dz, dgain, dinj;
+  DBuf<int32_t> ddel;
+  DBuf<uint64_t> dfid;
+  int rc = LTE_OK;
+  auto cleanup = [&]() {
+    dx.release(); dy.release(); dcoef.release(); dout.release(); dph.release(); dpp.release(); dsl.release();
+    dnp.release(); dz.release(); dgain.release(); dinj.release(); ddel.release(); dfid.release();
+  };
+  if (dx.alloc(L) || dout.alloc((size_t)num_rx * L) || dpp.alloc((size_t)num_rx * nblk) || dsl.alloc(1) ||
+      dnp.alloc(num_rx) || dfid.alloc(1) || (ray && (dy.alloc((size_t)num_rx * L) ||
+      dcoef.alloc((size_t)num_rx * n_paths) || dph.alloc((size_t)num_rx * n_paths * 16)))) {
+    cleanup();
+    return fail(LTE_ENOMEM, "channel buffers");
+  }
+  const float sl = (float)std::pow(10.0, snr_db / 10.0);
+  const uint64_t fid0 = 0;
+  std::vector<float> hz, hp, hg;
+  bool ok = hipMemcpy(dx.p, x, L * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dsl.p, &sl, 4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dfid.p, &fid0, 8, hipMemcpyHostToDevice) == hipSuccess;
+  if (ok && ray) {
+    std::vector<int32_t> dl(delays, delays + n_paths);
+    hg.assign(gains, gains + n_paths);
+    ok = upload(ddel, dl) == 0 && upload(dgain, hg) == 0;
+    if (ok && phases) {
+      hp.assign(phases, phases + (size_t)num_rx * n_paths * 16);
+      ok = upload(dinj, hp) == 0;
+    }
+    ok = ok && launch_fading(nullptr, 1, num_rx, n_paths, dgain.p, dfid.p, seed, phases ? dinj.p : nullptr, 0,
+                             dph.p, dcoef.p) == 0;
+  }
+  if (ok && noise) {
+    hz.assign(noise, noise + (size_t)num_rx * 2 * L);
+    ok = upload(dz, hz) == 0;
+  }
+  ok = ok && launch_channel(nullptr, g, 1, num_rx, ray ? 1 : 0, n_paths, ddel.p, dgain.p, (float)fD, (float)fs,
+                            dph.p, dcoef.p, dx.p, dy.p, dpp.p, nblk) == 0;
+  ok = ok && launch_npow(nullptr, 1, num_rx, dpp.p, nblk, (int)L, dsl.p, dnp.p) == 0;
+  if (ok) {
+    const float2* ys = ray ? dy.p : dx.p;
+    hipLaunchKernelGGL(k_cap_rx, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
+                       1, ys, ray ? L : 0, ray ? (int64_t)num_rx * L : L, dnp.p, dfid.p, seed,
+                       noise ? dz.p : nullptr, 0, dout.p);
+    ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+         hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(float2), hipMemcpyDeviceToHost) == hipSuccess &&
+         (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess);
+  }
+  if (!ok) rc = fail(LTE_EHIP, std::string("channel failed: ") + hipGetErrorString(hipGetLastError()));
+  cleanup();
+  return rc;
 }
 
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t* src) {
@@ -676,7 +740,7 @@ int lte_plan_destroy(lte_plan* p) {
   p->tabs.release();
   p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release(); p->gains.release();
   p->pw.release(); p->cbw.release(); p->enc.release(); p->inj_bits.release();
-  p->x.release(); p->y.release(); p->coef.release(); p->H.release(); p->capbuf.release();
+  p->x.release(); p->y.release(); p->coef.release(); p->H.release(); p->capbuf.release(); p->captx.release();
   p->phases.release(); p->pow_part.release(); p->pstats.release(); p->npow.release(); p->llr.release();
   p->snr_lin.release(); p->inj_ph.release(); p->inj_z.release();
   p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->fid.release(); p->counts.release();
@@ -741,7 +805,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (B < 1 || B > d.max_frames) return fail(LTE_EINVAL, "n_frames out of range (1..max_frames)");
   if (!a->snr_db) return fail(LTE_EINVAL, "snr_db required");
   const int n_snr = std::max(1, a->n_snr);
-  const bool coded = d.chain == LTE_CHAIN_CODED, ray = d.channel == LTE_CH_RAYLEIGH;
+  const bool coded = d.chain == LTE_CHAIN_CODED, ray_cfg = d.channel == LTE_CH_RAYLEIGH;
   const int rx = d.num_rx;
   hipStream_t s = p->stream;
   if (p->counts.alloc((size_t)4 * n_snr)) return fail(LTE_ENOMEM, "counts");
@@ -777,7 +841,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   const float* inj_ph = nullptr;
   int64_t inj_ph_stride = 0;
   std::vector<float> hph;
-  if (a->phases && ray) {
+  if (a->phases && ray_cfg) {
     const int nf = a->phases_stride ? B : 1;
     const size_t per = (size_t)rx * d.n_paths * 16;
     hph.resize(nf * per);
@@ -804,19 +868,41 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   }
   HIPCHK(hipMemsetAsync(p->counts.p, 0, 4 * n_snr * sizeof(unsigned long long), s));
   HIPCHK(hipMemsetAsync(p->frame_err.p, 0, B * sizeof(uint32_t), s));
+  const int stages = a->stages ? a->stages : LTE_STAGE_ALL;
+  const bool do_tx = stages & LTE_STAGE_TX, do_ch = stages & LTE_STAGE_CHANNEL, do_rx = stages & LTE_STAGE_RX;
+  if (!do_tx && !a->in_signal) return fail(LTE_EINVAL, "in_signal required when the TX stage is skipped");
   const Grid& g = p->grid;
   p->evuse.clear();
-  {
+  if (do_tx || a->bits) {
     Timer t(p, KN_PAYLOAD);
     LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
   }
-  if (coded) {
-    Timer t(p, KN_ENCODE);
-    LCHK(launch_encode(s, p->pw.p, p->PW, p->cbw.p, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
-  }
-  {
+  if (do_tx) {
+    if (coded) {
+      Timer t(p, KN_ENCODE);
+      LCHK(launch_encode(s, p->pw.p, p->PW, p->cbw.p, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
+    }
+    float2* cts = nullptr;
+    if (a->cap_tx_syms) {
+      if (p->captx.alloc((size_t)B * p->n_sym * p->Nd)) return fail(LTE_ENOMEM, "capture");
+      cts = p->captx.p;
+    }
     Timer t(p, KN_OFDM_TX);
-    LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B));
+    LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B, cts));
+  } else {
+    std::vector<float> hx((size_t)B * p->L * 2);
+    for (int b = 0; b < B; ++b)
+      std::memcpy(&hx[(size_t)b * p->L * 2], a->in_signal + (size_t)b * a->in_signal_stride,
+                  (size_t)p->L * 2 * sizeof(float));
+    HIPCHK(hipMemcpyAsync(p->x.p, hx.data(), hx.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  // without the channel stage the input is the received signal: no fading, no noise
+  const bool ray = ray_cfg && do_ch;
+  if (!do_ch) {
+    std::vector<float> inf(B, INFINITY);
+    HIPCHK(hipMemcpyAsync(p->snr_lin.p, inf.data(), B * sizeof(float), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
   }
   const float2* ysrc = ray ? p->y.p : p->x.p;
   const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
@@ -829,11 +915,12 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     Timer t(p, KN_CHANNEL);
     LCHK(launch_channel(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
                         p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, p->nblk));
+    LCHK(launch_npow(s, B, rx, p->pow_part.p, p->nblk, p->L, p->snr_lin.p, p->npow.p));
   }
-  {
+  if (do_rx) {
     Timer t(p, KN_RX_CHEST);
-    LCHK(launch_rx_chest(s, g, B, rx, ysrc, yrs, yfs, p->pow_part.p, p->nblk, p->snr_lin.p, p->fid.p, a->seed,
-                         inj_z, inj_z_stride, p->H.p, p->pstats.p, p->npow.p));
+    LCHK(launch_rx_chest(s, g, B, rx, ysrc, yrs, yfs, p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, p->H.p,
+                         p->pstats.p));
   }
   float2* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
@@ -845,13 +932,13 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
     cap_bits_dev = p->cap_bits.p;
   }
-  {
+  if (do_rx) {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, p->H.p, p->npow.p, p->snr_lin.p,
                         p->fid.p, a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p, p->llr.p,
                         cap_syms_dev, coded ? nullptr : cap_bits_dev));
   }
-  if (coded) {
+  if (coded && do_rx) {
     {
       Timer t(p, KN_DEMATCH);
       LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
@@ -868,7 +955,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
                             p->frame_err.p, p->frame_crc.p, cap_bits_dev));
     }
   }
-  {
+  if (do_rx) {
     Timer t(p, KN_ACC);
     LCHK(launch_accumulate(s, B, coded ? 1 : 0, d.n_bits, p->snr_idx.p, p->frame_err.p, p->frame_crc.p,
                            p->counts.p));
@@ -890,7 +977,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     if (tmp.alloc((size_t)B * rx * p->L)) return fail(LTE_ENOMEM, "capture");
     {
       Timer t(p, KN_CAP);
-      hipLaunchKernelGGL(k_cap_rx, dim3((p->L + 255) / 256, rx, B), dim3(256), 0, s, p->L, rx, B, ysrc, yrs, yfs,
+      hipLaunchKernelGGL(k_cap_rx, dim3(((p->L + 255) / 256) * B, rx), dim3(256), 0, s, p->L, rx, B, ysrc, yrs, yfs,
                          p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p);
       LCHK((int)hipGetLastError());
     }
@@ -910,6 +997,9 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
   if (a->cap_llr && coded)
     HIPCHK(hipMemcpyAsync(a->cap_llr, p->llr.p, (size_t)B * p->n_re_bits * sizeof(float), hipMemcpyDeviceToHost, s));
+  if (a->cap_tx_syms && (stages & LTE_STAGE_TX))
+    HIPCHK(hipMemcpyAsync(a->cap_tx_syms, p->captx.p, (size_t)B * p->n_sym * p->Nd * sizeof(float2),
+                          hipMemcpyDeviceToHost, s));
   if (a->cap_noise_power)
     HIPCHK(hipMemcpyAsync(a->cap_noise_power, p->npow.p, (size_t)B * rx * sizeof(float), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));

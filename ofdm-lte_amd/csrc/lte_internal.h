@@ -31,16 +31,17 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 int launch_encode(hipStream_t s, const uint32_t* pw, int PW, uint32_t* cbw, int KWmax, uint32_t* enc,
                   int EW, const CbInfo* cbi_dev, int C, int B);
 int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                   int enc_words, const int32_t* tx_map, float2* x, int B);
+                   int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms = nullptr);
 int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* gains_dev, const uint64_t* fid,
                   uint64_t seed, const float* inj_ph, int64_t inj_stride, float* phases, float2* coef);
 int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
                    const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
                    const float2* coef, const float2* x, float2* y, float* pow_part, int nblk);
+int launch_npow(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
+                float* npow);
 int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float2* y, int64_t y_rx_stride,
-                    int64_t y_frame_stride, const float* pow_part, int nblk, const float* snr_lin,
-                    const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride,
-                    float2* H, float* pstats, float* npow_out);
+                    int64_t y_frame_stride, const float* npow, const uint64_t* fid, uint64_t seed,
+                    const float* inj_z, int64_t inj_stride, float2* H, float* pstats);
 int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, int num_rx,
                    const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                    const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,

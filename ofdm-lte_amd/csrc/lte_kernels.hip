@@ -78,7 +78,8 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 // 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, int coded, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
-                                                const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B) {
+                                                const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B,
+                                                float2* __restrict__ cap_syms) {
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
@@ -108,7 +109,9 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, int coded, const uint32_
         }
         idx = (idx << 1) | (int)bit;
       }
-      buf[g.data_idx[j]] = zero ? make_float2(0.f, 0.f) : g.constel[idx];
+      const float2 sym = zero ? make_float2(0.f, 0.f) : g.constel[idx];
+      buf[g.data_idx[j]] = sym;
+      if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + j] = sym;
     }
     for (int p = tid; p < g.Np; p += T) buf[g.pilot_idx[p]] = g.pilots[p];
   }
@@ -123,12 +126,12 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, int coded, const uint32_
 }
 
 int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                   int enc_words, const int32_t* tx_map, float2* x, int B) {
+                   int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms) {
   const int spw = WG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym;
   const int blocks = (int)((total + spw - 1) / spw);
   hipLaunchKernelGGL(k_ofdm_tx, dim3(blocks), dim3(WG), spw * g.N * sizeof(float2), s, g, coded, pw, PW, enc,
-                     enc_words, tx_map, x, B);
+                     enc_words, tx_map, x, B, cap_syms);
   return (int)hipGetLastError();
 }
 
@@ -198,8 +201,9 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
                                                 const float2* __restrict__ coef, const float2* __restrict__ x,
                                                 float2* __restrict__ y, float* __restrict__ pow_part, int nblk) {
   __shared__ float red[WG / 64];
-  const int n = blockIdx.x * WG + threadIdx.x;
-  const int rx = blockIdx.y, b = blockIdx.z;
+  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
+  const int n = blk * WG + threadIdx.x;
+  const int rx = blockIdx.y;
   const float2* xf = x + (size_t)b * L;
   float2 v = make_float2(0.f, 0.f);
   if (n < L) {
@@ -234,13 +238,13 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
     }
   }
   const float t = block_sum(v.x * v.x + v.y * v.y, red);
-  if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blockIdx.x] = t;
+  if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blk] = t;
 }
 
 int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
                    const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
                    const float2* coef, const float2* x, float2* y, float* pow_part, int nblk) {
-  hipLaunchKernelGGL(k_channel, dim3(nblk, num_rx, B), dim3(WG), 0, s, g.L, num_rx, rayleigh, n_paths, delays_dev,
+  hipLaunchKernelGGL(k_channel, dim3(nblk * B, num_rx), dim3(WG), 0, s, g.L, num_rx, rayleigh, n_paths, delays_dev,
                      gains_dev, fD, fs, phases, coef, x, y, pow_part, nblk);
   return (int)hipGetLastError();
 }
@@ -280,11 +284,9 @@ __device__ __forceinline__ void load_symbol_noisy(float2* buf, const float2* __r
 // LTEChannelEstimator.estimate_channel :40-96, _interpolate_channel :98-133).
 __global__ __launch_bounds__(WG) void k_rx_chest(Grid g, int B, int num_rx, const float2* __restrict__ y,
                                                  int64_t y_rx_stride, int64_t y_frame_stride,
-                                                 const float* __restrict__ pow_part, int nblk,
-                                                 const float* __restrict__ snr_lin, const uint64_t* __restrict__ fid,
+                                                 const float* __restrict__ npow_in, const uint64_t* __restrict__ fid,
                                                  uint64_t seed, const float* __restrict__ inj_z, int64_t inj_stride,
-                                                 float2* __restrict__ H, float* __restrict__ pstats,
-                                                 float* __restrict__ npow_out) {
+                                                 float2* __restrict__ H, float* __restrict__ pstats) {
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
@@ -294,11 +296,8 @@ __global__ __launch_bounds__(WG) void k_rx_chest(Grid g, int B, int num_rx, cons
   const bool active = slot < spw && b < B;
   float2* buf = sm + slot * N;
   float2* hp = sm + spw * N + slot * g.Np;
-  float npow = 0.f;
   if (active) {
-    const float P = frame_power(pow_part + ((size_t)b * num_rx + rx) * nblk, nblk, g.L);
-    npow = P / snr_lin[b];
-    const float sigma = sqrtf(npow * 0.5f);
+    const float sigma = sqrtf(npow_in[(size_t)b * num_rx + rx] * 0.5f);
     const float* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
     load_symbol_noisy(buf, y + b * y_frame_stride + rx * y_rx_stride, N, g.cp, grp * 14, sigma, seed, fid[b], rx,
                       zf, g.L, tid, T);
@@ -340,21 +339,34 @@ __global__ __launch_bounds__(WG) void k_rx_chest(Grid g, int B, int num_rx, cons
       float* st = pstats + (((size_t)b * num_rx + rx) * g.n_grp + grp) * 2;
       st[0] = pp / g.Np;
       st[1] = en / g.Np;
-      if (grp == 0) npow_out[(size_t)b * num_rx + rx] = npow;
     }
   }
 }
 
+// per (frame, rx): P = mean |y|^2 over the stream, noise power = P / SNR (channel.py:44-53, 217-224)
+__global__ void k_npow(int B, int num_rx, const float* __restrict__ pow_part, int nblk, int L,
+                       const float* __restrict__ snr_lin, float* __restrict__ npow) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * num_rx) return;
+  npow[i] = frame_power(pow_part + (size_t)i * nblk, nblk, L) / snr_lin[i / num_rx];
+}
+
+int launch_npow(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
+                float* npow) {
+  hipLaunchKernelGGL(k_npow, dim3((B * num_rx + WG - 1) / WG), dim3(WG), 0, s, B, num_rx, pow_part, nblk, L, snr_lin,
+                     npow);
+  return (int)hipGetLastError();
+}
+
 int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float2* y, int64_t y_rx_stride,
-                    int64_t y_frame_stride, const float* pow_part, int nblk, const float* snr_lin,
-                    const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride, float2* H,
-                    float* pstats, float* npow_out) {
+                    int64_t y_frame_stride, const float* npow, const uint64_t* fid, uint64_t seed,
+                    const float* inj_z, int64_t inj_stride, float2* H, float* pstats) {
   const int spw = WG / (g.N >> 3);
   const int64_t total = (int64_t)B * num_rx * g.n_grp;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = (size_t)spw * (g.N + g.Np) * sizeof(float2);
   hipLaunchKernelGGL(k_rx_chest, dim3(blocks), dim3(WG), shm, s, g, B, num_rx, y, y_rx_stride, y_frame_stride,
-                     pow_part, nblk, snr_lin, fid, seed, inj_z, inj_stride, H, pstats, npow_out);
+                     npow, fid, seed, inj_z, inj_stride, H, pstats);
   return (int)hipGetLastError();
 }
 

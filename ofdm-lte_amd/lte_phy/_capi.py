@@ -1,0 +1,154 @@
+"""ctypes binding of liblte_hip.so (include/lte_phy.h).
+
+The library is the product: every compute call of this package goes through
+it.  There is no CPU fallback -- if the library is missing or no gfx950 GPU is
+visible, calls raise loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('LTE_HIP_LIB', os.path.join(_HERE, 'liblte_hip.so'))
+
+LTE_OK, LTE_EINVAL, LTE_EHIP, LTE_ENOMEM, LTE_ENODEV, LTE_EUNSUP = 0, -1, -2, -3, -4, -5
+CHAIN_UNCODED, CHAIN_CODED, CHAIN_SIMO = 0, 1, 2
+CH_AWGN, CH_RAYLEIGH = 0, 1
+STAGE_TX, STAGE_CHANNEL, STAGE_RX, STAGE_ALL = 1, 2, 4, 7
+MAX_PATHS = 16
+
+c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+P = ctypes.POINTER
+
+
+class PlanDesc(ctypes.Structure):
+    _fields_ = [('N', c_i32), ('Nc', c_i32), ('cp_len', c_i32), ('bps', c_i32), ('n_sym', c_i32),
+                ('chain', c_i32), ('channel', c_i32), ('num_rx', c_i32), ('n_paths', c_i32),
+                ('delays', c_i32 * MAX_PATHS), ('gains', c_f64 * MAX_PATHS), ('fD', c_f64), ('fs', c_f64),
+                ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32)]
+
+
+class RunArgs(ctypes.Structure):
+    _fields_ = [('n_frames', c_i32), ('snr_db', P(ctypes.c_float)), ('snr_index', P(c_i32)), ('n_snr', c_i32),
+                ('seed', c_u64), ('frame_ids', P(c_u64)), ('frame_id0', c_u64),
+                ('bits', P(ctypes.c_uint8)), ('bits_stride', c_i64),
+                ('phases', P(c_f64)), ('phases_stride', c_i64),
+                ('noise', P(c_f64)), ('noise_stride', c_i64),
+                ('counts', P(c_u64)), ('frame_errors', P(ctypes.c_uint32)), ('frame_crc_ok', P(ctypes.c_uint8)),
+                ('stages', c_i32), ('in_signal', P(ctypes.c_float)), ('in_signal_stride', c_i64),
+                ('cap_signal_tx', P(ctypes.c_float)), ('cap_signal_rx', P(ctypes.c_float)),
+                ('cap_data_syms', P(ctypes.c_float)), ('cap_H', P(ctypes.c_float)),
+                ('cap_pilot_stats', P(ctypes.c_float)), ('cap_bits_rx', P(ctypes.c_uint8)),
+                ('cap_llr', P(ctypes.c_float)), ('cap_noise_power', P(ctypes.c_float)),
+                ('cap_tx_syms', P(ctypes.c_float))]
+
+
+# every symbol include/lte_phy.h declares, with its ctypes signature
+_SIGS = {
+    'lte_strerror': (ctypes.c_char_p, [ctypes.c_int]),
+    'lte_last_error': (ctypes.c_char_p, []),
+    'lte_device_init': (ctypes.c_int, [ctypes.c_int]),
+    'lte_version': (ctypes.c_int, []),
+    'lte_plan_create': (ctypes.c_int, [P(PlanDesc), P(ctypes.c_void_p)]),
+    'lte_plan_destroy': (ctypes.c_int, [ctypes.c_void_p]),
+    'lte_plan_info': (ctypes.c_int, [ctypes.c_void_p, P(c_i64)]),
+    'lte_run': (ctypes.c_int, [ctypes.c_void_p, P(RunArgs)]),
+    'lte_timing_enable': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    'lte_timing_read': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, P(c_f64), P(c_i64),
+                                       ctypes.c_int]),
+    'lte_timing_reset': (ctypes.c_int, [ctypes.c_void_p]),
+    'lte_fft_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_pilots': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P(c_f64)]),
+    'lte_llr_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_hard_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_uint8)]),
+    'lte_turbo_encode_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_uint8), P(ctypes.c_uint8)]),
+    'lte_turbo_decode_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float),
+                                             P(ctypes.c_uint8)]),
+    'lte_bcjr_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float),
+                                     P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_crc_host': (ctypes.c_int, [c_i64, P(ctypes.c_uint8), ctypes.c_uint32, ctypes.c_int,
+                                    P(ctypes.c_uint32)]),
+    'lte_rate_dematch_map': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32)]),
+    'lte_channel_host': (ctypes.c_int, [c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32), P(c_f64),
+                                        c_f64, c_f64, c_f64, c_u64, P(ctypes.c_float), P(c_f64), P(c_f64),
+                                        P(ctypes.c_float), P(ctypes.c_float)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+_device_ready = {}
+
+
+def load():
+    """Load liblte_hip.so (raises if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"liblte_hip.so not found at {LIB_PATH}: build it with "
+                                   f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                f = getattr(lib, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc):
+    if rc >= 0:
+        return rc
+    lib = load()
+    msg = lib.lte_last_error().decode(errors='replace') or lib.lte_strerror(rc).decode()
+    if rc == LTE_EINVAL:
+        raise ValueError(msg)
+    if rc == LTE_EUNSUP:
+        raise NotImplementedError(msg)
+    raise RuntimeError(f"liblte_hip: {lib.lte_strerror(rc).decode()}: {msg}")
+
+
+def device_init(device=None):
+    if device is None:
+        device = int(os.environ.get('LOCAL_RANK', '0')) if 'LTE_DEVICE' not in os.environ else \
+            int(os.environ['LTE_DEVICE'])
+    if not _device_ready.get(device):
+        check(load().lte_device_init(device))
+        _device_ready[device] = True
+    return device
+
+
+def ptr(a, t):
+    if a is None:
+        return None
+    return a.ctypes.data_as(P(t))
+
+
+F32, U8, U32, U64, I32, F64 = ctypes.c_float, ctypes.c_uint8, ctypes.c_uint32, c_u64, c_i32, c_f64
+
+
+def fft(x, inverse=False):
+    """Batched N-point FFT/sqrt(N) (inverse: IFFT*sqrt(N)) on the GPU; x [..., N] complex."""
+    device_init()
+    x = np.ascontiguousarray(x, dtype=np.complex64)
+    N = x.shape[-1]
+    out = np.empty_like(x)
+    check(load().lte_fft_host(N, 1 if inverse else 0, x.size // N, ptr(x.view(np.float32), F32),
+                              ptr(out.view(np.float32), F32)))
+    return out
+
+
+def pilots(cell_id, n):
+    out = np.empty(2 * n, dtype=np.float64)
+    check(load().lte_pilots(cell_id, n, ptr(out, F64)))
+    return out[0::2] + 1j * out[1::2]
+
+
+def rate_dematch_map(K, E, rv_idx=0):
+    src = np.empty(3 * K + 12, dtype=np.int32)
+    check(load().lte_rate_dematch_map(K, E, rv_idx, ptr(src, I32)))
+    return src

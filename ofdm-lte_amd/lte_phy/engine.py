@@ -1,0 +1,159 @@
+"""Plan cache and batch runner over the C ABI (lte_plan_create / lte_run).
+
+A plan is one device workspace for one configuration (numerology, chain,
+channel, payload size, capacity).  `Plan.run` executes the whole
+TX -> channel -> RX (-> turbo) chain for a batch of frames on the GPU and
+returns counters and any requested host captures.
+"""
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+
+from . import _capi as C
+
+
+class Plan:
+    def __init__(self, *, N, Nc, cp_len, bps, n_sym, chain, channel, num_rx=1, delays=(), gains=(), fD=0.0,
+                 fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0):
+        C.device_init()
+        d = C.PlanDesc()
+        d.N, d.Nc, d.cp_len, d.bps, d.n_sym = N, Nc, cp_len, bps, n_sym
+        d.chain, d.channel, d.num_rx = chain, channel, num_rx
+        d.n_paths = len(delays)
+        if d.n_paths > C.MAX_PATHS:
+            raise ValueError('too many multipath taps')
+        for i, (dl, g) in enumerate(zip(delays, gains)):
+            d.delays[i] = int(dl)
+            d.gains[i] = float(g)
+        d.fD, d.fs = float(fD), float(fs)
+        d.n_bits, d.turbo_iters, d.max_frames, d.cell_id = int(n_bits), int(turbo_iters), int(max_frames), cell_id
+        self.desc = d
+        h = ctypes.c_void_p()
+        C.check(C.load().lte_plan_create(ctypes.byref(d), ctypes.byref(h)))
+        self.h = h
+        info = np.zeros(8, dtype=np.int64)
+        C.check(C.load().lte_plan_info(h, C.ptr(info, C.c_i64)))
+        self.L, self.n_sym, self.Nd, self.Np, self.n_grp, self.n_cb, self.coded_bits, self.n_re_bits = \
+            (int(v) for v in info)
+        self.num_rx, self.N, self.bps, self.n_bits, self.max_frames = num_rx, N, bps, int(n_bits), int(max_frames)
+        self.chain = chain
+
+    def __del__(self):
+        try:
+            if getattr(self, 'h', None):
+                C.load().lte_plan_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------
+    def run(self, snr_db, *, snr_index=None, n_snr=1, seed=0, frame_ids=None, frame_id0=0, bits=None,
+            bits_broadcast=False, phases=None, phases_broadcast=False, noise=None, noise_broadcast=False,
+            stages=C.STAGE_ALL, in_signal=None, capture=()):
+        snr = np.ascontiguousarray(np.atleast_1d(snr_db), dtype=np.float32)
+        B = len(snr)
+        a = C.RunArgs()
+        a.n_frames = B
+        a.snr_db = C.ptr(snr, C.F32)
+        keep = [snr]
+        if snr_index is not None:
+            si = np.ascontiguousarray(snr_index, dtype=np.int32)
+            keep.append(si)
+            a.snr_index = C.ptr(si, C.I32)
+        a.n_snr = int(n_snr)
+        a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        if frame_ids is not None:
+            fi = np.ascontiguousarray(frame_ids, dtype=np.uint64)
+            keep.append(fi)
+            a.frame_ids = C.ptr(fi, C.U64)
+        a.frame_id0 = int(frame_id0)
+        if bits is not None:
+            b = np.ascontiguousarray(bits, dtype=np.uint8)
+            keep.append(b)
+            a.bits = C.ptr(b, C.U8)
+            a.bits_stride = 0 if bits_broadcast else self.n_bits
+        if phases is not None:
+            ph = np.ascontiguousarray(phases, dtype=np.float64)
+            keep.append(ph)
+            a.phases = C.ptr(ph, C.F64)
+            a.phases_stride = 0 if phases_broadcast else ph.size // B
+        if noise is not None:
+            z = np.ascontiguousarray(noise, dtype=np.float64)
+            keep.append(z)
+            a.noise = C.ptr(z, C.F64)
+            a.noise_stride = 0 if noise_broadcast else z.size // B
+        counts = np.zeros((max(1, n_snr), 4), dtype=np.uint64)
+        a.counts = C.ptr(counts, C.U64)
+        out = {'counts': counts}
+        ferr = np.zeros(B, dtype=np.uint32)
+        a.frame_errors = C.ptr(ferr, C.U32)
+        out['frame_errors'] = ferr
+        if self.chain == C.CHAIN_CODED:
+            crc = np.zeros(B, dtype=np.uint8)
+            a.frame_crc_ok = C.ptr(crc, C.U8)
+            out['crc_ok'] = crc
+        a.stages = int(stages)
+        if in_signal is not None:
+            xs = np.ascontiguousarray(in_signal, dtype=np.complex64).reshape(-1, self.L)
+            keep.append(xs)
+            a.in_signal = C.ptr(xs.view(np.float32), C.F32)
+            a.in_signal_stride = 0 if xs.shape[0] == 1 else 2 * self.L
+        shapes = {
+            'signal_tx': ((B, self.L), np.complex64, 'cap_signal_tx', C.F32),
+            'signal_rx': ((B, self.num_rx, self.L), np.complex64, 'cap_signal_rx', C.F32),
+            'data_syms': ((B, self.n_sym * self.Nd), np.complex64, 'cap_data_syms', C.F32),
+            'H': ((B, self.num_rx, self.n_grp, self.N), np.complex64, 'cap_H', C.F32),
+            'pilot_stats': ((B, self.num_rx, self.n_grp, 2), np.float32, 'cap_pilot_stats', C.F32),
+            'bits_rx': ((B, self.n_bits), np.uint8, 'cap_bits_rx', C.U8),
+            'llr': ((B, self.n_re_bits), np.float32, 'cap_llr', C.F32),
+            'noise_power': ((B, self.num_rx), np.float32, 'cap_noise_power', C.F32),
+            'tx_syms': ((B, self.n_sym * self.Nd), np.complex64, 'cap_tx_syms', C.F32),
+        }
+        for name in capture:
+            shp, dt, field, ct = shapes[name]
+            arr = np.zeros(shp, dtype=dt)
+            view = arr.view(np.float32) if dt == np.complex64 else arr
+            setattr(a, field, C.ptr(view, ct))
+            out[name] = arr
+        C.check(C.load().lte_run(self.h, ctypes.byref(a)))
+        del keep
+        return out
+
+    # ------------------------------------------------------------------
+    def timing(self, on=True):
+        C.check(C.load().lte_timing_enable(self.h, 1 if on else 0))
+
+    def timing_reset(self):
+        C.check(C.load().lte_timing_reset(self.h))
+
+    def timing_read(self):
+        names = ctypes.create_string_buffer(512)
+        ms = np.zeros(32, dtype=np.float64)
+        nl = np.zeros(32, dtype=np.int64)
+        n = C.check(C.load().lte_timing_read(self.h, names, 512, C.ptr(ms, C.F64), C.ptr(nl, C.c_i64), 32))
+        keys = names.value.decode().split(',')
+        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(keys[:n])}
+
+
+_CACHE: "OrderedDict[tuple, Plan]" = OrderedDict()
+_CACHE_MAX = 8
+
+
+def get_plan(**kw):
+    key = tuple(sorted((k, tuple(v) if isinstance(v, (list, tuple, np.ndarray)) else v) for k, v in kw.items()))
+    p = _CACHE.get(key)
+    if p is None:
+        p = Plan(**kw)
+        _CACHE[key] = p
+        while len(_CACHE) > _CACHE_MAX:
+            _CACHE.popitem(last=False)
+    else:
+        _CACHE.move_to_end(key)
+    return p
+
+
+def clear_cache():
+    _CACHE.clear()

@@ -1,0 +1,572 @@
+"""Drop-in mirror of the reference's orchestration layer (core/ofdm_core.py).
+
+`OFDMTransmitter`, `OFDMReceiver`, `OFDMChannel` and `OFDMSimulator` keep the
+reference's names, constructor arguments, defaults, return values and
+result-dict keys; all signal processing runs on the MI355X through
+liblte_hip.so (engine.Plan / _capi).
+
+Random numbers: single-call methods reproduce the reference's frozen global
+RNG exactly -- the host draws the same NumPy legacy-RNG values the reference
+consumes (pilot reseed, Jakes phases, unit normals), leaving the global RNG in
+the same final state, and the GPU consumes them ("ref-compat" injection).
+`run_grid` is the device-resident Monte-Carlo driver (Philox per frame).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import _capi as C
+from .config import ITU_CHANNEL_MODELS, LTEConfig
+from .engine import get_plan
+
+SLOT_SIZE = 14
+
+
+# ------------------------------------------------------------------ host-side grid mirror
+class ResourceGrid:
+    """LTEResourceGrid (core/resource_mapper.py:17-111): guard bands, DC null,
+    pilot on every 6th useful SC (offset 3), data elsewhere."""
+
+    def __init__(self, N, Nc):
+        self.N, self.Nc = N, Nc
+        self.num_guard_left = (N - Nc) // 2
+        self.num_guard_right = N - Nc - self.num_guard_left
+        self.dc_index = N // 2
+        self.pilot_spacing = 6
+        k = np.arange(N)
+        guard = (k < self.num_guard_left) | (k >= N - self.num_guard_right)
+        dc = (k == self.dc_index) & ~guard
+        pilot = ~guard & ~dc & (((k - self.num_guard_left) % 6) == 3)
+        self._data = k[~guard & ~dc & ~pilot]
+        self._pilot = k[pilot]
+        self._guard = k[guard]
+
+    def get_data_indices(self):
+        return self._data.copy()
+
+    def get_pilot_indices(self):
+        return self._pilot.copy()
+
+    def get_guard_indices(self):
+        return self._guard.copy()
+
+    def get_statistics(self):
+        return {'total_subcarriers': self.N, 'useful_subcarriers': self.Nc,
+                'data_subcarriers': len(self._data), 'pilot_subcarriers': len(self._pilot),
+                'guard_subcarriers': len(self._guard), 'dc_subcarriers': 1,
+                'guard_left': self.num_guard_left, 'guard_right': self.num_guard_right,
+                'pilot_spacing': self.pilot_spacing}
+
+
+def constellation(mod):
+    """QAMModulator._generate_constellation (core/modulator.py:28-59) (host table)."""
+    if mod == 'QPSK':
+        return np.array([1 + 1j, 1 - 1j, -1 + 1j, -1 - 1j]) / np.sqrt(2)
+    lv = [-3, -1, 1, 3] if mod == '16-QAM' else [-7, -5, -3, -1, 1, 3, 5, 7]
+    sc = np.sqrt(10) if mod == '16-QAM' else np.sqrt(42)
+    return np.array([r + 1j * i for r in lv for i in lv]) / sc
+
+
+def _reseed_pilots(cell_id, n):
+    """PilotPattern.generate_pilots side effect (core/resource_mapper.py:148):
+    the reference reseeds the GLOBAL NumPy RNG every time pilots are made."""
+    np.random.seed(cell_id)
+    np.random.choice([1, -1], size=n)
+
+
+def _check_mode(mode, enable_sc_fdm):
+    if enable_sc_fdm or mode == 'sc-fdm':
+        raise NotImplementedError("SC-FDM (DFT precoding) is not on the GPU path yet (SURVEY §8f rank 2)")
+    if mode != 'lte':
+        raise NotImplementedError(f"mode '{mode}' is not on the GPU path (only 'lte' resource mapping)")
+
+
+def itu_paths(profile, fs, spatial=False):
+    """RayleighMultiPathChannel._get_itu_profile_params (core/channel.py:162-186)
+    followed by RayleighChannel.__init__'s second dB->linear conversion
+    (core/rayleighchannel.py:16) -- quirk Q2 reproduced on purpose."""
+    if profile not in ITU_CHANNEL_MODELS:
+        raise ValueError(f"Perfil ITU no encontrado: {profile}. "
+                         f"Opciones disponibles: {list(ITU_CHANNEL_MODELS.keys())}")
+    d = ITU_CHANNEL_MODELS[profile]
+    delays_s = np.array(d['delays_us']) * 1e-6
+    g = 10 ** (np.array(d['power_db']) / 20)
+    g = 10 ** (np.array(g) / 20)
+    if spatial:
+        g = 10 ** (np.array(g) / 20)
+    return [int(np.round(t * fs)) for t in delays_s], [float(x) for x in g]
+
+
+def doppler(frequency_ghz, velocity_kmh, profile):
+    """RayleighMultiPathChannel fD rule (core/channel.py:113-143)."""
+    if frequency_ghz is not None and velocity_kmh is not None:
+        fc, v = frequency_ghz * 1e9, velocity_kmh / 3.6
+    else:
+        v = (5.0 if 'Pedestrian' in profile else 30.0 if 'Vehicular_A' in profile else
+             120.0 if 'Vehicular_B' in profile else 10.0) / 3.6
+        fc = 2e9
+    return (v * fc) / 3e8
+
+
+def papr(signal):
+    """OFDMTransmitter.calculate_papr (core/ofdm_core.py:114-147)."""
+    p = np.abs(signal) ** 2
+    pk, av = np.max(p), np.mean(p)
+    if av > 0:
+        lin = pk / av
+        return {'papr_db': 10 * np.log10(lin), 'papr_linear': lin, 'peak_power': pk, 'avg_power': av}
+    return {'papr_db': 0.0, 'papr_linear': 1.0, 'peak_power': pk, 'avg_power': av}
+
+
+# ------------------------------------------------------------------ TX
+class _ModulatorView:
+    """Read-only stand-in for OFDMModulator's inspectable state."""
+
+    def __init__(self, config):
+        from types import SimpleNamespace
+        self.config = config
+        self.mode = 'lte'
+        self.enable_sc_fdm = False
+        self.qam_modulator = SimpleNamespace(modulation_type=config.modulation,
+                                             constellation=constellation(config.modulation),
+                                             get_constellation=lambda: constellation(config.modulation))
+        self.resource_mapper = SimpleNamespace(grid=ResourceGrid(config.N, config.Nc))
+        self.resource_mapper.get_data_indices = self.resource_mapper.grid.get_data_indices
+
+
+class OFDMTransmitter:
+    """OFDMTransmitter (core/ofdm_core.py:42-155)."""
+
+    def __init__(self, config: LTEConfig, mode: str = 'lte', enable_sc_fdm: bool = False):
+        _check_mode(mode, enable_sc_fdm)
+        self.config, self.mode, self.enable_sc_fdm = config, mode, enable_sc_fdm
+        self.modulator = _ModulatorView(config)
+        self.grid = self.modulator.resource_mapper.grid
+        self.last_signal_tx = self.last_symbols_tx = self.last_mapping_infos = None
+
+    def _mapping_info(self, n_data):
+        g = self.grid
+        return {'num_data_mapped': n_data, 'num_pilots_mapped': len(g._pilot),
+                'num_nulls': len(g._guard) + 1, 'data_indices': g.get_data_indices()[:n_data],
+                'pilot_indices': g.get_pilot_indices(), 'guard_indices': g.get_guard_indices(),
+                'dc_index': g.dc_index, 'grid_statistics': g.get_statistics()}
+
+    def modulate(self, bits) -> Tuple[np.ndarray, List[np.ndarray], List[Dict]]:
+        """OFDMModulator.modulate_stream (core/modulator.py:252-302) on the GPU."""
+        if not isinstance(bits, np.ndarray):
+            bits = np.array(bits, dtype=int)
+        if bits.size == 0:
+            raise ValueError("Bits array cannot be empty")
+        cfg = self.config
+        Nd = len(self.grid._data)
+        n_sym = int(np.ceil(len(bits) / (Nd * cfg.bits_per_symbol)))
+        plan = get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
+                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=len(bits), max_frames=1)
+        r = plan.run([np.inf], bits=(np.asarray(bits) & 1).astype(np.uint8)[None], stages=C.STAGE_TX,
+                     capture=('signal_tx', 'tx_syms'))
+        _reseed_pilots(0, len(self.grid._pilot))
+        sig = r['signal_tx'][0].astype(np.complex128)
+        ts = r['tx_syms'][0].astype(np.complex128)
+        syms = [ts[i * Nd:(i + 1) * Nd] for i in range(n_sym)]
+        infos = [self._mapping_info(Nd) for _ in range(n_sym)]
+        self.last_signal_tx, self.last_symbols_tx, self.last_mapping_infos = sig, syms, infos
+        return sig, syms, infos
+
+    def calculate_papr(self, signal: np.ndarray) -> Dict:
+        return papr(signal)
+
+    def get_config(self) -> LTEConfig:
+        return self.config
+
+    def __repr__(self):
+        return f"OFDMTransmitter({self.config.modulation}, OFDM)"
+
+
+# ------------------------------------------------------------------ RX
+class _DemodulatorView:
+    def __init__(self, config):
+        from types import SimpleNamespace
+        self.config = config
+        c = constellation(config.modulation)
+        self.qam_demodulator = SimpleNamespace(modulation_type=config.modulation, constellation=c,
+                                               get_constellation=lambda: c)
+
+
+class OFDMReceiver:
+    """OFDMReceiver (core/ofdm_core.py:158-276)."""
+
+    def __init__(self, config: LTEConfig, mode: str = 'lte', enable_equalization: bool = True,
+                 enable_sc_fdm: bool = False):
+        _check_mode(mode, enable_sc_fdm)
+        self.config, self.mode = config, mode
+        self.enable_equalization, self.enable_sc_fdm = enable_equalization, enable_sc_fdm
+        self.demodulator = _DemodulatorView(config)
+        self.grid = ResourceGrid(config.N, config.Nc)
+        self.last_symbols_rx = self.last_bits_rx = self.channel_estimate = None
+
+    def demodulate(self, signal_rx: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """OFDMDemodulator.demodulate_stream 'lte' path (core/demodulator.py:120-147):
+        CP removal + FFT, slot-0 CRS estimation, ZF, nearest-point bits."""
+        if signal_rx.size == 0:
+            raise ValueError("Received signal cannot be empty")
+        if not self.enable_equalization:
+            raise NotImplementedError("enable_equalization=False receive path is not on the GPU path")
+        cfg = self.config
+        sl = cfg.N + cfg.cp_length
+        n_sym = max(1, len(signal_rx) // sl)
+        sig = np.zeros(n_sym * sl, dtype=np.complex128)
+        m = min(len(signal_rx), n_sym * sl)
+        sig[:m] = signal_rx[:m]
+        Nd = len(self.grid._data)
+        nb = n_sym * Nd * cfg.bits_per_symbol
+        plan = get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
+                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=nb, max_frames=1)
+        r = plan.run([0.0], stages=C.STAGE_RX, in_signal=sig[None], capture=('data_syms', 'bits_rx'))
+        _reseed_pilots(0, len(self.grid._pilot))
+        syms = r['data_syms'][0].astype(np.complex128)
+        bits = r['bits_rx'][0].astype(np.int64)
+        self.last_symbols_rx, self.last_bits_rx = syms, bits
+        return syms, bits
+
+    def estimate_channel(self) -> Dict:
+        return {'estimated': False, 'method': 'none'}
+
+    def calculate_ber(self, bits_tx: np.ndarray, bits_rx: np.ndarray) -> float:
+        n = min(len(bits_tx), len(bits_rx))
+        if n == 0:
+            return 0.0
+        return float(np.sum(bits_tx[:n] != bits_rx[:n]) / n)
+
+    def get_config(self) -> LTEConfig:
+        return self.config
+
+    def __repr__(self):
+        return f"OFDMReceiver({self.config.modulation}, OFDM)"
+
+
+# ------------------------------------------------------------------ channel
+class OFDMChannel:
+    """OFDMChannel (core/ofdm_core.py:279-557).  Any channel_type other than
+    'rayleigh_mp' is AWGN, as in the reference (:322-332)."""
+
+    def __init__(self, channel_type: str = 'awgn', snr_db: float = 10.0, fs: float = 15.36e6,
+                 itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0):
+        self.channel_type, self.snr_db, self.fs = channel_type, snr_db, fs
+        self.profile, self.frequency_ghz, self.velocity_kmh = itu_profile, frequency_ghz, velocity_kmh
+        self.rayleigh = channel_type == 'rayleigh_mp'
+        if self.rayleigh:
+            if fs is None:
+                raise ValueError("Se requiere fs (frecuencia de muestreo) para canal Rayleigh")
+            self.delays, self.gains = itu_paths(itu_profile, fs)
+            self.fD = doppler(frequency_ghz, velocity_kmh, itu_profile)
+        else:
+            self.delays, self.gains, self.fD = [], [], 0.0
+
+    def set_snr(self, snr_db: float) -> None:
+        self.snr_db = snr_db
+
+    @property
+    def kind(self):
+        return C.CH_RAYLEIGH if self.rayleigh else C.CH_AWGN
+
+    def draw(self, L, num_rx=1):
+        """Consume the global RNG like one ChannelSimulator.transmit per RX
+        antenna (rayleighchannel.py:31, channel.py:227-228).  Returns
+        phases [num_rx][P][16], unit normals [num_rx][2][L]."""
+        P = len(self.delays)
+        ph = np.zeros((num_rx, P, 16))
+        z = np.zeros((num_rx, 2, L))
+        for r in range(num_rx):
+            for p in range(P):
+                ph[r, p] = 2 * np.pi * np.random.rand(16)
+            z[r, 0] = np.random.normal(0, 1.0, L)
+            z[r, 1] = np.random.normal(0, 1.0, L)
+        return ph, z
+
+    def _apply(self, signal, num_rx):
+        C.device_init()
+        x = np.ascontiguousarray(signal, dtype=np.complex64)
+        L = len(x)
+        ph, z = self.draw(L, num_rx)
+        y = np.zeros((num_rx, L), dtype=np.complex64)
+        npow = np.zeros(num_rx, dtype=np.float32)
+        P = len(self.delays)
+        dl = np.array(self.delays, dtype=np.int32)
+        g = np.array(self.gains, dtype=np.float64)
+        C.check(C.load().lte_channel_host(L, num_rx, self.kind, P, C.ptr(dl, C.I32) if P else None,
+                                          C.ptr(g, C.F64) if P else None, float(self.fD), float(self.fs or 0.0),
+                                          float(self.snr_db), 0, C.ptr(x.view(np.float32), C.F32),
+                                          C.ptr(ph, C.F64) if P else None, C.ptr(z, C.F64),
+                                          C.ptr(y.view(np.float32), C.F32), C.ptr(npow, C.F32)))
+        return y.astype(np.complex128)
+
+    def transmit(self, signal: np.ndarray) -> np.ndarray:
+        """ChannelSimulator.transmit (core/channel.py:334-345)."""
+        return self._apply(signal, 1)[0]
+
+    def transmit_simo(self, signal_tx: np.ndarray, num_rx: int = 2) -> List[np.ndarray]:
+        """Independent fading + noise per RX antenna (core/ofdm_core.py:361-412)."""
+        if num_rx < 1:
+            raise ValueError("num_rx must be >= 1")
+        return list(self._apply(signal_tx, num_rx))
+
+    def transmit_mimo(self, signals_tx, num_rx: int = 1):
+        raise NotImplementedError("MIMO links (core/ofdm_core.py:434-543) are a later-round GPU path")
+
+    def get_config(self) -> Dict:
+        return {'type': self.channel_type, 'snr_db': self.snr_db, 'fs': self.fs, 'profile': self.profile,
+                'frequency_ghz': self.frequency_ghz, 'velocity_kmh': self.velocity_kmh}
+
+    def __repr__(self):
+        return f"OFDMChannel({self.channel_type}, SNR={self.snr_db}dB, {self.profile})"
+
+
+# ------------------------------------------------------------------ simulator
+class OFDMSimulator:
+    """OFDMSimulator (core/ofdm_core.py:560-2486): SISO, SISO+turbo and SIMO-MRC
+    on the GPU, plus the device-resident Monte-Carlo grid `run_grid`."""
+
+    def __init__(self, config: Optional[LTEConfig] = None, channel_type: str = 'awgn', mode: str = 'lte',
+                 enable_sc_fdm: bool = False, enable_equalization: bool = True, num_channels: int = 1,
+                 itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0.0):
+        if config is None:
+            config = LTEConfig()
+        self.config, self.channel_type, self.mode = config, channel_type, mode
+        self.enable_sc_fdm, self.enable_equalization = enable_sc_fdm, enable_equalization
+        self.itu_profile, self.frequency_ghz, self.velocity_kmh = itu_profile, frequency_ghz, velocity_kmh
+        self.tx = OFDMTransmitter(config, mode=mode, enable_sc_fdm=enable_sc_fdm)
+        self.rx = OFDMReceiver(config, mode=mode, enable_equalization=enable_equalization,
+                               enable_sc_fdm=enable_sc_fdm)
+        fs = getattr(config, 'fs', 15.36e6)
+        self.channels = []
+        for _ in range(num_channels):
+            if channel_type == 'rayleigh_mp':
+                ch = OFDMChannel('rayleigh_mp', 10.0, fs, itu_profile, frequency_ghz, velocity_kmh)
+            else:
+                ch = OFDMChannel('awgn', snr_db=10.0, fs=fs)
+            self.channels.append(ch)
+        self.grid = ResourceGrid(config.N, config.Nc)
+        self.last_results = None
+
+    # -------------------------------------------------------------- helpers
+    @property
+    def Nd(self):
+        return len(self.grid._data)
+
+    def _plan(self, chain, n_sym, n_bits, num_rx=1, max_frames=1, iters=8):
+        cfg, ch = self.config, self.channels[0]
+        return get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
+                        chain=chain, channel=ch.kind, num_rx=num_rx, delays=tuple(ch.delays),
+                        gains=tuple(ch.gains), fD=ch.fD, fs=cfg.fs, n_bits=n_bits, turbo_iters=iters,
+                        max_frames=max_frames)
+
+    def _ref_draws(self, L, num_rx=1):
+        """Exactly the global-RNG consumption of one reference simulate_* call:
+        TX pilot reseed -> per antenna channel draws -> RX pilot reseed (Q1)."""
+        np_ = len(self.grid._pilot)
+        _reseed_pilots(0, np_)
+        ph, z = self.channels[0].draw(L, num_rx)
+        _reseed_pilots(0, np_)
+        return ph, z
+
+    @staticmethod
+    def _bits_in(bits):
+        if not isinstance(bits, np.ndarray):
+            bits = np.array(bits, dtype=int)
+        if bits.size == 0:
+            raise ValueError("Bits array cannot be empty")
+        return bits
+
+    # -------------------------------------------------------------- SISO
+    def simulate_siso(self, bits: np.ndarray, snr_db: float = 10.0) -> Dict:
+        """core/ofdm_core.py:660-737"""
+        bits = self._bits_in(bits)
+        n0 = len(bits)
+        n_sym = int(np.ceil(n0 / (self.Nd * self.config.bits_per_symbol)))
+        plan = self._plan(C.CHAIN_UNCODED, n_sym, n0)
+        ph, z = self._ref_draws(plan.L)
+        r = plan.run([snr_db], bits=(bits & 1).astype(np.uint8)[None], phases=ph[None] if ph.size else None,
+                     noise=z[None], capture=('signal_tx', 'signal_rx', 'data_syms', 'bits_rx', 'tx_syms'))
+        brx = r['bits_rx'][0].astype(np.int64)
+        err = int(np.sum(bits != brx))
+        sig_tx = r['signal_tx'][0].astype(np.complex128)
+        pa = papr(sig_tx)
+        ts = r['tx_syms'][0].astype(np.complex128)
+        res = {'transmitted_bits': int(n0), 'received_bits': int(n0), 'bits_received_array': brx,
+               'bit_errors': err, 'errors': err, 'ber': float(err / n0), 'snr_db': float(snr_db),
+               'papr_db': float(pa['papr_db']), 'papr_linear': float(pa['papr_linear']), 'signal_tx': sig_tx,
+               'signal_rx': r['signal_rx'][0, 0].astype(np.complex128),
+               'symbols_tx': [ts[i * self.Nd:(i + 1) * self.Nd] for i in range(n_sym)],
+               'symbols_rx': r['data_syms'][0].astype(np.complex128)}
+        self.tx.last_signal_tx = sig_tx
+        self.rx.last_symbols_rx, self.rx.last_bits_rx = res['symbols_rx'], brx
+        self.last_results = res
+        return res
+
+    def calculate_noise_var_zf(self, H_estimate: np.ndarray, snr_db: float) -> float:
+        """core/ofdm_core.py:739-789 (harmonic-mean |H|^2)."""
+        s2 = 1.0 / (10 ** (snr_db / 10))
+        if H_estimate.size == 0:
+            return s2
+        hp = np.maximum(np.abs(np.atleast_1d(H_estimate)) ** 2, 1e-12)
+        if len(hp) == 1:
+            return s2 / hp[0]
+        return s2 / (len(hp) / np.sum(1.0 / hp))
+
+    # -------------------------------------------------------------- SISO + turbo
+    def simulate_siso_coded(self, bits: np.ndarray, snr_db: float = 10.0) -> Dict:
+        """core/ofdm_core.py:925-1338: CRC-24A -> segmentation -> turbo (rate 1/3)
+        -> rate matching -> QAM -> T/F interleave -> OFDM -> channel -> ZF ->
+        max-log LLRs -> dematch -> turbo max-log-MAP (8 it.) -> CRC."""
+        bits = self._bits_in(bits)
+        n0 = len(bits)
+        plan = self._plan(C.CHAIN_CODED, 0, n0, iters=8)
+        ph, z = self._ref_draws(plan.L)
+        r = plan.run([snr_db], bits=(bits & 1).astype(np.uint8)[None], phases=ph[None] if ph.size else None,
+                     noise=z[None], capture=('signal_tx', 'signal_rx', 'data_syms', 'bits_rx', 'tx_syms',
+                                             'H', 'pilot_stats'))
+        cfg = self.config
+        bps, Nd = cfg.bits_per_symbol, self.Nd
+        coded = plan.coded_bits
+        dec = r['bits_rx'][0].astype(np.uint8)
+        err = int(np.sum(bits != dec))
+        sig_tx = r['signal_tx'][0].astype(np.complex128)
+        pa = papr(sig_tx)
+        # T/F de-interleave of the captured TX / RX REs (core/ofdm_core.py:1040-1060, 1174-1207)
+        ncs_tx = -(-coded // bps)
+        rows = -(-ncs_tx // Nd)
+        q = np.arange(ncs_tx)
+        qam = r['tx_syms'][0].astype(np.complex128)[(q % Nd) * rows + q // Nd]
+        ncs = coded // bps
+        rows_rx = -(-ncs // Nd)
+        q = np.arange(ncs)
+        src = (q % Nd) * rows_rx + q // Nd
+        sy = r['data_syms'][0].astype(np.complex128)
+        Hs = r['H'][0, 0].astype(np.complex128)                        # [n_grp][N]
+        Hd = np.concatenate([Hs[l // SLOT_SIZE][self.grid._data] for l in range(plan.n_sym)])
+        sd, hd = sy[src], Hd[src]
+        s2 = 1.0 / (10 ** (snr_db / 10))
+        if self.channels[0].channel_type == 'awgn':
+            nv = np.full(len(sd), s2)
+        else:
+            nv = np.maximum(s2 / np.clip(np.abs(hd) ** 2, 1e-6, 1e6), s2 / 4.0)
+        st = r['pilot_stats'][0, 0].astype(np.float64)
+        ch_snr = float(np.mean(10 * np.log10(st[:, 0] / (st[:, 1] + 1e-10) + 1e-10)))
+        res = {'transmitted_bits': int(n0), 'received_bits': int(n0), 'bits_received_array': dec,
+               'bit_errors': err, 'ber': float(err / n0), 'crc_pass': bool(r['crc_ok'][0]),
+               'snr_db': float(snr_db), 'papr_db': float(pa['papr_db']), 'papr_linear': float(pa['papr_linear']),
+               'coded_bits_length': int(coded), 'signal_tx': sig_tx,
+               'signal_rx': r['signal_rx'][0, 0].astype(np.complex128), 'symbols_tx': qam, 'symbols_rx': sd,
+               'H_estimate': hd, 'channel_snr_db': ch_snr, 'noise_var_mean': float(np.mean(nv))}
+        self.last_results = res
+        return res
+
+    # -------------------------------------------------------------- SIMO
+    def simulate_simo(self, bits: np.ndarray, snr_db: float = 10.0, num_rx: int = 2, combining: str = 'mrc',
+                      parallel: bool = True) -> Dict:
+        """core/ofdm_core.py:1536-1679: independent channel per RX antenna, CRS
+        estimation per antenna, MRC sum(conj(H_i) Y_i)/(sum|H_i|^2 + 1e-10)."""
+        bits = self._bits_in(bits)
+        if num_rx < 1:
+            raise ValueError("num_rx must be >= 1")
+        n0 = len(bits)
+        n_sym = int(np.ceil(n0 / (self.Nd * self.config.bits_per_symbol)))
+        plan = self._plan(C.CHAIN_SIMO, n_sym, n0, num_rx=num_rx)
+        ph, z = self._ref_draws(plan.L, num_rx)
+        r = plan.run([snr_db], bits=(bits & 1).astype(np.uint8)[None], phases=ph[None] if ph.size else None,
+                     noise=z[None], capture=('signal_tx', 'signal_rx', 'data_syms', 'bits_rx', 'tx_syms', 'H'))
+        brx = r['bits_rx'][0].astype(np.int64)
+        err = int(np.sum(bits != brx))
+        sig_tx = r['signal_tx'][0].astype(np.complex128)
+        pa = papr(sig_tx)
+        ts = r['tx_syms'][0].astype(np.complex128)
+        H = r['H'][0].astype(np.complex128)
+        res = {'transmitted_bits': int(n0), 'received_bits': int(n0), 'bits_received_array': brx,
+               'bit_errors': err, 'errors': err, 'ber': float(err / n0), 'snr_db': float(snr_db),
+               'papr_db': float(pa['papr_db']), 'papr_linear': float(pa['papr_linear']), 'signal_tx': sig_tx,
+               'signal_rx_list': [r['signal_rx'][0, i].astype(np.complex128) for i in range(num_rx)],
+               'symbols_tx': [ts[i * self.Nd:(i + 1) * self.Nd] for i in range(n_sym)],
+               'symbols_rx_combined': r['data_syms'][0].astype(np.complex128),
+               'symbols_rx_list': None,
+               'channel_estimates_per_antenna': [[H[a, l // SLOT_SIZE] for l in range(n_sym)]
+                                                 for a in range(num_rx)],
+               'num_rx': num_rx, 'combining_method': combining, 'diversity_level': num_rx,
+               'parallel_processing': parallel}
+        self.last_results = res
+        return res
+
+    def simulate_miso(self, bits, snr_db=10.0):
+        raise NotImplementedError("SFBC Alamouti MISO/MIMO (config 4) is a later-round GPU path")
+
+    def simulate_mimo(self, bits, snr_db=10.0, num_rx=2):
+        raise NotImplementedError("SFBC Alamouti MISO/MIMO (config 4) is a later-round GPU path")
+
+    # -------------------------------------------------------------- sweeps
+    def run_ber_sweep(self, num_bits: int, snr_range, num_trials: int = 1,
+                      progress_callback: Optional[callable] = None) -> Dict:
+        """core/ofdm_core.py:1795-1846.  Bits are drawn once from the global RNG;
+        every trial reuses the reference's frozen channel/noise draws, so the
+        whole (SNR x trial) grid runs as ONE batched GPU call."""
+        bits = np.random.randint(0, 2, num_bits)
+        snrs = np.atleast_1d(snr_range)
+        S, T = len(snrs), int(num_trials)
+        if S * T == 0:
+            return {'snr_db': snrs, 'ber_mean': np.array([]), 'ber_values': np.array([]),
+                    'papr_values': np.array([])}
+        n_sym = int(np.ceil(num_bits / (self.Nd * self.config.bits_per_symbol)))
+        plan = self._plan(C.CHAIN_UNCODED, n_sym, num_bits, max_frames=S * T)
+        ph, z = self._ref_draws(plan.L)
+        snr_f = np.repeat(snrs.astype(np.float64), T)
+        sidx = np.repeat(np.arange(S), T)
+        r = plan.run(snr_f, snr_index=sidx, n_snr=S, bits=(bits & 1).astype(np.uint8)[None],
+                     bits_broadcast=True, phases=ph[None] if ph.size else None, phases_broadcast=True,
+                     noise=z[None], noise_broadcast=True, capture=('signal_tx',))
+        pa = float(papr(r['signal_tx'][0].astype(np.complex128))['papr_db'])
+        fe = r['frame_errors'].reshape(S, T).astype(np.float64)
+        ber = (fe / num_bits).mean(axis=1)
+        done = 0
+        for si, snr in enumerate(snrs):
+            for t in range(T):
+                done += 1
+                if progress_callback:
+                    progress_callback(int(done / (S * T) * 100), f"SNR: {snr:.1f} dB - Trial {t+1}/{T}")
+        return {'snr_db': snrs, 'ber_mean': ber, 'ber_values': ber.copy(), 'papr_values': np.full(S, pa)}
+
+    def run_grid(self, snr_range, num_trials: int, seed: int = 0, coded: bool = False, num_rx: int = 1,
+                 n_bits: Optional[int] = None, frames_per_call: int = 4096, rank: int = 0, world_size: int = 1,
+                 turbo_iters: int = 8) -> Dict:
+        """Device-resident Monte-Carlo BER/BLER grid (SNR x trials).  Frame
+        (s, t) has global id s*num_trials + t; all randomness is Philox keyed by
+        (seed, id), so results are identical for any sharding.  With
+        world_size > 1 this process handles trials t = rank, rank+W, ... and
+        the caller all-reduces the returned `counts`."""
+        snrs = np.atleast_1d(np.asarray(snr_range, dtype=np.float64))
+        S, T = len(snrs), int(num_trials)
+        cfg = self.config
+        if coded:
+            nb = int(n_bits or 27760)
+            plan = self._plan(C.CHAIN_CODED, 0, nb, max_frames=frames_per_call, iters=turbo_iters)
+        else:
+            nb = int(n_bits or SLOT_SIZE * self.Nd * cfg.bits_per_symbol)
+            n_sym = int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol)))
+            chain = C.CHAIN_SIMO if num_rx > 1 else C.CHAIN_UNCODED
+            plan = self._plan(chain, n_sym, nb, num_rx=num_rx, max_frames=frames_per_call)
+        ids = np.array([s * T + t for s in range(S) for t in range(rank, T, world_size)], dtype=np.uint64)
+        counts = np.zeros((S, 4), dtype=np.uint64)
+        for i in range(0, len(ids), frames_per_call):
+            chunk = ids[i:i + frames_per_call]
+            si = (chunk // T).astype(np.int32)
+            r = plan.run(snrs[si], snr_index=si, n_snr=S, seed=seed, frame_ids=chunk)
+            counts += r['counts']
+        with np.errstate(divide='ignore', invalid='ignore'):
+            ber = counts[:, 0] / np.maximum(counts[:, 1], 1)
+            bler = counts[:, 2] / np.maximum(counts[:, 3], 1)
+        return {'snr_db': snrs, 'counts': counts, 'ber': ber, 'bler': bler, 'bit_errors': counts[:, 0],
+                'bits': counts[:, 1], 'block_errors': counts[:, 2], 'blocks': counts[:, 3], 'plan': plan}
+
+
+def simulate_spatial_multiplexing(*args, **kwargs):
+    """core/ofdm_core.py:2489-2815 (4x4 MMSE, config 5): later-round GPU path."""
+    raise NotImplementedError("spatial multiplexing (config 5) is a later-round GPU path")

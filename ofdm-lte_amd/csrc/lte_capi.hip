@@ -944,10 +944,14 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
       LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
     }
     const int G = (B + 63) / 64;
+    std::vector<TurboJob> jobs(p->C);
     for (int r = 0; r < p->C; ++r) {
-      Timer t(p, KN_TURBO);
       const CbInfo& c = p->cbs[r];
-      LCHK(launch_turbo(s, p->blk[r].p, p->ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, d.turbo_iters, G, TM_DEC1));
+      jobs[r] = TurboJob{p->blk[r].p, p->ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, G};
+    }
+    {
+      Timer t(p, KN_TURBO);
+      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1));
     }
     {
       Timer t(p, KN_CRC);

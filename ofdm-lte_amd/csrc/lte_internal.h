@@ -51,6 +51,19 @@ int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t*
                    const int64_t* rows, int C);
 int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
                  int G, int mode);
+struct TurboJob {           // one CB slot of a batch: G groups of 64 code blocks of size K
+  float* blk;
+  float* ck;
+  uint32_t* bits;
+  int K, f1, f2, G;
+};
+constexpr int TURBO_MAX_JOBS = 16;
+struct TurboJobs {
+  TurboJob j[TURBO_MAX_JOBS];
+  int n;
+  int prefix[TURBO_MAX_JOBS + 1];
+};
+int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode);
 int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
                      const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
                      uint8_t* cap_bits);
@@ -65,7 +78,7 @@ enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_FINAL = 2, TM_APP = 3 };
 // turbo geometry: rows of one (r, group) block = 4K+12:
 //   [0,K+3) LS (sys + sys1 tail) | [K+3,2K+6) LP1 | [2K+6,3K+9) LP2 | [3K+9,3K+12) LS2T | [3K+12,4K+12) LE
 __host__ __device__ inline int64_t turbo_rows(int K) { return 4LL * K + 12; }
-__host__ __device__ inline int turbo_nwin(int K) { return K / 8 + 1; }
+__host__ __device__ inline int turbo_nwin(int K) { return K / 4 + 1; }  // sized for windows >= 4
 __host__ __device__ inline int turbo_kw(int K) { return (K + 31) / 32; }
 
 }  // namespace lte

@@ -90,6 +90,10 @@ __device__ __forceinline__ int modadd(int a, int b, int K) { a += b; return a >=
 __device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 0 ? a + K : a; }
 
 constexpr int RS = 64;  // row stride (floats): 64 lanes
+#ifndef LTE_TURBO_W
+#define LTE_TURBO_W 4
+#endif
+constexpr int TW = LTE_TURBO_W;  // window (steps between alpha checkpoints)
 
 // Buffer-resource row accessor: the 128-bit descriptor (SGPRs) covers one
 // wave's block; a row is addressed by a scalar byte offset (soffset) and the
@@ -137,7 +141,7 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   const RowPtr<float> LE{rb, 3 * K + 12, vo};
   const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * 8 * RS * 4)), 0, vo};
   const RowPtr<uint32_t> bout{make_rsrc(wbout, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
-  const int nfull = K >> 3;
+  const int nfull = K / TW;
   const int tf2 = (2 * f2) % K;
   const bool use_la = !first;
 
@@ -151,10 +155,10 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   for (int w = 0; w < nfull; ++w) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) ck.st(w * 8 + s, a[s]);
-    float ls[8], lp[8], la[8];
+    float ls[TW], lp[TW], la[TW];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = w * 8 + j;
+    for (int j = 0; j < TW; ++j) {
+      const int k = w * TW + j;
       const int p = (MODE == TM_DEC2) ? pi : k;
       ls[j] = LS.ld(p);
       lp[j] = LP.ld(k);
@@ -162,7 +166,7 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
       if (MODE == TM_DEC2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < TW; ++j) {
       float c[4], o[8];
       gam(ls[j], lp[j], la[j], c);
       fwd(a, c, o);
@@ -190,20 +194,20 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   // pi/d are now at k = K; step back to the start of the last full window
   if (MODE == TM_DEC2) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+    for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
   }
   uint32_t acc = 0;
 #pragma unroll 1
   for (int w = nfull - 1; w >= 0; --w) {
-    float A[8][8];
+    float A[TW][8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) A[0][s] = ck.ld(w * 8 + s);
-    float ls[8], lp[8], la[8];
-    int pl[8];
+    float ls[TW], lp[TW], la[TW];
+    int pl[TW];
     int pp = pi, dd = d;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = w * 8 + j;
+    for (int j = 0; j < TW; ++j) {
+      const int k = w * TW + j;
       const int p = (MODE == TM_DEC2) ? pp : k;
       pl[j] = p;
       ls[j] = LS.ld(p);
@@ -212,14 +216,14 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
       if (MODE == TM_DEC2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
     }
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
+    for (int j = 0; j < TW - 1; ++j) {
       float c[4];
       gam(ls[j], lp[j], la[j], c);
       fwd(A[j], c, A[j + 1]);
     }
 #pragma unroll
-    for (int j = 7; j >= 0; --j) {
-      const int k = w * 8 + j;
+    for (int j = TW - 1; j >= 0; --j) {
+      const int k = w * TW + j;
       float c[4], t0[8], t1[8];
       gam(ls[j], lp[j], la[j], c);
       bterms(b, c, t0, t1);
@@ -241,37 +245,59 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
     }
     if (MODE == TM_DEC2) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+      for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
     }
   }
 }
 
-// grid: ceil(G/4) blocks of 256 threads; wave = one group of 64 code blocks.
-__global__ __launch_bounds__(256) void k_turbo(float* __restrict__ blk, float* __restrict__ ckpt,
-                                               uint32_t* __restrict__ bits, int K, int f1, int f2,
-                                               int iters, int G, int mode) {
-  const int g = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// One launch decodes every code-block slot of the batch: wave w -> job r
+// (CB slot, i.e. one K) and frame group g.  256-thread blocks = 4 independent
+// waves (no LDS, no barriers).
+__global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mode) {
+  const int wg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (g >= G) return;
-  float* base = blk + (size_t)g * turbo_rows(K) * RS;
-  float* ck = ckpt + (size_t)g * (turbo_nwin(K) * 8) * RS;
-  uint32_t* bo = bits + (size_t)g * turbo_kw(K) * RS;
+  if (wg >= jobs.prefix[jobs.n]) return;
+  int r = 0;
+  while (wg >= jobs.prefix[r + 1]) ++r;
+  const TurboJob jb = jobs.j[r];
+  const int g = wg - jobs.prefix[r];
+  const int K = jb.K;
+  float* base = jb.blk + (size_t)g * turbo_rows(K) * RS;
+  float* ck = jb.ck + (size_t)g * (turbo_nwin(K) * 8) * RS;
+  uint32_t* bo = jb.bits + (size_t)g * turbo_kw(K) * RS;
   if (mode == TM_APP) {
-    half_pass<TM_APP>(base, ck, bo, lane, K, f1, f2, false);
+    half_pass<TM_APP>(base, ck, bo, lane, K, jb.f1, jb.f2, false);
     return;
   }
   for (int it = 0; it < iters; ++it) {
-    half_pass<TM_DEC1>(base, ck, bo, lane, K, f1, f2, it == 0);
-    half_pass<TM_DEC2>(base, ck, bo, lane, K, f1, f2, false);
+    half_pass<TM_DEC1>(base, ck, bo, lane, K, jb.f1, jb.f2, it == 0);
+    half_pass<TM_DEC2>(base, ck, bo, lane, K, jb.f1, jb.f2, false);
   }
-  half_pass<TM_FINAL>(base, ck, bo, lane, K, f1, f2, iters == 0);
+  half_pass<TM_FINAL>(base, ck, bo, lane, K, jb.f1, jb.f2, iters == 0);
+}
+
+int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode) {
+  for (int o = 0; o < n; o += TURBO_MAX_JOBS) {
+    TurboJobs J{};
+    J.n = n - o < TURBO_MAX_JOBS ? n - o : TURBO_MAX_JOBS;
+    J.prefix[0] = 0;
+    for (int i = 0; i < J.n; ++i) {
+      J.j[i] = jobs[o + i];
+      J.prefix[i + 1] = J.prefix[i] + jobs[o + i].G;
+    }
+    const int waves = J.prefix[J.n];
+    if (waves == 0) continue;
+    hipLaunchKernelGGL(k_turbo, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+  }
+  return 0;
 }
 
 int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
                  int G, int mode) {
-  if (G <= 0) return 0;
-  hipLaunchKernelGGL(k_turbo, dim3((G + 3) / 4), dim3(256), 0, s, blk, ckpt, bits, K, f1, f2, iters, G, mode);
-  return (int)hipGetLastError();
+  TurboJob j{blk, ckpt, bits, K, f1, f2, G};
+  return launch_turbo_jobs(s, &j, 1, iters, mode);
 }
 
 // ---------------------------------------------------------------------------

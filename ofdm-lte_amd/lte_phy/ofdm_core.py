@@ -524,15 +524,17 @@ class OFDMSimulator:
                      bits_broadcast=True, phases=ph[None] if ph.size else None, phases_broadcast=True,
                      noise=z[None], noise_broadcast=True, capture=('signal_tx',))
         pa = float(papr(r['signal_tx'][0].astype(np.complex128))['papr_db'])
-        fe = r['frame_errors'].reshape(S, T).astype(np.float64)
-        ber = (fe / num_bits).mean(axis=1)
+        fe = r['frame_errors'].reshape(S, T)
+        # same reduction as the reference: np.mean over the per-trial python floats
+        ber = np.array([np.mean([float(int(e) / num_bits) for e in fe[i]]) for i in range(S)])
+        papr_v = np.array([np.mean([pa] * T) for _ in range(S)])
         done = 0
         for si, snr in enumerate(snrs):
             for t in range(T):
                 done += 1
                 if progress_callback:
                     progress_callback(int(done / (S * T) * 100), f"SNR: {snr:.1f} dB - Trial {t+1}/{T}")
-        return {'snr_db': snrs, 'ber_mean': ber, 'ber_values': ber.copy(), 'papr_values': np.full(S, pa)}
+        return {'snr_db': snrs, 'ber_mean': ber, 'ber_values': ber.copy(), 'papr_values': papr_v}
 
     def run_grid(self, snr_range, num_trials: int, seed: int = 0, coded: bool = False, num_rx: int = 1,
                  n_bits: Optional[int] = None, frames_per_call: int = 4096, rank: int = 0, world_size: int = 1,

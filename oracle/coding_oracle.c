@@ -202,3 +202,92 @@ void or_turbo_decode_batch(const double *llr, int ncb, int K, int iters,
         or_turbo_decode(llr + (size_t)c * (3 * K + 12), K, iters, perm,
                         out + (size_t)c * K, NULL);
 }
+
+/*
+ * Kernel-verification model (NOT the reference semantics): the GPU decoder's
+ * float32 arithmetic -- metrics normalised to state 0 every step, -1e30
+ * sentinels, gamma = (L_s/2 +- L_p/2) +- L_a/2, LLR = max(a + t0) - max(a + t1)
+ * with t = beta + gamma -- restated in C so the HIP kernel can be checked
+ * bit-for-bit.  Its distance to the float64 reference above is what the
+ * BER-level parity tests measure.
+ */
+static inline float fmx(float a, float b) { return a > b ? a : (b > a ? b : a); }
+
+static void bcjr_f32(const float *Ls, const float *Lp, const float *La, int n, int K, float *Lapp, float *alpha)
+{
+    build_trellis();
+    const float NEG = -1.0e30f;
+    float a[8], b[8], t0[8], t1[8];
+    a[0] = 0.0f;
+    for (int s = 1; s < 8; ++s) a[s] = NEG;
+    for (int k = 0; k < K; ++k) {
+        memcpy(alpha + (size_t)k * 8, a, sizeof a);
+        float hs = 0.5f * Ls[k], hp = 0.5f * Lp[k], ha = 0.5f * La[k];
+        float sp = hs + hp, sm = hs - hp;
+        float c[4] = {sp + ha, sp - ha, sm + ha, sm - ha};
+        float o[8];
+        for (int ns = 0; ns < 8; ++ns) {
+            int f = ns >> 2, s0 = (ns >> 1) & 1, s1 = ns & 1;
+            int p0 = f ^ s0, u0 = f ^ s1, p1 = f ^ s0 ^ 1, u1 = f ^ s1 ^ 1;
+            float g0 = f == 0 ? c[p0 * 2 + u0] : -c[(1 - p0) * 2 + (1 - u0)];
+            float g1 = f == 0 ? c[p1 * 2 + u1] : -c[(1 - p1) * 2 + (1 - u1)];
+            float v0 = a[4 * s0 + 2 * s1] + g0, v1 = a[4 * s0 + 2 * s1 + 1] + g1;
+            o[ns] = fmx(v0, v1);
+        }
+        float n0 = o[0];
+        a[0] = 0.0f;
+        for (int s = 1; s < 8; ++s) a[s] = o[s] - n0;
+    }
+    b[0] = 0.0f;
+    for (int s = 1; s < 8; ++s) b[s] = NEG;
+    for (int k = n - 1; k >= 0; --k) {
+        float la = k < K ? La[k] : 0.0f;
+        float hs = 0.5f * Ls[k], hp = 0.5f * Lp[k], ha = 0.5f * la;
+        float sp = hs + hp, sm = hs - hp;
+        float c[4] = {sp + ha, sp - ha, sm + ha, sm - ha};
+        for (int s = 0; s < 8; ++s) {
+            int s0 = s >> 2, s1 = (s >> 1) & 1, s2 = s & 1;
+            int fb = s1 ^ s2, par = fb ^ s0 ^ s2, ns = 4 * fb + 2 * s0 + s1;
+            float g = fb == 0 ? c[par * 2] : -c[(1 - par) * 2 + 1];
+            t0[s] = b[ns] + g;
+            t1[s] = b[ns ^ 4] - g;
+        }
+        if (k < K) {
+            const float *A = alpha + (size_t)k * 8;
+            float m0 = A[0] + t0[0], m1 = A[0] + t1[0];
+            for (int s = 1; s < 8; ++s) { m0 = fmx(m0, A[s] + t0[s]); m1 = fmx(m1, A[s] + t1[s]); }
+            Lapp[k] = m0 - m1;
+        }
+        for (int s = 0; s < 8; ++s) b[s] = fmx(t0[s], t1[s]);
+        float n0 = b[0];
+        b[0] = 0.0f;
+        for (int s = 1; s < 8; ++s) b[s] -= n0;
+    }
+}
+
+void or_turbo_decode_f32(const float *llr, int K, int iters, const int32_t *perm, uint8_t *out)
+{
+    const int n = K + 3;
+    float *ls1 = malloc(sizeof(float) * n), *lp1 = malloc(sizeof(float) * n);
+    float *ls2 = malloc(sizeof(float) * n), *lp2 = malloc(sizeof(float) * n);
+    float *la = malloc(sizeof(float) * n), *lapp = malloc(sizeof(float) * n);
+    float *le = calloc(K, sizeof(float)), *alpha = malloc(sizeof(float) * 8 * (size_t)n);
+    for (int k = 0; k < K; ++k) { ls1[k] = llr[3 * k]; lp1[k] = llr[3 * k + 1]; lp2[k] = llr[3 * k + 2]; }
+    for (int t = 0; t < 3; ++t) {
+        ls1[K + t] = llr[3 * K + t]; lp1[K + t] = llr[3 * K + 3 + t];
+        ls2[K + t] = llr[3 * K + 6 + t]; lp2[K + t] = llr[3 * K + 9 + t];
+    }
+    for (int k = 0; k < K; ++k) ls2[k] = ls1[perm[k]];
+    for (int it = 0; it < iters; ++it) {
+        for (int k = 0; k < K; ++k) la[k] = it == 0 ? 0.0f : le[k];
+        bcjr_f32(ls1, lp1, la, n, K, lapp, alpha);
+        for (int k = 0; k < K; ++k) le[k] = (lapp[k] - la[k]) - ls1[k];
+        for (int k = 0; k < K; ++k) la[k] = le[perm[k]];
+        bcjr_f32(ls2, lp2, la, n, K, lapp, alpha);
+        for (int k = 0; k < K; ++k) le[perm[k]] = (lapp[k] - la[k]) - ls2[k];
+    }
+    for (int k = 0; k < K; ++k) la[k] = iters == 0 ? 0.0f : le[k];
+    bcjr_f32(ls1, lp1, la, n, K, lapp, alpha);
+    for (int k = 0; k < K; ++k) out[k] = lapp[k] < 0.0f ? 1 : 0;
+    free(ls1); free(lp1); free(ls2); free(lp2); free(la); free(lapp); free(le); free(alpha);
+}

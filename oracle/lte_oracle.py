@@ -488,6 +488,8 @@ def lib():
         L.or_turbo_decode.argtypes = [P(ctypes.c_double), ctypes.c_int, ctypes.c_int,
                                       P(ctypes.c_int32), P(ctypes.c_uint8), P(ctypes.c_double)]
         L.or_bcjr_maxlog.argtypes = [P(ctypes.c_double)] * 3 + [ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
+        L.or_turbo_decode_f32.argtypes = [P(ctypes.c_float), ctypes.c_int, ctypes.c_int, P(ctypes.c_int32),
+                                          P(ctypes.c_uint8)]
         L.or_bcjr_scratch_doubles.restype = ctypes.c_size_t
         L.or_bcjr_scratch_doubles.argtypes = [ctypes.c_int]
         _lib = L
@@ -759,6 +761,17 @@ def turbo_decode(llr, K, num_iterations=5, trace=False):
     return (out, tr) if trace else out
 
 
+def turbo_decode_f32_model(llr, K, num_iterations=8):
+    """Kernel-verification model: the GPU decoder's float32 algorithm
+    (coding_oracle.c or_turbo_decode_f32).  Not the reference semantics."""
+    L = np.ascontiguousarray(np.asarray(llr, dtype=np.float32))
+    perm = np.ascontiguousarray(qpp_perm(K))
+    out = np.zeros(K, dtype=np.uint8)
+    lib().or_turbo_decode_f32(_p(L, ctypes.c_float), K, num_iterations, _p(perm, ctypes.c_int32),
+                              _p(out, ctypes.c_uint8))
+    return out
+
+
 def bcjr_app(ls, lp, la):
     """LogMAPDecoder.decode a-posteriori output (turbo_decoder.py:181-278)."""
     n = len(ls)
@@ -837,14 +850,15 @@ def coded_rx_llrs(num: Numerology, rx, coded_len, snr_db, channel):
     return L, sd, hd, nv, snr_est
 
 
-def coded_rx_decode(L, plan, rm_lens, iters=8):
-    """RX decoding chain (core/ofdm_core.py:1267-1299)."""
+def coded_rx_decode(L, plan, rm_lens, iters=8, f32_model=False):
+    """RX decoding chain (core/ofdm_core.py:1267-1299).  f32_model=True swaps
+    the float64 reference decoder for the GPU kernel's float32 model."""
     off = 0
     dec = []
     for (K, F, info, o, crc), E in zip(plan, rm_lens):
         dm = rate_dematch(L[off:off + E], K, 0)
         off += E
-        dec.append(turbo_decode(dm, K, iters))
+        dec.append(turbo_decode_f32_model(dm, K, iters) if f32_model else turbo_decode(dm, K, iters))
     tbc = desegment(dec, plan)
     ok = check_crc24a(tbc)
     return (tbc[:-24] if len(tbc) >= 24 else tbc), ok

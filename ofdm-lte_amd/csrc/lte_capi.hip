@@ -335,7 +335,7 @@ struct lte_plan {
   DBuf<CbInfo> cbi;
   DBuf<int32_t> tx_map, rx_map, delays;
   DBuf<float> gains;
-  DBuf<uint32_t> pw, cbw, enc, inj_bits;
+  DBuf<uint32_t> pw, enc, inj_bits;
   DBuf<float2> x, y, coef, H, capbuf, captx;
   DBuf<float> phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
   DBuf<uint32_t> frame_err, frame_crc;
@@ -648,7 +648,6 @@ static int plan_alloc(lte_plan* p) {
   bad |= p->frame_err.alloc(B) != 0;
   bad |= p->frame_crc.alloc(B) != 0;
   if (coded) {
-    bad |= p->cbw.alloc(B * p->C * p->KWmax) != 0;
     bad |= p->enc.alloc(B * p->enc_words) != 0;
     bad |= p->llr.alloc(B * p->n_re_bits) != 0;
     p->blk.resize(p->C);
@@ -662,7 +661,7 @@ static int plan_alloc(lte_plan* p) {
       const int K = p->cbs[r].K;
       rows[r] = turbo_rows(K);
       bad |= p->blk[r].alloc((size_t)G * rows[r] * 64) != 0;
-      bad |= p->ckpt[r].alloc((size_t)G * turbo_nwin(K) * 8 * 64) != 0;
+      bad |= p->ckpt[r].alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS * 64) != 0;
       kw[r] = turbo_kw(K);
       bad |= p->decb[r].alloc((size_t)G * kw[r] * 64) != 0;
       if (!bad) HIPCHK(hipMemset(p->blk[r].p, 0, p->blk[r].n * sizeof(float)));
@@ -739,7 +738,7 @@ int lte_plan_destroy(lte_plan* p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   p->tabs.release();
   p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release(); p->gains.release();
-  p->pw.release(); p->cbw.release(); p->enc.release(); p->inj_bits.release();
+  p->pw.release(); p->enc.release(); p->inj_bits.release();
   p->x.release(); p->y.release(); p->coef.release(); p->H.release(); p->capbuf.release(); p->captx.release();
   p->phases.release(); p->pow_part.release(); p->pstats.release(); p->npow.release(); p->llr.release();
   p->snr_lin.release(); p->inj_ph.release(); p->inj_z.release();
@@ -880,7 +879,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (do_tx) {
     if (coded) {
       Timer t(p, KN_ENCODE);
-      LCHK(launch_encode(s, p->pw.p, p->PW, p->cbw.p, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
+      LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
     }
     float2* cts = nullptr;
     if (a->cap_tx_syms) {
@@ -1111,15 +1110,15 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out)
   std::vector<uint32_t> w((size_t)ncb * PW);
   for (int64_t c = 0; c < ncb; ++c) pack_bits(bits + c * K, K, &w[c * PW], PW);
   CbInfo ci{K, 0, K, 0, 0, f1, f2, 3 * K + 12};
-  DBuf<uint32_t> dpw, dcb, denc;
+  DBuf<uint32_t> dpw, denc;
   DBuf<CbInfo> dci;
   std::vector<CbInfo> vci{ci};
-  if (dpw.alloc(w.size()) || dcb.alloc((size_t)ncb * KW) || denc.alloc((size_t)ncb * 3 * EW) || upload(dci, vci))
+  if (dpw.alloc(w.size()) || denc.alloc((size_t)ncb * 3 * EW) || upload(dci, vci))
     return fail(LTE_ENOMEM, "buffers");
   std::vector<uint32_t> e((size_t)ncb * 3 * EW);
   int rc = LTE_OK;
   if (hipMemcpy(dpw.p, w.data(), w.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      launch_encode(nullptr, dpw.p, PW, dcb.p, KW, denc.p, EW, dci.p, 1, (int)ncb) ||
+      launch_encode(nullptr, dpw.p, PW, KW, denc.p, EW, dci.p, 1, (int)ncb) ||
       hipMemcpy(e.data(), denc.p, e.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "encode failed");
   if (rc == LTE_OK) {
@@ -1138,7 +1137,7 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out)
       }
     }
   }
-  dpw.release(); dcb.release(); denc.release(); dci.release();
+  dpw.release(); denc.release(); dci.release();
   return rc;
 }
 
@@ -1179,7 +1178,7 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const float* llr, const
   DBuf<float> db, dck;
   DBuf<uint32_t> dbits;
   const int KW = turbo_kw(K);
-  if (db.alloc(h.size()) || dck.alloc((size_t)G * turbo_nwin(K) * 8 * 64) || dbits.alloc((size_t)G * KW * 64))
+  if (db.alloc(h.size()) || dck.alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS * 64) || dbits.alloc((size_t)G * KW * 64))
     return fail(LTE_ENOMEM, "turbo buffers");
   int rc = LTE_OK;
   std::vector<uint32_t> hb((size_t)G * KW * 64);

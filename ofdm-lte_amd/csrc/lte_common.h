@@ -84,7 +84,7 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N, int log2N, const flo
                                         int tid, bool active) {
   const int T = N >> 3;
   const int q4 = N >> 2;
-  int Ns = 1;
+  int Ns = 1, lNs = 0;   // Ns = 4^s; all index arithmetic is shifts (N, Ns powers of 2)
   const int n4 = log2N >> 1;
   for (int s = 0; s < n4; ++s) {
     float2 v[2][4];
@@ -95,7 +95,7 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N, int log2N, const flo
         const int j = tid + q * T;
         jj[q] = j;
         const int k = j & (Ns - 1);
-        const int step = N / (Ns << 2);
+        const int step = 1 << (log2N - lNs - 2);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[q][r] = buf[j + r * q4];
 #pragma unroll
@@ -115,13 +115,14 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N, int log2N, const flo
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int j = jj[q];
-        const int idx = (j / Ns) * (Ns << 2) + (j & (Ns - 1));
+        const int idx = ((j >> lNs) << (lNs + 2)) + (j & (Ns - 1));
 #pragma unroll
         for (int r = 0; r < 4; ++r) buf[idx + r * Ns] = v[q][r];
       }
     }
     __syncthreads();
     Ns <<= 2;
+    lNs += 2;
   }
   if (log2N & 1) {  // final radix-2 stage (Ns == N/2)
     const int h = N >> 1;
@@ -133,7 +134,7 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N, int log2N, const flo
         const int j = tid + q * T;
         jj[q] = j;
         const int k = j & (Ns - 1);
-        const int step = N / (Ns << 1);
+        const int step = 1 << (log2N - lNs - 1);
         v[q][0] = buf[j];
         v[q][1] = cmul(buf[j + h], twid<INV>(tw, k * step));
         const float2 t0 = cadd(v[q][0], v[q][1]), t1 = csub(v[q][0], v[q][1]);
@@ -146,7 +147,7 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N, int log2N, const flo
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = jj[q];
-        const int idx = (j / Ns) * (Ns << 1) + (j & (Ns - 1));
+        const int idx = ((j >> lNs) << (lNs + 1)) + (j & (Ns - 1));
         buf[idx] = v[q][0];
         buf[idx + Ns] = v[q][1];
       }

@@ -28,8 +28,8 @@ struct Grid {                 // device pointers + numerology for one plan
 // launchers (return hipError_t as int)
 int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, const uint64_t* fid,
                    uint64_t seed, int B, const uint32_t* inj, int64_t inj_stride);
-int launch_encode(hipStream_t s, const uint32_t* pw, int PW, uint32_t* cbw, int KWmax, uint32_t* enc,
-                  int EW, const CbInfo* cbi_dev, int C, int B);
+int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
+                  const CbInfo* cbi_dev, int C, int B);
 int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
                    int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms = nullptr);
 int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* gains_dev, const uint64_t* fid,
@@ -79,6 +79,8 @@ enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_FINAL = 2, TM_APP = 3 };
 //   [0,K+3) LS (sys + sys1 tail) | [K+3,2K+6) LP1 | [2K+6,3K+9) LP2 | [3K+9,3K+12) LS2T | [3K+12,4K+12) LE
 __host__ __device__ inline int64_t turbo_rows(int K) { return 4LL * K + 12; }
 __host__ __device__ inline int turbo_nwin(int K) { return K / 4 + 1; }  // sized for windows >= 4
+// alpha checkpoint rows per window: states 1..7 (state 0 is 0 after normalisation)
+constexpr int TURBO_CK_ROWS = 7;
 __host__ __device__ inline int turbo_kw(int K) { return (K + 31) / 32; }
 
 }  // namespace lte

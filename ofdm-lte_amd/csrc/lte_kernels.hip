@@ -76,15 +76,34 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 // tx_map (rate_match_turbo + T/F interleaver, rate_matching.py:193-297,
 // ofdm_core.py:1040-1099), ResourceMapper.map_symbols (resource_mapper.py:
 // 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
-__global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, int coded, const uint32_t* __restrict__ pw, int PW,
+// QAM point of natural-binary index idx (modulator.py:28-59, I-major; QPSK
+// [1+1j, 1-1j, -1+1j, -1-1j]/sqrt 2), levels folded to float constants equal
+// to the float64 table cast to float.
+template <int BPS>
+__device__ __forceinline__ float2 qam_point(int idx) {
+  if constexpr (BPS == 2) {
+    constexpr float a = (float)(1.0 / 1.4142135623730951);
+    return make_float2((idx & 2) ? -a : a, (idx & 1) ? -a : a);
+  } else {
+    constexpr int H = BPS / 2, NL = 1 << H;
+    constexpr double S = BPS == 4 ? 3.1622776601683795 : 6.48074069840786;
+    float lv[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) lv[i] = (float)((2.0 * i - (NL - 1)) / S);
+    return make_float2(lv[idx >> H], lv[idx & (NL - 1)]);
+  }
+}
+
+template <int CODED, int BPS>
+__global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
                                                 const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B,
                                                 float2* __restrict__ cap_syms) {
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
-  const int64_t gs = (int64_t)blockIdx.x * spw + slot;
-  const int b = (int)(gs / g.n_sym), l = (int)(gs % g.n_sym);
+  const int gs = blockIdx.x * spw + slot;
+  const int b = gs / g.n_sym, l = gs - b * g.n_sym;
   const bool active = slot < spw && b < B;
   float2* buf = sm + slot * N;
   if (active) {
@@ -95,21 +114,24 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, int coded, const uint32_
     const uint32_t* fb = pw + (size_t)b * PW;
     const uint32_t* fe = enc + (size_t)b * enc_words;
     for (int j = tid; j < g.Nd; j += T) {
-      const int64_t t0 = ((int64_t)l * g.Nd + j) * g.bps;
+      const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
       int idx = 0;
       bool zero = false;
-      for (int m = 0; m < g.bps; ++m) {
-        uint32_t bit;
-        if (coded) {
-          const int src = tx_map[t0 + m];
-          if (src == -2) { zero = true; bit = 0; }
-          else bit = src >= 0 ? getbit(fe, src) : 0u;
-        } else {
-          bit = getbit(fb, t0 + m);
+      if constexpr (CODED) {
+        int src[BPS];
+#pragma unroll
+        for (int m = 0; m < BPS; ++m) src[m] = tx_map[t0 + m];
+#pragma unroll
+        for (int m = 0; m < BPS; ++m) {
+          zero |= src[m] == -2;
+          const uint32_t bit = src[m] >= 0 ? getbit(fe, src[m]) : 0u;
+          idx = (idx << 1) | (int)bit;
         }
-        idx = (idx << 1) | (int)bit;
+      } else {
+#pragma unroll
+        for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, t0 + m);
       }
-      const float2 sym = zero ? make_float2(0.f, 0.f) : g.constel[idx];
+      const float2 sym = zero ? make_float2(0.f, 0.f) : qam_point<BPS>(idx);
       buf[g.data_idx[j]] = sym;
       if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + j] = sym;
     }
@@ -129,9 +151,18 @@ int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, 
                    int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms) {
   const int spw = WG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym;
+  if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
-  hipLaunchKernelGGL(k_ofdm_tx, dim3(blocks), dim3(WG), spw * g.N * sizeof(float2), s, g, coded, pw, PW, enc,
-                     enc_words, tx_map, x, B, cap_syms);
+  const size_t shm = spw * g.N * sizeof(float2);
+#define LTE_TX(C_, B_)                                                                                             \
+  hipLaunchKernelGGL((k_ofdm_tx<C_, B_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words, tx_map, x, B, \
+                     cap_syms)
+  if (coded) {
+    if (g.bps == 2) LTE_TX(1, 2); else if (g.bps == 4) LTE_TX(1, 4); else LTE_TX(1, 6);
+  } else {
+    if (g.bps == 2) LTE_TX(0, 2); else if (g.bps == 4) LTE_TX(0, 4); else LTE_TX(0, 6);
+  }
+#undef LTE_TX
   return (int)hipGetLastError();
 }
 
@@ -387,34 +418,78 @@ __device__ __forceinline__ int hard_index(float2 y, int bps, float scale) {
   return (level_idx(y.x, scale, nl) << (bps >> 1)) | level_idx(y.y, scale, nl);
 }
 
+// sqrt(2), sqrt(10), sqrt(42): the QAM normalisations of modulator.py:28-59
+template <int BPS>
+__host__ __device__ constexpr double qam_norm() { return BPS == 2 ? 1.4142135623730951 : (BPS == 4 ? 3.1622776601683795 : 6.48074069840786); }
+
 // max-log LLRs (core/ofdm_core.py:791-923): QPSK 2*sqrt(2)*y/nv (no clip);
 // 16/64-QAM (min_{b=1} d^2 - min_{b=0} d^2)/(2 nv) clipped to +-10.  The
-// natural-binary map makes the metric separable per axis.
-__device__ __forceinline__ void llr_axis(float v, float scale, int nbits, float inv2nv, float* out) {
-  const int nl = 1 << nbits;
-  float m0[3] = {3.4e38f, 3.4e38f, 3.4e38f}, m1[3] = {3.4e38f, 3.4e38f, 3.4e38f};
-  for (int i = 0; i < nl; ++i) {
-    const float lv = (float)(2 * i - (nl - 1)) / scale;
+// natural-binary map makes the metric separable per axis.  NB bits per axis,
+// levels folded to constants (correctly rounded from the float64 grid).
+template <int NB>
+__device__ __forceinline__ void llr_axis(float v, float inv2nv, float* out) {
+  constexpr int NL = 1 << NB;
+  constexpr double S = NB == 2 ? 3.1622776601683795 : 6.48074069840786;
+  float m0[NB], m1[NB];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb) { m0[bb] = 3.4e38f; m1[bb] = 3.4e38f; }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const float lv = (float)((2.0 * i - (NL - 1)) / S);
     const float d = (v - lv) * (v - lv);
-    for (int bb = 0; bb < nbits; ++bb) {
-      if ((i >> (nbits - 1 - bb)) & 1) m1[bb] = fminf(m1[bb], d);
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+      if ((i >> (NB - 1 - bb)) & 1) m1[bb] = fminf(m1[bb], d);
       else m0[bb] = fminf(m0[bb], d);
     }
   }
-  for (int bb = 0; bb < nbits; ++bb) out[bb] = fminf(10.f, fmaxf(-10.f, (m1[bb] - m0[bb]) * inv2nv));
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb) out[bb] = fminf(10.f, fmaxf(-10.f, (m1[bb] - m0[bb]) * inv2nv));
 }
 
-__device__ __forceinline__ void soft_demap(float2 y, float nv, int bps, float scale, float* out) {
-  if (bps == 2) {
-    const float k = (2.0f / nv) * 1.41421356237309515f;
+template <int BPS>
+__device__ __forceinline__ void soft_demap(float2 y, float nv, float* out) {
+  if constexpr (BPS == 2) {
     out[0] = (2.0f / nv) * y.x * 1.41421356237309515f;
     out[1] = (2.0f / nv) * y.y * 1.41421356237309515f;
-    (void)k;
+  } else {
+    const float inv2nv = 1.0f / (2.0f * nv);
+    llr_axis<BPS / 2>(y.x, inv2nv, out);
+    llr_axis<BPS / 2>(y.y, inv2nv, out + BPS / 2);
+  }
+}
+
+// y / h (lte_receiver.py:154-180 divides by H + 1e-6): multiply by the conjugate
+// over |h|^2; f32 relative error a few ulp (no over/underflow at these magnitudes).
+__device__ __forceinline__ float2 zf_div(float2 y, float2 h) {
+  const float r = 1.0f / (h.x * h.x + h.y * h.y);
+  return make_float2((y.x * h.x + y.y * h.y) * r, (y.y * h.x - y.x * h.y) * r);
+}
+
+// Noise-add for one OFDM symbol into LDS, one Philox call per pair of
+// samples (sample n uses half (n&1) of counter n>>1 -- same draws as
+// load_symbol_noisy, at half the generator cost).
+__device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __restrict__ yf, int N, int cp, int l,
+                                                   float sigma, uint64_t seed, uint64_t frame, int rx,
+                                                   const float* __restrict__ zf, int L, int tid, int T) {
+  const int off = l * (N + cp) + cp;
+  if (zf) {
+    load_symbol_noisy(buf, yf, N, cp, l, sigma, seed, frame, rx, zf, L, tid, T);
     return;
   }
-  const float inv2nv = 1.0f / (2.0f * nv);
-  llr_axis(y.x, scale, bps >> 1, inv2nv, out);
-  llr_axis(y.y, scale, bps >> 1, inv2nv, out + (bps >> 1));
+  const int p0 = off >> 1, p1 = (off + N - 1) >> 1;
+  for (int p = p0 + tid; p <= p1; p += T) {
+    const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
+    const int n0 = 2 * p;
+    if (n0 >= off) {
+      const float2 z = box_muller(r.x, r.y), v = yf[n0];
+      buf[n0 - off] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+    }
+    if (n0 + 1 < off + N) {
+      const float2 z = box_muller(r.z, r.w), v = yf[n0 + 1];
+      buf[n0 + 1 - off] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -423,7 +498,9 @@ __device__ __forceinline__ void soft_demap(float2 y, float nv, int bps, float sc
 //  UNCODED: ZF Y/(H+1e-6) (lte_receiver.py:154-180) -> hard bits -> bit errors
 //  CODED:   ZF -> sigma2_eff (ofdm_core.py:1224-1243) -> LLRs (RE order)
 //  SIMO:    MRC sum conj(H_i)Y_i / (sum|H_i|^2 + 1e-10) (ofdm_core.py:1405-1534)
-__global__ __launch_bounds__(WG) void k_rx_data(Grid g, int chain, int rayleigh, int B, int num_rx,
+// Templated on chain and bits/symbol so every per-RE array stays in VGPRs.
+template <int CHAIN, int BPS>
+__global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int num_rx,
                                                 const float2* __restrict__ y, int64_t y_rx_stride,
                                                 int64_t y_frame_stride, const float2* __restrict__ H,
                                                 const float* __restrict__ npow, const float* __restrict__ snr_lin,
@@ -435,23 +512,25 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int chain, int rayleigh,
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
-  const int64_t gs = (int64_t)blockIdx.x * spw + slot;
-  const int b = (int)(gs / g.n_sym), l = (int)(gs % g.n_sym);
+  const int gs = blockIdx.x * spw + slot;
+  const int b = gs / g.n_sym, l = gs - b * g.n_sym;
   const bool active = slot < spw && b < B;
   float2* buf = sm + slot * N;
   const int grp = l / 14;
   const float sc = rsqrtf((float)N);
+  constexpr float QS = (float)qam_norm<BPS>();
   constexpr int QM = 4;  // data REs per thread (Nd < N/2 for every LTE profile)
+  constexpr int NRX = CHAIN == LTE_CHAIN_SIMO ? 8 : 1;
   float2 num[QM];
   float den[QM];
 #pragma unroll
   for (int q = 0; q < QM; ++q) { num[q] = make_float2(0.f, 0.f); den[q] = 0.f; }
-  for (int rx = 0; rx < num_rx; ++rx) {
+  for (int rx = 0; rx < (NRX == 1 ? 1 : num_rx); ++rx) {
     if (active) {
       const float sigma = sqrtf(npow[(size_t)b * num_rx + rx] * 0.5f);
       const float* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-      load_symbol_noisy(buf, y + b * y_frame_stride + rx * y_rx_stride, N, g.cp, l, sigma, seed, fid[b], rx, zf,
-                        g.L, tid, T);
+      load_symbol_noisy2(buf, y + b * y_frame_stride + rx * y_rx_stride, N, g.cp, l, sigma, seed, fid[b], rx, zf,
+                         g.L, tid, T);
     }
     __syncthreads();
     fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
@@ -463,52 +542,83 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int chain, int rayleigh,
         if (j < g.Nd) {
           const int k = g.data_idx[j];
           const float2 Y = cscale(buf[k], sc), h = Hf[k];
-          if (chain == LTE_CHAIN_SIMO) {
+          if constexpr (CHAIN == LTE_CHAIN_SIMO) {
             num[q] = cadd(num[q], cmulc(Y, h));
             den[q] += h.x * h.x + h.y * h.y;
           } else {
-            num[q] = cdiv(Y, make_float2(h.x + 1e-6f, h.y));
+            num[q] = zf_div(Y, make_float2(h.x + 1e-6f, h.y));
             den[q] = h.x * h.x + h.y * h.y;
           }
         }
       }
     }
-    __syncthreads();
+    if constexpr (NRX > 1) __syncthreads();
   }
   if (!active) return;
-  const float* const unused = nullptr;
-  (void)unused;
   uint32_t errs = 0;
   const uint32_t* fb = pw + (size_t)b * PW;
+  const size_t fre = (size_t)b * g.n_sym * g.Nd;
 #pragma unroll
   for (int q = 0; q < QM; ++q) {
     const int j = tid + q * T;
     if (j >= g.Nd) continue;
-    const int64_t re = (int64_t)l * g.Nd + j;
+    const int re = l * g.Nd + j;
     float2 z = num[q];
-    if (chain == LTE_CHAIN_SIMO) z = make_float2(z.x / (den[q] + 1e-10f), z.y / (den[q] + 1e-10f));
-    if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + re] = z;
-    if (chain == LTE_CHAIN_CODED) {
+    if constexpr (CHAIN == LTE_CHAIN_SIMO) {
+      const float r = 1.0f / (den[q] + 1e-10f);
+      z = make_float2(z.x * r, z.y * r);
+    }
+    if (cap_syms) cap_syms[fre + re] = z;
+    if constexpr (CHAIN == LTE_CHAIN_CODED) {
       const float s2 = 1.0f / snr_lin[b];
       float nv = s2;
       if (rayleigh) nv = fmaxf(s2 / fminf(fmaxf(den[q], 1e-6f), 1e6f), s2 * 0.25f);
-      float o[6];
-      soft_demap(z, nv, g.bps, g.qscale, o);
-      float* lo = llr + ((size_t)b * g.n_sym * g.Nd + re) * g.bps;
-      for (int m = 0; m < g.bps; ++m) lo[m] = o[m];
+      float o[BPS];
+      soft_demap<BPS>(z, nv, o);
+      float* lo = llr + (fre + re) * BPS;
+      if constexpr (BPS == 4) {
+        *reinterpret_cast<float4*>(lo) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int m = 0; m < BPS; m += 2) *reinterpret_cast<float2*>(lo + m) = make_float2(o[m], o[m + 1]);
+      }
     } else {
-      const int idx = hard_index(z, g.bps, g.qscale);
-      for (int m = 0; m < g.bps; ++m) {
-        const int64_t pbit = re * g.bps + m;
+      const int idx = hard_index(z, BPS, QS);
+      const int64_t pb0 = (int64_t)re * BPS;
+#pragma unroll
+      for (int m = 0; m < BPS; ++m) {
+        const int64_t pbit = pb0 + m;
         if (pbit < n_bits) {
-          const uint32_t bit = (idx >> (g.bps - 1 - m)) & 1;
+          const uint32_t bit = (idx >> (BPS - 1 - m)) & 1;
           errs += bit ^ getbit(fb, pbit);
           if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
         }
       }
     }
   }
-  if (chain != LTE_CHAIN_CODED && errs) atomicAdd(frame_err + b, errs);
+  if (CHAIN != LTE_CHAIN_CODED && errs) atomicAdd(frame_err + b, errs);
+}
+
+template <int CHAIN, int BPS>
+static void rx_data_inst(hipStream_t s, int blocks, size_t shm, const Grid& g, int rayleigh, int B, int num_rx,
+                         const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
+                         const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
+                         const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
+                         uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits) {
+  hipLaunchKernelGGL((k_rx_data<CHAIN, BPS>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, num_rx, y, y_rx_stride,
+                     y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
+                     cap_syms, cap_bits);
+}
+
+template <int CHAIN>
+static void rx_data_bps(int bps, hipStream_t s, int blocks, size_t shm, const Grid& g, int rayleigh, int B,
+                        int num_rx, const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
+                        const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
+                        const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
+                        uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits) {
+  auto* f = bps == 2 ? &rx_data_inst<CHAIN, 2> : (bps == 4 ? &rx_data_inst<CHAIN, 4> : &rx_data_inst<CHAIN, 6>);
+  f(s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z,
+    inj_stride, pw, PW, n_bits, frame_err, llr, cap_syms, cap_bits);
 }
 
 int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, int num_rx, const float2* y,
@@ -516,12 +626,25 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                    const float* snr_lin, const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride,
                    const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, float* llr, float2* cap_syms,
                    uint8_t* cap_bits) {
+  if (g.bps != 2 && g.bps != 4 && g.bps != 6) return (int)hipErrorInvalidValue;
+  if (chain == LTE_CHAIN_SIMO && num_rx > 8) return (int)hipErrorInvalidValue;
   const int spw = WG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym;
+  if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
-  hipLaunchKernelGGL(k_rx_data, dim3(blocks), dim3(WG), spw * g.N * sizeof(float2), s, g, chain, rayleigh, B,
-                     num_rx, y, y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW,
-                     n_bits, frame_err, llr, cap_syms, cap_bits);
+  const size_t shm = spw * g.N * sizeof(float2);
+  if (chain == LTE_CHAIN_CODED)
+    rx_data_bps<LTE_CHAIN_CODED>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H,
+                                 npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
+                                 cap_syms, cap_bits);
+  else if (chain == LTE_CHAIN_SIMO)
+    rx_data_bps<LTE_CHAIN_SIMO>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H,
+                                npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
+                                cap_syms, cap_bits);
+  else
+    rx_data_bps<LTE_CHAIN_UNCODED>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride,
+                                   H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
+                                   cap_syms, cap_bits);
   return (int)hipGetLastError();
 }
 
@@ -575,33 +698,41 @@ int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const f
   return (int)hipGetLastError();
 }
 
-__device__ __forceinline__ float qam_scale(int bps) {
-  return bps == 2 ? 1.41421356237309515f : (bps == 4 ? 3.16227766016837952f : 6.48074069840786023f);
-}
-
-__global__ void k_llr(int bps, int64_t n, const float2* __restrict__ syms, const float* __restrict__ nv,
+template <int BPS>
+__global__ void k_llr(int64_t n, const float2* __restrict__ syms, const float* __restrict__ nv,
                       float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float o[6];
-  soft_demap(syms[i], nv[i], bps, qam_scale(bps), o);
-  for (int m = 0; m < bps; ++m) out[i * bps + m] = o[m];
+  float o[BPS];
+  soft_demap<BPS>(syms[i], nv[i], o);
+#pragma unroll
+  for (int m = 0; m < BPS; ++m) out[i * BPS + m] = o[m];
 }
 
 int launch_llr(hipStream_t s, int bps, int64_t n, const float2* syms, const float* nv, float* llr) {
-  hipLaunchKernelGGL(k_llr, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, bps, n, syms, nv, llr);
+  const dim3 grid((unsigned)((n + WG - 1) / WG));
+  if (bps == 2) hipLaunchKernelGGL(k_llr<2>, grid, dim3(WG), 0, s, n, syms, nv, llr);
+  else if (bps == 4) hipLaunchKernelGGL(k_llr<4>, grid, dim3(WG), 0, s, n, syms, nv, llr);
+  else if (bps == 6) hipLaunchKernelGGL(k_llr<6>, grid, dim3(WG), 0, s, n, syms, nv, llr);
+  else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 
-__global__ void k_hard(int bps, int64_t n, const float2* __restrict__ syms, uint8_t* __restrict__ bits) {
+template <int BPS>
+__global__ void k_hard(int64_t n, const float2* __restrict__ syms, uint8_t* __restrict__ bits) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int idx = hard_index(syms[i], bps, qam_scale(bps));
-  for (int m = 0; m < bps; ++m) bits[i * bps + m] = (idx >> (bps - 1 - m)) & 1;
+  const int idx = hard_index(syms[i], BPS, (float)qam_norm<BPS>());
+#pragma unroll
+  for (int m = 0; m < BPS; ++m) bits[i * BPS + m] = (idx >> (BPS - 1 - m)) & 1;
 }
 
 int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* bits) {
-  hipLaunchKernelGGL(k_hard, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, bps, n, syms, bits);
+  const dim3 grid((unsigned)((n + WG - 1) / WG));
+  if (bps == 2) hipLaunchKernelGGL(k_hard<2>, grid, dim3(WG), 0, s, n, syms, bits);
+  else if (bps == 4) hipLaunchKernelGGL(k_hard<4>, grid, dim3(WG), 0, s, n, syms, bits);
+  else if (bps == 6) hipLaunchKernelGGL(k_hard<6>, grid, dim3(WG), 0, s, n, syms, bits);
+  else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

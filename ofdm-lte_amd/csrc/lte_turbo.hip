@@ -10,8 +10,9 @@
 //    pi(k) is wave-uniform (computed incrementally on the scalar unit) so the
 //    interleaved accesses of decoder 2 are coalesced rows too.
 //  * full-length recursion exactly as the reference (no sliding-window
-//    approximation): the forward pass stores alpha checkpoints every 8 steps,
-//    the backward pass recomputes each 8-step window from its checkpoint.
+//    approximation): the forward pass stores alpha checkpoints every TW steps
+//    (states 1..7; state 0 is 0 after normalisation), the backward pass
+//    recomputes each TW-step window from its checkpoint.
 //  * metrics are normalised to state 0 every step (max-log is shift
 //    invariant, so decisions equal the unnormalised float64 reference up to
 //    rounding).
@@ -129,6 +130,7 @@ struct RowPtr {
 // All pointers are wave-uniform (scalar) bases; `lane` is the only per-lane
 // offset, so every access is a global load/store with an SGPR base + one
 // shared VGPR offset (no per-load 64-bit vector addresses).
+#if LTE_TURBO_PLAIN
 template <int MODE>
 __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck,
                                           uint32_t* __restrict__ wbout, int lane, int K, int f1, int f2,
@@ -139,7 +141,7 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   const RowPtr<float> LP{rb, ((MODE == TM_DEC2) ? 2 : 1) * (K + 3), vo};
   const RowPtr<float> LS2T{rb, 3 * K + 9, vo};
   const RowPtr<float> LE{rb, 3 * K + 12, vo};
-  const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * 8 * RS * 4)), 0, vo};
+  const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * TURBO_CK_ROWS * RS * 4)), 0, vo};
   const RowPtr<uint32_t> bout{make_rsrc(wbout, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
   const int nfull = K / TW;
   const int tf2 = (2 * f2) % K;
@@ -154,7 +156,7 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
 #pragma unroll 1
   for (int w = 0; w < nfull; ++w) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) ck.st(w * 8 + s, a[s]);
+    for (int s = 1; s < 8; ++s) ck.st(w * TURBO_CK_ROWS + s - 1, a[s]);
     float ls[TW], lp[TW], la[TW];
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
@@ -200,8 +202,9 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
 #pragma unroll 1
   for (int w = nfull - 1; w >= 0; --w) {
     float A[TW][8];
+    A[0][0] = 0.0f;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) A[0][s] = ck.ld(w * 8 + s);
+    for (int s = 1; s < 8; ++s) A[0][s] = ck.ld(w * TURBO_CK_ROWS + s - 1);
     float ls[TW], lp[TW], la[TW];
     int pl[TW];
     int pp = pi, dd = d;
@@ -250,6 +253,157 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   }
 }
 
+#else
+// Inputs of one TW-step window (and, backward, its alpha checkpoint and the
+// interleaved positions), double-buffered in registers so the loads of the
+// next window are in flight while the current one is computed.
+struct Win {
+  float ls[TW], lp[TW], la[TW];
+  int pl[TW];
+  float ck[7];
+};
+
+template <int MODE>
+__device__ __forceinline__ void load_win(Win& W, int w, int pi, int d, int K, int tf2, bool use_la, bool with_ck,
+                                         const RowPtr<float>& LS, const RowPtr<float>& LP, const RowPtr<float>& LE,
+                                         const RowPtr<float>& ck) {
+#pragma unroll
+  for (int j = 0; j < TW; ++j) {
+    const int k = w * TW + j;
+    const int p = (MODE == TM_DEC2) ? pi : k;
+    W.pl[j] = p;
+    W.ls[j] = LS.ld(p);
+    W.lp[j] = LP.ld(k);
+    W.la[j] = use_la ? LE.ld(p) : 0.0f;
+    if (MODE == TM_DEC2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
+  }
+  if (with_ck) {
+#pragma unroll
+    for (int s = 1; s < 8; ++s) W.ck[s - 1] = ck.ld(w * TURBO_CK_ROWS + s - 1);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck,
+                                          uint32_t* __restrict__ wbout, int lane, int K, int f1, int f2,
+                                          bool first) {
+  const int vo = lane * 4;
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * 4));
+  const RowPtr<float> LS{rb, 0, vo};
+  const RowPtr<float> LP{rb, ((MODE == TM_DEC2) ? 2 : 1) * (K + 3), vo};
+  const RowPtr<float> LS2T{rb, 3 * K + 9, vo};
+  const RowPtr<float> LE{rb, 3 * K + 12, vo};
+  const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * TURBO_CK_ROWS * RS * 4)), 0, vo};
+  const RowPtr<uint32_t> bout{make_rsrc(wbout, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
+  const int nfull = K / TW;
+  const int tf2 = (2 * f2) % K;
+  const bool use_la = !first;
+
+  // ---------------- forward pass: alpha, checkpoint every TW steps
+  float a[8];
+  a[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; ++s) a[s] = LTE_NEG_BIG;
+  int pi = 0, d = (f1 + f2) % K;   // pi state at the start of the next window to load
+  Win cur, nxt;
+  load_win<MODE>(cur, 0, pi, d, K, tf2, use_la, false, LS, LP, LE, ck);
+  if (MODE == TM_DEC2) {
+#pragma unroll
+    for (int j = 0; j < TW; ++j) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
+  }
+#pragma unroll 1
+  for (int w = 0; w < nfull; ++w) {
+    if (w + 1 < nfull) {
+      load_win<MODE>(nxt, w + 1, pi, d, K, tf2, use_la, false, LS, LP, LE, ck);
+      if (MODE == TM_DEC2) {
+#pragma unroll
+        for (int j = 0; j < TW; ++j) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
+      }
+    }
+#pragma unroll
+    for (int s = 1; s < 8; ++s) ck.st(w * TURBO_CK_ROWS + s - 1, a[s]);
+#pragma unroll
+    for (int j = 0; j < TW; ++j) {
+      float c[4], o[8];
+      gam(cur.ls[j], cur.lp[j], cur.la[j], c);
+      fwd(a, c, o);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) a[s] = o[s];
+    }
+    cur = nxt;
+  }
+  // pi/d now sit at k = K (DEC2)
+
+  // ---------------- backward pass
+  float b[8];
+  b[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; ++s) b[s] = LTE_NEG_BIG;
+  // trellis-termination steps k = K+2, K+1, K (only beta is needed there)
+#pragma unroll
+  for (int j = 2; j >= 0; --j) {
+    const int k = K + j;
+    const float ls = (MODE == TM_DEC2) ? LS2T.ld(j) : LS.ld(k);
+    const float lp = LP.ld(k);
+    float c[4], t0[8], t1[8];
+    gam(ls, lp, 0.0f, c);
+    bterms(b, c, t0, t1);
+    bnext(t0, t1, b);
+  }
+  // step back to the start of the last full window
+  if (MODE == TM_DEC2) {
+#pragma unroll
+    for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+  }
+  load_win<MODE>(cur, nfull - 1, pi, d, K, tf2, use_la, true, LS, LP, LE, ck);
+  uint32_t acc = 0;
+#pragma unroll 1
+  for (int w = nfull - 1; w >= 0; --w) {
+    if (w > 0) {
+      if (MODE == TM_DEC2) {
+#pragma unroll
+        for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+      }
+      load_win<MODE>(nxt, w - 1, pi, d, K, tf2, use_la, true, LS, LP, LE, ck);
+    }
+    float A[TW][8];
+    A[0][0] = 0.0f;
+#pragma unroll
+    for (int s = 1; s < 8; ++s) A[0][s] = cur.ck[s - 1];
+#pragma unroll
+    for (int j = 0; j < TW - 1; ++j) {
+      float c[4];
+      gam(cur.ls[j], cur.lp[j], cur.la[j], c);
+      fwd(A[j], c, A[j + 1]);
+    }
+#pragma unroll
+    for (int j = TW - 1; j >= 0; --j) {
+      const int k = w * TW + j;
+      float c[4], t0[8], t1[8];
+      gam(cur.ls[j], cur.lp[j], cur.la[j], c);
+      bterms(b, c, t0, t1);
+      const float L = llr_app(A[j], t0, t1);
+      if (MODE == TM_DEC1) {
+        LE.st(k, (L - cur.la[j]) - cur.ls[j]);
+      } else if (MODE == TM_DEC2) {
+        LE.st(cur.pl[j], (L - cur.la[j]) - cur.ls[j]);
+      } else if (MODE == TM_APP) {
+        LE.st(k, L);
+      } else {  // TM_FINAL: hard decision (L < 0) packed MSB-first
+        acc |= (L < 0.0f ? 1u : 0u) << (31 - (k & 31));
+        if ((k & 31) == 0) {
+          bout.st(k >> 5, acc);
+          acc = 0;
+        }
+      }
+      bnext(t0, t1, b);
+    }
+    cur = nxt;
+  }
+}
+
+#endif
+
 // One launch decodes every code-block slot of the batch: wave w -> job r
 // (CB slot, i.e. one K) and frame group g.  256-thread blocks = 4 independent
 // waves (no LDS, no barriers).
@@ -263,7 +417,7 @@ __global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mo
   const int g = wg - jobs.prefix[r];
   const int K = jb.K;
   float* base = jb.blk + (size_t)g * turbo_rows(K) * RS;
-  float* ck = jb.ck + (size_t)g * (turbo_nwin(K) * 8) * RS;
+  float* ck = jb.ck + (size_t)g * (turbo_nwin(K) * TURBO_CK_ROWS) * RS;
   uint32_t* bo = jb.bits + (size_t)g * turbo_kw(K) * RS;
   if (mode == TM_APP) {
     half_pass<TM_APP>(base, ck, bo, lane, K, jb.f1, jb.f2, false);
@@ -307,24 +461,39 @@ int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, 
 // of a frame in RE order, the destination (r<<24 | row) or -1.  A block loads
 // a [64 frames][256 t] tile (coalesced rows), then every wave writes whole
 // 256-B decoder rows.
-constexpr int DM_CH = 256;
+constexpr int DM_CH = 64;
 __global__ __launch_bounds__(256) void k_dematch(const float* __restrict__ llr, int T, int B,
                                                  const int32_t* __restrict__ rx_map,
                                                  float* const* __restrict__ blk, const int64_t* __restrict__ rows) {
-  __shared__ float tile[64][DM_CH + 1];
+  __shared__ float tile[64][DM_CH + 1];   // [frame][t], +1: conflict-free column reads
   const int g = blockIdx.y;
   const int t0 = blockIdx.x * DM_CH;
-  for (int idx = threadIdx.x; idx < 64 * DM_CH; idx += 256) {
-    const int f = idx / DM_CH, c = idx % DM_CH;
-    const int b = g * 64 + f, t = t0 + c;
-    tile[f][c] = (b < B && t < T) ? llr[(size_t)b * T + t] : 0.0f;
+  const int nt = min(DM_CH, T - t0);
+  // load: 16 lanes x float4 per frame row (256-B coalesced); scalar tail
+  const int c4 = (threadIdx.x & 15) * 4;
+  for (int f = threadIdx.x >> 4; f < 64; f += 16) {
+    const int b = g * 64 + f;
+    const float* src = llr + (size_t)b * T + t0;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (b < B) {
+      if ((T & 3) == 0 && c4 + 3 < nt) v = *reinterpret_cast<const float4*>(src + c4);
+      else {
+        if (c4 + 0 < nt) v.x = src[c4 + 0];
+        if (c4 + 1 < nt) v.y = src[c4 + 1];
+        if (c4 + 2 < nt) v.z = src[c4 + 2];
+        if (c4 + 3 < nt) v.w = src[c4 + 3];
+      }
+    }
+    tile[f][c4 + 0] = v.x;
+    tile[f][c4 + 1] = v.y;
+    tile[f][c4 + 2] = v.z;
+    tile[f][c4 + 3] = v.w;
   }
   __syncthreads();
-  const int wv = threadIdx.x >> 6, f = threadIdx.x & 63;
-  for (int c = wv; c < DM_CH; c += 4) {
-    const int t = t0 + c;
-    if (t >= T) break;
-    const int m = rx_map[t];
+  // store: each wave writes whole 256-B decoder rows (64 frames of one LLR)
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), f = threadIdx.x & 63;
+  for (int c = wv; c < nt; c += 4) {
+    const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
     blk[r][((size_t)g * rows[r] + row) * RS + f] = tile[f][c];
@@ -335,6 +504,7 @@ int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t*
                    const int64_t* rows, int C) {
   (void)C;
   const int G = (B + 63) / 64;
+  if (G > 65535) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_dematch, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B, rx_map, blk, rows);
   return (int)hipGetLastError();
 }
@@ -342,83 +512,139 @@ int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t*
 // ---------------------------------------------------------------------------
 // TX: CB construction (segmentation.py:212-247 + CRC-24B crc.py:162-184) and
 // turbo encoding (turbo_encoder.py:137-313).  One lane = one (CB slot, frame).
-struct BitWriter {
+struct BitWriter {   // MSB-first stream writer; one store per completed word
   uint32_t* p;
-  uint32_t acc;
+  uint64_t acc;
   int n;
-  __device__ void put(uint32_t bit) {
-    acc = (acc << 1) | bit;
-    if (++n == 32) { *p++ = acc; acc = 0; n = 0; }
+  __device__ __forceinline__ void put(uint32_t bits, int nb) {   // nb in [1, 32]
+    acc = (acc << nb) | (nb == 32 ? (uint64_t)bits : (uint64_t)(bits & ((1u << nb) - 1u)));
+    n += nb;
+    if (n >= 32) {
+      *p++ = (uint32_t)(acc >> (n - 32));
+      n -= 32;
+    }
   }
-  __device__ void flush() {
-    if (n) { *p = acc << (32 - n); }
+  __device__ __forceinline__ void flush() {
+    if (n) *p = (uint32_t)(acc << (32 - n));
   }
 };
 
-__global__ __launch_bounds__(256) void k_encode(const uint32_t* __restrict__ pw, int PW, uint32_t* __restrict__ cbw,
-                                                int KWmax, uint32_t* __restrict__ enc, int EW,
-                                                const CbInfo* __restrict__ cbi, int C, int B) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= C * B) return;
+// nb (<= 32) bits of the RSC code (turbo_encoder.py:137-211) on u (MSB-first):
+// returns feedback ("systematic", Q13) bits in *fbw and parity bits.
+__device__ __forceinline__ uint32_t rsc_bits(uint32_t u, int nb, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                             uint32_t* fbw) {
+  uint32_t f = 0, q = 0;
+  for (int i = 0; i < nb; ++i) {
+    const uint32_t bit = (u >> (nb - 1 - i)) & 1u;
+    const uint32_t fb = bit ^ s1 ^ s2;
+    f = (f << 1) | fb;
+    q = (q << 1) | (fb ^ s0 ^ s2);
+    s2 = s1; s1 = s0; s0 = fb;
+  }
+  *fbw = f;
+  return q;
+}
+
+// Bit-serial recursion in registers, memory traffic in 32-bit words: TB words
+// through a 64-bit window, one store per completed output word.  The code
+// block itself stays in LDS as [word][lane] for encoder 2's QPP gathers: pi(i)
+// is wave-uniform (all lanes share K), so every gather is one conflict-free
+// 64-lane LDS read instead of a scattered global load.
+constexpr int ENC_WG = 64;
+__global__ __launch_bounds__(ENC_WG) void k_encode(const uint32_t* __restrict__ pw, int PW, int KWmax,
+                                                   uint32_t* __restrict__ enc, int EW,
+                                                   const CbInfo* __restrict__ cbi, int C, int B) {
+  extern __shared__ uint32_t cwl[];   // [KWmax][64]
+  const int gid = blockIdx.x * ENC_WG + threadIdx.x;
+  if (gid >= C * B) return;           // no barriers below: early exit is safe
   const int r = gid / B, b = gid % B;
   const CbInfo ci = cbi[r];
   const int K = ci.K;
   const uint32_t* tb = pw + (size_t)b * PW;
-  uint32_t* cw = cbw + ((size_t)b * C + r) * KWmax;
+  uint32_t* cw = cwl + threadIdx.x;   // word w of this lane's block at cw[w * 64]
+  (void)KWmax;
   uint32_t* e = enc + ((size_t)b * C + r) * 3 * EW;
-  BitWriter w0{e, 0, 0}, w1{e + EW, 0, 0}, w2{e + 2 * EW, 0, 0}, wc{cw, 0, 0};
+  BitWriter w0{e, 0, 0}, w1{e + EW, 0, 0}, w2{e + 2 * EW, 0, 0};
   const int Kd = ci.crc ? K - 24 : K;
   uint32_t crc = 0, s0 = 0, s1 = 0, s2 = 0;
-  for (int p = 0; p < K; ++p) {
-    uint32_t bit;
-    if (p < ci.F) bit = 0;
-    else if (p < ci.F + ci.info) bit = getbit(tb, (int64_t)ci.off + p - ci.F);
-    else bit = (crc >> (23 - (p - Kd))) & 1u;
-    if (ci.crc && p < Kd) {
-      const uint32_t msb = (crc >> 23) & 1u;
-      crc = (crc << 1) & 0xFFFFFFu;
-      if (msb ^ bit) crc ^= 0x800063u;  // CRC-24B (0x1800063)
+  // TB bit (ci.off - ci.F + p) for CB bit p in [F, F+info)
+  const int64_t base = (int64_t)ci.off - ci.F;
+  for (int w = 0; w * 32 < K; ++w) {
+    const int p0 = w * 32, nb = min(32, K - p0);
+    // 32 TB bits starting at base + p0 (window of two words; bits outside [F, Kd) are masked below)
+    uint32_t t = 0;
+    {
+      const int64_t q = base + p0;
+      if (q + 32 > 0 && q < (int64_t)PW * 32) {
+        const int64_t i0 = q >> 5;   // arithmetic shift: floor for negative q
+        const int o = (int)(q & 31);
+        const uint32_t a = (i0 >= 0 && i0 < PW) ? tb[i0] : 0u;
+        const uint32_t c = (i0 + 1 >= 0 && i0 + 1 < PW) ? tb[i0 + 1] : 0u;
+        t = o ? ((a << o) | (c >> (32 - o))) : a;
+      }
     }
-    wc.put(bit);
-    const uint32_t fb = bit ^ s1 ^ s2;
-    w0.put(fb);                 // "systematic" = feedback bit (Q13)
-    w1.put(fb ^ s0 ^ s2);
-    s2 = s1; s1 = s0; s0 = fb;
+    uint32_t u = 0;
+    for (int i = 0; i < nb; ++i) {
+      const int p = p0 + i;
+      uint32_t bit;
+      if (p < ci.F) bit = 0;
+      else if (p < Kd) bit = (t >> (31 - i)) & 1u;
+      else bit = (crc >> (23 - (p - Kd))) & 1u;
+      if (ci.crc && p < Kd) {
+        const uint32_t msb = (crc >> 23) & 1u;
+        crc = (crc << 1) & 0xFFFFFFu;
+        if (msb ^ bit) crc ^= 0x800063u;  // CRC-24B (0x1800063), crc.py:162-184
+      }
+      u = (u << 1) | bit;
+    }
+    cw[w * ENC_WG] = nb == 32 ? u : (u << (32 - nb));
+    uint32_t f;
+    const uint32_t q = rsc_bits(u, nb, s0, s1, s2, &f);
+    w0.put(f, nb);
+    w1.put(q, nb);
   }
-  wc.flush();
   for (int t = 0; t < 3; ++t) {  // trellis termination, encoder 1
     const uint32_t tail = s1 ^ s2, fb = tail ^ s1 ^ s2;
-    w0.put(fb);
-    w1.put(fb ^ s0 ^ s2);
+    w0.put(fb, 1);
+    w1.put(fb ^ s0 ^ s2, 1);
     s2 = s1; s1 = s0; s0 = fb;
   }
   w1.flush();
-  // encoder 2 on the QPP-interleaved block
+  // encoder 2 on the QPP-interleaved block (turbo_encoder.py:213-313)
   s0 = s1 = s2 = 0;
   int pi = 0, d = (ci.f1 + ci.f2) % K;
   const int tf2 = (2 * ci.f2) % K;
-  for (int i = 0; i < K; ++i) {
-    const uint32_t bit = getbit(cw, pi);
-    const uint32_t fb = bit ^ s1 ^ s2;
-    w2.put(fb ^ s0 ^ s2);
-    s2 = s1; s1 = s0; s0 = fb;
-    pi += d; if (pi >= K) pi -= K;
-    d += tf2; if (d >= K) d -= K;
+  for (int w = 0; w * 32 < K; ++w) {
+    const int nb = min(32, K - w * 32);
+    uint32_t u = 0;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) {
+      if (i < nb) {
+        u |= ((cw[(pi >> 5) * ENC_WG] >> (31 - (pi & 31))) & 1u) << (nb - 1 - i);
+        pi += d; if (pi >= K) pi -= K;
+        d += tf2; if (d >= K) d -= K;
+      }
+    }
+    uint32_t f;
+    w2.put(rsc_bits(u, nb, s0, s1, s2, &f), nb);
   }
   for (int t = 0; t < 3; ++t) {
     const uint32_t tail = s1 ^ s2, fb = tail ^ s1 ^ s2;
-    w0.put(fb);                 // sys2 tail -> d0[K+3..K+5]
-    w2.put(fb ^ s0 ^ s2);
+    w0.put(fb, 1);               // sys2 tail -> d0[K+3..K+5]
+    w2.put(fb ^ s0 ^ s2, 1);
     s2 = s1; s1 = s0; s0 = fb;
   }
   w0.flush();
   w2.flush();
 }
 
-int launch_encode(hipStream_t s, const uint32_t* pw, int PW, uint32_t* cbw, int KWmax, uint32_t* enc, int EW,
+int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
                   const CbInfo* cbi_dev, int C, int B) {
-  const int n = C * B;
-  hipLaunchKernelGGL(k_encode, dim3((n + 255) / 256), dim3(256), 0, s, pw, PW, cbw, KWmax, enc, EW, cbi_dev, C, B);
+  const int64_t n = (int64_t)C * B;
+  const size_t shm = (size_t)KWmax * ENC_WG * sizeof(uint32_t);
+  if (n > 0x7FFFFFFF || shm > 65536) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + ENC_WG - 1) / ENC_WG)), dim3(ENC_WG), shm, s, pw, PW, KWmax, enc,
+                     EW, cbi_dev, C, B);
   return (int)hipGetLastError();
 }
 

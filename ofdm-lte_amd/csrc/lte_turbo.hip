@@ -87,14 +87,38 @@ __device__ __forceinline__ float llr_app(const float a[8], const float t0[8], co
   return m0 - m1;
 }
 
+// bterms + llr_app + bnext streamed over the states (same operations in the
+// same order, so bit-identical): returns the a-posteriori LLR of this step and
+// advances beta in place, without holding both branch-term vectors.
+__device__ __forceinline__ float bstep(float b[8], const float c[4], const float a[8]) {
+  float bn[8], m0 = 0.0f, m1 = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int s0 = s >> 2, s1 = (s >> 1) & 1, s2 = s & 1;
+    const int fb = s1 ^ s2, par = fb ^ s0 ^ s2, ns = 4 * fb + 2 * s0 + s1;
+    const float g = gsel(c, fb, par, 0);
+    const float t0 = b[ns] + g, t1 = b[ns ^ 4] - g;
+    if (s == 0) {
+      m0 = a[0] + t0;
+      m1 = a[0] + t1;
+    } else {
+      m0 = fmaxf(m0, a[s] + t0);
+      m1 = fmaxf(m1, a[s] + t1);
+    }
+    bn[s] = fmaxf(t0, t1);
+  }
+  const float n0 = bn[0];
+  b[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; ++s) b[s] = bn[s] - n0;
+  return m0 - m1;
+}
+
 __device__ __forceinline__ int modadd(int a, int b, int K) { a += b; return a >= K ? a - K : a; }
 __device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 0 ? a + K : a; }
 
 constexpr int RS = 64;  // row stride (floats): 64 lanes
-#ifndef LTE_TURBO_W
-#define LTE_TURBO_W 4
-#endif
-constexpr int TW = LTE_TURBO_W;  // window (steps between alpha checkpoints)
+constexpr int TW = 8;  // steps between alpha checkpoints (recomputed in halves)
 
 // Buffer-resource row accessor: the 128-bit descriptor (SGPRs) covers one
 // wave's block; a row is addressed by a scalar byte offset (soffset) and the
@@ -130,11 +154,18 @@ struct RowPtr {
 // All pointers are wave-uniform (scalar) bases; `lane` is the only per-lane
 // offset, so every access is a global load/store with an SGPR base + one
 // shared VGPR offset (no per-load 64-bit vector addresses).
-#if LTE_TURBO_PLAIN
+// One half-iteration (one constituent decoder pass) for the code block of this lane.
+// Forward: alpha over the whole block, checkpoint (states 1..7) every TW = 8
+// steps.  Backward: per 8-step window, reload its inputs and checkpoint and
+// recompute the alphas in two halves of TH = 4 (first the upper half from
+// alpha(8w+4), then the lower half from the checkpoint), so only 4 alpha
+// vectors are ever live.  Recomputed alphas are bit-identical to the forward
+// pass (same operations, same order).  HBM bytes per step: 3 input loads x 2
+// passes + 1 extrinsic store + 7/8 checkpoint store + 7/8 checkpoint load.
 template <int MODE>
-__device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck,
-                                          uint32_t* __restrict__ wbout, int lane, int K, int f1, int f2,
-                                          bool first) {
+__device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck, int lane, int K,
+                                          int f1, int f2, bool first) {
+  constexpr int TH = TW / 2;
   const int vo = lane * 4;
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * 4));
   const RowPtr<float> LS{rb, 0, vo};
@@ -142,12 +173,11 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   const RowPtr<float> LS2T{rb, 3 * K + 9, vo};
   const RowPtr<float> LE{rb, 3 * K + 12, vo};
   const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * TURBO_CK_ROWS * RS * 4)), 0, vo};
-  const RowPtr<uint32_t> bout{make_rsrc(wbout, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
-  const int nfull = K / TW;
+  const int nfull = K / TW;   // every LTE K is a multiple of 8
   const int tf2 = (2 * f2) % K;
   const bool use_la = !first;
 
-  // ---------------- forward pass: alpha, checkpoint every 8 steps
+  // ---------------- forward pass
   float a[8];
   a[0] = 0.0f;
 #pragma unroll
@@ -193,18 +223,17 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
     bterms(b, c, t0, t1);
     bnext(t0, t1, b);
   }
-  // pi/d are now at k = K; step back to the start of the last full window
+  // pi/d are now at k = K; step back to the start of the last window
   if (MODE == TM_DEC2) {
 #pragma unroll
     for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
   }
-  uint32_t acc = 0;
 #pragma unroll 1
   for (int w = nfull - 1; w >= 0; --w) {
-    float A[TW][8];
-    A[0][0] = 0.0f;
+    float cka[8];
+    cka[0] = 0.0f;
 #pragma unroll
-    for (int s = 1; s < 8; ++s) A[0][s] = ck.ld(w * TURBO_CK_ROWS + s - 1);
+    for (int s = 1; s < 8; ++s) cka[s] = ck.ld(w * TURBO_CK_ROWS + s - 1);
     float ls[TW], lp[TW], la[TW];
     int pl[TW];
     int pp = pi, dd = d;
@@ -219,32 +248,57 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
       if (MODE == TM_DEC2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
     }
 #pragma unroll
-    for (int j = 0; j < TW - 1; ++j) {
-      float c[4];
-      gam(ls[j], lp[j], la[j], c);
-      fwd(A[j], c, A[j + 1]);
-    }
+    for (int h = 1; h >= 0; --h) {
+      if (h == 0) {
+        // the lower half's recompute repeats the chain the upper half ran from
+        // the checkpoint; hide that from CSE so it is recomputed (cheap VALU)
+        // instead of holding 3 alpha vectors live across the upper half
 #pragma unroll
-    for (int j = TW - 1; j >= 0; --j) {
-      const int k = w * TW + j;
-      float c[4], t0[8], t1[8];
-      gam(ls[j], lp[j], la[j], c);
-      bterms(b, c, t0, t1);
-      const float L = llr_app(A[j], t0, t1);
-      if (MODE == TM_DEC1) {
-        LE.st(k, (L - la[j]) - ls[j]);
-      } else if (MODE == TM_DEC2) {
-        LE.st(pl[j], (L - la[j]) - ls[j]);
-      } else if (MODE == TM_APP) {
-        LE.st(k, L);
-      } else {  // TM_FINAL: hard decision (L < 0) packed MSB-first
-        acc |= (L < 0.0f ? 1u : 0u) << (31 - (k & 31));
-        if ((k & 31) == 0) {
-          bout.st(k >> 5, acc);
-          acc = 0;
+        for (int s = 1; s < 8; ++s) asm volatile("" : "+v"(cka[s]));
+#pragma unroll
+        for (int j = 0; j < TH; ++j) asm volatile("" : "+v"(ls[j]), "+v"(lp[j]), "+v"(la[j]));
+      }
+      // A[j] = alpha before step w*TW + h*TH + j
+      float A[TH][8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) A[0][s] = cka[s];
+      if (h == 1) {
+#pragma unroll
+        for (int j = 0; j < TH; ++j) {
+          float c[4], o[8];
+          gam(ls[j], lp[j], la[j], c);
+          fwd(A[0], c, o);
+#pragma unroll
+          for (int s = 0; s < 8; ++s) A[0][s] = o[s];
         }
       }
-      bnext(t0, t1, b);
+#pragma unroll
+      for (int j = 0; j < TH - 1; ++j) {
+        const int jj = h * TH + j;
+        float c[4];
+        gam(ls[jj], lp[jj], la[jj], c);
+        fwd(A[j], c, A[j + 1]);
+      }
+      // gamma is 7 VALU ops: recompute it below rather than keep the
+      // recompute's 4 gamma vectors live next to the inputs
+#pragma unroll
+      for (int j = 0; j < TH; ++j)
+        asm volatile("" : "+v"(ls[h * TH + j]), "+v"(lp[h * TH + j]), "+v"(la[h * TH + j]));
+#pragma unroll
+      for (int j = TH - 1; j >= 0; --j) {
+        const int jj = h * TH + j;
+        const int k = w * TW + jj;
+        float c[4];
+        gam(ls[jj], lp[jj], la[jj], c);
+        const float L = bstep(b, c, A[j]);
+        if (MODE == TM_DEC1) {
+          LE.st(k, (L - la[jj]) - ls[jj]);
+        } else if (MODE == TM_DEC2) {
+          LE.st(pl[jj], (L - la[jj]) - ls[jj]);
+        } else {  // TM_APP: a-posteriori LLR in place of the extrinsic row
+          LE.st(k, L);
+        }
+      }
     }
     if (MODE == TM_DEC2) {
 #pragma unroll
@@ -252,157 +306,6 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
     }
   }
 }
-
-#else
-// Inputs of one TW-step window (and, backward, its alpha checkpoint and the
-// interleaved positions), double-buffered in registers so the loads of the
-// next window are in flight while the current one is computed.
-struct Win {
-  float ls[TW], lp[TW], la[TW];
-  int pl[TW];
-  float ck[7];
-};
-
-template <int MODE>
-__device__ __forceinline__ void load_win(Win& W, int w, int pi, int d, int K, int tf2, bool use_la, bool with_ck,
-                                         const RowPtr<float>& LS, const RowPtr<float>& LP, const RowPtr<float>& LE,
-                                         const RowPtr<float>& ck) {
-#pragma unroll
-  for (int j = 0; j < TW; ++j) {
-    const int k = w * TW + j;
-    const int p = (MODE == TM_DEC2) ? pi : k;
-    W.pl[j] = p;
-    W.ls[j] = LS.ld(p);
-    W.lp[j] = LP.ld(k);
-    W.la[j] = use_la ? LE.ld(p) : 0.0f;
-    if (MODE == TM_DEC2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
-  }
-  if (with_ck) {
-#pragma unroll
-    for (int s = 1; s < 8; ++s) W.ck[s - 1] = ck.ld(w * TURBO_CK_ROWS + s - 1);
-  }
-}
-
-template <int MODE>
-__device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck,
-                                          uint32_t* __restrict__ wbout, int lane, int K, int f1, int f2,
-                                          bool first) {
-  const int vo = lane * 4;
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * 4));
-  const RowPtr<float> LS{rb, 0, vo};
-  const RowPtr<float> LP{rb, ((MODE == TM_DEC2) ? 2 : 1) * (K + 3), vo};
-  const RowPtr<float> LS2T{rb, 3 * K + 9, vo};
-  const RowPtr<float> LE{rb, 3 * K + 12, vo};
-  const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * TURBO_CK_ROWS * RS * 4)), 0, vo};
-  const RowPtr<uint32_t> bout{make_rsrc(wbout, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
-  const int nfull = K / TW;
-  const int tf2 = (2 * f2) % K;
-  const bool use_la = !first;
-
-  // ---------------- forward pass: alpha, checkpoint every TW steps
-  float a[8];
-  a[0] = 0.0f;
-#pragma unroll
-  for (int s = 1; s < 8; ++s) a[s] = LTE_NEG_BIG;
-  int pi = 0, d = (f1 + f2) % K;   // pi state at the start of the next window to load
-  Win cur, nxt;
-  load_win<MODE>(cur, 0, pi, d, K, tf2, use_la, false, LS, LP, LE, ck);
-  if (MODE == TM_DEC2) {
-#pragma unroll
-    for (int j = 0; j < TW; ++j) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
-  }
-#pragma unroll 1
-  for (int w = 0; w < nfull; ++w) {
-    if (w + 1 < nfull) {
-      load_win<MODE>(nxt, w + 1, pi, d, K, tf2, use_la, false, LS, LP, LE, ck);
-      if (MODE == TM_DEC2) {
-#pragma unroll
-        for (int j = 0; j < TW; ++j) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
-      }
-    }
-#pragma unroll
-    for (int s = 1; s < 8; ++s) ck.st(w * TURBO_CK_ROWS + s - 1, a[s]);
-#pragma unroll
-    for (int j = 0; j < TW; ++j) {
-      float c[4], o[8];
-      gam(cur.ls[j], cur.lp[j], cur.la[j], c);
-      fwd(a, c, o);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) a[s] = o[s];
-    }
-    cur = nxt;
-  }
-  // pi/d now sit at k = K (DEC2)
-
-  // ---------------- backward pass
-  float b[8];
-  b[0] = 0.0f;
-#pragma unroll
-  for (int s = 1; s < 8; ++s) b[s] = LTE_NEG_BIG;
-  // trellis-termination steps k = K+2, K+1, K (only beta is needed there)
-#pragma unroll
-  for (int j = 2; j >= 0; --j) {
-    const int k = K + j;
-    const float ls = (MODE == TM_DEC2) ? LS2T.ld(j) : LS.ld(k);
-    const float lp = LP.ld(k);
-    float c[4], t0[8], t1[8];
-    gam(ls, lp, 0.0f, c);
-    bterms(b, c, t0, t1);
-    bnext(t0, t1, b);
-  }
-  // step back to the start of the last full window
-  if (MODE == TM_DEC2) {
-#pragma unroll
-    for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
-  }
-  load_win<MODE>(cur, nfull - 1, pi, d, K, tf2, use_la, true, LS, LP, LE, ck);
-  uint32_t acc = 0;
-#pragma unroll 1
-  for (int w = nfull - 1; w >= 0; --w) {
-    if (w > 0) {
-      if (MODE == TM_DEC2) {
-#pragma unroll
-        for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
-      }
-      load_win<MODE>(nxt, w - 1, pi, d, K, tf2, use_la, true, LS, LP, LE, ck);
-    }
-    float A[TW][8];
-    A[0][0] = 0.0f;
-#pragma unroll
-    for (int s = 1; s < 8; ++s) A[0][s] = cur.ck[s - 1];
-#pragma unroll
-    for (int j = 0; j < TW - 1; ++j) {
-      float c[4];
-      gam(cur.ls[j], cur.lp[j], cur.la[j], c);
-      fwd(A[j], c, A[j + 1]);
-    }
-#pragma unroll
-    for (int j = TW - 1; j >= 0; --j) {
-      const int k = w * TW + j;
-      float c[4], t0[8], t1[8];
-      gam(cur.ls[j], cur.lp[j], cur.la[j], c);
-      bterms(b, c, t0, t1);
-      const float L = llr_app(A[j], t0, t1);
-      if (MODE == TM_DEC1) {
-        LE.st(k, (L - cur.la[j]) - cur.ls[j]);
-      } else if (MODE == TM_DEC2) {
-        LE.st(cur.pl[j], (L - cur.la[j]) - cur.ls[j]);
-      } else if (MODE == TM_APP) {
-        LE.st(k, L);
-      } else {  // TM_FINAL: hard decision (L < 0) packed MSB-first
-        acc |= (L < 0.0f ? 1u : 0u) << (31 - (k & 31));
-        if ((k & 31) == 0) {
-          bout.st(k >> 5, acc);
-          acc = 0;
-        }
-      }
-      bnext(t0, t1, b);
-    }
-    cur = nxt;
-  }
-}
-
-#endif
 
 // One launch decodes every code-block slot of the batch: wave w -> job r
 // (CB slot, i.e. one K) and frame group g.  256-thread blocks = 4 independent
@@ -420,14 +323,30 @@ __global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mo
   float* ck = jb.ck + (size_t)g * (turbo_nwin(K) * TURBO_CK_ROWS) * RS;
   uint32_t* bo = jb.bits + (size_t)g * turbo_kw(K) * RS;
   if (mode == TM_APP) {
-    half_pass<TM_APP>(base, ck, bo, lane, K, jb.f1, jb.f2, false);
+    half_pass<TM_APP>(base, ck, lane, K, jb.f1, jb.f2, false);
     return;
   }
   for (int it = 0; it < iters; ++it) {
-    half_pass<TM_DEC1>(base, ck, bo, lane, K, jb.f1, jb.f2, it == 0);
-    half_pass<TM_DEC2>(base, ck, bo, lane, K, jb.f1, jb.f2, false);
+    half_pass<TM_DEC1>(base, ck, lane, K, jb.f1, jb.f2, it == 0);
+    half_pass<TM_DEC2>(base, ck, lane, K, jb.f1, jb.f2, false);
   }
-  half_pass<TM_FINAL>(base, ck, bo, lane, K, jb.f1, jb.f2, iters == 0);
+  // final pass = decoder 1 a-posteriori LLRs (turbo_decoder.py:436-446), then
+  // hard decisions L < 0 packed MSB-first from the rows this lane just wrote
+  // (kept out of the pass loop: accumulating bits there costs ~30 VGPRs).
+  half_pass<TM_APP>(base, ck, lane, K, jb.f1, jb.f2, iters == 0);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(base, (uint32_t)(turbo_rows(K) * RS * 4));
+  const RowPtr<float> LE{rb, 3 * K + 12, lane * 4};
+  const RowPtr<uint32_t> bout{make_rsrc(bo, (uint32_t)(turbo_kw(K) * RS * 4)), 0, lane * 4};
+#pragma unroll 1
+  for (int w = 0; w * 32 < K; ++w) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int k = w * 32 + i;
+      if (k < K) acc |= (LE.ld(k) < 0.0f ? 1u : 0u) << (31 - i);
+    }
+    bout.st(w, acc);
+  }
 }
 
 int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode) {

@@ -1175,6 +1175,7 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const float* llr, const
       }
     }
   }
+  for (float& v : h) v *= 0.5f;   // decoder rows hold LLR/2 (exact; lte_turbo.hip gam2)
   DBuf<float> db, dck;
   DBuf<uint32_t> dbits;
   const int KW = turbo_kw(K);

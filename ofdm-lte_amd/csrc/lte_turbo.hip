@@ -27,8 +27,12 @@ __device__ __forceinline__ float gsel(const float c[4], int fb, int par, int u) 
   return fb == 0 ? c[par * 2 + u] : -c[(1 - par) * 2 + (1 - u)];
 }
 
-__device__ __forceinline__ void gam(float ls, float lp, float la, float c[4]) {
-  const float hs = 0.5f * ls, hp = 0.5f * lp, ha = 0.5f * la;
+// Decoder rows hold LLR/2 (the dematch / host entry points scale by 0.5,
+// exact): those halves ARE the +-L/2 metric terms, so gamma needs no
+// multiplies and alpha, beta and the a-posteriori L are unchanged (LLR units).
+// The extrinsic is stored halved as (L/2 - La/2) - Ls/2, exactly half of
+// (L - La) - Ls (scaling by 2 commutes with rounding).
+__device__ __forceinline__ void gam(float hs, float hp, float ha, float c[4]) {
   const float sp = hs + hp, sm = hs - hp;
   c[0] = sp + ha;
   c[1] = sp - ha;
@@ -292,9 +296,9 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
         gam(ls[jj], lp[jj], la[jj], c);
         const float L = bstep(b, c, A[j]);
         if (MODE == TM_DEC1) {
-          LE.st(k, (L - la[jj]) - ls[jj]);
+          LE.st(k, (0.5f * L - la[jj]) - ls[jj]);
         } else if (MODE == TM_DEC2) {
-          LE.st(pl[jj], (L - la[jj]) - ls[jj]);
+          LE.st(pl[jj], (0.5f * L - la[jj]) - ls[jj]);
         } else {  // TM_APP: a-posteriori LLR in place of the extrinsic row
           LE.st(k, L);
         }
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(256) void k_dematch(const float* __restrict__ llr, 
     const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
-    blk[r][((size_t)g * rows[r] + row) * RS + f] = tile[f][c];
+    blk[r][((size_t)g * rows[r] + row) * RS + f] = 0.5f * tile[f][c];   // rows hold LLR/2 (exact)
   }
 }
 

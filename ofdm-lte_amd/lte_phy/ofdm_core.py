@@ -18,6 +18,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _capi as C
+from .dist import trial_shard
 from .config import ITU_CHANNEL_MODELS, LTEConfig
 from .engine import get_plan
 
@@ -555,7 +556,7 @@ class OFDMSimulator:
             n_sym = int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol)))
             chain = C.CHAIN_SIMO if num_rx > 1 else C.CHAIN_UNCODED
             plan = self._plan(chain, n_sym, nb, num_rx=num_rx, max_frames=frames_per_call)
-        ids = np.array([s * T + t for s in range(S) for t in range(rank, T, world_size)], dtype=np.uint64)
+        ids = np.array([s * T + t for s in range(S) for t in trial_shard(T, rank, world_size)], dtype=np.uint64)
         counts = np.zeros((S, 4), dtype=np.uint64)
         for i in range(0, len(ids), frames_per_call):
             chunk = ids[i:i + frames_per_call]

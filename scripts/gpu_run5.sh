@@ -3,7 +3,7 @@ cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"
 tail -25 gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
-summ() { python -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print('$1', d['value'], d['ms_per_step'], {k: round(v/d['steps'],2) for k,v in d['roofline']['kernel_ms'].items()})"; }
+summ() { python -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print('$1', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_per_step'])"; }
 timeout -k 10 400 python bench.py --frames 32768 --steps 3 --warmup 1 --no-cpu > gpurun_out/bench_default.log 2>&1 || { echo "bench failed rc=$?"; tail -5 gpurun_out/bench_default.log; exit 1; }
 summ gpurun_out/bench_default.log
 for V in ${VARIANTS:-plain}; do

@@ -11,6 +11,7 @@ for p in (ROOT, PKG):
         sys.path.insert(0, p)
 
 GOLDEN = os.path.join(ROOT, 'tests', 'golden', 'golden.npz')
+GOLDEN_MIMO = os.path.join(ROOT, 'tests', 'golden', 'golden_mimo.npz')
 
 
 def pytest_configure(config):
@@ -37,6 +38,17 @@ def pytest_collection_modifyitems(config, items):
 @pytest.fixture(scope='session')
 def golden():
     return np.load(GOLDEN, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def golden_mimo():
+    return np.load(GOLDEN_MIMO, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def mimo_oracle():
+    from oracle import mimo_oracle
+    return mimo_oracle
 
 
 @pytest.fixture(scope='session')

@@ -34,7 +34,16 @@ enum {
 enum {
   LTE_CHAIN_UNCODED = 0, /* OFDMSimulator.simulate_siso      core/ofdm_core.py:660-737   */
   LTE_CHAIN_CODED = 1,   /* OFDMSimulator.simulate_siso_coded core/ofdm_core.py:925-1338 */
-  LTE_CHAIN_SIMO = 2     /* OFDMSimulator.simulate_simo (MRC) core/ofdm_core.py:1536-1679 */
+  LTE_CHAIN_SIMO = 2,    /* OFDMSimulator.simulate_simo (MRC) core/ofdm_core.py:1536-1679 */
+  /* SFBC Alamouti 2 x num_rx, uncoded: simulate_miso / simulate_mimo
+   * (core/ofdm_core.py:1850-2258) with the estimator fix of SURVEY Q19 */
+  LTE_CHAIN_SFBC = 3,
+  /* config 4: the SISO coding chain (simulate_siso_coded TX/RX coding,
+   * core/ofdm_core.py:1003-1299) around SFBC 2 x num_rx */
+  LTE_CHAIN_SFBC_CODED = 4,
+  /* config 5: TM4 spatial multiplexing 4x4, rank 4, PMI 0 (W = I4), MMSE:
+   * simulate_spatial_multiplexing core/ofdm_core.py:2489-2815 */
+  LTE_CHAIN_SPATIAL = 5
 };
 enum { LTE_CH_AWGN = 0, LTE_CH_RAYLEIGH = 1 }; /* core/channel.py:10-245 */
 
@@ -60,6 +69,10 @@ typedef struct {
   int32_t turbo_iters;     /* coded: decoder iterations (reference passes 8)     */
   int32_t max_frames;      /* workspace capacity (frames per lte_run call)       */
   int32_t cell_id;         /* pilot PN seed (PilotPattern cell_id), normally 0   */
+  int32_t num_tx;          /* TX antennas: 1 (SISO/SIMO), 2 (SFBC), 4 (spatial).
+                            * Multi-antenna gains: SFBC as RayleighChannel holds
+                            * them; spatial links convert once more (Q2).  The
+                            * multi-antenna chains use one link per (rx, tx).   */
 } lte_plan_desc;
 
 typedef struct lte_plan lte_plan;
@@ -80,7 +93,8 @@ typedef struct {
   uint64_t frame_id0;
   /* injection (host, optional) */
   const uint8_t *bits; int64_t bits_stride;     /* [.][n_bits] values 0/1          */
-  const double *phases; int64_t phases_stride;  /* [.][num_rx][n_paths][16] rad    */
+  const double *phases; int64_t phases_stride;  /* [.][num_rx][n_paths][16] rad
+                                                   (multi-antenna: [.][num_rx][num_tx][n_paths][16]) */
   const double *noise; int64_t noise_stride;    /* [.][num_rx][2][L] unit normals  */
   /* outputs */
   uint64_t *counts;            /* host [n_snr][4] += {bit_err, bits, blk_err, blks} */
@@ -92,15 +106,25 @@ typedef struct {
   int32_t stages;
   const float *in_signal; int64_t in_signal_stride; /* [.][L] complex64 */
   /* captures (host, optional; used by the single-call Python API) */
-  float *cap_signal_tx;        /* [n_frames][L] complex64                           */
+  float *cap_signal_tx;        /* [n_frames][L] complex64 ([n_frames][num_tx][L] multi-antenna) */
   float *cap_signal_rx;        /* [n_frames][num_rx][L] complex64 (noisy)           */
-  float *cap_data_syms;        /* [n_frames][n_sym*Nd] complex64 (ZF or MRC output) */
+  float *cap_data_syms;        /* [n_frames][n_sym*Nd] complex64 (ZF / MRC / SFBC / MMSE output;
+                                  multi-antenna: n_sym*res, res = Nd&~1 SFBC, Nd spatial) */
   float *cap_H;                /* [n_frames][num_rx][n_grp][N] complex64            */
   float *cap_pilot_stats;      /* [n_frames][num_rx][n_grp][2] float (P, noise)     */
   uint8_t *cap_bits_rx;        /* [n_frames][n_bits]                                */
   float *cap_llr;              /* [n_frames][n_sym*Nd*bps] (coded, RE order)        */
   float *cap_noise_power;      /* [n_frames][num_rx]                                */
   float *cap_tx_syms;          /* [n_frames][n_sym*Nd] complex64 TX data REs        */
+  /* multi-antenna injection (optional): link noise of transmit_mimo's 100 dB
+   * per-link channels [.][num_rx][num_tx][2][L] unit normals; flat spatial
+   * link gains [.][num_rx][num_tx][2] (re, im of h ~ CN(0,1)) */
+  const double *link_noise; int64_t link_noise_stride;
+  const double *link_h; int64_t link_h_stride;
+  /* multi-antenna capture: per link [n_frames][num_rx][num_tx][4] = mean|x_tx|^2,
+   * mean|y_link|^2, Re and Im of mean(y_link conj(x_tx)) -- the statistics
+   * transmit_mimo reports its channel_matrix from (core/ofdm_core.py:505-516) */
+  float *cap_link_stats;
 } lte_run_args;
 
 /* Library / device. */

@@ -349,6 +349,13 @@ struct lte_plan {
   DBuf<int64_t> rows_dev;
   DBuf<uint32_t*> dec_ptrs;
   DBuf<int> kw_dev;
+  // multi-antenna chains (lte_mimo.hip)
+  bool mimo = false;
+  int res = 0;                       // QAM symbols per OFDM symbol (= Nd for SISO / SIMO)
+  MimoGrid mg{};
+  DBuf<int32_t> m_np, m_ppos, m_pseg;
+  DBuf<float2> m_pval, Ym, Hm;
+  DBuf<float> m_pig, link_part, link_sigma, inj_lz, inj_lh;
   // timing
   bool timing = false;
   double kms[KN_COUNT] = {0};
@@ -553,7 +560,7 @@ static int plan_coded_maps(lte_plan* p) {
   p->KWmax = (Kmax + 31) / 32 + 1;
   p->EW = (Kmax + 6 + 31) / 32;
   p->enc_words = p->C * 3 * p->EW;
-  const int bps = d.bps, Nd = p->Nd;
+  const int bps = d.bps, Nd = p->res;   // REs per OFDM symbol (SFBC: Nd & ~1)
   const int ncs_tx = (p->coded_len + bps - 1) / bps;  // bits_to_symbols pads (modulator.py:74-75)
   const int rows = (ncs_tx + Nd - 1) / Nd;
   p->n_sym = rows;
@@ -623,24 +630,88 @@ static int plan_coded_maps(lte_plan* p) {
   return LTE_OK;
 }
 
+// Per-TX CRS subsets (MIMOChannelEstimatorPeriodic.get_orthogonal_pilot_indices,
+// core/mimo_channel_estimator_periodic.py:75-107: pilots[t::step], step =
+// min(num_tx, 4); SFBCResourceMapper uses the same even/odd split for 2 TX)
+// with PilotPattern(t % 4) symbols, gaps and, for every data SC that carries
+// data, its left pilot within the subset.
+static int plan_mimo_tables(lte_plan* p) {
+  const lte_plan_desc& d = p->d;
+  const int nt = d.num_tx, step = nt <= 4 ? nt : 4;
+  std::vector<std::vector<int>> sub(nt);
+  for (int t = 0; t < nt; ++t)
+    for (int i = t % step; i < p->Np; i += step) sub[t].push_back(p->gh.pilot[i]);
+  int maxP = 1;
+  for (auto& v : sub) maxP = std::max<int>(maxP, (int)v.size());
+  const int nd = p->mg.n_dsc;
+  std::vector<int32_t> np(nt), ppos((size_t)nt * maxP, 0), pseg((size_t)nt * nd, -1);
+  std::vector<float2> pval((size_t)nt * maxP, make_float2(0.f, 0.f));
+  std::vector<float> pig((size_t)nt * maxP, 0.f);
+  for (int t = 0; t < nt; ++t) {
+    const int n = (int)sub[t].size();
+    if (n < 1) return fail(LTE_EUNSUP, "no pilots for a TX antenna");
+    np[t] = n;
+    std::vector<double> pr;
+    make_pilots(t % 4, n, pr);
+    for (int i = 0; i < n; ++i) {
+      ppos[(size_t)t * maxP + i] = sub[t][i];
+      pval[(size_t)t * maxP + i] = make_float2((float)pr[2 * i], (float)pr[2 * i + 1]);
+      if (i + 1 < n) pig[(size_t)t * maxP + i] = (float)(1.0 * (1.0 / (sub[t][i + 1] - sub[t][i])));
+    }
+    int sidx = -1;
+    for (int j = 0; j < nd; ++j) {
+      const int k = p->gh.data[j];
+      while (sidx + 1 < n && sub[t][sidx + 1] <= k) ++sidx;
+      pseg[(size_t)t * nd + j] = sidx;
+    }
+  }
+  if (upload(p->m_np, np) || upload(p->m_ppos, ppos) || upload(p->m_pseg, pseg) || upload(p->m_pval, pval) ||
+      upload(p->m_pig, pig))
+    return fail(LTE_ENOMEM, "mimo table upload failed");
+  p->mg.maxP = maxP;
+  p->mg.np_tx = p->m_np.p;
+  p->mg.ppos = p->m_ppos.p;
+  p->mg.pval = p->m_pval.p;
+  p->mg.pig = p->m_pig.p;
+  p->mg.pseg = p->m_pseg.p;
+  return LTE_OK;
+}
+
 static int plan_alloc(lte_plan* p) {
   const lte_plan_desc& d = p->d;
   const size_t B = (size_t)d.max_frames;
   const int G = (int)((B + 63) / 64);
   const int rx = d.num_rx;
   const bool ray = d.channel == LTE_CH_RAYLEIGH;
-  const bool coded = d.chain == LTE_CHAIN_CODED;
+  const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
   bool bad = false;
   bad |= p->pw.alloc(B * p->PW) != 0;
-  bad |= p->x.alloc(B * p->L) != 0;
-  if (ray) {
+  if (p->mimo) {
+    const MimoGrid& m = p->mg;
+    const size_t links = (size_t)m.num_rx * m.num_tx;
+    const int np = ray ? d.n_paths : 1;
+    bad |= p->x.alloc(B * m.num_tx * p->L) != 0;
+    bad |= p->y.alloc(B * m.num_rx * p->L) != 0;
+    bad |= p->coef.alloc(B * links * np * m.n_cs * 3) != 0;
+    if (ray && d.chain != LTE_CHAIN_SPATIAL) {
+      bad |= p->link_part.alloc(B * links * p->nblk) != 0;
+      bad |= p->link_sigma.alloc(B * links) != 0;
+    }
+    bad |= p->Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
+    bad |= p->Hm.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
+  } else {
+    bad |= p->x.alloc(B * p->L) != 0;
+  }
+  if (ray && !p->mimo) {
     bad |= p->y.alloc(B * rx * p->L) != 0;
     bad |= p->phases.alloc(std::max<size_t>(B * rx * d.n_paths * 16, 1)) != 0;
     bad |= p->coef.alloc(std::max<size_t>(B * rx * d.n_paths, 1)) != 0;
   }
   bad |= p->pow_part.alloc(B * rx * p->nblk) != 0;
-  bad |= p->H.alloc(B * rx * p->n_grp * d.N) != 0;
-  bad |= p->pstats.alloc(B * rx * p->n_grp * 2) != 0;
+  if (!p->mimo) {
+    bad |= p->H.alloc(B * rx * p->n_grp * d.N) != 0;
+    bad |= p->pstats.alloc(B * rx * p->n_grp * 2) != 0;
+  }
   bad |= p->npow.alloc(B * rx) != 0;
   bad |= p->snr_lin.alloc(B) != 0;
   bad |= p->snr_idx.alloc(B) != 0;
@@ -681,34 +752,61 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
   if (d.N < 128 || d.N > 2048 || (d.N & (d.N - 1))) return fail(LTE_EUNSUP, "N must be a power of two in [128, 2048]");
   if (d.Nc <= 0 || d.Nc >= d.N || d.cp_len < 0 || d.cp_len > d.N) return fail(LTE_EINVAL, "bad Nc / cp_len");
   if (d.bps != 2 && d.bps != 4 && d.bps != 6) return fail(LTE_EINVAL, "Unsupported modulation");
-  if (d.chain < 0 || d.chain > 2) return fail(LTE_EINVAL, "bad chain");
+  if (d.chain < 0 || d.chain > LTE_CHAIN_SPATIAL) return fail(LTE_EINVAL, "bad chain");
   if (d.channel != LTE_CH_AWGN && d.channel != LTE_CH_RAYLEIGH) return fail(LTE_EINVAL, "Tipo de canal desconocido");
   if (d.num_rx < 1 || d.num_rx > 16) return fail(LTE_EINVAL, "num_rx must be >= 1");
-  if (d.chain != LTE_CHAIN_SIMO && d.num_rx != 1) return fail(LTE_EINVAL, "SISO chains need num_rx == 1");
+  const bool mimo = d.chain >= LTE_CHAIN_SFBC;
+  const int num_tx = d.num_tx > 0 ? d.num_tx : 1;
+  if (!mimo && num_tx != 1) return fail(LTE_EINVAL, "num_tx > 1 needs a multi-antenna chain");
+  if (!mimo && d.chain != LTE_CHAIN_SIMO && d.num_rx != 1) return fail(LTE_EINVAL, "SISO chains need num_rx == 1");
+  if ((d.chain == LTE_CHAIN_SFBC || d.chain == LTE_CHAIN_SFBC_CODED) && num_tx != 2)
+    return fail(LTE_EINVAL, "Alamouti SFBC requires exactly 2 TX antennas");
+  if ((d.chain == LTE_CHAIN_SFBC || d.chain == LTE_CHAIN_SFBC_CODED) && d.num_rx > 8)
+    return fail(LTE_EUNSUP, "SFBC: at most 8 RX antennas");
+  if (d.chain == LTE_CHAIN_SPATIAL && (num_tx != 4 || d.num_rx != 4))
+    return fail(LTE_EUNSUP, "spatial multiplexing: 4x4, rank 4 (TM4 PMI 0) only");
   if (d.channel == LTE_CH_RAYLEIGH && (d.n_paths < 1 || d.n_paths > LTE_MAX_PATHS))
     return fail(LTE_EINVAL, "bad n_paths");
   if (d.max_frames < 1) return fail(LTE_EINVAL, "max_frames must be >= 1");
   if (d.n_bits < 1) return fail(LTE_EINVAL, "Bits array cannot be empty");
   lte_plan* p = new lte_plan();
   p->d = d;
-  if (d.chain == LTE_CHAIN_CODED && d.turbo_iters < 0) { delete p; return fail(LTE_EINVAL, "bad turbo_iters"); }
+  p->d.num_tx = num_tx;
+  p->mimo = mimo;
+  const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
+  if (coded && d.turbo_iters < 0) { delete p; return fail(LTE_EINVAL, "bad turbo_iters"); }
   int rc = plan_tables(p);
   if (rc) { delete p; return rc; }
   // Nd < N/2 is assumed by k_rx_data (4 data REs per thread)
   if (p->Nd * 2 >= d.N) { delete p; return fail(LTE_EUNSUP, "Nd >= N/2 not supported"); }
-  if (d.chain == LTE_CHAIN_CODED) {
+  const bool sfbc = d.chain == LTE_CHAIN_SFBC || d.chain == LTE_CHAIN_SFBC_CODED;
+  // REs per OFDM symbol: SFBC drops an odd last data SC (core/sfbc_alamouti.py:196-200, Q18)
+  p->res = sfbc ? (p->Nd & ~1) : p->Nd;
+  if (coded) {
     rc = plan_coded_maps(p);
     if (rc) { p->tabs.release(); delete p; return rc; }
     p->PW = (d.n_bits + 24 + 31) / 32 + 1;
   } else {
     if (d.n_sym < 1) { delete p; return fail(LTE_EINVAL, "n_sym must be >= 1"); }
     p->n_sym = d.n_sym;
-    if ((int64_t)d.n_bits > (int64_t)p->n_sym * p->Nd * d.bps) { delete p; return fail(LTE_EINVAL, "n_bits exceeds frame capacity"); }
-    p->PW = (p->n_sym * p->Nd * d.bps + 31) / 32 + 1;
+    if ((int64_t)d.n_bits > (int64_t)p->n_sym * p->res * d.bps) { delete p; return fail(LTE_EINVAL, "n_bits exceeds frame capacity"); }
+    p->PW = (p->n_sym * p->res * d.bps + 31) / 32 + 1;
   }
   p->L = p->n_sym * (d.N + d.cp_len);
   p->n_grp = (p->n_sym + 13) / 14;
   p->nblk = (p->L + 255) / 256;
+  if (mimo) {
+    MimoGrid& m = p->mg;
+    m.mode = sfbc ? MIMO_SFBC : MIMO_SPATIAL;
+    m.num_tx = num_tx;
+    m.num_rx = d.num_rx;
+    m.res = p->res;
+    m.n_dsc = sfbc ? p->res : (p->Nd + num_tx - 1) / num_tx;
+    m.n_est = sfbc ? p->n_grp : p->n_sym;
+    m.n_cs = (d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0) ? p->n_sym : 1;
+    rc = plan_mimo_tables(p);
+    if (rc) { p->tabs.release(); delete p; return rc; }
+  }
   p->grid = Grid{d.N, p->log2N, d.Nc, d.cp_len, p->Nd, p->Np, d.bps, p->n_sym, p->L, p->n_grp,
                  p->tabs.data.p, p->tabs.pilot.p, p->tabs.pilots.p, p->tabs.seg.p, p->tabs.inv_gap.p,
                  p->tabs.tw.p, p->tabs.constel.p,
@@ -748,6 +846,9 @@ int lte_plan_destroy(lte_plan* p) {
   for (auto& b : p->ckpt) b.release();
   for (auto& b : p->decb) b.release();
   p->blk_ptrs.release(); p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
+  p->m_np.release(); p->m_ppos.release(); p->m_pseg.release(); p->m_pval.release(); p->Ym.release();
+  p->Hm.release(); p->m_pig.release(); p->link_part.release(); p->link_sigma.release(); p->inj_lz.release();
+  p->inj_lh.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -797,6 +898,184 @@ static void pack_bits(const uint8_t* bits, int n, uint32_t* w, int nw) {
     if (bits[i] & 1) w[i >> 5] |= 1u << (31 - (i & 31));
 }
 
+// Multi-antenna chains (SFBC 2xN, uncoded / coded; spatial 4x4 MMSE).
+static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const uint32_t* inj_bits,
+                    int64_t inj_bits_stride, const float* inj_ph, int64_t inj_ph_stride, const float* inj_z,
+                    int64_t inj_z_stride) {
+  const lte_plan_desc& d = p->d;
+  const Grid& g = p->grid;
+  const MimoGrid& m = p->mg;
+  hipStream_t s = p->stream;
+  const bool coded = d.chain == LTE_CHAIN_SFBC_CODED;
+  const bool ray = d.channel == LTE_CH_RAYLEIGH;
+  const bool sfbc = m.mode == MIMO_SFBC;
+  const bool link_noise = sfbc && ray;  // transmit_mimo's per-link 100 dB ChannelSimulator (core/ofdm_core.py:490-503)
+  const size_t links = (size_t)m.num_rx * m.num_tx;
+  // link injections
+  const float* inj_lz = nullptr;
+  int64_t inj_lz_stride = 0;
+  std::vector<float> hlz;
+  if (a->link_noise && link_noise) {
+    const int nf = a->link_noise_stride ? B : 1;
+    const size_t per = links * 2 * p->L;
+    hlz.resize(nf * per);
+    for (int f = 0; f < nf; ++f)
+      for (size_t i = 0; i < per; ++i) hlz[f * per + i] = (float)a->link_noise[(size_t)f * a->link_noise_stride + i];
+    if (p->inj_lz.alloc(hlz.size())) return fail(LTE_ENOMEM, "inj link noise");
+    HIPCHK(hipMemcpyAsync(p->inj_lz.p, hlz.data(), hlz.size() * 4, hipMemcpyHostToDevice, s));
+    inj_lz = p->inj_lz.p;
+    inj_lz_stride = a->link_noise_stride ? (int64_t)per : 0;
+  }
+  const float* inj_lh = nullptr;
+  int64_t inj_lh_stride = 0;
+  std::vector<float> hlh;
+  if (a->link_h && !ray && !sfbc) {
+    const int nf = a->link_h_stride ? B : 1;
+    const size_t per = links * 2;
+    hlh.resize(nf * per);
+    for (int f = 0; f < nf; ++f)
+      for (size_t i = 0; i < per; ++i) hlh[f * per + i] = (float)a->link_h[(size_t)f * a->link_h_stride + i];
+    if (p->inj_lh.alloc(hlh.size())) return fail(LTE_ENOMEM, "inj link gains");
+    HIPCHK(hipMemcpyAsync(p->inj_lh.p, hlh.data(), hlh.size() * 4, hipMemcpyHostToDevice, s));
+    inj_lh = p->inj_lh.p;
+    inj_lh_stride = a->link_h_stride ? (int64_t)per : 0;
+  }
+  {
+    Timer t(p, KN_PAYLOAD);
+    LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
+  }
+  if (coded) {
+    Timer t(p, KN_ENCODE);
+    LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
+  }
+  {
+    Timer t(p, KN_OFDM_TX);
+    LCHK(launch_ofdm_tx_mimo(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B));
+  }
+  const int np = ray ? d.n_paths : 1;
+  {
+    Timer t(p, KN_FADING);
+    LCHK(launch_fading_mimo(s, g, m, B, ray ? 1 : 0, d.n_paths, p->gains.p, d.fD, d.fs, p->fid.p, a->seed, inj_ph,
+                            inj_ph_stride, inj_lh, inj_lh_stride, p->coef.p));
+  }
+  {
+    Timer t(p, KN_CHANNEL);
+    LCHK(launch_channel_mimo(s, g, m, B, np, ray ? p->delays.p : nullptr, p->coef.p, p->x.p, p->y.p,
+                             link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, p->link_part.p,
+                             p->link_sigma.p, p->pow_part.p, p->nblk));
+    // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
+    LCHK(launch_npow_mimo(s, B, m.num_rx, p->pow_part.p, p->nblk, p->L, p->snr_lin.p,
+                          sfbc ? 1.0f / (float)m.num_tx : 1.0f, p->npow.p));
+  }
+  {
+    Timer t(p, KN_RX_CHEST);
+    LCHK(launch_rx_fft_mimo(s, g, m, B, p->y.p, p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, p->Ym.p, p->Hm.p));
+  }
+  float2* cap_syms_dev = nullptr;
+  uint8_t* cap_bits_dev = nullptr;
+  if (a->cap_data_syms) {
+    if (p->capbuf.alloc((size_t)B * p->n_sym * m.res)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = p->capbuf.p;
+  }
+  if (a->cap_bits_rx) {
+    if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
+    cap_bits_dev = p->cap_bits.p;
+  }
+  {
+    Timer t(p, KN_RX_DATA);
+    if (sfbc)
+      LCHK(launch_det_sfbc(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, p->Ym.p, p->Hm.p, p->snr_lin.p, p->pw.p, p->PW,
+                           d.n_bits, p->frame_err.p, p->llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev));
+    else
+      LCHK(launch_det_mmse(s, g, m, B, p->Ym.p, p->Hm.p, p->snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+                           cap_syms_dev, cap_bits_dev));
+  }
+  if (coded) {
+    {
+      Timer t(p, KN_DEMATCH);
+      LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
+    }
+    const int G = (B + 63) / 64;
+    std::vector<TurboJob> jobs(p->C);
+    for (int r = 0; r < p->C; ++r) {
+      const CbInfo& c = p->cbs[r];
+      jobs[r] = TurboJob{p->blk[r].p, p->ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, G};
+    }
+    {
+      Timer t(p, KN_TURBO);
+      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1));
+    }
+    {
+      Timer t(p, KN_CRC);
+      LCHK(launch_crc_count(s, p->cbi.p, p->C, p->dec_ptrs.p, p->kw_dev.p, B, p->pw.p, p->PW, d.n_bits,
+                            p->frame_err.p, p->frame_crc.p, cap_bits_dev));
+    }
+  }
+  {
+    Timer t(p, KN_ACC);
+    LCHK(launch_accumulate(s, B, coded ? 1 : 0, d.n_bits, p->snr_idx.p, p->frame_err.p, p->frame_crc.p, p->counts.p));
+  }
+  std::vector<unsigned long long> hc((size_t)4 * n_snr);
+  HIPCHK(hipMemcpyAsync(hc.data(), p->counts.p, hc.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  if (a->frame_errors)
+    HIPCHK(hipMemcpyAsync(a->frame_errors, p->frame_err.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  std::vector<uint32_t> crc;
+  if (a->frame_crc_ok && coded) {
+    crc.resize(B);
+    HIPCHK(hipMemcpyAsync(crc.data(), p->frame_crc.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
+  if (a->cap_signal_tx)
+    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, p->x.p, (size_t)B * m.num_tx * p->L * sizeof(float2),
+                          hipMemcpyDeviceToHost, s));
+  if (a->cap_signal_rx) {
+    DBuf<float2> tmp;
+    if (tmp.alloc((size_t)B * m.num_rx * p->L)) return fail(LTE_ENOMEM, "capture");
+    {
+      Timer t(p, KN_CAP);
+      hipLaunchKernelGGL(k_cap_rx, dim3(((p->L + 255) / 256) * B, m.num_rx), dim3(256), 0, s, p->L, m.num_rx, B,
+                         p->y.p, (int64_t)p->L, (int64_t)m.num_rx * p->L, p->npow.p, p->fid.p, a->seed, inj_z,
+                         inj_z_stride, tmp.p);
+      LCHK((int)hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * m.num_rx * p->L * sizeof(float2),
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    tmp.release();
+  }
+  if (a->cap_data_syms)
+    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->n_sym * m.res * sizeof(float2),
+                          hipMemcpyDeviceToHost, s));
+  if (a->cap_H)   // multi-antenna layout [B][num_rx][n_est][num_tx][n_dsc]
+    HIPCHK(hipMemcpyAsync(a->cap_H, p->Hm.p, (size_t)B * m.num_rx * m.n_est * m.num_tx * m.n_dsc * sizeof(float2),
+                          hipMemcpyDeviceToHost, s));
+  if (a->cap_bits_rx)
+    HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
+  if (a->cap_llr && coded)
+    HIPCHK(hipMemcpyAsync(a->cap_llr, p->llr.p, (size_t)B * p->n_re_bits * sizeof(float), hipMemcpyDeviceToHost, s));
+  if (a->cap_noise_power)
+    HIPCHK(hipMemcpyAsync(a->cap_noise_power, p->npow.p, (size_t)B * m.num_rx * sizeof(float), hipMemcpyDeviceToHost,
+                          s));
+  DBuf<float> lpart, lstats;
+  if (a->cap_link_stats) {
+    if (lpart.alloc((size_t)B * links * 4 * p->nblk) || lstats.alloc((size_t)B * links * 4))
+      return fail(LTE_ENOMEM, "capture");
+    {
+      Timer t(p, KN_CAP);
+      LCHK(launch_link_stats(s, g, m, B, np, ray ? p->delays.p : nullptr, p->coef.p, p->x.p, lpart.p, p->nblk,
+                             lstats.p));
+    }
+    HIPCHK(hipMemcpyAsync(a->cap_link_stats, lstats.p, (size_t)B * links * 4 * sizeof(float), hipMemcpyDeviceToHost,
+                          s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  if (p->timing) collect_timing(p);
+  if (a->counts)
+    for (size_t i = 0; i < hc.size(); ++i) a->counts[i] += hc[i];
+  if (a->frame_crc_ok && coded)
+    for (int b = 0; b < B; ++b) a->frame_crc_ok[b] = (uint8_t)crc[b];
+  return LTE_OK;
+}
+
 int lte_run(lte_plan* p, const lte_run_args* a) {
   if (!p || !a) return fail(LTE_EINVAL, "null argument");
   const lte_plan_desc& d = p->d;
@@ -804,7 +1083,8 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (B < 1 || B > d.max_frames) return fail(LTE_EINVAL, "n_frames out of range (1..max_frames)");
   if (!a->snr_db) return fail(LTE_EINVAL, "snr_db required");
   const int n_snr = std::max(1, a->n_snr);
-  const bool coded = d.chain == LTE_CHAIN_CODED, ray_cfg = d.channel == LTE_CH_RAYLEIGH;
+  const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED,
+             ray_cfg = d.channel == LTE_CH_RAYLEIGH;
   const int rx = d.num_rx;
   hipStream_t s = p->stream;
   if (p->counts.alloc((size_t)4 * n_snr)) return fail(LTE_ENOMEM, "counts");
@@ -842,7 +1122,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   std::vector<float> hph;
   if (a->phases && ray_cfg) {
     const int nf = a->phases_stride ? B : 1;
-    const size_t per = (size_t)rx * d.n_paths * 16;
+    const size_t per = (size_t)rx * d.num_tx * d.n_paths * 16;
     hph.resize(nf * per);
     for (int f = 0; f < nf; ++f)
       for (size_t i = 0; i < per; ++i) hph[f * per + i] = (float)a->phases[(size_t)f * a->phases_stride + i];
@@ -872,6 +1152,10 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (!do_tx && !a->in_signal) return fail(LTE_EINVAL, "in_signal required when the TX stage is skipped");
   const Grid& g = p->grid;
   p->evuse.clear();
+  if (p->mimo) {
+    if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "multi-antenna chains run all stages");
+    return run_mimo(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_ph, inj_ph_stride, inj_z, inj_z_stride);
+  }
   if (do_tx || a->bits) {
     Timer t(p, KN_PAYLOAD);
     LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));

@@ -73,6 +73,48 @@ int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const f
 int launch_llr(hipStream_t s, int bps, int64_t n, const float2* syms, const float* nv, float* llr);
 int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* bits);
 
+// ---------------------------------------------------------------- multi-antenna chains
+// SFBC 2xN (configs 4 / simulate_miso / simulate_mimo) and TM4 spatial
+// multiplexing 4x4 (config 5).  lte_mimo.hip.
+enum { MIMO_SFBC = 0, MIMO_SPATIAL = 1 };
+struct MimoGrid {
+  int mode, num_tx, num_rx;
+  int res;                 // QAM symbols per OFDM symbol: SFBC Nd&~1, spatial Nd
+  int n_dsc;               // data SCs that carry data: SFBC Nd&~1, spatial ceil(Nd/num_tx)
+  int maxP;                // pilot stride of the per-TX tables
+  int n_est;               // channel estimates per frame (SFBC: one per 14-symbol group; spatial: every symbol)
+  int n_cs;                // fading coefficient sets per link path (1 if fD == 0, else n_sym)
+  const int32_t* np_tx;    // [num_tx] pilots of each TX
+  const int32_t* ppos;     // [num_tx][maxP] pilot subcarriers of TX t
+  const float2* pval;      // [num_tx][maxP] pilot symbols of TX t
+  const float* pig;        // [num_tx][maxP] 1/(gap to the next pilot of TX t)
+  const int32_t* pseg;     // [num_tx][n_dsc] left pilot (within TX t's set) of data SC j; -1 / >= np-1: edge hold
+};
+int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
+                        const uint32_t* enc, int enc_words, const int32_t* tx_map, float2* x, int B);
+// per link path: h(n) = A + B d + C d^2 around the centre of n's OFDM symbol (fD != 0), or A (fD == 0)
+int launch_fading_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int rayleigh, int n_paths,
+                       const float* gains, double fD, double fs, const uint64_t* fid, uint64_t seed,
+                       const float* inj_ph, int64_t inj_ph_stride, const float* inj_h, int64_t inj_h_stride,
+                       float2* coef);
+int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
+                        const float2* coef, const float2* x, float2* y, int link_noise, const uint64_t* fid,
+                        uint64_t seed, const float* inj_lz, int64_t inj_lz_stride, float* link_part,
+                        float* link_sigma, float* pow_part, int nblk);
+int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
+                      const float2* coef, const float2* x, float* part, int nblk, float* stats);
+int launch_npow_mimo(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
+                     float norm, float* npow);
+int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* y, const float* npow,
+                       const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride, float2* Y,
+                       float2* H);
+int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const float2* Y,
+                    const float2* H, const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    float* llr, float2* cap_syms, uint8_t* cap_bits);
+int launch_det_mmse(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
+                    const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    float2* cap_syms, uint8_t* cap_bits);
+
 // turbo modes
 enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3 };  // TM_DECODE: full decode (iterations + decisions)
 // turbo geometry: rows of one (r, group) block = 4K+12:

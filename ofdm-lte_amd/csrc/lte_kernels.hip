@@ -5,6 +5,7 @@
 // data once, coalesced, with per-symbol FFTs staged in LDS.
 #include "lte_common.h"
 #include "lte_internal.h"
+#include "lte_dev.h"
 
 namespace lte {
 
@@ -76,24 +77,6 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 // tx_map (rate_match_turbo + T/F interleaver, rate_matching.py:193-297,
 // ofdm_core.py:1040-1099), ResourceMapper.map_symbols (resource_mapper.py:
 // 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
-// QAM point of natural-binary index idx (modulator.py:28-59, I-major; QPSK
-// [1+1j, 1-1j, -1+1j, -1-1j]/sqrt 2), levels folded to float constants equal
-// to the float64 table cast to float.
-template <int BPS>
-__device__ __forceinline__ float2 qam_point(int idx) {
-  if constexpr (BPS == 2) {
-    constexpr float a = (float)(1.0 / 1.4142135623730951);
-    return make_float2((idx & 2) ? -a : a, (idx & 1) ? -a : a);
-  } else {
-    constexpr int H = BPS / 2, NL = 1 << H;
-    constexpr double S = BPS == 4 ? 3.1622776601683795 : 6.48074069840786;
-    float lv[NL];
-#pragma unroll
-    for (int i = 0; i < NL; ++i) lv[i] = (float)((2.0 * i - (NL - 1)) / S);
-    return make_float2(lv[idx >> H], lv[idx & (NL - 1)]);
-  }
-}
-
 template <int CODED, int BPS>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
@@ -214,18 +197,6 @@ int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* ga
 // rayleighchannel.py:44-58: stream-level delay with zero prefix, Q4) and the
 // per-block partial sums of |y|^2 for the measured-power SNR (channel.py:
 // 217-224, Q5).  AWGN: only the power of x.  grid (nblk, num_rx, B).
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  float t = 0.f;
-  if (threadIdx.x == 0) {
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
-  }
-  return t;
-}
-
 __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh, int n_paths,
                                                 const int32_t* __restrict__ delays, const float* __restrict__ gains,
                                                 float fD, float fs, const float* __restrict__ phases,
@@ -290,25 +261,6 @@ __device__ __forceinline__ float frame_power(const float* pp, int nblk, int L) {
 
 // Load one OFDM symbol (CP removed) of (frame, rx) into LDS adding AWGN:
 // noise = sigma * z, sigma = sqrt(P/SNR/2) (channel.py:52-60).
-__device__ __forceinline__ void load_symbol_noisy(float2* buf, const float2* __restrict__ yf, int N, int cp, int l,
-                                                  float sigma, uint64_t seed, uint64_t frame, int rx,
-                                                  const float* __restrict__ zf /*inj: [2][L] or null*/, int L,
-                                                  int tid, int T) {
-  const int off = l * (N + cp) + cp;
-  for (int k = tid; k < N; k += T) {
-    const int n = off + k;
-    float2 z;
-    if (zf) {
-      z = make_float2(zf[n], zf[L + n]);
-    } else {
-      const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)(n >> 1));
-      z = (n & 1) ? box_muller(r.z, r.w) : box_muller(r.x, r.y);
-    }
-    const float2 v = yf[n];
-    buf[k] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Channel estimation: one slot per (frame, rx, 14-symbol group) on the group's
 // first symbol (LTEReceiver._estimate_channel_periodic lte_receiver.py:360-411,
@@ -404,94 +356,6 @@ int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float
 // ---------------------------------------------------------------------------
 // Hard decision / soft demap.  Natural-binary QAM, I-level-major index
 // (modulator.py:28-59, Q9): bits = [I-level bits | Q-level bits], MSB first.
-__device__ __forceinline__ int level_idx(float v, float scale, int nl) {
-  // nearest of the nl levels (2i-(nl-1))/scale, ties -> lower level (argmin
-  // returns the first index, modulator.py:106)
-  const float t = (v * scale + (float)(nl - 1)) * 0.5f;
-  int i = (int)ceilf(t - 0.5f);
-  return i < 0 ? 0 : (i > nl - 1 ? nl - 1 : i);
-}
-
-__device__ __forceinline__ int hard_index(float2 y, int bps, float scale) {
-  if (bps == 2) return (y.x < 0.f ? 2 : 0) | (y.y < 0.f ? 1 : 0);  // [1+1j,1-1j,-1+1j,-1-1j]
-  const int nl = 1 << (bps >> 1);
-  return (level_idx(y.x, scale, nl) << (bps >> 1)) | level_idx(y.y, scale, nl);
-}
-
-// sqrt(2), sqrt(10), sqrt(42): the QAM normalisations of modulator.py:28-59
-template <int BPS>
-__host__ __device__ constexpr double qam_norm() { return BPS == 2 ? 1.4142135623730951 : (BPS == 4 ? 3.1622776601683795 : 6.48074069840786); }
-
-// max-log LLRs (core/ofdm_core.py:791-923): QPSK 2*sqrt(2)*y/nv (no clip);
-// 16/64-QAM (min_{b=1} d^2 - min_{b=0} d^2)/(2 nv) clipped to +-10.  The
-// natural-binary map makes the metric separable per axis.  NB bits per axis,
-// levels folded to constants (correctly rounded from the float64 grid).
-template <int NB>
-__device__ __forceinline__ void llr_axis(float v, float inv2nv, float* out) {
-  constexpr int NL = 1 << NB;
-  constexpr double S = NB == 2 ? 3.1622776601683795 : 6.48074069840786;
-  float m0[NB], m1[NB];
-#pragma unroll
-  for (int bb = 0; bb < NB; ++bb) { m0[bb] = 3.4e38f; m1[bb] = 3.4e38f; }
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const float lv = (float)((2.0 * i - (NL - 1)) / S);
-    const float d = (v - lv) * (v - lv);
-#pragma unroll
-    for (int bb = 0; bb < NB; ++bb) {
-      if ((i >> (NB - 1 - bb)) & 1) m1[bb] = fminf(m1[bb], d);
-      else m0[bb] = fminf(m0[bb], d);
-    }
-  }
-#pragma unroll
-  for (int bb = 0; bb < NB; ++bb) out[bb] = fminf(10.f, fmaxf(-10.f, (m1[bb] - m0[bb]) * inv2nv));
-}
-
-template <int BPS>
-__device__ __forceinline__ void soft_demap(float2 y, float nv, float* out) {
-  if constexpr (BPS == 2) {
-    out[0] = (2.0f / nv) * y.x * 1.41421356237309515f;
-    out[1] = (2.0f / nv) * y.y * 1.41421356237309515f;
-  } else {
-    const float inv2nv = 1.0f / (2.0f * nv);
-    llr_axis<BPS / 2>(y.x, inv2nv, out);
-    llr_axis<BPS / 2>(y.y, inv2nv, out + BPS / 2);
-  }
-}
-
-// y / h (lte_receiver.py:154-180 divides by H + 1e-6): multiply by the conjugate
-// over |h|^2; f32 relative error a few ulp (no over/underflow at these magnitudes).
-__device__ __forceinline__ float2 zf_div(float2 y, float2 h) {
-  const float r = 1.0f / (h.x * h.x + h.y * h.y);
-  return make_float2((y.x * h.x + y.y * h.y) * r, (y.y * h.x - y.x * h.y) * r);
-}
-
-// Noise-add for one OFDM symbol into LDS, one Philox call per pair of
-// samples (sample n uses half (n&1) of counter n>>1 -- same draws as
-// load_symbol_noisy, at half the generator cost).
-__device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __restrict__ yf, int N, int cp, int l,
-                                                   float sigma, uint64_t seed, uint64_t frame, int rx,
-                                                   const float* __restrict__ zf, int L, int tid, int T) {
-  const int off = l * (N + cp) + cp;
-  if (zf) {
-    load_symbol_noisy(buf, yf, N, cp, l, sigma, seed, frame, rx, zf, L, tid, T);
-    return;
-  }
-  const int p0 = off >> 1, p1 = (off + N - 1) >> 1;
-  for (int p = p0 + tid; p <= p1; p += T) {
-    const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
-    const int n0 = 2 * p;
-    if (n0 >= off) {
-      const float2 z = box_muller(r.x, r.y), v = yf[n0];
-      buf[n0 - off] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
-    }
-    if (n0 + 1 < off + N) {
-      const float2 z = box_muller(r.z, r.w), v = yf[n0 + 1];
-      buf[n0 + 1 - off] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Data path: one slot per (frame, OFDM symbol).  Per RX: CP-remove + noise +
 // FFT/sqrt(N) (lte_receiver.py:444-491); then

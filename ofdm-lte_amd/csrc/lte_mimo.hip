@@ -1,0 +1,680 @@
+// Multi-antenna chains for gfx950:
+//  * SFBC Alamouti 2 x num_rx (OFDMSimulator.simulate_miso / simulate_mimo,
+//    core/ofdm_core.py:1850-2258; config 4 = the same plus turbo coding),
+//  * TM4 spatial multiplexing 4x4, rank 4, W = I4, MMSE
+//    (simulate_spatial_multiplexing, core/ofdm_core.py:2489-2815; config 5).
+// Per frame:  TX  one slot per (frame, OFDM symbol, TX antenna): QAM map ->
+//                 SFBC pair coding / layer mapping -> per-TX CRS pilots -> IFFT + CP
+//             CH  per link path coefficients (Jakes, fD = 0 constant or a
+//                 per-symbol quadratic expansion when fD != 0), sum over TX,
+//                 measured-power noise per RX (transmit_mimo / _spatial_multiplexing)
+//             RX  one slot per (frame, RX, OFDM symbol): noise + CP removal + FFT;
+//                 on estimation symbols LS at each TX's pilot subset + linear
+//                 interpolation (MIMOChannelEstimatorPeriodic); data SCs to HBM
+//             DET SFBC combine averaged over RX -> hard bits / LLRs, or a
+//                 float64 4x4 MMSE per subcarrier -> hard bits.
+#include "lte_common.h"
+#include "lte_internal.h"
+#include "lte_dev.h"
+
+namespace lte {
+
+constexpr int MWG = 256;
+
+// ---------------------------------------------------------------------------
+// TX.  SFBCAlamouti.encode (core/sfbc_alamouti.py:45-78) + SFBCResourceMapper
+// (:213-256): data RE j of symbol l carries, for the pair (s0, s1) =
+// (q[l*res + (j&~1)], q[.. + 1]): TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)].
+// Spatial (core/ofdm_core.py:2596-2655): layer t = q[4j + t] on data SC j <
+// ceil(Nd/4) (Q20), W = I4.  Pilots: TX t at its subset (cell t % 4).
+template <int CODED, int BPS>
+__device__ __forceinline__ float2 qam_at(int64_t q, const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fe,
+                                         const int32_t* __restrict__ tx_map) {
+  int idx = 0;
+  bool zero = false;
+  if constexpr (CODED) {
+#pragma unroll
+    for (int m = 0; m < BPS; ++m) {
+      const int src = tx_map[q * BPS + m];
+      zero |= src == -2;
+      idx = (idx << 1) | (int)(src >= 0 ? getbit(fe, src) : 0u);
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, q * BPS + m);
+  }
+  return zero ? make_float2(0.f, 0.f) : qam_point<BPS>(idx);
+}
+
+template <int MODE, int CODED, int BPS>
+__global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
+                                                      const uint32_t* __restrict__ enc, int enc_words,
+                                                      const int32_t* __restrict__ tx_map, float2* __restrict__ x,
+                                                      int B) {
+  extern __shared__ float2 sm[];
+  const int N = g.N, T = N >> 3, spw = MWG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int per = g.n_sym * m.num_tx;
+  const int gs = blockIdx.x * spw + slot;
+  const int b = gs / per, r = gs - b * per, l = r / m.num_tx, t = r - l * m.num_tx;
+  const bool active = slot < spw && b < B;
+  float2* buf = sm + slot * N;
+  if (active)
+    for (int k = tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
+  __syncthreads();
+  if (active) {
+    const uint32_t* fb = pw + (size_t)b * PW;
+    const uint32_t* fe = enc + (size_t)b * enc_words;
+    const int64_t q0 = (int64_t)l * m.res;
+    for (int j = tid; j < m.n_dsc; j += T) {
+      float2 v;
+      if constexpr (MODE == MIMO_SFBC) {
+        const int64_t qp = q0 + (j & ~1);
+        const float2 s0 = qam_at<CODED, BPS>(qp, fb, fe, tx_map), s1 = qam_at<CODED, BPS>(qp + 1, fb, fe, tx_map);
+        if ((j & 1) == 0) v = t == 0 ? s0 : s1;
+        else v = t == 0 ? make_float2(-s1.x, s1.y) : make_float2(s0.x, -s0.y);   // -conj(s1) / conj(s0)
+      } else {
+        const int qi = 4 * j + t;
+        v = qi < m.res ? qam_at<CODED, BPS>(q0 + qi, fb, fe, tx_map) : make_float2(0.f, 0.f);
+      }
+      buf[g.data_idx[j]] = v;
+    }
+    const int npt = m.np_tx[t];
+    for (int p = tid; p < npt; p += T) buf[m.ppos[t * m.maxP + p]] = m.pval[t * m.maxP + p];
+  }
+  __syncthreads();
+  fft_lds<true>(buf, N, g.log2N, g.tw, tid, active);
+  if (active) {
+    const float sc = rsqrtf((float)N);
+    float2* xo = x + ((size_t)b * m.num_tx + t) * g.L + (size_t)l * (N + g.cp);
+    for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
+    for (int k = tid; k < g.cp; k += T) xo[k] = cscale(buf[N - g.cp + k], sc);
+  }
+}
+
+int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
+                        const uint32_t* enc, int enc_words, const int32_t* tx_map, float2* x, int B) {
+  const int spw = MWG / (g.N >> 3);
+  const int64_t total = (int64_t)B * g.n_sym * m.num_tx;
+  if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
+  const int blocks = (int)((total + spw - 1) / spw);
+  const size_t shm = spw * g.N * sizeof(float2);
+#define LTE_TXM(M_, C_, B_)                                                                                          \
+  hipLaunchKernelGGL((k_ofdm_tx_mimo<M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words,   \
+                     tx_map, x, B)
+#define LTE_TXM_BPS(M_, C_) \
+  do { if (g.bps == 2) LTE_TXM(M_, C_, 2); else if (g.bps == 4) LTE_TXM(M_, C_, 4); else LTE_TXM(M_, C_, 6); } while (0)
+  if (m.mode == MIMO_SFBC) {
+    if (coded) LTE_TXM_BPS(MIMO_SFBC, 1); else LTE_TXM_BPS(MIMO_SFBC, 0);
+  } else {
+    if (coded) LTE_TXM_BPS(MIMO_SPATIAL, 1); else LTE_TXM_BPS(MIMO_SPATIAL, 0);
+  }
+#undef LTE_TXM_BPS
+#undef LTE_TXM
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Link fading.  One thread per (frame, rx, tx, path).  Rayleigh:
+// RayleighChannel.jakes_fading (core/rayleighchannel.py:20-42) with 16 phases
+// (injected, or Philox): h(n) = g sqrt(2/16) sum_m exp(j(w_m n + phi_m)),
+// w_m = 2 pi fD cos(2 pi (m+1)/16) / fs.  fD == 0: constant A.  Otherwise,
+// per OFDM symbol s with centre c_s, the exact second-order expansion
+// h(c_s + d) = A + B d + C d^2 (|w d| <= 1.3e-3 rad at 3 km/h, 20 MHz: the
+// truncation error ~1e-10 is far below float32), computed in float64.
+// AWGN links: SFBC h = exp(j t pi/2) (core/ofdm_core.py:476-487); spatial
+// h ~ CN(0,1) (core/channel.py:473-480), injected or Philox.
+// coef layout: [B][rx][tx][path][n_cs][3] (A, B, C).
+__global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_tx, int n_paths, int n_cs, int mode,
+                                                     int rayleigh, const float* __restrict__ gains, double fD,
+                                                     double fs, int sym_len, const uint64_t* __restrict__ fid,
+                                                     uint64_t seed, const float* __restrict__ inj_ph,
+                                                     int64_t inj_ph_stride, const float* __restrict__ inj_h,
+                                                     int64_t inj_h_stride, float2* __restrict__ coef) {
+  const int per = num_rx * num_tx * n_paths;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * per) return;
+  const int b = i / per, rem = i - b * per, link = rem / n_paths, p = rem - link * n_paths;
+  const int rx = link / num_tx, tx = link - rx * num_tx;
+  float2* out = coef + (size_t)i * n_cs * 3;
+  if (!rayleigh) {
+    double hr = 0.0, hi = 0.0;
+    if (mode == MIMO_SFBC) {
+      if (tx == 0) { hr = 1.0; hi = 0.0; }
+      else { hr = cos(tx * 1.5707963267948966); hi = sin(tx * 1.5707963267948966); }
+    } else if (inj_h) {
+      const float* hh = inj_h + (size_t)b * inj_h_stride + (size_t)link * 2;
+      hr = hh[0]; hi = hh[1];
+    } else {
+      const u32x4 r = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, 0x7FFFFFFFu);
+      const float2 z = box_muller(r.x, r.y);
+      hr = z.x * 0.7071067811865476; hi = z.y * 0.7071067811865476;
+    }
+    out[0] = make_float2((float)hr, (float)hi);
+    out[1] = out[2] = make_float2(0.f, 0.f);
+    return;
+  }
+  double ph[16];
+  for (int mm = 0; mm < 16; ++mm) {
+    if (inj_ph) {
+      ph[mm] = inj_ph[(size_t)b * inj_ph_stride + (size_t)rem * 16 + mm];
+    } else {
+      const u32x4 r = rng4(seed, fid[b], RNG_STREAM_MIMO_FADE + (uint32_t)rem, (uint32_t)(mm >> 2));
+      const int q = mm & 3;
+      const uint32_t u = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+      ph[mm] = 6.283185307179586 * ((u >> 8) * (1.0 / 16777216.0));
+    }
+  }
+  const double k = sqrt(2.0 / 16.0) * (double)gains[p];
+  // per sinusoid: phasor at the first symbol centre, then rotate by w * sym_len
+  // per symbol (float64 recurrence: 2 sincos per sinusoid instead of one per symbol)
+  double w[16], zr[16], zi[16], rr[16], ri[16];
+  const double c0 = fD == 0.0 ? 0.0 : 0.5 * (sym_len - 1);
+  for (int mm = 0; mm < 16; ++mm) {
+    w[mm] = fD == 0.0 ? 0.0 : 6.283185307179586 * fD * cos(6.283185307179586 * (mm + 1) / 16.0) / fs;
+    sincos(w[mm] * c0 + ph[mm], &zi[mm], &zr[mm]);
+    sincos(w[mm] * (double)sym_len, &ri[mm], &rr[mm]);
+  }
+  for (int sidx = 0; sidx < n_cs; ++sidx) {
+    double ar = 0, ai = 0, br = 0, bi = 0, cr = 0, ci = 0;
+    for (int mm = 0; mm < 16; ++mm) {
+      const double cv = zr[mm], sv = zi[mm], wm = w[mm];
+      ar += cv; ai += sv;
+      br += -wm * sv; bi += wm * cv;                   // j w e^{j th}
+      cr += -0.5 * wm * wm * cv; ci += -0.5 * wm * wm * sv;
+      zr[mm] = cv * rr[mm] - sv * ri[mm];
+      zi[mm] = cv * ri[mm] + sv * rr[mm];
+    }
+    out[sidx * 3 + 0] = make_float2((float)(ar * k), (float)(ai * k));
+    out[sidx * 3 + 1] = make_float2((float)(br * k), (float)(bi * k));
+    out[sidx * 3 + 2] = make_float2((float)(cr * k), (float)(ci * k));
+  }
+}
+
+int launch_fading_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int rayleigh, int n_paths,
+                       const float* gains, double fD, double fs, const uint64_t* fid, uint64_t seed,
+                       const float* inj_ph, int64_t inj_ph_stride, const float* inj_h, int64_t inj_h_stride,
+                       float2* coef) {
+  const int np = rayleigh ? n_paths : 1;
+  const int n = B * m.num_rx * m.num_tx * np;
+  hipLaunchKernelGGL(k_fading_mimo, dim3((n + MWG - 1) / MWG), dim3(MWG), 0, s, B, m.num_rx, m.num_tx, np, m.n_cs,
+                     m.mode, rayleigh, gains, fD, fs, g.N + g.cp, fid, seed, inj_ph, inj_ph_stride, inj_h,
+                     inj_h_stride, coef);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Channel.  y_rx[n] = sum_tx sum_p h_{rx,tx,p}(n) x_tx[n - d_p] (stream-level
+// delay with a zero prefix, Q4) + (transmit_mimo Rayleigh only) the link noise
+// of each link's own 100 dB ChannelSimulator (core/ofdm_core.py:490-503:
+// sigma^2 = P_link / 1e10, still drawn).  Power partials -> noise per RX:
+// SFBC (P_rx / num_tx) / SNR (:524-534), spatial P_rx / SNR (channel.py:457-467).
+__device__ __forceinline__ float2 link_sample(const float2* __restrict__ cf, int n_cs, int np, int n, int sym_len,
+                                              const int32_t* __restrict__ delays, const float2* __restrict__ xf) {
+  const int sidx = n_cs > 1 ? n / sym_len : 0;
+  const float d = n_cs > 1 ? (float)(n - sidx * sym_len) - 0.5f * (float)(sym_len - 1) : 0.f;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int p = 0; p < np; ++p) {
+    const int src = n - (delays ? delays[p] : 0);
+    if (src < 0) continue;
+    const float2* c = cf + ((size_t)p * n_cs + sidx) * 3;
+    float2 h = c[0];
+    if (n_cs > 1) {   // A + B d + C d^2
+      h.x += d * (c[1].x + d * c[2].x);
+      h.y += d * (c[1].y + d * c[2].y);
+    }
+    acc = cadd(acc, cmul(h, xf[src]));
+  }
+  return acc;
+}
+
+// pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal
+__global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
+                                                    const int32_t* __restrict__ delays,
+                                                    const float2* __restrict__ coef, const float2* __restrict__ x,
+                                                    float* __restrict__ part, int nblk) {
+  __shared__ float red[MWG / 64];
+  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
+  const int link = blockIdx.y, rx = link / num_tx, tx = link - rx * num_tx;
+  const int n = blk * MWG + threadIdx.x;
+  float v = 0.f;
+  if (n < L) {
+    const float2* cf = coef + (((size_t)b * num_rx + rx) * num_tx + tx) * np * n_cs * 3;
+    const float2 yv = link_sample(cf, n_cs, np, n, sym_len, delays, x + ((size_t)b * num_tx + tx) * L);
+    v = yv.x * yv.x + yv.y * yv.y;
+  }
+  const float t = block_sum(v, red);
+  if (threadIdx.x == 0) part[(((size_t)b * num_rx * num_tx) + link) * nblk + blk] = t;
+}
+
+// sigma_link = sqrt(P_link / 1e10 / 2)
+__global__ void k_link_sigma(int n_links_total, const float* __restrict__ part, int nblk, int L,
+                             float* __restrict__ sigma) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_links_total) return;
+  double acc = 0.0;
+  for (int k = 0; k < nblk; ++k) acc += part[(size_t)i * nblk + k];
+  sigma[i] = (float)sqrt(acc / L / 1e10 * 0.5);
+}
+
+__global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
+                                                      const int32_t* __restrict__ delays,
+                                                      const float2* __restrict__ coef, const float2* __restrict__ x,
+                                                      float2* __restrict__ y, const float* __restrict__ link_sigma,
+                                                      const uint64_t* __restrict__ fid, uint64_t seed,
+                                                      const float* __restrict__ inj_lz, int64_t inj_lz_stride,
+                                                      float* __restrict__ pow_part, int nblk) {
+  __shared__ float red[MWG / 64];
+  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
+  const int rx = blockIdx.y;
+  const int n = blk * MWG + threadIdx.x;
+  float2 v = make_float2(0.f, 0.f);
+  if (n < L) {
+    for (int tx = 0; tx < num_tx; ++tx) {
+      const size_t link = (size_t)rx * num_tx + tx;
+      const float2* cf = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3;
+      float2 yl = link_sample(cf, n_cs, np, n, sym_len, delays, x + ((size_t)b * num_tx + tx) * L);
+      if (link_sigma) {
+        const float sg = link_sigma[(size_t)b * num_rx * num_tx + link];
+        float2 z;
+        if (inj_lz) {
+          const float* zf = inj_lz + (size_t)b * inj_lz_stride + link * 2 * L;
+          z = make_float2(zf[n], zf[L + n]);
+        } else {
+          const u32x4 r = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
+          z = (n & 1) ? box_muller(r.z, r.w) : box_muller(r.x, r.y);
+        }
+        yl = make_float2(yl.x + sg * z.x, yl.y + sg * z.y);
+      }
+      v = cadd(v, yl);
+    }
+    y[((size_t)b * num_rx + rx) * L + n] = v;
+  }
+  const float t = block_sum(v.x * v.x + v.y * v.y, red);
+  if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blk] = t;
+}
+
+int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
+                        const float2* coef, const float2* x, float2* y, int link_noise, const uint64_t* fid,
+                        uint64_t seed, const float* inj_lz, int64_t inj_lz_stride, float* link_part,
+                        float* link_sigma, float* pow_part, int nblk) {
+  const int sym_len = g.N + g.cp;
+  if (link_noise) {
+    hipLaunchKernelGGL(k_link_power, dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx,
+                       n_paths, m.n_cs, sym_len, delays, coef, x, link_part, nblk);
+    const int nl = B * m.num_rx * m.num_tx;
+    hipLaunchKernelGGL(k_link_sigma, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nblk, g.L, link_sigma);
+  }
+  hipLaunchKernelGGL(k_channel_mimo, dim3(nblk * B, m.num_rx), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths,
+                     m.n_cs, sym_len, delays, coef, x, y, link_noise ? link_sigma : nullptr, fid, seed, inj_lz,
+                     inj_lz_stride, pow_part, nblk);
+  return (int)hipGetLastError();
+}
+
+// Per-link statistics for the reported channel matrix (transmit_mimo,
+// core/ofdm_core.py:505-516): mean|x|^2, mean|y_link|^2, mean(y_link conj(x)).
+__global__ __launch_bounds__(MWG) void k_link_stats_part(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
+                                                         const int32_t* __restrict__ delays,
+                                                         const float2* __restrict__ coef,
+                                                         const float2* __restrict__ x, float* __restrict__ part,
+                                                         int nblk) {
+  __shared__ float red[MWG / 64];
+  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
+  const int link = blockIdx.y, rx = link / num_tx, tx = link - rx * num_tx;
+  const int n = blk * MWG + threadIdx.x;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (n < L) {
+    const float2* xf = x + ((size_t)b * num_tx + tx) * L;
+    const float2* cf = coef + (((size_t)b * num_rx + rx) * num_tx + tx) * np * n_cs * 3;
+    const float2 yv = link_sample(cf, n_cs, np, n, sym_len, delays, xf), xv = xf[n];
+    v[0] = xv.x * xv.x + xv.y * xv.y;
+    v[1] = yv.x * yv.x + yv.y * yv.y;
+    const float2 c = cmulc(yv, xv);
+    v[2] = c.x;
+    v[3] = c.y;
+  }
+  for (int q = 0; q < 4; ++q) {
+    const float t = block_sum(v[q], red);
+    if (threadIdx.x == 0) part[((((size_t)b * num_rx * num_tx) + link) * 4 + q) * nblk + blk] = t;
+    __syncthreads();
+  }
+}
+
+__global__ void k_link_stats_fin(int n, const float* __restrict__ part, int nblk, int L, float* __restrict__ stats) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double acc = 0.0;
+  for (int k = 0; k < nblk; ++k) acc += part[(size_t)i * nblk + k];
+  stats[i] = (float)(acc / L);
+}
+
+int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
+                      const float2* coef, const float2* x, float* part, int nblk, float* stats) {
+  hipLaunchKernelGGL(k_link_stats_part, dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx,
+                     m.num_tx, n_paths, m.n_cs, g.N + g.cp, delays, coef, x, part, nblk);
+  const int n = B * m.num_rx * m.num_tx * 4;
+  hipLaunchKernelGGL(k_link_stats_fin, dim3((n + 255) / 256), dim3(256), 0, s, n, part, nblk, g.L, stats);
+  return (int)hipGetLastError();
+}
+
+__global__ void k_npow_mimo(int n, const float* __restrict__ pow_part, int nblk, int L, const float* __restrict__ snr_lin,
+                            int num_rx, float norm, float* __restrict__ npow) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double acc = 0.0;
+  for (int k = 0; k < nblk; ++k) acc += pow_part[(size_t)i * nblk + k];
+  npow[i] = (float)(acc / L * norm / snr_lin[i / num_rx]);
+}
+
+int launch_npow_mimo(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
+                     float norm, float* npow) {
+  const int n = B * num_rx;
+  hipLaunchKernelGGL(k_npow_mimo, dim3((n + 255) / 256), dim3(256), 0, s, n, pow_part, nblk, L, snr_lin, num_rx,
+                     norm, npow);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// RX FFT + MIMO CRS estimation.  One slot per (frame, rx, OFDM symbol):
+// noise + CP removal + FFT/sqrt(N) (demodulate_and_estimate_mimo, core/
+// mimo_channel_estimator_periodic.py:236-273); the n_dsc data SCs go to
+// Y[b][l][rx][n_dsc].  On estimation symbols (SFBC: first of each 14-symbol
+// group, :195-234; spatial: every symbol, core/ofdm_core.py:2752) LS at each
+// TX's pilot subset + linear interpolation with edge hold (:108-185 +
+// lte_receiver.py:98-133) at the data SCs -> H[b][rx][e][tx][n_dsc].
+__global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const float2* __restrict__ y,
+                                                     const float* __restrict__ npow, const uint64_t* __restrict__ fid,
+                                                     uint64_t seed, const float* __restrict__ inj_z,
+                                                     int64_t inj_stride, float2* __restrict__ Y,
+                                                     float2* __restrict__ H) {
+  extern __shared__ float2 sm[];
+  const int N = g.N, T = N >> 3, spw = MWG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int per = m.num_rx * g.n_sym;
+  const int gs = blockIdx.x * spw + slot;
+  const int b = gs / per, r = gs - b * per, rx = r / g.n_sym, l = r - rx * g.n_sym;
+  const bool active = slot < spw && b < B;
+  float2* buf = sm + slot * N;
+  float2* hp = sm + spw * N + slot * (m.num_tx * m.maxP);
+  if (active) {
+    const float sigma = sqrtf(npow[(size_t)b * m.num_rx + rx] * 0.5f);
+    const float* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+    load_symbol_noisy2(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf, g.L, tid,
+                       T);
+  }
+  __syncthreads();
+  fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
+  const int e = m.mode == MIMO_SFBC ? l / 14 : l;
+  const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
+  const float sc = rsqrtf((float)N);
+  if (active && est) {
+    for (int t = 0; t < m.num_tx; ++t)
+      for (int p = tid; p < m.np_tx[t]; p += T)
+        hp[t * m.maxP + p] = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), m.pval[t * m.maxP + p]);
+  }
+  __syncthreads();
+  if (active) {
+    float2* Yo = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
+    for (int j = tid; j < m.n_dsc; j += T) Yo[j] = cscale(buf[g.data_idx[j]], sc);
+    if (est) {
+      for (int t = 0; t < m.num_tx; ++t) {
+        const float2* hpt = hp + t * m.maxP;
+        const int npt = m.np_tx[t];
+        float2* Ho = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + t) * m.n_dsc;
+        for (int j = tid; j < m.n_dsc; j += T) {
+          const int sidx = m.pseg[t * m.n_dsc + j];
+          float2 h;
+          if (sidx < 0) h = hpt[0];
+          else if (sidx >= npt - 1) h = hpt[npt - 1];
+          else {
+            const float2 v0 = hpt[sidx], v1 = hpt[sidx + 1];
+            const float fk = (float)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
+            const float ig = m.pig[t * m.maxP + sidx];
+            h = make_float2(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+          }
+          Ho[j] = h;
+        }
+      }
+    }
+  }
+}
+
+int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* y, const float* npow,
+                       const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride, float2* Y,
+                       float2* H) {
+  const int spw = MWG / (g.N >> 3);
+  const int64_t total = (int64_t)B * m.num_rx * g.n_sym;
+  if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
+  const int blocks = (int)((total + spw - 1) / spw);
+  const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(float2);
+  hipLaunchKernelGGL(k_rx_fft_mimo, dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z, inj_stride,
+                     Y, H);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// SFBC detection.  One thread per (frame, OFDM symbol, SC pair).
+// SFBCAlamouti.decode (core/sfbc_alamouti.py:80-163) per RX with that RX's
+// slot estimate, averaged over RX (core/ofdm_core.py:2204, Q17).  Uncoded:
+// nearest-point hard bits vs the payload (bit errors).  Coded (config 4):
+// max-log LLRs (core/ofdm_core.py:791-923) with the per-RE noise variance of
+// the combined estimate, sigma^2 / R^2 * sum_r 1 / clip(norm_r, 1e-6, 1e6),
+// floored at sigma^2 / 4 as in the SISO rule (ofdm_core.py:1224-1243) -- the
+// reference has no coded SFBC chain; DESIGN.md documents this composition.
+template <int CODED, int BPS>
+__global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, const float2* __restrict__ Y,
+                                                  const float2* __restrict__ H, const float* __restrict__ snr_lin,
+                                                  const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                  uint32_t* __restrict__ frame_err, float* __restrict__ llr,
+                                                  float2* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+  const int npair = m.n_dsc >> 1;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)g.n_sym * npair;
+  const int b = (int)(i / per);
+  if (b >= B) return;
+  const int rem = (int)(i - (int64_t)b * per), l = rem / npair, pr = rem - l * npair, j = 2 * pr;
+  const int e = l / 14;
+  float2 z0 = make_float2(0.f, 0.f), z1 = make_float2(0.f, 0.f);
+  float inv_g = 0.f;
+  for (int rx = 0; rx < m.num_rx; ++rx) {
+    const float2* Yr = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
+    const float2* H0 = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + 0) * m.n_dsc;
+    const float2* H1 = H0 + m.n_dsc;
+    const float2 rk = Yr[j], rk1 = Yr[j + 1];
+    const float2 h0k = H0[j], h1k = H1[j], h0k1 = H0[j + 1], h1k1 = H1[j + 1];
+    const float2 rc = make_float2(rk1.x, -rk1.y);
+    const float2 s0 = cadd(cmulc(rk, h0k), cmul(h1k1, rc));      // conj(h0k) rk + h1k1 conj(rk1)
+    const float2 s1 = csub(cmulc(rk, h1k), cmul(h0k1, rc));      // conj(h1k) rk - h0k1 conj(rk1)
+    const float2 a0 = make_float2(0.5f * (h0k.x + h0k1.x), 0.5f * (h0k.y + h0k1.y));
+    const float2 a1 = make_float2(0.5f * (h1k.x + h1k1.x), 0.5f * (h1k.y + h1k1.y));
+    const float nrm = (a0.x * a0.x + a0.y * a0.y) + (a1.x * a1.x + a1.y * a1.y) + 1e-10f;
+    z0 = make_float2(z0.x + s0.x / nrm, z0.y + s0.y / nrm);
+    z1 = make_float2(z1.x + s1.x / nrm, z1.y + s1.y / nrm);
+    inv_g += 1.0f / fminf(fmaxf(nrm, 1e-6f), 1e6f);
+  }
+  const float ir = 1.0f / (float)m.num_rx;
+  z0 = make_float2(z0.x * ir, z0.y * ir);
+  z1 = make_float2(z1.x * ir, z1.y * ir);
+  const int64_t re = (int64_t)l * m.res + j;
+  if (cap_syms) {
+    cap_syms[(size_t)b * g.n_sym * m.res + re] = z0;
+    cap_syms[(size_t)b * g.n_sym * m.res + re + 1] = z1;
+  }
+  if constexpr (CODED) {
+    const float s2 = 1.0f / snr_lin[b];
+    const float nv = fmaxf(s2 * ir * ir * inv_g, s2 * 0.25f);
+    float o[BPS];
+    float* lo = llr + ((size_t)b * g.n_sym * m.res + re) * BPS;
+    soft_demap<BPS>(z0, nv, o);
+#pragma unroll
+    for (int q = 0; q < BPS; ++q) lo[q] = o[q];
+    soft_demap<BPS>(z1, nv, o);
+#pragma unroll
+    for (int q = 0; q < BPS; ++q) lo[BPS + q] = o[q];
+  } else {
+    const uint32_t* fb = pw + (size_t)b * PW;
+    uint32_t errs = 0;
+    for (int h = 0; h < 2; ++h) {
+      const int idx = hard_index(h ? z1 : z0, BPS, (float)qam_norm<BPS>());
+#pragma unroll
+      for (int q = 0; q < BPS; ++q) {
+        const int64_t pbit = (re + h) * BPS + q;
+        if (pbit < n_bits) {
+          const uint32_t bit = (idx >> (BPS - 1 - q)) & 1;
+          errs += bit ^ getbit(fb, pbit);
+          if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
+        }
+      }
+    }
+    if (errs) atomicAdd(frame_err + b, errs);
+  }
+}
+
+int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const float2* Y,
+                    const float2* H, const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    float* llr, float2* cap_syms, uint8_t* cap_bits) {
+  (void)rayleigh;
+  const int64_t n = (int64_t)B * g.n_sym * (m.n_dsc >> 1);
+  const dim3 grid((unsigned)((n + MWG - 1) / MWG));
+#define LTE_DS(C_, B_) \
+  hipLaunchKernelGGL((k_det_sfbc<C_, B_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits, frame_err, \
+                     llr, cap_syms, cap_bits)
+  if (coded) {
+    if (g.bps == 2) LTE_DS(1, 2); else if (g.bps == 4) LTE_DS(1, 4); else LTE_DS(1, 6);
+  } else {
+    if (g.bps == 2) LTE_DS(0, 2); else if (g.bps == 4) LTE_DS(0, 4); else LTE_DS(0, 6);
+  }
+#undef LTE_DS
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// MMSE 4x4 (MIMODetector._mmse_detect, core/mimo_detector.py:135-173): per
+// (frame, symbol, data SC j < ceil(Nd/4)), s = (H^H H + s2 I)^-1 H^H y with
+// the nominal s2 = 10^(-SNR/10) (core/ofdm_core.py:2737) and W = I4.  Solved in
+// float64 (Cholesky of the Hermitian positive definite H^H H + s2 I; the
+// reference inverts with LAPACK LU -- both are backward stable here); ~600
+// flops per SC, negligible next to the FFTs.  Layer t of SC j is QAM symbol
+// 4j + t of the OFDM symbol (LayerMapper.demap_from_layers :81-115).
+struct dc { double x, y; };
+__device__ __forceinline__ dc dmul(dc a, dc b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ dc dmulc(dc a, dc b) { return {a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y}; }  // a*conj(b)
+__device__ __forceinline__ dc dsub(dc a, dc b) { return {a.x - b.x, a.y - b.y}; }
+
+template <int BPS>
+__global__ __launch_bounds__(MWG) void k_det_mmse(Grid g, MimoGrid m, int B, const float2* __restrict__ Y,
+                                                  const float2* __restrict__ H, const float* __restrict__ snr_lin,
+                                                  const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                  uint32_t* __restrict__ frame_err, float2* __restrict__ cap_syms,
+                                                  uint8_t* __restrict__ cap_bits) {
+  constexpr int NT = 4, NR = 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)g.n_sym * m.n_dsc;
+  const int b = (int)(i / per);
+  if (b >= B) return;
+  const int rem = (int)(i - (int64_t)b * per), l = rem / m.n_dsc, j = rem - l * m.n_dsc;
+  dc h[NR][NT], yv[NR];
+  for (int r = 0; r < NR; ++r) {
+    const float2 v = Y[(((size_t)b * g.n_sym + l) * NR + r) * m.n_dsc + j];
+    yv[r] = {v.x, v.y};
+    for (int t = 0; t < NT; ++t) {
+      const float2 hv = H[((((size_t)b * NR + r) * m.n_est + l) * NT + t) * m.n_dsc + j];
+      h[r][t] = {hv.x, hv.y};
+    }
+  }
+  const double s2 = 1.0 / (double)snr_lin[b];
+  // A = H^H H + s2 I is Hermitian positive definite: Cholesky A = L L^H (no
+  // pivoting needed, fully unrolled -> registers only), then L u = H^H y and
+  // L^H s = u.  Float64 throughout.
+  dc A[NT][NT], rhs[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+#pragma unroll
+    for (int c = 0; c <= a; ++c) {
+      dc acc = {0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const dc p = dmulc(h[r][c], h[r][a]);   // conj(h[r][a]) h[r][c] = (H^H H)[a][c]
+        acc.x += p.x; acc.y += p.y;
+      }
+      if (a == c) acc.x += s2;
+      A[a][c] = acc;
+    }
+    dc acc = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const dc p = dmulc(yv[r], h[r][a]);
+      acc.x += p.x; acc.y += p.y;
+    }
+    rhs[a] = acc;
+  }
+  dc Lm[NT][NT];
+  double ld[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    double d = A[i][i].x;
+#pragma unroll
+    for (int k = 0; k < i; ++k) d -= Lm[i][k].x * Lm[i][k].x + Lm[i][k].y * Lm[i][k].y;
+    ld[i] = sqrt(fmax(d, 1e-300));
+    const double inv = 1.0 / ld[i];
+#pragma unroll
+    for (int j = i + 1; j < NT; ++j) {
+      dc v = A[j][i];
+#pragma unroll
+      for (int k = 0; k < i; ++k) v = dsub(v, dmulc(Lm[j][k], Lm[i][k]));   // L[j][k] conj(L[i][k])
+      Lm[j][i] = {v.x * inv, v.y * inv};
+    }
+  }
+  dc u[NT], sv[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    dc v = rhs[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) v = dsub(v, dmul(Lm[i][k], u[k]));
+    u[i] = {v.x / ld[i], v.y / ld[i]};
+  }
+#pragma unroll
+  for (int i = NT - 1; i >= 0; --i) {
+    dc v = u[i];
+#pragma unroll
+    for (int k = i + 1; k < NT; ++k) v = dsub(v, dmulc(sv[k], Lm[k][i]));  // conj(L[k][i]) s[k]
+    sv[i] = {v.x / ld[i], v.y / ld[i]};
+  }
+  const uint32_t* fb = pw + (size_t)b * PW;
+  uint32_t errs = 0;
+  for (int t = 0; t < NT; ++t) {
+    const int qi = NT * j + t;
+    if (qi >= m.res) break;
+    const float2 z = make_float2((float)sv[t].x, (float)sv[t].y);
+    const int64_t re = (int64_t)l * m.res + qi;
+    if (cap_syms) cap_syms[(size_t)b * g.n_sym * m.res + re] = z;
+    const int idx = hard_index(z, BPS, (float)qam_norm<BPS>());
+#pragma unroll
+    for (int q = 0; q < BPS; ++q) {
+      const int64_t pbit = re * BPS + q;
+      if (pbit < n_bits) {
+        const uint32_t bit = (idx >> (BPS - 1 - q)) & 1;
+        errs += bit ^ getbit(fb, pbit);
+        if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
+      }
+    }
+  }
+  if (errs) atomicAdd(frame_err + b, errs);
+}
+
+int launch_det_mmse(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
+                    const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    float2* cap_syms, uint8_t* cap_bits) {
+  if (m.num_tx != 4 || m.num_rx != 4) return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * g.n_sym * m.n_dsc;
+  const dim3 grid((unsigned)((n + MWG - 1) / MWG));
+  if (g.bps == 2) hipLaunchKernelGGL(k_det_mmse<2>, grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits,
+                                     frame_err, cap_syms, cap_bits);
+  else if (g.bps == 4) hipLaunchKernelGGL(k_det_mmse<4>, grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW,
+                                          n_bits, frame_err, cap_syms, cap_bits);
+  else hipLaunchKernelGGL(k_det_mmse<6>, grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits, frame_err,
+                          cap_syms, cap_bits);
+  return (int)hipGetLastError();
+}
+
+}  // namespace lte

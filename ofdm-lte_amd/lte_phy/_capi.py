@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('LTE_HIP_LIB', os.path.join(_HERE, 'liblte_hip.so'))
 
 LTE_OK, LTE_EINVAL, LTE_EHIP, LTE_ENOMEM, LTE_ENODEV, LTE_EUNSUP = 0, -1, -2, -3, -4, -5
-CHAIN_UNCODED, CHAIN_CODED, CHAIN_SIMO = 0, 1, 2
+CHAIN_UNCODED, CHAIN_CODED, CHAIN_SIMO, CHAIN_SFBC, CHAIN_SFBC_CODED, CHAIN_SPATIAL = 0, 1, 2, 3, 4, 5
 CH_AWGN, CH_RAYLEIGH = 0, 1
 STAGE_TX, STAGE_CHANNEL, STAGE_RX, STAGE_ALL = 1, 2, 4, 7
 MAX_PATHS = 16
@@ -29,7 +29,8 @@ class PlanDesc(ctypes.Structure):
     _fields_ = [('N', c_i32), ('Nc', c_i32), ('cp_len', c_i32), ('bps', c_i32), ('n_sym', c_i32),
                 ('chain', c_i32), ('channel', c_i32), ('num_rx', c_i32), ('n_paths', c_i32),
                 ('delays', c_i32 * MAX_PATHS), ('gains', c_f64 * MAX_PATHS), ('fD', c_f64), ('fs', c_f64),
-                ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32)]
+                ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32),
+                ('num_tx', c_i32)]
 
 
 class RunArgs(ctypes.Structure):
@@ -44,7 +45,10 @@ class RunArgs(ctypes.Structure):
                 ('cap_data_syms', P(ctypes.c_float)), ('cap_H', P(ctypes.c_float)),
                 ('cap_pilot_stats', P(ctypes.c_float)), ('cap_bits_rx', P(ctypes.c_uint8)),
                 ('cap_llr', P(ctypes.c_float)), ('cap_noise_power', P(ctypes.c_float)),
-                ('cap_tx_syms', P(ctypes.c_float))]
+                ('cap_tx_syms', P(ctypes.c_float)),
+                ('link_noise', P(c_f64)), ('link_noise_stride', c_i64),
+                ('link_h', P(c_f64)), ('link_h_stride', c_i64),
+                ('cap_link_stats', P(ctypes.c_float))]
 
 
 # every symbol include/lte_phy.h declares, with its ctypes signature

@@ -17,7 +17,7 @@ from . import _capi as C
 
 class Plan:
     def __init__(self, *, N, Nc, cp_len, bps, n_sym, chain, channel, num_rx=1, delays=(), gains=(), fD=0.0,
-                 fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0):
+                 fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0, num_tx=1):
         C.device_init()
         d = C.PlanDesc()
         d.N, d.Nc, d.cp_len, d.bps, d.n_sym = N, Nc, cp_len, bps, n_sym
@@ -30,6 +30,7 @@ class Plan:
             d.gains[i] = float(g)
         d.fD, d.fs = float(fD), float(fs)
         d.n_bits, d.turbo_iters, d.max_frames, d.cell_id = int(n_bits), int(turbo_iters), int(max_frames), cell_id
+        d.num_tx = int(num_tx)
         self.desc = d
         h = ctypes.c_void_p()
         C.check(C.load().lte_plan_create(ctypes.byref(d), ctypes.byref(h)))
@@ -40,6 +41,15 @@ class Plan:
             (int(v) for v in info)
         self.num_rx, self.N, self.bps, self.n_bits, self.max_frames = num_rx, N, bps, int(n_bits), int(max_frames)
         self.chain = chain
+        self.num_tx = int(num_tx)
+        self.coded = chain in (C.CHAIN_CODED, C.CHAIN_SFBC_CODED)
+        self.mimo = chain >= C.CHAIN_SFBC
+        sfbc = chain in (C.CHAIN_SFBC, C.CHAIN_SFBC_CODED)
+        # multi-antenna geometry (lte_capi.hip lte_plan_create): REs per OFDM symbol,
+        # data SCs carrying data, channel estimates per frame
+        self.res = (self.Nd & ~1) if sfbc else self.Nd
+        self.n_dsc = self.res if sfbc else -(-self.Nd // max(1, self.num_tx))
+        self.n_est = self.n_grp if sfbc else self.n_sym
 
     def __del__(self):
         try:
@@ -52,7 +62,7 @@ class Plan:
     # ------------------------------------------------------------------
     def run(self, snr_db, *, snr_index=None, n_snr=1, seed=0, frame_ids=None, frame_id0=0, bits=None,
             bits_broadcast=False, phases=None, phases_broadcast=False, noise=None, noise_broadcast=False,
-            stages=C.STAGE_ALL, in_signal=None, capture=()):
+            stages=C.STAGE_ALL, in_signal=None, capture=(), link_noise=None, link_h=None, link_broadcast=False):
         snr = np.ascontiguousarray(np.atleast_1d(snr_db), dtype=np.float32)
         B = len(snr)
         a = C.RunArgs()
@@ -85,13 +95,23 @@ class Plan:
             keep.append(z)
             a.noise = C.ptr(z, C.F64)
             a.noise_stride = 0 if noise_broadcast else z.size // B
+        if link_noise is not None:
+            lz = np.ascontiguousarray(link_noise, dtype=np.float64)
+            keep.append(lz)
+            a.link_noise = C.ptr(lz, C.F64)
+            a.link_noise_stride = 0 if link_broadcast else lz.size // B
+        if link_h is not None:
+            lh = np.ascontiguousarray(link_h, dtype=np.float64)
+            keep.append(lh)
+            a.link_h = C.ptr(lh, C.F64)
+            a.link_h_stride = 0 if link_broadcast else lh.size // B
         counts = np.zeros((max(1, n_snr), 4), dtype=np.uint64)
         a.counts = C.ptr(counts, C.U64)
         out = {'counts': counts}
         ferr = np.zeros(B, dtype=np.uint32)
         a.frame_errors = C.ptr(ferr, C.U32)
         out['frame_errors'] = ferr
-        if self.chain == C.CHAIN_CODED:
+        if self.coded:
             crc = np.zeros(B, dtype=np.uint8)
             a.frame_crc_ok = C.ptr(crc, C.U8)
             out['crc_ok'] = crc
@@ -112,6 +132,14 @@ class Plan:
             'noise_power': ((B, self.num_rx), np.float32, 'cap_noise_power', C.F32),
             'tx_syms': ((B, self.n_sym * self.Nd), np.complex64, 'cap_tx_syms', C.F32),
         }
+        if self.mimo:
+            shapes.update({
+                'signal_tx': ((B, self.num_tx, self.L), np.complex64, 'cap_signal_tx', C.F32),
+                'data_syms': ((B, self.n_sym * self.res), np.complex64, 'cap_data_syms', C.F32),
+                'H': ((B, self.num_rx, self.n_est, self.num_tx, self.n_dsc), np.complex64, 'cap_H', C.F32),
+                'link_stats': ((B, self.num_rx, self.num_tx, 4), np.float32, 'cap_link_stats', C.F32)})
+            shapes.pop('pilot_stats')
+            shapes.pop('tx_syms')
         for name in capture:
             shp, dt, field, ct = shapes[name]
             arr = np.zeros(shp, dtype=dt)

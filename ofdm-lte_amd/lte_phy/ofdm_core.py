@@ -498,11 +498,92 @@ class OFDMSimulator:
         self.last_results = res
         return res
 
-    def simulate_miso(self, bits, snr_db=10.0):
-        raise NotImplementedError("SFBC Alamouti MISO/MIMO (config 4) is a later-round GPU path")
+    # -------------------------------------------------------------- SFBC (config 4)
+    def _sfbc_plan(self, n_sym, n_bits, num_rx, coded=False, max_frames=1, iters=8):
+        cfg, ch = self.config, self.channels[0]
+        return get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
+                        chain=C.CHAIN_SFBC_CODED if coded else C.CHAIN_SFBC, channel=ch.kind, num_rx=num_rx,
+                        num_tx=2, delays=tuple(ch.delays), gains=tuple(ch.gains), fD=ch.fD, fs=cfg.fs,
+                        n_bits=n_bits, turbo_iters=iters, max_frames=max_frames)
 
-    def simulate_mimo(self, bits, snr_db=10.0, num_rx=2):
-        raise NotImplementedError("SFBC Alamouti MISO/MIMO (config 4) is a later-round GPU path")
+    def _simulate_sfbc(self, bits, snr_db, num_rx, mode):
+        """simulate_miso (core/ofdm_core.py:1850-2047) / simulate_mimo (:2049-2258)
+        with the documented estimator fix (H0 = H[0,0,:],
+        H1 = H[0,1,:] of MIMOChannelEstimatorPeriodic.estimate_channel_from_grid;
+        the reference itself raises at core/mimo_channel_estimator_periodic.py:219).
+        One GPU call; the global RNG is consumed exactly as the reference would:
+        TX pilot reseeds (cells 0, 1 per OFDM symbol, core/sfbc_alamouti.py:248-256)
+        -> transmit_mimo (per RX, per TX link: 16 phases per path + the link's
+        100 dB noise; then the RX noise, core/ofdm_core.py:468-541) -> RX pilot
+        reseeds (per RX per slot)."""
+        bits = self._bits_in(bits)
+        if num_rx < 1:
+            raise ValueError("num_rx must be >= 1")
+        n0 = len(bits)
+        cfg, ch = self.config, self.channels[0]
+        res = self.Nd & ~1
+        n_sym = int(np.ceil(n0 / (res * cfg.bits_per_symbol)))
+        plan = self._sfbc_plan(n_sym, n0, num_rx)
+        L = plan.L
+        pil = self.grid._pilot
+        p0, p1 = len(pil[0::2]), len(pil[1::2])
+        _reseed_pilots(0, p0)
+        _reseed_pilots(1, p1)
+        ray = ch.kind == C.CH_RAYLEIGH
+        P = len(ch.delays)
+        ph = np.zeros((num_rx, 2, max(P, 1), 16))
+        lz = np.zeros((num_rx, 2, 2, L))
+        z = np.zeros((num_rx, 2, L))
+        for r in range(num_rx):
+            for t in range(2):
+                if ray:
+                    for p in range(P):
+                        ph[r, t, p] = 2 * np.pi * np.random.rand(16)
+                    lz[r, t, 0] = np.random.normal(0, 1.0, L)
+                    lz[r, t, 1] = np.random.normal(0, 1.0, L)
+            z[r, 0] = np.random.normal(0, 1.0, L)
+            z[r, 1] = np.random.normal(0, 1.0, L)
+        _reseed_pilots(0, p0)
+        _reseed_pilots(1, p1)
+        r = plan.run([snr_db], bits=(bits & 1).astype(np.uint8)[None], phases=ph[None] if ray else None,
+                     noise=z[None], link_noise=lz[None] if ray else None,
+                     capture=('signal_tx', 'bits_rx', 'data_syms', 'link_stats'))
+        brx = r['bits_rx'][0].astype(np.int64)
+        err = int(np.sum(bits != brx))
+        Hm = np.zeros((num_rx, 2), dtype=complex)
+        st = r['link_stats'][0].astype(np.float64)
+        for a in range(num_rx):
+            for t in range(2):
+                if not ray:
+                    Hm[a, t] = 1.0 + 0j if t == 0 else np.exp(1j * (t * np.pi / 2))
+                elif st[a, t, 0] > 1e-12:
+                    Hm[a, t] = np.sqrt(st[a, t, 1] / st[a, t, 0]) * np.exp(1j * np.angle(st[a, t, 2] + 1j * st[a, t, 3]))
+                else:
+                    Hm[a, t] = 1.0 + 0j
+        sig = r['signal_tx'][0].astype(np.complex128)
+        sl = cfg.N + cfg.cp_length
+        pap = []
+        for t in range(2):
+            syms = sig[t, :n_sym * sl].reshape(n_sym, sl)
+            pw_ = np.abs(syms) ** 2
+            pap.append(float(np.mean(10 * np.log10(np.max(pw_, axis=1) / np.mean(pw_, axis=1)))))
+        res_d = {'transmitted_bits': int(n0), 'received_bits': int(n0), 'bits_received_array': brx,
+                 'bit_errors': err, 'errors': err, 'ber': float(err / n0), 'snr_db': float(snr_db),
+                 'num_tx': 2, 'num_rx': num_rx, 'mode': mode, 'diversity_order': 2 * num_rx,
+                 'channel_matrix': Hm, 'papr_db_tx0': pap[0], 'papr_db_tx1': pap[1],
+                 'papr_db': float(np.mean([pap[0], pap[1]])),
+                 'papr_linear': 10 ** (np.mean([pap[0], pap[1]]) / 10),
+                 'symbols_rx': r['data_syms'][0].astype(np.complex128)}
+        self.last_results = res_d
+        return res_d
+
+    def simulate_miso(self, bits: np.ndarray, snr_db: float = 10.0) -> Dict:
+        """core/ofdm_core.py:1850-2047: 2 TX SFBC Alamouti, 1 RX (see _simulate_sfbc)."""
+        return self._simulate_sfbc(bits, snr_db, 1, 'MISO-SFBC')
+
+    def simulate_mimo(self, bits: np.ndarray, snr_db: float = 10.0, num_rx: int = 2) -> Dict:
+        """core/ofdm_core.py:2049-2258: 2 TX SFBC, num_rx RX, decodes averaged over RX."""
+        return self._simulate_sfbc(bits, snr_db, num_rx, 'MIMO-SFBC')
 
     # -------------------------------------------------------------- sweeps
     def run_ber_sweep(self, num_bits: int, snr_range, num_trials: int = 1,
@@ -539,16 +620,42 @@ class OFDMSimulator:
 
     def run_grid(self, snr_range, num_trials: int, seed: int = 0, coded: bool = False, num_rx: int = 1,
                  n_bits: Optional[int] = None, frames_per_call: int = 4096, rank: int = 0, world_size: int = 1,
-                 turbo_iters: int = 8) -> Dict:
+                 turbo_iters: int = 8, mimo: Optional[str] = None, velocity_kmh: float = 3,
+                 frequency_ghz: float = 2.0) -> Dict:
         """Device-resident Monte-Carlo BER/BLER grid (SNR x trials).  Frame
         (s, t) has global id s*num_trials + t; all randomness is Philox keyed by
         (seed, id), so results are identical for any sharding.  With
         world_size > 1 this process handles trials t = rank, rank+W, ... and
-        the caller all-reduces the returned `counts`."""
+        the caller all-reduces the returned `counts`.
+
+        mimo=None: SISO (coded: config 2) / SIMO MRC (num_rx > 1: config 3);
+        mimo='sfbc': 2 x num_rx Alamouti (coded: config 4);
+        mimo='spatial': 4x4 rank-4 MMSE (config 5; the spatial channel of
+        simulate_spatial_multiplexing: gains converted once more, fD from
+        velocity_kmh / frequency_ghz)."""
         snrs = np.atleast_1d(np.asarray(snr_range, dtype=np.float64))
         S, T = len(snrs), int(num_trials)
         cfg = self.config
-        if coded:
+        if mimo == 'sfbc':
+            res = self.Nd & ~1
+            if coded:
+                nb = int(n_bits or 27760)
+                plan = self._sfbc_plan(0, nb, num_rx, coded=True, max_frames=frames_per_call, iters=turbo_iters)
+            else:
+                nb = int(n_bits or SLOT_SIZE * res * cfg.bits_per_symbol)
+                plan = self._sfbc_plan(int(np.ceil(nb / (res * cfg.bits_per_symbol))), nb, num_rx,
+                                       max_frames=frames_per_call)
+        elif mimo == 'spatial':
+            if coded:
+                raise NotImplementedError("config 5 is uncoded MMSE detection")
+            nb = int(n_bits or SLOT_SIZE * self.Nd * cfg.bits_per_symbol)
+            ch = self.channels[0]
+            ctype = 'rayleigh_mp' if ch.kind == C.CH_RAYLEIGH else 'awgn'
+            plan = _spatial_plan(cfg, ctype, ch.profile, velocity_kmh, frequency_ghz,
+                                 int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol))), nb, frames_per_call)[0]
+        elif mimo is not None:
+            raise ValueError(f"unknown mimo mode {mimo!r}")
+        elif coded:
             nb = int(n_bits or 27760)
             plan = self._plan(C.CHAIN_CODED, 0, nb, max_frames=frames_per_call, iters=turbo_iters)
         else:
@@ -570,6 +677,102 @@ class OFDMSimulator:
                 'bits': counts[:, 1], 'block_errors': counts[:, 2], 'blocks': counts[:, 3], 'plan': plan}
 
 
-def simulate_spatial_multiplexing(*args, **kwargs):
-    """core/ofdm_core.py:2489-2815 (4x4 MMSE, config 5): later-round GPU path."""
-    raise NotImplementedError("spatial multiplexing (config 5) is a later-round GPU path")
+def _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n_bits, max_frames=1):
+    ch = {'awgn': C.CH_AWGN, 'rayleigh_mp': C.CH_RAYLEIGH}.get(channel_type)
+    if ch is None:
+        raise ValueError(f"Tipo de canal desconocido: {channel_type}")
+    if ch == C.CH_RAYLEIGH:
+        # transmit_spatial_multiplexing re-wraps the already-converted gains once
+        # more (core/channel.py:435-444, Q2); fD from velocity and carrier (:113-143)
+        delays, gains = itu_paths(itu_profile, config.fs, spatial=True)
+        fD = doppler(frequency_ghz, velocity_kmh, itu_profile)
+    else:
+        delays, gains, fD = [], [], 0.0
+    return get_plan(N=config.N, Nc=config.Nc, cp_len=config.cp_length, bps=config.bits_per_symbol, n_sym=n_sym,
+                    chain=C.CHAIN_SPATIAL, channel=ch, num_rx=4, num_tx=4, delays=tuple(delays),
+                    gains=tuple(gains), fD=fD, fs=config.fs, n_bits=n_bits, max_frames=max_frames), gains, fD
+
+
+def simulate_spatial_multiplexing(bits, num_tx=4, num_rx=2, rank='adaptive', detector_type='MMSE',
+                                  modulation='64-QAM', snr_db=15, config=None, channel_type='awgn',
+                                  itu_profile='Pedestrian_A', velocity_kmh=3, frequency_ghz=2.0,
+                                  enable_csi_feedback=True, coherence_time_symbols=None, enable_parallel=False,
+                                  codebook_type='TM4'):
+    """simulate_spatial_multiplexing (core/ofdm_core.py:2489-2815), config 5:
+    TM4 4x4, rank 4, PMI 0 (W = I4), CRS estimation on every OFDM symbol, MMSE
+    with the nominal sigma^2 = 10^(-SNR/10), layer demapping, hard decisions --
+    one GPU call.  Global-RNG consumption as the reference: H_initial (:2581,
+    drawn even at fixed rank) -> TX pilot reseeds per symbol and TX (cell
+    tx % 4) -> transmit_spatial_multiplexing draws (core/channel.py:397-493:
+    rayleigh_mp per link 16 phases per path for filter() and 16 per path for
+    impulse_response(); 'awgn' per link h ~ CN(0,1); then noise per RX) -> RX
+    pilot reseeds.  Rank adaptation, PMI search and the ZF / SIC / MRC
+    detectors are SURVEY §8f "next" and raise NotImplementedError."""
+    bits = np.asarray(bits)
+    if bits.size == 0:
+        raise ValueError("Bits array cannot be empty")
+    if str(detector_type).upper() not in ('MMSE', 'IRC'):
+        raise NotImplementedError(f"detector '{detector_type}': only MMSE/IRC is on the GPU path (SURVEY §8f)")
+    rank_used = min(num_tx, num_rx) if rank == 'adaptive' and not enable_csi_feedback else rank
+    if rank == 'adaptive' and enable_csi_feedback:
+        raise NotImplementedError("rank adaptation / CSI feedback (core/rank_adaptation.py) is SURVEY §8f 'next'; "
+                                  "pass rank=4 or enable_csi_feedback=False")
+    if num_tx != 4 or num_rx != 4 or int(rank_used) != 4:
+        raise NotImplementedError("spatial multiplexing on the GPU path: 4x4, rank 4 (TM4 PMI 0)")
+    if num_rx < int(rank_used):
+        raise ValueError(f"num_rx ({num_rx}) debe ser >= num_layers ({rank_used})")
+    if config is None:
+        config = LTEConfig(modulation=modulation)
+    n0 = len(bits)
+    grid = ResourceGrid(config.N, config.Nc)
+    Nd = len(grid._data)
+    bpo = Nd * config.bits_per_symbol
+    n_sym = int(np.ceil(n0 / bpo))
+    plan, gains, fD = _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n0)
+    L = plan.L
+    ray = channel_type == 'rayleigh_mp'
+    np.random.randn(num_rx, num_tx)                  # H_initial (core/ofdm_core.py:2581)
+    np.random.randn(num_rx, num_tx)
+    pidx = [grid._pilot[t::4] for t in range(num_tx)]
+    for t in range(num_tx):
+        _reseed_pilots(t % 4, len(pidx[t]))
+    P = len(plan.desc.delays[:plan.desc.n_paths]) if ray else 0
+    ph = np.zeros((num_rx, num_tx, max(P, 1), 16))
+    ir = np.zeros((num_rx, num_tx, max(P, 1), 16))
+    lh = np.zeros((num_rx, num_tx, 2))
+    for r in range(num_rx):
+        for t in range(num_tx):
+            if ray:
+                for p in range(P):
+                    ph[r, t, p] = 2 * np.pi * np.random.rand(16)
+                for p in range(P):
+                    ir[r, t, p] = 2 * np.pi * np.random.rand(16)
+            else:
+                lh[r, t, 0] = np.random.normal(0, 1 / np.sqrt(2))
+                lh[r, t, 1] = np.random.normal(0, 1 / np.sqrt(2))
+    z = np.zeros((num_rx, 2, L))
+    for r in range(num_rx):
+        z[r, 0] = np.random.normal(0, 1.0, L)
+        z[r, 1] = np.random.normal(0, 1.0, L)
+    for t in range(num_tx):
+        _reseed_pilots(t % 4, len(pidx[t]))
+    out = plan.run([snr_db], bits=(bits & 1).astype(np.uint8)[None], phases=ph[None] if ray else None,
+                   noise=z[None], link_h=None if ray else lh[None], capture=('bits_rx', 'data_syms'))
+    brx = out['bits_rx'][0].astype(np.int64)
+    err = int(np.sum(bits != brx))
+    Hm = np.zeros((num_rx, num_tx), dtype=complex)
+    for r in range(num_rx):
+        for t in range(num_tx):
+            if ray:   # RayleighChannel.impulse_response(N=1) first tap (core/rayleighchannel.py:99-113)
+                h = np.zeros(1, dtype=complex)
+                for m in range(16):
+                    h += np.exp(1j * (2 * np.pi * fD * np.cos(2 * np.pi * (m + 1) / 16) * np.zeros(1) + ir[r, t, 0, m]))
+                Hm[r, t] = gains[0] * (h * np.sqrt(2 / 16))[0]
+            else:
+                Hm[r, t] = lh[r, t, 0] + 1j * lh[r, t, 1]
+    return {'transmitted_bits': int(n0), 'received_bits': int(n0), 'bits_received_array': brx,
+            'bit_errors': err, 'errors': err, 'ber': float(err / n0), 'snr_db': float(snr_db),
+            'num_tx': num_tx, 'num_rx': num_rx, 'rank': int(rank_used), 'detector_type': detector_type,
+            'mode': 'Spatial Multiplexing TM4', 'codebook_type': codebook_type, 'channel_matrix': Hm,
+            'precoder_matrix': np.eye(4, dtype=complex), 'pmi_used': 0, 'velocity_kmh': velocity_kmh,
+            'modulation': modulation, 'symbols_rx': out['data_syms'][0].astype(np.complex128)}

@@ -1,0 +1,159 @@
+"""GPU parity of the multi-antenna chains (SURVEY §8 a12, a13, a33-a37;
+configs 4 and 5) against the reference's own outputs (tests/golden/
+golden_mimo.npz, frozen global RNG) and the oracle (oracle/mimo_oracle.py).
+
+Bars: BER |dBER| < 1e-3 absolute vs the reference (north_star tolerance);
+identical global-RNG side effects; channel matrices to float32 precision;
+coded SFBC: in-chain LLRs vs the oracle's max-log demapper (1e-4 relative) and
+decoding bit-exact vs the decoder's float32 model."""
+import numpy as np
+import pytest
+
+from conftest import unpack
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def C():
+    from lte_phy import _capi
+    _capi.device_init(0)
+    return _capi
+
+
+def _state():
+    return np.array(np.random.get_state()[1][:8], dtype=np.uint32)
+
+
+def _sim(bw, mod, chan):
+    import lte_phy
+    return lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type=chan)
+
+
+@pytest.mark.parametrize('name,bw,mod,chan,snrs,nrx', [
+    ('sfbc_c1', 1.25, 'QPSK', 'awgn', [4], 2),
+    ('sfbc_c1miso', 1.25, 'QPSK', 'rayleigh_mp', [10], 1),
+    ('sfbc_c4', 20.0, '64-QAM', 'rayleigh_mp', [10, 20, 30], 2)])
+def test_sfbc_ref_compat(C, golden_mimo, name, bw, mod, chan, snrs, nrx):
+    """simulate_miso / simulate_mimo (with the Q19 estimator fix) == the fixed
+    reference: bit errors, global RNG state, channel matrix, per-TX PAPR."""
+    sim = _sim(bw, mod, chan)
+    nb = int(golden_mimo[name + '_nbits'][0])
+    bits = unpack(golden_mimo[name + '_bits'], nb).astype(np.int64)
+    for snr in snrs:
+        k = f'{name}_snr{snr}'
+        r = sim.simulate_miso(bits, snr) if nrx == 1 else sim.simulate_mimo(bits, snr, num_rx=nrx)
+        ref_err = int(golden_mimo[k + '_errors'][0])
+        assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
+        assert np.mean(r['bits_received_array'] != unpack(golden_mimo[k + '_rx'], nb)) < 1e-3
+        assert np.array_equal(_state(), golden_mimo[k + '_state'])
+        H = golden_mimo[k + '_H']
+        assert np.max(np.abs(r['channel_matrix'] - H)) < 1e-4 * (1 + np.max(np.abs(H))), k
+        p = golden_mimo[k + '_papr']
+        assert np.allclose([r['papr_db_tx0'], r['papr_db_tx1'], r['papr_db']], p, atol=1e-3), k
+
+
+@pytest.mark.parametrize('name,bw,mod,chan,snrs', [
+    ('sm_c1', 1.25, 'QPSK', 'awgn', [15]),
+    ('sm_c5awgn', 20.0, '64-QAM', 'awgn', [25]),
+    ('sm_c5ray', 20.0, '64-QAM', 'rayleigh_mp', [25, 35])])
+def test_spatial_ref_compat(C, golden_mimo, name, bw, mod, chan, snrs):
+    """simulate_spatial_multiplexing 4x4 rank 4 MMSE == the reference."""
+    import lte_phy
+    nb = int(golden_mimo[name + '_nbits'][0])
+    bits = unpack(golden_mimo[name + '_bits'], nb).astype(np.int64)
+    for snr in snrs:
+        k = f'{name}_snr{snr}'
+        c = lte_phy.LTEConfig(bandwidth=bw, modulation=mod)
+        r = lte_phy.simulate_spatial_multiplexing(bits, num_tx=4, num_rx=4, rank=4, detector_type='MMSE',
+                                                  modulation=mod, snr_db=snr, config=c, channel_type=chan,
+                                                  itu_profile='Pedestrian_A', velocity_kmh=3,
+                                                  enable_csi_feedback=False)
+        ref_err = int(golden_mimo[k + '_errors'][0])
+        assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
+        assert np.mean(r['bits_received_array'] != unpack(golden_mimo[k + '_rx'], nb)) < 1e-3
+        assert np.array_equal(_state(), golden_mimo[k + '_state'])
+        assert np.array_equal(r['channel_matrix'], golden_mimo[k + '_H'])
+        assert np.array_equal(r['precoder_matrix'], golden_mimo[k + '_W'])
+
+
+def test_spatial_vs_oracle_awgn_high_snr(C, oracle, mimo_oracle):
+    """Config 5 at 40 dB, flat channel: GPU and oracle decode the same bits."""
+    import lte_phy
+    num = oracle.Numerology(bandwidth=5.0, modulation='16-QAM')
+    bits = np.random.RandomState(4).randint(0, 2, 14 * num.Nd * 4)
+    np.random.seed(17)
+    o = mimo_oracle.simulate_spatial(num, bits, 40.0, channel='awgn')
+    np.random.seed(17)
+    r = lte_phy.simulate_spatial_multiplexing(bits, num_tx=4, num_rx=4, rank=4, modulation='16-QAM', snr_db=40,
+                                              config=lte_phy.LTEConfig(bandwidth=5.0, modulation='16-QAM'),
+                                              channel_type='awgn', enable_csi_feedback=False)
+    assert abs(r['bit_errors'] - o['bit_errors']) / len(bits) < 1e-3
+    assert np.array_equal(r['channel_matrix'], o['channel_matrix'])
+
+
+@pytest.mark.parametrize('chan', ['awgn', 'rayleigh_mp'])
+def test_sfbc_coded_llrs_and_decoding(C, oracle, chan):
+    """Config 4 chain on Philox frames: the LLRs k_det_sfbc writes equal the
+    oracle's max-log LLRs of the same combined symbols with the documented
+    noise-variance rule, and the GPU decoder's output equals the float32
+    decoder model run on those LLRs (T/F de-interleave with cols = Nd & ~1,
+    rate dematch, turbo, CRC)."""
+    sim = _sim(20.0, '64-QAM', chan)
+    plan = sim._sfbc_plan(0, 27760, 2, coded=True, max_frames=4)
+    snrs = np.array([8.0, 14.0, 20.0, 30.0])
+    r = plan.run(snrs, seed=9, capture=('llr', 'data_syms', 'H', 'bits_rx'))
+    num = oracle.Numerology(bandwidth=20.0, modulation='64-QAM')
+    res, bps = plan.res, 6
+    d = num.data_idx[:res]
+    tb = np.zeros(27760, dtype=np.uint8)
+    _, seg_plan = oracle.segment(oracle.attach_crc24a(tb))
+    rm = [3 * p[0] + 12 for p in seg_plan]
+    coded = plan.coded_bits
+    ncs = coded // bps
+    rows = -(-ncs // res)
+    q = np.arange(ncs)
+    src = (q % res) * rows + q // res
+    for b, snr in enumerate(snrs):
+        z = r['data_syms'][b].astype(np.complex128)
+        H = r['H'][b].astype(np.complex128)
+        s2 = 10 ** (-snr / 10)
+        nv = np.zeros(len(z))
+        for l in range(plan.n_sym):
+            e = l // 14
+            inv_g = np.zeros(res // 2)
+            for a in range(2):
+                h0, h1 = H[a, e, 0], H[a, e, 1]
+                nrm = np.abs((h0[0::2] + h0[1::2]) / 2) ** 2 + np.abs((h1[0::2] + h1[1::2]) / 2) ** 2 + 1e-10
+                inv_g += 1.0 / np.clip(nrm, 1e-6, 1e6)
+            v = np.maximum(s2 / 4.0 * inv_g, s2 / 4.0)   # s2 / R^2 * sum 1/norm, R = 2
+            nv[l * res:(l + 1) * res] = np.repeat(v, 2)
+        ref = oracle.llrs(z, nv, '64-QAM')
+        got = r['llr'][b].astype(np.float64)[:len(ref)]
+        assert np.max(np.abs(got - ref) / (1 + np.abs(ref))) < 1e-4, (chan, snr)
+        L = got.reshape(-1, bps)[src].reshape(-1)[:coded]
+        dec, ok = oracle.coded_rx_decode(L, seg_plan, rm, 8, f32_model=True)
+        assert np.array_equal(dec, r['bits_rx'][b]) and bool(ok) == bool(r['crc_ok'][b]), (chan, snr)
+    if chan == 'awgn':
+        assert r['crc_ok'][-1] == 1 and r['frame_errors'][-1] == 0
+
+
+@pytest.mark.parametrize('mimo,coded,chan', [('sfbc', True, 'rayleigh_mp'), ('spatial', False, 'rayleigh_mp'),
+                                            ('spatial', False, 'awgn')])
+def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan):
+    sim = _sim(20.0, '64-QAM', chan)
+    kw = dict(mimo=mimo, coded=coded, num_rx=2 if mimo == 'sfbc' else 4)
+    a = sim.run_grid([10.0, 25.0], 24, seed=5, **kw)
+    b0 = sim.run_grid([10.0, 25.0], 24, seed=5, rank=0, world_size=2, **kw)
+    b1 = sim.run_grid([10.0, 25.0], 24, seed=5, rank=1, world_size=2, **kw)
+    assert np.array_equal(a['counts'], b0['counts'] + b1['counts'])
+    assert a['ber'][1] <= a['ber'][0] + 1e-12
+
+
+def test_mimo_argument_errors(C):
+    import lte_phy
+    sim = _sim(1.25, 'QPSK', 'awgn')
+    with pytest.raises(ValueError):
+        sim.simulate_mimo(np.array([], dtype=int), 10.0)
+    with pytest.raises(NotImplementedError):
+        lte_phy.simulate_spatial_multiplexing(np.ones(100, dtype=int), num_tx=4, num_rx=2, rank='adaptive')

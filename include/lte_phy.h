@@ -172,6 +172,22 @@ int lte_crc_host(int64_t n, const uint8_t *bits, uint32_t poly, int len, uint32_
 int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int32_t *delays, const double *gains,
                      double fD, double fs, double snr_db, uint64_t seed, const float *x, const double *phases,
                      const double *noise, float *y, float *noise_power);
+/* Multi-antenna channel on arbitrary streams.
+ * mode 0: OFDMChannel.transmit_mimo (core/ofdm_core.py:434-543) -- AWGN links
+ *   h = exp(j tx pi/2); Rayleigh links each a 100 dB ChannelSimulator (fading +
+ *   link noise); RX noise (P_rx / num_tx) / SNR.
+ * mode 1: ChannelSimulator.transmit_spatial_multiplexing (core/channel.py:
+ *   397-493) -- AWGN links h ~ CN(0,1) (link_h); Rayleigh links with the given
+ *   gains and fD (time-varying Jakes); RX noise P_rx / SNR.
+ * x [num_tx][L] complex64 -> y [num_rx][L] complex64; link_stats (optional)
+ * [num_rx][num_tx][4] = mean|x|^2, mean|y_link|^2, Re / Im mean(y_link conj(x)).
+ * phases [num_rx][num_tx][n_paths][16], link_noise [num_rx][num_tx][2][L],
+ * link_h [num_rx][num_tx][2], noise [num_rx][2][L]: NULL -> Philox(seed). */
+int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,
+                          const int32_t *delays, const double *gains, double fD, double fs, double snr_db,
+                          uint64_t seed, const float *x, const double *phases, const double *link_noise,
+                          const double *link_h, const double *noise, float *y, float *link_stats,
+                          float *noise_power);
 /* Rate dematching map: rate_dematching_turbo core/channel_coding/rate_matching.py:374-489
  * src[j] = index into the E rate-matched LLRs feeding output j of [3K+12], -1 = zero. */
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t *src);

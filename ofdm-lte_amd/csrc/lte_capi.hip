@@ -502,6 +502,93 @@ int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int3
   return rc;
 }
 
+int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,
+                          const int32_t* delays, const double* gains, double fD, double fs, double snr_db,
+                          uint64_t seed, const float* x, const double* phases, const double* link_noise,
+                          const double* link_h, const double* noise, float* y, float* link_stats,
+                          float* noise_power) {
+  if (L < 1 || L > (1LL << 28) || num_tx < 1 || num_tx > 8 || num_rx < 1 || num_rx > 16 || !x || !y)
+    return fail(LTE_EINVAL, "bad channel arguments");
+  if (mode != 0 && mode != 1) return fail(LTE_EINVAL, "mode must be 0 (transmit_mimo) or 1 (spatial)");
+  const bool ray = channel == LTE_CH_RAYLEIGH;
+  if (!ray && channel != LTE_CH_AWGN) return fail(LTE_EINVAL, "Tipo de canal desconocido");
+  if (ray && (n_paths < 1 || n_paths > LTE_MAX_PATHS || !delays || !gains)) return fail(LTE_EINVAL, "bad paths");
+  // an arbitrary stream is cut into 1024-sample chunks for the fD != 0 expansion
+  const int chunk = 1024;
+  Grid g{};
+  g.N = chunk;
+  g.cp = 0;
+  g.L = (int)L;
+  MimoGrid m{};
+  m.mode = mode == 0 ? MIMO_SFBC : MIMO_SPATIAL;
+  m.num_tx = num_tx;
+  m.num_rx = num_rx;
+  m.n_cs = (ray && fD != 0.0) ? (int)((L + chunk - 1) / chunk) : 1;
+  const int np = ray ? n_paths : 1;
+  const int nblk = (int)((L + 255) / 256);
+  const size_t links = (size_t)num_rx * num_tx;
+  const bool link_noise_on = mode == 0 && ray;
+  DBuf<float2> dx, dy, dcoef, dout;
+  DBuf<float> dgain, dph, dlz, dlh, dz, dpp, dlp, dls, dsl, dnp, dstp, dst;
+  DBuf<int32_t> ddel;
+  DBuf<uint64_t> dfid;
+  auto cleanup = [&]() {
+    dx.release(); dy.release(); dcoef.release(); dout.release(); dgain.release(); dph.release(); dlz.release();
+    dlh.release(); dz.release(); dpp.release(); dlp.release(); dls.release(); dsl.release(); dnp.release();
+    dstp.release(); dst.release(); ddel.release(); dfid.release();
+  };
+  if (dx.alloc((size_t)num_tx * L) || dy.alloc((size_t)num_rx * L) || dout.alloc((size_t)num_rx * L) ||
+      dcoef.alloc(links * np * m.n_cs * 3) || dpp.alloc((size_t)num_rx * nblk) || dsl.alloc(1) ||
+      dnp.alloc(num_rx) || dfid.alloc(1) ||
+      (link_noise_on && (dlp.alloc(links * nblk) || dls.alloc(links)))) {
+    cleanup();
+    return fail(LTE_ENOMEM, "channel buffers");
+  }
+  auto up = [&](DBuf<float>& d, const double* src, size_t n) {
+    std::vector<float> h(src, src + n);
+    return upload(d, h) == 0;
+  };
+  const float sl = (float)std::pow(10.0, snr_db / 10.0);
+  const uint64_t fid0 = 0;
+  bool ok = hipMemcpy(dx.p, x, (size_t)num_tx * L * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dsl.p, &sl, 4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dfid.p, &fid0, 8, hipMemcpyHostToDevice) == hipSuccess;
+  if (ok && ray) {
+    std::vector<int32_t> dl(delays, delays + n_paths);
+    ok = upload(ddel, dl) == 0 && up(dgain, gains, n_paths);
+  }
+  if (ok && ray && phases) ok = up(dph, phases, links * n_paths * 16);
+  if (ok && link_noise_on && link_noise) ok = up(dlz, link_noise, links * 2 * L);
+  if (ok && !ray && mode == 1 && link_h) ok = up(dlh, link_h, links * 2);
+  if (ok && noise) ok = up(dz, noise, (size_t)num_rx * 2 * L);
+  ok = ok && launch_fading_mimo(nullptr, g, m, 1, ray ? 1 : 0, n_paths, dgain.p, fD, fs, dfid.p, seed,
+                                (ray && phases) ? dph.p : nullptr, 0, (!ray && mode == 1 && link_h) ? dlh.p : nullptr,
+                                0, dcoef.p) == 0;
+  ok = ok && launch_channel_mimo(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dx.p, dy.p,
+                                 link_noise_on ? 1 : 0, dfid.p, seed, (link_noise_on && link_noise) ? dlz.p : nullptr,
+                                 0, dlp.p, dls.p, dpp.p, nblk) == 0;
+  ok = ok && launch_npow_mimo(nullptr, 1, num_rx, dpp.p, nblk, (int)L, dsl.p, mode == 0 ? 1.0f / num_tx : 1.0f,
+                              dnp.p) == 0;
+  if (ok) {
+    hipLaunchKernelGGL(k_cap_rx, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
+                       dy.p, (int64_t)L, (int64_t)num_rx * L, dnp.p, dfid.p, seed, noise ? dz.p : nullptr, 0,
+                       dout.p);
+    ok = hipGetLastError() == hipSuccess;
+  }
+  if (ok && link_stats) {
+    ok = dstp.alloc(links * 4 * nblk) == 0 && dst.alloc(links * 4) == 0 &&
+         launch_link_stats(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dx.p, dstp.p, nblk, dst.p) == 0;
+  }
+  ok = ok && hipDeviceSynchronize() == hipSuccess &&
+       hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(float2), hipMemcpyDeviceToHost) == hipSuccess &&
+       (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess) &&
+       (!link_stats || hipMemcpy(link_stats, dst.p, links * 4 * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess);
+  int rc = LTE_OK;
+  if (!ok) rc = fail(LTE_EHIP, std::string("mimo channel failed: ") + hipGetErrorString(hipGetLastError()));
+  cleanup();
+  return rc;
+}
+
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t* src) {
   int f1, f2;
   if (!qpp_lookup(K, &f1, &f2)) return fail(LTE_EINVAL, "Invalid interleaver size K=" + std::to_string(K));

@@ -7,12 +7,12 @@ decoder run as hand-written gfx950 HIP kernels in liblte_hip.so.
 """
 from .config import (CP_VALUES, ITU_CHANNEL_MODELS, LTE_PROFILES, MODULATION_SCHEMES, SUBCARRIER_SPACING,
                      LTEConfig)
-from .ofdm_core import (OFDMChannel, OFDMReceiver, OFDMSimulator, OFDMTransmitter,
+from .ofdm_core import (ChannelSimulator, OFDMChannel, OFDMReceiver, OFDMSimulator, OFDMTransmitter,
                         simulate_spatial_multiplexing)
 from .ofdm_module import OFDMModule
 from . import channel_coding
 
 __version__ = '0.1.0'
 __all__ = ['LTEConfig', 'OFDMModule', 'OFDMSimulator', 'OFDMTransmitter', 'OFDMReceiver', 'OFDMChannel',
-           'simulate_spatial_multiplexing', 'channel_coding', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
+           'ChannelSimulator', 'simulate_spatial_multiplexing', 'channel_coding', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
            'LTE_PROFILES', 'CP_VALUES', 'SUBCARRIER_SPACING']

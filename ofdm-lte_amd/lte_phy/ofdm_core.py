@@ -248,6 +248,25 @@ class OFDMReceiver:
 
 
 # ------------------------------------------------------------------ channel
+def _link_matrix(st, rayleigh):
+    """channel_matrix of transmit_mimo (core/ofdm_core.py:476-518) from the
+    per-link statistics [rx][tx][mean|x|^2, mean|y|^2, Re, Im mean(y x*)]:
+    AWGN h = exp(j tx pi/2); Rayleigh sqrt(P_y / P_x) exp(j angle(mean(y x*)))
+    (h = 1 if P_x <= 1e-12)."""
+    st = np.asarray(st, dtype=np.float64)
+    num_rx, num_tx = st.shape[:2]
+    Hm = np.zeros((num_rx, num_tx), dtype=complex)
+    for a in range(num_rx):
+        for t in range(num_tx):
+            if not rayleigh:
+                Hm[a, t] = 1.0 + 0j if t == 0 else np.exp(1j * (t * np.pi / 2))
+            elif st[a, t, 0] > 1e-12:
+                Hm[a, t] = np.sqrt(st[a, t, 1] / st[a, t, 0]) * np.exp(1j * np.angle(st[a, t, 2] + 1j * st[a, t, 3]))
+            else:
+                Hm[a, t] = 1.0 + 0j
+    return Hm
+
+
 class OFDMChannel:
     """OFDMChannel (core/ofdm_core.py:279-557).  Any channel_type other than
     'rayleigh_mp' is AWGN, as in the reference (:322-332)."""
@@ -314,7 +333,47 @@ class OFDMChannel:
         return list(self._apply(signal_tx, num_rx))
 
     def transmit_mimo(self, signals_tx, num_rx: int = 1):
-        raise NotImplementedError("MIMO links (core/ofdm_core.py:434-543) are a later-round GPU path")
+        """OFDMChannel.transmit_mimo (core/ofdm_core.py:434-543) on the device
+        (lte_channel_mimo_host).  AWGN links h = exp(j tx pi/2); Rayleigh links
+        are each a 100 dB ChannelSimulator (fading + link noise); RX noise
+        (P_rx / num_tx) / SNR.  The global RNG is consumed in the reference's
+        order (per RX: per TX link [16 phases per path, link noise re, im],
+        then the RX noise).  Returns (signals_rx list, channel_matrix
+        [num_rx][num_tx]), the matrix by the reference's power-ratio /
+        correlation-phase rule."""
+        num_tx = len(signals_tx)
+        if num_tx == 0:
+            raise ValueError("No transmitted signals provided")
+        L = len(signals_tx[0])
+        for t, sg in enumerate(signals_tx):
+            if len(sg) != L:
+                raise ValueError(f"TX signal {t} length mismatch")
+        C.device_init()
+        x = np.ascontiguousarray(np.stack([np.asarray(sg) for sg in signals_tx]), dtype=np.complex64)
+        P = len(self.delays)
+        ph = np.zeros((num_rx, num_tx, max(P, 1), 16))
+        lz = np.zeros((num_rx, num_tx, 2, L))
+        z = np.zeros((num_rx, 2, L))
+        for r in range(num_rx):
+            for t in range(num_tx):
+                if self.rayleigh:
+                    for p in range(P):
+                        ph[r, t, p] = 2 * np.pi * np.random.rand(16)
+                    lz[r, t, 0] = np.random.normal(0, 1.0, L)
+                    lz[r, t, 1] = np.random.normal(0, 1.0, L)
+            z[r, 0] = np.random.normal(0, 1.0, L)
+            z[r, 1] = np.random.normal(0, 1.0, L)
+        y = np.zeros((num_rx, L), dtype=np.complex64)
+        st = np.zeros((num_rx, num_tx, 4), dtype=np.float32)
+        dl = np.array(self.delays, dtype=np.int32)
+        g = np.array(self.gains, dtype=np.float64)
+        ray = self.rayleigh
+        C.check(C.load().lte_channel_mimo_host(
+            L, num_tx, num_rx, 0, self.kind, P, C.ptr(dl, C.I32) if P else None, C.ptr(g, C.F64) if P else None,
+            float(self.fD), float(self.fs or 0.0), float(self.snr_db), 0, C.ptr(x.view(np.float32), C.F32),
+            C.ptr(ph, C.F64) if ray else None, C.ptr(lz, C.F64) if ray else None, None, C.ptr(z, C.F64),
+            C.ptr(y.view(np.float32), C.F32), C.ptr(st, C.F32) if ray else None, None))
+        return list(y.astype(np.complex128)), _link_matrix(st, ray)
 
     def get_config(self) -> Dict:
         return {'type': self.channel_type, 'snr_db': self.snr_db, 'fs': self.fs, 'profile': self.profile,
@@ -322,6 +381,83 @@ class OFDMChannel:
 
     def __repr__(self):
         return f"OFDMChannel({self.channel_type}, SNR={self.snr_db}dB, {self.profile})"
+
+
+
+class ChannelSimulator:
+    """ChannelSimulator (core/channel.py:297-493): 'awgn' and 'rayleigh_mp'
+    ('fading', FadingChannel, is outside the GPU path: NotImplementedError).
+    The fD rule and gain conversions are the reference's (doppler(), Q2)."""
+
+    def __init__(self, channel_type='awgn', snr_db=10.0, fs=None, itu_profile='Vehicular_A', frequency_ghz=None,
+                 velocity_kmh=None, verbose=True):
+        if channel_type == 'fading':
+            raise NotImplementedError("FadingChannel is outside the GPU path (SURVEY §8)")
+        if channel_type not in ('awgn', 'rayleigh_mp'):
+            raise ValueError(f"Tipo de canal desconocido: {channel_type}")
+        self.channel_type, self.fs, self.itu_profile = channel_type, fs, itu_profile
+        self.frequency_ghz, self.velocity_kmh = frequency_ghz, velocity_kmh
+        self._ch = OFDMChannel(channel_type, snr_db, fs, itu_profile, frequency_ghz, velocity_kmh)
+
+    @property
+    def snr_db(self):
+        return self._ch.snr_db
+
+    def set_snr(self, snr_db):
+        self._ch.set_snr(snr_db)
+
+    def transmit(self, signal):
+        """core/channel.py:334-345."""
+        return self._ch.transmit(signal)
+
+    def transmit_spatial_multiplexing(self, tx_signals, num_rx=2):
+        """core/channel.py:397-493 on the device (lte_channel_mimo_host mode 1).
+        Streams are cut to the shortest.  rayleigh_mp: each link an independent
+        RayleighChannel with the gains converted a third time (Q2) and this
+        simulator's fD; H[rx, tx] = first tap of the link's impulse_response
+        (its own 16 phases per path, drawn after the filter's).  awgn: h ~
+        CN(0, 1) per link.  Noise per RX: P_rx / SNR.  Global RNG consumed in the
+        reference's order."""
+        num_tx = len(tx_signals)
+        L = min(len(sg) for sg in tx_signals)
+        ch = self._ch
+        ray = ch.rayleigh
+        C.device_init()
+        x = np.ascontiguousarray(np.stack([np.asarray(sg)[:L] for sg in tx_signals]), dtype=np.complex64)
+        if ray:
+            delays, gains = itu_paths(self.itu_profile, self.fs, spatial=True)
+        else:
+            delays, gains = [], []
+        P = len(delays)
+        ph = np.zeros((num_rx, num_tx, max(P, 1), 16))
+        lh = np.zeros((num_rx, num_tx, 2))
+        Hm = np.zeros((num_rx, num_tx), dtype=complex)
+        for r in range(num_rx):
+            for t in range(num_tx):
+                if ray:
+                    for p in range(P):
+                        ph[r, t, p] = 2 * np.pi * np.random.rand(16)
+                    ir0 = 2 * np.pi * np.random.rand(16)     # impulse_response(N=1): path 0 is the tap kept
+                    for _ in range(1, P):
+                        np.random.rand(16)
+                    Hm[r, t] = gains[0] * np.sqrt(2 / 16) * np.sum(np.exp(1j * ir0))
+                else:
+                    lh[r, t, 0] = np.random.normal(0, 1 / np.sqrt(2))
+                    lh[r, t, 1] = np.random.normal(0, 1 / np.sqrt(2))
+                    Hm[r, t] = lh[r, t, 0] + 1j * lh[r, t, 1]
+        z = np.zeros((num_rx, 2, L))
+        for r in range(num_rx):
+            z[r, 0] = np.random.normal(0, 1.0, L)
+            z[r, 1] = np.random.normal(0, 1.0, L)
+        y = np.zeros((num_rx, L), dtype=np.complex64)
+        dl = np.array(delays, dtype=np.int32)
+        g = np.array(gains, dtype=np.float64)
+        C.check(C.load().lte_channel_mimo_host(
+            L, num_tx, num_rx, 1, ch.kind, P, C.ptr(dl, C.I32) if P else None, C.ptr(g, C.F64) if P else None,
+            float(ch.fD), float(self.fs or 0.0), float(ch.snr_db), 0, C.ptr(x.view(np.float32), C.F32),
+            C.ptr(ph, C.F64) if ray else None, None, None if ray else C.ptr(lh, C.F64), C.ptr(z, C.F64),
+            C.ptr(y.view(np.float32), C.F32), None, None))
+        return list(y.astype(np.complex128)), Hm
 
 
 # ------------------------------------------------------------------ simulator
@@ -550,16 +686,7 @@ class OFDMSimulator:
                      capture=('signal_tx', 'bits_rx', 'data_syms', 'link_stats'))
         brx = r['bits_rx'][0].astype(np.int64)
         err = int(np.sum(bits != brx))
-        Hm = np.zeros((num_rx, 2), dtype=complex)
-        st = r['link_stats'][0].astype(np.float64)
-        for a in range(num_rx):
-            for t in range(2):
-                if not ray:
-                    Hm[a, t] = 1.0 + 0j if t == 0 else np.exp(1j * (t * np.pi / 2))
-                elif st[a, t, 0] > 1e-12:
-                    Hm[a, t] = np.sqrt(st[a, t, 1] / st[a, t, 0]) * np.exp(1j * np.angle(st[a, t, 2] + 1j * st[a, t, 3]))
-                else:
-                    Hm[a, t] = 1.0 + 0j
+        Hm = _link_matrix(r['link_stats'][0], ray)
         sig = r['signal_tx'][0].astype(np.complex128)
         sl = cfg.N + cfg.cp_length
         pap = []

@@ -150,6 +150,36 @@ def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan):
     assert a['ber'][1] <= a['ber'][0] + 1e-12
 
 
+@pytest.mark.parametrize('chan', ['awgn', 'rayleigh_mp'])
+def test_transmit_mimo_stage(C, golden_mimo, chan):
+    """OFDMChannel.transmit_mimo (a12) == the reference on the same seed:
+    received streams to float32 precision, channel matrix, RNG state."""
+    import lte_phy
+    x = [golden_mimo['txmimo_x0'], golden_mimo['txmimo_x1']]
+    ch = lte_phy.OFDMChannel(channel_type=chan, snr_db=12.0, fs=30.72e6, itu_profile='Pedestrian_A')
+    np.random.seed(123)
+    ys, Hm = ch.transmit_mimo(x, num_rx=2)
+    ref = golden_mimo[f'txmimo_{chan}_y']
+    assert np.max(np.abs(np.array(ys) - ref)) < 1e-5 * (1 + np.max(np.abs(ref)))
+    assert np.allclose(Hm, golden_mimo[f'txmimo_{chan}_H'], rtol=1e-5, atol=1e-6)
+    assert np.array_equal(_state(), golden_mimo[f'txmimo_{chan}_state'])
+
+
+@pytest.mark.parametrize('chan', ['awgn', 'rayleigh_mp'])
+def test_transmit_spatial_multiplexing_stage(C, golden_mimo, chan):
+    """ChannelSimulator.transmit_spatial_multiplexing (a13), 4x4, PedA 3 km/h
+    (time-varying Jakes) == the reference on the same seed."""
+    import lte_phy
+    cs = lte_phy.ChannelSimulator(channel_type=chan, snr_db=18.0, fs=30.72e6, itu_profile='Pedestrian_A',
+                                  frequency_ghz=2.0, velocity_kmh=3, verbose=False)
+    np.random.seed(321)
+    ys, Hm = cs.transmit_spatial_multiplexing(list(golden_mimo['txsm_x']), num_rx=4)
+    ref = golden_mimo[f'txsm_{chan}_y']
+    assert np.max(np.abs(np.array(ys) - ref)) < 1e-5 * (1 + np.max(np.abs(ref)))
+    assert np.allclose(Hm, golden_mimo[f'txsm_{chan}_H'], rtol=1e-9, atol=1e-12)
+    assert np.array_equal(_state(), golden_mimo[f'txsm_{chan}_state'])
+
+
 def test_mimo_argument_errors(C):
     import lte_phy
     sim = _sim(1.25, 'QPSK', 'awgn')
@@ -157,3 +187,7 @@ def test_mimo_argument_errors(C):
         sim.simulate_mimo(np.array([], dtype=int), 10.0)
     with pytest.raises(NotImplementedError):
         lte_phy.simulate_spatial_multiplexing(np.ones(100, dtype=int), num_tx=4, num_rx=2, rank='adaptive')
+    with pytest.raises(ValueError):
+        lte_phy.OFDMChannel().transmit_mimo([])
+    with pytest.raises(ValueError):
+        lte_phy.OFDMChannel().transmit_mimo([np.ones(10), np.ones(11)])

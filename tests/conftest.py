@@ -12,6 +12,7 @@ for p in (ROOT, PKG):
 
 GOLDEN = os.path.join(ROOT, 'tests', 'golden', 'golden.npz')
 GOLDEN_MIMO = os.path.join(ROOT, 'tests', 'golden', 'golden_mimo.npz')
+GOLDEN_TM4 = os.path.join(ROOT, 'tests', 'golden', 'golden_tm4.npz')
 
 
 def pytest_configure(config):
@@ -43,6 +44,17 @@ def golden():
 @pytest.fixture(scope='session')
 def golden_mimo():
     return np.load(GOLDEN_MIMO, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def golden_tm4():
+    return np.load(GOLDEN_TM4, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def tm4_oracle():
+    from oracle import tm4_oracle
+    return tm4_oracle
 
 
 @pytest.fixture(scope='session')

@@ -41,10 +41,13 @@ enum {
   /* config 4: the SISO coding chain (simulate_siso_coded TX/RX coding,
    * core/ofdm_core.py:1003-1299) around SFBC 2 x num_rx */
   LTE_CHAIN_SFBC_CODED = 4,
-  /* config 5: TM4 spatial multiplexing 4x4, rank 4, PMI 0 (W = I4), MMSE:
-   * simulate_spatial_multiplexing core/ofdm_core.py:2489-2815 */
+  /* TM4 spatial multiplexing, 2 / 4 TX x 1-4 RX, rank 1-4, codebook precoder,
+   * MMSE / ZF / SIC / MRC detection: simulate_spatial_multiplexing
+   * core/ofdm_core.py:2489-2815 (config 5 = 4x4, rank 4, PMI 0, MMSE) */
   LTE_CHAIN_SPATIAL = 5
 };
+/* MIMODetector.detector_type (core/mimo_detector.py:116-133); IRC == MMSE */
+enum { LTE_DET_MMSE = 0, LTE_DET_ZF = 1, LTE_DET_SIC = 2, LTE_DET_MRC = 3 };
 enum { LTE_CH_AWGN = 0, LTE_CH_RAYLEIGH = 1 }; /* core/channel.py:10-245 */
 
 #define LTE_MAX_PATHS 16
@@ -73,6 +76,11 @@ typedef struct {
                             * Multi-antenna gains: SFBC as RayleighChannel holds
                             * them; spatial links convert once more (Q2).  The
                             * multi-antenna chains use one link per (rx, tx).   */
+  /* spatial chain only (LTE_CHAIN_SPATIAL): */
+  int32_t rank;            /* layers, 1..min(num_tx, num_rx, 4); 0 -> num_tx with W = I */
+  int32_t detector;        /* LTE_DET_*                                          */
+  double precoder[32];     /* W [num_tx][rank] (LTECodebook.get_precoder, core/codebook_lte.py:
+                            * 317-330): entry (t, c) at [(t*4 + c)*2] re, [+1] im */
 } lte_plan_desc;
 
 typedef struct lte_plan lte_plan;
@@ -188,6 +196,13 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
                           uint64_t seed, const float *x, const double *phases, const double *link_noise,
                           const double *link_h, const double *noise, float *y, float *link_stats,
                           float *noise_power);
+/* TM4 detection: MIMODetector.detect (core/mimo_detector.py:55-369) per
+ * subcarrier, float64 on the device.  y [num_rx][n_sc] complex128, H
+ * [num_rx][num_tx][n_sc] complex128, W [num_tx][rank] complex128 (row-major),
+ * detector LTE_DET_*; bps 2/4/6 is SIC's constellation (0: none -> SIC uses
+ * MMSE, :225-228) -> out [rank][n_sc] complex128.  num_rx, num_tx <= 4. */
+int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps, int64_t n_sc, const double *y,
+                         const double *H, const double *W, double sigma2, double *out);
 /* Rate dematching map: rate_dematching_turbo core/channel_coding/rate_matching.py:374-489
  * src[j] = index into the E rate-matched LLRs feeding output j of [3K+12], -1 = zero. */
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t *src);

@@ -356,6 +356,7 @@ struct lte_plan {
   DBuf<int32_t> m_np, m_ppos, m_pseg;
   DBuf<float2> m_pval, Ym, Hm;
   DBuf<float> m_pig, link_part, link_sigma, inj_lz, inj_lh;
+  DBuf<double> m_W;
   // timing
   bool timing = false;
   double kms[KN_COUNT] = {0};
@@ -586,6 +587,35 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
   int rc = LTE_OK;
   if (!ok) rc = fail(LTE_EHIP, std::string("mimo channel failed: ") + hipGetErrorString(hipGetLastError()));
   cleanup();
+  return rc;
+}
+
+int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps, int64_t n_sc, const double* y,
+                         const double* H, const double* W, double sigma2, double* out) {
+  if (num_rx < rank) return fail(LTE_EINVAL, "num_rx (" + std::to_string(num_rx) + ") debe ser >= num_layers (" +
+                                                 std::to_string(rank) + ")");
+  if (detector < LTE_DET_MMSE || detector > LTE_DET_MRC) return fail(LTE_EINVAL, "Detector no soportado");
+  if (detector == LTE_DET_MRC && rank != 1) return fail(LTE_EINVAL, "MRC solo soporta num_layers=1 (rank-1)");
+  if (num_rx < 1 || num_rx > 4 || num_tx < 1 || num_tx > 4 || rank < 1 || rank > num_tx)
+    return fail(LTE_EUNSUP, "GPU detector: num_rx, num_tx <= 4, 1 <= rank <= num_tx");
+  if (bps != 0 && bps != 2 && bps != 4 && bps != 6) return fail(LTE_EINVAL, "Unsupported modulation");
+  if (n_sc < 1 || n_sc > (1LL << 26) || !y || !H || !W || !out) return fail(LTE_EINVAL, "bad detector arguments");
+  std::vector<double> w4(32, 0.0);
+  for (int t = 0; t < num_tx; ++t)
+    for (int c = 0; c < rank; ++c) {
+      w4[(t * 4 + c) * 2] = W[(t * rank + c) * 2];
+      w4[(t * 4 + c) * 2 + 1] = W[(t * rank + c) * 2 + 1];
+    }
+  DBuf<double> dy, dH, dW, dout;
+  const size_t ny = (size_t)num_rx * n_sc * 2, nh = (size_t)num_rx * num_tx * n_sc * 2, no = (size_t)rank * n_sc * 2;
+  bool ok = dy.alloc(ny) == 0 && dH.alloc(nh) == 0 && dout.alloc(no) == 0 && upload(dW, w4) == 0 &&
+            hipMemcpy(dy.p, y, ny * 8, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dH.p, H, nh * 8, hipMemcpyHostToDevice) == hipSuccess;
+  ok = ok && launch_det_stage(nullptr, detector, num_rx, num_tx, rank, bps, n_sc, dy.p, dH.p, dW.p, sigma2, dout.p) == 0;
+  ok = ok && hipDeviceSynchronize() == hipSuccess && hipMemcpy(out, dout.p, no * 8, hipMemcpyDeviceToHost) == hipSuccess;
+  int rc = LTE_OK;
+  if (!ok) rc = fail(LTE_EHIP, std::string("mimo detect failed: ") + hipGetErrorString(hipGetLastError()));
+  dy.release(); dH.release(); dW.release(); dout.release();
   return rc;
 }
 
@@ -850,8 +880,16 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
     return fail(LTE_EINVAL, "Alamouti SFBC requires exactly 2 TX antennas");
   if ((d.chain == LTE_CHAIN_SFBC || d.chain == LTE_CHAIN_SFBC_CODED) && d.num_rx > 8)
     return fail(LTE_EUNSUP, "SFBC: at most 8 RX antennas");
-  if (d.chain == LTE_CHAIN_SPATIAL && (num_tx != 4 || d.num_rx != 4))
-    return fail(LTE_EUNSUP, "spatial multiplexing: 4x4, rank 4 (TM4 PMI 0) only");
+  const int rank = d.chain == LTE_CHAIN_SPATIAL ? (d.rank > 0 ? d.rank : num_tx) : 0;
+  if (d.chain == LTE_CHAIN_SPATIAL) {
+    if (d.num_rx < rank)
+      return fail(LTE_EINVAL, "num_rx (" + std::to_string(d.num_rx) + ") debe ser >= num_layers (" +
+                                  std::to_string(rank) + ")");
+    if (d.detector < LTE_DET_MMSE || d.detector > LTE_DET_MRC) return fail(LTE_EINVAL, "Detector no soportado");
+    if (d.detector == LTE_DET_MRC && rank != 1) return fail(LTE_EINVAL, "MRC solo soporta num_layers=1 (rank-1)");
+    if ((num_tx != 2 && num_tx != 4) || d.num_rx > 4 || rank < 1 || rank > num_tx)
+      return fail(LTE_EUNSUP, "spatial multiplexing on the GPU path: 2 or 4 TX, 1-4 RX, rank <= num_tx");
+  }
   if (d.channel == LTE_CH_RAYLEIGH && (d.n_paths < 1 || d.n_paths > LTE_MAX_PATHS))
     return fail(LTE_EINVAL, "bad n_paths");
   if (d.max_frames < 1) return fail(LTE_EINVAL, "max_frames must be >= 1");
@@ -888,11 +926,27 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
     m.num_tx = num_tx;
     m.num_rx = d.num_rx;
     m.res = p->res;
-    m.n_dsc = sfbc ? p->res : (p->Nd + num_tx - 1) / num_tx;
+    m.rank = rank;
+    m.det = d.detector;
+    m.n_dsc = sfbc ? p->res : (p->Nd + rank - 1) / rank;   // layers fill the first ceil(Nd/rank) data SCs (Q20)
     m.n_est = sfbc ? p->n_grp : p->n_sym;
     m.n_cs = (d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0) ? p->n_sym : 1;
     rc = plan_mimo_tables(p);
     if (rc) { p->tabs.release(); delete p; return rc; }
+    if (!sfbc) {   // precoder W [num_tx][rank] in a [4][4] table; rank 0 in the descriptor -> identity
+      std::vector<double> w4(32, 0.0);
+      for (int t = 0; t < num_tx; ++t)
+        for (int c = 0; c < rank; ++c) {
+          if (d.rank > 0) {
+            w4[(t * 4 + c) * 2] = d.precoder[(t * 4 + c) * 2];
+            w4[(t * 4 + c) * 2 + 1] = d.precoder[(t * 4 + c) * 2 + 1];
+          } else {
+            w4[(t * 4 + c) * 2] = t == c ? 1.0 : 0.0;
+          }
+        }
+      if (upload(p->m_W, w4)) { p->tabs.release(); delete p; return fail(LTE_ENOMEM, "precoder upload"); }
+      m.W = p->m_W.p;
+    }
   }
   p->grid = Grid{d.N, p->log2N, d.Nc, d.cp_len, p->Nd, p->Np, d.bps, p->n_sym, p->L, p->n_grp,
                  p->tabs.data.p, p->tabs.pilot.p, p->tabs.pilots.p, p->tabs.seg.p, p->tabs.inv_gap.p,
@@ -935,7 +989,7 @@ int lte_plan_destroy(lte_plan* p) {
   p->blk_ptrs.release(); p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
   p->m_np.release(); p->m_ppos.release(); p->m_pseg.release(); p->m_pval.release(); p->Ym.release();
   p->Hm.release(); p->m_pig.release(); p->link_part.release(); p->link_sigma.release(); p->inj_lz.release();
-  p->inj_lh.release();
+  p->inj_lh.release(); p->m_W.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -985,7 +1039,7 @@ static void pack_bits(const uint8_t* bits, int n, uint32_t* w, int nw) {
     if (bits[i] & 1) w[i >> 5] |= 1u << (31 - (i & 31));
 }
 
-// Multi-antenna chains (SFBC 2xN, uncoded / coded; spatial 4x4 MMSE).
+// Multi-antenna chains (SFBC 2xN, uncoded / coded; TM4 spatial multiplexing).
 static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const uint32_t* inj_bits,
                     int64_t inj_bits_stride, const float* inj_ph, int64_t inj_ph_stride, const float* inj_z,
                     int64_t inj_z_stride) {
@@ -1074,8 +1128,8 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
       LCHK(launch_det_sfbc(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, p->Ym.p, p->Hm.p, p->snr_lin.p, p->pw.p, p->PW,
                            d.n_bits, p->frame_err.p, p->llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev));
     else
-      LCHK(launch_det_mmse(s, g, m, B, p->Ym.p, p->Hm.p, p->snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
-                           cap_syms_dev, cap_bits_dev));
+      LCHK(launch_det_spatial(s, g, m, B, p->Ym.p, p->Hm.p, p->snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+                              cap_syms_dev, cap_bits_dev));
   }
   if (coded) {
     {

@@ -147,5 +147,22 @@ __device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __
   }
 }
 
+// frame_err[b] += errs for every lane, with one atomic per distinct frame per
+// wave instead of one per lane (thousands of lanes of a frame otherwise
+// serialise on the same L2 address).  Must be reached by all lanes of the
+// wave; lanes without work pass errs = 0.
+__device__ __forceinline__ void frame_err_add(uint32_t* __restrict__ frame_err, int b, uint32_t errs) {
+  unsigned long long pending = __ballot(errs != 0u);
+  while (pending) {
+    const int src = __ffsll((long long)pending) - 1;
+    const int bb = __shfl(b, src);
+    const bool mine = errs != 0u && b == bb;
+    uint32_t v = mine ? errs : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((int)__lane_id() == src) atomicAdd(frame_err + bb, v);
+    pending &= ~__ballot(mine);
+  }
+}
 
 }  // namespace lte

@@ -75,7 +75,7 @@ int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* 
 
 // ---------------------------------------------------------------- multi-antenna chains
 // SFBC 2xN (configs 4 / simulate_miso / simulate_mimo) and TM4 spatial
-// multiplexing 4x4 (config 5).  lte_mimo.hip.
+// multiplexing (config 5 and its generalisation).  lte_mimo.hip.
 enum { MIMO_SFBC = 0, MIMO_SPATIAL = 1 };
 struct MimoGrid {
   int mode, num_tx, num_rx;
@@ -89,6 +89,8 @@ struct MimoGrid {
   const float2* pval;      // [num_tx][maxP] pilot symbols of TX t
   const float* pig;        // [num_tx][maxP] 1/(gap to the next pilot of TX t)
   const int32_t* pseg;     // [num_tx][n_dsc] left pilot (within TX t's set) of data SC j; -1 / >= np-1: edge hold
+  int rank, det;           // spatial: layers, LTE_DET_*
+  const double* W;         // spatial: [4][4] complex (re, im) precoder, entry (t, c) at (t*4 + c)*2
 };
 int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
                         const uint32_t* enc, int enc_words, const int32_t* tx_map, float2* x, int B);
@@ -111,9 +113,11 @@ int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, c
 int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const float2* Y,
                     const float2* H, const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
                     float* llr, float2* cap_syms, uint8_t* cap_bits);
-int launch_det_mmse(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
-                    const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                    float2* cap_syms, uint8_t* cap_bits);
+int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
+                       const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                       float2* cap_syms, uint8_t* cap_bits);
+int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int64_t n, const double* y,
+                     const double* H, const double* W, double s2, double* out);
 
 // turbo modes
 enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3 };  // TM_DECODE: full decode (iterations + decisions)

@@ -1,8 +1,9 @@
 // Multi-antenna chains for gfx950:
 //  * SFBC Alamouti 2 x num_rx (OFDMSimulator.simulate_miso / simulate_mimo,
 //    core/ofdm_core.py:1850-2258; config 4 = the same plus turbo coding),
-//  * TM4 spatial multiplexing 4x4, rank 4, W = I4, MMSE
-//    (simulate_spatial_multiplexing, core/ofdm_core.py:2489-2815; config 5).
+//  * TM4 spatial multiplexing, 2 / 4 TX, 1-4 RX, rank 1-4, codebook precoder W,
+//    MMSE / ZF / SIC / MRC (simulate_spatial_multiplexing,
+//    core/ofdm_core.py:2489-2815; config 5 = 4x4 rank 4 MMSE).
 // Per frame:  TX  one slot per (frame, OFDM symbol, TX antenna): QAM map ->
 //                 SFBC pair coding / layer mapping -> per-TX CRS pilots -> IFFT + CP
 //             CH  per link path coefficients (Jakes, fD = 0 constant or a
@@ -12,7 +13,7 @@
 //                 on estimation symbols LS at each TX's pilot subset + linear
 //                 interpolation (MIMOChannelEstimatorPeriodic); data SCs to HBM
 //             DET SFBC combine averaged over RX -> hard bits / LLRs, or a
-//                 float64 4x4 MMSE per subcarrier -> hard bits.
+//                 float64 MMSE / ZF / SIC / MRC per subcarrier -> hard bits.
 #include "lte_common.h"
 #include "lte_internal.h"
 #include "lte_dev.h"
@@ -25,8 +26,9 @@ constexpr int MWG = 256;
 // TX.  SFBCAlamouti.encode (core/sfbc_alamouti.py:45-78) + SFBCResourceMapper
 // (:213-256): data RE j of symbol l carries, for the pair (s0, s1) =
 // (q[l*res + (j&~1)], q[.. + 1]): TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)].
-// Spatial (core/ofdm_core.py:2596-2655): layer t = q[4j + t] on data SC j <
-// ceil(Nd/4) (Q20), W = I4.  Pilots: TX t at its subset (cell t % 4).
+// Spatial (core/ofdm_core.py:2596-2655): layer c = q[R j + c] on data SC j <
+// ceil(Nd/R) (Q20), x_t = sum_c W[t][c] layer_c.  Pilots: TX t at its subset
+// (cell t % 4).
 template <int CODED, int BPS>
 __device__ __forceinline__ float2 qam_at(int64_t q, const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fe,
                                          const int32_t* __restrict__ tx_map) {
@@ -74,8 +76,14 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
         if ((j & 1) == 0) v = t == 0 ? s0 : s1;
         else v = t == 0 ? make_float2(-s1.x, s1.y) : make_float2(s0.x, -s0.y);   // -conj(s1) / conj(s0)
       } else {
-        const int qi = 4 * j + t;
-        v = qi < m.res ? qam_at<CODED, BPS>(q0 + qi, fb, fe, tx_map) : make_float2(0.f, 0.f);
+        v = make_float2(0.f, 0.f);
+        for (int c = 0; c < m.rank; ++c) {
+          const int qi = m.rank * j + c;
+          if (qi >= m.res) break;
+          const float2 sq = qam_at<CODED, BPS>(q0 + qi, fb, fe, tx_map);
+          const float2 w = make_float2((float)m.W[(t * 4 + c) * 2], (float)m.W[(t * 4 + c) * 2 + 1]);
+          v = cadd(v, cmul(w, sq));
+        }
       }
       buf[g.data_idx[j]] = v;
     }
@@ -470,9 +478,11 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
   const int npair = m.n_dsc >> 1;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t per = (int64_t)g.n_sym * npair;
-  const int b = (int)(i / per);
-  if (b >= B) return;
-  const int rem = (int)(i - (int64_t)b * per), l = rem / npair, pr = rem - l * npair, j = 2 * pr;
+  // lanes past the batch stay in the wave (convergent error reduction) and
+  // work on a clamped, valid index without storing anything
+  const bool act = i < (int64_t)B * per;
+  const int b = act ? (int)(i / per) : B - 1;
+  const int rem = act ? (int)(i - (int64_t)b * per) : 0, l = rem / npair, pr = rem - l * npair, j = 2 * pr;
   const int e = l / 14;
   float2 z0 = make_float2(0.f, 0.f), z1 = make_float2(0.f, 0.f);
   float inv_g = 0.f;
@@ -496,7 +506,7 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
   z0 = make_float2(z0.x * ir, z0.y * ir);
   z1 = make_float2(z1.x * ir, z1.y * ir);
   const int64_t re = (int64_t)l * m.res + j;
-  if (cap_syms) {
+  if (cap_syms && act) {
     cap_syms[(size_t)b * g.n_sym * m.res + re] = z0;
     cap_syms[(size_t)b * g.n_sym * m.res + re + 1] = z1;
   }
@@ -505,6 +515,7 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
     const float nv = fmaxf(s2 * ir * ir * inv_g, s2 * 0.25f);
     float o[BPS];
     float* lo = llr + ((size_t)b * g.n_sym * m.res + re) * BPS;
+    if (!act) return;
     soft_demap<BPS>(z0, nv, o);
 #pragma unroll
     for (int q = 0; q < BPS; ++q) lo[q] = o[q];
@@ -519,14 +530,14 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
 #pragma unroll
       for (int q = 0; q < BPS; ++q) {
         const int64_t pbit = (re + h) * BPS + q;
-        if (pbit < n_bits) {
+        if (act && pbit < n_bits) {
           const uint32_t bit = (idx >> (BPS - 1 - q)) & 1;
           errs += bit ^ getbit(fb, pbit);
           if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
         }
       }
     }
-    if (errs) atomicAdd(frame_err + b, errs);
+    frame_err_add(frame_err, b, errs);
   }
 }
 
@@ -549,131 +560,310 @@ int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, 
 }
 
 // ---------------------------------------------------------------------------
-// MMSE 4x4 (MIMODetector._mmse_detect, core/mimo_detector.py:135-173): per
-// (frame, symbol, data SC j < ceil(Nd/4)), s = (H^H H + s2 I)^-1 H^H y with
-// the nominal s2 = 10^(-SNR/10) (core/ofdm_core.py:2737) and W = I4.  Solved in
-// float64 (Cholesky of the Hermitian positive definite H^H H + s2 I; the
-// reference inverts with LAPACK LU -- both are backward stable here); ~600
-// flops per SC, negligible next to the FFTs.  Layer t of SC j is QAM symbol
-// 4j + t of the OFDM symbol (LayerMapper.demap_from_layers :81-115).
+// TM4 detection (MIMODetector, core/mimo_detector.py:55-369) per (frame,
+// symbol, data SC j < ceil(Nd/rank)): H_eff = H W (num_rx x rank, W the TM4
+// codebook precoder), nominal s2 = 10^(-SNR/10) (core/ofdm_core.py:2737):
+//   MMSE / IRC  s = (He^H He + s2 I)^-1 He^H y                      (:135-173)
+//   ZF          s = pinv(He) y = (He^H He)^-1 He^H y (full column rank) (:175-198)
+//   SIC         layers ordered by ||h_i||^2 / (sum_{j!=i} ||h_j||^2 + s2 + 1e-10)
+//               (np.argsort()[::-1]: descending, ties -> higher index), each
+//               detected by MMSE over the still-undetected columns, sliced to
+//               the nearest constellation point (first index on ties) and
+//               cancelled with its original column                  (:200-350)
+//   MRC         rank 1: s = conj(h) y / ||h||^2                      (:352-369)
+// Layer t of SC j is QAM symbol rank*j + t of the OFDM symbol
+// (LayerMapper.demap_from_layers, core/layer_mapper.py:81-115).  Float64 in
+// registers throughout: every dimension is unrolled to 4 with runtime guards
+// (num_rx, rank <= 4), so nothing is indexed dynamically (no scratch).  An
+// undetected / absent layer is a zero column: the masked normal matrix is then
+// block diagonal with s2 on the masked diagonal, and the Cholesky solve of the
+// full 4x4 system equals the solve over the remaining columns.
 struct dc { double x, y; };
 __device__ __forceinline__ dc dmul(dc a, dc b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 __device__ __forceinline__ dc dmulc(dc a, dc b) { return {a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y}; }  // a*conj(b)
 __device__ __forceinline__ dc dsub(dc a, dc b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ dc dadd(dc a, dc b) { return {a.x + b.x, a.y + b.y}; }
 
-template <int BPS>
-__global__ __launch_bounds__(MWG) void k_det_mmse(Grid g, MimoGrid m, int B, const float2* __restrict__ Y,
-                                                  const float2* __restrict__ H, const float* __restrict__ snr_lin,
-                                                  const uint32_t* __restrict__ pw, int PW, int n_bits,
-                                                  uint32_t* __restrict__ frame_err, float2* __restrict__ cap_syms,
-                                                  uint8_t* __restrict__ cap_bits) {
-  constexpr int NT = 4, NR = 4;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t per = (int64_t)g.n_sym * m.n_dsc;
-  const int b = (int)(i / per);
-  if (b >= B) return;
-  const int rem = (int)(i - (int64_t)b * per), l = rem / m.n_dsc, j = rem - l * m.n_dsc;
-  dc h[NR][NT], yv[NR];
-  for (int r = 0; r < NR; ++r) {
-    const float2 v = Y[(((size_t)b * g.n_sym + l) * NR + r) * m.n_dsc + j];
-    yv[r] = {v.x, v.y};
-    for (int t = 0; t < NT; ++t) {
-      const float2 hv = H[((((size_t)b * NR + r) * m.n_est + l) * NT + t) * m.n_dsc + j];
-      h[r][t] = {hv.x, hv.y};
-    }
-  }
-  const double s2 = 1.0 / (double)snr_lin[b];
-  // A = H^H H + s2 I is Hermitian positive definite: Cholesky A = L L^H (no
-  // pivoting needed, fully unrolled -> registers only), then L u = H^H y and
-  // L^H s = u.  Float64 throughout.
-  dc A[NT][NT], rhs[NT];
+constexpr int DMAX = 4;   // num_rx, rank <= 4 on the GPU path
+
+// Solve (He_m^H He_m + s2 I) s = He_m^H y over the columns with mask bit set
+// (others -> 0) by Cholesky; s2 = 0 gives the ZF normal equations.
+__device__ __forceinline__ void masked_solve(const dc (&He)[DMAX][DMAX], const dc (&y)[DMAX], int mask, double s2,
+                                             dc (&sv)[DMAX]) {
+  dc A[DMAX][DMAX], rhs[DMAX];
 #pragma unroll
-  for (int a = 0; a < NT; ++a) {
+  for (int a = 0; a < DMAX; ++a) {
+    const bool ia = (mask >> a) & 1;
 #pragma unroll
     for (int c = 0; c <= a; ++c) {
+      const bool ic = (mask >> c) & 1;
       dc acc = {0.0, 0.0};
+      if (ia && ic) {
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const dc p = dmulc(h[r][c], h[r][a]);   // conj(h[r][a]) h[r][c] = (H^H H)[a][c]
-        acc.x += p.x; acc.y += p.y;
+        for (int r = 0; r < DMAX; ++r) {
+          const dc p = dmulc(He[r][c], He[r][a]);   // conj(He[r][a]) He[r][c] = (He^H He)[a][c]
+          acc.x += p.x; acc.y += p.y;
+        }
       }
-      if (a == c) acc.x += s2;
+      if (a == c) acc.x += ia ? s2 : 1.0;
       A[a][c] = acc;
     }
     dc acc = {0.0, 0.0};
+    if (ia) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const dc p = dmulc(yv[r], h[r][a]);
-      acc.x += p.x; acc.y += p.y;
+      for (int r = 0; r < DMAX; ++r) {
+        const dc p = dmulc(y[r], He[r][a]);
+        acc.x += p.x; acc.y += p.y;
+      }
     }
     rhs[a] = acc;
   }
-  dc Lm[NT][NT];
-  double ld[NT];
+  dc Lm[DMAX][DMAX];
+  double ld[DMAX];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
+  for (int i = 0; i < DMAX; ++i) {
     double d = A[i][i].x;
 #pragma unroll
     for (int k = 0; k < i; ++k) d -= Lm[i][k].x * Lm[i][k].x + Lm[i][k].y * Lm[i][k].y;
     ld[i] = sqrt(fmax(d, 1e-300));
     const double inv = 1.0 / ld[i];
 #pragma unroll
-    for (int j = i + 1; j < NT; ++j) {
+    for (int j = i + 1; j < DMAX; ++j) {
       dc v = A[j][i];
 #pragma unroll
       for (int k = 0; k < i; ++k) v = dsub(v, dmulc(Lm[j][k], Lm[i][k]));   // L[j][k] conj(L[i][k])
       Lm[j][i] = {v.x * inv, v.y * inv};
     }
   }
-  dc u[NT], sv[NT];
+  dc u[DMAX];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
+  for (int i = 0; i < DMAX; ++i) {
     dc v = rhs[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) v = dsub(v, dmul(Lm[i][k], u[k]));
     u[i] = {v.x / ld[i], v.y / ld[i]};
   }
 #pragma unroll
-  for (int i = NT - 1; i >= 0; --i) {
+  for (int i = DMAX - 1; i >= 0; --i) {
     dc v = u[i];
 #pragma unroll
-    for (int k = i + 1; k < NT; ++k) v = dsub(v, dmulc(sv[k], Lm[k][i]));  // conj(L[k][i]) s[k]
-    sv[i] = {v.x / ld[i], v.y / ld[i]};
+    for (int k = i + 1; k < DMAX; ++k) v = dsub(v, dmulc(sv[k], Lm[k][i]));  // conj(L[k][i]) s[k]
+    sv[i] = ((mask >> i) & 1) ? dc{v.x / ld[i], v.y / ld[i]} : dc{0.0, 0.0};
   }
+}
+
+// nearest constellation point in float64 (QAMModulator constellation,
+// core/modulator.py:28-59; argmin |c - s| with the first index on ties)
+__device__ __forceinline__ int level_idx_d(double v, double scale, int nl) {
+  const double t = (v * scale + (double)(nl - 1)) * 0.5;
+  int i = (int)ceil(t - 0.5);
+  return i < 0 ? 0 : (i > nl - 1 ? nl - 1 : i);
+}
+
+__device__ __forceinline__ dc slice_d(dc s, int bps) {
+  if (bps == 2) {
+    const double a = 1.0 / 1.4142135623730951;
+    return {s.x < 0.0 ? -a : a, s.y < 0.0 ? -a : a};
+  }
+  const int nl = 1 << (bps >> 1);
+  const double S = bps == 4 ? 3.1622776601683795 : 6.48074069840786;
+  const int i = level_idx_d(s.x, S, nl), q = level_idx_d(s.y, S, nl);
+  const double inv = 1.0 / S;   // NumPy's complex / real scalar multiplies by the reciprocal
+  return {(2.0 * i - (nl - 1)) * inv, (2.0 * q - (nl - 1)) * inv};
+}
+
+// One subcarrier.  He rows >= num_rx and columns >= R are zero on entry.
+// SIC_ON = false compiles only the linear detectors (the SIC branch would
+// otherwise set the register budget of every launch).
+template <bool SIC_ON>
+__device__ __forceinline__ void detect_sc(const dc (&He)[DMAX][DMAX], const dc (&y)[DMAX], int R, int det, double s2,
+                                          int bps, dc (&sv)[DMAX]) {
+  const int full = (1 << R) - 1;
+  if (det == LTE_DET_MRC) {
+    double n2 = 0.0;
+    dc acc = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < DMAX; ++r) {
+      n2 += He[r][0].x * He[r][0].x + He[r][0].y * He[r][0].y;
+      const dc p = dmulc(y[r], He[r][0]);
+      acc.x += p.x; acc.y += p.y;
+    }
+    sv[0] = {acc.x / n2, acc.y / n2};
+#pragma unroll
+    for (int l = 1; l < DMAX; ++l) sv[l] = {0.0, 0.0};
+    return;
+  }
+  if (!SIC_ON || det != LTE_DET_SIC || bps == 0) {   // MMSE / IRC / ZF; SIC without a constellation -> MMSE (:225-228)
+    masked_solve(He, y, full, det == LTE_DET_ZF ? 0.0 : s2, sv);
+    return;
+  }
+  // SIC: detection position of every layer (descending SINR, ties -> higher index first)
+  double nrm[DMAX];
+#pragma unroll
+  for (int l = 0; l < DMAX; ++l) {
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < DMAX; ++r) a += He[r][l].x * He[r][l].x + He[r][l].y * He[r][l].y;
+    nrm[l] = a;
+  }
+  double sinr[DMAX];
+#pragma unroll
+  for (int l = 0; l < DMAX; ++l) {
+    double itf = 0.0;
+#pragma unroll
+    for (int j = 0; j < DMAX; ++j)
+      if (j != l && j < R) itf += nrm[j];
+    sinr[l] = nrm[l] / (itf + s2 + 1e-10);
+  }
+  int pos[DMAX];
+#pragma unroll
+  for (int l = 0; l < DMAX; ++l) {
+    int p = 0;
+#pragma unroll
+    for (int j = 0; j < DMAX; ++j)
+      if (j < R && j != l) p += (sinr[j] > sinr[l]) || (sinr[j] == sinr[l] && j > l);
+    pos[l] = p;
+  }
+  dc yr[DMAX];
+#pragma unroll
+  for (int r = 0; r < DMAX; ++r) yr[r] = y[r];
+  int mask = full;
+#pragma unroll
+  for (int it = 0; it < DMAX; ++it) {
+    if (it < R) {
+      dc est[DMAX];
+      masked_solve(He, yr, mask, s2, est);
+#pragma unroll
+      for (int l = 0; l < DMAX; ++l) {
+        if (l < R && pos[l] == it) {
+          const dc sh = slice_d(est[l], bps);
+          sv[l] = sh;
+#pragma unroll
+          for (int r = 0; r < DMAX; ++r) yr[r] = dsub(yr[r], dmul(He[r][l], sh));
+          mask &= ~(1 << l);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < DMAX; ++l)
+    if (l >= R) sv[l] = {0.0, 0.0};
+}
+
+template <int BPS, bool SIC_ON>
+__global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, const float2* __restrict__ Y,
+                                                     const float2* __restrict__ H, const float* __restrict__ snr_lin,
+                                                     const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                     uint32_t* __restrict__ frame_err, float2* __restrict__ cap_syms,
+                                                     uint8_t* __restrict__ cap_bits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)g.n_sym * m.n_dsc;
+  // lanes past the batch stay in the wave (convergent error reduction) and
+  // work on a clamped, valid index without storing anything
+  const bool act = i < (int64_t)B * per;
+  const int b = act ? (int)(i / per) : B - 1;
+  const int rem = act ? (int)(i - (int64_t)b * per) : 0, l = rem / m.n_dsc, j = rem - l * m.n_dsc;
+  const int NR = m.num_rx, NT = m.num_tx, R = m.rank;
+  dc He[DMAX][DMAX], yv[DMAX];
+#pragma unroll
+  for (int r = 0; r < DMAX; ++r) {
+    yv[r] = {0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < DMAX; ++c) He[r][c] = {0.0, 0.0};
+    if (r < NR) {
+      const float2 v = Y[(((size_t)b * g.n_sym + l) * NR + r) * m.n_dsc + j];
+      yv[r] = {v.x, v.y};
+      const float2* Hr = H + (((size_t)b * NR + r) * m.n_est + l) * NT * m.n_dsc + j;
+      for (int t = 0; t < NT; ++t) {                 // He[r][c] = sum_t H[r][t] W[t][c]
+        const float2 hv = Hr[(size_t)t * m.n_dsc];
+        const dc h = {hv.x, hv.y};
+#pragma unroll
+        for (int c = 0; c < DMAX; ++c)
+          if (c < R) He[r][c] = dadd(He[r][c], dmul(h, dc{m.W[(t * DMAX + c) * 2], m.W[(t * DMAX + c) * 2 + 1]}));
+      }
+    }
+  }
+  dc sv[DMAX];
+  detect_sc<SIC_ON>(He, yv, R, m.det, 1.0 / (double)snr_lin[b], BPS, sv);
   const uint32_t* fb = pw + (size_t)b * PW;
   uint32_t errs = 0;
-  for (int t = 0; t < NT; ++t) {
-    const int qi = NT * j + t;
-    if (qi >= m.res) break;
+#pragma unroll
+  for (int t = 0; t < DMAX; ++t) {
+    const int qi = R * j + t;
+    if (t >= R || qi >= m.res) break;
     const float2 z = make_float2((float)sv[t].x, (float)sv[t].y);
     const int64_t re = (int64_t)l * m.res + qi;
-    if (cap_syms) cap_syms[(size_t)b * g.n_sym * m.res + re] = z;
+    if (cap_syms && act) cap_syms[(size_t)b * g.n_sym * m.res + re] = z;
     const int idx = hard_index(z, BPS, (float)qam_norm<BPS>());
 #pragma unroll
     for (int q = 0; q < BPS; ++q) {
       const int64_t pbit = re * BPS + q;
-      if (pbit < n_bits) {
+      if (act && pbit < n_bits) {
         const uint32_t bit = (idx >> (BPS - 1 - q)) & 1;
         errs += bit ^ getbit(fb, pbit);
         if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
       }
     }
   }
-  if (errs) atomicAdd(frame_err + b, errs);
+  frame_err_add(frame_err, b, errs);
 }
 
-int launch_det_mmse(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
-                    const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                    float2* cap_syms, uint8_t* cap_bits) {
-  if (m.num_tx != 4 || m.num_rx != 4) return (int)hipErrorInvalidValue;
+int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
+                       const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                       float2* cap_syms, uint8_t* cap_bits) {
+  if (m.num_tx < 1 || m.num_tx > DMAX || m.num_rx < 1 || m.num_rx > DMAX || m.rank < 1 || m.rank > m.num_rx ||
+      m.rank > m.num_tx || !m.W)
+    return (int)hipErrorInvalidValue;
   const int64_t n = (int64_t)B * g.n_sym * m.n_dsc;
   const dim3 grid((unsigned)((n + MWG - 1) / MWG));
-  if (g.bps == 2) hipLaunchKernelGGL(k_det_mmse<2>, grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits,
-                                     frame_err, cap_syms, cap_bits);
-  else if (g.bps == 4) hipLaunchKernelGGL(k_det_mmse<4>, grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW,
-                                          n_bits, frame_err, cap_syms, cap_bits);
-  else hipLaunchKernelGGL(k_det_mmse<6>, grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits, frame_err,
-                          cap_syms, cap_bits);
+#define LTE_DSP(B_, S_)                                                                                            \
+  hipLaunchKernelGGL((k_det_spatial<B_, S_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits,        \
+                     frame_err, cap_syms, cap_bits)
+  const bool sic = m.det == LTE_DET_SIC;
+  if (g.bps == 2) { if (sic) LTE_DSP(2, true); else LTE_DSP(2, false); }
+  else if (g.bps == 4) { if (sic) LTE_DSP(4, true); else LTE_DSP(4, false); }
+  else { if (sic) LTE_DSP(6, true); else LTE_DSP(6, false); }
+#undef LTE_DSP
+  return (int)hipGetLastError();
+}
+
+// Stage entry (MIMODetector.detect on host arrays): one thread per subcarrier,
+// float64 y [num_rx][n], H [num_rx][num_tx][n], W [4][4] -> out [rank][n].
+__global__ __launch_bounds__(MWG) void k_det_stage(int det, int NR, int NT, int R, int bps, int64_t n,
+                                                   const double* __restrict__ y, const double* __restrict__ H,
+                                                   const double* __restrict__ W, double s2, double* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  dc He[DMAX][DMAX], yv[DMAX];
+#pragma unroll
+  for (int r = 0; r < DMAX; ++r) {
+    yv[r] = {0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < DMAX; ++c) He[r][c] = {0.0, 0.0};
+    if (r < NR) {
+      yv[r] = {y[((size_t)r * n + k) * 2], y[((size_t)r * n + k) * 2 + 1]};
+      for (int t = 0; t < NT; ++t) {
+        const dc h = {H[(((size_t)r * NT + t) * n + k) * 2], H[(((size_t)r * NT + t) * n + k) * 2 + 1]};
+#pragma unroll
+        for (int c = 0; c < DMAX; ++c)
+          if (c < R) He[r][c] = dadd(He[r][c], dmul(h, dc{W[(t * DMAX + c) * 2], W[(t * DMAX + c) * 2 + 1]}));
+      }
+    }
+  }
+  dc sv[DMAX];
+  detect_sc<true>(He, yv, R, det, s2, bps, sv);
+#pragma unroll
+  for (int l = 0; l < DMAX; ++l)
+    if (l < R) {
+      out[((size_t)l * n + k) * 2] = sv[l].x;
+      out[((size_t)l * n + k) * 2 + 1] = sv[l].y;
+    }
+}
+
+int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int64_t n, const double* y,
+                     const double* H, const double* W, double s2, double* out) {
+  hipLaunchKernelGGL(k_det_stage, dim3((unsigned)((n + MWG - 1) / MWG)), dim3(MWG), 0, s, det, NR, NT, R, bps, n, y,
+                     H, W, s2, out);
   return (int)hipGetLastError();
 }
 

@@ -11,8 +11,10 @@ from .ofdm_core import (ChannelSimulator, OFDMChannel, OFDMReceiver, OFDMSimulat
                         simulate_spatial_multiplexing)
 from .ofdm_module import OFDMModule
 from . import channel_coding
+from .tm4 import LTECodebook, LayerMapper, MIMODetector, RankAdaptation
 
 __version__ = '0.1.0'
 __all__ = ['LTEConfig', 'OFDMModule', 'OFDMSimulator', 'OFDMTransmitter', 'OFDMReceiver', 'OFDMChannel',
-           'ChannelSimulator', 'simulate_spatial_multiplexing', 'channel_coding', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
+           'ChannelSimulator', 'simulate_spatial_multiplexing', 'channel_coding', 'LTECodebook', 'LayerMapper',
+           'MIMODetector', 'RankAdaptation', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
            'LTE_PROFILES', 'CP_VALUES', 'SUBCARRIER_SPACING']

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get('LTE_HIP_LIB', os.path.join(_HERE, 'liblte_hip.so'))
 LTE_OK, LTE_EINVAL, LTE_EHIP, LTE_ENOMEM, LTE_ENODEV, LTE_EUNSUP = 0, -1, -2, -3, -4, -5
 CHAIN_UNCODED, CHAIN_CODED, CHAIN_SIMO, CHAIN_SFBC, CHAIN_SFBC_CODED, CHAIN_SPATIAL = 0, 1, 2, 3, 4, 5
 CH_AWGN, CH_RAYLEIGH = 0, 1
+DET_MMSE, DET_ZF, DET_SIC, DET_MRC = 0, 1, 2, 3
 STAGE_TX, STAGE_CHANNEL, STAGE_RX, STAGE_ALL = 1, 2, 4, 7
 MAX_PATHS = 16
 
@@ -30,7 +31,7 @@ class PlanDesc(ctypes.Structure):
                 ('chain', c_i32), ('channel', c_i32), ('num_rx', c_i32), ('n_paths', c_i32),
                 ('delays', c_i32 * MAX_PATHS), ('gains', c_f64 * MAX_PATHS), ('fD', c_f64), ('fs', c_f64),
                 ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32),
-                ('num_tx', c_i32)]
+                ('num_tx', c_i32), ('rank', c_i32), ('detector', c_i32), ('precoder', c_f64 * 32)]
 
 
 class RunArgs(ctypes.Structure):
@@ -76,6 +77,8 @@ _SIGS = {
                                      P(ctypes.c_float), P(ctypes.c_float)]),
     'lte_crc_host': (ctypes.c_int, [c_i64, P(ctypes.c_uint8), ctypes.c_uint32, ctypes.c_int,
                                     P(ctypes.c_uint32)]),
+    'lte_mimo_detect_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            c_i64, P(c_f64), P(c_f64), P(c_f64), c_f64, P(c_f64)]),
     'lte_rate_dematch_map': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32)]),
     'lte_channel_host': (ctypes.c_int, [c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32), P(c_f64),
                                         c_f64, c_f64, c_f64, c_u64, P(ctypes.c_float), P(c_f64), P(c_f64),
@@ -160,3 +163,21 @@ def rate_dematch_map(K, E, rv_idx=0):
     src = np.empty(3 * K + 12, dtype=np.int32)
     check(load().lte_rate_dematch_map(K, E, rv_idx, ptr(src, I32)))
     return src
+
+
+def mimo_detect(det, y, H, sigma2, W, bps=0):
+    """MIMODetector.detect per subcarrier on the GPU (lte_mimo_detect_host):
+    y [num_rx, n] , H [num_rx, num_tx, n], W [num_tx, rank] -> [rank, n]."""
+    device_init()
+    y = np.ascontiguousarray(y, dtype=np.complex128)
+    H = np.ascontiguousarray(H, dtype=np.complex128)
+    W = np.ascontiguousarray(W, dtype=np.complex128)
+    nr, n = y.shape
+    nt, rank = W.shape
+    if H.shape != (nr, nt, n):
+        raise ValueError(f"H shape {H.shape} does not match y {y.shape} and W {W.shape}")
+    out = np.empty((rank, n), dtype=np.complex128)
+    check(load().lte_mimo_detect_host(int(det), nr, nt, rank, int(bps), n, ptr(y.view(np.float64), F64),
+                                      ptr(H.view(np.float64), F64), ptr(W.view(np.float64), F64), float(sigma2),
+                                      ptr(out.view(np.float64), F64)))
+    return out

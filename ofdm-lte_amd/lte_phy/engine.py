@@ -17,7 +17,8 @@ from . import _capi as C
 
 class Plan:
     def __init__(self, *, N, Nc, cp_len, bps, n_sym, chain, channel, num_rx=1, delays=(), gains=(), fD=0.0,
-                 fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0, num_tx=1):
+                 fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0, num_tx=1, rank=0, detector=0,
+                 precoder=()):
         C.device_init()
         d = C.PlanDesc()
         d.N, d.Nc, d.cp_len, d.bps, d.n_sym = N, Nc, cp_len, bps, n_sym
@@ -31,6 +32,14 @@ class Plan:
         d.fD, d.fs = float(fD), float(fs)
         d.n_bits, d.turbo_iters, d.max_frames, d.cell_id = int(n_bits), int(turbo_iters), int(max_frames), cell_id
         d.num_tx = int(num_tx)
+        d.rank, d.detector = int(rank), int(detector)
+        if rank and num_tx <= 4 and rank <= 4:   # W [num_tx][rank] -> the [4][4] table of lte_plan_desc.precoder
+            #                                    (larger arrays: lte_plan_create rejects them, LTE_EUNSUP)
+            W = np.asarray(precoder, dtype=np.complex128).reshape(int(num_tx), int(rank))
+            for t in range(W.shape[0]):
+                for c in range(W.shape[1]):
+                    d.precoder[(t * 4 + c) * 2] = float(W[t, c].real)
+                    d.precoder[(t * 4 + c) * 2 + 1] = float(W[t, c].imag)
         self.desc = d
         h = ctypes.c_void_p()
         C.check(C.load().lte_plan_create(ctypes.byref(d), ctypes.byref(h)))
@@ -48,7 +57,8 @@ class Plan:
         # multi-antenna geometry (lte_capi.hip lte_plan_create): REs per OFDM symbol,
         # data SCs carrying data, channel estimates per frame
         self.res = (self.Nd & ~1) if sfbc else self.Nd
-        self.n_dsc = self.res if sfbc else -(-self.Nd // max(1, self.num_tx))
+        self.rank = int(rank) if rank else self.num_tx
+        self.n_dsc = self.res if sfbc else -(-self.Nd // max(1, self.rank))
         self.n_est = self.n_grp if sfbc else self.n_sym
 
     def __del__(self):

@@ -748,7 +748,7 @@ class OFDMSimulator:
     def run_grid(self, snr_range, num_trials: int, seed: int = 0, coded: bool = False, num_rx: int = 1,
                  n_bits: Optional[int] = None, frames_per_call: int = 4096, rank: int = 0, world_size: int = 1,
                  turbo_iters: int = 8, mimo: Optional[str] = None, velocity_kmh: float = 3,
-                 frequency_ghz: float = 2.0) -> Dict:
+                 frequency_ghz: float = 2.0, spatial: Optional[Dict] = None) -> Dict:
         """Device-resident Monte-Carlo BER/BLER grid (SNR x trials).  Frame
         (s, t) has global id s*num_trials + t; all randomness is Philox keyed by
         (seed, id), so results are identical for any sharding.  With
@@ -757,9 +757,10 @@ class OFDMSimulator:
 
         mimo=None: SISO (coded: config 2) / SIMO MRC (num_rx > 1: config 3);
         mimo='sfbc': 2 x num_rx Alamouti (coded: config 4);
-        mimo='spatial': 4x4 rank-4 MMSE (config 5; the spatial channel of
+        mimo='spatial': TM4 (config 5 = 4x4 rank-4 PMI-0 MMSE; the spatial channel of
         simulate_spatial_multiplexing: gains converted once more, fD from
-        velocity_kmh / frequency_ghz)."""
+        velocity_kmh / frequency_ghz).  `spatial` overrides any of
+        {'num_tx': 4, 'num_rx': 4, 'rank': 4, 'detector': 'MMSE', 'pmi': 0}."""
         snrs = np.atleast_1d(np.asarray(snr_range, dtype=np.float64))
         S, T = len(snrs), int(num_trials)
         cfg = self.config
@@ -778,8 +779,14 @@ class OFDMSimulator:
             nb = int(n_bits or SLOT_SIZE * self.Nd * cfg.bits_per_symbol)
             ch = self.channels[0]
             ctype = 'rayleigh_mp' if ch.kind == C.CH_RAYLEIGH else 'awgn'
+            from .tm4 import DETECTORS, LTECodebook
+            sp = {'num_tx': 4, 'num_rx': 4, 'rank': 4, 'detector': 'MMSE', 'pmi': 0}
+            sp.update(spatial or {})
+            W = LTECodebook(sp['num_tx'], transmission_mode='TM4', rank=sp['rank']).get_precoder(sp['pmi'])
             plan = _spatial_plan(cfg, ctype, ch.profile, velocity_kmh, frequency_ghz,
-                                 int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol))), nb, frames_per_call)[0]
+                                 int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol))), nb, frames_per_call,
+                                 num_tx=sp['num_tx'], num_rx=sp['num_rx'], rank=sp['rank'],
+                                 detector=DETECTORS[sp['detector'].upper()], W=W)[0]
         elif mimo is not None:
             raise ValueError(f"unknown mimo mode {mimo!r}")
         elif coded:
@@ -804,7 +811,8 @@ class OFDMSimulator:
                 'bits': counts[:, 1], 'block_errors': counts[:, 2], 'blocks': counts[:, 3], 'plan': plan}
 
 
-def _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n_bits, max_frames=1):
+def _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n_bits, max_frames=1,
+                  num_tx=4, num_rx=4, rank=4, detector=C.DET_MMSE, W=None):
     ch = {'awgn': C.CH_AWGN, 'rayleigh_mp': C.CH_RAYLEIGH}.get(channel_type)
     if ch is None:
         raise ValueError(f"Tipo de canal desconocido: {channel_type}")
@@ -815,9 +823,13 @@ def _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz
         fD = doppler(frequency_ghz, velocity_kmh, itu_profile)
     else:
         delays, gains, fD = [], [], 0.0
+    if W is None:
+        W = np.eye(num_tx, dtype=complex)[:, :rank]
+    Wt = tuple(complex(v) for v in np.asarray(W, dtype=complex).ravel())
     return get_plan(N=config.N, Nc=config.Nc, cp_len=config.cp_length, bps=config.bits_per_symbol, n_sym=n_sym,
-                    chain=C.CHAIN_SPATIAL, channel=ch, num_rx=4, num_tx=4, delays=tuple(delays),
-                    gains=tuple(gains), fD=fD, fs=config.fs, n_bits=n_bits, max_frames=max_frames), gains, fD
+                    chain=C.CHAIN_SPATIAL, channel=ch, num_rx=num_rx, num_tx=num_tx, delays=tuple(delays),
+                    gains=tuple(gains), fD=fD, fs=config.fs, n_bits=n_bits, max_frames=max_frames, rank=rank,
+                    detector=detector, precoder=Wt), gains, fD
 
 
 def simulate_spatial_multiplexing(bits, num_tx=4, num_rx=2, rank='adaptive', detector_type='MMSE',
@@ -825,29 +837,25 @@ def simulate_spatial_multiplexing(bits, num_tx=4, num_rx=2, rank='adaptive', det
                                   itu_profile='Pedestrian_A', velocity_kmh=3, frequency_ghz=2.0,
                                   enable_csi_feedback=True, coherence_time_symbols=None, enable_parallel=False,
                                   codebook_type='TM4'):
-    """simulate_spatial_multiplexing (core/ofdm_core.py:2489-2815), config 5:
-    TM4 4x4, rank 4, PMI 0 (W = I4), CRS estimation on every OFDM symbol, MMSE
-    with the nominal sigma^2 = 10^(-SNR/10), layer demapping, hard decisions --
-    one GPU call.  Global-RNG consumption as the reference: H_initial (:2581,
-    drawn even at fixed rank) -> TX pilot reseeds per symbol and TX (cell
-    tx % 4) -> transmit_spatial_multiplexing draws (core/channel.py:397-493:
-    rayleigh_mp per link 16 phases per path for filter() and 16 per path for
-    impulse_response(); 'awgn' per link h ~ CN(0,1); then noise per RX) -> RX
-    pilot reseeds.  Rank adaptation, PMI search and the ZF / SIC / MRC
-    detectors are SURVEY §8f "next" and raise NotImplementedError."""
+    """simulate_spatial_multiplexing (core/ofdm_core.py:2489-2815): TM4 with
+    2 / 4 TX, 1-4 RX, rank 1-4 -- one GPU call.  Host: H_initial (:2573-2574,
+    drawn even at fixed rank) -> RankAdaptation.get_feedback on it for
+    rank='adaptive' with CSI (RI / PMI / W, core/rank_adaptation.py:212-265),
+    else the TM4 codebook's PMI 0 of the given rank (min(tx, rx) for
+    'adaptive' without CSI).  GPU: QAM -> layers (first ceil(Nd/rank) data
+    SCs, Q20) -> x = W layers -> CRS pilots per TX (cell tx % 4) -> IFFT/CP
+    -> transmit_spatial_multiplexing -> FFT -> CRS estimate per symbol ->
+    H_eff = H W -> MMSE / IRC / ZF / SIC / MRC with the nominal sigma^2 =
+    10^(-SNR/10) -> layer demap -> hard bits.  Global-RNG consumption as the
+    reference: H_initial -> TX pilot reseeds per symbol and TX -> channel draws
+    (core/channel.py:397-493: rayleigh_mp per link 16 phases per path for
+    filter() and 16 per path for impulse_response(); 'awgn' per link h ~
+    CN(0,1); then noise per RX) -> RX pilot reseeds."""
+    from .tm4 import DETECTORS, LTECodebook, RankAdaptation
     bits = np.asarray(bits)
     if bits.size == 0:
         raise ValueError("Bits array cannot be empty")
-    if str(detector_type).upper() not in ('MMSE', 'IRC'):
-        raise NotImplementedError(f"detector '{detector_type}': only MMSE/IRC is on the GPU path (SURVEY §8f)")
-    rank_used = min(num_tx, num_rx) if rank == 'adaptive' and not enable_csi_feedback else rank
-    if rank == 'adaptive' and enable_csi_feedback:
-        raise NotImplementedError("rank adaptation / CSI feedback (core/rank_adaptation.py) is SURVEY §8f 'next'; "
-                                  "pass rank=4 or enable_csi_feedback=False")
-    if num_tx != 4 or num_rx != 4 or int(rank_used) != 4:
-        raise NotImplementedError("spatial multiplexing on the GPU path: 4x4, rank 4 (TM4 PMI 0)")
-    if num_rx < int(rank_used):
-        raise ValueError(f"num_rx ({num_rx}) debe ser >= num_layers ({rank_used})")
+    det = DETECTORS.get(str(detector_type).upper())
     if config is None:
         config = LTEConfig(modulation=modulation)
     n0 = len(bits)
@@ -855,12 +863,26 @@ def simulate_spatial_multiplexing(bits, num_tx=4, num_rx=2, rank='adaptive', det
     Nd = len(grid._data)
     bpo = Nd * config.bits_per_symbol
     n_sym = int(np.ceil(n0 / bpo))
-    plan, gains, fD = _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n0)
+    H_initial = (np.random.randn(num_rx, num_tx) + 1j * np.random.randn(num_rx, num_tx)) / np.sqrt(2 * num_tx)
+    if rank == 'adaptive' and enable_csi_feedback:
+        fb = RankAdaptation(num_tx, num_rx, snr_db=snr_db).get_feedback(H_initial)
+        rank_used, pmi_used, W = fb['ri'], fb['pmi'], fb['W']
+    else:
+        rank_used = int(rank) if rank != 'adaptive' else min(num_tx, num_rx)
+        pmi_used = 0
+        W = LTECodebook(num_tx, transmission_mode='TM4', rank=rank_used).get_precoder(0)
+    if num_rx < rank_used:
+        raise ValueError(f"num_rx ({num_rx}) debe ser >= num_layers ({rank_used})")
+    if det is None:
+        raise ValueError(f"Detector '{detector_type}' no soportado")
+    if det == C.DET_MRC and rank_used != 1:
+        raise ValueError("MRC solo soporta num_layers=1 (rank-1)")
+    plan, gains, fD = _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n0,
+                                    num_tx=num_tx, num_rx=num_rx, rank=rank_used, detector=det, W=W)
     L = plan.L
     ray = channel_type == 'rayleigh_mp'
-    np.random.randn(num_rx, num_tx)                  # H_initial (core/ofdm_core.py:2581)
-    np.random.randn(num_rx, num_tx)
-    pidx = [grid._pilot[t::4] for t in range(num_tx)]
+    step = num_tx if num_tx <= 4 else 4
+    pidx = [grid._pilot[t % step::step] for t in range(num_tx)]
     for t in range(num_tx):
         _reseed_pilots(t % 4, len(pidx[t]))
     P = len(plan.desc.delays[:plan.desc.n_paths]) if ray else 0
@@ -901,5 +923,5 @@ def simulate_spatial_multiplexing(bits, num_tx=4, num_rx=2, rank='adaptive', det
             'bit_errors': err, 'errors': err, 'ber': float(err / n0), 'snr_db': float(snr_db),
             'num_tx': num_tx, 'num_rx': num_rx, 'rank': int(rank_used), 'detector_type': detector_type,
             'mode': 'Spatial Multiplexing TM4', 'codebook_type': codebook_type, 'channel_matrix': Hm,
-            'precoder_matrix': np.eye(4, dtype=complex), 'pmi_used': 0, 'velocity_kmh': velocity_kmh,
+            'precoder_matrix': W, 'pmi_used': pmi_used, 'velocity_kmh': velocity_kmh,
             'modulation': modulation, 'symbols_rx': out['data_syms'][0].astype(np.complex128)}

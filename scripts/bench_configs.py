@@ -47,6 +47,17 @@ def configs(lte_phy, C):
             return _spatial_plan(cfg, chan, 'Pedestrian_A', 3, 2.0, 14, 14 * nd * 6, F)[0]
         return f
 
+    def tm4(num_tx, num_rx, rank, det, pmi=0):
+        def f(F):
+            from lte_phy.ofdm_core import _spatial_plan, ResourceGrid
+            from lte_phy.tm4 import DETECTORS, LTECodebook
+            cfg = Cfg(bandwidth=20.0, modulation='64-QAM')
+            nd = len(ResourceGrid(cfg.N, cfg.Nc)._data)
+            W = LTECodebook(num_tx, transmission_mode='TM4', rank=rank).get_precoder(pmi)
+            return _spatial_plan(cfg, 'awgn', 'Pedestrian_A', 3, 2.0, 14, 14 * nd * 6, F, num_tx=num_tx,
+                                 num_rx=num_rx, rank=rank, detector=DETECTORS[det], W=W)[0]
+        return f
+
     return {
         'c1': ('config 1: SISO 1.25 MHz QPSK AWGN, 14 symbols uncoded', c1),
         'c2': ('config 2: SISO 20 MHz 64-QAM PedA + turbo (TB 27760)', c2),
@@ -54,6 +65,9 @@ def configs(lte_phy, C):
         'c4': ('config 4: SFBC 2x2 Alamouti + turbo, 20 MHz 64-QAM PedA (TB 27760)', c4),
         'c5': ('config 5: spatial 4x4 rank-4 MMSE, 20 MHz 64-QAM, flat CN(0,1) links', c5('awgn')),
         'c5r': ('config 5: spatial 4x4 rank-4 MMSE, 20 MHz 64-QAM, PedA 3 km/h links', c5('rayleigh_mp')),
+        'tm4_sic44': ('TM4 4x4 rank-4 SIC (PMI 1), 20 MHz 64-QAM, flat CN(0,1) links', tm4(4, 4, 4, 'SIC', 1)),
+        'tm4_zf22': ('TM4 2x2 rank-2 ZF (PMI 1), 20 MHz 64-QAM, flat CN(0,1) links', tm4(2, 2, 2, 'ZF', 1)),
+        'tm4_mrc41': ('TM4 4x1 rank-1 MRC (PMI 3), 20 MHz 64-QAM, flat CN(0,1) links', tm4(4, 1, 1, 'MRC', 3)),
     }
 
 

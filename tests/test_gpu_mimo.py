@@ -185,8 +185,9 @@ def test_mimo_argument_errors(C):
     sim = _sim(1.25, 'QPSK', 'awgn')
     with pytest.raises(ValueError):
         sim.simulate_mimo(np.array([], dtype=int), 10.0)
-    with pytest.raises(NotImplementedError):
-        lte_phy.simulate_spatial_multiplexing(np.ones(100, dtype=int), num_tx=4, num_rx=2, rank='adaptive')
+    with pytest.raises(NotImplementedError):      # 8 TX: outside the GPU path (num_tx 2 / 4)
+        lte_phy.simulate_spatial_multiplexing(np.ones(100, dtype=int), num_tx=8, num_rx=2, rank=2,
+                                              enable_csi_feedback=False)
     with pytest.raises(ValueError):
         lte_phy.OFDMChannel().transmit_mimo([])
     with pytest.raises(ValueError):

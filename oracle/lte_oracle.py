@@ -177,9 +177,21 @@ def ofdm_symbols_tx(num: Numerology, data_syms: np.ndarray, pil: np.ndarray) -> 
     return np.concatenate([td[:, num.N - num.cp:], td], axis=1).reshape(-1)
 
 
-def modulate_stream(num: Numerology, bits: np.ndarray):
-    """OFDMModulator.modulate_stream (core/modulator.py:252-302), 'lte' mode.
-    Returns (signal, list-of-per-symbol-data-symbols, n_sym)."""
+def dft_matrix(M: int, inverse: bool = False) -> np.ndarray:
+    """DFTPrecodifier._compute_dft_matrix / IDFTDecodifier._compute_idft_matrix
+    (core/dft_precoding.py:43-54, 156-175): exp(-+j 2 pi k n / M) / sqrt(M)."""
+    k = np.arange(M).reshape(-1, 1)
+    n = np.arange(M).reshape(1, -1)
+    sgn = 1j if inverse else -1j
+    return np.exp(sgn * 2 * np.pi * k * n / M) / np.sqrt(M)
+
+
+def modulate_stream(num: Numerology, bits: np.ndarray, sc_fdm: bool = False):
+    """OFDMModulator.modulate_stream (core/modulator.py:252-302), 'lte' mode;
+    sc_fdm: each OFDM symbol's Nd QAM symbols are multiplied by the M = Nd DFT
+    matrix before mapping (_modulate_lte :232-236, one matrix-vector product per
+    symbol as the reference).  Returns (signal, list-of-per-symbol QAM symbols
+    (un-precoded, as the reference returns them), n_sym)."""
     bits = np.asarray(bits)
     bpo = num.Nd * num.bps
     n_sym = int(np.ceil(len(bits) / bpo))
@@ -187,8 +199,12 @@ def modulate_stream(num: Numerology, bits: np.ndarray):
     if len(bits) < total:
         bits = np.pad(bits, (0, total - len(bits)), 'constant')
     syms = bits_to_symbols(bits[:total], num.modulation).reshape(n_sym, num.Nd)
+    mapped = syms
+    if sc_fdm:
+        D = dft_matrix(num.Nd)
+        mapped = np.stack([D @ syms[i] for i in range(n_sym)])
     pil = pilots(0, num.Np)                    # reseed side effect (Q1)
-    sig = ofdm_symbols_tx(num, syms, pil)
+    sig = ofdm_symbols_tx(num, mapped, pil)
     return sig, [syms[i] for i in range(n_sym)], n_sym
 
 
@@ -360,9 +376,10 @@ def estimate_periodic(num: Numerology, Yf: np.ndarray, slot: int = 14):
     return Hs, (np.mean(snrs) if snrs else 0.0)
 
 
-def receive(num: Numerology, y: np.ndarray, equalize=True):
-    """LTEReceiver.receive_and_decode data path (core/lte_receiver.py:259-316)
-    + OFDMDemodulator.demodulate_stream (core/demodulator.py:138-147).
+def receive(num: Numerology, y: np.ndarray, equalize=True, sc_fdm=False):
+    """LTEReceiver.receive_and_decode data path (core/lte_receiver.py:259-333)
+    + OFDMDemodulator.demodulate_stream (core/demodulator.py:138-147); sc_fdm:
+    the IDFT matrix applied to each symbol's Nd equalised data REs (:318-333).
     Returns (data symbols, bits, channel_snr_db)."""
     Yf = demod_stream(num, y)
     Hs, snr_db = estimate_periodic(num, Yf)
@@ -370,23 +387,28 @@ def receive(num: Numerology, y: np.ndarray, equalize=True):
         eq = np.stack([Yf[i] / (Hs[i] + 1e-6) for i in range(Yf.shape[0])])   # Q8
     else:
         eq = Yf
-    data = eq[:, num.data_idx].reshape(-1)
+    data = eq[:, num.data_idx]
+    if sc_fdm:
+        D = dft_matrix(num.Nd, inverse=True)
+        data = np.stack([D @ data[i] for i in range(data.shape[0])])
+    data = data.reshape(-1)
     return data, symbols_to_bits(data, num.modulation), snr_db
 
 
 def simulate_siso(num: Numerology, bits, snr_db, channel='awgn',
-                  profile='Pedestrian_A', fD=0.0, draws=None):
+                  profile='Pedestrian_A', fD=0.0, draws=None, sc_fdm=False):
     """OFDMSimulator.simulate_siso (core/ofdm_core.py:660-737).  draws=None
-    consumes the global RNG like the reference; else uses the given draws."""
+    consumes the global RNG like the reference; else uses the given draws.
+    sc_fdm: DFT precoding at TX and IDFT after ZF at RX."""
     bits = np.asarray(bits)
     if bits.size == 0:
         raise ValueError("Bits array cannot be empty")
     n0 = len(bits)
-    sig, syms, n_sym = modulate_stream(num, bits)
+    sig, syms, n_sym = modulate_stream(num, bits, sc_fdm)
     pa = papr(sig)
     d = None if draws is None else draws[0]
     rx = channel_transmit(num, sig, channel, snr_db, profile, fD, d)
-    data, brx, _ = receive(num, rx, True)
+    data, brx, _ = receive(num, rx, True, sc_fdm)
     if draws is None:
         pass  # reseed already happened inside estimate_channel
     brx = np.pad(brx, (0, n0 - len(brx))) if len(brx) < n0 else brx[:n0]
@@ -400,13 +422,15 @@ def simulate_siso(num: Numerology, bits, snr_db, channel='awgn',
 
 
 def simulate_simo(num: Numerology, bits, snr_db, num_rx=2, channel='awgn',
-                  profile='Pedestrian_A', fD=0.0, draws=None):
+                  profile='Pedestrian_A', fD=0.0, draws=None, sc_fdm=False):
     """OFDMSimulator.simulate_simo (core/ofdm_core.py:1536-1679) with
     transmit_simo (:361-412), _demodulate_with_channel_est (:1340-1403) and
-    _combine_symbols_mrc (:1405-1534), hard decision on the MRC output."""
+    _combine_symbols_mrc (:1405-1534), hard decision on the MRC output.
+    sc_fdm: the transmitter DFT-precodes but this receiver never applies the
+    IDFT (the reference's behaviour, BER ~ 0.5)."""
     bits = np.asarray(bits)
     n0 = len(bits)
-    sig, syms, n_sym = modulate_stream(num, bits)
+    sig, syms, n_sym = modulate_stream(num, bits, sc_fdm)
     pa = papr(sig)
     rxs = []
     for r in range(num_rx):

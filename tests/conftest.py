@@ -13,6 +13,7 @@ for p in (ROOT, PKG):
 GOLDEN = os.path.join(ROOT, 'tests', 'golden', 'golden.npz')
 GOLDEN_MIMO = os.path.join(ROOT, 'tests', 'golden', 'golden_mimo.npz')
 GOLDEN_TM4 = os.path.join(ROOT, 'tests', 'golden', 'golden_tm4.npz')
+GOLDEN_SCFDM = os.path.join(ROOT, 'tests', 'golden', 'golden_scfdm.npz')
 
 
 def pytest_configure(config):
@@ -49,6 +50,11 @@ def golden_mimo():
 @pytest.fixture(scope='session')
 def golden_tm4():
     return np.load(GOLDEN_TM4, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def golden_scfdm():
+    return np.load(GOLDEN_SCFDM, allow_pickle=False)
 
 
 @pytest.fixture(scope='session')

@@ -81,6 +81,12 @@ typedef struct {
   int32_t detector;        /* LTE_DET_*                                          */
   double precoder[32];     /* W [num_tx][rank] (LTECodebook.get_precoder, core/codebook_lte.py:
                             * 317-330): entry (t, c) at [(t*4 + c)*2] re, [+1] im */
+  /* SC-FDM (enable_sc_fdm, core/dft_precoding.py): the uncoded SISO / SIMO
+   * transmitters DFT-precode each symbol's Nd QAM symbols (core/modulator.py:
+   * 232-236); the uncoded SISO receiver applies the IDFT after ZF
+   * (core/lte_receiver.py:318-333).  As in the reference, the SIMO receiver
+   * does not de-precode and the coded chain ignores the flag. */
+  int32_t sc_fdm;
 } lte_plan_desc;
 
 typedef struct lte_plan lte_plan;
@@ -160,6 +166,10 @@ int lte_timing_reset(lte_plan *plan);
 int lte_fft_host(int N, int inverse, int64_t batch, const float *in, float *out);
 /* Pilots: PilotPattern.generate_pilots core/resource_mapper.py:137-152 (MT19937 seed(cell_id) + choice([1,-1])) */
 int lte_pilots(int cell_id, int n, double *out_re_im);
+/* SC-FDM DFT / IDFT of size M (<= 1024): DFTPrecodifier.precoding /
+ * IDFTDecodifier.decoding core/dft_precoding.py:66-118, 199-226 (unitary,
+ * 1/sqrt(M)); in / out [batch][M] complex64.  Bluestein on the device. */
+int lte_dft_host(int M, int inverse, int64_t batch, const float *in, float *out);
 /* Soft demap: _calculate_llrs_* core/ofdm_core.py:791-923 (bps 2/4/6) */
 int lte_llr_host(int bps, int64_t n, const float *syms, const float *noise_var, float *llr);
 /* Hard decision: QAMModulator.symbols_to_bits core/modulator.py:90-112 */

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <complex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -262,6 +263,48 @@ std::vector<float2> make_twiddles(int N) {
   return t;
 }
 
+// SC-FDM tables for the M-point DFT by Bluestein on N-point FFTs (N >= 2M - 1):
+// chirp[n] = exp(-i pi n^2 / M); bhat = FFT_N(b) / (N sqrt(M)) with the circular
+// b[m] = b[N - m] = exp(+i pi m^2 / M), |m| < M.  Angles reduced with exact
+// integer n^2 mod 2M; the FFT of b is a float64 radix-2 on the host.
+void make_bluestein(int N, int M, std::vector<float2>& chirp, std::vector<float2>& bhat) {
+  auto w = [M](int64_t m) {
+    const int64_t r = (m * m) % (2LL * M);
+    const double a = M_PI * (double)r / (double)M;
+    return std::complex<double>(std::cos(a), std::sin(a));
+  };
+  chirp.resize(M);
+  for (int n = 0; n < M; ++n) {
+    const std::complex<double> c = std::conj(w(n));
+    chirp[n] = make_float2((float)c.real(), (float)c.imag());
+  }
+  std::vector<std::complex<double>> b(N, 0.0);
+  for (int m = 0; m < M; ++m) {
+    b[m] = w(m);
+    if (m) b[N - m] = w(m);
+  }
+  // iterative radix-2 forward FFT, exp(-2 pi i k n / N)
+  for (int i = 1, j = 0; i < N; ++i) {
+    int bit = N >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) std::swap(b[i], b[j]);
+  }
+  for (int len = 2; len <= N; len <<= 1) {
+    const double a = -2.0 * M_PI / len;
+    for (int i = 0; i < N; i += len)
+      for (int k = 0; k < len / 2; ++k) {
+        const std::complex<double> tw(std::cos(a * k), std::sin(a * k));
+        const std::complex<double> u = b[i + k], v = b[i + k + len / 2] * tw;
+        b[i + k] = u + v;
+        b[i + k + len / 2] = u - v;
+      }
+  }
+  const double sc = 1.0 / ((double)N * std::sqrt((double)M));
+  bhat.resize(N);
+  for (int k = 0; k < N; ++k) bhat[k] = make_float2((float)(b[k].real() * sc), (float)(b[k].imag() * sc));
+}
+
 void make_pilots(int cell, int n, std::vector<double>& re_im) {
   MT19937 mt((uint32_t)cell);
   re_im.resize(2 * (size_t)n);
@@ -276,10 +319,10 @@ void make_pilots(int cell, int n, std::vector<double>& re_im) {
 struct TableSet {  // device copies of the static grid tables for one N
   DBuf<int32_t> data, pilot, seg;
   DBuf<float> inv_gap;
-  DBuf<float2> pilots, tw, constel;
+  DBuf<float2> pilots, tw, constel, chirp, bhat;
   void release() {
     data.release(); pilot.release(); seg.release(); inv_gap.release(); pilots.release(); tw.release();
-    constel.release();
+    constel.release(); chirp.release(); bhat.release();
   }
 };
 
@@ -660,6 +703,11 @@ static int plan_tables(lte_plan* p) {
       upload(p->tabs.inv_gap, p->gh.inv_gap) || upload(p->tabs.pilots, pil) ||
       upload(p->tabs.tw, make_twiddles(d.N)) || upload(p->tabs.constel, make_constellation(d.bps)))
     return fail(LTE_ENOMEM, "table upload failed");
+  if (d.sc_fdm) {   // SC-FDM DFT of size M = Nd (DFTPrecodifier, core/dft_precoding.py:20-118)
+    std::vector<float2> ch, bh;
+    make_bluestein(d.N, p->Nd, ch, bh);
+    if (upload(p->tabs.chirp, ch) || upload(p->tabs.bhat, bh)) return fail(LTE_ENOMEM, "table upload failed");
+  }
   return LTE_OK;
 }
 
@@ -951,7 +999,8 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
   p->grid = Grid{d.N, p->log2N, d.Nc, d.cp_len, p->Nd, p->Np, d.bps, p->n_sym, p->L, p->n_grp,
                  p->tabs.data.p, p->tabs.pilot.p, p->tabs.pilots.p, p->tabs.seg.p, p->tabs.inv_gap.p,
                  p->tabs.tw.p, p->tabs.constel.p,
-                 (float)(d.bps == 2 ? std::sqrt(2.0) : d.bps == 4 ? std::sqrt(10.0) : std::sqrt(42.0))};
+                 (float)(d.bps == 2 ? std::sqrt(2.0) : d.bps == 4 ? std::sqrt(10.0) : std::sqrt(42.0)),
+                 p->tabs.chirp.p, p->tabs.bhat.p};
   if (d.channel == LTE_CH_RAYLEIGH) {
     std::vector<int32_t> dl(d.delays, d.delays + d.n_paths);
     p->gains_f.assign(d.n_paths, 0.f);
@@ -1312,7 +1361,10 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
       cts = p->captx.p;
     }
     Timer t(p, KN_OFDM_TX);
-    LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B, cts));
+    // SC-FDM precodes the uncoded SISO / SIMO transmitters only: simulate_siso_coded
+    // builds its own grids without the precoder (core/ofdm_core.py:1062-1099)
+    LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B, cts,
+                        (d.sc_fdm && !coded) ? 1 : 0));
   } else {
     std::vector<float> hx((size_t)B * p->L * 2);
     for (int b = 0; b < B; ++b)
@@ -1360,7 +1412,10 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, p->H.p, p->npow.p, p->snr_lin.p,
                         p->fid.p, a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p, p->llr.p,
-                        cap_syms_dev, coded ? nullptr : cap_bits_dev));
+                        cap_syms_dev, coded ? nullptr : cap_bits_dev,
+                        // the IDFT runs in receive_and_decode only (core/lte_receiver.py:318-333): the SIMO
+                        // MRC receiver (core/ofdm_core.py:1340-1534) never de-precodes
+                        (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0));
   }
   if (coded && do_rx) {
     {
@@ -1465,6 +1520,30 @@ int lte_fft_host(int N, int inverse, int64_t batch, const float* in, float* out)
       launch_fft(nullptr, g, inverse, batch, di.p, dout.p) != 0 || hipDeviceSynchronize() != hipSuccess ||
       hipMemcpy(out, dout.p, batch * N * sizeof(float2), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "fft failed");
+  di.release(); dout.release(); t.release();
+  return rc;
+}
+
+int lte_dft_host(int M, int inverse, int64_t batch, const float* in, float* out) {
+  if (M < 1 || M > 1024 || batch < 0 || (!in && batch) || (!out && batch)) return fail(LTE_EINVAL, "bad dft arguments");
+  if (batch == 0) return LTE_OK;
+  int N = 64;
+  while (N < 2 * M - 1) N <<= 1;
+  TableSet t;
+  Grid g;
+  std::vector<float2> ch, bh;
+  make_bluestein(N, M, ch, bh);
+  if (stage_grid(N, t, g) || upload(t.chirp, ch) || upload(t.bhat, bh)) { t.release(); return fail(LTE_ENOMEM, "tables"); }
+  g.Nd = M;
+  g.chirp = t.chirp.p;
+  g.bhat = t.bhat.p;
+  DBuf<float2> di, dout;
+  if (di.alloc(batch * M) || dout.alloc(batch * M)) { t.release(); return fail(LTE_ENOMEM, "dft buffers"); }
+  int rc = LTE_OK;
+  if (hipMemcpy(di.p, in, batch * M * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+      launch_dft(nullptr, g, inverse, batch, di.p, dout.p) != 0 || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, dout.p, batch * M * sizeof(float2), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, "dft failed");
   di.release(); dout.release(); t.release();
   return rc;
 }

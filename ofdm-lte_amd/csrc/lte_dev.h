@@ -147,6 +147,27 @@ __device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __
   }
 }
 
+// SC-FDM DFT (DFTPrecodifier, core/dft_precoding.py:43-90: X_k = sum_n x_n
+// exp(-2 pi i k n / M) / sqrt(M), M = Nd) in place on buf[0, M), buf[M, N)
+// zero on entry.  Bluestein: X_k = conj(w_k) sum_n (x_n conj(w_n)) w_{k-n},
+// w_m = exp(i pi m^2 / M), the convolution by N-point LDS FFTs (N >= 2M - 1
+// since Nd < N/2).  The inverse (IDFTDecodifier) is conj(DFT(conj(x))).  All
+// threads of the block call it; it begins and ends with a barrier.
+__device__ __forceinline__ void dft_bluestein(float2* buf, const Grid& g, int tid, int T, bool active) {
+  __syncthreads();
+  if (active)
+    for (int n = tid; n < g.Nd; n += T) buf[n] = cmul(buf[n], g.chirp[n]);
+  __syncthreads();
+  fft_lds<false>(buf, g.N, g.log2N, g.tw, tid, active);
+  if (active)
+    for (int k = tid; k < g.N; k += T) buf[k] = cmul(buf[k], g.bhat[k]);
+  __syncthreads();
+  fft_lds<true>(buf, g.N, g.log2N, g.tw, tid, active);
+  if (active)
+    for (int k = tid; k < g.Nd; k += T) buf[k] = cmul(buf[k], g.chirp[k]);
+  __syncthreads();
+}
+
 // frame_err[b] += errs for every lane, with one atomic per distinct frame per
 // wave instead of one per lane (thousands of lanes of a frame otherwise
 // serialise on the same L2 address).  Must be reached by all lanes of the

@@ -23,6 +23,9 @@ struct Grid {                 // device pointers + numerology for one plan
   const float2* tw;           // [N]
   const float2* constel;      // [M]
   float qscale;               // sqrt(2) / sqrt(10) / sqrt(42)
+  // SC-FDM (M = Nd point DFT by Bluestein's chirp-z on N-point FFTs, Nd < N/2):
+  const float2* chirp;        // [Nd] exp(-i pi n^2 / Nd)
+  const float2* bhat;         // [N]  FFT_N(exp(+i pi m^2 / Nd), circular) / (N sqrt(Nd))
 };
 
 // launchers (return hipError_t as int)
@@ -31,7 +34,8 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
                   const CbInfo* cbi_dev, int C, int B);
 int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                   int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms = nullptr);
+                   int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms = nullptr,
+                   int sc_fdm = 0);
 int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* gains_dev, const uint64_t* fid,
                   uint64_t seed, const float* inj_ph, int64_t inj_stride, float* phases, float2* coef);
 int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
@@ -46,7 +50,7 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                    const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                    const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                    const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
-                   uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits);
+                   uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, int sc_fdm = 0);
 int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
                    const int64_t* rows, int C);
 int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
@@ -70,6 +74,7 @@ int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* cons
 int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, const int32_t* snr_idx,
                       const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts);
 int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);
+int launch_dft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);
 int launch_llr(hipStream_t s, int bps, int64_t n, const float2* syms, const float* nv, float* llr);
 int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* bits);
 

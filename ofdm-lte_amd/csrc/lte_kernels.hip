@@ -77,7 +77,9 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 // tx_map (rate_match_turbo + T/F interleaver, rate_matching.py:193-297,
 // ofdm_core.py:1040-1099), ResourceMapper.map_symbols (resource_mapper.py:
 // 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
-template <int CODED, int BPS>
+// SCF (SC-FDM, uncoded chains): the Nd QAM symbols of the OFDM symbol are
+// DFT-precoded (M = Nd, core/modulator.py:232-236) in a second LDS buffer first.
+template <int CODED, int BPS, bool SCF = false>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
                                                 const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B,
@@ -89,8 +91,11 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   const int b = gs / g.n_sym, l = gs - b * g.n_sym;
   const bool active = slot < spw && b < B;
   float2* buf = sm + slot * N;
+  float2* pre = SCF ? sm + (spw + slot) * N : buf;   // SC-FDM: QAM symbols -> DFT buffer
   if (active) {
     for (int k = tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
+    if constexpr (SCF)
+      for (int k = g.Nd + tid; k < N; k += T) pre[k] = make_float2(0.f, 0.f);
   }
   __syncthreads();
   if (active) {
@@ -115,10 +120,16 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
         for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, t0 + m);
       }
       const float2 sym = zero ? make_float2(0.f, 0.f) : qam_point<BPS>(idx);
-      buf[g.data_idx[j]] = sym;
+      if constexpr (SCF) pre[j] = sym;
+      else buf[g.data_idx[j]] = sym;
       if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + j] = sym;
     }
     for (int p = tid; p < g.Np; p += T) buf[g.pilot_idx[p]] = g.pilots[p];
+  }
+  if constexpr (SCF) {
+    dft_bluestein(pre, g, tid, T, active);
+    if (active)
+      for (int j = tid; j < g.Nd; j += T) buf[g.data_idx[j]] = pre[j];
   }
   __syncthreads();
   fft_lds<true>(buf, N, g.log2N, g.tw, tid, active);
@@ -131,19 +142,22 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
 }
 
 int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                   int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms) {
+                   int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms, int sc_fdm) {
   const int spw = WG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym;
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
+  if (sc_fdm && (coded || !g.chirp || !g.bhat || 2 * g.Nd > g.N)) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
-  const size_t shm = spw * g.N * sizeof(float2);
-#define LTE_TX(C_, B_)                                                                                             \
-  hipLaunchKernelGGL((k_ofdm_tx<C_, B_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words, tx_map, x, B, \
-                     cap_syms)
+  const size_t shm = (sc_fdm ? 2 : 1) * spw * g.N * sizeof(float2);
+#define LTE_TX(C_, B_, S_)                                                                                         \
+  hipLaunchKernelGGL((k_ofdm_tx<C_, B_, S_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words, tx_map, x, \
+                     B, cap_syms)
   if (coded) {
-    if (g.bps == 2) LTE_TX(1, 2); else if (g.bps == 4) LTE_TX(1, 4); else LTE_TX(1, 6);
+    if (g.bps == 2) LTE_TX(1, 2, false); else if (g.bps == 4) LTE_TX(1, 4, false); else LTE_TX(1, 6, false);
+  } else if (sc_fdm) {
+    if (g.bps == 2) LTE_TX(0, 2, true); else if (g.bps == 4) LTE_TX(0, 4, true); else LTE_TX(0, 6, true);
   } else {
-    if (g.bps == 2) LTE_TX(0, 2); else if (g.bps == 4) LTE_TX(0, 4); else LTE_TX(0, 6);
+    if (g.bps == 2) LTE_TX(0, 2, false); else if (g.bps == 4) LTE_TX(0, 4, false); else LTE_TX(0, 6, false);
   }
 #undef LTE_TX
   return (int)hipGetLastError();
@@ -363,7 +377,9 @@ int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float
 //  CODED:   ZF -> sigma2_eff (ofdm_core.py:1224-1243) -> LLRs (RE order)
 //  SIMO:    MRC sum conj(H_i)Y_i / (sum|H_i|^2 + 1e-10) (ofdm_core.py:1405-1534)
 // Templated on chain and bits/symbol so every per-RE array stays in VGPRs.
-template <int CHAIN, int BPS>
+//  SCF (SC-FDM, UNCODED): the ZF outputs of the symbol's Nd data REs go
+//       through the M = Nd IDFT (core/lte_receiver.py:318-333) before slicing.
+template <int CHAIN, int BPS, bool SCF = false>
 __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int num_rx,
                                                 const float2* __restrict__ y, int64_t y_rx_stride,
                                                 int64_t y_frame_stride, const float2* __restrict__ H,
@@ -418,6 +434,25 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
     }
     if constexpr (NRX > 1) __syncthreads();
   }
+  if constexpr (SCF) {   // IDFT(z) = conj(DFT(conj(z))) over the Nd data REs, in the (consumed) FFT buffer
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) {
+        const int j = tid + q * T;
+        if (j < g.Nd) buf[j] = make_float2(num[q].x, -num[q].y);
+      }
+      for (int k = g.Nd + tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
+    }
+    dft_bluestein(buf, g, tid, T, active);
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) {
+        const int j = tid + q * T;
+        if (j < g.Nd) num[q] = make_float2(buf[j].x, -buf[j].y);
+      }
+    }
+  }
   if (!active) return;
   uint32_t errs = 0;
   const uint32_t* fb = pw + (size_t)b * PW;
@@ -463,24 +498,25 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
   if (CHAIN != LTE_CHAIN_CODED && errs) atomicAdd(frame_err + b, errs);
 }
 
-template <int CHAIN, int BPS>
+template <int CHAIN, int BPS, bool SCF>
 static void rx_data_inst(hipStream_t s, int blocks, size_t shm, const Grid& g, int rayleigh, int B, int num_rx,
                          const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                          const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                          const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
                          uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits) {
-  hipLaunchKernelGGL((k_rx_data<CHAIN, BPS>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, num_rx, y, y_rx_stride,
-                     y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
-                     cap_syms, cap_bits);
+  hipLaunchKernelGGL((k_rx_data<CHAIN, BPS, SCF>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, num_rx, y,
+                     y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits,
+                     frame_err, llr, cap_syms, cap_bits);
 }
 
-template <int CHAIN>
+template <int CHAIN, bool SCF = false>
 static void rx_data_bps(int bps, hipStream_t s, int blocks, size_t shm, const Grid& g, int rayleigh, int B,
                         int num_rx, const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                         const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                         const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
                         uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits) {
-  auto* f = bps == 2 ? &rx_data_inst<CHAIN, 2> : (bps == 4 ? &rx_data_inst<CHAIN, 4> : &rx_data_inst<CHAIN, 6>);
+  auto* f = bps == 2 ? &rx_data_inst<CHAIN, 2, SCF>
+                     : (bps == 4 ? &rx_data_inst<CHAIN, 4, SCF> : &rx_data_inst<CHAIN, 6, SCF>);
   f(s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z,
     inj_stride, pw, PW, n_bits, frame_err, llr, cap_syms, cap_bits);
 }
@@ -489,8 +525,9 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                    int64_t y_rx_stride, int64_t y_frame_stride, const float2* H, const float* npow,
                    const float* snr_lin, const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride,
                    const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, float* llr, float2* cap_syms,
-                   uint8_t* cap_bits) {
+                   uint8_t* cap_bits, int sc_fdm) {
   if (g.bps != 2 && g.bps != 4 && g.bps != 6) return (int)hipErrorInvalidValue;
+  if (sc_fdm && (chain != LTE_CHAIN_UNCODED || !g.chirp || !g.bhat)) return (int)hipErrorInvalidValue;
   if (chain == LTE_CHAIN_SIMO && num_rx > 8) return (int)hipErrorInvalidValue;
   const int spw = WG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym;
@@ -505,6 +542,10 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
     rx_data_bps<LTE_CHAIN_SIMO>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H,
                                 npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
                                 cap_syms, cap_bits);
+  else if (sc_fdm)
+    rx_data_bps<LTE_CHAIN_UNCODED, true>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride,
+                                         y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW,
+                                         n_bits, frame_err, llr, cap_syms, cap_bits);
   else
     rx_data_bps<LTE_CHAIN_UNCODED>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride,
                                    H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
@@ -597,6 +638,44 @@ int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* 
   else if (bps == 4) hipLaunchKernelGGL(k_hard<4>, grid, dim3(WG), 0, s, n, syms, bits);
   else if (bps == 6) hipLaunchKernelGGL(k_hard<6>, grid, dim3(WG), 0, s, n, syms, bits);
   else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Stage entry: batched SC-FDM DFT / IDFT of size M = g.Nd (DFTPrecodifier.
+// precoding / IDFTDecodifier.decoding, core/dft_precoding.py:66-118, 199-226)
+// on host-supplied vectors; one slot per vector, the same dft_bluestein the
+// chains run in-line.
+__global__ __launch_bounds__(WG) void k_dft_stage(Grid g, int inverse, int64_t batch, const float2* __restrict__ in,
+                                                  float2* __restrict__ out) {
+  extern __shared__ float2 sm[];
+  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int64_t v = (int64_t)blockIdx.x * spw + slot;
+  const bool active = slot < spw && v < batch;
+  float2* buf = sm + slot * N;
+  if (active) {
+    for (int k = tid; k < N; k += T) {
+      float2 x = k < g.Nd ? in[v * g.Nd + k] : make_float2(0.f, 0.f);
+      if (inverse) x.y = -x.y;
+      buf[k] = x;
+    }
+  }
+  dft_bluestein(buf, g, tid, T, active);
+  if (active)
+    for (int k = tid; k < g.Nd; k += T) {
+      float2 x = buf[k];
+      if (inverse) x.y = -x.y;
+      out[v * g.Nd + k] = x;
+    }
+}
+
+int launch_dft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out) {
+  const int spw = WG / (g.N >> 3);
+  const int64_t blocks = (batch + spw - 1) / spw;
+  if (blocks > 0x7FFFFFFF || !g.chirp || !g.bhat || 2 * g.Nd - 1 > g.N) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dft_stage, dim3((unsigned)blocks), dim3(WG), spw * g.N * sizeof(float2), s, g, inverse, batch,
+                     in, out);
   return (int)hipGetLastError();
 }
 

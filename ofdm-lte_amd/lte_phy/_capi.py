@@ -31,7 +31,8 @@ class PlanDesc(ctypes.Structure):
                 ('chain', c_i32), ('channel', c_i32), ('num_rx', c_i32), ('n_paths', c_i32),
                 ('delays', c_i32 * MAX_PATHS), ('gains', c_f64 * MAX_PATHS), ('fD', c_f64), ('fs', c_f64),
                 ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32),
-                ('num_tx', c_i32), ('rank', c_i32), ('detector', c_i32), ('precoder', c_f64 * 32)]
+                ('num_tx', c_i32), ('rank', c_i32), ('detector', c_i32), ('precoder', c_f64 * 32),
+                ('sc_fdm', c_i32)]
 
 
 class RunArgs(ctypes.Structure):
@@ -68,6 +69,7 @@ _SIGS = {
     'lte_timing_reset': (ctypes.c_int, [ctypes.c_void_p]),
     'lte_fft_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float)]),
     'lte_pilots': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P(c_f64)]),
+    'lte_dft_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float)]),
     'lte_llr_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float), P(ctypes.c_float)]),
     'lte_hard_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_uint8)]),
     'lte_turbo_encode_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_uint8), P(ctypes.c_uint8)]),
@@ -149,6 +151,17 @@ def fft(x, inverse=False):
     N = x.shape[-1]
     out = np.empty_like(x)
     check(load().lte_fft_host(N, 1 if inverse else 0, x.size // N, ptr(x.view(np.float32), F32),
+                              ptr(out.view(np.float32), F32)))
+    return out
+
+
+def dft(x, inverse=False):
+    """SC-FDM DFT (inverse: IDFT) of size M = x.shape[-1], unitary (1/sqrt(M)), on the GPU."""
+    device_init()
+    x = np.ascontiguousarray(x, dtype=np.complex64)
+    M = x.shape[-1]
+    out = np.empty_like(x)
+    check(load().lte_dft_host(M, 1 if inverse else 0, x.size // M, ptr(x.view(np.float32), F32),
                               ptr(out.view(np.float32), F32)))
     return out
 

@@ -78,10 +78,12 @@ def _reseed_pilots(cell_id, n):
 
 
 def _check_mode(mode, enable_sc_fdm):
-    if enable_sc_fdm or mode == 'sc-fdm':
-        raise NotImplementedError("SC-FDM (DFT precoding) is not on the GPU path yet (SURVEY §8f rank 2)")
-    if mode != 'lte':
-        raise NotImplementedError(f"mode '{mode}' is not on the GPU path (only 'lte' resource mapping)")
+    """OFDMModulator mode rule (core/modulator.py:128-131): enable_sc_fdm or
+    mode 'sc-fdm' -> LTE mapping + DFT precoding.  Returns the SC-FDM flag."""
+    sc = bool(enable_sc_fdm) or mode == 'sc-fdm'
+    if mode not in ('lte', 'sc-fdm'):
+        raise NotImplementedError(f"mode '{mode}' is not on the GPU path (only 'lte' / 'sc-fdm' resource mapping)")
+    return sc
 
 
 def itu_paths(profile, fs, spatial=False):
@@ -141,9 +143,11 @@ class OFDMTransmitter:
     """OFDMTransmitter (core/ofdm_core.py:42-155)."""
 
     def __init__(self, config: LTEConfig, mode: str = 'lte', enable_sc_fdm: bool = False):
-        _check_mode(mode, enable_sc_fdm)
+        sc = _check_mode(mode, enable_sc_fdm)
         self.config, self.mode, self.enable_sc_fdm = config, mode, enable_sc_fdm
         self.modulator = _ModulatorView(config)
+        self.modulator.enable_sc_fdm = sc
+        self.modulator.mode = 'sc-fdm' if sc else mode
         self.grid = self.modulator.resource_mapper.grid
         self.last_signal_tx = self.last_symbols_tx = self.last_mapping_infos = None
 
@@ -164,7 +168,8 @@ class OFDMTransmitter:
         Nd = len(self.grid._data)
         n_sym = int(np.ceil(len(bits) / (Nd * cfg.bits_per_symbol)))
         plan = get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
-                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=len(bits), max_frames=1)
+                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=len(bits), max_frames=1,
+                        sc_fdm=int(self.modulator.enable_sc_fdm))
         r = plan.run([np.inf], bits=(np.asarray(bits) & 1).astype(np.uint8)[None], stages=C.STAGE_TX,
                      capture=('signal_tx', 'tx_syms'))
         _reseed_pilots(0, len(self.grid._pilot))
@@ -182,7 +187,7 @@ class OFDMTransmitter:
         return self.config
 
     def __repr__(self):
-        return f"OFDMTransmitter({self.config.modulation}, OFDM)"
+        return f"OFDMTransmitter({self.config.modulation}, {'SC-FDM' if self.enable_sc_fdm else 'OFDM'})"
 
 
 # ------------------------------------------------------------------ RX
@@ -200,7 +205,7 @@ class OFDMReceiver:
 
     def __init__(self, config: LTEConfig, mode: str = 'lte', enable_equalization: bool = True,
                  enable_sc_fdm: bool = False):
-        _check_mode(mode, enable_sc_fdm)
+        self._sc = _check_mode(mode, enable_sc_fdm)
         self.config, self.mode = config, mode
         self.enable_equalization, self.enable_sc_fdm = enable_equalization, enable_sc_fdm
         self.demodulator = _DemodulatorView(config)
@@ -223,7 +228,7 @@ class OFDMReceiver:
         Nd = len(self.grid._data)
         nb = n_sym * Nd * cfg.bits_per_symbol
         plan = get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
-                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=nb, max_frames=1)
+                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=nb, max_frames=1, sc_fdm=int(self._sc))
         r = plan.run([0.0], stages=C.STAGE_RX, in_signal=sig[None], capture=('data_syms', 'bits_rx'))
         _reseed_pilots(0, len(self.grid._pilot))
         syms = r['data_syms'][0].astype(np.complex128)
@@ -244,7 +249,7 @@ class OFDMReceiver:
         return self.config
 
     def __repr__(self):
-        return f"OFDMReceiver({self.config.modulation}, OFDM)"
+        return f"OFDMReceiver({self.config.modulation}, {'SC-FDM' if self.enable_sc_fdm else 'OFDM'})"
 
 
 # ------------------------------------------------------------------ channel
@@ -493,11 +498,15 @@ class OFDMSimulator:
         return len(self.grid._data)
 
     def _plan(self, chain, n_sym, n_bits, num_rx=1, max_frames=1, iters=8):
+        """SC-FDM (enable_sc_fdm / mode 'sc-fdm') reaches the uncoded SISO / SIMO
+        transmitters and the SISO receiver; simulate_siso_coded ignores it, as
+        the reference does (lte_plan_desc.sc_fdm, include/lte_phy.h)."""
         cfg, ch = self.config, self.channels[0]
+        sc = int(self.tx.modulator.enable_sc_fdm and chain in (C.CHAIN_UNCODED, C.CHAIN_SIMO))
         return get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
                         chain=chain, channel=ch.kind, num_rx=num_rx, delays=tuple(ch.delays),
                         gains=tuple(ch.gains), fD=ch.fD, fs=cfg.fs, n_bits=n_bits, turbo_iters=iters,
-                        max_frames=max_frames)
+                        max_frames=max_frames, sc_fdm=sc)
 
     def _ref_draws(self, L, num_rx=1):
         """Exactly the global-RNG consumption of one reference simulate_* call:

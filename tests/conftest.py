@@ -14,6 +14,7 @@ GOLDEN = os.path.join(ROOT, 'tests', 'golden', 'golden.npz')
 GOLDEN_MIMO = os.path.join(ROOT, 'tests', 'golden', 'golden_mimo.npz')
 GOLDEN_TM4 = os.path.join(ROOT, 'tests', 'golden', 'golden_tm4.npz')
 GOLDEN_SCFDM = os.path.join(ROOT, 'tests', 'golden', 'golden_scfdm.npz')
+GOLDEN_IMAGE = os.path.join(ROOT, 'tests', 'golden', 'golden_image.npz')
 
 
 def pytest_configure(config):
@@ -55,6 +56,11 @@ def golden_tm4():
 @pytest.fixture(scope='session')
 def golden_scfdm():
     return np.load(GOLDEN_SCFDM, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def golden_image():
+    return np.load(GOLDEN_IMAGE, allow_pickle=False)
 
 
 @pytest.fixture(scope='session')

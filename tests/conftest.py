@@ -15,6 +15,7 @@ GOLDEN_MIMO = os.path.join(ROOT, 'tests', 'golden', 'golden_mimo.npz')
 GOLDEN_TM4 = os.path.join(ROOT, 'tests', 'golden', 'golden_tm4.npz')
 GOLDEN_SCFDM = os.path.join(ROOT, 'tests', 'golden', 'golden_scfdm.npz')
 GOLDEN_IMAGE = os.path.join(ROOT, 'tests', 'golden', 'golden_image.npz')
+GOLDEN_BF = os.path.join(ROOT, 'tests', 'golden', 'golden_bf.npz')
 
 
 def pytest_configure(config):
@@ -61,6 +62,17 @@ def golden_scfdm():
 @pytest.fixture(scope='session')
 def golden_image():
     return np.load(GOLDEN_IMAGE, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def golden_bf():
+    return np.load(GOLDEN_BF, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def bf_oracle():
+    from oracle import bf_oracle
+    return bf_oracle
 
 
 @pytest.fixture(scope='session')

@@ -44,7 +44,12 @@ enum {
   /* TM4 spatial multiplexing, 2 / 4 TX x 1-4 RX, rank 1-4, codebook precoder,
    * MMSE / ZF / SIC / MRC detection: simulate_spatial_multiplexing
    * core/ofdm_core.py:2489-2815 (config 5 = 4x4, rank 4, PMI 0, MMSE) */
-  LTE_CHAIN_SPATIAL = 5
+  LTE_CHAIN_SPATIAL = 5,
+  /* beamforming, frequency domain only as in the reference: flat H per frame,
+   * rank-1 codebook PMI feedback, static codebook or adaptive MRT precoder, MRC:
+   * OFDMSimulator.simulate_beamforming core/ofdm_core.py:2260-2477.  num_tx
+   * 2 / 4 / 8, num_rx 1-8; L = n_sym * Nd REs per antenna (noise layout). */
+  LTE_CHAIN_BEAMFORMING = 6
 };
 /* MIMODetector.detector_type (core/mimo_detector.py:116-133); IRC == MMSE */
 enum { LTE_DET_MMSE = 0, LTE_DET_ZF = 1, LTE_DET_SIC = 2, LTE_DET_MRC = 3 };
@@ -87,6 +92,9 @@ typedef struct {
    * (core/lte_receiver.py:318-333).  As in the reference, the SIMO receiver
    * does not de-precode and the coded chain ignores the flag. */
   int32_t sc_fdm;
+  /* beamforming chain: 0 = update_mode 'static' (the CSI-feedback codebook
+   * vector), 1 = 'adaptive' (MRT, AdaptiveBeamforming) */
+  int32_t bf_adaptive;
 } lte_plan_desc;
 
 typedef struct lte_plan lte_plan;
@@ -139,6 +147,10 @@ typedef struct {
    * mean|y_link|^2, Re and Im of mean(y_link conj(x_tx)) -- the statistics
    * transmit_mimo reports its channel_matrix from (core/ofdm_core.py:505-516) */
   float *cap_link_stats;
+  /* beamforming capture: per frame PMI (CSIFeedback) and beamforming gain (dB);
+   * cap_H holds H [n_frames][num_rx][num_tx] for this chain */
+  int32_t *cap_pmi;
+  float *cap_bf_gain;
 } lte_run_args;
 
 /* Library / device. */

@@ -394,6 +394,11 @@ struct lte_plan {
   DBuf<int> kw_dev;
   // multi-antenna chains (lte_mimo.hip)
   bool mimo = false;
+  // beamforming chain (lte_bf.hip)
+  bool bf = false;
+  int bf_ncb = 0;
+  DBuf<double> bf_cb;
+  DBuf<BfFrame> bf_fr;
   int res = 0;                       // QAM symbols per OFDM symbol (= Nd for SISO / SIMO)
   MimoGrid mg{};
   DBuf<int32_t> m_np, m_ppos, m_pseg;
@@ -864,6 +869,8 @@ static int plan_alloc(lte_plan* p) {
     }
     bad |= p->Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
     bad |= p->Hm.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
+  } else if (p->bf) {
+    bad |= p->bf_fr.alloc(B) != 0;
   } else {
     bad |= p->x.alloc(B * p->L) != 0;
   }
@@ -873,7 +880,7 @@ static int plan_alloc(lte_plan* p) {
     bad |= p->coef.alloc(std::max<size_t>(B * rx * d.n_paths, 1)) != 0;
   }
   bad |= p->pow_part.alloc(B * rx * p->nblk) != 0;
-  if (!p->mimo) {
+  if (!p->mimo && !p->bf) {
     bad |= p->H.alloc(B * rx * p->n_grp * d.N) != 0;
     bad |= p->pstats.alloc(B * rx * p->n_grp * 2) != 0;
   }
@@ -917,13 +924,18 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
   if (d.N < 128 || d.N > 2048 || (d.N & (d.N - 1))) return fail(LTE_EUNSUP, "N must be a power of two in [128, 2048]");
   if (d.Nc <= 0 || d.Nc >= d.N || d.cp_len < 0 || d.cp_len > d.N) return fail(LTE_EINVAL, "bad Nc / cp_len");
   if (d.bps != 2 && d.bps != 4 && d.bps != 6) return fail(LTE_EINVAL, "Unsupported modulation");
-  if (d.chain < 0 || d.chain > LTE_CHAIN_SPATIAL) return fail(LTE_EINVAL, "bad chain");
+  if (d.chain < 0 || d.chain > LTE_CHAIN_BEAMFORMING) return fail(LTE_EINVAL, "bad chain");
   if (d.channel != LTE_CH_AWGN && d.channel != LTE_CH_RAYLEIGH) return fail(LTE_EINVAL, "Tipo de canal desconocido");
   if (d.num_rx < 1 || d.num_rx > 16) return fail(LTE_EINVAL, "num_rx must be >= 1");
-  const bool mimo = d.chain >= LTE_CHAIN_SFBC;
+  const bool bf = d.chain == LTE_CHAIN_BEAMFORMING;
+  const bool mimo = d.chain >= LTE_CHAIN_SFBC && !bf;
   const int num_tx = d.num_tx > 0 ? d.num_tx : 1;
-  if (!mimo && num_tx != 1) return fail(LTE_EINVAL, "num_tx > 1 needs a multi-antenna chain");
-  if (!mimo && d.chain != LTE_CHAIN_SIMO && d.num_rx != 1) return fail(LTE_EINVAL, "SISO chains need num_rx == 1");
+  if (!mimo && !bf && num_tx != 1) return fail(LTE_EINVAL, "num_tx > 1 needs a multi-antenna chain");
+  if (!mimo && !bf && d.chain != LTE_CHAIN_SIMO && d.num_rx != 1)
+    return fail(LTE_EINVAL, "SISO chains need num_rx == 1");
+  if (bf && num_tx != 2 && num_tx != 4 && num_tx != 8)
+    return fail(LTE_EINVAL, "num_tx=" + std::to_string(num_tx) + " no soportado en TM6");
+  if (bf && d.num_rx > LTE_BF_MAX_RX) return fail(LTE_EUNSUP, "beamforming: at most 8 RX antennas");
   if ((d.chain == LTE_CHAIN_SFBC || d.chain == LTE_CHAIN_SFBC_CODED) && num_tx != 2)
     return fail(LTE_EINVAL, "Alamouti SFBC requires exactly 2 TX antennas");
   if ((d.chain == LTE_CHAIN_SFBC || d.chain == LTE_CHAIN_SFBC_CODED) && d.num_rx > 8)
@@ -965,9 +977,31 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
     if ((int64_t)d.n_bits > (int64_t)p->n_sym * p->res * d.bps) { delete p; return fail(LTE_EINVAL, "n_bits exceeds frame capacity"); }
     p->PW = (p->n_sym * p->res * d.bps + 31) / 32 + 1;
   }
-  p->L = p->n_sym * (d.N + d.cp_len);
+  p->L = bf ? p->n_sym * p->Nd : p->n_sym * (d.N + d.cp_len);   // beamforming: REs per antenna
   p->n_grp = (p->n_sym + 13) / 14;
   p->nblk = (p->L + 255) / 256;
+  p->bf = bf;
+  if (bf) {   // rank-1 codebook (TM6 == TM4 rank 1), core/codebook_lte.py:58-96
+    std::vector<double> cb;
+    const double r2 = 1.0 / std::sqrt(2.0);
+    if (num_tx == 2) {
+      const double v[4][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}};
+      for (int i = 0; i < 4; ++i) {
+        cb.push_back(r2); cb.push_back(0.0);
+        cb.push_back(v[i][0] * r2); cb.push_back(v[i][1] * r2);
+      }
+    } else {
+      const double sc = num_tx == 4 ? 0.5 : 1.0 / std::sqrt(8.0);
+      for (int i = 0; i < 16; ++i)
+        for (int a = 0; a < num_tx; ++a) {
+          const double ph = 2.0 * M_PI * i * a / 16.0;
+          cb.push_back(std::cos(ph) * sc);
+          cb.push_back(std::sin(ph) * sc);
+        }
+    }
+    p->bf_ncb = (int)(cb.size() / (2 * num_tx));
+    if (upload(p->bf_cb, cb)) { p->tabs.release(); delete p; return fail(LTE_ENOMEM, "codebook upload"); }
+  }
   if (mimo) {
     MimoGrid& m = p->mg;
     m.mode = sfbc ? MIMO_SFBC : MIMO_SPATIAL;
@@ -1038,7 +1072,7 @@ int lte_plan_destroy(lte_plan* p) {
   p->blk_ptrs.release(); p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
   p->m_np.release(); p->m_ppos.release(); p->m_pseg.release(); p->m_pval.release(); p->Ym.release();
   p->Hm.release(); p->m_pig.release(); p->link_part.release(); p->link_sigma.release(); p->inj_lz.release();
-  p->inj_lh.release(); p->m_W.release();
+  p->inj_lh.release(); p->m_W.release(); p->bf_cb.release(); p->bf_fr.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -1266,6 +1300,80 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   return LTE_OK;
 }
 
+// Beamforming chain (frequency domain, flat H per frame).
+static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const uint32_t* inj_bits,
+                  int64_t inj_bits_stride, const float* inj_z, int64_t inj_z_stride) {
+  const lte_plan_desc& d = p->d;
+  hipStream_t s = p->stream;
+  const size_t links = (size_t)d.num_rx * d.num_tx;
+  const float* inj_h = nullptr;
+  int64_t inj_h_stride = 0;
+  if (a->link_h) {
+    const int nf = a->link_h_stride ? B : 1;
+    std::vector<float> hh((size_t)nf * links * 2);
+    for (int f = 0; f < nf; ++f)
+      for (size_t i = 0; i < links * 2; ++i) hh[f * links * 2 + i] = (float)a->link_h[(size_t)f * a->link_h_stride + i];
+    if (p->inj_lh.alloc(hh.size())) return fail(LTE_ENOMEM, "inj channel");
+    HIPCHK(hipMemcpyAsync(p->inj_lh.p, hh.data(), hh.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    inj_h = p->inj_lh.p;
+    inj_h_stride = a->link_h_stride ? (int64_t)links * 2 : 0;
+  }
+  {
+    Timer t(p, KN_PAYLOAD);
+    LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
+  }
+  float2* cap_syms_dev = nullptr;
+  uint8_t* cap_bits_dev = nullptr;
+  if (a->cap_data_syms) {
+    if (p->capbuf.alloc((size_t)B * p->L)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = p->capbuf.p;
+  }
+  if (a->cap_bits_rx) {
+    if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
+    cap_bits_dev = p->cap_bits.p;
+  }
+  {
+    Timer t(p, KN_RX_DATA);
+    LCHK(launch_bf(s, B, p->n_sym, p->Nd, d.bps, d.num_tx, d.num_rx, d.bf_adaptive, p->bf_ncb, p->bf_cb.p, p->fid.p,
+                   a->seed, inj_h, inj_h_stride, p->bf_fr.p, p->snr_lin.p, p->pw.p, p->PW, d.n_bits, inj_z,
+                   inj_z_stride, p->frame_err.p, cap_syms_dev, cap_bits_dev));
+  }
+  {
+    Timer t(p, KN_ACC);
+    LCHK(launch_accumulate(s, B, 0, d.n_bits, p->snr_idx.p, p->frame_err.p, p->frame_crc.p, p->counts.p));
+  }
+  std::vector<unsigned long long> hc((size_t)4 * n_snr);
+  HIPCHK(hipMemcpyAsync(hc.data(), p->counts.p, hc.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  if (a->frame_errors)
+    HIPCHK(hipMemcpyAsync(a->frame_errors, p->frame_err.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (a->cap_data_syms)
+    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->L * sizeof(float2), hipMemcpyDeviceToHost, s));
+  if (a->cap_bits_rx)
+    HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
+  std::vector<BfFrame> fr;
+  if (a->cap_H || a->cap_pmi || a->cap_bf_gain) {
+    fr.resize(B);
+    HIPCHK(hipMemcpyAsync(fr.data(), p->bf_fr.p, B * sizeof(BfFrame), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  if (p->timing) collect_timing(p);
+  for (int b = 0; b < (int)fr.size(); ++b) {
+    if (a->cap_H)
+      for (int r = 0; r < d.num_rx; ++r)
+        for (int t = 0; t < d.num_tx; ++t) {
+          float* o = a->cap_H + (((size_t)b * d.num_rx + r) * d.num_tx + t) * 2;
+          o[0] = fr[b].H[r][t].x;
+          o[1] = fr[b].H[r][t].y;
+        }
+    if (a->cap_pmi) a->cap_pmi[b] = fr[b].pmi;
+    if (a->cap_bf_gain) a->cap_bf_gain[b] = fr[b].gain_db;
+  }
+  if (a->counts)
+    for (size_t i = 0; i < hc.size(); ++i) a->counts[i] += hc[i];
+  return LTE_OK;
+}
+
 int lte_run(lte_plan* p, const lte_run_args* a) {
   if (!p || !a) return fail(LTE_EINVAL, "null argument");
   const lte_plan_desc& d = p->d;
@@ -1345,6 +1453,10 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (p->mimo) {
     if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "multi-antenna chains run all stages");
     return run_mimo(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_ph, inj_ph_stride, inj_z, inj_z_stride);
+  }
+  if (p->bf) {
+    if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "the beamforming chain runs all stages");
+    return run_bf(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_z, inj_z_stride);
   }
   if (do_tx || a->bits) {
     Timer t(p, KN_PAYLOAD);

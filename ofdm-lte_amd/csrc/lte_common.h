@@ -29,6 +29,7 @@ enum : uint32_t {
   RNG_STREAM_NOISE = 0x10000u, // + rx
   RNG_STREAM_MIMO_FADE = 0x20000u,  // + (rx*16 + tx)*16 + path
   RNG_STREAM_MIMO_LINK = 0x30000u,  // + rx*16 + tx : link noise (transmit_mimo) / flat link gain (spatial)
+  RNG_STREAM_BF = 0x40000u,         // + rx*num_tx + tx : beamforming flat channel H
 };
 
 __device__ __forceinline__ u32x4 rng4(uint64_t seed, uint64_t frame, uint32_t stream, uint32_t idx) {

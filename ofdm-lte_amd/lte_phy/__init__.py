@@ -12,9 +12,12 @@ from .ofdm_core import (ChannelSimulator, OFDMChannel, OFDMReceiver, OFDMSimulat
 from .ofdm_module import OFDMModule
 from . import channel_coding
 from .tm4 import LTECodebook, LayerMapper, MIMODetector, RankAdaptation
+from .beamforming import AdaptiveBeamforming, BeamformingPrecoder, CSIFeedback
+from .image_processing import ImageProcessor
 
 __version__ = '0.1.0'
 __all__ = ['LTEConfig', 'OFDMModule', 'OFDMSimulator', 'OFDMTransmitter', 'OFDMReceiver', 'OFDMChannel',
            'ChannelSimulator', 'simulate_spatial_multiplexing', 'channel_coding', 'LTECodebook', 'LayerMapper',
-           'MIMODetector', 'RankAdaptation', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
+           'MIMODetector', 'RankAdaptation', 'BeamformingPrecoder', 'AdaptiveBeamforming', 'CSIFeedback',
+           'ImageProcessor', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
            'LTE_PROFILES', 'CP_VALUES', 'SUBCARRIER_SPACING']

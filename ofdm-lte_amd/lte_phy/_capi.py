@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('LTE_HIP_LIB', os.path.join(_HERE, 'liblte_hip.so'))
 
 LTE_OK, LTE_EINVAL, LTE_EHIP, LTE_ENOMEM, LTE_ENODEV, LTE_EUNSUP = 0, -1, -2, -3, -4, -5
-CHAIN_UNCODED, CHAIN_CODED, CHAIN_SIMO, CHAIN_SFBC, CHAIN_SFBC_CODED, CHAIN_SPATIAL = 0, 1, 2, 3, 4, 5
+CHAIN_UNCODED, CHAIN_CODED, CHAIN_SIMO, CHAIN_SFBC, CHAIN_SFBC_CODED, CHAIN_SPATIAL, CHAIN_BEAMFORMING = 0, 1, 2, 3, 4, 5, 6
 CH_AWGN, CH_RAYLEIGH = 0, 1
 DET_MMSE, DET_ZF, DET_SIC, DET_MRC = 0, 1, 2, 3
 STAGE_TX, STAGE_CHANNEL, STAGE_RX, STAGE_ALL = 1, 2, 4, 7
@@ -32,7 +32,7 @@ class PlanDesc(ctypes.Structure):
                 ('delays', c_i32 * MAX_PATHS), ('gains', c_f64 * MAX_PATHS), ('fD', c_f64), ('fs', c_f64),
                 ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32),
                 ('num_tx', c_i32), ('rank', c_i32), ('detector', c_i32), ('precoder', c_f64 * 32),
-                ('sc_fdm', c_i32)]
+                ('sc_fdm', c_i32), ('bf_adaptive', c_i32)]
 
 
 class RunArgs(ctypes.Structure):
@@ -50,7 +50,8 @@ class RunArgs(ctypes.Structure):
                 ('cap_tx_syms', P(ctypes.c_float)),
                 ('link_noise', P(c_f64)), ('link_noise_stride', c_i64),
                 ('link_h', P(c_f64)), ('link_h_stride', c_i64),
-                ('cap_link_stats', P(ctypes.c_float))]
+                ('cap_link_stats', P(ctypes.c_float)),
+                ('cap_pmi', P(c_i32)), ('cap_bf_gain', P(ctypes.c_float))]
 
 
 # every symbol include/lte_phy.h declares, with its ctypes signature

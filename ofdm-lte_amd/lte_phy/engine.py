@@ -18,7 +18,7 @@ from . import _capi as C
 class Plan:
     def __init__(self, *, N, Nc, cp_len, bps, n_sym, chain, channel, num_rx=1, delays=(), gains=(), fD=0.0,
                  fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0, num_tx=1, rank=0, detector=0,
-                 precoder=(), sc_fdm=0):
+                 precoder=(), sc_fdm=0, bf_adaptive=0):
         C.device_init()
         d = C.PlanDesc()
         d.N, d.Nc, d.cp_len, d.bps, d.n_sym = N, Nc, cp_len, bps, n_sym
@@ -32,7 +32,7 @@ class Plan:
         d.fD, d.fs = float(fD), float(fs)
         d.n_bits, d.turbo_iters, d.max_frames, d.cell_id = int(n_bits), int(turbo_iters), int(max_frames), cell_id
         d.num_tx = int(num_tx)
-        d.rank, d.detector, d.sc_fdm = int(rank), int(detector), int(sc_fdm)
+        d.rank, d.detector, d.sc_fdm, d.bf_adaptive = int(rank), int(detector), int(sc_fdm), int(bf_adaptive)
         if rank and num_tx <= 4 and rank <= 4:   # W [num_tx][rank] -> the [4][4] table of lte_plan_desc.precoder
             #                                    (larger arrays: lte_plan_create rejects them, LTE_EUNSUP)
             W = np.asarray(precoder, dtype=np.complex128).reshape(int(num_tx), int(rank))
@@ -52,7 +52,8 @@ class Plan:
         self.chain = chain
         self.num_tx = int(num_tx)
         self.coded = chain in (C.CHAIN_CODED, C.CHAIN_SFBC_CODED)
-        self.mimo = chain >= C.CHAIN_SFBC
+        self.bf = chain == C.CHAIN_BEAMFORMING
+        self.mimo = chain >= C.CHAIN_SFBC and not self.bf
         sfbc = chain in (C.CHAIN_SFBC, C.CHAIN_SFBC_CODED)
         # multi-antenna geometry (lte_capi.hip lte_plan_create): REs per OFDM symbol,
         # data SCs carrying data, channel estimates per frame
@@ -150,6 +151,12 @@ class Plan:
                 'link_stats': ((B, self.num_rx, self.num_tx, 4), np.float32, 'cap_link_stats', C.F32)})
             shapes.pop('pilot_stats')
             shapes.pop('tx_syms')
+        if self.bf:
+            shapes.update({'H': ((B, self.num_rx, self.num_tx), np.complex64, 'cap_H', C.F32),
+                           'pmi': ((B,), np.int32, 'cap_pmi', C.I32),
+                           'bf_gain': ((B,), np.float32, 'cap_bf_gain', C.F32)})
+            for k in ('pilot_stats', 'tx_syms', 'signal_tx', 'signal_rx', 'llr', 'noise_power'):
+                shapes.pop(k)
         for name in capture:
             shp, dt, field, ct = shapes[name]
             arr = np.zeros(shp, dtype=dt)

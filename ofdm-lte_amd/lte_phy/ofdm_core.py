@@ -754,10 +754,20 @@ class OFDMSimulator:
                     progress_callback(int(done / (S * T) * 100), f"SNR: {snr:.1f} dB - Trial {t+1}/{T}")
         return {'snr_db': snrs, 'ber_mean': ber, 'ber_values': ber.copy(), 'papr_values': papr_v}
 
+    def simulate_beamforming(self, bits: np.ndarray, snr_db: float = 10.0, num_tx: int = 2, num_rx: int = 1,
+                             codebook_type: str = 'TM6', velocity_kmh: float = 3.0,
+                             update_mode: str = 'adaptive') -> Dict:
+        """core/ofdm_core.py:2260-2477 (frequency-domain TM6 beamforming with
+        CSI feedback; lte_phy/beamforming.py, LTE_CHAIN_BEAMFORMING)."""
+        from .beamforming import simulate_beamforming
+        return simulate_beamforming(self, self._bits_in(bits), snr_db, num_tx, num_rx, codebook_type, velocity_kmh,
+                                    update_mode)
+
     def run_grid(self, snr_range, num_trials: int, seed: int = 0, coded: bool = False, num_rx: int = 1,
                  n_bits: Optional[int] = None, frames_per_call: int = 4096, rank: int = 0, world_size: int = 1,
                  turbo_iters: int = 8, mimo: Optional[str] = None, velocity_kmh: float = 3,
-                 frequency_ghz: float = 2.0, spatial: Optional[Dict] = None) -> Dict:
+                 frequency_ghz: float = 2.0, spatial: Optional[Dict] = None,
+                 beamforming: Optional[Dict] = None) -> Dict:
         """Device-resident Monte-Carlo BER/BLER grid (SNR x trials).  Frame
         (s, t) has global id s*num_trials + t; all randomness is Philox keyed by
         (seed, id), so results are identical for any sharding.  With
@@ -769,7 +779,10 @@ class OFDMSimulator:
         mimo='spatial': TM4 (config 5 = 4x4 rank-4 PMI-0 MMSE; the spatial channel of
         simulate_spatial_multiplexing: gains converted once more, fD from
         velocity_kmh / frequency_ghz).  `spatial` overrides any of
-        {'num_tx': 4, 'num_rx': 4, 'rank': 4, 'detector': 'MMSE', 'pmi': 0}."""
+        {'num_tx': 4, 'num_rx': 4, 'rank': 4, 'detector': 'MMSE', 'pmi': 0}.
+        mimo='beamforming': simulate_beamforming's frequency-domain chain, H ~
+        CN(0, 1) per frame; `beamforming` overrides {'num_tx': 4, 'num_rx': 1,
+        'update_mode': 'adaptive'}."""
         snrs = np.atleast_1d(np.asarray(snr_range, dtype=np.float64))
         S, T = len(snrs), int(num_trials)
         cfg = self.config
@@ -796,6 +809,13 @@ class OFDMSimulator:
                                  int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol))), nb, frames_per_call,
                                  num_tx=sp['num_tx'], num_rx=sp['num_rx'], rank=sp['rank'],
                                  detector=DETECTORS[sp['detector'].upper()], W=W)[0]
+        elif mimo == 'beamforming':
+            from .beamforming import bf_plan
+            bfo = {'num_tx': 4, 'num_rx': 1, 'update_mode': 'adaptive'}
+            bfo.update(beamforming or {})
+            nb = int(n_bits or SLOT_SIZE * self.Nd * cfg.bits_per_symbol)
+            plan = bf_plan(cfg, int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol))), nb, bfo['num_tx'],
+                           bfo['num_rx'], bfo['update_mode'] == 'adaptive', frames_per_call)
         elif mimo is not None:
             raise ValueError(f"unknown mimo mode {mimo!r}")
         elif coded:

@@ -453,14 +453,13 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
       }
     }
   }
-  if (!active) return;
   uint32_t errs = 0;
   const uint32_t* fb = pw + (size_t)b * PW;
   const size_t fre = (size_t)b * g.n_sym * g.Nd;
 #pragma unroll
   for (int q = 0; q < QM; ++q) {
     const int j = tid + q * T;
-    if (j >= g.Nd) continue;
+    if (!active || j >= g.Nd) continue;
     const int re = l * g.Nd + j;
     float2 z = num[q];
     if constexpr (CHAIN == LTE_CHAIN_SIMO) {
@@ -495,7 +494,8 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
       }
     }
   }
-  if (CHAIN != LTE_CHAIN_CODED && errs) atomicAdd(frame_err + b, errs);
+  // one atomic per frame per wave (all lanes reach this point; inactive lanes carry 0)
+  if constexpr (CHAIN != LTE_CHAIN_CODED) frame_err_add(frame_err, b, errs);
 }
 
 template <int CHAIN, int BPS, bool SCF>

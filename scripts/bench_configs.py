@@ -58,6 +58,10 @@ def configs(lte_phy, C):
                                  num_rx=num_rx, rank=rank, detector=DETECTORS[det], W=W)[0]
         return f
 
+    def c2u(F):
+        s = O(Cfg(bandwidth=20.0, modulation='64-QAM'), channel_type='rayleigh_mp', itu_profile='Pedestrian_A')
+        return s._plan(C.CHAIN_UNCODED, 14, 14 * s.Nd * 6, max_frames=F)
+
     def scfdm(F):
         s = O(Cfg(bandwidth=20.0, modulation='64-QAM'), channel_type='rayleigh_mp', itu_profile='Pedestrian_A',
               enable_sc_fdm=True)
@@ -81,6 +85,7 @@ def configs(lte_phy, C):
         'tm4_sic44': ('TM4 4x4 rank-4 SIC (PMI 1), 20 MHz 64-QAM, flat CN(0,1) links', tm4(4, 4, 4, 'SIC', 1)),
         'tm4_zf22': ('TM4 2x2 rank-2 ZF (PMI 1), 20 MHz 64-QAM, flat CN(0,1) links', tm4(2, 2, 2, 'ZF', 1)),
         'tm4_mrc41': ('TM4 4x1 rank-1 MRC (PMI 3), 20 MHz 64-QAM, flat CN(0,1) links', tm4(4, 1, 1, 'MRC', 3)),
+        'c2u': ('SISO 20 MHz 64-QAM PedA, 14 symbols uncoded (OFDM, for the SC-FDM comparison)', c2u),
         'scfdm': ('SC-FDM SISO 20 MHz 64-QAM PedA, 14 symbols uncoded (M = 999 DFT)', scfdm),
         'bf81': ('beamforming 8x1 adaptive MRT, 20 MHz 64-QAM, 14 symbols (frequency domain)', bf(8, 1, True)),
     }

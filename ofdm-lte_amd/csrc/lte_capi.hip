@@ -535,8 +535,8 @@ int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int3
     ok = upload(dz, hz) == 0;
   }
   ok = ok && launch_channel(nullptr, g, 1, num_rx, ray ? 1 : 0, n_paths, ddel.p, dgain.p, (float)fD, (float)fs,
-                            dph.p, dcoef.p, dx.p, dy.p, dpp.p, nblk) == 0;
-  ok = ok && launch_npow(nullptr, 1, num_rx, dpp.p, nblk, (int)L, dsl.p, dnp.p) == 0;
+                            dph.p, dcoef.p, dx.p, dy.p, dpp.p, channel_nblk((int)L)) == 0;
+  ok = ok && launch_npow(nullptr, 1, num_rx, dpp.p, channel_nblk((int)L), (int)L, dsl.p, dnp.p) == 0;
   if (ok) {
     const float2* ys = ray ? dy.p : dx.p;
     hipLaunchKernelGGL(k_cap_rx, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
@@ -616,7 +616,8 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
   ok = ok && launch_channel_mimo(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dx.p, dy.p,
                                  link_noise_on ? 1 : 0, dfid.p, seed, (link_noise_on && link_noise) ? dlz.p : nullptr,
                                  0, dlp.p, dls.p, dpp.p, nblk) == 0;
-  ok = ok && launch_npow_mimo(nullptr, 1, num_rx, dpp.p, nblk, (int)L, dsl.p, mode == 0 ? 1.0f / num_tx : 1.0f,
+  ok = ok && launch_npow_mimo(nullptr, 1, num_rx, dpp.p, mimo_channel_nblk((int)L), (int)L, dsl.p,
+                              mode == 0 ? 1.0f / num_tx : 1.0f,
                               dnp.p) == 0;
   if (ok) {
     hipLaunchKernelGGL(k_cap_rx, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
@@ -1188,7 +1189,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                              link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, p->link_part.p,
                              p->link_sigma.p, p->pow_part.p, p->nblk));
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
-    LCHK(launch_npow_mimo(s, B, m.num_rx, p->pow_part.p, p->nblk, p->L, p->snr_lin.p,
+    LCHK(launch_npow_mimo(s, B, m.num_rx, p->pow_part.p, mimo_channel_nblk(p->L), p->L, p->snr_lin.p,
                           sfbc ? 1.0f / (float)m.num_tx : 1.0f, p->npow.p));
   }
   {
@@ -1502,8 +1503,8 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   {
     Timer t(p, KN_CHANNEL);
     LCHK(launch_channel(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
-                        p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, p->nblk));
-    LCHK(launch_npow(s, B, rx, p->pow_part.p, p->nblk, p->L, p->snr_lin.p, p->npow.p));
+                        p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, channel_nblk(p->L)));
+    LCHK(launch_npow(s, B, rx, p->pow_part.p, channel_nblk(p->L), p->L, p->snr_lin.p, p->npow.p));
   }
   if (do_rx) {
     Timer t(p, KN_RX_CHEST);

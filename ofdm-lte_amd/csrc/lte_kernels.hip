@@ -210,7 +210,26 @@ int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* ga
 // Channel: y[n] = sum_p g_p h_p[n] x[n - d_p] (RayleighChannel.filter,
 // rayleighchannel.py:44-58: stream-level delay with zero prefix, Q4) and the
 // per-block partial sums of |y|^2 for the measured-power SNR (channel.py:
-// 217-224, Q5).  AWGN: only the power of x.  grid (nblk, num_rx, B).
+// 217-224, Q5).  AWGN: only the power of x.  grid (nblk, num_rx, B); a block
+// streams CH_CHUNK samples, CH_PER per thread with a 256-sample stride (every
+// load / store instruction is one coalesced 2-KB row), then one block
+// reduction of the power.
+constexpr int CH_PER = 8, CH_CHUNK = WG * CH_PER;
+
+__device__ __forceinline__ float2 jakes_coef(const float* __restrict__ ph, float gain, float fD, float t) {
+  float sr = 0.f, si = 0.f;
+  for (int m = 0; m < 16; ++m) {   // jakes_fading with t = n / fs
+    const float al = 6.2831853071795864f * (float)(m + 1) / 16.0f;
+    const float arg = 6.2831853071795864f * fD * cosf(al) * t + ph[m];
+    float sv, cv;
+    sincosf(arg, &sv, &cv);
+    sr += cv;
+    si += sv;
+  }
+  const float k = sqrtf(2.0f / 16.0f) * gain;
+  return make_float2(sr * k, si * k);
+}
+
 __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh, int n_paths,
                                                 const int32_t* __restrict__ delays, const float* __restrict__ gains,
                                                 float fD, float fs, const float* __restrict__ phases,
@@ -218,48 +237,39 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
                                                 float2* __restrict__ y, float* __restrict__ pow_part, int nblk) {
   __shared__ float red[WG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
-  const int n = blk * WG + threadIdx.x;
   const int rx = blockIdx.y;
   const float2* xf = x + (size_t)b * L;
-  float2 v = make_float2(0.f, 0.f);
-  if (n < L) {
+  float2* yf = y + ((size_t)b * num_rx + rx) * L;
+  const size_t cb = ((size_t)b * num_rx + rx) * n_paths;
+  float pw = 0.f;
+#pragma unroll
+  for (int i = 0; i < CH_PER; ++i) {
+    const int n = blk * CH_CHUNK + i * WG + threadIdx.x;
+    if (n >= L) break;
+    float2 v = make_float2(0.f, 0.f);
     if (!rayleigh) {
       v = xf[n];
     } else {
-      const size_t cb = ((size_t)b * num_rx + rx) * n_paths;
       for (int p = 0; p < n_paths; ++p) {
         const int src = n - delays[p];
         if (src < 0) continue;
-        float2 c;
-        if (fD == 0.0f) {
-          c = coef[cb + p];
-        } else {  // jakes_fading with t = n / fs
-          const float* ph = phases + (cb + p) * 16;
-          float sr = 0.f, si = 0.f;
-          const float t = (float)n / fs;
-          for (int m = 0; m < 16; ++m) {
-            const float al = 6.2831853071795864f * (float)(m + 1) / 16.0f;
-            const float arg = 6.2831853071795864f * fD * cosf(al) * t + ph[m];
-            float s, cc;
-            sincosf(arg, &s, &cc);
-            sr += cc;
-            si += s;
-          }
-          const float k = sqrtf(2.0f / 16.0f) * gains[p];
-          c = make_float2(sr * k, si * k);
-        }
+        const float2 c = fD == 0.0f ? coef[cb + p] : jakes_coef(phases + (cb + p) * 16, gains[p], fD, (float)n / fs);
         v = cadd(v, cmul(c, xf[src]));
       }
-      y[((size_t)b * num_rx + rx) * L + n] = v;
+      yf[n] = v;
     }
+    pw += v.x * v.x + v.y * v.y;
   }
-  const float t = block_sum(v.x * v.x + v.y * v.y, red);
+  const float t = block_sum(pw, red);
   if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blk] = t;
 }
+
+int channel_nblk(int L) { return (L + CH_CHUNK - 1) / CH_CHUNK; }
 
 int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
                    const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
                    const float2* coef, const float2* x, float2* y, float* pow_part, int nblk) {
+  if (nblk != channel_nblk(g.L)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_channel, dim3(nblk * B, num_rx), dim3(WG), 0, s, g.L, num_rx, rayleigh, n_paths, delays_dev,
                      gains_dev, fD, fs, phases, coef, x, y, pow_part, nblk);
   return (int)hipGetLastError();

@@ -265,6 +265,11 @@ __global__ void k_link_sigma(int n_links_total, const float* __restrict__ part, 
   sigma[i] = (float)sqrt(acc / L / 1e10 * 0.5);
 }
 
+// All RX of one frame per block: each TX stream sample is loaded once for every
+// RX (the [rx][tx] link loop runs on registers), MC_PER samples per thread
+// with a 256-sample stride (coalesced rows), one power reduction per RX.
+constexpr int MC_PER = 8, MC_CHUNK = MWG * MC_PER, MC_MAXRX = 8;
+
 __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
                                                       const float2* __restrict__ coef, const float2* __restrict__ x,
@@ -274,48 +279,71 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
                                                       float* __restrict__ pow_part, int nblk) {
   __shared__ float red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
-  const int rx = blockIdx.y;
-  const int n = blk * MWG + threadIdx.x;
-  float2 v = make_float2(0.f, 0.f);
-  if (n < L) {
+  float pw[MC_MAXRX];
+#pragma unroll
+  for (int r = 0; r < MC_MAXRX; ++r) pw[r] = 0.f;
+#pragma unroll 1
+  for (int i = 0; i < MC_PER; ++i) {
+    const int n = blk * MC_CHUNK + i * MWG + threadIdx.x;
+    if (n >= L) break;
+    float2 v[MC_MAXRX];
+#pragma unroll
+    for (int r = 0; r < MC_MAXRX; ++r) v[r] = make_float2(0.f, 0.f);
     for (int tx = 0; tx < num_tx; ++tx) {
-      const size_t link = (size_t)rx * num_tx + tx;
-      const float2* cf = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3;
-      float2 yl = link_sample(cf, n_cs, np, n, sym_len, delays, x + ((size_t)b * num_tx + tx) * L);
-      if (link_sigma) {
-        const float sg = link_sigma[(size_t)b * num_rx * num_tx + link];
-        float2 z;
-        if (inj_lz) {
-          const float* zf = inj_lz + (size_t)b * inj_lz_stride + link * 2 * L;
-          z = make_float2(zf[n], zf[L + n]);
-        } else {
-          const u32x4 r = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
-          z = (n & 1) ? box_muller(r.z, r.w) : box_muller(r.x, r.y);
+      const float2* xf = x + ((size_t)b * num_tx + tx) * L;
+#pragma unroll
+      for (int r = 0; r < MC_MAXRX; ++r) {
+        if (r >= num_rx) break;
+        const size_t link = (size_t)r * num_tx + tx;
+        const float2* cf = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3;
+        float2 yl = link_sample(cf, n_cs, np, n, sym_len, delays, xf);
+        if (link_sigma) {
+          const float sg = link_sigma[(size_t)b * num_rx * num_tx + link];
+          float2 z;
+          if (inj_lz) {
+            const float* zf = inj_lz + (size_t)b * inj_lz_stride + link * 2 * L;
+            z = make_float2(zf[n], zf[L + n]);
+          } else {
+            const u32x4 rr = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
+            z = (n & 1) ? box_muller(rr.z, rr.w) : box_muller(rr.x, rr.y);
+          }
+          yl = make_float2(yl.x + sg * z.x, yl.y + sg * z.y);
         }
-        yl = make_float2(yl.x + sg * z.x, yl.y + sg * z.y);
+        v[r] = cadd(v[r], yl);
       }
-      v = cadd(v, yl);
     }
-    y[((size_t)b * num_rx + rx) * L + n] = v;
+#pragma unroll
+    for (int r = 0; r < MC_MAXRX; ++r) {
+      if (r >= num_rx) break;
+      y[((size_t)b * num_rx + r) * L + n] = v[r];
+      pw[r] += v[r].x * v[r].x + v[r].y * v[r].y;
+    }
   }
-  const float t = block_sum(v.x * v.x + v.y * v.y, red);
-  if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blk] = t;
+  for (int r = 0; r < num_rx; ++r) {
+    const float t = block_sum(pw[r < MC_MAXRX ? r : 0], red);
+    if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
+    __syncthreads();
+  }
 }
+
+int mimo_channel_nblk(int L) { return (L + MC_CHUNK - 1) / MC_CHUNK; }
 
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
                         const float2* coef, const float2* x, float2* y, int link_noise, const uint64_t* fid,
                         uint64_t seed, const float* inj_lz, int64_t inj_lz_stride, float* link_part,
                         float* link_sigma, float* pow_part, int nblk) {
   const int sym_len = g.N + g.cp;
+  if (m.num_rx > MC_MAXRX) return (int)hipErrorInvalidValue;
   if (link_noise) {
     hipLaunchKernelGGL(k_link_power, dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx,
                        n_paths, m.n_cs, sym_len, delays, coef, x, link_part, nblk);
     const int nl = B * m.num_rx * m.num_tx;
     hipLaunchKernelGGL(k_link_sigma, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nblk, g.L, link_sigma);
   }
-  hipLaunchKernelGGL(k_channel_mimo, dim3(nblk * B, m.num_rx), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths,
-                     m.n_cs, sym_len, delays, coef, x, y, link_noise ? link_sigma : nullptr, fid, seed, inj_lz,
-                     inj_lz_stride, pow_part, nblk);
+  const int nch = mimo_channel_nblk(g.L);
+  hipLaunchKernelGGL(k_channel_mimo, dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths, m.n_cs,
+                     sym_len, delays, coef, x, y, link_noise ? link_sigma : nullptr, fid, seed, inj_lz, inj_lz_stride,
+                     pow_part, nch);
   return (int)hipGetLastError();
 }
 

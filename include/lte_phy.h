@@ -95,6 +95,10 @@ typedef struct {
   /* beamforming chain: 0 = update_mode 'static' (the CSI-feedback codebook
    * vector), 1 = 'adaptive' (MRT, AdaptiveBeamforming) */
   int32_t bf_adaptive;
+  /* uncoded SISO receiver without ZF (OFDMSimulator / OFDMReceiver
+   * enable_equalization=False: receive_and_decode slices the raw FFT output,
+   * core/lte_receiver.py:294-299; the CRS estimate still runs) */
+  int32_t no_equalization;
 } lte_plan_desc;
 
 typedef struct lte_plan lte_plan;

@@ -1035,7 +1035,7 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
                  p->tabs.data.p, p->tabs.pilot.p, p->tabs.pilots.p, p->tabs.seg.p, p->tabs.inv_gap.p,
                  p->tabs.tw.p, p->tabs.constel.p,
                  (float)(d.bps == 2 ? std::sqrt(2.0) : d.bps == 4 ? std::sqrt(10.0) : std::sqrt(42.0)),
-                 p->tabs.chirp.p, p->tabs.bhat.p};
+                 p->tabs.chirp.p, p->tabs.bhat.p, d.no_equalization && d.chain == LTE_CHAIN_UNCODED ? 1 : 0};
   if (d.channel == LTE_CH_RAYLEIGH) {
     std::vector<int32_t> dl(d.delays, d.delays + d.n_paths);
     p->gains_f.assign(d.n_paths, 0.f);

@@ -26,6 +26,7 @@ struct Grid {                 // device pointers + numerology for one plan
   // SC-FDM (M = Nd point DFT by Bluestein's chirp-z on N-point FFTs, Nd < N/2):
   const float2* chirp;        // [Nd] exp(-i pi n^2 / Nd)
   const float2* bhat;         // [N]  FFT_N(exp(+i pi m^2 / Nd), circular) / (N sqrt(Nd))
+  int no_eq;                  // uncoded SISO: slice the raw FFT output (enable_equalization=False)
 };
 
 // launchers (return hipError_t as int)

@@ -436,7 +436,7 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
             num[q] = cadd(num[q], cmulc(Y, h));
             den[q] += h.x * h.x + h.y * h.y;
           } else {
-            num[q] = zf_div(Y, make_float2(h.x + 1e-6f, h.y));
+            num[q] = (CHAIN == LTE_CHAIN_UNCODED && g.no_eq) ? Y : zf_div(Y, make_float2(h.x + 1e-6f, h.y));
             den[q] = h.x * h.x + h.y * h.y;
           }
         }

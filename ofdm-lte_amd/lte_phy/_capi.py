@@ -32,7 +32,7 @@ class PlanDesc(ctypes.Structure):
                 ('delays', c_i32 * MAX_PATHS), ('gains', c_f64 * MAX_PATHS), ('fD', c_f64), ('fs', c_f64),
                 ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32),
                 ('num_tx', c_i32), ('rank', c_i32), ('detector', c_i32), ('precoder', c_f64 * 32),
-                ('sc_fdm', c_i32), ('bf_adaptive', c_i32)]
+                ('sc_fdm', c_i32), ('bf_adaptive', c_i32), ('no_equalization', c_i32)]
 
 
 class RunArgs(ctypes.Structure):

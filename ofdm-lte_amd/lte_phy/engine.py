@@ -18,7 +18,7 @@ from . import _capi as C
 class Plan:
     def __init__(self, *, N, Nc, cp_len, bps, n_sym, chain, channel, num_rx=1, delays=(), gains=(), fD=0.0,
                  fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0, num_tx=1, rank=0, detector=0,
-                 precoder=(), sc_fdm=0, bf_adaptive=0):
+                 precoder=(), sc_fdm=0, bf_adaptive=0, no_equalization=0):
         C.device_init()
         d = C.PlanDesc()
         d.N, d.Nc, d.cp_len, d.bps, d.n_sym = N, Nc, cp_len, bps, n_sym
@@ -33,6 +33,7 @@ class Plan:
         d.n_bits, d.turbo_iters, d.max_frames, d.cell_id = int(n_bits), int(turbo_iters), int(max_frames), cell_id
         d.num_tx = int(num_tx)
         d.rank, d.detector, d.sc_fdm, d.bf_adaptive = int(rank), int(detector), int(sc_fdm), int(bf_adaptive)
+        d.no_equalization = int(no_equalization)
         if rank and num_tx <= 4 and rank <= 4:   # W [num_tx][rank] -> the [4][4] table of lte_plan_desc.precoder
             #                                    (larger arrays: lte_plan_create rejects them, LTE_EUNSUP)
             W = np.asarray(precoder, dtype=np.complex128).reshape(int(num_tx), int(rank))

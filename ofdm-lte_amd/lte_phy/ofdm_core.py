@@ -217,8 +217,6 @@ class OFDMReceiver:
         CP removal + FFT, slot-0 CRS estimation, ZF, nearest-point bits."""
         if signal_rx.size == 0:
             raise ValueError("Received signal cannot be empty")
-        if not self.enable_equalization:
-            raise NotImplementedError("enable_equalization=False receive path is not on the GPU path")
         cfg = self.config
         sl = cfg.N + cfg.cp_length
         n_sym = max(1, len(signal_rx) // sl)
@@ -228,7 +226,8 @@ class OFDMReceiver:
         Nd = len(self.grid._data)
         nb = n_sym * Nd * cfg.bits_per_symbol
         plan = get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
-                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=nb, max_frames=1, sc_fdm=int(self._sc))
+                        chain=C.CHAIN_UNCODED, channel=C.CH_AWGN, n_bits=nb, max_frames=1, sc_fdm=int(self._sc),
+                        no_equalization=int(not self.enable_equalization))
         r = plan.run([0.0], stages=C.STAGE_RX, in_signal=sig[None], capture=('data_syms', 'bits_rx'))
         _reseed_pilots(0, len(self.grid._pilot))
         syms = r['data_syms'][0].astype(np.complex128)
@@ -503,10 +502,13 @@ class OFDMSimulator:
         the reference does (lte_plan_desc.sc_fdm, include/lte_phy.h)."""
         cfg, ch = self.config, self.channels[0]
         sc = int(self.tx.modulator.enable_sc_fdm and chain in (C.CHAIN_UNCODED, C.CHAIN_SIMO))
+        # enable_equalization reaches simulate_siso's receiver only (the coded and SIMO
+        # drivers build their own LTEReceivers, core/ofdm_core.py:1117-1122, 1369-1373)
+        noeq = int(not self.enable_equalization and chain == C.CHAIN_UNCODED)
         return get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
                         chain=chain, channel=ch.kind, num_rx=num_rx, delays=tuple(ch.delays),
                         gains=tuple(ch.gains), fD=ch.fD, fs=cfg.fs, n_bits=n_bits, turbo_iters=iters,
-                        max_frames=max_frames, sc_fdm=sc)
+                        max_frames=max_frames, sc_fdm=sc, no_equalization=noeq)
 
     def _ref_draws(self, L, num_rx=1):
         """Exactly the global-RNG consumption of one reference simulate_* call:

@@ -396,10 +396,11 @@ def receive(num: Numerology, y: np.ndarray, equalize=True, sc_fdm=False):
 
 
 def simulate_siso(num: Numerology, bits, snr_db, channel='awgn',
-                  profile='Pedestrian_A', fD=0.0, draws=None, sc_fdm=False):
+                  profile='Pedestrian_A', fD=0.0, draws=None, sc_fdm=False, equalize=True):
     """OFDMSimulator.simulate_siso (core/ofdm_core.py:660-737).  draws=None
     consumes the global RNG like the reference; else uses the given draws.
-    sc_fdm: DFT precoding at TX and IDFT after ZF at RX."""
+    sc_fdm: DFT precoding at TX and IDFT after ZF at RX (SURVEY §8f rank 2);
+    equalize=False: OFDMSimulator(enable_equalization=False), no ZF (:294-299)."""
     bits = np.asarray(bits)
     if bits.size == 0:
         raise ValueError("Bits array cannot be empty")
@@ -408,7 +409,7 @@ def simulate_siso(num: Numerology, bits, snr_db, channel='awgn',
     pa = papr(sig)
     d = None if draws is None else draws[0]
     rx = channel_transmit(num, sig, channel, snr_db, profile, fD, d)
-    data, brx, _ = receive(num, rx, True, sc_fdm)
+    data, brx, _ = receive(num, rx, equalize, sc_fdm)
     if draws is None:
         pass  # reseed already happened inside estimate_channel
     brx = np.pad(brx, (0, n0 - len(brx))) if len(brx) < n0 else brx[:n0]

@@ -71,12 +71,18 @@ def test_transmitter_sc_fdm(C, golden_scfdm):
     ('sc_c5m', 5.0, 'QPSK', 'awgn', [3], 'siso'),
     ('sc_c2', 20.0, '64-QAM', 'rayleigh_mp', [10, 20, 30], 'siso'),
     ('sc_c3', 10.0, '16-QAM', 'rayleigh_mp', [15], 'siso'),
-    ('sc_simo', 1.25, 'QPSK', 'awgn', [10], 'simo')])
+    ('sc_simo', 1.25, 'QPSK', 'awgn', [10], 'simo'),
+    ('noeq_c1', 1.25, 'QPSK', 'awgn', [5, 10], 'noeq'),
+    ('noeq_c2', 20.0, '16-QAM', 'rayleigh_mp', [20], 'noeq'),
+    ('noeq_sc', 1.25, 'QPSK', 'awgn', [10], 'noeq_sc')])
 def test_sc_fdm_ref_compat(C, golden_scfdm, name, bw, mod, chan, snrs, fn):
+    """SC-FDM drivers, and the receiver without equalisation (noeq*:
+    enable_equalization=False, with and without SC-FDM)."""
     import lte_phy
     g = golden_scfdm
     sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type=chan,
-                                enable_sc_fdm=True)
+                                enable_sc_fdm=fn != 'noeq', enable_equalization=not fn.startswith('noeq'))
+    fn = 'siso' if fn.startswith('noeq') else fn
     nb = int(g[name + '_nbits'][0])
     bits = unpack(g[name + '_bits'], nb).astype(np.int64)
     for snr in snrs:

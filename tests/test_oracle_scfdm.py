@@ -43,7 +43,10 @@ E2E = [('sc_c1', 1.25, 'QPSK', 'awgn', [0, 5, 10], 'siso'),
        ('sc_c5m', 5.0, 'QPSK', 'awgn', [3], 'siso'),
        ('sc_c2', 20.0, '64-QAM', 'rayleigh_mp', [10, 20, 30], 'siso'),
        ('sc_c3', 10.0, '16-QAM', 'rayleigh_mp', [15], 'siso'),
-       ('sc_simo', 1.25, 'QPSK', 'awgn', [10], 'simo')]
+       ('sc_simo', 1.25, 'QPSK', 'awgn', [10], 'simo'),
+       ('noeq_c1', 1.25, 'QPSK', 'awgn', [5, 10], 'noeq'),
+       ('noeq_c2', 20.0, '16-QAM', 'rayleigh_mp', [20], 'noeq'),
+       ('noeq_sc', 1.25, 'QPSK', 'awgn', [10], 'noeq_sc')]
 
 
 @pytest.mark.parametrize('name,bw,mod,chan,snrs,fn', E2E)
@@ -56,6 +59,8 @@ def test_end_to_end_sc_fdm(golden_scfdm, oracle, name, bw, mod, chan, snrs, fn):
         k = f'{name}_snr{snr}'
         if fn == 'siso':
             r = oracle.simulate_siso(num, bits, snr, channel=chan, sc_fdm=True)
+        elif fn.startswith('noeq'):
+            r = oracle.simulate_siso(num, bits, snr, channel=chan, sc_fdm=fn == 'noeq_sc', equalize=False)
         else:
             r = oracle.simulate_simo(num, bits, snr, num_rx=2, channel=chan, sc_fdm=True)
         assert r['bit_errors'] == g[k + '_errors'][0], (k, r['bit_errors'], g[k + '_errors'][0])

@@ -75,7 +75,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--frames', type=int, default=32768, help='subframes per step per GPU')
+    ap.add_argument('--frames', type=int, default=65536, help='subframes per step per GPU (65536: 5120 turbo waves = 5 per SIMD, the VGPR-bound occupancy)')
     ap.add_argument('--iters', type=int, default=8)
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')

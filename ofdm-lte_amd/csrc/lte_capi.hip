@@ -535,7 +535,8 @@ int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int3
     ok = upload(dz, hz) == 0;
   }
   ok = ok && launch_channel(nullptr, g, 1, num_rx, ray ? 1 : 0, n_paths, ddel.p, dgain.p, (float)fD, (float)fs,
-                            dph.p, dcoef.p, dx.p, dy.p, dpp.p, channel_nblk((int)L)) == 0;
+                            dph.p, dcoef.p, dx.p, dy.p, dpp.p, channel_nblk((int)L),
+                            ray ? *std::max_element(delays, delays + n_paths) : 0) == 0;
   ok = ok && launch_npow(nullptr, 1, num_rx, dpp.p, channel_nblk((int)L), (int)L, dsl.p, dnp.p) == 0;
   if (ok) {
     const float2* ys = ray ? dy.p : dx.p;
@@ -1503,7 +1504,8 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   {
     Timer t(p, KN_CHANNEL);
     LCHK(launch_channel(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
-                        p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, channel_nblk(p->L)));
+                        p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, channel_nblk(p->L),
+                        ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0));
     LCHK(launch_npow(s, B, rx, p->pow_part.p, channel_nblk(p->L), p->L, p->snr_lin.p, p->npow.p));
   }
   if (do_rx) {

@@ -41,7 +41,7 @@ int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* ga
                   uint64_t seed, const float* inj_ph, int64_t inj_stride, float* phases, float2* coef);
 int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
                    const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
-                   const float2* coef, const float2* x, float2* y, float* pow_part, int nblk);
+                   const float2* coef, const float2* x, float2* y, float* pow_part, int nblk, int max_delay);
 int launch_npow(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
                 float* npow);
 int channel_nblk(int L);   // power partials per (frame, rx) written by launch_channel

@@ -230,21 +230,42 @@ __device__ __forceinline__ float2 jakes_coef(const float* __restrict__ ph, float
   return make_float2(sr * k, si * k);
 }
 
+// Rayleigh with every delay <= CH_HALO: the chunk plus its delay halo is staged
+// in LDS once with 16-B loads (2 samples per lane), so the n_paths delayed taps
+// read LDS instead of re-fetching x through L1/L2 (the kernel was latency
+// bound at ~2.2 TB/s); otherwise the taps load from global memory.
+constexpr int CH_HALO = 256;
+
 __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh, int n_paths,
                                                 const int32_t* __restrict__ delays, const float* __restrict__ gains,
                                                 float fD, float fs, const float* __restrict__ phases,
                                                 const float2* __restrict__ coef, const float2* __restrict__ x,
-                                                float2* __restrict__ y, float* __restrict__ pow_part, int nblk) {
+                                                float2* __restrict__ y, float* __restrict__ pow_part, int nblk,
+                                                int staged) {
   __shared__ float red[WG / 64];
+  __shared__ float2 xs[CH_CHUNK + CH_HALO];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
   const int rx = blockIdx.y;
   const float2* xf = x + (size_t)b * L;
   float2* yf = y + ((size_t)b * num_rx + rx) * L;
   const size_t cb = ((size_t)b * num_rx + rx) * n_paths;
+  const int n0 = blk * CH_CHUNK;
   float pw = 0.f;
+  if (rayleigh && staged) {
+    const float4* x4 = reinterpret_cast<const float4*>(xf);
+    for (int e = threadIdx.x; e < (CH_CHUNK + CH_HALO) / 2; e += WG) {
+      const int n = n0 - CH_HALO + 2 * e;   // even: 16-B aligned pair (L is even)
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n >= 0 && n + 1 < L) v = x4[n >> 1];
+      else if (n >= 0 && n < L) v.x = xf[n].x, v.y = xf[n].y;
+      xs[2 * e] = make_float2(v.x, v.y);
+      xs[2 * e + 1] = make_float2(v.z, v.w);
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < CH_PER; ++i) {
-    const int n = blk * CH_CHUNK + i * WG + threadIdx.x;
+    const int n = n0 + i * WG + threadIdx.x;
     if (n >= L) break;
     float2 v = make_float2(0.f, 0.f);
     if (!rayleigh) {
@@ -254,7 +275,7 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
         const int src = n - delays[p];
         if (src < 0) continue;
         const float2 c = fD == 0.0f ? coef[cb + p] : jakes_coef(phases + (cb + p) * 16, gains[p], fD, (float)n / fs);
-        v = cadd(v, cmul(c, xf[src]));
+        v = cadd(v, cmul(c, staged ? xs[src - n0 + CH_HALO] : xf[src]));
       }
       yf[n] = v;
     }
@@ -268,10 +289,12 @@ int channel_nblk(int L) { return (L + CH_CHUNK - 1) / CH_CHUNK; }
 
 int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
                    const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
-                   const float2* coef, const float2* x, float2* y, float* pow_part, int nblk) {
+                   const float2* coef, const float2* x, float2* y, float* pow_part, int nblk, int max_delay) {
   if (nblk != channel_nblk(g.L)) return (int)hipErrorInvalidValue;
+  // staging uses 16-B pairs: every frame's stream must start 16-B aligned (L even)
+  const int staged = rayleigh && max_delay >= 0 && max_delay <= CH_HALO && (g.L & 1) == 0;
   hipLaunchKernelGGL(k_channel, dim3(nblk * B, num_rx), dim3(WG), 0, s, g.L, num_rx, rayleigh, n_paths, delays_dev,
-                     gains_dev, fD, fs, phases, coef, x, y, pow_part, nblk);
+                     gains_dev, fD, fs, phases, coef, x, y, pow_part, nblk, staged);
   return (int)hipGetLastError();
 }
 

@@ -133,16 +133,29 @@ __device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __
     return;
   }
   const int p0 = off >> 1, p1 = (off + N - 1) >> 1;
-  for (int p = p0 + tid; p <= p1; p += T) {
+  // every sample load of this thread is issued before the first Philox call
+  // (the loop was latency bound with one pair in flight); T = N/8 threads
+  // cover the N/2 (+1) pairs in at most 5 rounds
+  constexpr int MAXR = 5;
+  float2 va[MAXR], vb[MAXR];
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int p = p0 + tid + i * T, n0 = 2 * p;
+    va[i] = (p <= p1 && n0 >= off) ? yf[n0] : make_float2(0.f, 0.f);
+    vb[i] = (p <= p1 && n0 + 1 < off + N) ? yf[n0 + 1] : make_float2(0.f, 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int p = p0 + tid + i * T, n0 = 2 * p;
+    if (p > p1) break;
     const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
-    const int n0 = 2 * p;
     if (n0 >= off) {
-      const float2 z = box_muller(r.x, r.y), v = yf[n0];
-      buf[n0 - off] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+      const float2 z = box_muller(r.x, r.y);
+      buf[n0 - off] = make_float2(va[i].x + sigma * z.x, va[i].y + sigma * z.y);
     }
     if (n0 + 1 < off + N) {
-      const float2 z = box_muller(r.z, r.w), v = yf[n0 + 1];
-      buf[n0 + 1 - off] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+      const float2 z = box_muller(r.z, r.w);
+      buf[n0 + 1 - off] = make_float2(vb[i].x + sigma * z.x, vb[i].y + sigma * z.y);
     }
   }
 }

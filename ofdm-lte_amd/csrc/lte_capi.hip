@@ -575,7 +575,8 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
   m.num_rx = num_rx;
   m.n_cs = (ray && fD != 0.0) ? (int)((L + chunk - 1) / chunk) : 1;
   const int np = ray ? n_paths : 1;
-  const int nblk = (int)((L + 255) / 256);
+  // partial-sum slots: 256-sample blocks (link stats) or OFDM-symbol blocks (channel), whichever is more
+  const int nblk = std::max((int)((L + 255) / 256), mimo_channel_nblk((int)L, g.N + g.cp));
   const size_t links = (size_t)num_rx * num_tx;
   const bool link_noise_on = mode == 0 && ray;
   DBuf<float2> dx, dy, dcoef, dout;
@@ -617,7 +618,7 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
   ok = ok && launch_channel_mimo(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dx.p, dy.p,
                                  link_noise_on ? 1 : 0, dfid.p, seed, (link_noise_on && link_noise) ? dlz.p : nullptr,
                                  0, dlp.p, dls.p, dpp.p, nblk) == 0;
-  ok = ok && launch_npow_mimo(nullptr, 1, num_rx, dpp.p, mimo_channel_nblk((int)L), (int)L, dsl.p,
+  ok = ok && launch_npow_mimo(nullptr, 1, num_rx, dpp.p, mimo_channel_nblk((int)L, g.N + g.cp), (int)L, dsl.p,
                               mode == 0 ? 1.0f / num_tx : 1.0f,
                               dnp.p) == 0;
   if (ok) {
@@ -981,7 +982,7 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
   }
   p->L = bf ? p->n_sym * p->Nd : p->n_sym * (d.N + d.cp_len);   // beamforming: REs per antenna
   p->n_grp = (p->n_sym + 13) / 14;
-  p->nblk = (p->L + 255) / 256;
+  p->nblk = bf ? (p->L + 255) / 256 : std::max((p->L + 255) / 256, mimo_channel_nblk(p->L, d.N + d.cp_len));
   p->bf = bf;
   if (bf) {   // rank-1 codebook (TM6 == TM4 rank 1), core/codebook_lte.py:58-96
     std::vector<double> cb;
@@ -1190,7 +1191,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                              link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, p->link_part.p,
                              p->link_sigma.p, p->pow_part.p, p->nblk));
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
-    LCHK(launch_npow_mimo(s, B, m.num_rx, p->pow_part.p, mimo_channel_nblk(p->L), p->L, p->snr_lin.p,
+    LCHK(launch_npow_mimo(s, B, m.num_rx, p->pow_part.p, mimo_channel_nblk(p->L, g.N + g.cp), p->L, p->snr_lin.p,
                           sfbc ? 1.0f / (float)m.num_tx : 1.0f, p->npow.p));
   }
   {

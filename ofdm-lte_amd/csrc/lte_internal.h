@@ -110,7 +110,7 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
                         const float2* coef, const float2* x, float2* y, int link_noise, const uint64_t* fid,
                         uint64_t seed, const float* inj_lz, int64_t inj_lz_stride, float* link_part,
                         float* link_sigma, float* pow_part, int nblk);
-int mimo_channel_nblk(int L);   // power partials per (frame, rx) written by launch_channel_mimo
+int mimo_channel_nblk(int L, int sym_len);   // power partials per (frame, rx) written by launch_channel_mimo
 int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
                       const float2* coef, const float2* x, float* part, int nblk, float* stats);
 int launch_npow_mimo(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,

@@ -236,7 +236,11 @@ __device__ __forceinline__ float2 link_sample(const float2* __restrict__ cf, int
   return acc;
 }
 
-// pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal
+// pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
+// one block per (frame, OFDM symbol, link) like k_channel_mimo
+__device__ __forceinline__ float2 link_sample_sym(const float2* __restrict__ cs, int n_cs, int np, int n, float d,
+                                                  const int32_t* __restrict__ delays, const float2* __restrict__ xf);
+
 __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                     const int32_t* __restrict__ delays,
                                                     const float2* __restrict__ coef, const float2* __restrict__ x,
@@ -244,12 +248,15 @@ __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_t
   __shared__ float red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
   const int link = blockIdx.y, rx = link / num_tx, tx = link - rx * num_tx;
-  const int n = blk * MWG + threadIdx.x;
+  const int sidx = n_cs > 1 ? blk : 0;
+  const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
+  const float dc = 0.5f * (float)(sym_len - 1);
+  const float2* cs = coef + (((size_t)b * num_rx + rx) * num_tx + tx) * np * n_cs * 3 + (size_t)sidx * 3;
+  const float2* xf = x + ((size_t)b * num_tx + tx) * L;
   float v = 0.f;
-  if (n < L) {
-    const float2* cf = coef + (((size_t)b * num_rx + rx) * num_tx + tx) * np * n_cs * 3;
-    const float2 yv = link_sample(cf, n_cs, np, n, sym_len, delays, x + ((size_t)b * num_tx + tx) * L);
-    v = yv.x * yv.x + yv.y * yv.y;
+  for (int n = nbeg + threadIdx.x; n < nend; n += MWG) {
+    const float2 yv = link_sample_sym(cs, n_cs, np, n, n_cs > 1 ? (float)(n - nbeg) - dc : 0.f, delays, xf);
+    v += yv.x * yv.x + yv.y * yv.y;
   }
   const float t = block_sum(v, red);
   if (threadIdx.x == 0) part[(((size_t)b * num_rx * num_tx) + link) * nblk + blk] = t;
@@ -265,10 +272,30 @@ __global__ void k_link_sigma(int n_links_total, const float* __restrict__ part, 
   sigma[i] = (float)sqrt(acc / L / 1e10 * 0.5);
 }
 
-// All RX of one frame per block: each TX stream sample is loaded once for every
-// RX (the [rx][tx] link loop runs on registers), MC_PER samples per thread
-// with a 256-sample stride (coalesced rows), one power reduction per RX.
-constexpr int MC_PER = 8, MC_CHUNK = MWG * MC_PER, MC_MAXRX = 8;
+// One block per (frame, OFDM symbol): the symbol index -- hence every link
+// path's fading coefficients (A, B, C) -- is uniform over the block, so they
+// are scalar loads; the sample offset d from the symbol centre is per lane.
+// All RX of the frame per block: each TX stream sample is loaded once for
+// every RX (the [rx][tx] link loop runs on registers), one power reduction
+// per RX.
+constexpr int MC_MAXRX = 8;
+
+__device__ __forceinline__ float2 link_sample_sym(const float2* __restrict__ cs, int n_cs, int np, int n, float d,
+                                                  const int32_t* __restrict__ delays, const float2* __restrict__ xf) {
+  float2 acc = make_float2(0.f, 0.f);
+  for (int p = 0; p < np; ++p) {
+    const int src = n - (delays ? delays[p] : 0);
+    if (src < 0) continue;
+    const float2* c = cs + (size_t)p * n_cs * 3;   // this symbol's (A, B, C) of path p
+    float2 h = c[0];
+    if (n_cs > 1) {   // A + B d + C d^2
+      h.x += d * (c[1].x + d * c[2].x);
+      h.y += d * (c[1].y + d * c[2].y);
+    }
+    acc = cadd(acc, cmul(h, xf[src]));
+  }
+  return acc;
+}
 
 __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
@@ -278,14 +305,16 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
                                                       const float* __restrict__ inj_lz, int64_t inj_lz_stride,
                                                       float* __restrict__ pow_part, int nblk) {
   __shared__ float red[MWG / 64];
-  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
+  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;   // blk = OFDM symbol (block of sym_len samples)
+  const int sidx = n_cs > 1 ? blk : 0;
+  const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
+  const float dc = 0.5f * (float)(sym_len - 1);
   float pw[MC_MAXRX];
 #pragma unroll
   for (int r = 0; r < MC_MAXRX; ++r) pw[r] = 0.f;
 #pragma unroll 1
-  for (int i = 0; i < MC_PER; ++i) {
-    const int n = blk * MC_CHUNK + i * MWG + threadIdx.x;
-    if (n >= L) break;
+  for (int n = nbeg + threadIdx.x; n < nend; n += MWG) {
+    const float d = n_cs > 1 ? (float)(n - nbeg) - dc : 0.f;
     float2 v[MC_MAXRX];
 #pragma unroll
     for (int r = 0; r < MC_MAXRX; ++r) v[r] = make_float2(0.f, 0.f);
@@ -295,8 +324,8 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
       for (int r = 0; r < MC_MAXRX; ++r) {
         if (r >= num_rx) break;
         const size_t link = (size_t)r * num_tx + tx;
-        const float2* cf = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3;
-        float2 yl = link_sample(cf, n_cs, np, n, sym_len, delays, xf);
+        const float2* cs = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3 + (size_t)sidx * 3;
+        float2 yl = link_sample_sym(cs, n_cs, np, n, d, delays, xf);
         if (link_sigma) {
           const float sg = link_sigma[(size_t)b * num_rx * num_tx + link];
           float2 z;
@@ -319,14 +348,16 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
       pw[r] += v[r].x * v[r].x + v[r].y * v[r].y;
     }
   }
-  for (int r = 0; r < num_rx; ++r) {
-    const float t = block_sum(pw[r < MC_MAXRX ? r : 0], red);
+#pragma unroll
+  for (int r = 0; r < MC_MAXRX; ++r) {
+    if (r >= num_rx) break;
+    const float t = block_sum(pw[r], red);
     if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
     __syncthreads();
   }
 }
 
-int mimo_channel_nblk(int L) { return (L + MC_CHUNK - 1) / MC_CHUNK; }
+int mimo_channel_nblk(int L, int sym_len) { return (L + sym_len - 1) / sym_len; }
 
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
                         const float2* coef, const float2* x, float2* y, int link_noise, const uint64_t* fid,
@@ -334,13 +365,14 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
                         float* link_sigma, float* pow_part, int nblk) {
   const int sym_len = g.N + g.cp;
   if (m.num_rx > MC_MAXRX) return (int)hipErrorInvalidValue;
+  const int nch = mimo_channel_nblk(g.L, sym_len);
+  if (nch > nblk) return (int)hipErrorInvalidValue;   // partial buffers are sized for nblk blocks
   if (link_noise) {
-    hipLaunchKernelGGL(k_link_power, dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx,
-                       n_paths, m.n_cs, sym_len, delays, coef, x, link_part, nblk);
+    hipLaunchKernelGGL(k_link_power, dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx,
+                       n_paths, m.n_cs, sym_len, delays, coef, x, link_part, nch);
     const int nl = B * m.num_rx * m.num_tx;
-    hipLaunchKernelGGL(k_link_sigma, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nblk, g.L, link_sigma);
+    hipLaunchKernelGGL(k_link_sigma, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L, link_sigma);
   }
-  const int nch = mimo_channel_nblk(g.L);
   hipLaunchKernelGGL(k_channel_mimo, dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths, m.n_cs,
                      sym_len, delays, coef, x, y, link_noise ? link_sigma : nullptr, fid, seed, inj_lz, inj_lz_stride,
                      pow_part, nch);

@@ -236,33 +236,86 @@ __device__ __forceinline__ float2 link_sample(const float2* __restrict__ cf, int
   return acc;
 }
 
-// pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
-// one block per (frame, OFDM symbol, link) like k_channel_mimo
-__device__ __forceinline__ float2 link_sample_sym(const float2* __restrict__ cs, int n_cs, int np, int n, float d,
-                                                  const int32_t* __restrict__ delays, const float2* __restrict__ xf);
+// One block per (frame, OFDM symbol); each thread owns J samples of the
+// symbol, n_j = base + tid + j*MWG, so every (link, path) coefficient triple
+// (wave-uniform: one symbol) is loaded once per thread and the J delayed loads
+// of a path are issued back to back.
+template <int J>
+struct SymSpan {
+  int n[J];
+  float d[J];
+  bool ok[J];
+  __device__ __forceinline__ SymSpan(int base, int nbeg, int nend, float dc, bool fading) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      n[j] = base + (int)threadIdx.x + j * MWG;
+      ok[j] = n[j] < nend;
+      d[j] = fading ? (float)(n[j] - nbeg) - dc : 0.f;
+    }
+  }
+};
 
+// acc[j] += sum_p h_p(d_j) x[n_j - delay_p] for one link (cs: the link's
+// coefficients at this symbol, stride n_cs*3 per path)
+template <int J>
+__device__ __forceinline__ void link_accumulate(float2 (&acc)[J], const SymSpan<J>& sp, const float2* __restrict__ cs,
+                                                int n_cs, int np, const int32_t* __restrict__ delays,
+                                                const float2* __restrict__ xf) {
+  for (int p = 0; p < np; ++p) {
+    const int dl = delays ? delays[p] : 0;
+    float2 xs[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int src = sp.n[j] - dl;
+      xs[j] = (sp.ok[j] && src >= 0) ? xf[src] : make_float2(0.f, 0.f);
+    }
+    const float2* c = cs + (size_t)p * n_cs * 3;
+    const float2 c0 = c[0];
+    if (n_cs > 1) {   // A + B d + C d^2
+      const float2 c1 = c[1], c2 = c[2];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const float dj = sp.d[j];
+        const float2 h = make_float2(c0.x + dj * (c1.x + dj * c2.x), c0.y + dj * (c1.y + dj * c2.y));
+        acc[j] = cadd(acc[j], cmul(h, xs[j]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < J; ++j) acc[j] = cadd(acc[j], cmul(c0, xs[j]));
+    }
+  }
+}
+
+// pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
+// one block per (frame, OFDM symbol, link)
+template <int J>
 __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                     const int32_t* __restrict__ delays,
                                                     const float2* __restrict__ coef, const float2* __restrict__ x,
                                                     float* __restrict__ part, int nblk) {
   __shared__ float red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
-  const int link = blockIdx.y, rx = link / num_tx, tx = link - rx * num_tx;
+  const int link = blockIdx.y, tx = link % num_tx;
   const int sidx = n_cs > 1 ? blk : 0;
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
   const float dc = 0.5f * (float)(sym_len - 1);
-  const float2* cs = coef + (((size_t)b * num_rx + rx) * num_tx + tx) * np * n_cs * 3 + (size_t)sidx * 3;
+  const float2* cs = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3 + (size_t)sidx * 3;
   const float2* xf = x + ((size_t)b * num_tx + tx) * L;
   float v = 0.f;
-  for (int n = nbeg + threadIdx.x; n < nend; n += MWG) {
-    const float2 yv = link_sample_sym(cs, n_cs, np, n, n_cs > 1 ? (float)(n - nbeg) - dc : 0.f, delays, xf);
-    v += yv.x * yv.x + yv.y * yv.y;
+  for (int base = nbeg; base < nend; base += J * MWG) {
+    const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
+    float2 acc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = make_float2(0.f, 0.f);
+    link_accumulate<J>(acc, sp, cs, n_cs, np, delays, xf);
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (sp.ok[j]) v += acc[j].x * acc[j].x + acc[j].y * acc[j].y;
   }
   const float t = block_sum(v, red);
-  if (threadIdx.x == 0) part[(((size_t)b * num_rx * num_tx) + link) * nblk + blk] = t;
+  if (threadIdx.x == 0) part[((size_t)b * num_rx * num_tx + link) * nblk + blk] = t;
 }
 
-// sigma_link = sqrt(P_link / 1e10 / 2)
 __global__ void k_link_sigma(int n_links_total, const float* __restrict__ part, int nblk, int L,
                              float* __restrict__ sigma) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -278,25 +331,10 @@ __global__ void k_link_sigma(int n_links_total, const float* __restrict__ part, 
 // All RX of the frame per block: each TX stream sample is loaded once for
 // every RX (the [rx][tx] link loop runs on registers), one power reduction
 // per RX.
-constexpr int MC_MAXRX = 8;
+constexpr int MC_MAXRX = 8;   // receive antennas per launch
+constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the transmit streams
 
-__device__ __forceinline__ float2 link_sample_sym(const float2* __restrict__ cs, int n_cs, int np, int n, float d,
-                                                  const int32_t* __restrict__ delays, const float2* __restrict__ xf) {
-  float2 acc = make_float2(0.f, 0.f);
-  for (int p = 0; p < np; ++p) {
-    const int src = n - (delays ? delays[p] : 0);
-    if (src < 0) continue;
-    const float2* c = cs + (size_t)p * n_cs * 3;   // this symbol's (A, B, C) of path p
-    float2 h = c[0];
-    if (n_cs > 1) {   // A + B d + C d^2
-      h.x += d * (c[1].x + d * c[2].x);
-      h.y += d * (c[1].y + d * c[2].y);
-    }
-    acc = cadd(acc, cmul(h, xf[src]));
-  }
-  return acc;
-}
-
+template <int J>
 __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
                                                       const float2* __restrict__ coef, const float2* __restrict__ x,
@@ -309,51 +347,67 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
   const int sidx = n_cs > 1 ? blk : 0;
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
   const float dc = 0.5f * (float)(sym_len - 1);
-  float pw[MC_MAXRX];
+  const size_t nl = (size_t)num_rx * num_tx;
+  for (int rg = 0; rg < num_rx; rg += MC_RXG) {
+    float pw[MC_RXG];
 #pragma unroll
-  for (int r = 0; r < MC_MAXRX; ++r) pw[r] = 0.f;
-#pragma unroll 1
-  for (int n = nbeg + threadIdx.x; n < nend; n += MWG) {
-    const float d = n_cs > 1 ? (float)(n - nbeg) - dc : 0.f;
-    float2 v[MC_MAXRX];
+    for (int q = 0; q < MC_RXG; ++q) pw[q] = 0.f;
+    for (int base = nbeg; base < nend; base += J * MWG) {
+      const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
+      float2 v[MC_RXG][J];
 #pragma unroll
-    for (int r = 0; r < MC_MAXRX; ++r) v[r] = make_float2(0.f, 0.f);
-    for (int tx = 0; tx < num_tx; ++tx) {
-      const float2* xf = x + ((size_t)b * num_tx + tx) * L;
+      for (int q = 0; q < MC_RXG; ++q)
 #pragma unroll
-      for (int r = 0; r < MC_MAXRX; ++r) {
-        if (r >= num_rx) break;
-        const size_t link = (size_t)r * num_tx + tx;
-        const float2* cs = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3 + (size_t)sidx * 3;
-        float2 yl = link_sample_sym(cs, n_cs, np, n, d, delays, xf);
-        if (link_sigma) {
-          const float sg = link_sigma[(size_t)b * num_rx * num_tx + link];
-          float2 z;
-          if (inj_lz) {
-            const float* zf = inj_lz + (size_t)b * inj_lz_stride + link * 2 * L;
-            z = make_float2(zf[n], zf[L + n]);
-          } else {
-            const u32x4 rr = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
-            z = (n & 1) ? box_muller(rr.z, rr.w) : box_muller(rr.x, rr.y);
+        for (int j = 0; j < J; ++j) v[q][j] = make_float2(0.f, 0.f);
+      for (int tx = 0; tx < num_tx; ++tx) {
+        const float2* xf = x + ((size_t)b * num_tx + tx) * L;
+#pragma unroll
+        for (int q = 0; q < MC_RXG; ++q) {
+          const int r = rg + q;
+          if (r >= num_rx) break;
+          const size_t link = (size_t)r * num_tx + tx;
+          link_accumulate<J>(v[q], sp, coef + ((size_t)b * nl + link) * np * n_cs * 3 + (size_t)sidx * 3, n_cs, np,
+                             delays, xf);
+          if (link_sigma) {   // the link's own ChannelSimulator noise
+            const float sg = link_sigma[(size_t)b * nl + link];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+              const int n = sp.n[j];
+              float2 z = make_float2(0.f, 0.f);
+              if (sp.ok[j]) {
+                if (inj_lz) {
+                  const float* zf = inj_lz + (size_t)b * inj_lz_stride + link * 2 * L;
+                  z = make_float2(zf[n], zf[L + n]);
+                } else {
+                  const u32x4 rr = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
+                  z = (n & 1) ? box_muller(rr.z, rr.w) : box_muller(rr.x, rr.y);
+                }
+              }
+              v[q][j] = make_float2(v[q][j].x + sg * z.x, v[q][j].y + sg * z.y);
+            }
           }
-          yl = make_float2(yl.x + sg * z.x, yl.y + sg * z.y);
         }
-        v[r] = cadd(v[r], yl);
+      }
+#pragma unroll
+      for (int q = 0; q < MC_RXG; ++q) {
+        const int r = rg + q;
+        if (r >= num_rx) break;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (sp.ok[j]) {
+            y[((size_t)b * num_rx + r) * L + sp.n[j]] = v[q][j];
+            pw[q] += v[q][j].x * v[q][j].x + v[q][j].y * v[q][j].y;
+          }
       }
     }
 #pragma unroll
-    for (int r = 0; r < MC_MAXRX; ++r) {
+    for (int q = 0; q < MC_RXG; ++q) {
+      const int r = rg + q;
       if (r >= num_rx) break;
-      y[((size_t)b * num_rx + r) * L + n] = v[r];
-      pw[r] += v[r].x * v[r].x + v[r].y * v[r].y;
+      const float t = block_sum(pw[q], red);
+      if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
+      __syncthreads();
     }
-  }
-#pragma unroll
-  for (int r = 0; r < MC_MAXRX; ++r) {
-    if (r >= num_rx) break;
-    const float t = block_sum(pw[r], red);
-    if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
-    __syncthreads();
   }
 }
 
@@ -367,15 +421,31 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   if (m.num_rx > MC_MAXRX) return (int)hipErrorInvalidValue;
   const int nch = mimo_channel_nblk(g.L, sym_len);
   if (nch > nblk) return (int)hipErrorInvalidValue;   // partial buffers are sized for nblk blocks
-  if (link_noise) {
-    hipLaunchKernelGGL(k_link_power, dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx,
-                       n_paths, m.n_cs, sym_len, delays, coef, x, link_part, nch);
-    const int nl = B * m.num_rx * m.num_tx;
-    hipLaunchKernelGGL(k_link_sigma, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L, link_sigma);
+  // samples per thread per pass: the smallest instantiated J covering one symbol (larger symbols loop)
+  const int jn = (sym_len + MWG - 1) / MWG;
+  const int J = jn <= 1 ? 1 : jn <= 2 ? 2 : jn <= 3 ? 3 : jn <= 5 ? 5 : jn <= 7 ? 7 : 9;
+#define LTE_CHM(J_)                                                                                                 \
+  do {                                                                                                             \
+    if (link_noise) {                                                                                              \
+      hipLaunchKernelGGL(k_link_power<J_>, dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx,     \
+                         m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, x, link_part, nch);                     \
+      const int nl = B * m.num_rx * m.num_tx;                                                                      \
+      hipLaunchKernelGGL(k_link_sigma, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L,          \
+                         link_sigma);                                                                              \
+    }                                                                                                              \
+    hipLaunchKernelGGL(k_channel_mimo<J_>, dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths,       \
+                       m.n_cs, sym_len, delays, coef, x, y, link_noise ? link_sigma : nullptr, fid, seed, inj_lz,  \
+                       inj_lz_stride, pow_part, nch);                                                              \
+  } while (0)
+  switch (J) {
+    case 1: LTE_CHM(1); break;
+    case 2: LTE_CHM(2); break;
+    case 3: LTE_CHM(3); break;
+    case 5: LTE_CHM(5); break;
+    case 7: LTE_CHM(7); break;
+    default: LTE_CHM(9); break;
   }
-  hipLaunchKernelGGL(k_channel_mimo, dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths, m.n_cs,
-                     sym_len, delays, coef, x, y, link_noise ? link_sigma : nullptr, fid, seed, inj_lz, inj_lz_stride,
-                     pow_part, nch);
+#undef LTE_CHM
   return (int)hipGetLastError();
 }
 

@@ -70,89 +70,143 @@ __device__ __forceinline__ float2 cdiv(float2 a, float2 b) {
 }
 
 // ---------------------------------------------------------------- FFT
-// Stockham radix-4 (+ one radix-2 stage when log2 N is odd) complex FFT held
-// in LDS.  One transform of N points is done by T = N/8 threads (tid in
-// [0,T)); every stage is register-staged (read -> barrier -> write ->
-// barrier), so several transforms of the same N can share a workgroup.
-// tw[e] = exp(-2*pi*i*e/N), e in [0, N).  Unscaled.  All threads of the
-// workgroup must call it (it contains __syncthreads).
+// Stockham radix-8 complex FFT held in LDS (+ one final radix-4 or radix-2
+// pass when log2 N is not a multiple of 3): N = 2048 takes 4 passes.  One
+// transform of N points is done by T = N/8 threads (tid in [0,T)), one radix-8
+// butterfly per thread per pass, every pass register-staged (read -> barrier
+// -> write -> barrier), so several transforms of the same N can share a
+// workgroup.  Between passes the data lives in an XOR-swizzled layout
+// (fft_sw) that makes the strided Stockham stores conflict-free for
+// ds_write_b64 (16-lane groups, banks mod 32); the caller's layout (input and
+// output) is the natural one.  tw[e] = exp(-2*pi*i*e/N), e in [0, N).
+// Unscaled.  N in [128, 2048].  All threads of the workgroup must call it (it
+// contains __syncthreads).
 template <bool INV>
 __device__ __forceinline__ float2 twid(const float2* __restrict__ tw, int e) {
   const float2 w = tw[e];
   return INV ? make_float2(w.x, -w.y) : w;
 }
 
+// logical -> physical float2 index between passes (bijection on each 128-block)
+__device__ __forceinline__ int fft_sw(int i) { return i ^ (((i >> 4) & 7) | ((i >> 3) & 8)); }
+
+// x * -j (forward) or x * +j (inverse)
+template <bool INV>
+__device__ __forceinline__ float2 mul_mj(float2 d) {
+  return INV ? make_float2(-d.y, d.x) : make_float2(d.y, -d.x);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4_inplace(float2& a0, float2& a1, float2& a2, float2& a3) {
+  const float2 b0 = cadd(a0, a2), b1 = csub(a0, a2), b2 = cadd(a1, a3), b3 = mul_mj<INV>(csub(a1, a3));
+  a0 = cadd(b0, b2);
+  a2 = csub(b0, b2);
+  a1 = cadd(b1, b3);
+  a3 = csub(b1, b3);
+}
+
+// radix-8 DFT in registers: out[m] = sum_r v[r] W8^(r m)
+template <bool INV>
+__device__ __forceinline__ void dft8_inplace(float2 (&v)[8]) {
+  dft4_inplace<INV>(v[0], v[2], v[4], v[6]);   // E[m] in v[0,2,4,6]
+  dft4_inplace<INV>(v[1], v[3], v[5], v[7]);   // O[m] in v[1,3,5,7]
+  const float s = 0.70710678118654752f;
+  const float2 o0 = v[1];
+  float2 o1 = v[3], o3 = v[7];
+  const float2 o2 = mul_mj<INV>(v[5]);         // W8^2 = -j (forward)
+  if (INV) {                                   // W8^1 = (1+j)/sqrt2, W8^3 = (-1+j)/sqrt2
+    o1 = make_float2((o1.x - o1.y) * s, (o1.x + o1.y) * s);
+    o3 = make_float2((-o3.x - o3.y) * s, (o3.x - o3.y) * s);
+  } else {                                     // W8^1 = (1-j)/sqrt2, W8^3 = (-1-j)/sqrt2
+    o1 = make_float2((o1.x + o1.y) * s, (o1.y - o1.x) * s);
+    o3 = make_float2((o3.y - o3.x) * s, (-o3.x - o3.y) * s);
+  }
+  const float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+  v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
+  v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
+  v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
+  v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
+}
+
 template <bool INV>
 __device__ __forceinline__ void fft_lds(float2* buf, int N, int log2N, const float2* __restrict__ tw,
                                         int tid, bool active) {
   const int T = N >> 3;
-  const int q4 = N >> 2;
-  int Ns = 1, lNs = 0;   // Ns = 4^s; all index arithmetic is shifts (N, Ns powers of 2)
-  const int n4 = log2N >> 1;
-  for (int s = 0; s < n4; ++s) {
+  const int n8 = log2N / 3, rem = log2N - 3 * n8;
+  int Ns = 1, lNs = 0;   // Ns = 8^s
+  for (int s = 0; s < n8; ++s) {
+    const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
+    float2 v[8];
+    const int j = tid;
+    if (active) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = j + r * T;
+        v[r] = buf[rsw ? fft_sw(i) : i];
+      }
+      if (s > 0) {
+        const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));   // k * N / (8 Ns)
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], twid<INV>(tw, r * ks));
+      }
+      dft8_inplace<INV>(v);
+    }
+    __syncthreads();
+    if (active) {
+      const int idx = ((j >> lNs) << (lNs + 3)) + (j & (Ns - 1));
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = idx + r * Ns;
+        buf[wsw ? fft_sw(i) : i] = v[r];
+      }
+    }
+    __syncthreads();
+    Ns <<= 3;
+    lNs += 3;
+  }
+  if (rem == 2) {   // final radix-4 pass (Ns == N/4): two butterflies per thread
+    const int q4 = N >> 2;
     float2 v[2][4];
-    int jj[2];
     if (active) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int j = tid + q * T;
-        jj[q] = j;
-        const int k = j & (Ns - 1);
-        const int step = 1 << (log2N - lNs - 2);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[q][r] = buf[j + r * q4];
+        for (int r = 0; r < 4; ++r) v[q][r] = buf[fft_sw(j + r * q4)];
 #pragma unroll
-        for (int r = 1; r < 4; ++r) v[q][r] = cmul(v[q][r], twid<INV>(tw, k * r * step));
-        // radix-4 butterfly
-        const float2 a0 = cadd(v[q][0], v[q][2]), a1 = csub(v[q][0], v[q][2]);
-        const float2 a2 = cadd(v[q][1], v[q][3]), d = csub(v[q][1], v[q][3]);
-        const float2 a3 = INV ? make_float2(-d.y, d.x) : make_float2(d.y, -d.x);
-        v[q][0] = cadd(a0, a2);
-        v[q][2] = csub(a0, a2);
-        v[q][1] = cadd(a1, a3);
-        v[q][3] = csub(a1, a3);
+        for (int r = 1; r < 4; ++r) v[q][r] = cmul(v[q][r], twid<INV>(tw, j * r));
+        dft4_inplace<INV>(v[q][0], v[q][1], v[q][2], v[q][3]);
       }
     }
     __syncthreads();
     if (active) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int j = jj[q];
-        const int idx = ((j >> lNs) << (lNs + 2)) + (j & (Ns - 1));
+        const int j = tid + q * T;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) buf[idx + r * Ns] = v[q][r];
+        for (int r = 0; r < 4; ++r) buf[j + r * q4] = v[q][r];
       }
     }
     __syncthreads();
-    Ns <<= 2;
-    lNs += 2;
-  }
-  if (log2N & 1) {  // final radix-2 stage (Ns == N/2)
+  } else if (rem == 1) {   // final radix-2 pass (Ns == N/2): four butterflies per thread
     const int h = N >> 1;
     float2 v[4][2];
-    int jj[4];
     if (active) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = tid + q * T;
-        jj[q] = j;
-        const int k = j & (Ns - 1);
-        const int step = 1 << (log2N - lNs - 1);
-        v[q][0] = buf[j];
-        v[q][1] = cmul(buf[j + h], twid<INV>(tw, k * step));
-        const float2 t0 = cadd(v[q][0], v[q][1]), t1 = csub(v[q][0], v[q][1]);
-        v[q][0] = t0;
-        v[q][1] = t1;
+        const float2 a = buf[fft_sw(j)], b = cmul(buf[fft_sw(j + h)], twid<INV>(tw, j));
+        v[q][0] = cadd(a, b);
+        v[q][1] = csub(a, b);
       }
     }
     __syncthreads();
     if (active) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int j = jj[q];
-        const int idx = ((j >> lNs) << (lNs + 1)) + (j & (Ns - 1));
-        buf[idx] = v[q][0];
-        buf[idx + Ns] = v[q][1];
+        const int j = tid + q * T;
+        buf[j] = v[q][0];
+        buf[j + h] = v[q][1];
       }
     }
     __syncthreads();

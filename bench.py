@@ -151,6 +151,12 @@ def main():
             # HBM bytes per launch from the committed PMC passes (profiles/pmc_turbo_traffic.json:
             # per-frame bytes, gfx950-corrected, scaled to this launch's frames)
             'traffic': (round(traffic['bytes_per_frame'] * Fp) if traffic else None),
+            # the same measured bytes over the measured launch time: how close the decoder's
+            # real stream (17 passes x fwd + bwd sweeps per code block) runs to the HBM peak
+            'traffic_GBs': (round(traffic['bytes_per_frame'] * Fp / (avg_launch_ms * 1e-3) / 1e9, 1)
+                            if traffic and t_n else None),
+            'traffic_frac': (round(traffic['bytes_per_frame'] * Fp / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if traffic and t_n else None),
             'avg_launch_ms': round(avg_launch_ms, 3), 'launches': t_n,
             'alg_bytes_per_launch': int(alg_per_launch),
             'turbo_share_of_step': round(t_ms / (el * 1e3) if el > 0 else 0, 3),

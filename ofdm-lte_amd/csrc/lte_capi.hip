@@ -378,7 +378,7 @@ struct lte_plan {
   DBuf<CbInfo> cbi;
   DBuf<int32_t> tx_map, rx_map, delays;
   DBuf<float> gains;
-  DBuf<uint32_t> pw, enc, inj_bits;
+  DBuf<uint32_t> pw, enc, enc_cw, inj_bits;
   DBuf<float2> x, y, coef, H, capbuf, captx;
   DBuf<float> phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
   DBuf<uint32_t> frame_err, frame_crc;
@@ -895,6 +895,7 @@ static int plan_alloc(lte_plan* p) {
   bad |= p->frame_crc.alloc(B) != 0;
   if (coded) {
     bad |= p->enc.alloc(B * p->enc_words) != 0;
+    bad |= p->enc_cw.alloc(encode_scratch_words(p->KWmax, p->C, (int)B)) != 0;
     bad |= p->llr.alloc(B * p->n_re_bits) != 0;
     p->blk.resize(p->C);
     p->ckpt.resize(p->C);
@@ -1063,7 +1064,7 @@ int lte_plan_destroy(lte_plan* p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   p->tabs.release();
   p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release(); p->gains.release();
-  p->pw.release(); p->enc.release(); p->inj_bits.release();
+  p->pw.release(); p->enc.release(); p->enc_cw.release(); p->inj_bits.release();
   p->x.release(); p->y.release(); p->coef.release(); p->H.release(); p->capbuf.release(); p->captx.release();
   p->phases.release(); p->pow_part.release(); p->pstats.release(); p->npow.release(); p->llr.release();
   p->snr_lin.release(); p->inj_ph.release(); p->inj_z.release();
@@ -1173,7 +1174,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   if (coded) {
     Timer t(p, KN_ENCODE);
-    LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
+    LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_cw.p));
   }
   {
     Timer t(p, KN_OFDM_TX);
@@ -1468,7 +1469,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (do_tx) {
     if (coded) {
       Timer t(p, KN_ENCODE);
-      LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B));
+      LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_cw.p));
     }
     float2* cts = nullptr;
     if (a->cap_tx_syms) {
@@ -1730,15 +1731,18 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out)
   std::vector<uint32_t> w((size_t)ncb * PW);
   for (int64_t c = 0; c < ncb; ++c) pack_bits(bits + c * K, K, &w[c * PW], PW);
   CbInfo ci{K, 0, K, 0, 0, f1, f2, 3 * K + 12};
-  DBuf<uint32_t> dpw, denc;
+  DBuf<uint32_t> dpw, denc, dcw;
   DBuf<CbInfo> dci;
   std::vector<CbInfo> vci{ci};
-  if (dpw.alloc(w.size()) || denc.alloc((size_t)ncb * 3 * EW) || upload(dci, vci))
+  if (dpw.alloc(w.size()) || denc.alloc((size_t)ncb * 3 * EW) || dcw.alloc(encode_scratch_words(KW, 1, (int)ncb)) ||
+      upload(dci, vci)) {
+    dpw.release(); denc.release(); dcw.release(); dci.release();
     return fail(LTE_ENOMEM, "buffers");
+  }
   std::vector<uint32_t> e((size_t)ncb * 3 * EW);
   int rc = LTE_OK;
   if (hipMemcpy(dpw.p, w.data(), w.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      launch_encode(nullptr, dpw.p, PW, KW, denc.p, EW, dci.p, 1, (int)ncb) ||
+      launch_encode(nullptr, dpw.p, PW, KW, denc.p, EW, dci.p, 1, (int)ncb, dcw.p) ||
       hipMemcpy(e.data(), denc.p, e.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "encode failed");
   if (rc == LTE_OK) {
@@ -1757,7 +1761,7 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out)
       }
     }
   }
-  dpw.release(); denc.release(); dci.release();
+  dpw.release(); denc.release(); dcw.release(); dci.release();
   return rc;
 }
 

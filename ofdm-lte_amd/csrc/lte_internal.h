@@ -32,8 +32,10 @@ struct Grid {                 // device pointers + numerology for one plan
 // launchers (return hipError_t as int)
 int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, const uint64_t* fid,
                    uint64_t seed, int B, const uint32_t* inj, int64_t inj_stride);
+// cw_scratch: encode_scratch_words(KWmax, C, B) words (the code blocks as [wave][word][lane])
+size_t encode_scratch_words(int KWmax, int C, int B);
 int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
-                  const CbInfo* cbi_dev, int C, int B);
+                  const CbInfo* cbi_dev, int C, int B, uint32_t* cw_scratch);
 int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
                    int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms = nullptr,
                    int sc_fdm = 0);

@@ -452,122 +452,183 @@ struct BitWriter {   // MSB-first stream writer; one store per completed word
   }
 };
 
-// nb (<= 32) bits of the RSC code (turbo_encoder.py:137-211) on u (MSB-first):
-// returns feedback ("systematic", Q13) bits in *fbw and parity bits.
-__device__ __forceinline__ uint32_t rsc_bits(uint32_t u, int nb, uint32_t& s0, uint32_t& s1, uint32_t& s2,
-                                             uint32_t* fbw) {
-  uint32_t f = 0, q = 0;
-  for (int i = 0; i < nb; ++i) {
-    const uint32_t bit = (u >> (nb - 1 - i)) & 1u;
-    const uint32_t fb = bit ^ s1 ^ s2;
-    f = (f << 1) | fb;
-    q = (q << 1) | (fb ^ s0 ^ s2);
-    s2 = s1; s1 = s0; s0 = fb;
-  }
-  *fbw = f;
+// CRC-24 byte table (MSB-first, zero init; poly without the x^24 term)
+__device__ __forceinline__ uint32_t crc24_table_entry(uint32_t i, uint32_t poly) {
+  uint32_t r = i << 16;
+  for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? ((r << 1) ^ poly) : (r << 1);
+  return r & 0xFFFFFFu;
+}
+
+// RSC code (turbo_encoder.py:137-211) 32 bits at a time, in closed form.  The
+// feedback ("systematic", Q13) sequence obeys a_k = u_k ^ a_{k-2} ^ a_{k-3}, i.e.
+// a = u / g0(D) with g0 = 1 + D^2 + D^3.  Since (1 + D^7) = g0 (1 + D^2 + D^3 +
+// D^4), 1/g0 = (1 + D^2 + D^3 + D^4) / (1 + D^7): four shifted XORs, then a
+// stride-7 prefix XOR in three doubling steps.  The state (s0, s1, s2) =
+// (a_{-1}, a_{-2}, a_{-3}) adds its zero-input response (period 7; the three
+// basis words below).  Parity q_k = a_k ^ a_{k-1} ^ a_{k-3}.  Words are
+// MSB-first (time runs toward bit 0); u holds nb (multiple of 8) bits
+// left-aligned, bits past nb are ignored.  Returns q, *fw = a (left-aligned),
+// and leaves the state at time nb-1.
+__device__ __forceinline__ uint32_t rsc_word(uint32_t u, int nb, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                             uint32_t* fw) {
+  uint32_t y = u ^ (u >> 2) ^ (u >> 3) ^ (u >> 4);
+  y ^= y >> 7;
+  y ^= y >> 14;
+  y ^= y >> 28;
+  const uint32_t a = y ^ (s0 ? 0x72e5cb97u : 0u) ^ (s1 ? 0xe5cb972eu : 0u) ^ (s2 ? 0xb972e5cbu : 0u);
+  const uint32_t q = a ^ ((a >> 1) | (s0 << 31)) ^ ((a >> 3) | (s2 << 31) | (s1 << 30) | (s0 << 29));
+  s0 = (a >> (32 - nb)) & 1u;
+  s1 = (a >> (33 - nb)) & 1u;
+  s2 = (a >> (34 - nb)) & 1u;
+  *fw = a;
   return q;
 }
 
-// Bit-serial recursion in registers, memory traffic in 32-bit words: TB words
-// through a 64-bit window, one store per completed output word.  The code
-// block itself stays in LDS as [word][lane] for encoder 2's QPP gathers: pi(i)
-// is wave-uniform (all lanes share K), so every gather is one conflict-free
-// 64-lane LDS read instead of a scattered global load.
-constexpr int ENC_WG = 64;
+// one trellis-termination step (turbo_encoder.py:190-211): input s1 ^ s2 makes
+// the feedback bit 0; returns fb | parity << 1
+__device__ __forceinline__ uint32_t rsc_tail(uint32_t& s0, uint32_t& s1, uint32_t& s2) {
+  const uint32_t fb = 0u, par = fb ^ s0 ^ s2;
+  s2 = s1; s1 = s0; s0 = fb;
+  return fb | (par << 1);
+}
+
+// TX coding in two kernels, one lane = one (CB slot, frame); lanes of a wave
+// are 64 consecutive frames of one CB slot, so they share K and the QPP
+// permutation.
+//  k_encode   CB construction (segmentation.py:212-247 + CRC-24B crc.py:
+//             162-184, a byte-table step per 8 bits) + encoder 1.  TB words
+//             stream in through a two-word window (next word prefetched).  The
+//             code block is written to a scratch as [wave][word][lane]
+//             (coalesced rows).  No big LDS: occupancy is set by VGPRs.
+//  k_encode2  encoder 2 on the QPP-interleaved block (turbo_encoder.py:
+//             213-313): the wave copies its 64 code blocks into LDS (48 KB at
+//             K = 6144, [word][lane]) and gathers from there -- pi(i) is
+//             wave-uniform, so each gather is one conflict-free LDS read.
+constexpr int ENC_WG = 256;
 __global__ __launch_bounds__(ENC_WG) void k_encode(const uint32_t* __restrict__ pw, int PW, int KWmax,
                                                    uint32_t* __restrict__ enc, int EW,
-                                                   const CbInfo* __restrict__ cbi, int C, int B) {
-  extern __shared__ uint32_t cwl[];   // [KWmax][64]
+                                                   const CbInfo* __restrict__ cbi, int C, int B,
+                                                   uint32_t* __restrict__ cw_scratch) {
+  __shared__ uint32_t crc_t[256];
+  for (int i = threadIdx.x; i < 256; i += ENC_WG) crc_t[i] = crc24_table_entry(i, 0x800063u);   // CRC-24B
+  __syncthreads();
   const int gid = blockIdx.x * ENC_WG + threadIdx.x;
   if (gid >= C * B) return;           // no barriers below: early exit is safe
   const int r = gid / B, b = gid % B;
   const CbInfo ci = cbi[r];
-  const int K = ci.K;
+  const int K = ci.K, F = ci.F;
   const uint32_t* tb = pw + (size_t)b * PW;
-  uint32_t* cw = cwl + threadIdx.x;   // word w of this lane's block at cw[w * 64]
-  (void)KWmax;
+  uint32_t* cw = cw_scratch + (size_t)(gid >> 6) * KWmax * 64 + (gid & 63);   // word w at cw[w * 64]
   uint32_t* e = enc + ((size_t)b * C + r) * 3 * EW;
-  BitWriter w0{e, 0, 0}, w1{e + EW, 0, 0}, w2{e + 2 * EW, 0, 0};
-  const int Kd = ci.crc ? K - 24 : K;
+  BitWriter w0{e, 0, 0}, w1{e + EW, 0, 0};
+  const int Kd = ci.crc ? K - 24 : K;   // every LTE K (and so Kd) is a multiple of 8
   uint32_t crc = 0, s0 = 0, s1 = 0, s2 = 0;
-  // TB bit (ci.off - ci.F + p) for CB bit p in [F, F+info)
-  const int64_t base = (int64_t)ci.off - ci.F;
+  // CB bit p in [F, Kd) is TB bit (off - F + p): the 32 bits of word w are a
+  // fixed-offset window over TB words i00 + w, i00 + w + 1
+  const int64_t base = (int64_t)ci.off - F;
+  const int64_t i00 = base >> 5;      // arithmetic shift: floor for negative base
+  const int o = (int)(base & 31);
+  auto ldw = [&](int64_t i) -> uint32_t { return (i >= 0 && i < PW) ? tb[i] : 0u; };
+  uint32_t wa = ldw(i00), wb = ldw(i00 + 1);
   for (int w = 0; w * 32 < K; ++w) {
+    const uint32_t wn = ldw(i00 + w + 2);   // next window word, in flight during this one
     const int p0 = w * 32, nb = min(32, K - p0);
-    // 32 TB bits starting at base + p0 (window of two words; bits outside [F, Kd) are masked below)
-    uint32_t t = 0;
-    {
-      const int64_t q = base + p0;
-      if (q + 32 > 0 && q < (int64_t)PW * 32) {
-        const int64_t i0 = q >> 5;   // arithmetic shift: floor for negative q
-        const int o = (int)(q & 31);
-        const uint32_t a = (i0 >= 0 && i0 < PW) ? tb[i0] : 0u;
-        const uint32_t c = (i0 + 1 >= 0 && i0 + 1 < PW) ? tb[i0 + 1] : 0u;
-        t = o ? ((a << o) | (c >> (32 - o))) : a;
-      }
-    }
+    uint32_t t = o ? ((wa << o) | (wb >> (32 - o))) : wa;
+    if (p0 < F) t &= (F - p0 >= 32) ? 0u : (0xFFFFFFFFu >> (F - p0));   // filler bits are 0
     uint32_t u = 0;
-    for (int i = 0; i < nb; ++i) {
-      const int p = p0 + i;
-      uint32_t bit;
-      if (p < ci.F) bit = 0;
-      else if (p < Kd) bit = (t >> (31 - i)) & 1u;
-      else bit = (crc >> (23 - (p - Kd))) & 1u;
-      if (ci.crc && p < Kd) {
-        const uint32_t msb = (crc >> 23) & 1u;
-        crc = (crc << 1) & 0xFFFFFFu;
-        if (msb ^ bit) crc ^= 0x800063u;  // CRC-24B (0x1800063), crc.py:162-184
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = p0 + 8 * k;
+      if (8 * k < nb) {
+        uint32_t byte;
+        if (p < Kd) {
+          byte = (t >> (24 - 8 * k)) & 0xFFu;
+          if (ci.crc) crc = ((crc << 8) & 0xFFFFFFu) ^ crc_t[((crc >> 16) ^ byte) & 0xFFu];
+        } else {
+          byte = (crc >> (16 - (p - Kd))) & 0xFFu;   // CRC-24B bits after the data
+        }
+        u |= byte << (24 - 8 * k);
       }
-      u = (u << 1) | bit;
     }
-    cw[w * ENC_WG] = nb == 32 ? u : (u << (32 - nb));
+    cw[w * 64] = u;                      // left-aligned
     uint32_t f;
-    const uint32_t q = rsc_bits(u, nb, s0, s1, s2, &f);
-    w0.put(f, nb);
-    w1.put(q, nb);
+    const uint32_t q = rsc_word(u, nb, s0, s1, s2, &f);
+    w0.put(f >> (32 - nb), nb);
+    w1.put(q >> (32 - nb), nb);
+    wa = wb;
+    wb = wn;
   }
   for (int t = 0; t < 3; ++t) {  // trellis termination, encoder 1
-    const uint32_t tail = s1 ^ s2, fb = tail ^ s1 ^ s2;
-    w0.put(fb, 1);
-    w1.put(fb ^ s0 ^ s2, 1);
-    s2 = s1; s1 = s0; s0 = fb;
+    const uint32_t v = rsc_tail(s0, s1, s2);
+    w0.put(v & 1u, 1);
+    w1.put(v >> 1, 1);
   }
+  w0.flush();                    // d0[K+3..K+5] (encoder 2's tail) is OR-ed in by k_encode2
   w1.flush();
-  // encoder 2 on the QPP-interleaved block (turbo_encoder.py:213-313)
-  s0 = s1 = s2 = 0;
+}
+
+__global__ __launch_bounds__(64) void k_encode2(int KWmax, uint32_t* __restrict__ enc, int EW,
+                                                const CbInfo* __restrict__ cbi, int C, int B,
+                                                const uint32_t* __restrict__ cw_scratch) {
+  extern __shared__ uint32_t cwl[];   // [KWmax][64]
+  const int gid = blockIdx.x * 64 + threadIdx.x;
+  if (gid >= C * B) return;           // no barriers: each lane reads back only its own column
+  const int lane = threadIdx.x;
+  const int r = gid / B, b = gid % B;
+  const CbInfo ci = cbi[r];
+  const int K = ci.K, KW = (K + 31) >> 5;
+  const uint32_t* cw = cw_scratch + (size_t)blockIdx.x * KWmax * 64 + lane;
+  for (int w = 0; w < KW; ++w) cwl[w * 64 + lane] = cw[w * 64];
+  uint32_t* e = enc + ((size_t)b * C + r) * 3 * EW;
+  BitWriter w2{e + 2 * EW, 0, 0};
+  uint32_t s0 = 0, s1 = 0, s2 = 0;
   int pi = 0, d = (ci.f1 + ci.f2) % K;
   const int tf2 = (2 * ci.f2) % K;
-  for (int w = 0; w * 32 < K; ++w) {
+  for (int w = 0; w < KW; ++w) {
     const int nb = min(32, K - w * 32);
     uint32_t u = 0;
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i) {
-      if (i < nb) {
-        u |= ((cw[(pi >> 5) * ENC_WG] >> (31 - (pi & 31))) & 1u) << (nb - 1 - i);
-        pi += d; if (pi >= K) pi -= K;
-        d += tf2; if (d >= K) d -= K;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {        // 16 gathers in flight together
+      uint32_t v[16];
+      int sh[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        v[i] = cwl[(pi >> 5) * 64 + lane];
+        sh[i] = pi & 31;
+        int pn = pi + d, dn = d + tf2;
+        pn -= pn >= K ? K : 0;
+        dn -= dn >= K ? K : 0;
+        const bool adv = 16 * h + i < nb;
+        pi = adv ? pn : pi;
+        d = adv ? dn : d;
       }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) u |= ((v[i] << sh[i]) >> 31) << (31 - 16 * h - i);
     }
     uint32_t f;
-    w2.put(rsc_bits(u, nb, s0, s1, s2, &f), nb);
+    w2.put(rsc_word(u, nb, s0, s1, s2, &f) >> (32 - nb), nb);
   }
   for (int t = 0; t < 3; ++t) {
-    const uint32_t tail = s1 ^ s2, fb = tail ^ s1 ^ s2;
-    w0.put(fb, 1);               // sys2 tail -> d0[K+3..K+5]
-    w2.put(fb ^ s0 ^ s2, 1);
-    s2 = s1; s1 = s0; s0 = fb;
+    const uint32_t v = rsc_tail(s0, s1, s2);
+    const int pos = K + 3 + t;   // sys2 tail -> d0[K+3..K+5]
+    if (v & 1u) e[pos >> 5] |= 1u << (31 - (pos & 31));
+    w2.put(v >> 1, 1);
   }
-  w0.flush();
   w2.flush();
 }
 
+size_t encode_scratch_words(int KWmax, int C, int B) { return (((size_t)C * B + 63) / 64) * KWmax * 64; }
+
 int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
-                  const CbInfo* cbi_dev, int C, int B) {
+                  const CbInfo* cbi_dev, int C, int B, uint32_t* cw_scratch) {
   const int64_t n = (int64_t)C * B;
-  const size_t shm = (size_t)KWmax * ENC_WG * sizeof(uint32_t);
-  if (n > 0x7FFFFFFF || shm > 65536) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + ENC_WG - 1) / ENC_WG)), dim3(ENC_WG), shm, s, pw, PW, KWmax, enc,
-                     EW, cbi_dev, C, B);
+  if (n > 0x7FFFFFFF || !cw_scratch) return (int)hipErrorInvalidValue;
+  const size_t shm = (size_t)KWmax * 64 * sizeof(uint32_t);
+  if (shm > 65536) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + ENC_WG - 1) / ENC_WG)), dim3(ENC_WG), 0, s, pw, PW, KWmax, enc,
+                     EW, cbi_dev, C, B, cw_scratch);
+  hipLaunchKernelGGL(k_encode2, dim3((unsigned)((n + 63) / 64)), dim3(64), shm, s, KWmax, enc, EW, cbi_dev, C, B,
+                     cw_scratch);
   return (int)hipGetLastError();
 }
 
@@ -577,11 +638,6 @@ int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t
 // reads are coalesced rows.  Replaces desegment_code_blocks
 // (segmentation.py:266-359), check_crc24a (crc.py:277-307) and the BER count
 // (core/ofdm_core.py:1304-1311).
-__device__ __forceinline__ uint32_t crc24_table_entry(uint32_t i, uint32_t poly) {
-  uint32_t r = i << 16;
-  for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? ((r << 1) ^ poly) : (r << 1);
-  return r & 0xFFFFFFu;
-}
 
 // 32 bits starting at bit position p of an MSB-first stream whose words are
 // strided by `st` elements.

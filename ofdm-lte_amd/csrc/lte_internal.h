@@ -146,7 +146,7 @@ int launch_bf(hipStream_t s, int B, int n_sym, int Nd, int bps, int num_tx, int 
               int64_t inj_z_stride, uint32_t* frame_err, float2* cap_syms, uint8_t* cap_bits);
 
 // turbo modes
-enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3 };  // TM_DECODE: full decode (iterations + decisions)
+enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3, TM_FINAL = 4 };  // TM_DECODE: full decode (iterations + decisions)
 // turbo geometry: rows of one (r, group) block = 4K+12:
 //   [0,K+3) LS (sys + sys1 tail) | [K+3,2K+6) LP1 | [2K+6,3K+9) LP2 | [3K+9,3K+12) LS2T | [3K+12,4K+12) LE
 __host__ __device__ inline int64_t turbo_rows(int K) { return 4LL * K + 12; }

@@ -83,7 +83,7 @@ template <int CODED, int BPS, bool SCF = false>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
                                                 const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B,
-                                                float2* __restrict__ cap_syms) {
+                                                float2* __restrict__ cap_syms, int stage_enc) {
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
@@ -92,6 +92,16 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   const bool active = slot < spw && b < B;
   float2* buf = sm + slot * N;
   float2* pre = SCF ? sm + (spw + slot) * N : buf;   // SC-FDM: QAM symbols -> DFT buffer
+  // coded: the frame's coded streams (~10 KB) are staged in LDS with coalesced
+  // loads, so the 6 rate-match / interleaver bit gathers per RE hit LDS
+  // instead of issuing scattered global loads
+  const uint32_t* fe = enc + (size_t)b * enc_words;
+  if (CODED && stage_enc) {
+    uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
+    if (active)
+      for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
+    fe = es;
+  }
   if (active) {
     for (int k = tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
     if constexpr (SCF)
@@ -100,7 +110,6 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   __syncthreads();
   if (active) {
     const uint32_t* fb = pw + (size_t)b * PW;
-    const uint32_t* fe = enc + (size_t)b * enc_words;
     for (int j = tid; j < g.Nd; j += T) {
       const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
       int idx = 0;
@@ -148,10 +157,12 @@ int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, 
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
   if (sc_fdm && (coded || !g.chirp || !g.bhat || 2 * g.Nd > g.N)) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
-  const size_t shm = (sc_fdm ? 2 : 1) * spw * g.N * sizeof(float2);
+  const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
+  const int stage_enc = coded && enc_shm <= 32768;
+  const size_t shm = (sc_fdm ? 2 : 1) * spw * g.N * sizeof(float2) + (stage_enc ? enc_shm : 0);
 #define LTE_TX(C_, B_, S_)                                                                                         \
   hipLaunchKernelGGL((k_ofdm_tx<C_, B_, S_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words, tx_map, x, \
-                     B, cap_syms)
+                     B, cap_syms, stage_enc)
   if (coded) {
     if (g.bps == 2) LTE_TX(1, 2, false); else if (g.bps == 4) LTE_TX(1, 4, false); else LTE_TX(1, 6, false);
   } else if (sc_fdm) {

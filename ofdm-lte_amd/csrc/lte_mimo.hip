@@ -52,7 +52,7 @@ template <int MODE, int CODED, int BPS>
 __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                       const uint32_t* __restrict__ enc, int enc_words,
                                                       const int32_t* __restrict__ tx_map, float2* __restrict__ x,
-                                                      int B) {
+                                                      int B, int stage_enc) {
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = MWG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
@@ -61,12 +61,20 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
   const int b = gs / per, r = gs - b * per, l = r / m.num_tx, t = r - l * m.num_tx;
   const bool active = slot < spw && b < B;
   float2* buf = sm + slot * N;
+  // coded: the frame's coded streams are staged in LDS (coalesced), so the
+  // rate-match / interleaver bit gathers hit LDS (as in k_ofdm_tx)
+  const uint32_t* fe = enc + (size_t)b * enc_words;
+  if (CODED && stage_enc) {
+    uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
+    if (active)
+      for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
+    fe = es;
+  }
   if (active)
     for (int k = tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
   __syncthreads();
   if (active) {
     const uint32_t* fb = pw + (size_t)b * PW;
-    const uint32_t* fe = enc + (size_t)b * enc_words;
     const int64_t q0 = (int64_t)l * m.res;
     for (int j = tid; j < m.n_dsc; j += T) {
       float2 v;
@@ -106,10 +114,12 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
   const int64_t total = (int64_t)B * g.n_sym * m.num_tx;
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
-  const size_t shm = spw * g.N * sizeof(float2);
+  const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
+  const int stage_enc = coded && enc_shm <= 32768;
+  const size_t shm = spw * g.N * sizeof(float2) + (stage_enc ? enc_shm : 0);
 #define LTE_TXM(M_, C_, B_)                                                                                          \
   hipLaunchKernelGGL((k_ofdm_tx_mimo<M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words,   \
-                     tx_map, x, B)
+                     tx_map, x, B, stage_enc)
 #define LTE_TXM_BPS(M_, C_) \
   do { if (g.bps == 2) LTE_TXM(M_, C_, 2); else if (g.bps == 4) LTE_TXM(M_, C_, 4); else LTE_TXM(M_, C_, 6); } while (0)
   if (m.mode == MIMO_SFBC) {

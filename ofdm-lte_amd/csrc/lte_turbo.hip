@@ -122,7 +122,15 @@ __device__ __forceinline__ int modadd(int a, int b, int K) { a += b; return a >=
 __device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 0 ? a + K : a; }
 
 constexpr int RS = 64;  // row stride (floats): 64 lanes
-constexpr int TW = 8;  // steps between alpha checkpoints (recomputed in halves)
+constexpr int TW = 8;   // steps per sub-window (recomputed in halves of 4)
+#ifndef LTE_TURBO_SUB
+#define LTE_TURBO_SUB 2
+#endif
+#ifndef LTE_TURBO_FINAL_FUSED
+#define LTE_TURBO_FINAL_FUSED 1
+#endif
+constexpr int TSUB = LTE_TURBO_SUB;   // sub-windows per stored alpha checkpoint
+constexpr int SW = TW * TSUB;         // steps per super-window (one checkpoint)
 
 // Buffer-resource row accessor: the 128-bit descriptor (SGPRs) covers one
 // wave's block; a row is addressed by a scalar byte offset (soffset) and the
@@ -156,19 +164,25 @@ struct RowPtr {
 
 // One half-iteration (one constituent decoder pass) for the code block of this lane.
 // All pointers are wave-uniform (scalar) bases; `lane` is the only per-lane
-// offset, so every access is a global load/store with an SGPR base + one
-// shared VGPR offset (no per-load 64-bit vector addresses).
-// One half-iteration (one constituent decoder pass) for the code block of this lane.
-// Forward: alpha over the whole block, checkpoint (states 1..7) every TW = 8
-// steps.  Backward: per 8-step window, reload its inputs and checkpoint and
-// recompute the alphas in two halves of TH = 4 (first the upper half from
-// alpha(8w+4), then the lower half from the checkpoint), so only 4 alpha
-// vectors are ever live.  Recomputed alphas are bit-identical to the forward
-// pass (same operations, same order).  HBM bytes per step: 3 input loads x 2
-// passes + 1 extrinsic store + 7/8 checkpoint store + 7/8 checkpoint load.
+// offset, so every access is a buffer load/store with a scalar row offset and
+// one shared VGPR lane offset.
+// Forward: alpha over the whole block, checkpoint (states 1..7) every SW = 8 *
+// TSUB steps.  Backward, per super-window of SW steps: load its inputs once
+// into VGPRs, recompute the alphas at each 8-step sub-window start from the
+// checkpoint (kept in VGPRs), then sweep the sub-windows top-down; each
+// sub-window recomputes its alphas in two halves of TH = 4 (first the upper
+// half from alpha(8m+4), then the lower half from the sub-window start), so
+// only 4 alpha vectors are ever live.  Recomputed alphas are bit-identical to
+// the forward pass (same operations, same order).  HBM rows per step: 3 input
+// loads x 2 passes + 1 extrinsic store + 7/SW checkpoint store + 7/SW
+// checkpoint load (TSUB = 2: 7.875 rows, against 8.75 with a checkpoint
+// every 8 steps).
+// MODE TM_FINAL: the decoder-1 a-posteriori pass that ends a decode; it also
+// packs the hard decisions L < 0 MSB-first into `bo` (words [kw][64 lanes]),
+// storing each word as the backward sweep reaches its bit 0 (no re-read pass).
 template <int MODE>
 __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck, int lane, int K,
-                                          int f1, int f2, bool first) {
+                                          int f1, int f2, bool first, uint32_t* __restrict__ bo = nullptr) {
   constexpr int TH = TW / 2;
   const int vo = lane * 4;
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * 4));
@@ -177,9 +191,12 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   const RowPtr<float> LS2T{rb, 3 * K + 9, vo};
   const RowPtr<float> LE{rb, 3 * K + 12, vo};
   const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * TURBO_CK_ROWS * RS * 4)), 0, vo};
-  const int nfull = K / TW;   // every LTE K is a multiple of 8
+  const int nsub = K / TW;   // every LTE K is a multiple of 8
   const int tf2 = (2 * f2) % K;
   const bool use_la = !first;
+  RowPtr<uint32_t> bout{};
+  uint32_t acc = 0;
+  if (MODE == TM_FINAL) bout = RowPtr<uint32_t>{make_rsrc(bo, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
 
   // ---------------- forward pass
   float a[8];
@@ -188,9 +205,11 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
   for (int s = 1; s < 8; ++s) a[s] = LTE_NEG_BIG;
   int pi = 0, d = (f1 + f2) % K;
 #pragma unroll 1
-  for (int w = 0; w < nfull; ++w) {
+  for (int w = 0; w < nsub; ++w) {
+    if (w % TSUB == 0) {
 #pragma unroll
-    for (int s = 1; s < 8; ++s) ck.st(w * TURBO_CK_ROWS + s - 1, a[s]);
+      for (int s = 1; s < 8; ++s) ck.st((w / TSUB) * TURBO_CK_ROWS + s - 1, a[s]);
+    }
     float ls[TW], lp[TW], la[TW];
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
@@ -227,87 +246,129 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
     bterms(b, c, t0, t1);
     bnext(t0, t1, b);
   }
-  // pi/d are now at k = K; step back to the start of the last window
-  if (MODE == TM_DEC2) {
-#pragma unroll
-    for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
-  }
+  // pi/d are now at k = K (decoder 2); each super-window steps them back to
+  // its start, walks forward while loading and back again while storing
+  const int nsw = (nsub + TSUB - 1) / TSUB;
 #pragma unroll 1
-  for (int w = nfull - 1; w >= 0; --w) {
-    float cka[8];
-    cka[0] = 0.0f;
-#pragma unroll
-    for (int s = 1; s < 8; ++s) cka[s] = ck.ld(w * TURBO_CK_ROWS + s - 1);
-    float ls[TW], lp[TW], la[TW];
-    int pl[TW];
+  for (int q = nsw - 1; q >= 0; --q) {
+    const int ns = min(TSUB, nsub - q * TSUB);   // sub-windows here (wave-uniform)
+    const int k0 = q * SW;
+    if (MODE == TM_DEC2) {
+#pragma unroll 1
+      for (int j = 0; j < ns * TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+    }
+    float ls[SW], lp[SW], la[SW];
     int pp = pi, dd = d;
 #pragma unroll
-    for (int j = 0; j < TW; ++j) {
-      const int k = w * TW + j;
-      const int p = (MODE == TM_DEC2) ? pp : k;
-      pl[j] = p;
-      ls[j] = LS.ld(p);
-      lp[j] = LP.ld(k);
-      la[j] = use_la ? LE.ld(p) : 0.0f;
-      if (MODE == TM_DEC2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
+    for (int m = 0; m < TSUB; ++m) {
+      if (m < ns) {
+#pragma unroll
+        for (int j = 0; j < TW; ++j) {
+          const int i = m * TW + j, k = k0 + i;
+          const int p = (MODE == TM_DEC2) ? pp : k;
+          ls[i] = LS.ld(p);
+          lp[i] = LP.ld(k);
+          la[i] = use_la ? LE.ld(p) : 0.0f;
+          if (MODE == TM_DEC2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
+        }
+      }
+    }
+    // alpha at every sub-window start: the checkpoint, then forward
+    float cks[TSUB][8];
+    cks[0][0] = 0.0f;
+#pragma unroll
+    for (int s = 1; s < 8; ++s) cks[0][s] = ck.ld(q * TURBO_CK_ROWS + s - 1);
+#pragma unroll
+    for (int m = 1; m < TSUB; ++m) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) cks[m][s] = cks[m - 1][s];
+      if (m < ns) {
+#pragma unroll
+        for (int j = 0; j < TW; ++j) {
+          const int i = (m - 1) * TW + j;
+          float c[4], o[8];
+          gam(ls[i], lp[i], la[i], c);
+          fwd(cks[m], c, o);
+#pragma unroll
+          for (int s = 0; s < 8; ++s) cks[m][s] = o[s];
+        }
+      }
     }
 #pragma unroll
-    for (int h = 1; h >= 0; --h) {
-      if (h == 0) {
-        // the lower half's recompute repeats the chain the upper half ran from
-        // the checkpoint; hide that from CSE so it is recomputed (cheap VALU)
-        // instead of holding 3 alpha vectors live across the upper half
+    for (int m = TSUB - 1; m >= 0; --m) {
+      if (m >= ns) continue;
 #pragma unroll
-        for (int s = 1; s < 8; ++s) asm volatile("" : "+v"(cka[s]));
+      for (int h = 1; h >= 0; --h) {
+        // each recompute repeats a chain already run (the lower half: the one
+        // the upper half ran from the sub-window start; the upper half: the
+        // one that produced the next sub-window's start); hide that from CSE
+        // so it is recomputed (cheap VALU) instead of holding alpha vectors live
 #pragma unroll
-        for (int j = 0; j < TH; ++j) asm volatile("" : "+v"(ls[j]), "+v"(lp[j]), "+v"(la[j]));
-      }
-      // A[j] = alpha before step w*TW + h*TH + j
-      float A[TH][8];
+        for (int s = 1; s < 8; ++s) asm volatile("" : "+v"(cks[m][s]));
 #pragma unroll
-      for (int s = 0; s < 8; ++s) A[0][s] = cka[s];
-      if (h == 1) {
+        for (int j = 0; j < (TSUB > 1 ? TW : TH); ++j)
+          asm volatile("" : "+v"(ls[m * TW + j]), "+v"(lp[m * TW + j]), "+v"(la[m * TW + j]));
+        // A[j] = alpha before step k0 + m*TW + h*TH + j
+        float A[TH][8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) A[0][s] = cks[m][s];
+        if (h == 1) {
+#pragma unroll
+          for (int j = 0; j < TH; ++j) {
+            const int i = m * TW + j;
+            float c[4], o[8];
+            gam(ls[i], lp[i], la[i], c);
+            fwd(A[0], c, o);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) A[0][s] = o[s];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < TH - 1; ++j) {
+          const int i = m * TW + h * TH + j;
+          float c[4];
+          gam(ls[i], lp[i], la[i], c);
+          fwd(A[j], c, A[j + 1]);
+        }
+        // gamma is 7 VALU ops: recompute it below rather than keep the
+        // recompute's 4 gamma vectors live next to the inputs
 #pragma unroll
         for (int j = 0; j < TH; ++j) {
-          float c[4], o[8];
-          gam(ls[j], lp[j], la[j], c);
-          fwd(A[0], c, o);
+          const int i = m * TW + h * TH + j;
+          asm volatile("" : "+v"(ls[i]), "+v"(lp[i]), "+v"(la[i]));
+        }
 #pragma unroll
-          for (int s = 0; s < 8; ++s) A[0][s] = o[s];
+        for (int j = TH - 1; j >= 0; --j) {
+          const int i = m * TW + h * TH + j;
+          const int k = k0 + i;
+          float c[4];
+          gam(ls[i], lp[i], la[i], c);
+          const float L = bstep(b, c, A[j]);
+          if (MODE == TM_DEC1) {
+            LE.st(k, (0.5f * L - la[i]) - ls[i]);
+          } else if (MODE == TM_DEC2) {
+            dd = modsub(dd, tf2, K);
+            pp = modsub(pp, dd, K);   // pp = pi(k)
+            LE.st(pp, (0.5f * L - la[i]) - ls[i]);
+          } else if (MODE == TM_APP) {  // a-posteriori LLR in place of the extrinsic row
+            LE.st(k, L);
+          } else {  // TM_FINAL
+            // L is still stored: without a per-step store into the block the
+            // compiler schedules this pass with ~40 more VGPRs
+            LE.st(k, L);
+            acc |= (L < 0.0f ? 1u : 0u) << (31 - (k & 31));
+          }
         }
       }
-#pragma unroll
-      for (int j = 0; j < TH - 1; ++j) {
-        const int jj = h * TH + j;
-        float c[4];
-        gam(ls[jj], lp[jj], la[jj], c);
-        fwd(A[j], c, A[j + 1]);
-      }
-      // gamma is 7 VALU ops: recompute it below rather than keep the
-      // recompute's 4 gamma vectors live next to the inputs
-#pragma unroll
-      for (int j = 0; j < TH; ++j)
-        asm volatile("" : "+v"(ls[h * TH + j]), "+v"(lp[h * TH + j]), "+v"(la[h * TH + j]));
-#pragma unroll
-      for (int j = TH - 1; j >= 0; --j) {
-        const int jj = h * TH + j;
-        const int k = w * TW + jj;
-        float c[4];
-        gam(ls[jj], lp[jj], la[jj], c);
-        const float L = bstep(b, c, A[j]);
-        if (MODE == TM_DEC1) {
-          LE.st(k, (0.5f * L - la[jj]) - ls[jj]);
-        } else if (MODE == TM_DEC2) {
-          LE.st(pl[jj], (0.5f * L - la[jj]) - ls[jj]);
-        } else {  // TM_APP: a-posteriori LLR in place of the extrinsic row
-          LE.st(k, L);
+      if (MODE == TM_FINAL) {   // words start on sub-window boundaries (32 = 4 * TW)
+        const int k = k0 + m * TW;
+        if ((k & 31) == 0) {
+          bout.st(k >> 5, acc);
+          acc = 0;
         }
       }
     }
-    if (MODE == TM_DEC2) {
-#pragma unroll
-      for (int j = 0; j < TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
-    }
+    if (MODE == TM_DEC2) { pi = pp; d = dd; }   // back at k0
   }
 }
 
@@ -334,9 +395,11 @@ __global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mo
     half_pass<TM_DEC1>(base, ck, lane, K, jb.f1, jb.f2, it == 0);
     half_pass<TM_DEC2>(base, ck, lane, K, jb.f1, jb.f2, false);
   }
-  // final pass = decoder 1 a-posteriori LLRs (turbo_decoder.py:436-446), then
-  // hard decisions L < 0 packed MSB-first from the rows this lane just wrote
-  // (kept out of the pass loop: accumulating bits there costs ~30 VGPRs).
+  // final pass = decoder 1 a-posteriori LLRs (turbo_decoder.py:436-446) and
+  // the hard decisions L < 0, packed MSB-first
+#if LTE_TURBO_FINAL_FUSED
+  half_pass<TM_FINAL>(base, ck, lane, K, jb.f1, jb.f2, iters == 0, bo);
+#else
   half_pass<TM_APP>(base, ck, lane, K, jb.f1, jb.f2, iters == 0);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(base, (uint32_t)(turbo_rows(K) * RS * 4));
   const RowPtr<float> LE{rb, 3 * K + 12, lane * 4};
@@ -351,6 +414,7 @@ __global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mo
     }
     bout.st(w, acc);
   }
+#endif
 }
 
 int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode) {

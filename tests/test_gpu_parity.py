@@ -117,7 +117,8 @@ def test_turbo_decode_golden(C, golden, oracle, K, its):
         assert np.array_equal(dec, ref)
 
 
-@pytest.mark.parametrize('K,n,snr', [(5568, 130, 1.5), (5632, 70, 3.0), (6144, 64, 5.0), (40, 200, 2.0)])
+@pytest.mark.parametrize('K,n,snr', [(5568, 130, 1.5), (5632, 70, 3.0), (6144, 64, 5.0), (40, 200, 2.0),
+                                     (48, 64, 2.0), (56, 64, 2.0), (1056, 64, 2.5)])
 def test_turbo_decode_batch_vs_oracle(C, oracle, K, n, snr):
     """Several decoder waves of one K: bit-exact vs the float32 model; where the
     reference decoder converges (5 dB) also bit-exact vs the float64 oracle."""

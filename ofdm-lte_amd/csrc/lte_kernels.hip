@@ -102,33 +102,55 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
       for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
     fe = es;
   }
+  // coded: every tx_map entry and RE position of this thread's (at most QM)
+  // data REs is loaded before the LDS zeroing and the barrier, so their
+  // latency overlaps that instead of serialising with the per-RE gathers
+  constexpr int QM = 4;   // Nd < N/2 = QM * T for every LTE profile
+  int srcs[CODED ? QM : 1][CODED ? BPS : 1];
+  int kpos[CODED ? QM : 1];
+  if constexpr (CODED) {
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = tid + q * T;
+      const bool ok = active && j < g.Nd;
+      const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
+#pragma unroll
+      for (int m = 0; m < BPS; ++m) srcs[q][m] = ok ? tx_map[t0 + m] : -1;
+      kpos[q] = ok ? g.data_idx[j] : 0;
+    }
+  }
   if (active) {
     for (int k = tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
     if constexpr (SCF)
       for (int k = g.Nd + tid; k < N; k += T) pre[k] = make_float2(0.f, 0.f);
   }
   __syncthreads();
-  if (active) {
-    const uint32_t* fb = pw + (size_t)b * PW;
-    for (int j = tid; j < g.Nd; j += T) {
-      const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
+  if (CODED && active) {
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = tid + q * T;
+      if (j >= g.Nd) break;
       int idx = 0;
       bool zero = false;
-      if constexpr (CODED) {
-        int src[BPS];
 #pragma unroll
-        for (int m = 0; m < BPS; ++m) src[m] = tx_map[t0 + m];
-#pragma unroll
-        for (int m = 0; m < BPS; ++m) {
-          zero |= src[m] == -2;
-          const uint32_t bit = src[m] >= 0 ? getbit(fe, src[m]) : 0u;
-          idx = (idx << 1) | (int)bit;
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, t0 + m);
+      for (int m = 0; m < BPS; ++m) {
+        zero |= srcs[q][m] == -2;
+        const uint32_t bit = srcs[q][m] >= 0 ? getbit(fe, srcs[q][m]) : 0u;
+        idx = (idx << 1) | (int)bit;
       }
       const float2 sym = zero ? make_float2(0.f, 0.f) : qam_point<BPS>(idx);
+      buf[kpos[q]] = sym;
+      if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + j] = sym;
+    }
+  }
+  if (active) {
+    const uint32_t* fb = pw + (size_t)b * PW;
+    for (int j = tid; j < (CODED ? 0 : g.Nd); j += T) {   // uncoded: payload bits in order
+      const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
+      int idx = 0;
+#pragma unroll
+      for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, t0 + m);
+      const float2 sym = qam_point<BPS>(idx);
       if constexpr (SCF) pre[j] = sym;
       else buf[g.data_idx[j]] = sym;
       if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + j] = sym;
@@ -246,6 +268,7 @@ __device__ __forceinline__ float2 jakes_coef(const float* __restrict__ ph, float
 // read LDS instead of re-fetching x through L1/L2 (the kernel was latency
 // bound at ~2.2 TB/s); otherwise the taps load from global memory.
 constexpr int CH_HALO = 256;
+constexpr int CH_MAXP = 8;   // taps held in registers (ITU profiles have <= 6)
 
 __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh, int n_paths,
                                                 const int32_t* __restrict__ delays, const float* __restrict__ gains,
@@ -273,6 +296,32 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
       xs[2 * e + 1] = make_float2(v.z, v.w);
     }
     __syncthreads();
+  }
+  if (rayleigh && staged && fD == 0.0f && n_paths <= CH_MAXP) {
+    // static taps (fD = 0, the OFDMSimulator default): coefficients and delays
+    // in registers, the halo (zero before the frame start) makes every tap an
+    // unconditional LDS read
+    float2 cf[CH_MAXP];
+    int dl[CH_MAXP];
+#pragma unroll
+    for (int p = 0; p < CH_MAXP; ++p) {
+      cf[p] = p < n_paths ? coef[cb + p] : make_float2(0.f, 0.f);
+      dl[p] = p < n_paths ? delays[p] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < CH_PER; ++i) {
+      const int n = n0 + i * WG + threadIdx.x;
+      if (n >= L) break;
+      float2 v = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int p = 0; p < CH_MAXP; ++p)
+        if (p < n_paths) v = cadd(v, cmul(cf[p], xs[n - dl[p] - n0 + CH_HALO]));
+      yf[n] = v;
+      pw += v.x * v.x + v.y * v.y;
+    }
+    const float t = block_sum(pw, red);
+    if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blk] = t;
+    return;
   }
 #pragma unroll
   for (int i = 0; i < CH_PER; ++i) {

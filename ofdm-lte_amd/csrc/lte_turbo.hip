@@ -126,6 +126,9 @@ constexpr int TW = 8;   // steps per sub-window (recomputed in halves of 4)
 #ifndef LTE_TURBO_SUB
 #define LTE_TURBO_SUB 2
 #endif
+#ifndef LTE_TURBO_HALVES
+#define LTE_TURBO_HALVES 2
+#endif
 #ifndef LTE_TURBO_FINAL_FUSED
 #define LTE_TURBO_FINAL_FUSED 1
 #endif
@@ -183,7 +186,7 @@ struct RowPtr {
 template <int MODE>
 __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck, int lane, int K,
                                           int f1, int f2, bool first, uint32_t* __restrict__ bo = nullptr) {
-  constexpr int TH = TW / 2;
+  constexpr int TH = TW / LTE_TURBO_HALVES;
   const int vo = lane * 4;
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * 4));
   const RowPtr<float> LS{rb, 0, vo};
@@ -298,7 +301,7 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
     for (int m = TSUB - 1; m >= 0; --m) {
       if (m >= ns) continue;
 #pragma unroll
-      for (int h = 1; h >= 0; --h) {
+      for (int h = LTE_TURBO_HALVES - 1; h >= 0; --h) {
         // each recompute repeats a chain already run (the lower half: the one
         // the upper half ran from the sub-window start; the upper half: the
         // one that produced the next sub-window's start); hide that from CSE
@@ -312,9 +315,9 @@ __device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __re
         float A[TH][8];
 #pragma unroll
         for (int s = 0; s < 8; ++s) A[0][s] = cks[m][s];
-        if (h == 1) {
+        if (h > 0) {
 #pragma unroll
-          for (int j = 0; j < TH; ++j) {
+          for (int j = 0; j < h * TH; ++j) {
             const int i = m * TW + j;
             float c[4], o[8];
             gam(ls[i], lp[i], la[i], c);

@@ -1,6 +1,6 @@
 # GPU session: config-2 throughput vs frames per step
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-for F in 32768 49152 65536 98304; do
+for F in ${FRAMES_LIST:-32768 49152 65536 98304}; do
   timeout -k 10 300 python bench.py --frames $F --steps 3 --warmup 1 --no-cpu > gpurun_out/bench_F$F.log 2> gpurun_out/bench_F$F.err || { echo "F=$F failed rc=$?"; tail -3 gpurun_out/bench_F$F.err; exit 1; }
   python -c "
 import json; d=json.loads(open('gpurun_out/bench_F$F.log').read().strip().splitlines()[-1]); r=d['roofline']

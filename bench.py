@@ -32,8 +32,11 @@ HBM_PEAK_GBS = 8000.0
 B_SF = 2_116_904
 # turbo work per subframe = sum(K+3) x 17 passes x ~100 ops
 TURBO_OPS_SF = 27_919 * 17 * 100
-# f32 VALU lane-ops/s of one MI355X: 256 CUs x 128 lanes x 2.4 GHz (MI355X_MICROARCH.md)
-VALU_PEAK_OPS = 256 * 128 * 2.4e9
+# VALU issue peak of one MI355X for the decoder's instruction mix (v_add_f32 /
+# v_sub_f32 / v_max_f32 / v_max3_f32, non-packed): one wave64 instruction per 4
+# cycles per SIMD (16 lanes, MI355X_MICROARCH.md "vector-instruction ISSUE
+# cost"), 1024 SIMDs at 2.4 GHz = 39.3 T lane-ops/s
+VALU_PEAK_OPS = 256 * 4 * 16 * 2.4e9
 
 
 def cpu_baseline(seconds=15.0):
@@ -59,9 +62,11 @@ def cpu_baseline(seconds=15.0):
                       f'{el:.1f} s on 1 host core (oracle: NumPy + C, float64)'}
 
 
-def load_traffic():
-    """HBM bytes per turbo launch from the committed rocprofv3 --pmc summary."""
-    p = os.path.join(ROOT, 'profiles', 'pmc_turbo_traffic.json')
+def load_traffic(name='pmc_turbo_traffic.json'):
+    """Per-frame counters of the turbo kernel from a committed rocprofv3 --pmc
+    summary (HBM bytes: pmc_turbo_traffic.json; SQ instruction counts:
+    pmc_turbo_sq.json)."""
+    p = os.path.join(ROOT, 'profiles', name)
     if os.path.exists(p):
         try:
             return json.load(open(p))
@@ -75,7 +80,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--frames', type=int, default=65536, help='subframes per step per GPU (65536: 5120 turbo waves = 5 per SIMD, the VGPR-bound occupancy)')
+    ap.add_argument('--frames', type=int, default=65536, help='subframes per step per GPU (65536: 5120 turbo waves, 1.7 generations at 3 waves per SIMD; '
+                         '39296 / 65536 / 78592 measured within 2 %% per frame)')
     ap.add_argument('--iters', type=int, default=8)
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
@@ -146,6 +152,7 @@ def main():
     alg_per_launch = alg_bytes_total / max(t_n, 1)
     achieved = alg_per_launch / (avg_launch_ms * 1e-3) / 1e9 if t_n else 0.0
     traffic = load_traffic()
+    sq = load_traffic('pmc_turbo_sq.json')
     roof = {'bound': 'hbm', 'kernel': 'k_turbo', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
             # HBM bytes per launch from the committed PMC passes (profiles/pmc_turbo_traffic.json:
@@ -169,9 +176,14 @@ def main():
             'turbo_valu': {'ops_per_subframe': TURBO_OPS_SF,
                            'achieved_Tops': round(TURBO_OPS_SF * F / (avg_launch_ms * 1e-3) / 1e12, 3)
                            if t_n else 0.0,
-                           'peak_Tops': VALU_PEAK_OPS / 1e12,
+                           'peak_Tops': round(VALU_PEAK_OPS / 1e12, 2),
                            'frac': round(TURBO_OPS_SF * F / (avg_launch_ms * 1e-3) / VALU_PEAK_OPS, 4)
-                           if t_n else 0.0}}
+                           if t_n else 0.0,
+                           # issued VALU lane-ops per subframe from the committed SQ_INSTS_VALU pass
+                           # (profiles/pmc_turbo_sq.json): what the SIMDs actually execute
+                           'issued_ops_per_subframe': round(sq['valu_wave_instr_per_frame'] * 64) if sq else None,
+                           'issued_frac': round(sq['valu_wave_instr_per_frame'] * 64 * Fp / (avg_launch_ms * 1e-3)
+                                                / VALU_PEAK_OPS, 4) if sq and t_n else None}}
     ber = (counts[:, 0] / np.maximum(counts[:, 1], 1)).tolist()
     bler = (counts[:, 2] / np.maximum(counts[:, 3], 1)).tolist()
     out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'subframes/s', 'n_gpus': world,

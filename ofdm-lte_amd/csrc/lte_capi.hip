@@ -372,6 +372,9 @@ struct lte_plan {
   TableSet tabs;
   Grid grid;
   hipStream_t stream = nullptr;
+  // pipelined coded SISO chain: decoder-side stream + one event per chunk (+ join)
+  hipStream_t stream2 = nullptr;
+  std::vector<hipEvent_t> pipe_ev;
   std::vector<CbInfo> cbs;
   std::vector<float> gains_f;
   // device
@@ -418,7 +421,8 @@ namespace {
 struct Timer {  // brackets one launch with events when timing is on
   lte_plan* p;
   int id, e0;
-  Timer(lte_plan* pl, int kid) : p(pl), id(kid), e0(-1) {
+  hipStream_t st;
+  Timer(lte_plan* pl, int kid, hipStream_t s_ = nullptr) : p(pl), id(kid), e0(-1), st(s_ ? s_ : pl->stream) {
     if (!p->timing) return;
     e0 = (int)p->evuse.size() * 2;
     if ((int)p->evpool.size() < e0 + 2) {
@@ -428,11 +432,11 @@ struct Timer {  // brackets one launch with events when timing is on
       p->evpool.push_back(a);
       p->evpool.push_back(b);
     }
-    (void)hipEventRecord(p->evpool[e0], p->stream);
+    (void)hipEventRecord(p->evpool[e0], st);
   }
   ~Timer() {
     if (e0 < 0) return;
-    (void)hipEventRecord(p->evpool[e0 + 1], p->stream);
+    (void)hipEventRecord(p->evpool[e0 + 1], st);
     p->evuse.push_back({id, e0});
   }
 };
@@ -1078,6 +1082,8 @@ int lte_plan_destroy(lte_plan* p) {
   p->Hm.release(); p->m_pig.release(); p->link_part.release(); p->link_sigma.release(); p->inj_lz.release();
   p->inj_lh.release(); p->m_W.release(); p->bf_cb.release(); p->bf_fr.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
+  for (auto e : p->pipe_ev) (void)hipEventDestroy(e);
+  if (p->stream2) (void)hipStreamDestroy(p->stream2);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
   return LTE_OK;
@@ -1378,6 +1384,125 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   return LTE_OK;
 }
 
+// Chunks of the pipelined coded SISO chain (LTE_PIPELINE_CHUNKS, default 1 =
+// off).  Measured on MI355X at 65536 frames: 2 / 3 / 4 chunks 4 / 7 / 26 %
+// slower than one pass -- the decoder already streams HBM at ~5.5 TB/s, so the
+// overlapped front end only takes bandwidth from it, and half-size decoder
+// launches fill the CUs less well.  Kept as an opt-in (parity-tested: results
+// do not depend on the chunking, every kernel is per frame with Philox keyed
+// by frame id and chunks are whole 64-frame groups).
+static int pipeline_chunks(const lte_plan* p, const lte_run_args* a, int B, int stages) {
+  const lte_plan_desc& d = p->d;
+  if (d.chain != LTE_CHAIN_CODED || p->mimo || p->bf || stages != LTE_STAGE_ALL) return 1;
+  if (a->bits || a->phases || a->noise || a->in_signal) return 1;
+  if (a->cap_signal_tx || a->cap_signal_rx || a->cap_data_syms || a->cap_H || a->cap_pilot_stats || a->cap_bits_rx ||
+      a->cap_llr || a->cap_tx_syms || a->cap_noise_power)
+    return 1;
+  const int G = (B + 63) / 64;
+  int n = 1;
+  if (const char* e = std::getenv("LTE_PIPELINE_CHUNKS")) n = std::atoi(e);
+  return std::max(1, std::min(n, G));
+}
+
+// Coded SISO chain with the batch cut into chunks of whole 64-frame groups:
+// the front end of chunk c+1 (payload .. dematch, on the plan's stream) runs
+// while the decoder side of chunk c (turbo, CRC, on stream2) runs, so the
+// compute-bound TX / RX kernels overlap the HBM-bound decoder.  Same kernels,
+// same per-frame buffers (offset by the chunk's first frame) as lte_run.
+static int run_coded_pipelined(lte_plan* p, const lte_run_args* a, int B, int chunks) {
+  const lte_plan_desc& d = p->d;
+  const Grid& g = p->grid;
+  const int rx = d.num_rx;
+  const bool ray = d.channel == LTE_CH_RAYLEIGH;
+  hipStream_t s = p->stream;
+  if (!p->stream2 && hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking) != hipSuccess)
+    return fail(LTE_EHIP, "stream creation failed");
+  while ((int)p->pipe_ev.size() < chunks + 1) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(LTE_EHIP, "event creation");
+    p->pipe_ev.push_back(e);
+  }
+  hipStream_t s2 = p->stream2;
+  const int G = (B + 63) / 64;
+  const int nblk = channel_nblk(p->L);
+  const int maxd = ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0;
+  const float2* ysrc = ray ? p->y.p : p->x.p;
+  const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
+  for (int c = 0; c < chunks; ++c) {
+    const int g0 = (int)((int64_t)G * c / chunks), g1 = (int)((int64_t)G * (c + 1) / chunks);
+    const int b0 = g0 * 64, bend = std::min(B, g1 * 64), Bc = bend - b0;
+    if (Bc <= 0) continue;
+    const size_t fr = (size_t)b0;
+    {
+      Timer t(p, KN_PAYLOAD);
+      LCHK(launch_payload(s, p->pw.p + fr * p->PW, p->PW, d.n_bits, 1, p->fid.p + fr, a->seed, Bc, nullptr, 0));
+    }
+    {
+      Timer t(p, KN_ENCODE);
+      LCHK(launch_encode(s, p->pw.p + fr * p->PW, p->PW, p->KWmax, p->enc.p + fr * p->enc_words, p->EW, p->cbi.p,
+                         p->C, Bc, p->enc_cw.p));
+    }
+    {
+      Timer t(p, KN_OFDM_TX);
+      LCHK(launch_ofdm_tx(s, g, 1, p->pw.p + fr * p->PW, p->PW, p->enc.p + fr * p->enc_words, p->enc_words,
+                          p->tx_map.p, p->x.p + fr * p->L, Bc, nullptr, 0));
+    }
+    const size_t fp = fr * rx * d.n_paths;
+    if (ray) {
+      Timer t(p, KN_FADING);
+      LCHK(launch_fading(s, Bc, rx, d.n_paths, p->gains.p, p->fid.p + fr, a->seed, nullptr, 0, p->phases.p + fp * 16,
+                         p->coef.p + fp));
+    }
+    {
+      Timer t(p, KN_CHANNEL);
+      LCHK(launch_channel(s, g, Bc, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
+                          p->phases.p + fp * 16, p->coef.p + fp, p->x.p + fr * p->L, p->y.p + fr * rx * p->L,
+                          p->pow_part.p + fr * rx * nblk, nblk, maxd));
+      LCHK(launch_npow(s, Bc, rx, p->pow_part.p + fr * rx * nblk, nblk, p->L, p->snr_lin.p + fr,
+                       p->npow.p + fr * rx));
+    }
+    const size_t fh = fr * rx * p->n_grp;
+    {
+      Timer t(p, KN_RX_CHEST);
+      LCHK(launch_rx_chest(s, g, Bc, rx, ysrc + fr * yfs, yrs, yfs, p->npow.p + fr * rx, p->fid.p + fr, a->seed,
+                           nullptr, 0, p->H.p + fh * d.N, p->pstats.p + fh * 2));
+    }
+    {
+      Timer t(p, KN_RX_DATA);
+      LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, Bc, rx, ysrc + fr * yfs, yrs, yfs, p->H.p + fh * d.N,
+                          p->npow.p + fr * rx, p->snr_lin.p + fr, p->fid.p + fr, a->seed, nullptr, 0,
+                          p->pw.p + fr * p->PW, p->PW, d.n_bits, p->frame_err.p + fr, p->llr.p + fr * p->n_re_bits,
+                          nullptr, nullptr, 0));
+    }
+    {
+      Timer t(p, KN_DEMATCH);
+      LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, bend, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C, g0));
+    }
+    // decoder side of this chunk on stream2, after its front end
+    HIPCHK(hipEventRecord(p->pipe_ev[c], s));
+    HIPCHK(hipStreamWaitEvent(s2, p->pipe_ev[c], 0));
+    std::vector<TurboJob> jobs(p->C);
+    for (int r = 0; r < p->C; ++r) {
+      const CbInfo& cb = p->cbs[r];
+      jobs[r] = TurboJob{p->blk[r].p + (size_t)g0 * turbo_rows(cb.K) * 64,
+                         p->ckpt[r].p + (size_t)g0 * turbo_nwin(cb.K) * TURBO_CK_ROWS * 64,
+                         p->decb[r].p + (size_t)g0 * turbo_kw(cb.K) * 64, cb.K, cb.f1, cb.f2, g1 - g0};
+    }
+    {
+      Timer t(p, KN_TURBO, s2);
+      LCHK(launch_turbo_jobs(s2, jobs.data(), p->C, d.turbo_iters, TM_DEC1));
+    }
+    {
+      Timer t(p, KN_CRC, s2);
+      LCHK(launch_crc_count(s2, p->cbi.p, p->C, p->dec_ptrs.p, p->kw_dev.p, bend, p->pw.p, p->PW, d.n_bits,
+                            p->frame_err.p, p->frame_crc.p, nullptr, b0));
+    }
+  }
+  HIPCHK(hipEventRecord(p->pipe_ev[chunks], s2));
+  HIPCHK(hipStreamWaitEvent(s, p->pipe_ev[chunks], 0));
+  return LTE_OK;
+}
+
 int lte_run(lte_plan* p, const lte_run_args* a) {
   if (!p || !a) return fail(LTE_EINVAL, "null argument");
   const lte_plan_desc& d = p->d;
@@ -1462,11 +1587,18 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "the beamforming chain runs all stages");
     return run_bf(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_z, inj_z_stride);
   }
-  if (do_tx || a->bits) {
+  const int chunks = pipeline_chunks(p, a, B, stages);
+  if (chunks > 1) {
+    const int e = run_coded_pipelined(p, a, B, chunks);
+    if (e != LTE_OK) return e;
+  }
+  const bool seq = chunks <= 1;   // the unpipelined chain
+  if (seq && (do_tx || a->bits)) {
     Timer t(p, KN_PAYLOAD);
     LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
   }
-  if (do_tx) {
+  if (!seq) {
+  } else if (do_tx) {
     if (coded) {
       Timer t(p, KN_ENCODE);
       LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_cw.p));
@@ -1498,19 +1630,19 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   }
   const float2* ysrc = ray ? p->y.p : p->x.p;
   const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
-  if (ray) {
+  if (seq && ray) {
     Timer t(p, KN_FADING);
     LCHK(launch_fading(s, B, rx, d.n_paths, p->gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, p->phases.p,
                        p->coef.p));
   }
-  {
+  if (seq) {
     Timer t(p, KN_CHANNEL);
     LCHK(launch_channel(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
                         p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, channel_nblk(p->L),
                         ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0));
     LCHK(launch_npow(s, B, rx, p->pow_part.p, channel_nblk(p->L), p->L, p->snr_lin.p, p->npow.p));
   }
-  if (do_rx) {
+  if (seq && do_rx) {
     Timer t(p, KN_RX_CHEST);
     LCHK(launch_rx_chest(s, g, B, rx, ysrc, yrs, yfs, p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, p->H.p,
                          p->pstats.p));
@@ -1525,7 +1657,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
     cap_bits_dev = p->cap_bits.p;
   }
-  if (do_rx) {
+  if (seq && do_rx) {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, p->H.p, p->npow.p, p->snr_lin.p,
                         p->fid.p, a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p, p->llr.p,
@@ -1534,7 +1666,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
                         // MRC receiver (core/ofdm_core.py:1340-1534) never de-precodes
                         (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0));
   }
-  if (coded && do_rx) {
+  if (seq && coded && do_rx) {
     {
       Timer t(p, KN_DEMATCH);
       LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));

@@ -55,8 +55,10 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                    const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                    const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
                    uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, int sc_fdm = 0);
+// g0 / b0: first 64-frame group / first frame of a frame range [.., B) of the
+// plan's buffers (the pipelined chain runs the decoder side per chunk)
 int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
-                   const int64_t* rows, int C);
+                   const int64_t* rows, int C, int g0 = 0);
 int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
                  int G, int mode);
 struct TurboJob {           // one CB slot of a batch: G groups of 64 code blocks of size K
@@ -74,7 +76,7 @@ struct TurboJobs {
 int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode);
 int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
                      const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
-                     uint8_t* cap_bits);
+                     uint8_t* cap_bits, int b0 = 0);
 int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, const int32_t* snr_idx,
                       const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts);
 int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);

@@ -454,9 +454,10 @@ int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, 
 constexpr int DM_CH = 64;
 __global__ __launch_bounds__(256) void k_dematch(const float* __restrict__ llr, int T, int B,
                                                  const int32_t* __restrict__ rx_map,
-                                                 float* const* __restrict__ blk, const int64_t* __restrict__ rows) {
+                                                 float* const* __restrict__ blk, const int64_t* __restrict__ rows,
+                                                 int g0) {
   __shared__ float tile[64][DM_CH + 1];   // [frame][t], +1: conflict-free column reads
-  const int g = blockIdx.y;
+  const int g = g0 + blockIdx.y;
   const int t0 = blockIdx.x * DM_CH;
   const int nt = min(DM_CH, T - t0);
   // load: 16 lanes x float4 per frame row (256-B coalesced); scalar tail
@@ -491,11 +492,12 @@ __global__ __launch_bounds__(256) void k_dematch(const float* __restrict__ llr, 
 }
 
 int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
-                   const int64_t* rows, int C) {
+                   const int64_t* rows, int C, int g0) {
   (void)C;
-  const int G = (B + 63) / 64;
-  if (G > 65535) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_dematch, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B, rx_map, blk, rows);
+  const int G = (B + 63) / 64 - g0;   // groups g0 .. ceil(B/64)-1
+  if (G < 1 || G > 65535) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dematch, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B, rx_map, blk, rows,
+                     g0);
   return (int)hipGetLastError();
 }
 
@@ -721,11 +723,11 @@ __global__ __launch_bounds__(256) void k_crc_count(const CbInfo* __restrict__ cb
                                                    uint32_t* const* __restrict__ dec, const int* __restrict__ KW,
                                                    int B, const uint32_t* __restrict__ pw, int PW, int n_bits,
                                                    uint32_t* __restrict__ frame_err, uint32_t* __restrict__ frame_crc,
-                                                   uint8_t* __restrict__ cap_bits) {
+                                                   uint8_t* __restrict__ cap_bits, int b0) {
   __shared__ uint32_t T[256];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_table_entry(i, 0x864CFBu);
   __syncthreads();
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = b0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int g = b >> 6, lane = b & 63;
   const uint32_t* tx = pw + (size_t)b * PW;
@@ -779,9 +781,10 @@ __global__ __launch_bounds__(256) void k_crc_count(const CbInfo* __restrict__ cb
 
 int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
                      const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
-                     uint8_t* cap_bits) {
-  hipLaunchKernelGGL(k_crc_count, dim3((B + 255) / 256), dim3(256), 0, s, cbi_dev, C, dec, KW, B, pw, PW, n_bits,
-                     frame_err, frame_crc, cap_bits);
+                     uint8_t* cap_bits, int b0) {
+  if (b0 < 0 || b0 >= B) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_crc_count, dim3((B - b0 + 255) / 256), dim3(256), 0, s, cbi_dev, C, dec, KW, B, pw, PW, n_bits,
+                     frame_err, frame_crc, cap_bits, b0);
   return (int)hipGetLastError();
 }
 

@@ -328,3 +328,23 @@ def test_coded_chain_llrs_vs_oracle(C, oracle, bw, mod):
         ref = oracle.llrs(sy, nv, mod)
         got = r['llr'][b].astype(np.float64)[:len(ref)]
         assert np.max(np.abs(got - ref) / (1 + np.abs(ref))) < 1e-4, (b, snr)
+
+
+@pytest.mark.parametrize('chunks', [2, 3])
+def test_pipelined_chain_matches_unpipelined(C, monkeypatch, chunks):
+    """The coded chain cut into chunks of 64-frame groups (front end of chunk
+    c+1 overlapping the decoder of chunk c on a second stream) gives the same
+    per-frame bit errors and CRC flags as the one-pass chain (ragged chunks:
+    5 groups, last group partial)."""
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp')
+    B = 4 * 64 + 37
+    plan = sim._plan(C.CHAIN_CODED, 0, 27760, max_frames=B)
+    snr = np.tile(np.arange(8.0, 24.0, 2.0), B)[:B]
+    monkeypatch.setenv('LTE_PIPELINE_CHUNKS', '1')
+    a = plan.run(snr, seed=0x5EED, frame_id0=1000)
+    monkeypatch.setenv('LTE_PIPELINE_CHUNKS', str(chunks))
+    b = plan.run(snr, seed=0x5EED, frame_id0=1000)
+    assert np.array_equal(a['frame_errors'], b['frame_errors'])
+    assert np.array_equal(a['crc_ok'], b['crc_ok'])
+    assert np.array_equal(a['counts'], b['counts'])
+    assert 0 < int(np.sum(a['crc_ok'])) < B   # both failing and passing frames at these SNRs

@@ -1247,7 +1247,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   {
     Timer t(p, KN_ACC);
-    LCHK(launch_accumulate(s, B, coded ? 1 : 0, d.n_bits, p->snr_idx.p, p->frame_err.p, p->frame_crc.p, p->counts.p));
+    LCHK(launch_accumulate(s, B, coded ? 1 : 0, d.n_bits, n_snr, p->snr_idx.p, p->frame_err.p, p->frame_crc.p, p->counts.p));
   }
   std::vector<unsigned long long> hc((size_t)4 * n_snr);
   HIPCHK(hipMemcpyAsync(hc.data(), p->counts.p, hc.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1351,7 +1351,7 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   }
   {
     Timer t(p, KN_ACC);
-    LCHK(launch_accumulate(s, B, 0, d.n_bits, p->snr_idx.p, p->frame_err.p, p->frame_crc.p, p->counts.p));
+    LCHK(launch_accumulate(s, B, 0, d.n_bits, n_snr, p->snr_idx.p, p->frame_err.p, p->frame_crc.p, p->counts.p));
   }
   std::vector<unsigned long long> hc((size_t)4 * n_snr);
   HIPCHK(hipMemcpyAsync(hc.data(), p->counts.p, hc.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1689,7 +1689,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   }
   if (do_rx) {
     Timer t(p, KN_ACC);
-    LCHK(launch_accumulate(s, B, coded ? 1 : 0, d.n_bits, p->snr_idx.p, p->frame_err.p, p->frame_crc.p,
+    LCHK(launch_accumulate(s, B, coded ? 1 : 0, d.n_bits, n_snr, p->snr_idx.p, p->frame_err.p, p->frame_crc.p,
                            p->counts.p));
   }
   // results

@@ -77,7 +77,7 @@ int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int
 int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
                      const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
                      uint8_t* cap_bits, int b0 = 0);
-int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, const int32_t* snr_idx,
+int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, int n_snr, const int32_t* snr_idx,
                       const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts);
 int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);
 int launch_dft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);

@@ -647,23 +647,45 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
 }
 
 // ---------------------------------------------------------------------------
-__global__ void k_accumulate(int B, int coded, int n_bits, const int32_t* __restrict__ snr_idx,
-                             const uint32_t* __restrict__ frame_err, const uint32_t* __restrict__ frame_crc,
-                             unsigned long long* __restrict__ counts) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int s = snr_idx[b];
-  const uint32_t e = frame_err[b];
-  const uint32_t blk = coded ? (frame_crc[b] ? 0u : 1u) : (e ? 1u : 0u);
-  atomicAdd(counts + 4 * s + 0, (unsigned long long)e);
-  atomicAdd(counts + 4 * s + 1, (unsigned long long)n_bits);
-  atomicAdd(counts + 4 * s + 2, (unsigned long long)blk);
-  atomicAdd(counts + 4 * s + 3, 1ull);
+// Per-SNR counters {bit errors, bits, block errors, blocks}.  Each block sums
+// its frames (grid-stride) into LDS counters, then adds them to the global
+// counters once: 4 * n_snr global atomics per block instead of 4 per frame
+// (262 144 u64 atomics onto 64 addresses at 65 536 frames).  n_snr too large
+// for LDS (> ACC_LDS_SNR): direct global atomics.
+constexpr int ACC_LDS_SNR = 1024;
+__global__ __launch_bounds__(WG) void k_accumulate(int B, int coded, int n_bits, int n_snr,
+                                                   const int32_t* __restrict__ snr_idx,
+                                                   const uint32_t* __restrict__ frame_err,
+                                                   const uint32_t* __restrict__ frame_crc,
+                                                   unsigned long long* __restrict__ counts) {
+  extern __shared__ unsigned long long acc[];   // [n_snr][4] when n_snr <= ACC_LDS_SNR
+  const bool lds = n_snr <= ACC_LDS_SNR;
+  unsigned long long* dst = lds ? acc : counts;
+  if (lds) {
+    for (int i = threadIdx.x; i < 4 * n_snr; i += WG) acc[i] = 0ull;
+    __syncthreads();
+  }
+  for (int b = blockIdx.x * WG + threadIdx.x; b < B; b += gridDim.x * WG) {
+    const int s = snr_idx[b];
+    const uint32_t e = frame_err[b];
+    const uint32_t blk = coded ? (frame_crc[b] ? 0u : 1u) : (e ? 1u : 0u);
+    atomicAdd(dst + 4 * s + 0, (unsigned long long)e);
+    atomicAdd(dst + 4 * s + 1, (unsigned long long)n_bits);
+    atomicAdd(dst + 4 * s + 2, (unsigned long long)blk);
+    atomicAdd(dst + 4 * s + 3, 1ull);
+  }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * n_snr; i += WG)
+      if (acc[i]) atomicAdd(counts + i, acc[i]);
+  }
 }
 
-int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, const int32_t* snr_idx,
+int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, int n_snr, const int32_t* snr_idx,
                       const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts) {
-  hipLaunchKernelGGL(k_accumulate, dim3((B + WG - 1) / WG), dim3(WG), 0, s, B, coded, n_bits, snr_idx, frame_err,
+  const int blocks = std::min((B + WG - 1) / WG, 512);
+  const size_t shm = n_snr <= ACC_LDS_SNR ? (size_t)4 * n_snr * sizeof(unsigned long long) : 0;
+  hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(WG), shm, s, B, coded, n_bits, n_snr, snr_idx, frame_err,
                      frame_crc, counts);
   return (int)hipGetLastError();
 }

@@ -92,10 +92,20 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     import torch
     dist = None
+    # LTE_BENCH_BACKEND=gloo: rehearse the N>1 path with several ranks sharing
+    # the visible GPUs (device = LOCAL_RANK mod device count); the default is
+    # RCCL ('nccl') with one rank per GPU
+    backend = os.environ.get('LTE_BENCH_BACKEND', 'nccl')
+    if backend == 'gloo':
+        local = local % max(1, torch.cuda.device_count())
+        os.environ['LTE_DEVICE'] = str(local)   # the device lte_phy plans bind to
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 

@@ -9,6 +9,6 @@ timeout -k 10 600 python scripts/bench_configs.py --frames 8192 --steps 3 > gpur
 echo "configs ok"
 timeout -k 10 600 python bench.py > gpurun_out/bench_default.log 2> gpurun_out/bench_default.err || { echo "bench failed rc=$?"; tail -5 gpurun_out/bench_default.err; exit 1; }
 tail -1 gpurun_out/bench_default.log | cut -c1-300
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_bench.log 2>&1 || { echo "rocprof rc=$?"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu > gpurun_out/prof_bench.log 2>&1 || { echo "rocprof rc=$?"; exit 1; }
 echo "rocprof ok"
 cut -d, -f1-4 gpurun_out/prof/run_kernel_stats.csv | head -8

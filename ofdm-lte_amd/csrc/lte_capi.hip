@@ -375,6 +375,7 @@ struct lte_plan {
   // pipelined coded SISO chain: decoder-side stream + one event per chunk (+ join)
   hipStream_t stream2 = nullptr;
   std::vector<hipEvent_t> pipe_ev;
+  DBuf<float2> xh;   // fused TX + channel: per-symbol head / tail TX samples
   std::vector<CbInfo> cbs;
   std::vector<float> gains_f;
   // device
@@ -1082,6 +1083,7 @@ int lte_plan_destroy(lte_plan* p) {
   p->Hm.release(); p->m_pig.release(); p->link_part.release(); p->link_sigma.release(); p->inj_lz.release();
   p->inj_lh.release(); p->m_W.release(); p->bf_cb.release(); p->bf_fr.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
+  p->xh.release();
   for (auto e : p->pipe_ev) (void)hipEventDestroy(e);
   if (p->stream2) (void)hipStreamDestroy(p->stream2);
   if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -1384,6 +1386,54 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   return LTE_OK;
 }
 
+// TX with the static-tap channel fused in (TxChannel): SISO Rayleigh with
+// fD = 0, delays within the CP, no TX / RX stream capture.  LTE_TXCH_FUSE=0
+// selects the separate TX and channel kernels (A/B and parity tests).
+static bool txch_fusable(const lte_plan* p, const lte_run_args* a, bool coded) {
+  const lte_plan_desc& d = p->d;
+  if (d.channel != LTE_CH_RAYLEIGH || d.fD != 0.0 || d.num_rx != 1 || p->mimo || p->bf) return false;
+  if ((d.sc_fdm && !coded) || a->in_signal || a->cap_signal_tx || a->cap_signal_rx) return false;
+  if (const char* e = std::getenv("LTE_TXCH_FUSE"))
+    if (std::atoi(e) == 0) return false;
+  return txch_supported(p->grid, d.n_paths, *std::max_element(d.delays, d.delays + d.n_paths));
+}
+
+// Fading taps, fused TX + channel, first-samples power fix-up and noise power
+// for frames [b0, b0 + Bc) of the plan's buffers.
+static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, size_t b0, int Bc, bool coded,
+                    const float* inj_ph, int64_t inj_ph_stride, float2* cap_tx_syms) {
+  const lte_plan_desc& d = p->d;
+  const int maxd = *std::max_element(d.delays, d.delays + d.n_paths);
+  if (p->xh.alloc((size_t)d.max_frames * p->n_sym * 2 * std::max(maxd, 1))) return fail(LTE_ENOMEM, "tx channel");
+  const size_t fp = b0 * d.n_paths;
+  {
+    Timer t(p, KN_FADING, s);
+    LCHK(launch_fading(s, Bc, 1, d.n_paths, p->gains.p, p->fid.p + b0, a->seed,
+                       inj_ph ? inj_ph + b0 * inj_ph_stride : nullptr, inj_ph_stride, p->phases.p + fp * 16,
+                       p->coef.p + fp));
+  }
+  TxChannel ch{};
+  ch.n_paths = d.n_paths;
+  ch.max_delay = maxd;
+  for (int i = 0; i < d.n_paths; ++i) ch.delays[i] = d.delays[i];
+  ch.coef = p->coef.p + fp;
+  ch.y = p->y.p + b0 * p->L;
+  ch.xh = p->xh.p + b0 * p->n_sym * 2 * maxd;
+  ch.pow_part = p->pow_part.p + b0 * p->n_sym;
+  {
+    Timer t(p, KN_OFDM_TX, s);
+    LCHK(launch_ofdm_tx_ch(s, p->grid, coded ? 1 : 0, p->pw.p + b0 * p->PW, p->PW, p->enc.p + b0 * p->enc_words,
+                           p->enc_words, p->tx_map.p, Bc, cap_tx_syms ? cap_tx_syms + b0 * p->n_sym * p->Nd : nullptr,
+                           ch));
+  }
+  {
+    Timer t(p, KN_CHANNEL, s);
+    LCHK(launch_chan_fix(s, p->grid, Bc, ch));
+    LCHK(launch_npow(s, Bc, 1, ch.pow_part, p->n_sym, p->L, p->snr_lin.p + b0, p->npow.p + b0));
+  }
+  return LTE_OK;
+}
+
 // Chunks of the pipelined coded SISO chain (LTE_PIPELINE_CHUNKS, default 1 =
 // off).  Measured on MI355X at 65536 frames: 2 / 3 / 4 chunks 4 / 7 / 26 %
 // slower than one pass -- the decoder already streams HBM at ~5.5 TB/s, so the
@@ -1428,6 +1478,7 @@ static int run_coded_pipelined(lte_plan* p, const lte_run_args* a, int B, int ch
   const int maxd = ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0;
   const float2* ysrc = ray ? p->y.p : p->x.p;
   const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
+  const bool fuse = txch_fusable(p, a, true);
   for (int c = 0; c < chunks; ++c) {
     const int g0 = (int)((int64_t)G * c / chunks), g1 = (int)((int64_t)G * (c + 1) / chunks);
     const int b0 = g0 * 64, bend = std::min(B, g1 * 64), Bc = bend - b0;
@@ -1442,18 +1493,21 @@ static int run_coded_pipelined(lte_plan* p, const lte_run_args* a, int B, int ch
       LCHK(launch_encode(s, p->pw.p + fr * p->PW, p->PW, p->KWmax, p->enc.p + fr * p->enc_words, p->EW, p->cbi.p,
                          p->C, Bc, p->enc_cw.p));
     }
-    {
-      Timer t(p, KN_OFDM_TX);
-      LCHK(launch_ofdm_tx(s, g, 1, p->pw.p + fr * p->PW, p->PW, p->enc.p + fr * p->enc_words, p->enc_words,
-                          p->tx_map.p, p->x.p + fr * p->L, Bc, nullptr, 0));
-    }
     const size_t fp = fr * rx * d.n_paths;
-    if (ray) {
-      Timer t(p, KN_FADING);
-      LCHK(launch_fading(s, Bc, rx, d.n_paths, p->gains.p, p->fid.p + fr, a->seed, nullptr, 0, p->phases.p + fp * 16,
-                         p->coef.p + fp));
-    }
-    {
+    if (fuse) {
+      const int e = run_txch(p, s, a, fr, Bc, true, nullptr, 0, nullptr);
+      if (e != LTE_OK) return e;
+    } else {
+      {
+        Timer t(p, KN_OFDM_TX);
+        LCHK(launch_ofdm_tx(s, g, 1, p->pw.p + fr * p->PW, p->PW, p->enc.p + fr * p->enc_words, p->enc_words,
+                            p->tx_map.p, p->x.p + fr * p->L, Bc, nullptr, 0));
+      }
+      if (ray) {
+        Timer t(p, KN_FADING);
+        LCHK(launch_fading(s, Bc, rx, d.n_paths, p->gains.p, p->fid.p + fr, a->seed, nullptr, 0,
+                           p->phases.p + fp * 16, p->coef.p + fp));
+      }
       Timer t(p, KN_CHANNEL);
       LCHK(launch_channel(s, g, Bc, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
                           p->phases.p + fp * 16, p->coef.p + fp, p->x.p + fr * p->L, p->y.p + fr * rx * p->L,
@@ -1593,6 +1647,8 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     if (e != LTE_OK) return e;
   }
   const bool seq = chunks <= 1;   // the unpipelined chain
+  // TX + static-tap channel in one kernel (the received stream is written once)
+  const bool fuse = seq && do_tx && do_ch && txch_fusable(p, a, coded);
   if (seq && (do_tx || a->bits)) {
     Timer t(p, KN_PAYLOAD);
     LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
@@ -1608,11 +1664,16 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
       if (p->captx.alloc((size_t)B * p->n_sym * p->Nd)) return fail(LTE_ENOMEM, "capture");
       cts = p->captx.p;
     }
-    Timer t(p, KN_OFDM_TX);
-    // SC-FDM precodes the uncoded SISO / SIMO transmitters only: simulate_siso_coded
-    // builds its own grids without the precoder (core/ofdm_core.py:1062-1099)
-    LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B, cts,
-                        (d.sc_fdm && !coded) ? 1 : 0));
+    if (fuse) {
+      const int e = run_txch(p, s, a, 0, B, coded, inj_ph, inj_ph_stride, cts);
+      if (e != LTE_OK) return e;
+    } else {
+      Timer t(p, KN_OFDM_TX);
+      // SC-FDM precodes the uncoded SISO / SIMO transmitters only: simulate_siso_coded
+      // builds its own grids without the precoder (core/ofdm_core.py:1062-1099)
+      LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B, cts,
+                          (d.sc_fdm && !coded) ? 1 : 0));
+    }
   } else {
     std::vector<float> hx((size_t)B * p->L * 2);
     for (int b = 0; b < B; ++b)
@@ -1630,12 +1691,12 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   }
   const float2* ysrc = ray ? p->y.p : p->x.p;
   const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
-  if (seq && ray) {
+  if (seq && ray && !fuse) {
     Timer t(p, KN_FADING);
     LCHK(launch_fading(s, B, rx, d.n_paths, p->gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, p->phases.p,
                        p->coef.p));
   }
-  if (seq) {
+  if (seq && !fuse) {
     Timer t(p, KN_CHANNEL);
     LCHK(launch_channel(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
                         p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, channel_nblk(p->L),

@@ -47,6 +47,25 @@ int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh
 int launch_npow(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
                 float* npow);
 int channel_nblk(int L);   // power partials per (frame, rx) written by launch_channel
+// OFDM TX with the static-tap multipath channel fused in (SISO, fD = 0, every
+// delay <= CP, N >= 512): k_ofdm_tx<.., CH> writes the received stream outside
+// each symbol's CP (the only samples the receiver reads) and the power of the
+// channel output over the symbol's samples [max_delay, N + cp); k_chan_fix adds
+// the power of the first max_delay samples, which need the previous symbol's
+// tail (kept per symbol in xh).  pow_part then holds n_sym partials per frame.
+constexpr int TXCH_MAXP = 8;
+struct TxChannel {
+  int n_paths, max_delay;
+  int delays[TXCH_MAXP];
+  const float2* coef;   // [B][n_paths]
+  float2* y;            // [B][L]
+  float2* xh;           // [B][n_sym][2 * max_delay]: first / last max_delay TX samples of each symbol
+  float* pow_part;      // [B][n_sym]
+};
+bool txch_supported(const Grid& g, int n_paths, int max_delay);
+int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
+                      int enc_words, const int32_t* tx_map, int B, float2* cap_syms, const TxChannel& ch);
+int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannel& ch);
 int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float2* y, int64_t y_rx_stride,
                     int64_t y_frame_stride, const float* npow, const uint64_t* fid, uint64_t seed,
                     const float* inj_z, int64_t inj_stride, float2* H, float* pstats);

@@ -79,11 +79,61 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 // 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
 // SCF (SC-FDM, uncoded chains): the Nd QAM symbols of the OFDM symbol are
 // DFT-precoded (M = Nd, core/modulator.py:232-236) in a second LDS buffer first.
-template <int CODED, int BPS, bool SCF = false>
+// Fused static-tap channel for one OFDM symbol held in LDS (TxChannel): y[m] =
+// sum_p c_p x[m - d_p] over the CP-extended symbol, whose sample j is
+// buf[j < cp ? N - cp + j : j - cp] (rayleighchannel.py:44-58; for m >=
+// max_delay every delayed tap stays inside the symbol); stores m >= cp only
+// and sums |y|^2 over m >= max_delay per slot in a fixed order.  Called by
+// every thread of the block.
+__device__ __forceinline__ void tx_channel(float2* buf, const Grid& g, const TxChannel& ch, int b, int l, int slot,
+                                           int tid, int T, bool active, float sc) {
+  __shared__ float red[WG / 64];
+  const int N = g.N, cp = g.cp, S = N + cp, D = ch.max_delay;
+  float pw = 0.f;
+  if (active) {
+    if (D > 0) {   // the TX samples x = buf / sqrt(N) at both ends of the symbol
+      float2* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
+      for (int i = tid; i < 2 * D; i += T) {
+        const int j = i < D ? i : S - 2 * D + i;
+        xh[i] = cscale(buf[(j - cp) & (N - 1)], sc);
+      }
+    }
+    // 1/sqrt(N) folded into the taps; sample j of the CP-extended symbol is
+    // buf[(j - cp) mod N] (N a power of 2)
+    float2 cf[TXCH_MAXP];
+    int off[TXCH_MAXP];
+#pragma unroll
+    for (int p = 0; p < TXCH_MAXP; ++p) {
+      cf[p] = p < ch.n_paths ? cscale(ch.coef[(size_t)b * ch.n_paths + p], sc) : make_float2(0.f, 0.f);
+      off[p] = ch.delays[p] + cp;
+    }
+    float2* yo = ch.y + (size_t)b * g.L + (size_t)l * S;
+    for (int m = D + tid; m < S; m += T) {
+      float2 v = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int p = 0; p < TXCH_MAXP; ++p)
+        if (p < ch.n_paths) v = cadd(v, cmul(cf[p], buf[(m - off[p]) & (N - 1)]));
+      if (m >= cp) yo[m] = v;
+      pw += v.x * v.x + v.y * v.y;
+    }
+  }
+  // per-slot sum in a fixed order: T >= 64 threads = T / 64 whole waves per slot
+  for (int o = 32; o > 0; o >>= 1) pw += __shfl_xor(pw, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pw;
+  __syncthreads();
+  if (active && tid == 0) {
+    const int wps = T >> 6;
+    float t = 0.f;
+    for (int w = 0; w < wps; ++w) t += red[slot * wps + w];
+    ch.pow_part[(size_t)b * g.n_sym + l] = t;
+  }
+}
+
+template <int CODED, int BPS, bool SCF = false, bool CH = false>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
                                                 const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B,
-                                                float2* __restrict__ cap_syms, int stage_enc) {
+                                                float2* __restrict__ cap_syms, int stage_enc, TxChannel ch) {
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
@@ -164,7 +214,9 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   }
   __syncthreads();
   fft_lds<true>(buf, N, g.log2N, g.tw, tid, active);
-  if (active) {
+  if constexpr (CH) {
+    tx_channel(buf, g, ch, b, l, slot, tid, T, active, rsqrtf((float)N));
+  } else if (active) {
     const float sc = rsqrtf((float)N);
     float2* xo = x + (size_t)b * g.L + (size_t)l * (N + g.cp);
     for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
@@ -184,7 +236,7 @@ int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, 
   const size_t shm = (sc_fdm ? 2 : 1) * spw * g.N * sizeof(float2) + (stage_enc ? enc_shm : 0);
 #define LTE_TX(C_, B_, S_)                                                                                         \
   hipLaunchKernelGGL((k_ofdm_tx<C_, B_, S_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words, tx_map, x, \
-                     B, cap_syms, stage_enc)
+                     B, cap_syms, stage_enc, TxChannel{})
   if (coded) {
     if (g.bps == 2) LTE_TX(1, 2, false); else if (g.bps == 4) LTE_TX(1, 4, false); else LTE_TX(1, 6, false);
   } else if (sc_fdm) {
@@ -193,6 +245,71 @@ int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, 
     if (g.bps == 2) LTE_TX(0, 2, false); else if (g.bps == 4) LTE_TX(0, 4, false); else LTE_TX(0, 6, false);
   }
 #undef LTE_TX
+  return (int)hipGetLastError();
+}
+
+bool txch_supported(const Grid& g, int n_paths, int max_delay) {
+  return g.N >= 512 && n_paths >= 1 && n_paths <= TXCH_MAXP && max_delay >= 0 && max_delay <= g.cp &&
+         2 * max_delay < g.N + g.cp;
+}
+
+int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
+                      int enc_words, const int32_t* tx_map, int B, float2* cap_syms, const TxChannel& ch) {
+  const int spw = WG / (g.N >> 3);
+  const int64_t total = (int64_t)B * g.n_sym;
+  if (!txch_supported(g, ch.n_paths, ch.max_delay) || total > 0x7FFFFFFF - spw ||
+      (g.bps != 2 && g.bps != 4 && g.bps != 6))
+    return (int)hipErrorInvalidValue;
+  const int blocks = (int)((total + spw - 1) / spw);
+  const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
+  const int stage_enc = coded && enc_shm <= 32768;
+  const size_t shm = (size_t)spw * g.N * sizeof(float2) + (stage_enc ? enc_shm : 0);
+#define LTE_TXC(C_, B_)                                                                                         \
+  hipLaunchKernelGGL((k_ofdm_tx<C_, B_, false, true>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words, \
+                     tx_map, (float2*)nullptr, B, cap_syms, stage_enc, ch)
+  if (coded) {
+    if (g.bps == 2) LTE_TXC(1, 2); else if (g.bps == 4) LTE_TXC(1, 4); else LTE_TXC(1, 6);
+  } else {
+    if (g.bps == 2) LTE_TXC(0, 2); else if (g.bps == 4) LTE_TXC(0, 4); else LTE_TXC(0, 6);
+  }
+#undef LTE_TXC
+  return (int)hipGetLastError();
+}
+
+// Power of each symbol's first max_delay channel-output samples (their delayed
+// taps reach into the previous symbol's tail, or the zero prefix of symbol 0),
+// added to the symbol's partial.  16 lanes per (frame, symbol), one sample
+// each (coalesced head / tail reads), summed by a fixed xor butterfly.
+constexpr int CHF_LANES = 16;
+__global__ __launch_bounds__(WG) void k_chan_fix(Grid g, int B, TxChannel ch) {
+  const int64_t i = ((int64_t)blockIdx.x * WG + threadIdx.x) / CHF_LANES;
+  const int lane = threadIdx.x % CHF_LANES;
+  const bool ok = i < (int64_t)B * g.n_sym;
+  float pw = 0.f;
+  if (ok) {
+    const int l = (int)(i % g.n_sym), b = (int)(i / g.n_sym);
+    const int D = ch.max_delay;
+    const float2* hd = ch.xh + (size_t)i * 2 * D;   // this symbol's head; hd[-D..-1] = previous symbol's tail
+    const float2* cb = ch.coef + (size_t)b * ch.n_paths;
+    for (int m = lane; m < D; m += CHF_LANES) {
+      float2 v = make_float2(0.f, 0.f);
+      for (int p = 0; p < ch.n_paths; ++p) {
+        const int j = m - ch.delays[p];
+        const float2 xv = (j >= 0 || l > 0) ? hd[j] : make_float2(0.f, 0.f);
+        v = cadd(v, cmul(cb[p], xv));
+      }
+      pw += v.x * v.x + v.y * v.y;
+    }
+  }
+#pragma unroll
+  for (int o = CHF_LANES / 2; o > 0; o >>= 1) pw += __shfl_xor(pw, o);
+  if (ok && lane == 0) ch.pow_part[i] += pw;
+}
+
+int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannel& ch) {
+  const int64_t n = (int64_t)B * g.n_sym * CHF_LANES;
+  if (ch.max_delay == 0 || n == 0) return 0;
+  hipLaunchKernelGGL(k_chan_fix, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, g, B, ch);
   return (int)hipGetLastError();
 }
 

@@ -348,3 +348,33 @@ def test_pipelined_chain_matches_unpipelined(C, monkeypatch, chunks):
     assert np.array_equal(a['crc_ok'], b['crc_ok'])
     assert np.array_equal(a['counts'], b['counts'])
     assert 0 < int(np.sum(a['crc_ok'])) < B   # both failing and passing frames at these SNRs
+
+
+@pytest.mark.parametrize('chain', ['coded', 'uncoded'])
+def test_fused_tx_channel_matches_separate_kernels(C, monkeypatch, chain):
+    """TX with the static-tap channel fused in (k_ofdm_tx<.., CH> + k_chan_fix)
+    vs the separate TX and channel kernels, on the same Philox frames: noise
+    power (the measured-power SNR, Q5), channel estimates and LLRs agree to
+    float32 round-off (the power is summed per symbol instead of per 2048-sample
+    block); decisions agree up to that round-off."""
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp')
+    B = 3 * 64 + 5
+    coded = chain == 'coded'
+    plan = sim._plan(C.CHAIN_CODED, 0, 27760, max_frames=B) if coded else \
+        sim._plan(C.CHAIN_UNCODED, 14, 14 * sim.Nd * 6, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('noise_power', 'H') + (('llr',) if coded else ())
+    monkeypatch.setenv('LTE_TXCH_FUSE', '0')
+    a = plan.run(snr, seed=0x5EED, frame_id0=77, capture=cap)
+    monkeypatch.setenv('LTE_TXCH_FUSE', '1')
+    b = plan.run(snr, seed=0x5EED, frame_id0=77, capture=cap)
+    assert np.max(np.abs(b['noise_power'] / a['noise_power'] - 1)) < 2e-6
+    assert np.max(np.abs(b['H'] - a['H'])) < 1e-4 * np.max(np.abs(a['H']))
+    if coded:
+        # LLR = d^2 difference / (2 sigma^2_eff): at 30 dB a 1e-7 change of the
+        # received sample moves it by ~1e-4 (measured 2e-4 at most)
+        assert np.max(np.abs(b['llr'] - a['llr']) / (1 + np.abs(a['llr']))) < 1e-3
+        assert int(np.sum(a['crc_ok'] != b['crc_ok'])) <= 1
+    ea, eb = int(a['counts'][:, 0].sum()), int(b['counts'][:, 0].sum())
+    assert abs(ea - eb) <= 1e-3 * ea + 5, (ea, eb)
+    assert np.array_equal(a['counts'][:, 1], b['counts'][:, 1])

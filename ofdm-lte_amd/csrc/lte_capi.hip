@@ -1434,6 +1434,26 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, size_t b0
   return LTE_OK;
 }
 
+// Coded SISO 16/64-QAM without an LLR capture: k_rx_data hands over the
+// equalised symbol and sigma^2_eff per RE (12 B) and k_dematch_zn demaps while
+// it builds the decoder rows, instead of a round trip of 4 * bps B of LLRs per
+// RE.  The (z, nv) arrays live in the LLR buffer ([max_frames][n_re] each; it
+// holds bps >= 4 floats per RE).  LTE_DEMAP_IN_DEMATCH=0 keeps the LLR path.
+static bool demap_in_dematch(const lte_plan* p, const lte_run_args* a) {
+  const lte_plan_desc& d = p->d;
+  if (d.chain != LTE_CHAIN_CODED || p->mimo || p->bf || (d.bps != 4 && d.bps != 6) || a->cap_llr) return false;
+  if (const char* e = std::getenv("LTE_DEMAP_IN_DEMATCH"))
+    if (std::atoi(e) == 0) return false;
+  return true;
+}
+static float2* zn_z(lte_plan* p, size_t b0) {
+  return reinterpret_cast<float2*>(p->llr.p) + b0 * (p->n_re_bits / p->d.bps);
+}
+static float* zn_nv(lte_plan* p, size_t b0) {
+  const size_t n_re = p->n_re_bits / p->d.bps;
+  return p->llr.p + 2 * (size_t)p->d.max_frames * n_re + b0 * n_re;
+}
+
 // Chunks of the pipelined coded SISO chain (LTE_PIPELINE_CHUNKS, default 1 =
 // off).  Measured on MI355X at 65536 frames: 2 / 3 / 4 chunks 4 / 7 / 26 %
 // slower than one pass -- the decoder already streams HBM at ~5.5 TB/s, so the
@@ -1479,6 +1499,7 @@ static int run_coded_pipelined(lte_plan* p, const lte_run_args* a, int B, int ch
   const float2* ysrc = ray ? p->y.p : p->x.p;
   const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
   const bool fuse = txch_fusable(p, a, true);
+  const bool zn = demap_in_dematch(p, a);
   for (int c = 0; c < chunks; ++c) {
     const int g0 = (int)((int64_t)G * c / chunks), g1 = (int)((int64_t)G * (c + 1) / chunks);
     const int b0 = g0 * 64, bend = std::min(B, g1 * 64), Bc = bend - b0;
@@ -1525,12 +1546,17 @@ static int run_coded_pipelined(lte_plan* p, const lte_run_args* a, int B, int ch
       Timer t(p, KN_RX_DATA);
       LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, Bc, rx, ysrc + fr * yfs, yrs, yfs, p->H.p + fh * d.N,
                           p->npow.p + fr * rx, p->snr_lin.p + fr, p->fid.p + fr, a->seed, nullptr, 0,
-                          p->pw.p + fr * p->PW, p->PW, d.n_bits, p->frame_err.p + fr, p->llr.p + fr * p->n_re_bits,
-                          nullptr, nullptr, 0));
+                          p->pw.p + fr * p->PW, p->PW, d.n_bits, p->frame_err.p + fr,
+                          zn ? reinterpret_cast<float*>(zn_z(p, fr)) : p->llr.p + fr * p->n_re_bits, nullptr,
+                          nullptr, 0, zn ? zn_nv(p, fr) : nullptr));
     }
     {
       Timer t(p, KN_DEMATCH);
-      LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, bend, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C, g0));
+      if (zn)
+        LCHK(launch_dematch_zn(s, zn_z(p, 0), zn_nv(p, 0), p->n_re_bits / d.bps, d.bps, bend, p->rx_map.p,
+                               p->blk_ptrs.p, p->rows_dev.p, g0));
+      else
+        LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, bend, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C, g0));
     }
     // decoder side of this chunk on stream2, after its front end
     HIPCHK(hipEventRecord(p->pipe_ev[c], s));
@@ -1718,19 +1744,25 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
     cap_bits_dev = p->cap_bits.p;
   }
+  const bool zn = seq && demap_in_dematch(p, a);
   if (seq && do_rx) {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, p->H.p, p->npow.p, p->snr_lin.p,
-                        p->fid.p, a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p, p->llr.p,
-                        cap_syms_dev, coded ? nullptr : cap_bits_dev,
+                        p->fid.p, a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+                        zn ? reinterpret_cast<float*>(zn_z(p, 0)) : p->llr.p, cap_syms_dev,
+                        coded ? nullptr : cap_bits_dev,
                         // the IDFT runs in receive_and_decode only (core/lte_receiver.py:318-333): the SIMO
                         // MRC receiver (core/ofdm_core.py:1340-1534) never de-precodes
-                        (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0));
+                        (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0, zn ? zn_nv(p, 0) : nullptr));
   }
   if (seq && coded && do_rx) {
     {
       Timer t(p, KN_DEMATCH);
-      LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
+      if (zn)
+        LCHK(launch_dematch_zn(s, zn_z(p, 0), zn_nv(p, 0), p->n_re_bits / d.bps, d.bps, B, p->rx_map.p,
+                               p->blk_ptrs.p, p->rows_dev.p));
+      else
+        LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
     }
     const int G = (B + 63) / 64;
     std::vector<TurboJob> jobs(p->C);

@@ -73,11 +73,17 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                    const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                    const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                    const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
-                   uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, int sc_fdm = 0);
+                   uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, int sc_fdm = 0,
+                   float* nv_out = nullptr);   // coded: nv_out set -> llr takes z (float2 per RE), nv_out sigma^2_eff
 // g0 / b0: first 64-frame group / first frame of a frame range [.., B) of the
 // plan's buffers (the pipelined chain runs the decoder side per chunk)
 int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
                    const int64_t* rows, int C, int g0 = 0);
+// dematch with the soft demapper fused in: reads the equalised symbols z and
+// their noise variances ([B][n_re] each, from k_rx_data's nv_out mode) instead
+// of LLRs; same decoder rows as launch_dematch (bps 4 / 6)
+int launch_dematch_zn(hipStream_t s, const float2* z, const float* nv, int n_re, int bps, int B,
+                      const int32_t* rx_map, float* const* blk, const int64_t* rows, int g0 = 0);
 int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
                  int G, int mode);
 struct TurboJob {           // one CB slot of a batch: G groups of 64 code blocks of size K

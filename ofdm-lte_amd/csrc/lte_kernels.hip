@@ -598,7 +598,8 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
                                                 const float* __restrict__ inj_z, int64_t inj_stride,
                                                 const uint32_t* __restrict__ pw, int PW, int n_bits,
                                                 uint32_t* __restrict__ frame_err, float* __restrict__ llr,
-                                                float2* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+                                                float2* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits,
+                                                float* __restrict__ nvo) {
   extern __shared__ float2 sm[];
   const int N = g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
@@ -681,6 +682,11 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
       const float s2 = 1.0f / snr_lin[b];
       float nv = s2;
       if (rayleigh) nv = fmaxf(s2 / fminf(fmaxf(den[q], 1e-6f), 1e6f), s2 * 0.25f);
+      if (nvo) {   // demap in k_dematch_zn: hand over the equalised symbol and its noise variance
+        reinterpret_cast<float2*>(llr)[fre + re] = z;
+        nvo[fre + re] = nv;
+        continue;
+      }
       float o[BPS];
       soft_demap<BPS>(z, nv, o);
       float* lo = llr + (fre + re) * BPS;
@@ -713,10 +719,10 @@ static void rx_data_inst(hipStream_t s, int blocks, size_t shm, const Grid& g, i
                          const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                          const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                          const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
-                         uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits) {
+                         uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, float* nvo) {
   hipLaunchKernelGGL((k_rx_data<CHAIN, BPS, SCF>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, num_rx, y,
                      y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits,
-                     frame_err, llr, cap_syms, cap_bits);
+                     frame_err, llr, cap_syms, cap_bits, nvo);
 }
 
 template <int CHAIN, bool SCF = false>
@@ -724,19 +730,20 @@ static void rx_data_bps(int bps, hipStream_t s, int blocks, size_t shm, const Gr
                         int num_rx, const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                         const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                         const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
-                        uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits) {
+                        uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, float* nvo) {
   auto* f = bps == 2 ? &rx_data_inst<CHAIN, 2, SCF>
                      : (bps == 4 ? &rx_data_inst<CHAIN, 4, SCF> : &rx_data_inst<CHAIN, 6, SCF>);
   f(s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z,
-    inj_stride, pw, PW, n_bits, frame_err, llr, cap_syms, cap_bits);
+    inj_stride, pw, PW, n_bits, frame_err, llr, cap_syms, cap_bits, nvo);
 }
 
 int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, int num_rx, const float2* y,
                    int64_t y_rx_stride, int64_t y_frame_stride, const float2* H, const float* npow,
                    const float* snr_lin, const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride,
                    const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, float* llr, float2* cap_syms,
-                   uint8_t* cap_bits, int sc_fdm) {
+                   uint8_t* cap_bits, int sc_fdm, float* nv_out) {
   if (g.bps != 2 && g.bps != 4 && g.bps != 6) return (int)hipErrorInvalidValue;
+  if (nv_out && chain != LTE_CHAIN_CODED) return (int)hipErrorInvalidValue;
   if (sc_fdm && (chain != LTE_CHAIN_UNCODED || !g.chirp || !g.bhat)) return (int)hipErrorInvalidValue;
   if (chain == LTE_CHAIN_SIMO && num_rx > 8) return (int)hipErrorInvalidValue;
   const int spw = WG / (g.N >> 3);
@@ -747,19 +754,19 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
   if (chain == LTE_CHAIN_CODED)
     rx_data_bps<LTE_CHAIN_CODED>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H,
                                  npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
-                                 cap_syms, cap_bits);
+                                 cap_syms, cap_bits, nv_out);
   else if (chain == LTE_CHAIN_SIMO)
     rx_data_bps<LTE_CHAIN_SIMO>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H,
                                 npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
-                                cap_syms, cap_bits);
+                                cap_syms, cap_bits, nullptr);
   else if (sc_fdm)
     rx_data_bps<LTE_CHAIN_UNCODED, true>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride,
                                          y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW,
-                                         n_bits, frame_err, llr, cap_syms, cap_bits);
+                                         n_bits, frame_err, llr, cap_syms, cap_bits, nullptr);
   else
     rx_data_bps<LTE_CHAIN_UNCODED>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride,
                                    H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
-                                   cap_syms, cap_bits);
+                                   cap_syms, cap_bits, nullptr);
   return (int)hipGetLastError();
 }
 

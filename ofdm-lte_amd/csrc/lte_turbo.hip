@@ -18,6 +18,7 @@
 //    rounding).
 #include "lte_common.h"
 #include "lte_internal.h"
+#include "lte_dev.h"
 
 namespace lte {
 
@@ -498,6 +499,62 @@ int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t*
   if (G < 1 || G > 65535) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_dematch, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B, rx_map, blk, rows,
                      g0);
+  return (int)hipGetLastError();
+}
+
+// Soft demap + dematch in one pass: a block covers DZ_RE resource elements of
+// 64 frames; it reads their equalised symbols and noise variances (12 B per RE
+// instead of 4 * bps B of LLRs), computes the max-log LLRs (soft_demap, the
+// function k_rx_data uses) into an LDS tile [frame][LLR], then writes whole
+// 256-B decoder rows exactly as k_dematch.
+constexpr int DZ_RE = 16;
+template <int BPS>
+__global__ __launch_bounds__(256) void k_dematch_zn(const float2* __restrict__ z, const float* __restrict__ nv,
+                                                    int n_re, int B, const int32_t* __restrict__ rx_map,
+                                                    float* const* __restrict__ blk,
+                                                    const int64_t* __restrict__ rows, int g0) {
+  constexpr int TC = DZ_RE * BPS, PER = 64 * DZ_RE / 256;
+  __shared__ float tile[64][TC + 1];
+  const int g = g0 + blockIdx.y;
+  const int re0 = blockIdx.x * DZ_RE;
+  const int nr = min(DZ_RE, n_re - re0);
+  // every (z, nv) load of this thread issued before the demapping
+  float2 zv[PER];
+  float nvv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = threadIdx.x + k * 256, f = e / DZ_RE, r = e % DZ_RE, b = g * 64 + f;
+    const bool ok = b < B && r < nr;
+    const size_t i = (size_t)b * n_re + re0 + r;
+    zv[k] = ok ? z[i] : make_float2(0.f, 0.f);
+    nvv[k] = ok ? nv[i] : 1.f;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = threadIdx.x + k * 256, f = e / DZ_RE, r = e % DZ_RE;
+    float o[BPS];
+    soft_demap<BPS>(zv[k], nvv[k], o);
+#pragma unroll
+    for (int m = 0; m < BPS; ++m) tile[f][r * BPS + m] = o[m];
+  }
+  __syncthreads();
+  const int t0 = re0 * BPS, nt = nr * BPS;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), f = threadIdx.x & 63;
+  for (int c = wv; c < nt; c += 4) {
+    const int m = rx_map[t0 + c];
+    if (m < 0) continue;
+    const int r = m >> 24, row = m & 0xFFFFFF;
+    blk[r][((size_t)g * rows[r] + row) * RS + f] = 0.5f * tile[f][c];   // rows hold LLR/2 (exact)
+  }
+}
+
+int launch_dematch_zn(hipStream_t s, const float2* z, const float* nv, int n_re, int bps, int B,
+                      const int32_t* rx_map, float* const* blk, const int64_t* rows, int g0) {
+  const int G = (B + 63) / 64 - g0;
+  if (G < 1 || G > 65535 || (bps != 4 && bps != 6)) return (int)hipErrorInvalidValue;
+  const dim3 grid((n_re + DZ_RE - 1) / DZ_RE, G);
+  if (bps == 4) hipLaunchKernelGGL(k_dematch_zn<4>, grid, dim3(256), 0, s, z, nv, n_re, B, rx_map, blk, rows, g0);
+  else hipLaunchKernelGGL(k_dematch_zn<6>, grid, dim3(256), 0, s, z, nv, n_re, B, rx_map, blk, rows, g0);
   return (int)hipGetLastError();
 }
 

@@ -378,3 +378,22 @@ def test_fused_tx_channel_matches_separate_kernels(C, monkeypatch, chain):
     ea, eb = int(a['counts'][:, 0].sum()), int(b['counts'][:, 0].sum())
     assert abs(ea - eb) <= 1e-3 * ea + 5, (ea, eb)
     assert np.array_equal(a['counts'][:, 1], b['counts'][:, 1])
+
+
+@pytest.mark.parametrize('mod', ['16-QAM', '64-QAM'])
+def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod):
+    """k_rx_data handing (z, sigma^2_eff) per RE to k_dematch_zn, which runs the
+    same max-log demapper while it builds the decoder rows, decodes exactly
+    like the LLR round trip (k_rx_data LLRs -> k_dematch): identical per-frame
+    bit errors and CRC flags on the same Philox frames."""
+    sim = _sim(20.0, mod, 'rayleigh_mp')
+    B = 2 * 64 + 9
+    plan = sim._plan(C.CHAIN_CODED, 0, 27760 if mod == '64-QAM' else 18000, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    monkeypatch.setenv('LTE_DEMAP_IN_DEMATCH', '0')
+    a = plan.run(snr, seed=0x5EED, frame_id0=5)
+    monkeypatch.setenv('LTE_DEMAP_IN_DEMATCH', '1')
+    b = plan.run(snr, seed=0x5EED, frame_id0=5)
+    assert np.array_equal(a['frame_errors'], b['frame_errors'])
+    assert np.array_equal(a['crc_ok'], b['crc_ok'])
+    assert 0 < int(np.sum(a['crc_ok'])) < B

@@ -631,6 +631,8 @@ __device__ __forceinline__ uint32_t rsc_tail(uint32_t& s0, uint32_t& s1, uint32_
 //             K = 6144, [word][lane]) and gathers from there -- pi(i) is
 //             wave-uniform, so each gather is one conflict-free LDS read.
 constexpr int ENC_WG = 256;
+constexpr int ENC_CH = 16;   // output words per bunched store (k_encode)
+constexpr int ENC2_CH = 8;   // (k_encode2)
 __global__ __launch_bounds__(ENC_WG) void k_encode(const uint32_t* __restrict__ pw, int PW, int KWmax,
                                                    uint32_t* __restrict__ enc, int EW,
                                                    const CbInfo* __restrict__ cbi, int C, int B,
@@ -646,8 +648,8 @@ __global__ __launch_bounds__(ENC_WG) void k_encode(const uint32_t* __restrict__ 
   const uint32_t* tb = pw + (size_t)b * PW;
   uint32_t* cw = cw_scratch + (size_t)(gid >> 6) * KWmax * 64 + (gid & 63);   // word w at cw[w * 64]
   uint32_t* e = enc + ((size_t)b * C + r) * 3 * EW;
-  BitWriter w0{e, 0, 0}, w1{e + EW, 0, 0};
   const int Kd = ci.crc ? K - 24 : K;   // every LTE K (and so Kd) is a multiple of 8
+  const int KWf = K >> 5;               // whole 32-bit words of the code block
   uint32_t crc = 0, s0 = 0, s1 = 0, s2 = 0;
   // CB bit p in [F, Kd) is TB bit (off - F + p): the 32 bits of word w are a
   // fixed-offset window over TB words i00 + w, i00 + w + 1
@@ -656,33 +658,63 @@ __global__ __launch_bounds__(ENC_WG) void k_encode(const uint32_t* __restrict__ 
   const int o = (int)(base & 31);
   auto ldw = [&](int64_t i) -> uint32_t { return (i >= 0 && i < PW) ? tb[i] : 0u; };
   uint32_t wa = ldw(i00), wb = ldw(i00 + 1);
-  for (int w = 0; w * 32 < K; ++w) {
-    const uint32_t wn = ldw(i00 + w + 2);   // next window word, in flight during this one
-    const int p0 = w * 32, nb = min(32, K - p0);
-    uint32_t t = o ? ((wa << o) | (wb >> (32 - o))) : wa;
-    if (p0 < F) t &= (F - p0 >= 32) ? 0u : (0xFFFFFFFFu >> (F - p0));   // filler bits are 0
-    uint32_t u = 0;
+  // Whole output words are kept in registers and stored ENC_CH at a time: each
+  // lane then completes its 64-B line pieces back to back instead of one word
+  // per loop trip (lanes are 64 different frames, so a store instruction
+  // touches 64 lines; spread over the loop, L2 evicted them half-written).
+  uint32_t pf = 0, pq = 0;              // the last, partial word (K % 32 bits), if any
+  int pnb = 0;
+  for (int wc = 0; wc * 32 < K; wc += ENC_CH) {
+    uint32_t fb[ENC_CH], qb[ENC_CH];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int p = p0 + 8 * k;
-      if (8 * k < nb) {
-        uint32_t byte;
-        if (p < Kd) {
-          byte = (t >> (24 - 8 * k)) & 0xFFu;
-          if (ci.crc) crc = ((crc << 8) & 0xFFFFFFu) ^ crc_t[((crc >> 16) ^ byte) & 0xFFu];
-        } else {
-          byte = (crc >> (16 - (p - Kd))) & 0xFFu;   // CRC-24B bits after the data
+    for (int i = 0; i < ENC_CH; ++i) {
+      const int w = wc + i;
+      fb[i] = qb[i] = 0u;
+      if (w * 32 >= K) break;
+      const uint32_t wn = ldw(i00 + w + 2);   // next window word, in flight during this one
+      const int p0 = w * 32, nb = min(32, K - p0);
+      uint32_t t = o ? ((wa << o) | (wb >> (32 - o))) : wa;
+      if (p0 < F) t &= (F - p0 >= 32) ? 0u : (0xFFFFFFFFu >> (F - p0));   // filler bits are 0
+      uint32_t u = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = p0 + 8 * k;
+        if (8 * k < nb) {
+          uint32_t byte;
+          if (p < Kd) {
+            byte = (t >> (24 - 8 * k)) & 0xFFu;
+            if (ci.crc) crc = ((crc << 8) & 0xFFFFFFu) ^ crc_t[((crc >> 16) ^ byte) & 0xFFu];
+          } else {
+            byte = (crc >> (16 - (p - Kd))) & 0xFFu;   // CRC-24B bits after the data
+          }
+          u |= byte << (24 - 8 * k);
         }
-        u |= byte << (24 - 8 * k);
       }
+      cw[w * 64] = u;                      // left-aligned
+      uint32_t f;
+      const uint32_t q = rsc_word(u, nb, s0, s1, s2, &f);
+      if (nb == 32) {
+        fb[i] = f;
+        qb[i] = q;
+      } else {
+        pf = f;
+        pq = q;
+        pnb = nb;
+      }
+      wa = wb;
+      wb = wn;
     }
-    cw[w * 64] = u;                      // left-aligned
-    uint32_t f;
-    const uint32_t q = rsc_word(u, nb, s0, s1, s2, &f);
-    w0.put(f >> (32 - nb), nb);
-    w1.put(q >> (32 - nb), nb);
-    wa = wb;
-    wb = wn;
+#pragma unroll
+    for (int i = 0; i < ENC_CH; ++i)
+      if (wc + i < KWf) e[wc + i] = fb[i];
+#pragma unroll
+    for (int i = 0; i < ENC_CH; ++i)
+      if (wc + i < KWf) e[EW + wc + i] = qb[i];
+  }
+  BitWriter w0{e + KWf, 0, 0}, w1{e + EW + KWf, 0, 0};
+  if (pnb) {
+    w0.put(pf >> (32 - pnb), pnb);
+    w1.put(pq >> (32 - pnb), pnb);
   }
   for (int t = 0; t < 3; ++t) {  // trellis termination, encoder 1
     const uint32_t v = rsc_tail(s0, s1, s2);
@@ -706,34 +738,54 @@ __global__ __launch_bounds__(64) void k_encode2(int KWmax, uint32_t* __restrict_
   const uint32_t* cw = cw_scratch + (size_t)blockIdx.x * KWmax * 64 + lane;
   for (int w = 0; w < KW; ++w) cwl[w * 64 + lane] = cw[w * 64];
   uint32_t* e = enc + ((size_t)b * C + r) * 3 * EW;
-  BitWriter w2{e + 2 * EW, 0, 0};
+  const int KWf = K >> 5;
   uint32_t s0 = 0, s1 = 0, s2 = 0;
   int pi = 0, d = (ci.f1 + ci.f2) % K;
   const int tf2 = (2 * ci.f2) % K;
-  for (int w = 0; w < KW; ++w) {
-    const int nb = min(32, K - w * 32);
-    uint32_t u = 0;
+  uint32_t pq = 0;                      // the last, partial parity word (K % 32 bits), if any
+  int pnb = 0;
+  for (int wc = 0; wc < KW; wc += ENC2_CH) {   // whole words stored ENC2_CH at a time (see k_encode)
+    uint32_t qb[ENC2_CH];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {        // 16 gathers in flight together
-      uint32_t v[16];
-      int sh[16];
+    for (int j = 0; j < ENC2_CH; ++j) {
+      const int w = wc + j;
+      qb[j] = 0u;
+      if (w >= KW) break;
+      const int nb = min(32, K - w * 32);
+      uint32_t u = 0;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        v[i] = cwl[(pi >> 5) * 64 + lane];
-        sh[i] = pi & 31;
-        int pn = pi + d, dn = d + tf2;
-        pn -= pn >= K ? K : 0;
-        dn -= dn >= K ? K : 0;
-        const bool adv = 16 * h + i < nb;
-        pi = adv ? pn : pi;
-        d = adv ? dn : d;
+      for (int h = 0; h < 2; ++h) {        // 16 gathers in flight together
+        uint32_t v[16];
+        int sh[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          v[i] = cwl[(pi >> 5) * 64 + lane];
+          sh[i] = pi & 31;
+          int pn = pi + d, dn = d + tf2;
+          pn -= pn >= K ? K : 0;
+          dn -= dn >= K ? K : 0;
+          const bool adv = 16 * h + i < nb;
+          pi = adv ? pn : pi;
+          d = adv ? dn : d;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) u |= ((v[i] << sh[i]) >> 31) << (31 - 16 * h - i);
       }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) u |= ((v[i] << sh[i]) >> 31) << (31 - 16 * h - i);
+      uint32_t f;
+      const uint32_t q = rsc_word(u, nb, s0, s1, s2, &f);
+      if (nb == 32) {
+        qb[j] = q;
+      } else {
+        pq = q;
+        pnb = nb;
+      }
     }
-    uint32_t f;
-    w2.put(rsc_word(u, nb, s0, s1, s2, &f) >> (32 - nb), nb);
+#pragma unroll
+    for (int j = 0; j < ENC2_CH; ++j)
+      if (wc + j < KWf) e[2 * EW + wc + j] = qb[j];
   }
+  BitWriter w2{e + 2 * EW + KWf, 0, 0};
+  if (pnb) w2.put(pq >> (32 - pnb), pnb);
   for (int t = 0; t < 3; ++t) {
     const uint32_t v = rsc_tail(s0, s1, s2);
     const int pos = K + 3 + t;   // sys2 tail -> d0[K+3..K+5]

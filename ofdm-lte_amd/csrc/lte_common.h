@@ -128,41 +128,82 @@ __device__ __forceinline__ void dft8_inplace(float2 (&v)[8]) {
   v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
 }
 
-template <bool INV>
-__device__ __forceinline__ void fft_lds(float2* buf, int N, int log2N, const float2* __restrict__ tw,
+// NC > 0: a kernel instance for one transform size (NC = N): pass count,
+// strides, swizzle predicates and twiddle strides fold and the passes unroll
+// (ofdm_tx / rx_data / rx_chest at N = 2048: -2..-15 % time).  NC = 0: runtime N.
+template <bool INV, int NC = 0>
+__device__ __forceinline__ void fft_lds(float2* buf, int N_, int log2N_, const float2* __restrict__ tw,
                                         int tid, bool active) {
+  const int N = NC ? NC : N_;
+  const int log2N = NC ? __builtin_ctz(NC) : log2N_;
   const int T = N >> 3;
   const int n8 = log2N / 3, rem = log2N - 3 * n8;
   int Ns = 1, lNs = 0;   // Ns = 8^s
-  for (int s = 0; s < n8; ++s) {
-    const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
-    float2 v[8];
-    const int j = tid;
-    if (active) {
+  // the same radix-8 passes twice: unrolled for a compile-time N; as a plain
+  // loop otherwise (any other form changes the runtime-N kernels' registers)
+  if constexpr (NC > 0) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int i = j + r * T;
-        v[r] = buf[rsw ? fft_sw(i) : i];
-      }
-      if (s > 0) {
-        const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));   // k * N / (8 Ns)
+    for (int s = 0; s < n8; ++s) {
+      const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
+      float2 v[8];
+      const int j = tid;
+      if (active) {
 #pragma unroll
-        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], twid<INV>(tw, r * ks));
+        for (int r = 0; r < 8; ++r) {
+          const int i = j + r * T;
+          v[r] = buf[rsw ? fft_sw(i) : i];
+        }
+        if (s > 0) {
+          const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));   // k * N / (8 Ns)
+#pragma unroll
+          for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], twid<INV>(tw, r * ks));
+        }
+        dft8_inplace<INV>(v);
       }
-      dft8_inplace<INV>(v);
+      __syncthreads();
+      if (active) {
+        const int idx = ((j >> lNs) << (lNs + 3)) + (j & (Ns - 1));
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int i = idx + r * Ns;
+          buf[wsw ? fft_sw(i) : i] = v[r];
+        }
+      }
+      __syncthreads();
+      Ns <<= 3;
+      lNs += 3;
     }
-    __syncthreads();
-    if (active) {
-      const int idx = ((j >> lNs) << (lNs + 3)) + (j & (Ns - 1));
+  } else {
+    for (int s = 0; s < n8; ++s) {
+      const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
+      float2 v[8];
+      const int j = tid;
+      if (active) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int i = idx + r * Ns;
-        buf[wsw ? fft_sw(i) : i] = v[r];
+        for (int r = 0; r < 8; ++r) {
+          const int i = j + r * T;
+          v[r] = buf[rsw ? fft_sw(i) : i];
+        }
+        if (s > 0) {
+          const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));   // k * N / (8 Ns)
+#pragma unroll
+          for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], twid<INV>(tw, r * ks));
+        }
+        dft8_inplace<INV>(v);
       }
+      __syncthreads();
+      if (active) {
+        const int idx = ((j >> lNs) << (lNs + 3)) + (j & (Ns - 1));
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int i = idx + r * Ns;
+          buf[wsw ? fft_sw(i) : i] = v[r];
+        }
+      }
+      __syncthreads();
+      Ns <<= 3;
+      lNs += 3;
     }
-    __syncthreads();
-    Ns <<= 3;
-    lNs += 3;
   }
   if (rem == 2) {   // final radix-4 pass (Ns == N/4): two butterflies per thread
     const int q4 = N >> 2;

@@ -129,13 +129,13 @@ __device__ __forceinline__ void tx_channel(float2* buf, const Grid& g, const TxC
   }
 }
 
-template <int CODED, int BPS, bool SCF = false, bool CH = false>
+template <int CODED, int BPS, bool SCF = false, bool CH = false, int NC = 0>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
                                                 const int32_t* __restrict__ tx_map, float2* __restrict__ x, int B,
                                                 float2* __restrict__ cap_syms, int stage_enc, TxChannel ch) {
   extern __shared__ float2 sm[];
-  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int N = NC ? NC : g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int gs = blockIdx.x * spw + slot;
   const int b = gs / g.n_sym, l = gs - b * g.n_sym;
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
       for (int j = tid; j < g.Nd; j += T) buf[g.data_idx[j]] = pre[j];
   }
   __syncthreads();
-  fft_lds<true>(buf, N, g.log2N, g.tw, tid, active);
+  fft_lds<true, NC>(buf, N, g.log2N, g.tw, tid, active);
   if constexpr (CH) {
     tx_channel(buf, g, ch, b, l, slot, tid, T, active, rsqrtf((float)N));
   } else if (active) {
@@ -264,9 +264,13 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
   const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
   const int stage_enc = coded && enc_shm <= 32768;
   const size_t shm = (size_t)spw * g.N * sizeof(float2) + (stage_enc ? enc_shm : 0);
-#define LTE_TXC(C_, B_)                                                                                         \
-  hipLaunchKernelGGL((k_ofdm_tx<C_, B_, false, true>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words, \
-                     tx_map, (float2*)nullptr, B, cap_syms, stage_enc, ch)
+#define LTE_TXC(C_, B_)                                                                                      \
+  if (g.N == 2048)                                                                                             \
+    hipLaunchKernelGGL((k_ofdm_tx<C_, B_, false, true, 2048>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, \
+                       enc_words, tx_map, (float2*)nullptr, B, cap_syms, stage_enc, ch);                         \
+  else                                                                                                         \
+    hipLaunchKernelGGL((k_ofdm_tx<C_, B_, false, true>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,        \
+                       enc_words, tx_map, (float2*)nullptr, B, cap_syms, stage_enc, ch)
   if (coded) {
     if (g.bps == 2) LTE_TXC(1, 2); else if (g.bps == 4) LTE_TXC(1, 4); else LTE_TXC(1, 6);
   } else {
@@ -489,13 +493,14 @@ __device__ __forceinline__ float frame_power(const float* pp, int nblk, int L) {
 // Channel estimation: one slot per (frame, rx, 14-symbol group) on the group's
 // first symbol (LTEReceiver._estimate_channel_periodic lte_receiver.py:360-411,
 // LTEChannelEstimator.estimate_channel :40-96, _interpolate_channel :98-133).
+template <int NC = 0>
 __global__ __launch_bounds__(WG) void k_rx_chest(Grid g, int B, int num_rx, const float2* __restrict__ y,
                                                  int64_t y_rx_stride, int64_t y_frame_stride,
                                                  const float* __restrict__ npow_in, const uint64_t* __restrict__ fid,
                                                  uint64_t seed, const float* __restrict__ inj_z, int64_t inj_stride,
                                                  float2* __restrict__ H, float* __restrict__ pstats) {
   extern __shared__ float2 sm[];
-  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int N = NC ? NC : g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int64_t gs = (int64_t)blockIdx.x * spw + slot;
   const int per = num_rx * g.n_grp;
@@ -510,7 +515,7 @@ __global__ __launch_bounds__(WG) void k_rx_chest(Grid g, int B, int num_rx, cons
                       zf, g.L, tid, T);
   }
   __syncthreads();
-  fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
+  fft_lds<false, NC>(buf, N, g.log2N, g.tw, tid, active);
   if (active) {
     const float sc = rsqrtf((float)N);
     for (int p = tid; p < g.Np; p += T) {
@@ -572,8 +577,12 @@ int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float
   const int64_t total = (int64_t)B * num_rx * g.n_grp;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = (size_t)spw * (g.N + g.Np) * sizeof(float2);
-  hipLaunchKernelGGL(k_rx_chest, dim3(blocks), dim3(WG), shm, s, g, B, num_rx, y, y_rx_stride, y_frame_stride,
-                     npow, fid, seed, inj_z, inj_stride, H, pstats);
+  if (g.N == 2048)
+    hipLaunchKernelGGL(k_rx_chest<2048>, dim3(blocks), dim3(WG), shm, s, g, B, num_rx, y, y_rx_stride, y_frame_stride,
+                       npow, fid, seed, inj_z, inj_stride, H, pstats);
+  else
+    hipLaunchKernelGGL(k_rx_chest<0>, dim3(blocks), dim3(WG), shm, s, g, B, num_rx, y, y_rx_stride, y_frame_stride,
+                       npow, fid, seed, inj_z, inj_stride, H, pstats);
   return (int)hipGetLastError();
 }
 
@@ -589,7 +598,7 @@ int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float
 // Templated on chain and bits/symbol so every per-RE array stays in VGPRs.
 //  SCF (SC-FDM, UNCODED): the ZF outputs of the symbol's Nd data REs go
 //       through the M = Nd IDFT (core/lte_receiver.py:318-333) before slicing.
-template <int CHAIN, int BPS, bool SCF = false>
+template <int CHAIN, int BPS, bool SCF = false, int NC = 0>
 __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int num_rx,
                                                 const float2* __restrict__ y, int64_t y_rx_stride,
                                                 int64_t y_frame_stride, const float2* __restrict__ H,
@@ -601,7 +610,7 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
                                                 float2* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits,
                                                 float* __restrict__ nvo) {
   extern __shared__ float2 sm[];
-  const int N = g.N, T = N >> 3, spw = WG / T;
+  const int N = NC ? NC : g.N, T = N >> 3, spw = WG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int gs = blockIdx.x * spw + slot;
   const int b = gs / g.n_sym, l = gs - b * g.n_sym;
@@ -624,7 +633,7 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
                          g.L, tid, T);
     }
     __syncthreads();
-    fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
+    fft_lds<false, NC>(buf, N, g.log2N, g.tw, tid, active);
     if (active) {
       const float2* Hf = H + (((size_t)b * num_rx + rx) * g.n_grp + grp) * N;
 #pragma unroll
@@ -714,25 +723,25 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
   if constexpr (CHAIN != LTE_CHAIN_CODED) frame_err_add(frame_err, b, errs);
 }
 
-template <int CHAIN, int BPS, bool SCF>
+template <int CHAIN, int BPS, bool SCF, int NC = 0>
 static void rx_data_inst(hipStream_t s, int blocks, size_t shm, const Grid& g, int rayleigh, int B, int num_rx,
                          const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                          const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                          const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
                          uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, float* nvo) {
-  hipLaunchKernelGGL((k_rx_data<CHAIN, BPS, SCF>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, num_rx, y,
+  hipLaunchKernelGGL((k_rx_data<CHAIN, BPS, SCF, NC>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, num_rx, y,
                      y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits,
                      frame_err, llr, cap_syms, cap_bits, nvo);
 }
 
-template <int CHAIN, bool SCF = false>
+template <int CHAIN, bool SCF = false, int NC = 0>
 static void rx_data_bps(int bps, hipStream_t s, int blocks, size_t shm, const Grid& g, int rayleigh, int B,
                         int num_rx, const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
                         const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
                         const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
                         uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, float* nvo) {
-  auto* f = bps == 2 ? &rx_data_inst<CHAIN, 2, SCF>
-                     : (bps == 4 ? &rx_data_inst<CHAIN, 4, SCF> : &rx_data_inst<CHAIN, 6, SCF>);
+  auto* f = bps == 2 ? &rx_data_inst<CHAIN, 2, SCF, NC>
+                     : (bps == 4 ? &rx_data_inst<CHAIN, 4, SCF, NC> : &rx_data_inst<CHAIN, 6, SCF, NC>);
   f(s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H, npow, snr_lin, fid, seed, inj_z,
     inj_stride, pw, PW, n_bits, frame_err, llr, cap_syms, cap_bits, nvo);
 }
@@ -751,7 +760,11 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = spw * g.N * sizeof(float2);
-  if (chain == LTE_CHAIN_CODED)
+  if (chain == LTE_CHAIN_CODED && g.N == 2048)   // the headline chain: compile-time FFT size
+    rx_data_bps<LTE_CHAIN_CODED, false, 2048>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride,
+                                              y_frame_stride, H, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW,
+                                              n_bits, frame_err, llr, cap_syms, cap_bits, nv_out);
+  else if (chain == LTE_CHAIN_CODED)
     rx_data_bps<LTE_CHAIN_CODED>(g.bps, s, blocks, shm, g, rayleigh, B, num_rx, y, y_rx_stride, y_frame_stride, H,
                                  npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,
                                  cap_syms, cap_bits, nv_out);

@@ -670,7 +670,7 @@ __global__ __launch_bounds__(ENC_WG) void k_encode(const uint32_t* __restrict__ 
     for (int i = 0; i < ENC_CH; ++i) {
       const int w = wc + i;
       fb[i] = qb[i] = 0u;
-      if (w * 32 >= K) break;
+      if (w * 32 >= K) continue;
       const uint32_t wn = ldw(i00 + w + 2);   // next window word, in flight during this one
       const int p0 = w * 32, nb = min(32, K - p0);
       uint32_t t = o ? ((wa << o) | (wb >> (32 - o))) : wa;
@@ -750,7 +750,7 @@ __global__ __launch_bounds__(64) void k_encode2(int KWmax, uint32_t* __restrict_
     for (int j = 0; j < ENC2_CH; ++j) {
       const int w = wc + j;
       qb[j] = 0u;
-      if (w >= KW) break;
+      if (w >= KW) continue;
       const int nb = min(32, K - w * 32);
       uint32_t u = 0;
 #pragma unroll

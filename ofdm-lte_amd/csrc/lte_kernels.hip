@@ -72,13 +72,6 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 }
 
 // ---------------------------------------------------------------------------
-// OFDM TX: one slot = one OFDM symbol; 2048/N slots per 256-thread block.
-// QAMModulator.bits_to_symbols (modulator.py:61-88) / coded RE mapping via
-// tx_map (rate_match_turbo + T/F interleaver, rate_matching.py:193-297,
-// ofdm_core.py:1040-1099), ResourceMapper.map_symbols (resource_mapper.py:
-// 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
-// SCF (SC-FDM, uncoded chains): the Nd QAM symbols of the OFDM symbol are
-// DFT-precoded (M = Nd, core/modulator.py:232-236) in a second LDS buffer first.
 // Fused static-tap channel for one OFDM symbol held in LDS (TxChannel): y[m] =
 // sum_p c_p x[m - d_p] over the CP-extended symbol, whose sample j is
 // buf[j < cp ? N - cp + j : j - cp] (rayleighchannel.py:44-58; for m >=
@@ -129,6 +122,14 @@ __device__ __forceinline__ void tx_channel(float2* buf, const Grid& g, const TxC
   }
 }
 
+// OFDM TX: one slot = one OFDM symbol; 2048/N slots per 256-thread block.
+// QAMModulator.bits_to_symbols (modulator.py:61-88) / coded RE mapping via
+// tx_map (rate_match_turbo + T/F interleaver, rate_matching.py:193-297,
+// ofdm_core.py:1040-1099), ResourceMapper.map_symbols (resource_mapper.py:
+// 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
+// SCF (SC-FDM, uncoded chains): the Nd QAM symbols of the OFDM symbol are
+// DFT-precoded (M = Nd, core/modulator.py:232-236) in a second LDS buffer first.
+// CH: the channel applied in place (tx_channel); NC: compile-time N (fft_lds).
 template <int CODED, int BPS, bool SCF = false, bool CH = false, int NC = 0>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,

@@ -640,9 +640,12 @@ __global__ __launch_bounds__(ENC_WG) void k_encode(const uint32_t* __restrict__ 
   __shared__ uint32_t crc_t[256];
   for (int i = threadIdx.x; i < 256; i += ENC_WG) crc_t[i] = crc24_table_entry(i, 0x800063u);   // CRC-24B
   __syncthreads();
+  // lanes = frames of ONE code-block slot: frame groups are padded to 64 per
+  // slot (Bp), so K, F, f1, f2 are wave-uniform (scalar registers)
+  const int Bp = (B + 63) & ~63;
   const int gid = blockIdx.x * ENC_WG + threadIdx.x;
-  if (gid >= C * B) return;           // no barriers below: early exit is safe
-  const int r = gid / B, b = gid % B;
+  const int r = __builtin_amdgcn_readfirstlane(gid / Bp), b = gid % Bp;
+  if (r >= C || b >= B) return;       // no barriers below: early exit is safe
   const CbInfo ci = cbi[r];
   const int K = ci.K, F = ci.F;
   const uint32_t* tb = pw + (size_t)b * PW;
@@ -729,10 +732,11 @@ __global__ __launch_bounds__(64) void k_encode2(int KWmax, uint32_t* __restrict_
                                                 const CbInfo* __restrict__ cbi, int C, int B,
                                                 const uint32_t* __restrict__ cw_scratch) {
   extern __shared__ uint32_t cwl[];   // [KWmax][64]
+  const int Bp = (B + 63) & ~63;     // frame groups padded per slot (see k_encode)
   const int gid = blockIdx.x * 64 + threadIdx.x;
-  if (gid >= C * B) return;           // no barriers: each lane reads back only its own column
   const int lane = threadIdx.x;
-  const int r = gid / B, b = gid % B;
+  const int r = __builtin_amdgcn_readfirstlane(gid / Bp), b = gid % Bp;
+  if (r >= C || b >= B) return;       // no barriers: each lane reads back only its own column
   const CbInfo ci = cbi[r];
   const int K = ci.K, KW = (K + 31) >> 5;
   const uint32_t* cw = cw_scratch + (size_t)blockIdx.x * KWmax * 64 + lane;
@@ -795,11 +799,11 @@ __global__ __launch_bounds__(64) void k_encode2(int KWmax, uint32_t* __restrict_
   w2.flush();
 }
 
-size_t encode_scratch_words(int KWmax, int C, int B) { return (((size_t)C * B + 63) / 64) * KWmax * 64; }
+size_t encode_scratch_words(int KWmax, int C, int B) { return (size_t)C * ((B + 63) / 64) * KWmax * 64; }
 
 int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
                   const CbInfo* cbi_dev, int C, int B, uint32_t* cw_scratch) {
-  const int64_t n = (int64_t)C * B;
+  const int64_t n = (int64_t)C * ((B + 63) & ~63);   // lanes: frames padded to 64 per CB slot
   if (n > 0x7FFFFFFF || !cw_scratch) return (int)hipErrorInvalidValue;
   const size_t shm = (size_t)KWmax * 64 * sizeof(uint32_t);
   if (shm > 65536) return (int)hipErrorInvalidValue;

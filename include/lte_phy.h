@@ -196,6 +196,12 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t *bits, uint8_t *out 
 int lte_turbo_decode_host(int K, int iters, int64_t ncb, const float *llr /*[ncb][3K+12]*/, uint8_t *bits);
 /* One max-log BCJR pass, a-posteriori output: LogMAPDecoder.decode turbo_decoder.py:181-278 */
 int lte_bcjr_host(int K, int64_t ncb, const float *ls, const float *lp, const float *la, float *app);
+/* float64 turbo decode, bit-exact with turbo_decode (core/channel_coding/turbo_decoder.py:338-450):
+ * the reference's unnormalised max-log recursion in its own operation order. */
+int lte_turbo_decode_host64(int K, int iters, int64_t ncb, const double *llr /*[ncb][3K+12]*/, uint8_t *bits);
+/* float64 single BCJR pass of any length n, a-posteriori output for every step:
+ * LogMAPDecoder.decode (turbo_decoder.py:181-278) with return_extrinsic=False. */
+int lte_bcjr_host64(int n, int64_t ncb, const double *ls, const double *lp, const double *la, double *app);
 /* CRC: _calculate_crc core/channel_coding/crc.py:89-134 (MSB-first, zero init) */
 int lte_crc_host(int64_t n, const uint8_t *bits, uint32_t poly, int len, uint32_t *crc);
 /* Channel on an arbitrary-length stream: ChannelSimulator.transmit (core/channel.py:

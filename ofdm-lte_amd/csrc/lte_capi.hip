@@ -913,7 +913,7 @@ static int plan_alloc(lte_plan* p) {
       const int K = p->cbs[r].K;
       rows[r] = turbo_rows(K);
       bad |= p->blk[r].alloc((size_t)G * rows[r] * 64) != 0;
-      bad |= p->ckpt[r].alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS * 64) != 0;
+      bad |= p->ckpt[r].alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS_F32 * 64) != 0;
       kw[r] = turbo_kw(K);
       bad |= p->decb[r].alloc((size_t)G * kw[r] * 64) != 0;
       if (!bad) HIPCHK(hipMemset(p->blk[r].p, 0, p->blk[r].n * sizeof(float)));
@@ -1239,7 +1239,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     }
     {
       Timer t(p, KN_TURBO);
-      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1));
+      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1, 0));
     }
     {
       Timer t(p, KN_CRC);
@@ -1565,12 +1565,12 @@ static int run_coded_pipelined(lte_plan* p, const lte_run_args* a, int B, int ch
     for (int r = 0; r < p->C; ++r) {
       const CbInfo& cb = p->cbs[r];
       jobs[r] = TurboJob{p->blk[r].p + (size_t)g0 * turbo_rows(cb.K) * 64,
-                         p->ckpt[r].p + (size_t)g0 * turbo_nwin(cb.K) * TURBO_CK_ROWS * 64,
+                         p->ckpt[r].p + (size_t)g0 * turbo_nwin(cb.K) * TURBO_CK_ROWS_F32 * 64,
                          p->decb[r].p + (size_t)g0 * turbo_kw(cb.K) * 64, cb.K, cb.f1, cb.f2, g1 - g0};
     }
     {
       Timer t(p, KN_TURBO, s2);
-      LCHK(launch_turbo_jobs(s2, jobs.data(), p->C, d.turbo_iters, TM_DEC1));
+      LCHK(launch_turbo_jobs(s2, jobs.data(), p->C, d.turbo_iters, TM_DEC1, 0));
     }
     {
       Timer t(p, KN_CRC, s2);
@@ -1772,7 +1772,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     }
     {
       Timer t(p, KN_TURBO);
-      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1));
+      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1, 0));
     }
     {
       Timer t(p, KN_CRC);
@@ -1990,27 +1990,31 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out)
   return rc;
 }
 
-// Host-side layout conversion [ncb][3K+12] -> decoder rows, shared by the two
-// turbo entry points.
-static int turbo_host_run(int K, int iters, int64_t ncb, const float* llr, const float* ls, const float* lp,
-                          const float* la, int mode, uint8_t* bits, float* app) {
+}  // extern "C"
+
+// Host-side layout conversion [ncb][3K+12] -> decoder rows, shared by the
+// turbo entry points.  T = float (fast mode) / double (the reference's precision).
+template <class T>
+static int turbo_host_run(int K, int iters, int64_t ncb, const T* llr, const T* ls, const T* lp, const T* la,
+                          int mode, uint8_t* bits, T* app) {
   int f1, f2;
   if (!qpp_lookup(K, &f1, &f2)) return fail(LTE_EINVAL, "Invalid interleaver size K=" + std::to_string(K));
   if (ncb < 0) return fail(LTE_EINVAL, "bad ncb");
   if (ncb == 0) return LTE_OK;
+  const int f64 = sizeof(T) == 8;
   const int G = (int)((ncb + 63) / 64);
   const int64_t rows = turbo_rows(K);
-  std::vector<float> h((size_t)G * rows * 64, 0.f);
-  auto at = [&](int64_t c, int64_t row) -> float& { return h[((c / 64) * rows + row) * 64 + (c % 64)]; };
+  std::vector<T> h((size_t)G * rows * 64, (T)0);
+  auto at = [&](int64_t c, int64_t row) -> T& { return h[((c / 64) * rows + row) * 64 + (c % 64)]; };
   for (int64_t c = 0; c < ncb; ++c) {
     if (mode == TM_APP) {
-      const float* s = ls + c * (K + 3);
-      const float* q = lp + c * (K + 3);
-      const float* A = la + c * (K + 3);
+      const T* s = ls + c * (K + 3);
+      const T* q = lp + c * (K + 3);
+      const T* A = la + c * (K + 3);
       for (int k = 0; k < K + 3; ++k) { at(c, k) = s[k]; at(c, K + 3 + k) = q[k]; }
       for (int k = 0; k < K; ++k) at(c, 3 * K + 12 + k) = A[k];
     } else {
-      const float* l = llr + c * (3 * K + 12);
+      const T* l = llr + c * (3 * K + 12);
       for (int k = 0; k < K; ++k) {
         at(c, k) = l[3 * k];
         at(c, K + 3 + k) = l[3 * k + 1];
@@ -2024,20 +2028,23 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const float* llr, const
       }
     }
   }
-  for (float& v : h) v *= 0.5f;   // decoder rows hold LLR/2 (exact; lte_turbo.hip gam2)
-  DBuf<float> db, dck;
+  for (T& v : h) v *= (T)0.5;   // decoder rows hold LLR/2 (exact; lte_decoder.hip gam)
+  DBuf<T> db, dck;
   DBuf<uint32_t> dbits;
   const int KW = turbo_kw(K);
-  if (db.alloc(h.size()) || dck.alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS * 64) || dbits.alloc((size_t)G * KW * 64))
+  if (db.alloc(h.size()) || dck.alloc((size_t)G * turbo_nwin(K) * turbo_ck_rows(f64) * 64) ||
+      dbits.alloc((size_t)G * KW * 64))
     return fail(LTE_ENOMEM, "turbo buffers");
   int rc = LTE_OK;
   std::vector<uint32_t> hb((size_t)G * KW * 64);
-  if (hipMemcpy(db.p, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      launch_turbo(nullptr, db.p, dck.p, dbits.p, K, f1, f2, iters, G, mode) || hipDeviceSynchronize() != hipSuccess)
+  if (hipMemcpy(db.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess ||
+      launch_turbo(nullptr, db.p, dck.p, dbits.p, K, f1, f2, iters, G, mode, f64) ||
+      hipDeviceSynchronize() != hipSuccess)
     rc = fail(LTE_EHIP, std::string("turbo failed: ") + hipGetErrorString(hipGetLastError()));
   if (rc == LTE_OK) {
     if (mode == TM_APP) {
-      if (hipMemcpy(h.data(), db.p, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(LTE_EHIP, "copy");
+      if (hipMemcpy(h.data(), db.p, h.size() * sizeof(T), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(LTE_EHIP, "copy");
       for (int64_t c = 0; c < ncb && rc == LTE_OK; ++c)
         for (int k = 0; k < K; ++k) app[c * K + k] = at(c, 3 * K + 12 + k);
     } else {
@@ -2053,14 +2060,39 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const float* llr, const
   return rc;
 }
 
+extern "C" {
+
 int lte_turbo_decode_host(int K, int iters, int64_t ncb, const float* llr, uint8_t* bits) {
   if (iters < 0 || (ncb > 0 && (!llr || !bits))) return fail(LTE_EINVAL, "bad arguments");
-  return turbo_host_run(K, iters, ncb, llr, nullptr, nullptr, nullptr, TM_DEC1, bits, nullptr);
+  return turbo_host_run<float>(K, iters, ncb, llr, nullptr, nullptr, nullptr, TM_DEC1, bits, nullptr);
+}
+
+int lte_turbo_decode_host64(int K, int iters, int64_t ncb, const double* llr, uint8_t* bits) {
+  if (iters < 0 || (ncb > 0 && (!llr || !bits))) return fail(LTE_EINVAL, "bad arguments");
+  return turbo_host_run<double>(K, iters, ncb, llr, nullptr, nullptr, nullptr, TM_DEC1, bits, nullptr);
 }
 
 int lte_bcjr_host(int K, int64_t ncb, const float* ls, const float* lp, const float* la, float* app) {
   if (ncb > 0 && (!ls || !lp || !la || !app)) return fail(LTE_EINVAL, "bad arguments");
-  return turbo_host_run(K, 0, ncb, nullptr, ls, lp, la, TM_APP, nullptr, app);
+  return turbo_host_run<float>(K, 0, ncb, nullptr, ls, lp, la, TM_APP, nullptr, app);
+}
+
+int lte_bcjr_host64(int n, int64_t ncb, const double* ls, const double* lp, const double* la, double* app) {
+  if (n < 1 || ncb < 0 || (ncb > 0 && (!ls || !lp || !la || !app))) return fail(LTE_EINVAL, "bad arguments");
+  if (ncb == 0) return LTE_OK;
+  const size_t sz = (size_t)ncb * n;
+  DBuf<double> dls, dlp, dla, dal, dapp;
+  if (dls.alloc(sz) || dlp.alloc(sz) || dla.alloc(sz) || dal.alloc(sz * 8) || dapp.alloc(sz))
+    return fail(LTE_ENOMEM, "bcjr buffers");
+  int rc = LTE_OK;
+  if (hipMemcpy(dls.p, ls, sz * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dlp.p, lp, sz * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dla.p, la, sz * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_bcjr64(nullptr, dls.p, dlp.p, dla.p, n, (int)ncb, dal.p, dapp.p) ||
+      hipDeviceSynchronize() != hipSuccess || hipMemcpy(app, dapp.p, sz * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, std::string("bcjr failed: ") + hipGetErrorString(hipGetLastError()));
+  dls.release(); dlp.release(); dla.release(); dal.release(); dapp.release();
+  return rc;
 }
 
 }  // extern "C"

@@ -5,6 +5,21 @@
 
 #define LTE_NEG_BIG (-1.0e30f)
 
+// ---------------------------------------------------------------- precision
+// The signal chains compute in R = double (the default: the reference is
+// float64 / complex128 throughout) or R = float (opt-in fast mode).  cx<R> is
+// the matching complex type (float2 / double2), re_t<V> a complex's real type.
+template <class R> struct cx_of;
+template <> struct cx_of<float> { using type = float2; };
+template <> struct cx_of<double> { using type = double2; };
+template <class R> using cx = typename cx_of<R>::type;
+template <class V> struct re_of;
+template <> struct re_of<float2> { using type = float; };
+template <> struct re_of<double2> { using type = double; };
+template <class V> using re_t = typename re_of<V>::type;
+__host__ __device__ __forceinline__ float2 mkc(float a, float b) { return make_float2(a, b); }
+__host__ __device__ __forceinline__ double2 mkc(double a, double b) { return make_double2(a, b); }
+
 // ---------------------------------------------------------------- RNG
 // Philox4x32-10 (counter-based, stateless): every random number is a pure
 // function of (seed, frame id, stream, index), so results do not depend on
@@ -48,6 +63,20 @@ __device__ __forceinline__ float2 box_muller(uint32_t a, uint32_t b) {
   return make_float2(r * c, r * s);
 }
 
+// float64 Box-Muller for the f64 chain's synthetic noise: 32-bit uniforms in
+// (0, 1), float64 log / sqrt / sincos (the arithmetic type of the chain)
+__device__ __forceinline__ double2 box_muller64(uint32_t a, uint32_t b) {
+  const double u = ((double)a + 0.5) * 2.3283064365386962890625e-10;   // 2^-32
+  const double v = ((double)b + 0.5) * 2.3283064365386962890625e-10;
+  const double r = sqrt(-2.0 * log(u));
+  double s, c;
+  sincospi(2.0 * v, &s, &c);
+  return make_double2(r * c, r * s);
+}
+template <class R> __device__ __forceinline__ cx<R> gauss2(uint32_t a, uint32_t b);
+template <> __device__ __forceinline__ float2 gauss2<float>(uint32_t a, uint32_t b) { return box_muller(a, b); }
+template <> __device__ __forceinline__ double2 gauss2<double>(uint32_t a, uint32_t b) { return box_muller64(a, b); }
+
 // ---------------------------------------------------------------- complex
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -58,6 +87,15 @@ __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
   return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
 }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {
+  return make_double2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+__device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
 // Complex division with Smith's scaling (the algorithm NumPy's complex divide uses).
 __device__ __forceinline__ float2 cdiv(float2 a, float2 b) {
   if (fabsf(b.x) >= fabsf(b.y)) {
@@ -67,6 +105,15 @@ __device__ __forceinline__ float2 cdiv(float2 a, float2 b) {
   }
   const float rat = b.x / b.y, scl = 1.0f / (b.y + b.x * rat);
   return make_float2((a.x * rat + a.y) * scl, (a.y * rat - a.x) * scl);
+}
+__device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
+  if (fabs(b.x) >= fabs(b.y)) {
+    if (b.x == 0.0 && b.y == 0.0) return make_double2(a.x / b.x, a.y / b.x);
+    const double rat = b.y / b.x, scl = 1.0 / (b.x + b.y * rat);
+    return make_double2((a.x + a.y * rat) * scl, (a.y - a.x * rat) * scl);
+  }
+  const double rat = b.x / b.y, scl = 1.0 / (b.y + b.x * rat);
+  return make_double2((a.x * rat + a.y) * scl, (a.y * rat - a.x) * scl);
 }
 
 // ---------------------------------------------------------------- FFT
@@ -79,26 +126,28 @@ __device__ __forceinline__ float2 cdiv(float2 a, float2 b) {
 // (fft_sw) that makes the strided Stockham stores conflict-free for
 // ds_write_b64 (16-lane groups, banks mod 32); the caller's layout (input and
 // output) is the natural one.  tw[e] = exp(-2*pi*i*e/N), e in [0, N).
+// V = float2 or double2 (the chain precision; fft_sw's swizzle is tuned for
+// the 8-B float2 element).
 // Unscaled.  N in [128, 2048].  All threads of the workgroup must call it (it
 // contains __syncthreads).
-template <bool INV>
-__device__ __forceinline__ float2 twid(const float2* __restrict__ tw, int e) {
-  const float2 w = tw[e];
-  return INV ? make_float2(w.x, -w.y) : w;
+template <bool INV, class V>
+__device__ __forceinline__ V twid(const V* __restrict__ tw, int e) {
+  const V w = tw[e];
+  return INV ? mkc(w.x, -w.y) : w;
 }
 
 // logical -> physical float2 index between passes (bijection on each 128-block)
 __device__ __forceinline__ int fft_sw(int i) { return i ^ (((i >> 4) & 7) | ((i >> 3) & 8)); }
 
 // x * -j (forward) or x * +j (inverse)
-template <bool INV>
-__device__ __forceinline__ float2 mul_mj(float2 d) {
-  return INV ? make_float2(-d.y, d.x) : make_float2(d.y, -d.x);
+template <bool INV, class V>
+__device__ __forceinline__ V mul_mj(V d) {
+  return INV ? mkc(-d.y, d.x) : mkc(d.y, -d.x);
 }
 
-template <bool INV>
-__device__ __forceinline__ void dft4_inplace(float2& a0, float2& a1, float2& a2, float2& a3) {
-  const float2 b0 = cadd(a0, a2), b1 = csub(a0, a2), b2 = cadd(a1, a3), b3 = mul_mj<INV>(csub(a1, a3));
+template <bool INV, class V>
+__device__ __forceinline__ void dft4_inplace(V& a0, V& a1, V& a2, V& a3) {
+  const V b0 = cadd(a0, a2), b1 = csub(a0, a2), b2 = cadd(a1, a3), b3 = mul_mj<INV>(csub(a1, a3));
   a0 = cadd(b0, b2);
   a2 = csub(b0, b2);
   a1 = cadd(b1, b3);
@@ -106,22 +155,23 @@ __device__ __forceinline__ void dft4_inplace(float2& a0, float2& a1, float2& a2,
 }
 
 // radix-8 DFT in registers: out[m] = sum_r v[r] W8^(r m)
-template <bool INV>
-__device__ __forceinline__ void dft8_inplace(float2 (&v)[8]) {
+template <bool INV, class V>
+__device__ __forceinline__ void dft8_inplace(V (&v)[8]) {
+  using R = re_t<V>;
   dft4_inplace<INV>(v[0], v[2], v[4], v[6]);   // E[m] in v[0,2,4,6]
   dft4_inplace<INV>(v[1], v[3], v[5], v[7]);   // O[m] in v[1,3,5,7]
-  const float s = 0.70710678118654752f;
-  const float2 o0 = v[1];
-  float2 o1 = v[3], o3 = v[7];
-  const float2 o2 = mul_mj<INV>(v[5]);         // W8^2 = -j (forward)
+  const R s = (R)0.70710678118654752440;
+  const V o0 = v[1];
+  V o1 = v[3], o3 = v[7];
+  const V o2 = mul_mj<INV>(v[5]);         // W8^2 = -j (forward)
   if (INV) {                                   // W8^1 = (1+j)/sqrt2, W8^3 = (-1+j)/sqrt2
-    o1 = make_float2((o1.x - o1.y) * s, (o1.x + o1.y) * s);
-    o3 = make_float2((-o3.x - o3.y) * s, (o3.x - o3.y) * s);
+    o1 = mkc((o1.x - o1.y) * s, (o1.x + o1.y) * s);
+    o3 = mkc((-o3.x - o3.y) * s, (o3.x - o3.y) * s);
   } else {                                     // W8^1 = (1-j)/sqrt2, W8^3 = (-1-j)/sqrt2
-    o1 = make_float2((o1.x + o1.y) * s, (o1.y - o1.x) * s);
-    o3 = make_float2((o3.y - o3.x) * s, (-o3.x - o3.y) * s);
+    o1 = mkc((o1.x + o1.y) * s, (o1.y - o1.x) * s);
+    o3 = mkc((o3.y - o3.x) * s, (-o3.x - o3.y) * s);
   }
-  const float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+  const V e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
   v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
   v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
   v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
@@ -131,9 +181,8 @@ __device__ __forceinline__ void dft8_inplace(float2 (&v)[8]) {
 // NC > 0: a kernel instance for one transform size (NC = N): pass count,
 // strides, swizzle predicates and twiddle strides fold and the passes unroll
 // (ofdm_tx / rx_data / rx_chest at N = 2048: -2..-15 % time).  NC = 0: runtime N.
-template <bool INV, int NC = 0>
-__device__ __forceinline__ void fft_lds(float2* buf, int N_, int log2N_, const float2* __restrict__ tw,
-                                        int tid, bool active) {
+template <bool INV, int NC = 0, class V>
+__device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __restrict__ tw, int tid, bool active) {
   const int N = NC ? NC : N_;
   const int log2N = NC ? __builtin_ctz(NC) : log2N_;
   const int T = N >> 3;
@@ -145,7 +194,7 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N_, int log2N_, const f
 #pragma unroll
     for (int s = 0; s < n8; ++s) {
       const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
-      float2 v[8];
+      V v[8];
       const int j = tid;
       if (active) {
 #pragma unroll
@@ -176,7 +225,7 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N_, int log2N_, const f
   } else {
     for (int s = 0; s < n8; ++s) {
       const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
-      float2 v[8];
+      V v[8];
       const int j = tid;
       if (active) {
 #pragma unroll
@@ -207,7 +256,7 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N_, int log2N_, const f
   }
   if (rem == 2) {   // final radix-4 pass (Ns == N/4): two butterflies per thread
     const int q4 = N >> 2;
-    float2 v[2][4];
+    V v[2][4];
     if (active) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -231,12 +280,12 @@ __device__ __forceinline__ void fft_lds(float2* buf, int N_, int log2N_, const f
     __syncthreads();
   } else if (rem == 1) {   // final radix-2 pass (Ns == N/2): four butterflies per thread
     const int h = N >> 1;
-    float2 v[4][2];
+    V v[4][2];
     if (active) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = tid + q * T;
-        const float2 a = buf[fft_sw(j)], b = cmul(buf[fft_sw(j + h)], twid<INV>(tw, j));
+        const V a = buf[fft_sw(j)], b = cmul(buf[fft_sw(j + h)], twid<INV>(tw, j));
         v[q][0] = cadd(a, b);
         v[q][1] = csub(a, b);
       }

@@ -1,6 +1,8 @@
 // Device helpers shared by the kernel translation units (lte_kernels.hip,
-// lte_mimo.hip): QAM points / slicers / max-log demappers, the noisy symbol
-// loader and block reductions.
+// lte_turbo.hip, lte_mimo.hip, lte_bf.hip): QAM points / slicers / max-log
+// demappers, the noisy symbol loader and block reductions.  The SISO / SIMO
+// chains instantiate them for both precisions (R = float / double, V =
+// cx<R>); the multi-antenna chains use the float instances.
 #pragma once
 #include "lte_common.h"
 #include "lte_internal.h"
@@ -8,11 +10,21 @@
 namespace lte {
 
 // QAM point of natural-binary index idx (modulator.py:28-59, I-major; QPSK
-// [1+1j, 1-1j, -1+1j, -1-1j]/sqrt 2), levels folded to float constants equal
-// to the float64 table cast to float.
-template <int BPS>
-__device__ __forceinline__ float2 qam_point(int idx) {
-  if constexpr (BPS == 2) {
+// [1+1j, 1-1j, -1+1j, -1-1j]/sqrt 2).  f64: NumPy's complex128 table exactly
+// -- level * (1/S) (NumPy's complex / real divide multiplies by the
+// reciprocal); f32: the float64 table's values cast to float.
+template <int BPS, class R = float>
+__device__ __forceinline__ cx<R> qam_point(int idx) {
+  if constexpr (sizeof(R) == 8) {
+    constexpr double S = BPS == 2 ? 1.4142135623730951 : (BPS == 4 ? 3.1622776601683795 : 6.48074069840786);
+    constexpr double inv = 1.0 / S;
+    if constexpr (BPS == 2) {
+      return make_double2((idx & 2) ? -inv : inv, (idx & 1) ? -inv : inv);
+    } else {
+      constexpr int H = BPS / 2, NL = 1 << H;
+      return make_double2((double)(2 * (idx >> H) - (NL - 1)) * inv, (double)(2 * (idx & (NL - 1)) - (NL - 1)) * inv);
+    }
+  } else if constexpr (BPS == 2) {
     constexpr float a = (float)(1.0 / 1.4142135623730951);
     return make_float2((idx & 2) ? -a : a, (idx & 1) ? -a : a);
   } else {
@@ -25,39 +37,41 @@ __device__ __forceinline__ float2 qam_point(int idx) {
   }
 }
 
-
-__device__ __forceinline__ float block_sum(float v, float* red) {
+template <class R>
+__device__ __forceinline__ R block_sum(R v, R* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) red[w] = v;
   __syncthreads();
-  float t = 0.f;
+  R t = (R)0;
   if (threadIdx.x == 0) {
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
   }
   return t;
 }
 
-
-__device__ __forceinline__ void load_symbol_noisy(float2* buf, const float2* __restrict__ yf, int N, int cp, int l,
-                                                  float sigma, uint64_t seed, uint64_t frame, int rx,
-                                                  const float* __restrict__ zf /*inj: [2][L] or null*/, int L,
+// Load one OFDM symbol (CP removed) of (frame, rx) into LDS adding AWGN:
+// noise = sigma * z, sigma = sqrt(P/SNR/2) (channel.py:52-60).
+template <class V>
+__device__ __forceinline__ void load_symbol_noisy(V* buf, const V* __restrict__ yf, int N, int cp, int l,
+                                                  re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
+                                                  const re_t<V>* __restrict__ zf /*inj: [2][L] or null*/, int L,
                                                   int tid, int T) {
+  using R = re_t<V>;
   const int off = l * (N + cp) + cp;
   for (int k = tid; k < N; k += T) {
     const int n = off + k;
-    float2 z;
+    V z;
     if (zf) {
-      z = make_float2(zf[n], zf[L + n]);
+      z = mkc(zf[n], zf[L + n]);
     } else {
       const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)(n >> 1));
-      z = (n & 1) ? box_muller(r.z, r.w) : box_muller(r.x, r.y);
+      z = (n & 1) ? gauss2<R>(r.z, r.w) : gauss2<R>(r.x, r.y);
     }
-    const float2 v = yf[n];
-    buf[k] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+    const V v = yf[n];
+    buf[k] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
   }
 }
-
 
 __device__ __forceinline__ int level_idx(float v, float scale, int nl) {
   // nearest of the nl levels (2i-(nl-1))/scale, ties -> lower level (argmin
@@ -66,9 +80,16 @@ __device__ __forceinline__ int level_idx(float v, float scale, int nl) {
   int i = (int)ceilf(t - 0.5f);
   return i < 0 ? 0 : (i > nl - 1 ? nl - 1 : i);
 }
+__device__ __forceinline__ int level_idx(double v, double scale, int nl) {
+  const double t = (v * scale + (double)(nl - 1)) * 0.5;
+  int i = (int)ceil(t - 0.5);
+  return i < 0 ? 0 : (i > nl - 1 ? nl - 1 : i);
+}
 
-__device__ __forceinline__ int hard_index(float2 y, int bps, float scale) {
-  if (bps == 2) return (y.x < 0.f ? 2 : 0) | (y.y < 0.f ? 1 : 0);  // [1+1j,1-1j,-1+1j,-1-1j]
+template <class V>
+__device__ __forceinline__ int hard_index(V y, int bps, re_t<V> scale) {
+  using R = re_t<V>;
+  if (bps == 2) return (y.x < (R)0 ? 2 : 0) | (y.y < (R)0 ? 1 : 0);  // [1+1j,1-1j,-1+1j,-1-1j]
   const int nl = 1 << (bps >> 1);
   return (level_idx(y.x, scale, nl) << (bps >> 1)) | level_idx(y.y, scale, nl);
 }
@@ -79,38 +100,44 @@ __host__ __device__ constexpr double qam_norm() { return BPS == 2 ? 1.4142135623
 
 // max-log LLRs (core/ofdm_core.py:791-923): QPSK 2*sqrt(2)*y/nv (no clip);
 // 16/64-QAM (min_{b=1} d^2 - min_{b=0} d^2)/(2 nv) clipped to +-10.  The
-// natural-binary map makes the metric separable per axis.  NB bits per axis,
-// levels folded to constants (correctly rounded from the float64 grid).
-template <int NB>
-__device__ __forceinline__ void llr_axis(float v, float inv2nv, float* out) {
+// natural-binary map makes the metric separable per axis.  NB bits per axis.
+// f32: levels folded to constants, 1/(2 nv) as a multiplier (q = 1/(2 nv));
+// f64: NumPy's level values and the reference's division (q = 2 nv).
+template <int NB, class R>
+__device__ __forceinline__ void llr_axis(R v, R q, R* out) {
   constexpr int NL = 1 << NB;
   constexpr double S = NB == 2 ? 3.1622776601683795 : 6.48074069840786;
-  float m0[NB], m1[NB];
+  R m0[NB], m1[NB];
 #pragma unroll
-  for (int bb = 0; bb < NB; ++bb) { m0[bb] = 3.4e38f; m1[bb] = 3.4e38f; }
+  for (int bb = 0; bb < NB; ++bb) { m0[bb] = (R)3.4e38f; m1[bb] = (R)3.4e38f; }
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const float lv = (float)((2.0 * i - (NL - 1)) / S);
-    const float d = (v - lv) * (v - lv);
+    const R lv = sizeof(R) == 8 ? (R)((double)(2 * i - (NL - 1)) * (1.0 / S)) : (R)((2.0 * i - (NL - 1)) / S);
+    const R d = (v - lv) * (v - lv);
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
-      if ((i >> (NB - 1 - bb)) & 1) m1[bb] = fminf(m1[bb], d);
-      else m0[bb] = fminf(m0[bb], d);
+      if ((i >> (NB - 1 - bb)) & 1) m1[bb] = fmin(m1[bb], d);
+      else m0[bb] = fmin(m0[bb], d);
     }
   }
 #pragma unroll
-  for (int bb = 0; bb < NB; ++bb) out[bb] = fminf(10.f, fmaxf(-10.f, (m1[bb] - m0[bb]) * inv2nv));
+  for (int bb = 0; bb < NB; ++bb) {
+    const R x = sizeof(R) == 8 ? (m1[bb] - m0[bb]) / q : (m1[bb] - m0[bb]) * q;
+    out[bb] = fmin((R)10, fmax((R)-10, x));
+  }
 }
 
-template <int BPS>
-__device__ __forceinline__ void soft_demap(float2 y, float nv, float* out) {
+template <int BPS, class V>
+__device__ __forceinline__ void soft_demap(V y, re_t<V> nv, re_t<V>* out) {
+  using R = re_t<V>;
   if constexpr (BPS == 2) {
-    out[0] = (2.0f / nv) * y.x * 1.41421356237309515f;
-    out[1] = (2.0f / nv) * y.y * 1.41421356237309515f;
+    const R s2 = sizeof(R) == 8 ? (R)1.4142135623730951 : (R)1.41421356237309515f;
+    out[0] = ((R)2 / nv) * y.x * s2;
+    out[1] = ((R)2 / nv) * y.y * s2;
   } else {
-    const float inv2nv = 1.0f / (2.0f * nv);
-    llr_axis<BPS / 2>(y.x, inv2nv, out);
-    llr_axis<BPS / 2>(y.y, inv2nv, out + BPS / 2);
+    const R q = sizeof(R) == 8 ? (R)2 * nv : (R)1 / ((R)2 * nv);
+    llr_axis<BPS / 2, R>(y.x, q, out);
+    llr_axis<BPS / 2, R>(y.y, q, out + BPS / 2);
   }
 }
 
@@ -120,13 +147,19 @@ __device__ __forceinline__ float2 zf_div(float2 y, float2 h) {
   const float r = 1.0f / (h.x * h.x + h.y * h.y);
   return make_float2((y.x * h.x + y.y * h.y) * r, (y.y * h.x - y.x * h.y) * r);
 }
+// ZF equaliser Y / (H + 1e-6): f32 as above; f64 NumPy's complex division
+// (Smith's algorithm)
+__device__ __forceinline__ float2 zf_eq(float2 y, float2 h) { return zf_div(y, make_float2(h.x + 1e-6f, h.y)); }
+__device__ __forceinline__ double2 zf_eq(double2 y, double2 h) { return cdiv(y, make_double2(h.x + 1e-6, h.y)); }
 
 // Noise-add for one OFDM symbol into LDS, one Philox call per pair of
 // samples (sample n uses half (n&1) of counter n>>1 -- same draws as
 // load_symbol_noisy, at half the generator cost).
-__device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __restrict__ yf, int N, int cp, int l,
-                                                   float sigma, uint64_t seed, uint64_t frame, int rx,
-                                                   const float* __restrict__ zf, int L, int tid, int T) {
+template <class V>
+__device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__ yf, int N, int cp, int l,
+                                                   re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
+                                                   const re_t<V>* __restrict__ zf, int L, int tid, int T) {
+  using R = re_t<V>;
   const int off = l * (N + cp) + cp;
   if (zf) {
     load_symbol_noisy(buf, yf, N, cp, l, sigma, seed, frame, rx, zf, L, tid, T);
@@ -137,12 +170,12 @@ __device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __
   // (the loop was latency bound with one pair in flight); T = N/8 threads
   // cover the N/2 (+1) pairs in at most 5 rounds
   constexpr int MAXR = 5;
-  float2 va[MAXR], vb[MAXR];
+  V va[MAXR], vb[MAXR];
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int p = p0 + tid + i * T, n0 = 2 * p;
-    va[i] = (p <= p1 && n0 >= off) ? yf[n0] : make_float2(0.f, 0.f);
-    vb[i] = (p <= p1 && n0 + 1 < off + N) ? yf[n0 + 1] : make_float2(0.f, 0.f);
+    va[i] = (p <= p1 && n0 >= off) ? yf[n0] : mkc((R)0, (R)0);
+    vb[i] = (p <= p1 && n0 + 1 < off + N) ? yf[n0 + 1] : mkc((R)0, (R)0);
   }
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
@@ -150,12 +183,12 @@ __device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __
     if (p > p1) break;
     const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
     if (n0 >= off) {
-      const float2 z = box_muller(r.x, r.y);
-      buf[n0 - off] = make_float2(va[i].x + sigma * z.x, va[i].y + sigma * z.y);
+      const V z = gauss2<R>(r.x, r.y);
+      buf[n0 - off] = mkc(va[i].x + sigma * z.x, va[i].y + sigma * z.y);
     }
     if (n0 + 1 < off + N) {
-      const float2 z = box_muller(r.z, r.w);
-      buf[n0 + 1 - off] = make_float2(vb[i].x + sigma * z.x, vb[i].y + sigma * z.y);
+      const V z = gauss2<R>(r.z, r.w);
+      buf[n0 + 1 - off] = mkc(vb[i].x + sigma * z.x, vb[i].y + sigma * z.y);
     }
   }
 }
@@ -166,18 +199,20 @@ __device__ __forceinline__ void load_symbol_noisy2(float2* buf, const float2* __
 // w_m = exp(i pi m^2 / M), the convolution by N-point LDS FFTs (N >= 2M - 1
 // since Nd < N/2).  The inverse (IDFTDecodifier) is conj(DFT(conj(x))).  All
 // threads of the block call it; it begins and ends with a barrier.
-__device__ __forceinline__ void dft_bluestein(float2* buf, const Grid& g, int tid, int T, bool active) {
+template <class V>
+__device__ __forceinline__ void dft_bluestein(V* buf, const Grid& g, int tid, int T, bool active) {
+  using G = GridT<re_t<V>>;
   __syncthreads();
   if (active)
-    for (int n = tid; n < g.Nd; n += T) buf[n] = cmul(buf[n], g.chirp[n]);
+    for (int n = tid; n < g.Nd; n += T) buf[n] = cmul(buf[n], G::chirp(g)[n]);
   __syncthreads();
-  fft_lds<false>(buf, g.N, g.log2N, g.tw, tid, active);
+  fft_lds<false>(buf, g.N, g.log2N, G::tw(g), tid, active);
   if (active)
-    for (int k = tid; k < g.N; k += T) buf[k] = cmul(buf[k], g.bhat[k]);
+    for (int k = tid; k < g.N; k += T) buf[k] = cmul(buf[k], G::bhat(g)[k]);
   __syncthreads();
-  fft_lds<true>(buf, g.N, g.log2N, g.tw, tid, active);
+  fft_lds<true>(buf, g.N, g.log2N, G::tw(g), tid, active);
   if (active)
-    for (int k = tid; k < g.Nd; k += T) buf[k] = cmul(buf[k], g.chirp[k]);
+    for (int k = tid; k < g.Nd; k += T) buf[k] = cmul(buf[k], G::chirp(g)[k]);
   __syncthreads();
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/lte_phy.h"
+#include "lte_common.h"
 
 namespace lte {
 
@@ -27,6 +28,28 @@ struct Grid {                 // device pointers + numerology for one plan
   const float2* chirp;        // [Nd] exp(-i pi n^2 / Nd)
   const float2* bhat;         // [N]  FFT_N(exp(+i pi m^2 / Nd), circular) / (N sqrt(Nd))
   int no_eq;                  // uncoded SISO: slice the raw FFT output (enable_equalization=False)
+  // float64 copies of the tables for the f64 chain (null in f32 plans)
+  const double2* pilots64;
+  const double* inv_gap64;
+  const double2* tw64;
+  const double2* chirp64;
+  const double2* bhat64;
+};
+// precision-selected table accessors (R = float / double)
+template <class R> struct GridT;
+template <> struct GridT<float> {
+  __host__ __device__ static const float2* tw(const Grid& g) { return g.tw; }
+  __host__ __device__ static const float2* pilots(const Grid& g) { return g.pilots; }
+  __host__ __device__ static const float* inv_gap(const Grid& g) { return g.inv_gap; }
+  __host__ __device__ static const float2* chirp(const Grid& g) { return g.chirp; }
+  __host__ __device__ static const float2* bhat(const Grid& g) { return g.bhat; }
+};
+template <> struct GridT<double> {
+  __host__ __device__ static const double2* tw(const Grid& g) { return g.tw64; }
+  __host__ __device__ static const double2* pilots(const Grid& g) { return g.pilots64; }
+  __host__ __device__ static const double* inv_gap(const Grid& g) { return g.inv_gap64; }
+  __host__ __device__ static const double2* chirp(const Grid& g) { return g.chirp64; }
+  __host__ __device__ static const double2* bhat(const Grid& g) { return g.bhat64; }
 };
 
 // launchers (return hipError_t as int)
@@ -84,11 +107,12 @@ int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t*
 // of LLRs; same decoder rows as launch_dematch (bps 4 / 6)
 int launch_dematch_zn(hipStream_t s, const float2* z, const float* nv, int n_re, int bps, int B,
                       const int32_t* rx_map, float* const* blk, const int64_t* rows, int g0 = 0);
-int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
-                 int G, int mode);
+// f64 != 0: the float64 decoder (bit-exact with the reference), blk / ckpt hold doubles
+int launch_turbo(hipStream_t s, void* blk, void* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
+                 int G, int mode, int f64);
 struct TurboJob {           // one CB slot of a batch: G groups of 64 code blocks of size K
-  float* blk;
-  float* ck;
+  void* blk;                // float / double rows (lte_decoder.hip)
+  void* ck;
   uint32_t* bits;
   int K, f1, f2, G;
 };
@@ -98,7 +122,11 @@ struct TurboJobs {
   int n;
   int prefix[TURBO_MAX_JOBS + 1];
 };
-int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode);
+int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode, int f64);
+// one float64 BCJR pass of any length n (LogMAPDecoder.decode): app [ncb][n];
+// alpha_scratch n * ncb * 8 doubles
+int launch_bcjr64(hipStream_t s, const double* ls, const double* lp, const double* la, int n, int ncb,
+                  double* alpha_scratch, double* app);
 int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
                      const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
                      uint8_t* cap_bits, int b0 = 0);
@@ -178,8 +206,12 @@ enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3, TM_FINAL = 4 };  // 
 //   [0,K+3) LS (sys + sys1 tail) | [K+3,2K+6) LP1 | [2K+6,3K+9) LP2 | [3K+9,3K+12) LS2T | [3K+12,4K+12) LE
 __host__ __device__ inline int64_t turbo_rows(int K) { return 4LL * K + 12; }
 __host__ __device__ inline int turbo_nwin(int K) { return K / 4 + 1; }  // sized for windows >= 4
-// alpha checkpoint rows per window: states 1..7 (state 0 is 0 after normalisation)
-constexpr int TURBO_CK_ROWS = 7;
+// alpha checkpoint rows per window: f32 states 1..7 (state 0 is 0 after
+// normalisation); f64 all 8 states (unnormalised, as the reference)
+constexpr int TURBO_CK_ROWS_F32 = 7;
+constexpr int TURBO_CK_ROWS_F64 = 8;
+__host__ __device__ inline int turbo_ck_rows(int f64) { return f64 ? TURBO_CK_ROWS_F64 : TURBO_CK_ROWS_F32; }
+constexpr int TURBO_RS = 64;   // decoder row stride (elements): 64 code blocks per wave
 __host__ __device__ inline int turbo_kw(int K) { return (K + 31) / 32; }
 
 }  // namespace lte

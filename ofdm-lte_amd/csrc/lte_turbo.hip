@@ -1,449 +1,14 @@
-// Turbo decoder (max-log BCJR, 8-state RSC) for gfx950.
-//
-// Replaces turbo_decode / LogMAPDecoder (core/channel_coding/turbo_decoder.py:
-// 118-450).  Design:
-//  * one lane = one code block; a wave = 64 code blocks of the same K taken
-//    from 64 consecutive frames.  All state (8 alpha/beta metrics, window of
-//    recomputed alphas) lives in VGPRs -> no cross-lane traffic at all.
-//  * batch-innermost layout [row][64 lanes] per (CB slot r, frame group g):
-//    every load/store of a step is one 256-B coalesced row; the QPP index
-//    pi(k) is wave-uniform (computed incrementally on the scalar unit) so the
-//    interleaved accesses of decoder 2 are coalesced rows too.
-//  * full-length recursion exactly as the reference (no sliding-window
-//    approximation): the forward pass stores alpha checkpoints every TW steps
-//    (states 1..7; state 0 is 0 after normalisation), the backward pass
-//    recomputes each TW-step window from its checkpoint.
-//  * metrics are normalised to state 0 every step (max-log is shift
-//    invariant, so decisions equal the unnormalised float64 reference up to
-//    rounding).
+// Channel-coding kernels around the turbo decoder (lte_decoder.hip) for
+// gfx950: RX rate dematch into the decoder's row layout (with the soft
+// demapper fused in), TX code-block construction + turbo encoding, and the
+// RX CRC-24A / desegmentation / bit-error count.
 #include "lte_common.h"
 #include "lte_internal.h"
 #include "lte_dev.h"
 
 namespace lte {
 
-// gamma for (fb, par, u); c = {g(0,0,0), g(0,0,1), g(0,1,0), g(0,1,1)}.  The
-// other four are exact negations (turbo_decoder.py:305-333 sums +/-L/2 terms).
-__device__ __forceinline__ float gsel(const float c[4], int fb, int par, int u) {
-  return fb == 0 ? c[par * 2 + u] : -c[(1 - par) * 2 + (1 - u)];
-}
-
-// Decoder rows hold LLR/2 (the dematch / host entry points scale by 0.5,
-// exact): those halves ARE the +-L/2 metric terms, so gamma needs no
-// multiplies and alpha, beta and the a-posteriori L are unchanged (LLR units).
-// The extrinsic is stored halved as (L/2 - La/2) - Ls/2, exactly half of
-// (L - La) - Ls (scaling by 2 commutes with rounding).
-__device__ __forceinline__ void gam(float hs, float hp, float ha, float c[4]) {
-  const float sp = hs + hp, sm = hs - hp;
-  c[0] = sp + ha;
-  c[1] = sp - ha;
-  c[2] = sm + ha;
-  c[3] = sm - ha;
-}
-
-// forward recursion (turbo_decoder.py:227-235) + normalisation.
-// State s = 4*s0 + 2*s1 + s2; next = 4*fb + 2*s0 + s1, fb = u^s1^s2,
-// par = fb^s0^s2.  Predecessors of ns=(f,a,b): (a,b,0) with u=f^b, par=f^a and
-// (a,b,1) with u=f^b^1, par=f^a^1.
-__device__ __forceinline__ void fwd(const float a[8], const float c[4], float o[8]) {
-#pragma unroll
-  for (int ns = 0; ns < 8; ++ns) {
-    const int f = ns >> 2, s0 = (ns >> 1) & 1, s1 = ns & 1;
-    const float v0 = a[4 * s0 + 2 * s1] + gsel(c, f, f ^ s0, f ^ s1);
-    const float v1 = a[4 * s0 + 2 * s1 + 1] + gsel(c, f, f ^ s0 ^ 1, f ^ s1 ^ 1);
-    o[ns] = fmaxf(v0, v1);
-  }
-  const float n0 = o[0];
-  o[0] = 0.0f;
-#pragma unroll
-  for (int s = 1; s < 8; ++s) o[s] -= n0;
-}
-
-// backward branch terms (turbo_decoder.py:238-245): t0[s] = beta[next(s,0)] +
-// g(s,0), t1[s] = beta[next(s,1)] + g(s,1) = beta[next(s,0)^4] - g(s,0).
-__device__ __forceinline__ void bterms(const float b[8], const float c[4], float t0[8], float t1[8]) {
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int s0 = s >> 2, s1 = (s >> 1) & 1, s2 = s & 1;
-    const int fb = s1 ^ s2, par = fb ^ s0 ^ s2, ns = 4 * fb + 2 * s0 + s1;
-    const float g = gsel(c, fb, par, 0);
-    t0[s] = b[ns] + g;
-    t1[s] = b[ns ^ 4] - g;
-  }
-}
-
-__device__ __forceinline__ void bnext(const float t0[8], const float t1[8], float b[8]) {
-#pragma unroll
-  for (int s = 0; s < 8; ++s) b[s] = fmaxf(t0[s], t1[s]);
-  const float n0 = b[0];
-  b[0] = 0.0f;
-#pragma unroll
-  for (int s = 1; s < 8; ++s) b[s] -= n0;
-}
-
-// a-posteriori LLR (turbo_decoder.py:250-266)
-__device__ __forceinline__ float llr_app(const float a[8], const float t0[8], const float t1[8]) {
-  float m0 = a[0] + t0[0], m1 = a[0] + t1[0];
-#pragma unroll
-  for (int s = 1; s < 8; ++s) {
-    m0 = fmaxf(m0, a[s] + t0[s]);
-    m1 = fmaxf(m1, a[s] + t1[s]);
-  }
-  return m0 - m1;
-}
-
-// bterms + llr_app + bnext streamed over the states (same operations in the
-// same order, so bit-identical): returns the a-posteriori LLR of this step and
-// advances beta in place, without holding both branch-term vectors.
-__device__ __forceinline__ float bstep(float b[8], const float c[4], const float a[8]) {
-  float bn[8], m0 = 0.0f, m1 = 0.0f;
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int s0 = s >> 2, s1 = (s >> 1) & 1, s2 = s & 1;
-    const int fb = s1 ^ s2, par = fb ^ s0 ^ s2, ns = 4 * fb + 2 * s0 + s1;
-    const float g = gsel(c, fb, par, 0);
-    const float t0 = b[ns] + g, t1 = b[ns ^ 4] - g;
-    if (s == 0) {
-      m0 = a[0] + t0;
-      m1 = a[0] + t1;
-    } else {
-      m0 = fmaxf(m0, a[s] + t0);
-      m1 = fmaxf(m1, a[s] + t1);
-    }
-    bn[s] = fmaxf(t0, t1);
-  }
-  const float n0 = bn[0];
-  b[0] = 0.0f;
-#pragma unroll
-  for (int s = 1; s < 8; ++s) b[s] = bn[s] - n0;
-  return m0 - m1;
-}
-
-__device__ __forceinline__ int modadd(int a, int b, int K) { a += b; return a >= K ? a - K : a; }
-__device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 0 ? a + K : a; }
-
-constexpr int RS = 64;  // row stride (floats): 64 lanes
-constexpr int TW = 8;   // steps per sub-window (recomputed in halves of 4)
-#ifndef LTE_TURBO_SUB
-#define LTE_TURBO_SUB 2
-#endif
-#ifndef LTE_TURBO_HALVES
-#define LTE_TURBO_HALVES 2
-#endif
-#ifndef LTE_TURBO_FINAL_FUSED
-#define LTE_TURBO_FINAL_FUSED 1
-#endif
-constexpr int TSUB = LTE_TURBO_SUB;   // sub-windows per stored alpha checkpoint
-constexpr int SW = TW * TSUB;         // steps per super-window (one checkpoint)
-
-// Buffer-resource row accessor: the 128-bit descriptor (SGPRs) covers one
-// wave's block; a row is addressed by a scalar byte offset (soffset) and the
-// lane by one shared 32-bit VGPR (voffset = 4*lane).  T8/T20 of the CDNA
-// guide: no per-load 64-bit vector addresses, no waterfall loops.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* pu = (void*)(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(pu, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-template <class T>
-struct RowPtr {
-  __amdgpu_buffer_rsrc_t r;
-  int row0;   // first row of this sub-array inside the block
-  int voff;   // 4 * lane
-  __device__ __forceinline__ T ld(int row) const {
-    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(r, voff, (row0 + row) * (RS * 4), 0);
-    if constexpr (sizeof(T) == 4 && (T)0.5f == 0.5f) return __uint_as_float(v);
-    else return (T)v;
-  }
-  __device__ __forceinline__ void st(int row, T v) const {
-    uint32_t u;
-    if constexpr ((T)0.5f == 0.5f) u = __float_as_uint(v);
-    else u = (uint32_t)v;
-    __builtin_amdgcn_raw_buffer_store_b32(u, r, voff, (row0 + row) * (RS * 4), 0);
-  }
-};
-
-// One half-iteration (one constituent decoder pass) for the code block of this lane.
-// All pointers are wave-uniform (scalar) bases; `lane` is the only per-lane
-// offset, so every access is a buffer load/store with a scalar row offset and
-// one shared VGPR lane offset.
-// Forward: alpha over the whole block, checkpoint (states 1..7) every SW = 8 *
-// TSUB steps.  Backward, per super-window of SW steps: load its inputs once
-// into VGPRs, recompute the alphas at each 8-step sub-window start from the
-// checkpoint (kept in VGPRs), then sweep the sub-windows top-down; each
-// sub-window recomputes its alphas in two halves of TH = 4 (first the upper
-// half from alpha(8m+4), then the lower half from the sub-window start), so
-// only 4 alpha vectors are ever live.  Recomputed alphas are bit-identical to
-// the forward pass (same operations, same order).  HBM rows per step: 3 input
-// loads x 2 passes + 1 extrinsic store + 7/SW checkpoint store + 7/SW
-// checkpoint load (TSUB = 2: 7.875 rows, against 8.75 with a checkpoint
-// every 8 steps).
-// MODE TM_FINAL: the decoder-1 a-posteriori pass that ends a decode; it also
-// packs the hard decisions L < 0 MSB-first into `bo` (words [kw][64 lanes]),
-// storing each word as the backward sweep reaches its bit 0 (no re-read pass).
-template <int MODE>
-__device__ __forceinline__ void half_pass(float* __restrict__ wbase, float* __restrict__ wck, int lane, int K,
-                                          int f1, int f2, bool first, uint32_t* __restrict__ bo = nullptr) {
-  constexpr int TH = TW / LTE_TURBO_HALVES;
-  const int vo = lane * 4;
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * 4));
-  const RowPtr<float> LS{rb, 0, vo};
-  const RowPtr<float> LP{rb, ((MODE == TM_DEC2) ? 2 : 1) * (K + 3), vo};
-  const RowPtr<float> LS2T{rb, 3 * K + 9, vo};
-  const RowPtr<float> LE{rb, 3 * K + 12, vo};
-  const RowPtr<float> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * TURBO_CK_ROWS * RS * 4)), 0, vo};
-  const int nsub = K / TW;   // every LTE K is a multiple of 8
-  const int tf2 = (2 * f2) % K;
-  const bool use_la = !first;
-  RowPtr<uint32_t> bout{};
-  uint32_t acc = 0;
-  if (MODE == TM_FINAL) bout = RowPtr<uint32_t>{make_rsrc(bo, (uint32_t)(turbo_kw(K) * RS * 4)), 0, vo};
-
-  // ---------------- forward pass
-  float a[8];
-  a[0] = 0.0f;
-#pragma unroll
-  for (int s = 1; s < 8; ++s) a[s] = LTE_NEG_BIG;
-  int pi = 0, d = (f1 + f2) % K;
-#pragma unroll 1
-  for (int w = 0; w < nsub; ++w) {
-    if (w % TSUB == 0) {
-#pragma unroll
-      for (int s = 1; s < 8; ++s) ck.st((w / TSUB) * TURBO_CK_ROWS + s - 1, a[s]);
-    }
-    float ls[TW], lp[TW], la[TW];
-#pragma unroll
-    for (int j = 0; j < TW; ++j) {
-      const int k = w * TW + j;
-      const int p = (MODE == TM_DEC2) ? pi : k;
-      ls[j] = LS.ld(p);
-      lp[j] = LP.ld(k);
-      la[j] = use_la ? LE.ld(p) : 0.0f;
-      if (MODE == TM_DEC2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
-    }
-#pragma unroll
-    for (int j = 0; j < TW; ++j) {
-      float c[4], o[8];
-      gam(ls[j], lp[j], la[j], c);
-      fwd(a, c, o);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) a[s] = o[s];
-    }
-  }
-
-  // ---------------- backward pass
-  float b[8];
-  b[0] = 0.0f;
-#pragma unroll
-  for (int s = 1; s < 8; ++s) b[s] = LTE_NEG_BIG;
-  // trellis-termination steps k = K+2, K+1, K (only beta is needed there)
-#pragma unroll
-  for (int j = 2; j >= 0; --j) {
-    const int k = K + j;
-    const float ls = (MODE == TM_DEC2) ? LS2T.ld(j) : LS.ld(k);
-    const float lp = LP.ld(k);
-    float c[4], t0[8], t1[8];
-    gam(ls, lp, 0.0f, c);
-    bterms(b, c, t0, t1);
-    bnext(t0, t1, b);
-  }
-  // pi/d are now at k = K (decoder 2); each super-window steps them back to
-  // its start, walks forward while loading and back again while storing
-  const int nsw = (nsub + TSUB - 1) / TSUB;
-#pragma unroll 1
-  for (int q = nsw - 1; q >= 0; --q) {
-    const int ns = min(TSUB, nsub - q * TSUB);   // sub-windows here (wave-uniform)
-    const int k0 = q * SW;
-    if (MODE == TM_DEC2) {
-#pragma unroll 1
-      for (int j = 0; j < ns * TW; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
-    }
-    float ls[SW], lp[SW], la[SW];
-    int pp = pi, dd = d;
-#pragma unroll
-    for (int m = 0; m < TSUB; ++m) {
-      if (m < ns) {
-#pragma unroll
-        for (int j = 0; j < TW; ++j) {
-          const int i = m * TW + j, k = k0 + i;
-          const int p = (MODE == TM_DEC2) ? pp : k;
-          ls[i] = LS.ld(p);
-          lp[i] = LP.ld(k);
-          la[i] = use_la ? LE.ld(p) : 0.0f;
-          if (MODE == TM_DEC2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
-        }
-      }
-    }
-    // alpha at every sub-window start: the checkpoint, then forward
-    float cks[TSUB][8];
-    cks[0][0] = 0.0f;
-#pragma unroll
-    for (int s = 1; s < 8; ++s) cks[0][s] = ck.ld(q * TURBO_CK_ROWS + s - 1);
-#pragma unroll
-    for (int m = 1; m < TSUB; ++m) {
-#pragma unroll
-      for (int s = 0; s < 8; ++s) cks[m][s] = cks[m - 1][s];
-      if (m < ns) {
-#pragma unroll
-        for (int j = 0; j < TW; ++j) {
-          const int i = (m - 1) * TW + j;
-          float c[4], o[8];
-          gam(ls[i], lp[i], la[i], c);
-          fwd(cks[m], c, o);
-#pragma unroll
-          for (int s = 0; s < 8; ++s) cks[m][s] = o[s];
-        }
-      }
-    }
-#pragma unroll
-    for (int m = TSUB - 1; m >= 0; --m) {
-      if (m >= ns) continue;
-#pragma unroll
-      for (int h = LTE_TURBO_HALVES - 1; h >= 0; --h) {
-        // each recompute repeats a chain already run (the lower half: the one
-        // the upper half ran from the sub-window start; the upper half: the
-        // one that produced the next sub-window's start); hide that from CSE
-        // so it is recomputed (cheap VALU) instead of holding alpha vectors live
-#pragma unroll
-        for (int s = 1; s < 8; ++s) asm volatile("" : "+v"(cks[m][s]));
-#pragma unroll
-        for (int j = 0; j < (TSUB > 1 ? TW : TH); ++j)
-          asm volatile("" : "+v"(ls[m * TW + j]), "+v"(lp[m * TW + j]), "+v"(la[m * TW + j]));
-        // A[j] = alpha before step k0 + m*TW + h*TH + j
-        float A[TH][8];
-#pragma unroll
-        for (int s = 0; s < 8; ++s) A[0][s] = cks[m][s];
-        if (h > 0) {
-#pragma unroll
-          for (int j = 0; j < h * TH; ++j) {
-            const int i = m * TW + j;
-            float c[4], o[8];
-            gam(ls[i], lp[i], la[i], c);
-            fwd(A[0], c, o);
-#pragma unroll
-            for (int s = 0; s < 8; ++s) A[0][s] = o[s];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < TH - 1; ++j) {
-          const int i = m * TW + h * TH + j;
-          float c[4];
-          gam(ls[i], lp[i], la[i], c);
-          fwd(A[j], c, A[j + 1]);
-        }
-        // gamma is 7 VALU ops: recompute it below rather than keep the
-        // recompute's 4 gamma vectors live next to the inputs
-#pragma unroll
-        for (int j = 0; j < TH; ++j) {
-          const int i = m * TW + h * TH + j;
-          asm volatile("" : "+v"(ls[i]), "+v"(lp[i]), "+v"(la[i]));
-        }
-#pragma unroll
-        for (int j = TH - 1; j >= 0; --j) {
-          const int i = m * TW + h * TH + j;
-          const int k = k0 + i;
-          float c[4];
-          gam(ls[i], lp[i], la[i], c);
-          const float L = bstep(b, c, A[j]);
-          if (MODE == TM_DEC1) {
-            LE.st(k, (0.5f * L - la[i]) - ls[i]);
-          } else if (MODE == TM_DEC2) {
-            dd = modsub(dd, tf2, K);
-            pp = modsub(pp, dd, K);   // pp = pi(k)
-            LE.st(pp, (0.5f * L - la[i]) - ls[i]);
-          } else if (MODE == TM_APP) {  // a-posteriori LLR in place of the extrinsic row
-            LE.st(k, L);
-          } else {  // TM_FINAL
-            // L is still stored: without a per-step store into the block the
-            // compiler schedules this pass with ~40 more VGPRs
-            LE.st(k, L);
-            acc |= (L < 0.0f ? 1u : 0u) << (31 - (k & 31));
-          }
-        }
-      }
-      if (MODE == TM_FINAL) {   // words start on sub-window boundaries (32 = 4 * TW)
-        const int k = k0 + m * TW;
-        if ((k & 31) == 0) {
-          bout.st(k >> 5, acc);
-          acc = 0;
-        }
-      }
-    }
-    if (MODE == TM_DEC2) { pi = pp; d = dd; }   // back at k0
-  }
-}
-
-// One launch decodes every code-block slot of the batch: wave w -> job r
-// (CB slot, i.e. one K) and frame group g.  256-thread blocks = 4 independent
-// waves (no LDS, no barriers).
-__global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mode) {
-  const int wg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (wg >= jobs.prefix[jobs.n]) return;
-  int r = 0;
-  while (wg >= jobs.prefix[r + 1]) ++r;
-  const TurboJob jb = jobs.j[r];
-  const int g = wg - jobs.prefix[r];
-  const int K = jb.K;
-  float* base = jb.blk + (size_t)g * turbo_rows(K) * RS;
-  float* ck = jb.ck + (size_t)g * (turbo_nwin(K) * TURBO_CK_ROWS) * RS;
-  uint32_t* bo = jb.bits + (size_t)g * turbo_kw(K) * RS;
-  if (mode == TM_APP) {
-    half_pass<TM_APP>(base, ck, lane, K, jb.f1, jb.f2, false);
-    return;
-  }
-  for (int it = 0; it < iters; ++it) {
-    half_pass<TM_DEC1>(base, ck, lane, K, jb.f1, jb.f2, it == 0);
-    half_pass<TM_DEC2>(base, ck, lane, K, jb.f1, jb.f2, false);
-  }
-  // final pass = decoder 1 a-posteriori LLRs (turbo_decoder.py:436-446) and
-  // the hard decisions L < 0, packed MSB-first
-#if LTE_TURBO_FINAL_FUSED
-  half_pass<TM_FINAL>(base, ck, lane, K, jb.f1, jb.f2, iters == 0, bo);
-#else
-  half_pass<TM_APP>(base, ck, lane, K, jb.f1, jb.f2, iters == 0);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(base, (uint32_t)(turbo_rows(K) * RS * 4));
-  const RowPtr<float> LE{rb, 3 * K + 12, lane * 4};
-  const RowPtr<uint32_t> bout{make_rsrc(bo, (uint32_t)(turbo_kw(K) * RS * 4)), 0, lane * 4};
-#pragma unroll 1
-  for (int w = 0; w * 32 < K; ++w) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const int k = w * 32 + i;
-      if (k < K) acc |= (LE.ld(k) < 0.0f ? 1u : 0u) << (31 - i);
-    }
-    bout.st(w, acc);
-  }
-#endif
-}
-
-int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode) {
-  for (int o = 0; o < n; o += TURBO_MAX_JOBS) {
-    TurboJobs J{};
-    J.n = n - o < TURBO_MAX_JOBS ? n - o : TURBO_MAX_JOBS;
-    J.prefix[0] = 0;
-    for (int i = 0; i < J.n; ++i) {
-      J.j[i] = jobs[o + i];
-      J.prefix[i + 1] = J.prefix[i] + jobs[o + i].G;
-    }
-    const int waves = J.prefix[J.n];
-    if (waves == 0) continue;
-    hipLaunchKernelGGL(k_turbo, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
-    const int e = (int)hipGetLastError();
-    if (e) return e;
-  }
-  return 0;
-}
-
-int launch_turbo(hipStream_t s, float* blk, float* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
-                 int G, int mode) {
-  TurboJob j{blk, ckpt, bits, K, f1, f2, G};
-  return launch_turbo_jobs(s, &j, 1, iters, mode);
-}
+constexpr int RS = TURBO_RS;   // decoder row stride (elements): 64 lanes
 
 // ---------------------------------------------------------------------------
 // RX rate-dematch + transpose into the decoder layout.

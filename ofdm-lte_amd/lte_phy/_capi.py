@@ -78,6 +78,8 @@ _SIGS = {
                                              P(ctypes.c_uint8)]),
     'lte_bcjr_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float),
                                      P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_turbo_decode_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(c_f64), P(ctypes.c_uint8)]),
+    'lte_bcjr_host64': (ctypes.c_int, [ctypes.c_int, c_i64, P(c_f64), P(c_f64), P(c_f64), P(c_f64)]),
     'lte_crc_host': (ctypes.c_int, [c_i64, P(ctypes.c_uint8), ctypes.c_uint32, ctypes.c_int,
                                     P(ctypes.c_uint32)]),
     'lte_mimo_detect_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -112,6 +114,19 @@ def load():
                 f.argtypes = args
             _lib = lib
     return _lib
+
+
+PRECISIONS = ('f64', 'f32')
+
+
+def precision(p=None):
+    """Arithmetic type of the GPU chains: 'f64' (the default -- the reference
+    computes in float64 / complex128 throughout) or 'f32' (opt-in fast mode).
+    LTE_PRECISION in the environment changes the default."""
+    p = p or os.environ.get('LTE_PRECISION', 'f64')
+    if p not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {p!r}")
+    return p
 
 
 def check(rc):

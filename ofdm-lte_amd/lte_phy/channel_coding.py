@@ -69,17 +69,25 @@ def turbo_encode(input_bits):
     return out
 
 
-def turbo_decode(llr_encoded, K, num_iterations=5, debug=False):
-    """turbo_decoder.py:338-450 on the GPU (max-log BCJR, float32)."""
-    return turbo_decode_batch(np.asarray(llr_encoded)[None], K, num_iterations)[0]
+def turbo_decode(llr_encoded, K, num_iterations=5, debug=False, precision=None):
+    """turbo_decoder.py:338-450 on the GPU (max-log BCJR).  precision 'f64'
+    (default, bit-exact with the reference) or 'f32' (fast mode)."""
+    return turbo_decode_batch(np.asarray(llr_encoded)[None], K, num_iterations, precision)[0]
 
 
-def turbo_decode_batch(llrs, K, num_iterations=8):
+def turbo_decode_batch(llrs, K, num_iterations=8, precision=None):
     """Decode many code blocks of the same K at once: llrs [ncb][3K+12]."""
     C.device_init()
-    L = np.ascontiguousarray(llrs, dtype=np.float32).reshape(-1, 3 * K + 12)
-    out = np.zeros((L.shape[0], K), dtype=np.uint8)
-    C.check(C.load().lte_turbo_decode_host(K, int(num_iterations), L.shape[0], C.ptr(L, C.F32), C.ptr(out, C.U8)))
+    prec = C.precision(precision)
+    out = np.zeros((np.asarray(llrs).size // (3 * K + 12), K), dtype=np.uint8)
+    if prec == 'f64':
+        L = np.ascontiguousarray(llrs, dtype=np.float64).reshape(-1, 3 * K + 12)
+        C.check(C.load().lte_turbo_decode_host64(K, int(num_iterations), L.shape[0], C.ptr(L, C.F64),
+                                                 C.ptr(out, C.U8)))
+    else:
+        L = np.ascontiguousarray(llrs, dtype=np.float32).reshape(-1, 3 * K + 12)
+        C.check(C.load().lte_turbo_decode_host(K, int(num_iterations), L.shape[0], C.ptr(L, C.F32),
+                                               C.ptr(out, C.U8)))
     return out
 
 

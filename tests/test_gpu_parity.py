@@ -92,6 +92,7 @@ def test_crc24a(C, golden, vec):
 
 
 def test_bcjr_app(C, golden):
+    """f32 fast mode: K + 3 steps through the decoder rows, within f32 round-off."""
     ls, lp, la = golden['bcjr_ls'], golden['bcjr_lp'], golden['bcjr_la']
     K = len(ls) - 3
     app = np.zeros(K, dtype=np.float32)
@@ -102,15 +103,39 @@ def test_bcjr_app(C, golden):
     assert np.array_equal(app < 0, ref < 0)
 
 
+def test_bcjr_app_f64_exact(C, golden, oracle):
+    """float64 LogMAPDecoder.decode (return_extrinsic=False) over all K + 3
+    steps: bit-identical to the reference's output and to the C oracle."""
+    ls, lp, la = (np.ascontiguousarray(golden[k], dtype=np.float64) for k in ('bcjr_ls', 'bcjr_lp', 'bcjr_la'))
+    n = len(ls)
+    app = np.zeros(n)
+    C.check(C.load().lte_bcjr_host64(n, 1, *[C.ptr(v, C.F64) for v in (ls, lp, la)], C.ptr(app, C.F64)))
+    assert np.array_equal(app, golden['bcjr_app'])
+    assert np.array_equal(app, oracle.bcjr_app(ls, lp, la))
+
+
 @pytest.mark.parametrize('K,its', [(40, 8), (1024, 1), (1024, 8), (5568, 2)])
 def test_turbo_decode_golden(C, golden, oracle, K, its):
-    """Kernel == its float32 algorithm bit-for-bit, on the reference's own
-    decoder inputs.  (How that algorithm relates to the float64 reference is
-    pinned on the CPU: tests/test_turbo_model.py.)"""
+    """Default (float64) decoder == the reference's own decoded bits on its own
+    decoder inputs, for every case (north_star: BER match; here exact)."""
+    from lte_phy import channel_coding as cc
+    key = f'td_{K}_{its}'
+    llr = golden[key + '_llr'].astype(np.float64)
+    dec = cc.turbo_decode(llr, K, its)
+    ref = unpack(golden[key + '_dec'], K)
+    assert np.array_equal(dec, ref)
+    assert np.array_equal(dec, oracle.turbo_decode(llr, K, its))
+
+
+@pytest.mark.parametrize('K,its', [(40, 8), (1024, 1), (1024, 8), (5568, 2)])
+def test_turbo_decode_golden_f32(C, golden, oracle, K, its):
+    """f32 fast mode == its float32 algorithm bit-for-bit (how that algorithm
+    relates to the float64 reference is pinned on the CPU:
+    tests/test_turbo_model.py)."""
     from lte_phy import channel_coding as cc
     key = f'td_{K}_{its}'
     llr = golden[key + '_llr'].astype(np.float32)
-    dec = cc.turbo_decode(llr, K, its)
+    dec = cc.turbo_decode(llr, K, its, precision='f32')
     assert np.array_equal(dec, oracle.turbo_decode_f32_model(llr, K, its))
     ref = unpack(golden[key + '_dec'], K)
     if its <= 2 or K == 40:    # converging cases: equal to the reference itself
@@ -120,8 +145,10 @@ def test_turbo_decode_golden(C, golden, oracle, K, its):
 @pytest.mark.parametrize('K,n,snr', [(5568, 130, 1.5), (5632, 70, 3.0), (6144, 64, 5.0), (40, 200, 2.0),
                                      (48, 64, 2.0), (56, 64, 2.0), (1056, 64, 2.5)])
 def test_turbo_decode_batch_vs_oracle(C, oracle, K, n, snr):
-    """Several decoder waves of one K: bit-exact vs the float32 model; where the
-    reference decoder converges (5 dB) also bit-exact vs the float64 oracle."""
+    """Several decoder waves of one K (partial last wave included), below and
+    above the turbo cliff: the float64 decoder is bit-exact vs the float64
+    oracle (= the reference) on every code block; the f32 fast mode is
+    bit-exact vs its float32 model."""
     from lte_phy import channel_coding as cc
     rs = np.random.RandomState(K)
     cbs = rs.randint(0, 2, (n, K)).astype(np.uint8)
@@ -130,13 +157,13 @@ def test_turbo_decode_batch_vs_oracle(C, oracle, K, n, snr):
     for i in range(n):
         s = 1 - 2.0 * oracle.turbo_encode(cbs[i])
         llr[i] = 2 * (s + np.sqrt(s2) * rs.randn(len(s))) / s2
-    llr = llr.astype(np.float32)
     dec = cc.turbo_decode_batch(llr, K, 8)
     for i in range(n):
-        assert np.array_equal(dec[i], oracle.turbo_decode_f32_model(llr[i], K, 8)), i
-    if snr >= 5.0:
-        for i in range(n):
-            assert np.array_equal(dec[i], oracle.turbo_decode(llr[i].astype(np.float64), K, 8)), i
+        assert np.array_equal(dec[i], oracle.turbo_decode(llr[i], K, 8)), i
+    l32 = llr.astype(np.float32)
+    dec = cc.turbo_decode_batch(l32, K, 8, precision='f32')
+    for i in range(n):
+        assert np.array_equal(dec[i], oracle.turbo_decode_f32_model(l32[i], K, 8)), i
 
 
 def _sim(bw, mod, chan):

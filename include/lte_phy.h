@@ -55,6 +55,12 @@ enum {
 enum { LTE_DET_MMSE = 0, LTE_DET_ZF = 1, LTE_DET_SIC = 2, LTE_DET_MRC = 3 };
 enum { LTE_CH_AWGN = 0, LTE_CH_RAYLEIGH = 1 }; /* core/channel.py:10-245 */
 
+/* Arithmetic type of a plan's signal chain and turbo decoder.  DEFAULT =
+ * float64 for the SISO / SIMO chains (uncoded, coded, MRC: the reference
+ * computes in float64 / complex128 throughout) and float32 for the
+ * multi-antenna and beamforming chains, which have no float64 path. */
+enum { LTE_PREC_DEFAULT = 0, LTE_PREC_F32 = 32, LTE_PREC_F64 = 64 };
+
 #define LTE_MAX_PATHS 16
 enum { LTE_STAGE_TX = 1, LTE_STAGE_CHANNEL = 2, LTE_STAGE_RX = 4, LTE_STAGE_ALL = 7 };
 
@@ -99,6 +105,7 @@ typedef struct {
    * enable_equalization=False: receive_and_decode slices the raw FFT output,
    * core/lte_receiver.py:294-299; the CRS estimate still runs) */
   int32_t no_equalization;
+  int32_t precision;       /* LTE_PREC_*                                         */
 } lte_plan_desc;
 
 typedef struct lte_plan lte_plan;
@@ -130,18 +137,21 @@ typedef struct {
    * time-domain TX signal comes from in_signal; without LTE_STAGE_CHANNEL,
    * in_signal is taken as the already-received signal (no fading, no noise). */
   int32_t stages;
-  const float *in_signal; int64_t in_signal_stride; /* [.][L] complex64 */
+  /* in_signal and the real / complex captures below hold the plan's
+   * arithmetic type (lte_plan_precision): float / complex64 (interleaved
+   * float pairs) in f32 plans, double / complex128 in f64 plans. */
+  const void *in_signal; int64_t in_signal_stride; /* [.][L] complex (stride in real elements) */
   /* captures (host, optional; used by the single-call Python API) */
-  float *cap_signal_tx;        /* [n_frames][L] complex64 ([n_frames][num_tx][L] multi-antenna) */
-  float *cap_signal_rx;        /* [n_frames][num_rx][L] complex64 (noisy)           */
-  float *cap_data_syms;        /* [n_frames][n_sym*Nd] complex64 (ZF / MRC / SFBC / MMSE output;
+  void *cap_signal_tx;         /* [n_frames][L] complex ([n_frames][num_tx][L] multi-antenna) */
+  void *cap_signal_rx;         /* [n_frames][num_rx][L] complex (noisy)             */
+  void *cap_data_syms;         /* [n_frames][n_sym*Nd] complex (ZF / MRC / SFBC / MMSE output;
                                   multi-antenna: n_sym*res, res = Nd&~1 SFBC, Nd spatial) */
-  float *cap_H;                /* [n_frames][num_rx][n_grp][N] complex64            */
-  float *cap_pilot_stats;      /* [n_frames][num_rx][n_grp][2] float (P, noise)     */
+  void *cap_H;                 /* [n_frames][num_rx][n_grp][N] complex              */
+  void *cap_pilot_stats;       /* [n_frames][num_rx][n_grp][2] real (P, noise)      */
   uint8_t *cap_bits_rx;        /* [n_frames][n_bits]                                */
-  float *cap_llr;              /* [n_frames][n_sym*Nd*bps] (coded, RE order)        */
-  float *cap_noise_power;      /* [n_frames][num_rx]                                */
-  float *cap_tx_syms;          /* [n_frames][n_sym*Nd] complex64 TX data REs        */
+  void *cap_llr;               /* [n_frames][n_sym*Nd*bps] real (coded, RE order)   */
+  void *cap_noise_power;       /* [n_frames][num_rx] real                           */
+  void *cap_tx_syms;           /* [n_frames][n_sym*Nd] complex TX data REs          */
   /* multi-antenna injection (optional): link noise of transmit_mimo's 100 dB
    * per-link channels [.][num_rx][num_tx][2][L] unit normals; flat spatial
    * link gains [.][num_rx][num_tx][2] (re, im of h ~ CN(0,1)) */
@@ -168,6 +178,8 @@ int lte_plan_create(const lte_plan_desc *desc, lte_plan **out);
 int lte_plan_destroy(lte_plan *plan);
 /* Geometry derived by the plan: [L, n_sym, Nd, Np, n_grp, n_cb, coded_bits, n_re_bits] */
 int lte_plan_info(const lte_plan *plan, int64_t *info8);
+/* Arithmetic type the plan runs in: LTE_PREC_F32 or LTE_PREC_F64. */
+int lte_plan_precision(const lte_plan *plan);
 /* Run the full chain (TX -> channel -> RX (-> turbo)) for one batch of frames. */
 int lte_run(lte_plan *plan, const lte_run_args *args);
 /* Per-kernel device time accumulated by lte_run while timing is on (HIP events
@@ -180,16 +192,20 @@ int lte_timing_reset(lte_plan *plan);
 /* ---- stage entry points (parity tests; host in/out, same device kernels) ---- */
 /* IFFT*sqrt(N) / FFT/sqrt(N): core/modulator.py:242 / core/lte_receiver.py:487 */
 int lte_fft_host(int N, int inverse, int64_t batch, const float *in, float *out);
+int lte_fft_host64(int N, int inverse, int64_t batch, const double *in, double *out);
 /* Pilots: PilotPattern.generate_pilots core/resource_mapper.py:137-152 (MT19937 seed(cell_id) + choice([1,-1])) */
 int lte_pilots(int cell_id, int n, double *out_re_im);
 /* SC-FDM DFT / IDFT of size M (<= 1024): DFTPrecodifier.precoding /
  * IDFTDecodifier.decoding core/dft_precoding.py:66-118, 199-226 (unitary,
  * 1/sqrt(M)); in / out [batch][M] complex64.  Bluestein on the device. */
 int lte_dft_host(int M, int inverse, int64_t batch, const float *in, float *out);
+int lte_dft_host64(int M, int inverse, int64_t batch, const double *in, double *out);
 /* Soft demap: _calculate_llrs_* core/ofdm_core.py:791-923 (bps 2/4/6) */
 int lte_llr_host(int bps, int64_t n, const float *syms, const float *noise_var, float *llr);
+int lte_llr_host64(int bps, int64_t n, const double *syms, const double *noise_var, double *llr);
 /* Hard decision: QAMModulator.symbols_to_bits core/modulator.py:90-112 */
 int lte_hard_host(int bps, int64_t n, const float *syms, uint8_t *bits);
+int lte_hard_host64(int bps, int64_t n, const double *syms, uint8_t *bits);
 /* Turbo encode: turbo_encode core/channel_coding/turbo_encoder.py:214-313 */
 int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t *bits, uint8_t *out /*[ncb][3K+12]*/);
 /* Turbo decode: turbo_decode core/channel_coding/turbo_decoder.py:338-450 */

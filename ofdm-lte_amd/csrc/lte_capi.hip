@@ -254,12 +254,19 @@ std::vector<float2> make_constellation(int bps) {  // modulator.py:28-59
   return c;
 }
 
-std::vector<float2> make_twiddles(int N) {
-  std::vector<float2> t(N);
+std::vector<double2> make_twiddles64(int N) {
+  std::vector<double2> t(N);
   for (int k = 0; k < N; ++k) {
     const double a = -2.0 * M_PI * (double)k / (double)N;
-    t[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+    t[k] = make_double2(std::cos(a), std::sin(a));
   }
+  return t;
+}
+
+std::vector<float2> make_twiddles(int N) {
+  const std::vector<double2> w = make_twiddles64(N);
+  std::vector<float2> t(N);
+  for (int k = 0; k < N; ++k) t[k] = make_float2((float)w[k].x, (float)w[k].y);
   return t;
 }
 
@@ -267,7 +274,7 @@ std::vector<float2> make_twiddles(int N) {
 // chirp[n] = exp(-i pi n^2 / M); bhat = FFT_N(b) / (N sqrt(M)) with the circular
 // b[m] = b[N - m] = exp(+i pi m^2 / M), |m| < M.  Angles reduced with exact
 // integer n^2 mod 2M; the FFT of b is a float64 radix-2 on the host.
-void make_bluestein(int N, int M, std::vector<float2>& chirp, std::vector<float2>& bhat) {
+void make_bluestein64(int N, int M, std::vector<double2>& chirp, std::vector<double2>& bhat) {
   auto w = [M](int64_t m) {
     const int64_t r = (m * m) % (2LL * M);
     const double a = M_PI * (double)r / (double)M;
@@ -276,7 +283,7 @@ void make_bluestein(int N, int M, std::vector<float2>& chirp, std::vector<float2
   chirp.resize(M);
   for (int n = 0; n < M; ++n) {
     const std::complex<double> c = std::conj(w(n));
-    chirp[n] = make_float2((float)c.real(), (float)c.imag());
+    chirp[n] = make_double2(c.real(), c.imag());
   }
   std::vector<std::complex<double>> b(N, 0.0);
   for (int m = 0; m < M; ++m) {
@@ -302,7 +309,16 @@ void make_bluestein(int N, int M, std::vector<float2>& chirp, std::vector<float2
   }
   const double sc = 1.0 / ((double)N * std::sqrt((double)M));
   bhat.resize(N);
-  for (int k = 0; k < N; ++k) bhat[k] = make_float2((float)(b[k].real() * sc), (float)(b[k].imag() * sc));
+  for (int k = 0; k < N; ++k) bhat[k] = make_double2(b[k].real() * sc, b[k].imag() * sc);
+}
+
+void make_bluestein(int N, int M, std::vector<float2>& chirp, std::vector<float2>& bhat) {
+  std::vector<double2> c, b;
+  make_bluestein64(N, M, c, b);
+  chirp.resize(c.size());
+  bhat.resize(b.size());
+  for (size_t i = 0; i < c.size(); ++i) chirp[i] = make_float2((float)c[i].x, (float)c[i].y);
+  for (size_t i = 0; i < b.size(); ++i) bhat[i] = make_float2((float)b[i].x, (float)b[i].y);
 }
 
 void make_pilots(int cell, int n, std::vector<double>& re_im) {
@@ -316,13 +332,33 @@ void make_pilots(int cell, int n, std::vector<double>& re_im) {
   }
 }
 
-struct TableSet {  // device copies of the static grid tables for one N
+struct TableSet {  // device copies of the static grid tables for one N (f64 copies in f64 plans)
   DBuf<int32_t> data, pilot, seg;
   DBuf<float> inv_gap;
   DBuf<float2> pilots, tw, constel, chirp, bhat;
+  DBuf<double> inv_gap64;
+  DBuf<double2> pilots64, tw64, chirp64, bhat64;
   void release() {
     data.release(); pilot.release(); seg.release(); inv_gap.release(); pilots.release(); tw.release();
     constel.release(); chirp.release(); bhat.release();
+    inv_gap64.release(); pilots64.release(); tw64.release(); chirp64.release(); bhat64.release();
+  }
+};
+
+// per-precision device buffers of the signal chains (R = float / double)
+template <class R>
+struct ChainBufs {
+  DBuf<cx<R>> x, y, coef, H, capbuf, captx, xh;
+  DBuf<R> gains, phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
+  std::vector<DBuf<R>> blk, ckpt;
+  DBuf<R*> blk_ptrs;
+  void release() {
+    x.release(); y.release(); coef.release(); H.release(); capbuf.release(); captx.release(); xh.release();
+    gains.release(); phases.release(); pow_part.release(); pstats.release(); npow.release(); llr.release();
+    snr_lin.release(); inj_ph.release(); inj_z.release();
+    for (auto& b : blk) b.release();
+    for (auto& b : ckpt) b.release();
+    blk_ptrs.release();
   }
 };
 
@@ -342,24 +378,26 @@ enum { KN_PAYLOAD, KN_ENCODE, KN_OFDM_TX, KN_FADING, KN_CHANNEL, KN_RX_CHEST, KN
 
 // ------------------------------------------------------------------ capture kernel
 namespace lte {
-__global__ void k_cap_rx(int L, int num_rx, int B, const float2* __restrict__ y, int64_t y_rx_stride,
-                         int64_t y_frame_stride, const float* __restrict__ npow, const uint64_t* __restrict__ fid,
-                         uint64_t seed, const float* __restrict__ inj_z, int64_t inj_stride, float2* __restrict__ out) {
+// received stream with its noise, as the reference returns it (signal + noise)
+template <class R>
+__global__ void k_cap_rx(int L, int num_rx, int B, const cx<R>* __restrict__ y, int64_t y_rx_stride,
+                         int64_t y_frame_stride, const R* __restrict__ npow, const uint64_t* __restrict__ fid,
+                         uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride, cx<R>* __restrict__ out) {
   const int nb = (L + 255) / 256;
   const int n = (blockIdx.x % nb) * blockDim.x + threadIdx.x;
   const int rx = blockIdx.y, b = blockIdx.x / nb;
   if (n >= L) return;
-  const float sigma = sqrtf(npow[(size_t)b * num_rx + rx] * 0.5f);
-  float2 z;
+  const R sigma = sqrt(npow[(size_t)b * num_rx + rx] / (R)2);
+  cx<R> z;
   if (inj_z) {
-    const float* zf = inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * L;
-    z = make_float2(zf[n], zf[L + n]);
+    const R* zf = inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * L;
+    z = mkc(zf[n], zf[L + n]);
   } else {
     const u32x4 r = rng4(seed, fid[b], RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)(n >> 1));
-    z = (n & 1) ? box_muller(r.z, r.w) : box_muller(r.x, r.y);
+    z = (n & 1) ? gauss2<R>(r.z, r.w) : gauss2<R>(r.x, r.y);
   }
-  const float2 v = y[b * y_frame_stride + rx * y_rx_stride + n];
-  out[((size_t)b * num_rx + rx) * L + n] = make_float2(v.x + sigma * z.x, v.y + sigma * z.y);
+  const cx<R> v = y[b * y_frame_stride + rx * y_rx_stride + n];
+  out[((size_t)b * num_rx + rx) * L + n] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
 }
 }  // namespace lte
 
@@ -372,27 +410,21 @@ struct lte_plan {
   TableSet tabs;
   Grid grid;
   hipStream_t stream = nullptr;
-  // pipelined coded SISO chain: decoder-side stream + one event per chunk (+ join)
-  hipStream_t stream2 = nullptr;
-  std::vector<hipEvent_t> pipe_ev;
-  DBuf<float2> xh;   // fused TX + channel: per-symbol head / tail TX samples
+  int f64 = 0;                       // signal chain + decoder in float64 (SISO / SIMO chains)
+  int n_layers = 1;                  // rx_map layers (> 1: rate-matching repetition, E > N_cb)
   std::vector<CbInfo> cbs;
-  std::vector<float> gains_f;
   // device
   DBuf<CbInfo> cbi;
   DBuf<int32_t> tx_map, rx_map, delays;
-  DBuf<float> gains;
   DBuf<uint32_t> pw, enc, enc_cw, inj_bits;
-  DBuf<float2> x, y, coef, H, capbuf, captx;
-  DBuf<float> phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
+  ChainBufs<float> c32;              // f32 plans (and every multi-antenna chain)
+  ChainBufs<double> c64;             // f64 plans
   DBuf<uint32_t> frame_err, frame_crc;
   DBuf<int32_t> snr_idx;
   DBuf<uint64_t> fid;
   DBuf<unsigned long long> counts;
   DBuf<uint8_t> cap_bits;
-  std::vector<DBuf<float>> blk, ckpt;
   std::vector<DBuf<uint32_t>> decb;
-  DBuf<float*> blk_ptrs;
   DBuf<int64_t> rows_dev;
   DBuf<uint32_t*> dec_ptrs;
   DBuf<int> kw_dev;
@@ -441,6 +473,10 @@ struct Timer {  // brackets one launch with events when timing is on
     p->evuse.push_back({id, e0});
   }
 };
+
+template <class R> ChainBufs<R>& cbuf(lte_plan* p);
+template <> ChainBufs<float>& cbuf<float>(lte_plan* p) { return p->c32; }
+template <> ChainBufs<double>& cbuf<double>(lte_plan* p) { return p->c64; }
 
 void collect_timing(lte_plan* p) {
   for (auto& u : p->evuse) {
@@ -545,7 +581,7 @@ int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int3
   ok = ok && launch_npow(nullptr, 1, num_rx, dpp.p, channel_nblk((int)L), (int)L, dsl.p, dnp.p) == 0;
   if (ok) {
     const float2* ys = ray ? dy.p : dx.p;
-    hipLaunchKernelGGL(k_cap_rx, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
+    hipLaunchKernelGGL(k_cap_rx<float>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
                        1, ys, ray ? L : 0, ray ? (int64_t)num_rx * L : L, dnp.p, dfid.p, seed,
                        noise ? dz.p : nullptr, 0, dout.p);
     ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
@@ -627,7 +663,7 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
                               mode == 0 ? 1.0f / num_tx : 1.0f,
                               dnp.p) == 0;
   if (ok) {
-    hipLaunchKernelGGL(k_cap_rx, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
+    hipLaunchKernelGGL(k_cap_rx<float>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
                        dy.p, (int64_t)L, (int64_t)num_rx * L, dnp.p, dfid.p, seed, noise ? dz.p : nullptr, 0,
                        dout.p);
     ok = hipGetLastError() == hipSuccess;
@@ -721,6 +757,20 @@ static int plan_tables(lte_plan* p) {
     make_bluestein(d.N, p->Nd, ch, bh);
     if (upload(p->tabs.chirp, ch) || upload(p->tabs.bhat, bh)) return fail(LTE_ENOMEM, "table upload failed");
   }
+  if (p->f64) {   // float64 copies for the f64 chain
+    std::vector<double2> pil64(p->Np);
+    for (int i = 0; i < p->Np; ++i) pil64[i] = make_double2(pr[2 * i], pr[2 * i + 1]);
+    std::vector<double> ig64(std::max(p->Np, 1), 0.0);
+    for (int i = 0; i + 1 < p->Np; ++i) ig64[i] = 1.0 / (double)(p->gh.pilot[i + 1] - p->gh.pilot[i]);
+    if (upload(p->tabs.pilots64, pil64) || upload(p->tabs.inv_gap64, ig64) ||
+        upload(p->tabs.tw64, make_twiddles64(d.N)))
+      return fail(LTE_ENOMEM, "table upload failed");
+    if (d.sc_fdm) {
+      std::vector<double2> ch, bh;
+      make_bluestein64(d.N, p->Nd, ch, bh);
+      if (upload(p->tabs.chirp64, ch) || upload(p->tabs.bhat64, bh)) return fail(LTE_ENOMEM, "table upload failed");
+    }
+  }
   return LTE_OK;
 }
 
@@ -753,7 +803,15 @@ static int plan_coded_maps(lte_plan* p) {
     while (e >= Eoff[r + 1]) ++r;
     i = e - Eoff[r];
   };
-  std::vector<int32_t> txm(p->n_re_bits), rxm(p->n_re_bits);
+  // rx_map layers: LLR i of CB r goes to layer i / N_cb (E > N_cb repeats the
+  // circular buffer; rate_dematching_turbo sums the repeats in order of i)
+  int layers = 1;
+  for (int r = 0; r < p->C; ++r) {
+    const int ncb = 3 * (p->cbs[r].K + 6);
+    layers = std::max(layers, (p->cbs[r].E + ncb - 1) / ncb);
+  }
+  p->n_layers = layers;
+  std::vector<int32_t> txm(p->n_re_bits), rxm((size_t)layers * p->n_re_bits, -1);
   for (int re = 0; re < n_re; ++re) {
     // TX: interleaved position re <- padded coded symbol q (ofdm_core.py:1046-1060)
     const int c = re / rows, rr = re % rows;
@@ -782,27 +840,21 @@ static int plan_coded_maps(lte_plan* p) {
       if (qr >= ncs_rx) qr = -1;
     }
     for (int m = 0; m < bps; ++m) {
-      int32_t v = -1;
-      if (qr >= 0) {
-        const int e = qr * bps + m;
-        if (e < p->coded_len) {
-          int r, i;
-          locate(e, r, i);
-          const int K = p->cbs[r].K;
-          const RmSrc s = rs[r][i];
-          int row = -1;
-          if (s.stream == 0) row = s.idx < K + 3 ? s.idx : 3 * K + 9 + (s.idx - K - 3);
-          else if (s.stream == 1) row = K + 3 + s.idx;
-          else if (s.stream == 2) row = 2 * K + 6 + s.idx;
-          if (row >= 0) v = (r << 24) | row;
-        }
-      }
-      rxm[(size_t)re * bps + m] = v;
-      (void)base;
+      if (qr < 0) continue;
+      const int e = qr * bps + m;
+      if (e >= p->coded_len) continue;
+      int r, i;
+      locate(e, r, i);
+      const int K = p->cbs[r].K;
+      const RmSrc s = rs[r][i];
+      int row = -1;
+      if (s.stream == 0) row = s.idx < K + 3 ? s.idx : 3 * K + 9 + (s.idx - K - 3);
+      else if (s.stream == 1) row = K + 3 + s.idx;
+      else if (s.stream == 2) row = 2 * K + 6 + s.idx;
+      if (row >= 0) rxm[(size_t)(i / (3 * (K + 6))) * p->n_re_bits + (size_t)re * bps + m] = (r << 24) | row;
     }
+    (void)base;
   }
-  for (int r = 0; r < p->C; ++r)
-    if (p->cbs[r].E > 3 * (p->cbs[r].K + 6)) return fail(LTE_EUNSUP, "rate-matching repetition not supported");
   if (upload(p->tx_map, txm) || upload(p->rx_map, rxm) || upload(p->cbi, p->cbs))
     return fail(LTE_ENOMEM, "map upload failed");
   return LTE_OK;
@@ -855,6 +907,53 @@ static int plan_mimo_tables(lte_plan* p) {
   return LTE_OK;
 }
 
+}  // extern "C"
+
+// Device workspace of the SISO / SIMO chains in precision R.  The TX signal x
+// is allocated on first use (the fused TX + channel path never writes it).
+template <class R>
+static bool alloc_siso(lte_plan* p, bool coded) {
+  const lte_plan_desc& d = p->d;
+  ChainBufs<R>& c = cbuf<R>(p);
+  const size_t B = (size_t)d.max_frames;
+  const int G = (int)((B + 63) / 64);
+  const int rx = d.num_rx;
+  const bool ray = d.channel == LTE_CH_RAYLEIGH;
+  bool bad = false;
+  if (ray) {
+    bad |= c.y.alloc(B * rx * p->L) != 0;
+    bad |= c.phases.alloc(std::max<size_t>(B * rx * d.n_paths * 16, 1)) != 0;
+    bad |= c.coef.alloc(std::max<size_t>(B * rx * d.n_paths, 1)) != 0;
+    std::vector<R> gh(d.gains, d.gains + d.n_paths);
+    bad |= upload(c.gains, gh) != 0;
+  }
+  bad |= c.pow_part.alloc(B * rx * p->nblk) != 0;
+  bad |= c.H.alloc(B * rx * p->n_grp * d.N) != 0;
+  bad |= c.pstats.alloc(B * rx * p->n_grp * 2) != 0;
+  bad |= c.npow.alloc(B * rx) != 0;
+  bad |= c.snr_lin.alloc(B) != 0;
+  if (coded) {
+    // the fused demap path keeps (z, nv) = 3 R per RE here; the LLR path
+    // (captures, QPSK) grows it to bps R per RE on first use
+    const size_t n_re = p->n_re_bits / d.bps;
+    bad |= c.llr.alloc(B * (d.bps >= 4 ? 3 * n_re : (size_t)p->n_re_bits)) != 0;
+    c.blk.resize(p->C);
+    c.ckpt.resize(p->C);
+    std::vector<R*> bp(p->C);
+    for (int r = 0; r < p->C; ++r) {
+      const int K = p->cbs[r].K;
+      bad |= c.blk[r].alloc((size_t)G * turbo_rows(K) * 64) != 0;
+      bad |= c.ckpt[r].alloc((size_t)G * turbo_nwin(K) * turbo_ck_rows(sizeof(R) == 8) * 64) != 0;
+      if (!bad && hipMemset(c.blk[r].p, 0, c.blk[r].n * sizeof(R)) != hipSuccess) bad = true;
+      bp[r] = c.blk[r].p;
+    }
+    if (!bad) bad |= upload(c.blk_ptrs, bp) != 0;
+  }
+  return !bad;
+}
+
+extern "C" {
+
 static int plan_alloc(lte_plan* p) {
   const lte_plan_desc& d = p->d;
   const size_t B = (size_t)d.max_frames;
@@ -864,36 +963,47 @@ static int plan_alloc(lte_plan* p) {
   const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
   bool bad = false;
   bad |= p->pw.alloc(B * p->PW) != 0;
-  if (p->mimo) {
-    const MimoGrid& m = p->mg;
-    const size_t links = (size_t)m.num_rx * m.num_tx;
-    const int np = ray ? d.n_paths : 1;
-    bad |= p->x.alloc(B * m.num_tx * p->L) != 0;
-    bad |= p->y.alloc(B * m.num_rx * p->L) != 0;
-    bad |= p->coef.alloc(B * links * np * m.n_cs * 3) != 0;
-    if (ray && d.chain != LTE_CHAIN_SPATIAL) {
-      bad |= p->link_part.alloc(B * links * p->nblk) != 0;
-      bad |= p->link_sigma.alloc(B * links) != 0;
+  if (p->mimo || p->bf) {   // float32 chains
+    ChainBufs<float>& c = p->c32;
+    if (p->mimo) {
+      const MimoGrid& m = p->mg;
+      const size_t links = (size_t)m.num_rx * m.num_tx;
+      bad |= c.x.alloc(B * m.num_tx * p->L) != 0;
+      bad |= c.y.alloc(B * m.num_rx * p->L) != 0;
+      bad |= c.coef.alloc(B * links * (ray ? d.n_paths : 1) * m.n_cs * 3) != 0;
+      if (ray && d.chain != LTE_CHAIN_SPATIAL) {
+        bad |= p->link_part.alloc(B * links * p->nblk) != 0;
+        bad |= p->link_sigma.alloc(B * links) != 0;
+      }
+      bad |= p->Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
+      bad |= p->Hm.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
+      if (ray) {
+        std::vector<float> gh(d.gains, d.gains + d.n_paths);
+        bad |= upload(c.gains, gh) != 0;
+      }
+    } else {
+      bad |= p->bf_fr.alloc(B) != 0;
     }
-    bad |= p->Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
-    bad |= p->Hm.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
-  } else if (p->bf) {
-    bad |= p->bf_fr.alloc(B) != 0;
+    bad |= c.pow_part.alloc(B * rx * p->nblk) != 0;
+    bad |= c.npow.alloc(B * rx) != 0;
+    bad |= c.snr_lin.alloc(B) != 0;
+    if (coded) {
+      bad |= c.llr.alloc(B * p->n_re_bits) != 0;
+      c.blk.resize(p->C);
+      c.ckpt.resize(p->C);
+      std::vector<float*> bp(p->C);
+      for (int r = 0; r < p->C; ++r) {
+        const int K = p->cbs[r].K;
+        bad |= c.blk[r].alloc((size_t)G * turbo_rows(K) * 64) != 0;
+        bad |= c.ckpt[r].alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS_F32 * 64) != 0;
+        if (!bad) HIPCHK(hipMemset(c.blk[r].p, 0, c.blk[r].n * sizeof(float)));
+        bp[r] = c.blk[r].p;
+      }
+      if (!bad) bad |= upload(c.blk_ptrs, bp) != 0;
+    }
   } else {
-    bad |= p->x.alloc(B * p->L) != 0;
+    bad |= !(p->f64 ? alloc_siso<double>(p, coded) : alloc_siso<float>(p, coded));
   }
-  if (ray && !p->mimo) {
-    bad |= p->y.alloc(B * rx * p->L) != 0;
-    bad |= p->phases.alloc(std::max<size_t>(B * rx * d.n_paths * 16, 1)) != 0;
-    bad |= p->coef.alloc(std::max<size_t>(B * rx * d.n_paths, 1)) != 0;
-  }
-  bad |= p->pow_part.alloc(B * rx * p->nblk) != 0;
-  if (!p->mimo && !p->bf) {
-    bad |= p->H.alloc(B * rx * p->n_grp * d.N) != 0;
-    bad |= p->pstats.alloc(B * rx * p->n_grp * 2) != 0;
-  }
-  bad |= p->npow.alloc(B * rx) != 0;
-  bad |= p->snr_lin.alloc(B) != 0;
   bad |= p->snr_idx.alloc(B) != 0;
   bad |= p->fid.alloc(B) != 0;
   bad |= p->frame_err.alloc(B) != 0;
@@ -901,27 +1011,18 @@ static int plan_alloc(lte_plan* p) {
   if (coded) {
     bad |= p->enc.alloc(B * p->enc_words) != 0;
     bad |= p->enc_cw.alloc(encode_scratch_words(p->KWmax, p->C, (int)B)) != 0;
-    bad |= p->llr.alloc(B * p->n_re_bits) != 0;
-    p->blk.resize(p->C);
-    p->ckpt.resize(p->C);
     p->decb.resize(p->C);
-    std::vector<float*> bp(p->C);
     std::vector<int64_t> rows(p->C);
     std::vector<uint32_t*> dp(p->C);
     std::vector<int> kw(p->C);
     for (int r = 0; r < p->C; ++r) {
       const int K = p->cbs[r].K;
       rows[r] = turbo_rows(K);
-      bad |= p->blk[r].alloc((size_t)G * rows[r] * 64) != 0;
-      bad |= p->ckpt[r].alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS_F32 * 64) != 0;
       kw[r] = turbo_kw(K);
       bad |= p->decb[r].alloc((size_t)G * kw[r] * 64) != 0;
-      if (!bad) HIPCHK(hipMemset(p->blk[r].p, 0, p->blk[r].n * sizeof(float)));
-      bp[r] = p->blk[r].p;
       dp[r] = p->decb[r].p;
     }
-    if (!bad) bad |= upload(p->blk_ptrs, bp) || upload(p->rows_dev, rows) || upload(p->dec_ptrs, dp) ||
-                     upload(p->kw_dev, kw);
+    if (!bad) bad |= upload(p->rows_dev, rows) || upload(p->dec_ptrs, dp) || upload(p->kw_dev, kw);
   }
   if (bad) return fail(LTE_ENOMEM, "device workspace allocation failed (max_frames too large?)");
   return LTE_OK;
@@ -963,10 +1064,17 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
     return fail(LTE_EINVAL, "bad n_paths");
   if (d.max_frames < 1) return fail(LTE_EINVAL, "max_frames must be >= 1");
   if (d.n_bits < 1) return fail(LTE_EINVAL, "Bits array cannot be empty");
+  if (d.precision != LTE_PREC_DEFAULT && d.precision != LTE_PREC_F32 && d.precision != LTE_PREC_F64)
+    return fail(LTE_EINVAL, "precision must be LTE_PREC_DEFAULT, LTE_PREC_F32 or LTE_PREC_F64");
+  // float64 (the reference's arithmetic) is the default of the SISO / SIMO
+  // chains; the multi-antenna and beamforming chains compute in float32
+  if ((mimo || bf) && d.precision == LTE_PREC_F64)
+    return fail(LTE_EUNSUP, "the multi-antenna and beamforming chains compute in float32 (LTE_PREC_F32)");
   lte_plan* p = new lte_plan();
   p->d = d;
   p->d.num_tx = num_tx;
   p->mimo = mimo;
+  p->f64 = !(mimo || bf) && d.precision != LTE_PREC_F32;
   const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
   if (coded && d.turbo_iters < 0) { delete p; return fail(LTE_EINVAL, "bad turbo_iters"); }
   int rc = plan_tables(p);
@@ -1043,15 +1151,13 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
                  p->tabs.data.p, p->tabs.pilot.p, p->tabs.pilots.p, p->tabs.seg.p, p->tabs.inv_gap.p,
                  p->tabs.tw.p, p->tabs.constel.p,
                  (float)(d.bps == 2 ? std::sqrt(2.0) : d.bps == 4 ? std::sqrt(10.0) : std::sqrt(42.0)),
-                 p->tabs.chirp.p, p->tabs.bhat.p, d.no_equalization && d.chain == LTE_CHAIN_UNCODED ? 1 : 0};
+                 p->tabs.chirp.p, p->tabs.bhat.p, d.no_equalization && d.chain == LTE_CHAIN_UNCODED ? 1 : 0,
+                 p->tabs.pilots64.p, p->tabs.inv_gap64.p, p->tabs.tw64.p, p->tabs.chirp64.p, p->tabs.bhat64.p};
   if (d.channel == LTE_CH_RAYLEIGH) {
     std::vector<int32_t> dl(d.delays, d.delays + d.n_paths);
-    p->gains_f.assign(d.n_paths, 0.f);
-    for (int i = 0; i < d.n_paths; ++i) {
-      if (dl[i] < 0) { delete p; return fail(LTE_EINVAL, "negative delay"); }
-      p->gains_f[i] = (float)d.gains[i];
-    }
-    if (upload(p->delays, dl) || upload(p->gains, p->gains_f)) { delete p; return fail(LTE_ENOMEM, "upload"); }
+    for (int i = 0; i < d.n_paths; ++i)
+      if (dl[i] < 0) { p->tabs.release(); delete p; return fail(LTE_EINVAL, "negative delay"); }
+    if (upload(p->delays, dl)) { p->tabs.release(); delete p; return fail(LTE_ENOMEM, "upload"); }
   }
   if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
     delete p;
@@ -1068,24 +1174,17 @@ int lte_plan_destroy(lte_plan* p) {
   if (!p) return LTE_OK;
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   p->tabs.release();
-  p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release(); p->gains.release();
+  p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release();
   p->pw.release(); p->enc.release(); p->enc_cw.release(); p->inj_bits.release();
-  p->x.release(); p->y.release(); p->coef.release(); p->H.release(); p->capbuf.release(); p->captx.release();
-  p->phases.release(); p->pow_part.release(); p->pstats.release(); p->npow.release(); p->llr.release();
-  p->snr_lin.release(); p->inj_ph.release(); p->inj_z.release();
+  p->c32.release(); p->c64.release();
   p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->fid.release(); p->counts.release();
   p->cap_bits.release();
-  for (auto& b : p->blk) b.release();
-  for (auto& b : p->ckpt) b.release();
   for (auto& b : p->decb) b.release();
-  p->blk_ptrs.release(); p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
+  p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
   p->m_np.release(); p->m_ppos.release(); p->m_pseg.release(); p->m_pval.release(); p->Ym.release();
   p->Hm.release(); p->m_pig.release(); p->link_part.release(); p->link_sigma.release(); p->inj_lz.release();
   p->inj_lh.release(); p->m_W.release(); p->bf_cb.release(); p->bf_fr.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
-  p->xh.release();
-  for (auto e : p->pipe_ev) (void)hipEventDestroy(e);
-  if (p->stream2) (void)hipStreamDestroy(p->stream2);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
   return LTE_OK;
@@ -1096,6 +1195,11 @@ int lte_plan_info(const lte_plan* p, int64_t* info) {
   info[0] = p->L; info[1] = p->n_sym; info[2] = p->Nd; info[3] = p->Np;
   info[4] = p->n_grp; info[5] = p->C; info[6] = p->coded_len; info[7] = p->n_re_bits;
   return LTE_OK;
+}
+
+int lte_plan_precision(const lte_plan* p) {
+  if (!p) return fail(LTE_EINVAL, "null plan");
+  return p->f64 ? LTE_PREC_F64 : LTE_PREC_F32;
 }
 
 int lte_timing_enable(lte_plan* p, int on) {
@@ -1186,32 +1290,32 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   {
     Timer t(p, KN_OFDM_TX);
-    LCHK(launch_ofdm_tx_mimo(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B));
+    LCHK(launch_ofdm_tx_mimo(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->c32.x.p, B));
   }
   const int np = ray ? d.n_paths : 1;
   {
     Timer t(p, KN_FADING);
-    LCHK(launch_fading_mimo(s, g, m, B, ray ? 1 : 0, d.n_paths, p->gains.p, d.fD, d.fs, p->fid.p, a->seed, inj_ph,
-                            inj_ph_stride, inj_lh, inj_lh_stride, p->coef.p));
+    LCHK(launch_fading_mimo(s, g, m, B, ray ? 1 : 0, d.n_paths, p->c32.gains.p, d.fD, d.fs, p->fid.p, a->seed, inj_ph,
+                            inj_ph_stride, inj_lh, inj_lh_stride, p->c32.coef.p));
   }
   {
     Timer t(p, KN_CHANNEL);
-    LCHK(launch_channel_mimo(s, g, m, B, np, ray ? p->delays.p : nullptr, p->coef.p, p->x.p, p->y.p,
+    LCHK(launch_channel_mimo(s, g, m, B, np, ray ? p->delays.p : nullptr, p->c32.coef.p, p->c32.x.p, p->c32.y.p,
                              link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, p->link_part.p,
-                             p->link_sigma.p, p->pow_part.p, p->nblk));
+                             p->link_sigma.p, p->c32.pow_part.p, p->nblk));
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
-    LCHK(launch_npow_mimo(s, B, m.num_rx, p->pow_part.p, mimo_channel_nblk(p->L, g.N + g.cp), p->L, p->snr_lin.p,
-                          sfbc ? 1.0f / (float)m.num_tx : 1.0f, p->npow.p));
+    LCHK(launch_npow_mimo(s, B, m.num_rx, p->c32.pow_part.p, mimo_channel_nblk(p->L, g.N + g.cp), p->L, p->c32.snr_lin.p,
+                          sfbc ? 1.0f / (float)m.num_tx : 1.0f, p->c32.npow.p));
   }
   {
     Timer t(p, KN_RX_CHEST);
-    LCHK(launch_rx_fft_mimo(s, g, m, B, p->y.p, p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, p->Ym.p, p->Hm.p));
+    LCHK(launch_rx_fft_mimo(s, g, m, B, p->c32.y.p, p->c32.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, p->Ym.p, p->Hm.p));
   }
   float2* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
   if (a->cap_data_syms) {
-    if (p->capbuf.alloc((size_t)B * p->n_sym * m.res)) return fail(LTE_ENOMEM, "capture");
-    cap_syms_dev = p->capbuf.p;
+    if (p->c32.capbuf.alloc((size_t)B * p->n_sym * m.res)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = p->c32.capbuf.p;
   }
   if (a->cap_bits_rx) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
@@ -1220,22 +1324,22 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   {
     Timer t(p, KN_RX_DATA);
     if (sfbc)
-      LCHK(launch_det_sfbc(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, p->Ym.p, p->Hm.p, p->snr_lin.p, p->pw.p, p->PW,
-                           d.n_bits, p->frame_err.p, p->llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev));
+      LCHK(launch_det_sfbc(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, p->Ym.p, p->Hm.p, p->c32.snr_lin.p, p->pw.p, p->PW,
+                           d.n_bits, p->frame_err.p, p->c32.llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev));
     else
-      LCHK(launch_det_spatial(s, g, m, B, p->Ym.p, p->Hm.p, p->snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+      LCHK(launch_det_spatial(s, g, m, B, p->Ym.p, p->Hm.p, p->c32.snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
                               cap_syms_dev, cap_bits_dev));
   }
   if (coded) {
     {
       Timer t(p, KN_DEMATCH);
-      LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
+      LCHK(launch_dematch(s, p->c32.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, p->c32.blk_ptrs.p, p->rows_dev.p));
     }
     const int G = (B + 63) / 64;
     std::vector<TurboJob> jobs(p->C);
     for (int r = 0; r < p->C; ++r) {
       const CbInfo& c = p->cbs[r];
-      jobs[r] = TurboJob{p->blk[r].p, p->ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, G};
+      jobs[r] = TurboJob{p->c32.blk[r].p, p->c32.ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, G};
     }
     {
       Timer t(p, KN_TURBO);
@@ -1261,15 +1365,15 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     HIPCHK(hipMemcpyAsync(crc.data(), p->frame_crc.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   }
   if (a->cap_signal_tx)
-    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, p->x.p, (size_t)B * m.num_tx * p->L * sizeof(float2),
+    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, p->c32.x.p, (size_t)B * m.num_tx * p->L * sizeof(float2),
                           hipMemcpyDeviceToHost, s));
   if (a->cap_signal_rx) {
     DBuf<float2> tmp;
     if (tmp.alloc((size_t)B * m.num_rx * p->L)) return fail(LTE_ENOMEM, "capture");
     {
       Timer t(p, KN_CAP);
-      hipLaunchKernelGGL(k_cap_rx, dim3(((p->L + 255) / 256) * B, m.num_rx), dim3(256), 0, s, p->L, m.num_rx, B,
-                         p->y.p, (int64_t)p->L, (int64_t)m.num_rx * p->L, p->npow.p, p->fid.p, a->seed, inj_z,
+      hipLaunchKernelGGL(k_cap_rx<float>, dim3(((p->L + 255) / 256) * B, m.num_rx), dim3(256), 0, s, p->L, m.num_rx, B,
+                         p->c32.y.p, (int64_t)p->L, (int64_t)m.num_rx * p->L, p->c32.npow.p, p->fid.p, a->seed, inj_z,
                          inj_z_stride, tmp.p);
       LCHK((int)hipGetLastError());
     }
@@ -1287,9 +1391,9 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   if (a->cap_bits_rx)
     HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
   if (a->cap_llr && coded)
-    HIPCHK(hipMemcpyAsync(a->cap_llr, p->llr.p, (size_t)B * p->n_re_bits * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_llr, p->c32.llr.p, (size_t)B * p->n_re_bits * sizeof(float), hipMemcpyDeviceToHost, s));
   if (a->cap_noise_power)
-    HIPCHK(hipMemcpyAsync(a->cap_noise_power, p->npow.p, (size_t)B * m.num_rx * sizeof(float), hipMemcpyDeviceToHost,
+    HIPCHK(hipMemcpyAsync(a->cap_noise_power, p->c32.npow.p, (size_t)B * m.num_rx * sizeof(float), hipMemcpyDeviceToHost,
                           s));
   DBuf<float> lpart, lstats;
   if (a->cap_link_stats) {
@@ -1297,7 +1401,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
       return fail(LTE_ENOMEM, "capture");
     {
       Timer t(p, KN_CAP);
-      LCHK(launch_link_stats(s, g, m, B, np, ray ? p->delays.p : nullptr, p->coef.p, p->x.p, lpart.p, p->nblk,
+      LCHK(launch_link_stats(s, g, m, B, np, ray ? p->delays.p : nullptr, p->c32.coef.p, p->c32.x.p, lpart.p, p->nblk,
                              lstats.p));
     }
     HIPCHK(hipMemcpyAsync(a->cap_link_stats, lstats.p, (size_t)B * links * 4 * sizeof(float), hipMemcpyDeviceToHost,
@@ -1338,8 +1442,8 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   float2* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
   if (a->cap_data_syms) {
-    if (p->capbuf.alloc((size_t)B * p->L)) return fail(LTE_ENOMEM, "capture");
-    cap_syms_dev = p->capbuf.p;
+    if (p->c32.capbuf.alloc((size_t)B * p->L)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = p->c32.capbuf.p;
   }
   if (a->cap_bits_rx) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
@@ -1348,7 +1452,7 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_bf(s, B, p->n_sym, p->Nd, d.bps, d.num_tx, d.num_rx, d.bf_adaptive, p->bf_ncb, p->bf_cb.p, p->fid.p,
-                   a->seed, inj_h, inj_h_stride, p->bf_fr.p, p->snr_lin.p, p->pw.p, p->PW, d.n_bits, inj_z,
+                   a->seed, inj_h, inj_h_stride, p->bf_fr.p, p->c32.snr_lin.p, p->pw.p, p->PW, d.n_bits, inj_z,
                    inj_z_stride, p->frame_err.p, cap_syms_dev, cap_bits_dev));
   }
   {
@@ -1374,7 +1478,7 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
     if (a->cap_H)
       for (int r = 0; r < d.num_rx; ++r)
         for (int t = 0; t < d.num_tx; ++t) {
-          float* o = a->cap_H + (((size_t)b * d.num_rx + r) * d.num_tx + t) * 2;
+          float* o = static_cast<float*>(a->cap_H) + (((size_t)b * d.num_rx + r) * d.num_tx + t) * 2;
           o[0] = fr[b].H[r][t].x;
           o[1] = fr[b].H[r][t].y;
         }
@@ -1386,7 +1490,9 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   return LTE_OK;
 }
 
-// TX with the static-tap channel fused in (TxChannel): SISO Rayleigh with
+}  // extern "C"
+
+// TX with the static-tap channel fused in (TxChannelT): SISO Rayleigh with
 // fD = 0, delays within the CP, no TX / RX stream capture.  LTE_TXCH_FUSE=0
 // selects the separate TX and channel kernels (A/B and parity tests).
 static bool txch_fusable(const lte_plan* p, const lte_run_args* a, bool coded) {
@@ -1398,47 +1504,63 @@ static bool txch_fusable(const lte_plan* p, const lte_run_args* a, bool coded) {
   return txch_supported(p->grid, d.n_paths, *std::max_element(d.delays, d.delays + d.n_paths));
 }
 
-// Fading taps, fused TX + channel, first-samples power fix-up and noise power
-// for frames [b0, b0 + Bc) of the plan's buffers.
-static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, size_t b0, int Bc, bool coded,
-                    const float* inj_ph, int64_t inj_ph_stride, float2* cap_tx_syms) {
+
+// Host injection (float64 from the caller) -> device buffer of R, frames
+// [0, nf) of `per` values each; synchronous (the host copy is a temporary).
+template <class R>
+static int upload_inj(DBuf<R>& dst, const double* src, int64_t stride, int B, size_t per, hipStream_t s,
+                      const R** out, int64_t* out_stride) {
+  const int nf = stride ? B : 1;
+  std::vector<R> h((size_t)nf * per);
+  for (int f = 0; f < nf; ++f)
+    for (size_t i = 0; i < per; ++i) h[f * per + i] = (R)src[(size_t)f * stride + i];
+  if (dst.alloc(h.size())) return fail(LTE_ENOMEM, "injection buffer");
+  HIPCHK(hipMemcpyAsync(dst.p, h.data(), h.size() * sizeof(R), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *out = dst.p;
+  *out_stride = stride ? (int64_t)per : 0;
+  return LTE_OK;
+}
+
+// Fading taps, fused TX + channel, first-samples power fix-up and noise power.
+template <class R>
+static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bool coded, const R* inj_ph,
+                    int64_t inj_ph_stride, cx<R>* cap_tx_syms) {
   const lte_plan_desc& d = p->d;
+  ChainBufs<R>& c = cbuf<R>(p);
   const int maxd = *std::max_element(d.delays, d.delays + d.n_paths);
-  if (p->xh.alloc((size_t)d.max_frames * p->n_sym * 2 * std::max(maxd, 1))) return fail(LTE_ENOMEM, "tx channel");
-  const size_t fp = b0 * d.n_paths;
+  if (c.xh.alloc((size_t)d.max_frames * p->n_sym * 2 * std::max(maxd, 1))) return fail(LTE_ENOMEM, "tx channel");
   {
     Timer t(p, KN_FADING, s);
-    LCHK(launch_fading(s, Bc, 1, d.n_paths, p->gains.p, p->fid.p + b0, a->seed,
-                       inj_ph ? inj_ph + b0 * inj_ph_stride : nullptr, inj_ph_stride, p->phases.p + fp * 16,
-                       p->coef.p + fp));
+    LCHK(launch_fading<R>(s, B, 1, d.n_paths, c.gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, c.phases.p,
+                          c.coef.p));
   }
-  TxChannel ch{};
+  TxChannelT<R> ch{};
   ch.n_paths = d.n_paths;
   ch.max_delay = maxd;
   for (int i = 0; i < d.n_paths; ++i) ch.delays[i] = d.delays[i];
-  ch.coef = p->coef.p + fp;
-  ch.y = p->y.p + b0 * p->L;
-  ch.xh = p->xh.p + b0 * p->n_sym * 2 * maxd;
-  ch.pow_part = p->pow_part.p + b0 * p->n_sym;
+  ch.coef = c.coef.p;
+  ch.y = c.y.p;
+  ch.xh = c.xh.p;
+  ch.pow_part = c.pow_part.p;
   {
     Timer t(p, KN_OFDM_TX, s);
-    LCHK(launch_ofdm_tx_ch(s, p->grid, coded ? 1 : 0, p->pw.p + b0 * p->PW, p->PW, p->enc.p + b0 * p->enc_words,
-                           p->enc_words, p->tx_map.p, Bc, cap_tx_syms ? cap_tx_syms + b0 * p->n_sym * p->Nd : nullptr,
-                           ch));
+    LCHK(launch_ofdm_tx_ch<R>(s, p->grid, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, B,
+                              cap_tx_syms, ch));
   }
   {
     Timer t(p, KN_CHANNEL, s);
-    LCHK(launch_chan_fix(s, p->grid, Bc, ch));
-    LCHK(launch_npow(s, Bc, 1, ch.pow_part, p->n_sym, p->L, p->snr_lin.p + b0, p->npow.p + b0));
+    LCHK(launch_chan_fix<R>(s, p->grid, B, ch));
+    LCHK(launch_npow<R>(s, B, 1, ch.pow_part, p->n_sym, p->L, c.snr_lin.p, c.npow.p));
   }
   return LTE_OK;
 }
 
 // Coded SISO 16/64-QAM without an LLR capture: k_rx_data hands over the
-// equalised symbol and sigma^2_eff per RE (12 B) and k_dematch_zn demaps while
-// it builds the decoder rows, instead of a round trip of 4 * bps B of LLRs per
-// RE.  The (z, nv) arrays live in the LLR buffer ([max_frames][n_re] each; it
-// holds bps >= 4 floats per RE).  LTE_DEMAP_IN_DEMATCH=0 keeps the LLR path.
+// equalised symbol and sigma^2_eff per RE and k_dematch_zn demaps while it
+// builds the decoder rows, instead of a round trip of bps LLRs per RE.  The
+// (z, nv) arrays live in the LLR buffer ([max_frames][n_re] z, then
+// [max_frames][n_re] nv: 3 R per RE).  LTE_DEMAP_IN_DEMATCH=0 keeps the LLR path.
 static bool demap_in_dematch(const lte_plan* p, const lte_run_args* a) {
   const lte_plan_desc& d = p->d;
   if (d.chain != LTE_CHAIN_CODED || p->mimo || p->bf || (d.bps != 4 && d.bps != 6) || a->cap_llr) return false;
@@ -1446,333 +1568,140 @@ static bool demap_in_dematch(const lte_plan* p, const lte_run_args* a) {
     if (std::atoi(e) == 0) return false;
   return true;
 }
-static float2* zn_z(lte_plan* p, size_t b0) {
-  return reinterpret_cast<float2*>(p->llr.p) + b0 * (p->n_re_bits / p->d.bps);
-}
-static float* zn_nv(lte_plan* p, size_t b0) {
-  const size_t n_re = p->n_re_bits / p->d.bps;
-  return p->llr.p + 2 * (size_t)p->d.max_frames * n_re + b0 * n_re;
-}
-
-// Chunks of the pipelined coded SISO chain (LTE_PIPELINE_CHUNKS, default 1 =
-// off).  Measured on MI355X at 65536 frames: 2 / 3 / 4 chunks 4 / 7 / 26 %
-// slower than one pass -- the decoder already streams HBM at ~5.5 TB/s, so the
-// overlapped front end only takes bandwidth from it, and half-size decoder
-// launches fill the CUs less well.  Kept as an opt-in (parity-tested: results
-// do not depend on the chunking, every kernel is per frame with Philox keyed
-// by frame id and chunks are whole 64-frame groups).
-static int pipeline_chunks(const lte_plan* p, const lte_run_args* a, int B, int stages) {
-  const lte_plan_desc& d = p->d;
-  if (d.chain != LTE_CHAIN_CODED || p->mimo || p->bf || stages != LTE_STAGE_ALL) return 1;
-  if (a->bits || a->phases || a->noise || a->in_signal) return 1;
-  if (a->cap_signal_tx || a->cap_signal_rx || a->cap_data_syms || a->cap_H || a->cap_pilot_stats || a->cap_bits_rx ||
-      a->cap_llr || a->cap_tx_syms || a->cap_noise_power)
-    return 1;
-  const int G = (B + 63) / 64;
-  int n = 1;
-  if (const char* e = std::getenv("LTE_PIPELINE_CHUNKS")) n = std::atoi(e);
-  return std::max(1, std::min(n, G));
+template <class R>
+static cx<R>* zn_z(lte_plan* p) { return reinterpret_cast<cx<R>*>(cbuf<R>(p).llr.p); }
+template <class R>
+static R* zn_nv(lte_plan* p) {
+  return cbuf<R>(p).llr.p + 2 * (size_t)p->d.max_frames * (p->n_re_bits / p->d.bps);
 }
 
-// Coded SISO chain with the batch cut into chunks of whole 64-frame groups:
-// the front end of chunk c+1 (payload .. dematch, on the plan's stream) runs
-// while the decoder side of chunk c (turbo, CRC, on stream2) runs, so the
-// compute-bound TX / RX kernels overlap the HBM-bound decoder.  Same kernels,
-// same per-frame buffers (offset by the chunk's first frame) as lte_run.
-static int run_coded_pipelined(lte_plan* p, const lte_run_args* a, int B, int chunks) {
+// SISO / SIMO chains (uncoded, coded, MRC) in precision R.
+template <class R>
+static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const std::vector<double>& snr_lin,
+                    const uint32_t* inj_bits, int64_t inj_bits_stride) {
+  using V = cx<R>;
   const lte_plan_desc& d = p->d;
+  ChainBufs<R>& c = cbuf<R>(p);
   const Grid& g = p->grid;
-  const int rx = d.num_rx;
-  const bool ray = d.channel == LTE_CH_RAYLEIGH;
-  hipStream_t s = p->stream;
-  if (!p->stream2 && hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking) != hipSuccess)
-    return fail(LTE_EHIP, "stream creation failed");
-  while ((int)p->pipe_ev.size() < chunks + 1) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(LTE_EHIP, "event creation");
-    p->pipe_ev.push_back(e);
-  }
-  hipStream_t s2 = p->stream2;
-  const int G = (B + 63) / 64;
-  const int nblk = channel_nblk(p->L);
-  const int maxd = ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0;
-  const float2* ysrc = ray ? p->y.p : p->x.p;
-  const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
-  const bool fuse = txch_fusable(p, a, true);
-  const bool zn = demap_in_dematch(p, a);
-  for (int c = 0; c < chunks; ++c) {
-    const int g0 = (int)((int64_t)G * c / chunks), g1 = (int)((int64_t)G * (c + 1) / chunks);
-    const int b0 = g0 * 64, bend = std::min(B, g1 * 64), Bc = bend - b0;
-    if (Bc <= 0) continue;
-    const size_t fr = (size_t)b0;
-    {
-      Timer t(p, KN_PAYLOAD);
-      LCHK(launch_payload(s, p->pw.p + fr * p->PW, p->PW, d.n_bits, 1, p->fid.p + fr, a->seed, Bc, nullptr, 0));
-    }
-    {
-      Timer t(p, KN_ENCODE);
-      LCHK(launch_encode(s, p->pw.p + fr * p->PW, p->PW, p->KWmax, p->enc.p + fr * p->enc_words, p->EW, p->cbi.p,
-                         p->C, Bc, p->enc_cw.p));
-    }
-    const size_t fp = fr * rx * d.n_paths;
-    if (fuse) {
-      const int e = run_txch(p, s, a, fr, Bc, true, nullptr, 0, nullptr);
-      if (e != LTE_OK) return e;
-    } else {
-      {
-        Timer t(p, KN_OFDM_TX);
-        LCHK(launch_ofdm_tx(s, g, 1, p->pw.p + fr * p->PW, p->PW, p->enc.p + fr * p->enc_words, p->enc_words,
-                            p->tx_map.p, p->x.p + fr * p->L, Bc, nullptr, 0));
-      }
-      if (ray) {
-        Timer t(p, KN_FADING);
-        LCHK(launch_fading(s, Bc, rx, d.n_paths, p->gains.p, p->fid.p + fr, a->seed, nullptr, 0,
-                           p->phases.p + fp * 16, p->coef.p + fp));
-      }
-      Timer t(p, KN_CHANNEL);
-      LCHK(launch_channel(s, g, Bc, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
-                          p->phases.p + fp * 16, p->coef.p + fp, p->x.p + fr * p->L, p->y.p + fr * rx * p->L,
-                          p->pow_part.p + fr * rx * nblk, nblk, maxd));
-      LCHK(launch_npow(s, Bc, rx, p->pow_part.p + fr * rx * nblk, nblk, p->L, p->snr_lin.p + fr,
-                       p->npow.p + fr * rx));
-    }
-    const size_t fh = fr * rx * p->n_grp;
-    {
-      Timer t(p, KN_RX_CHEST);
-      LCHK(launch_rx_chest(s, g, Bc, rx, ysrc + fr * yfs, yrs, yfs, p->npow.p + fr * rx, p->fid.p + fr, a->seed,
-                           nullptr, 0, p->H.p + fh * d.N, p->pstats.p + fh * 2));
-    }
-    {
-      Timer t(p, KN_RX_DATA);
-      LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, Bc, rx, ysrc + fr * yfs, yrs, yfs, p->H.p + fh * d.N,
-                          p->npow.p + fr * rx, p->snr_lin.p + fr, p->fid.p + fr, a->seed, nullptr, 0,
-                          p->pw.p + fr * p->PW, p->PW, d.n_bits, p->frame_err.p + fr,
-                          zn ? reinterpret_cast<float*>(zn_z(p, fr)) : p->llr.p + fr * p->n_re_bits, nullptr,
-                          nullptr, 0, zn ? zn_nv(p, fr) : nullptr));
-    }
-    {
-      Timer t(p, KN_DEMATCH);
-      if (zn)
-        LCHK(launch_dematch_zn(s, zn_z(p, 0), zn_nv(p, 0), p->n_re_bits / d.bps, d.bps, bend, p->rx_map.p,
-                               p->blk_ptrs.p, p->rows_dev.p, g0));
-      else
-        LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, bend, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C, g0));
-    }
-    // decoder side of this chunk on stream2, after its front end
-    HIPCHK(hipEventRecord(p->pipe_ev[c], s));
-    HIPCHK(hipStreamWaitEvent(s2, p->pipe_ev[c], 0));
-    std::vector<TurboJob> jobs(p->C);
-    for (int r = 0; r < p->C; ++r) {
-      const CbInfo& cb = p->cbs[r];
-      jobs[r] = TurboJob{p->blk[r].p + (size_t)g0 * turbo_rows(cb.K) * 64,
-                         p->ckpt[r].p + (size_t)g0 * turbo_nwin(cb.K) * TURBO_CK_ROWS_F32 * 64,
-                         p->decb[r].p + (size_t)g0 * turbo_kw(cb.K) * 64, cb.K, cb.f1, cb.f2, g1 - g0};
-    }
-    {
-      Timer t(p, KN_TURBO, s2);
-      LCHK(launch_turbo_jobs(s2, jobs.data(), p->C, d.turbo_iters, TM_DEC1, 0));
-    }
-    {
-      Timer t(p, KN_CRC, s2);
-      LCHK(launch_crc_count(s2, p->cbi.p, p->C, p->dec_ptrs.p, p->kw_dev.p, bend, p->pw.p, p->PW, d.n_bits,
-                            p->frame_err.p, p->frame_crc.p, nullptr, b0));
-    }
-  }
-  HIPCHK(hipEventRecord(p->pipe_ev[chunks], s2));
-  HIPCHK(hipStreamWaitEvent(s, p->pipe_ev[chunks], 0));
-  return LTE_OK;
-}
-
-int lte_run(lte_plan* p, const lte_run_args* a) {
-  if (!p || !a) return fail(LTE_EINVAL, "null argument");
-  const lte_plan_desc& d = p->d;
-  const int B = a->n_frames;
-  if (B < 1 || B > d.max_frames) return fail(LTE_EINVAL, "n_frames out of range (1..max_frames)");
-  if (!a->snr_db) return fail(LTE_EINVAL, "snr_db required");
-  const int n_snr = std::max(1, a->n_snr);
-  const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED,
-             ray_cfg = d.channel == LTE_CH_RAYLEIGH;
+  const bool coded = d.chain == LTE_CHAIN_CODED, ray_cfg = d.channel == LTE_CH_RAYLEIGH;
   const int rx = d.num_rx;
   hipStream_t s = p->stream;
-  if (p->counts.alloc((size_t)4 * n_snr)) return fail(LTE_ENOMEM, "counts");
-  // per-frame parameters
-  std::vector<float> sl(B);
-  std::vector<int32_t> si(B, 0);
-  std::vector<uint64_t> fid(B);
-  for (int b = 0; b < B; ++b) {
-    sl[b] = (float)std::pow(10.0, (double)a->snr_db[b] / 10.0);
-    if (a->snr_index) {
-      si[b] = a->snr_index[b];
-      if (si[b] < 0 || si[b] >= n_snr) return fail(LTE_EINVAL, "snr_index out of range");
-    }
-    fid[b] = a->frame_ids ? a->frame_ids[b] : a->frame_id0 + (uint64_t)b;
-  }
-  HIPCHK(hipMemcpyAsync(p->snr_lin.p, sl.data(), B * sizeof(float), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(p->snr_idx.p, si.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(p->fid.p, fid.data(), B * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  // injection
-  const uint32_t* inj_bits = nullptr;
-  int64_t inj_bits_stride = 0;
-  std::vector<uint32_t> hb;
-  if (a->bits) {
-    const int nf = a->bits_stride ? B : 1;
-    const int nwd = (d.n_bits + 31) / 32;
-    hb.assign((size_t)nf * nwd, 0);
-    for (int f = 0; f < nf; ++f) pack_bits(a->bits + (size_t)f * a->bits_stride, d.n_bits, &hb[(size_t)f * nwd], nwd);
-    if (p->inj_bits.alloc(hb.size())) return fail(LTE_ENOMEM, "inj bits");
-    HIPCHK(hipMemcpyAsync(p->inj_bits.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, s));
-    inj_bits = p->inj_bits.p;
-    inj_bits_stride = a->bits_stride ? nwd : 0;
-  }
-  const float* inj_ph = nullptr;
-  int64_t inj_ph_stride = 0;
-  std::vector<float> hph;
-  if (a->phases && ray_cfg) {
-    const int nf = a->phases_stride ? B : 1;
-    const size_t per = (size_t)rx * d.num_tx * d.n_paths * 16;
-    hph.resize(nf * per);
-    for (int f = 0; f < nf; ++f)
-      for (size_t i = 0; i < per; ++i) hph[f * per + i] = (float)a->phases[(size_t)f * a->phases_stride + i];
-    if (p->inj_ph.alloc(hph.size())) return fail(LTE_ENOMEM, "inj phases");
-    HIPCHK(hipMemcpyAsync(p->inj_ph.p, hph.data(), hph.size() * 4, hipMemcpyHostToDevice, s));
-    inj_ph = p->inj_ph.p;
-    inj_ph_stride = a->phases_stride ? (int64_t)per : 0;
-  }
-  const float* inj_z = nullptr;
-  int64_t inj_z_stride = 0;
-  std::vector<float> hz;
-  if (a->noise) {
-    const int nf = a->noise_stride ? B : 1;
-    const size_t per = (size_t)rx * 2 * p->L;
-    hz.resize(nf * per);
-    for (int f = 0; f < nf; ++f)
-      for (size_t i = 0; i < per; ++i) hz[f * per + i] = (float)a->noise[(size_t)f * a->noise_stride + i];
-    if (p->inj_z.alloc(hz.size())) return fail(LTE_ENOMEM, "inj noise");
-    HIPCHK(hipMemcpyAsync(p->inj_z.p, hz.data(), hz.size() * 4, hipMemcpyHostToDevice, s));
-    inj_z = p->inj_z.p;
-    inj_z_stride = a->noise_stride ? (int64_t)per : 0;
-  }
-  HIPCHK(hipMemsetAsync(p->counts.p, 0, 4 * n_snr * sizeof(unsigned long long), s));
-  HIPCHK(hipMemsetAsync(p->frame_err.p, 0, B * sizeof(uint32_t), s));
   const int stages = a->stages ? a->stages : LTE_STAGE_ALL;
   const bool do_tx = stages & LTE_STAGE_TX, do_ch = stages & LTE_STAGE_CHANNEL, do_rx = stages & LTE_STAGE_RX;
-  if (!do_tx && !a->in_signal) return fail(LTE_EINVAL, "in_signal required when the TX stage is skipped");
-  const Grid& g = p->grid;
-  p->evuse.clear();
-  if (p->mimo) {
-    if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "multi-antenna chains run all stages");
-    return run_mimo(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_ph, inj_ph_stride, inj_z, inj_z_stride);
-  }
-  if (p->bf) {
-    if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "the beamforming chain runs all stages");
-    return run_bf(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_z, inj_z_stride);
-  }
-  const int chunks = pipeline_chunks(p, a, B, stages);
-  if (chunks > 1) {
-    const int e = run_coded_pipelined(p, a, B, chunks);
+  // per-frame linear SNR (computed in float64 on the host, as 10 ** (snr_db / 10));
+  // without the channel stage the input is the received signal: no noise
+  std::vector<R> sl(B);
+  for (int b = 0; b < B; ++b) sl[b] = do_ch ? (R)snr_lin[b] : (R)INFINITY;
+  HIPCHK(hipMemcpyAsync(c.snr_lin.p, sl.data(), B * sizeof(R), hipMemcpyHostToDevice, s));
+  const R* inj_ph = nullptr;
+  int64_t inj_ph_stride = 0;
+  if (a->phases && ray_cfg) {
+    const int e = upload_inj<R>(c.inj_ph, a->phases, a->phases_stride, B, (size_t)rx * d.n_paths * 16, s, &inj_ph,
+                                &inj_ph_stride);
     if (e != LTE_OK) return e;
   }
-  const bool seq = chunks <= 1;   // the unpipelined chain
+  const R* inj_z = nullptr;
+  int64_t inj_z_stride = 0;
+  if (a->noise) {
+    const int e = upload_inj<R>(c.inj_z, a->noise, a->noise_stride, B, (size_t)rx * 2 * p->L, s, &inj_z,
+                                &inj_z_stride);
+    if (e != LTE_OK) return e;
+  }
   // TX + static-tap channel in one kernel (the received stream is written once)
-  const bool fuse = seq && do_tx && do_ch && txch_fusable(p, a, coded);
-  if (seq && (do_tx || a->bits)) {
+  const bool fuse = do_tx && do_ch && txch_fusable(p, a, coded);
+  if (do_tx || a->bits) {
     Timer t(p, KN_PAYLOAD);
     LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
   }
-  if (!seq) {
-  } else if (do_tx) {
+  if (!fuse && c.x.alloc((size_t)d.max_frames * p->L)) return fail(LTE_ENOMEM, "TX signal buffer");
+  if (do_tx) {
     if (coded) {
       Timer t(p, KN_ENCODE);
       LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_cw.p));
     }
-    float2* cts = nullptr;
+    V* cts = nullptr;
     if (a->cap_tx_syms) {
-      if (p->captx.alloc((size_t)B * p->n_sym * p->Nd)) return fail(LTE_ENOMEM, "capture");
-      cts = p->captx.p;
+      if (c.captx.alloc((size_t)B * p->n_sym * p->Nd)) return fail(LTE_ENOMEM, "capture");
+      cts = c.captx.p;
     }
     if (fuse) {
-      const int e = run_txch(p, s, a, 0, B, coded, inj_ph, inj_ph_stride, cts);
+      const int e = run_txch<R>(p, s, a, B, coded, inj_ph, inj_ph_stride, cts);
       if (e != LTE_OK) return e;
     } else {
       Timer t(p, KN_OFDM_TX);
       // SC-FDM precodes the uncoded SISO / SIMO transmitters only: simulate_siso_coded
       // builds its own grids without the precoder (core/ofdm_core.py:1062-1099)
-      LCHK(launch_ofdm_tx(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->x.p, B, cts,
-                          (d.sc_fdm && !coded) ? 1 : 0));
+      LCHK(launch_ofdm_tx<R>(s, g, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, c.x.p, B, cts,
+                             (d.sc_fdm && !coded) ? 1 : 0));
     }
   } else {
-    std::vector<float> hx((size_t)B * p->L * 2);
+    const R* in = static_cast<const R*>(a->in_signal);
+    std::vector<R> hx((size_t)B * p->L * 2);
     for (int b = 0; b < B; ++b)
-      std::memcpy(&hx[(size_t)b * p->L * 2], a->in_signal + (size_t)b * a->in_signal_stride,
-                  (size_t)p->L * 2 * sizeof(float));
-    HIPCHK(hipMemcpyAsync(p->x.p, hx.data(), hx.size() * sizeof(float), hipMemcpyHostToDevice, s));
+      std::memcpy(&hx[(size_t)b * p->L * 2], in + (size_t)b * a->in_signal_stride, (size_t)p->L * 2 * sizeof(R));
+    HIPCHK(hipMemcpyAsync(c.x.p, hx.data(), hx.size() * sizeof(R), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
   }
-  // without the channel stage the input is the received signal: no fading, no noise
   const bool ray = ray_cfg && do_ch;
-  if (!do_ch) {
-    std::vector<float> inf(B, INFINITY);
-    HIPCHK(hipMemcpyAsync(p->snr_lin.p, inf.data(), B * sizeof(float), hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
-  }
-  const float2* ysrc = ray ? p->y.p : p->x.p;
+  const V* ysrc = ray ? c.y.p : c.x.p;
   const int64_t yrs = ray ? p->L : 0, yfs = ray ? (int64_t)rx * p->L : p->L;
-  if (seq && ray && !fuse) {
+  if (ray && !fuse) {
     Timer t(p, KN_FADING);
-    LCHK(launch_fading(s, B, rx, d.n_paths, p->gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, p->phases.p,
-                       p->coef.p));
+    LCHK(launch_fading<R>(s, B, rx, d.n_paths, c.gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, c.phases.p,
+                          c.coef.p));
   }
-  if (seq && !fuse) {
+  if (!fuse) {
     Timer t(p, KN_CHANNEL);
-    LCHK(launch_channel(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, p->gains.p, (float)d.fD, (float)d.fs,
-                        p->phases.p, p->coef.p, p->x.p, p->y.p, p->pow_part.p, channel_nblk(p->L),
-                        ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0));
-    LCHK(launch_npow(s, B, rx, p->pow_part.p, channel_nblk(p->L), p->L, p->snr_lin.p, p->npow.p));
+    LCHK(launch_channel<R>(s, g, B, rx, ray ? 1 : 0, d.n_paths, p->delays.p, c.gains.p, (R)d.fD, (R)d.fs,
+                           c.phases.p, c.coef.p, c.x.p, c.y.p, c.pow_part.p, channel_nblk(p->L),
+                           ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0));
+    LCHK(launch_npow<R>(s, B, rx, c.pow_part.p, channel_nblk(p->L), p->L, c.snr_lin.p, c.npow.p));
   }
-  if (seq && do_rx) {
+  if (do_rx) {
     Timer t(p, KN_RX_CHEST);
-    LCHK(launch_rx_chest(s, g, B, rx, ysrc, yrs, yfs, p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, p->H.p,
-                         p->pstats.p));
+    LCHK(launch_rx_chest<R>(s, g, B, rx, ysrc, yrs, yfs, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.H.p,
+                            c.pstats.p));
   }
-  float2* cap_syms_dev = nullptr;
+  V* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
   if (a->cap_data_syms) {
-    if (p->capbuf.alloc((size_t)B * p->n_sym * p->Nd)) return fail(LTE_ENOMEM, "capture");
-    cap_syms_dev = p->capbuf.p;
+    if (c.capbuf.alloc((size_t)B * p->n_sym * p->Nd)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = c.capbuf.p;
   }
   if (a->cap_bits_rx) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
     cap_bits_dev = p->cap_bits.p;
   }
-  const bool zn = seq && demap_in_dematch(p, a);
-  if (seq && do_rx) {
+  const bool zn = demap_in_dematch(p, a);
+  if (coded && !zn && c.llr.alloc((size_t)d.max_frames * p->n_re_bits)) return fail(LTE_ENOMEM, "LLR buffer");
+  if (do_rx) {
     Timer t(p, KN_RX_DATA);
-    LCHK(launch_rx_data(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, p->H.p, p->npow.p, p->snr_lin.p,
-                        p->fid.p, a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
-                        zn ? reinterpret_cast<float*>(zn_z(p, 0)) : p->llr.p, cap_syms_dev,
-                        coded ? nullptr : cap_bits_dev,
-                        // the IDFT runs in receive_and_decode only (core/lte_receiver.py:318-333): the SIMO
-                        // MRC receiver (core/ofdm_core.py:1340-1534) never de-precodes
-                        (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0, zn ? zn_nv(p, 0) : nullptr));
+    LCHK(launch_rx_data<R>(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, c.H.p, c.npow.p, c.snr_lin.p, p->fid.p,
+                           a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+                           zn ? reinterpret_cast<R*>(zn_z<R>(p)) : c.llr.p, cap_syms_dev,
+                           coded ? nullptr : cap_bits_dev,
+                           // the IDFT runs in receive_and_decode only (core/lte_receiver.py:318-333): the SIMO
+                           // MRC receiver (core/ofdm_core.py:1340-1534) never de-precodes
+                           (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0, zn ? zn_nv<R>(p) : nullptr));
   }
-  if (seq && coded && do_rx) {
+  if (coded && do_rx) {
     {
       Timer t(p, KN_DEMATCH);
       if (zn)
-        LCHK(launch_dematch_zn(s, zn_z(p, 0), zn_nv(p, 0), p->n_re_bits / d.bps, d.bps, B, p->rx_map.p,
-                               p->blk_ptrs.p, p->rows_dev.p));
+        LCHK(launch_dematch_zn<R>(s, zn_z<R>(p), zn_nv<R>(p), p->n_re_bits / d.bps, d.bps, B, p->rx_map.p,
+                                  p->n_layers, c.blk_ptrs.p, p->rows_dev.p));
       else
-        LCHK(launch_dematch(s, p->llr.p, p->n_re_bits, B, p->rx_map.p, p->blk_ptrs.p, p->rows_dev.p, p->C));
+        LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p));
     }
     const int G = (B + 63) / 64;
     std::vector<TurboJob> jobs(p->C);
     for (int r = 0; r < p->C; ++r) {
-      const CbInfo& c = p->cbs[r];
-      jobs[r] = TurboJob{p->blk[r].p, p->ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, G};
+      const CbInfo& cb = p->cbs[r];
+      jobs[r] = TurboJob{c.blk[r].p, c.ckpt[r].p, p->decb[r].p, cb.K, cb.f1, cb.f2, G};
     }
     {
       Timer t(p, KN_TURBO);
-      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1, 0));
+      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1, sizeof(R) == 8 ? 1 : 0));
     }
     {
       Timer t(p, KN_CRC);
@@ -1796,37 +1725,37 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     HIPCHK(hipMemcpyAsync(crc.data(), p->frame_crc.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   }
   if (a->cap_signal_tx)
-    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, p->x.p, (size_t)B * p->L * sizeof(float2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, c.x.p, (size_t)B * p->L * sizeof(V), hipMemcpyDeviceToHost, s));
   if (a->cap_signal_rx) {
-    DBuf<float2> tmp;
+    DBuf<V> tmp;
     if (tmp.alloc((size_t)B * rx * p->L)) return fail(LTE_ENOMEM, "capture");
     {
       Timer t(p, KN_CAP);
-      hipLaunchKernelGGL(k_cap_rx, dim3(((p->L + 255) / 256) * B, rx), dim3(256), 0, s, p->L, rx, B, ysrc, yrs, yfs,
-                         p->npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p);
+      hipLaunchKernelGGL(k_cap_rx<R>, dim3(((p->L + 255) / 256) * B, rx), dim3(256), 0, s, p->L, rx, B, ysrc, yrs, yfs,
+                         c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p);
       LCHK((int)hipGetLastError());
     }
-    HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * rx * p->L * sizeof(float2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * rx * p->L * sizeof(V), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     tmp.release();
   }
   if (a->cap_data_syms)
-    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->n_sym * p->Nd * sizeof(float2),
+    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->n_sym * p->Nd * sizeof(V),
                           hipMemcpyDeviceToHost, s));
   if (a->cap_H)
-    HIPCHK(hipMemcpyAsync(a->cap_H, p->H.p, (size_t)B * rx * p->n_grp * d.N * sizeof(float2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_H, c.H.p, (size_t)B * rx * p->n_grp * d.N * sizeof(V), hipMemcpyDeviceToHost, s));
   if (a->cap_pilot_stats)
-    HIPCHK(hipMemcpyAsync(a->cap_pilot_stats, p->pstats.p, (size_t)B * rx * p->n_grp * 2 * sizeof(float),
+    HIPCHK(hipMemcpyAsync(a->cap_pilot_stats, c.pstats.p, (size_t)B * rx * p->n_grp * 2 * sizeof(R),
                           hipMemcpyDeviceToHost, s));
   if (a->cap_bits_rx)
     HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
   if (a->cap_llr && coded)
-    HIPCHK(hipMemcpyAsync(a->cap_llr, p->llr.p, (size_t)B * p->n_re_bits * sizeof(float), hipMemcpyDeviceToHost, s));
-  if (a->cap_tx_syms && (stages & LTE_STAGE_TX))
-    HIPCHK(hipMemcpyAsync(a->cap_tx_syms, p->captx.p, (size_t)B * p->n_sym * p->Nd * sizeof(float2),
-                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_llr, c.llr.p, (size_t)B * p->n_re_bits * sizeof(R), hipMemcpyDeviceToHost, s));
+  if (a->cap_tx_syms && do_tx)
+    HIPCHK(hipMemcpyAsync(a->cap_tx_syms, c.captx.p, (size_t)B * p->n_sym * p->Nd * sizeof(V), hipMemcpyDeviceToHost,
+                          s));
   if (a->cap_noise_power)
-    HIPCHK(hipMemcpyAsync(a->cap_noise_power, p->npow.p, (size_t)B * rx * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_noise_power, c.npow.p, (size_t)B * rx * sizeof(R), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (p->timing) collect_timing(p);
   if (a->counts)
@@ -1836,87 +1765,211 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   return LTE_OK;
 }
 
+extern "C" {
+
+int lte_run(lte_plan* p, const lte_run_args* a) {
+  if (!p || !a) return fail(LTE_EINVAL, "null argument");
+  const lte_plan_desc& d = p->d;
+  const int B = a->n_frames;
+  if (B < 1 || B > d.max_frames) return fail(LTE_EINVAL, "n_frames out of range (1..max_frames)");
+  if (!a->snr_db) return fail(LTE_EINVAL, "snr_db required");
+  const int n_snr = std::max(1, a->n_snr);
+  const int rx = d.num_rx;
+  hipStream_t s = p->stream;
+  if (p->counts.alloc((size_t)4 * n_snr)) return fail(LTE_ENOMEM, "counts");
+  // per-frame parameters
+  std::vector<double> sl(B);
+  std::vector<int32_t> si(B, 0);
+  std::vector<uint64_t> fid(B);
+  for (int b = 0; b < B; ++b) {
+    sl[b] = std::pow(10.0, (double)a->snr_db[b] / 10.0);   // snr_linear = 10 ** (snr_db / 10) (channel.py:32)
+    if (a->snr_index) {
+      si[b] = a->snr_index[b];
+      if (si[b] < 0 || si[b] >= n_snr) return fail(LTE_EINVAL, "snr_index out of range");
+    }
+    fid[b] = a->frame_ids ? a->frame_ids[b] : a->frame_id0 + (uint64_t)b;
+  }
+  HIPCHK(hipMemcpyAsync(p->snr_idx.p, si.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(p->fid.p, fid.data(), B * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  // payload injection (packed MSB-first)
+  const uint32_t* inj_bits = nullptr;
+  int64_t inj_bits_stride = 0;
+  std::vector<uint32_t> hb;
+  if (a->bits) {
+    const int nf = a->bits_stride ? B : 1;
+    const int nwd = (d.n_bits + 31) / 32;
+    hb.assign((size_t)nf * nwd, 0);
+    for (int f = 0; f < nf; ++f) pack_bits(a->bits + (size_t)f * a->bits_stride, d.n_bits, &hb[(size_t)f * nwd], nwd);
+    if (p->inj_bits.alloc(hb.size())) return fail(LTE_ENOMEM, "inj bits");
+    HIPCHK(hipMemcpyAsync(p->inj_bits.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, s));
+    inj_bits = p->inj_bits.p;
+    inj_bits_stride = a->bits_stride ? nwd : 0;
+  }
+  HIPCHK(hipMemsetAsync(p->counts.p, 0, 4 * n_snr * sizeof(unsigned long long), s));
+  HIPCHK(hipMemsetAsync(p->frame_err.p, 0, B * sizeof(uint32_t), s));
+  const int stages = a->stages ? a->stages : LTE_STAGE_ALL;
+  if (!(stages & LTE_STAGE_TX) && !a->in_signal) return fail(LTE_EINVAL, "in_signal required when the TX stage is skipped");
+  p->evuse.clear();
+  if (!p->mimo && !p->bf) {
+    const int e = p->f64 ? run_siso<double>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride)
+                         : run_siso<float>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride);
+    HIPCHK(hipStreamSynchronize(s));
+    return e;
+  }
+  // multi-antenna / beamforming chains: float32
+  if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "multi-antenna chains run all stages");
+  ChainBufs<float>& c = p->c32;
+  std::vector<float> slf(B);
+  for (int b = 0; b < B; ++b) slf[b] = (float)sl[b];
+  HIPCHK(hipMemcpyAsync(c.snr_lin.p, slf.data(), B * sizeof(float), hipMemcpyHostToDevice, s));
+  const float* inj_ph = nullptr;
+  int64_t inj_ph_stride = 0;
+  if (a->phases && d.channel == LTE_CH_RAYLEIGH) {
+    const int e = upload_inj<float>(c.inj_ph, a->phases, a->phases_stride, B, (size_t)rx * d.num_tx * d.n_paths * 16,
+                                    s, &inj_ph, &inj_ph_stride);
+    if (e != LTE_OK) return e;
+  }
+  const float* inj_z = nullptr;
+  int64_t inj_z_stride = 0;
+  if (a->noise) {
+    const int e = upload_inj<float>(c.inj_z, a->noise, a->noise_stride, B, (size_t)rx * 2 * p->L, s, &inj_z,
+                                    &inj_z_stride);
+    if (e != LTE_OK) return e;
+  }
+  if (p->bf) return run_bf(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_z, inj_z_stride);
+  return run_mimo(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_ph, inj_ph_stride, inj_z, inj_z_stride);
+}
+
 // ------------------------------------------------------------------ stage entry points
+}  // extern "C"
+
+// Stage entry points (host in / out, the chains' device kernels), R = float / double.
+template <class R>
 static int stage_grid(int N, TableSet& t, Grid& g) {
-  const std::vector<float2> tw = make_twiddles(N);
-  if (upload(t.tw, tw)) return -1;
   g = Grid{};
   g.N = N;
   g.log2N = ilog2(N);
-  g.tw = t.tw.p;
+  if (sizeof(R) == 8) {
+    if (upload(t.tw64, make_twiddles64(N))) return -1;
+    g.tw64 = t.tw64.p;
+  } else {
+    if (upload(t.tw, make_twiddles(N))) return -1;
+    g.tw = t.tw.p;
+  }
   return 0;
 }
 
-int lte_fft_host(int N, int inverse, int64_t batch, const float* in, float* out) {
+template <class R>
+static int fft_host(int N, int inverse, int64_t batch, const R* in, R* out) {
   if (N < 8 || N > 2048 || (N & (N - 1)) || batch < 0 || (!in && batch) || (!out && batch))
     return fail(LTE_EINVAL, "bad fft arguments");
   if (batch == 0) return LTE_OK;
   if (N < 64) return fail(LTE_EUNSUP, "N < 64");
   TableSet t;
   Grid g;
-  if (stage_grid(N, t, g)) return fail(LTE_ENOMEM, "tables");
-  DBuf<float2> di, dout;
+  if (stage_grid<R>(N, t, g)) return fail(LTE_ENOMEM, "tables");
+  DBuf<cx<R>> di, dout;
   if (di.alloc(batch * N) || dout.alloc(batch * N)) { t.release(); return fail(LTE_ENOMEM, "fft buffers"); }
   int rc = LTE_OK;
-  if (hipMemcpy(di.p, in, batch * N * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
-      launch_fft(nullptr, g, inverse, batch, di.p, dout.p) != 0 || hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(out, dout.p, batch * N * sizeof(float2), hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(di.p, in, batch * N * sizeof(cx<R>), hipMemcpyHostToDevice) != hipSuccess ||
+      launch_fft<R>(nullptr, g, inverse, batch, di.p, dout.p) != 0 || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, dout.p, batch * N * sizeof(cx<R>), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "fft failed");
   di.release(); dout.release(); t.release();
   return rc;
 }
 
-int lte_dft_host(int M, int inverse, int64_t batch, const float* in, float* out) {
+template <class R>
+static int dft_host(int M, int inverse, int64_t batch, const R* in, R* out) {
   if (M < 1 || M > 1024 || batch < 0 || (!in && batch) || (!out && batch)) return fail(LTE_EINVAL, "bad dft arguments");
   if (batch == 0) return LTE_OK;
   int N = 64;
   while (N < 2 * M - 1) N <<= 1;
   TableSet t;
   Grid g;
-  std::vector<float2> ch, bh;
-  make_bluestein(N, M, ch, bh);
-  if (stage_grid(N, t, g) || upload(t.chirp, ch) || upload(t.bhat, bh)) { t.release(); return fail(LTE_ENOMEM, "tables"); }
+  bool bad = stage_grid<R>(N, t, g) != 0;
+  if (!bad && sizeof(R) == 8) {
+    std::vector<double2> ch, bh;
+    make_bluestein64(N, M, ch, bh);
+    bad = upload(t.chirp64, ch) || upload(t.bhat64, bh);
+    g.chirp64 = t.chirp64.p;
+    g.bhat64 = t.bhat64.p;
+  } else if (!bad) {
+    std::vector<float2> ch, bh;
+    make_bluestein(N, M, ch, bh);
+    bad = upload(t.chirp, ch) || upload(t.bhat, bh);
+    g.chirp = t.chirp.p;
+    g.bhat = t.bhat.p;
+  }
+  if (bad) { t.release(); return fail(LTE_ENOMEM, "tables"); }
   g.Nd = M;
-  g.chirp = t.chirp.p;
-  g.bhat = t.bhat.p;
-  DBuf<float2> di, dout;
+  DBuf<cx<R>> di, dout;
   if (di.alloc(batch * M) || dout.alloc(batch * M)) { t.release(); return fail(LTE_ENOMEM, "dft buffers"); }
   int rc = LTE_OK;
-  if (hipMemcpy(di.p, in, batch * M * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
-      launch_dft(nullptr, g, inverse, batch, di.p, dout.p) != 0 || hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(out, dout.p, batch * M * sizeof(float2), hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(di.p, in, batch * M * sizeof(cx<R>), hipMemcpyHostToDevice) != hipSuccess ||
+      launch_dft<R>(nullptr, g, inverse, batch, di.p, dout.p) != 0 || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, dout.p, batch * M * sizeof(cx<R>), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "dft failed");
   di.release(); dout.release(); t.release();
   return rc;
 }
 
-int lte_llr_host(int bps, int64_t n, const float* syms, const float* nv, float* llr) {
+template <class R>
+static int llr_host(int bps, int64_t n, const R* syms, const R* nv, R* llr) {
   if ((bps != 2 && bps != 4 && bps != 6) || n < 0) return fail(LTE_EINVAL, "bad llr arguments");
   if (n == 0) return LTE_OK;
-  DBuf<float2> ds;
-  DBuf<float> dn, dl;
+  DBuf<cx<R>> ds;
+  DBuf<R> dn, dl;
   if (ds.alloc(n) || dn.alloc(n) || dl.alloc(n * bps)) return fail(LTE_ENOMEM, "llr buffers");
   int rc = LTE_OK;
-  if (hipMemcpy(ds.p, syms, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(dn.p, nv, n * 4, hipMemcpyHostToDevice) != hipSuccess || launch_llr(nullptr, bps, n, ds.p, dn.p, dl.p) ||
-      hipMemcpy(llr, dl.p, n * bps * 4, hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(ds.p, syms, n * sizeof(cx<R>), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dn.p, nv, n * sizeof(R), hipMemcpyHostToDevice) != hipSuccess ||
+      launch_llr<R>(nullptr, bps, n, ds.p, dn.p, dl.p) ||
+      hipMemcpy(llr, dl.p, n * bps * sizeof(R), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "llr failed");
   ds.release(); dn.release(); dl.release();
   return rc;
 }
 
-int lte_hard_host(int bps, int64_t n, const float* syms, uint8_t* bits) {
+template <class R>
+static int hard_host(int bps, int64_t n, const R* syms, uint8_t* bits) {
   if ((bps != 2 && bps != 4 && bps != 6) || n < 0) return fail(LTE_EINVAL, "bad hard arguments");
   if (n == 0) return LTE_OK;
-  DBuf<float2> ds;
+  DBuf<cx<R>> ds;
   DBuf<uint8_t> db;
   if (ds.alloc(n) || db.alloc(n * bps)) return fail(LTE_ENOMEM, "buffers");
   int rc = LTE_OK;
-  if (hipMemcpy(ds.p, syms, n * 8, hipMemcpyHostToDevice) != hipSuccess || launch_hard(nullptr, bps, n, ds.p, db.p) ||
+  if (hipMemcpy(ds.p, syms, n * sizeof(cx<R>), hipMemcpyHostToDevice) != hipSuccess ||
+      launch_hard<R>(nullptr, bps, n, ds.p, db.p) ||
       hipMemcpy(bits, db.p, n * bps, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "hard failed");
   ds.release(); db.release();
   return rc;
+}
+
+extern "C" {
+
+int lte_fft_host(int N, int inverse, int64_t batch, const float* in, float* out) {
+  return fft_host<float>(N, inverse, batch, in, out);
+}
+int lte_fft_host64(int N, int inverse, int64_t batch, const double* in, double* out) {
+  return fft_host<double>(N, inverse, batch, in, out);
+}
+int lte_dft_host(int M, int inverse, int64_t batch, const float* in, float* out) {
+  return dft_host<float>(M, inverse, batch, in, out);
+}
+int lte_dft_host64(int M, int inverse, int64_t batch, const double* in, double* out) {
+  return dft_host<double>(M, inverse, batch, in, out);
+}
+int lte_llr_host(int bps, int64_t n, const float* syms, const float* nv, float* llr) {
+  return llr_host<float>(bps, n, syms, nv, llr);
+}
+int lte_llr_host64(int bps, int64_t n, const double* syms, const double* nv, double* llr) {
+  return llr_host<double>(bps, n, syms, nv, llr);
+}
+int lte_hard_host(int bps, int64_t n, const float* syms, uint8_t* bits) { return hard_host<float>(bps, n, syms, bits); }
+int lte_hard_host64(int bps, int64_t n, const double* syms, uint8_t* bits) {
+  return hard_host<double>(bps, n, syms, bits);
 }
 
 int lte_crc_host(int64_t n, const uint8_t* bits, uint32_t poly, int len, uint32_t* crc) {

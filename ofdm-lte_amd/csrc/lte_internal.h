@@ -59,16 +59,21 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
 size_t encode_scratch_words(int KWmax, int C, int B);
 int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
                   const CbInfo* cbi_dev, int C, int B, uint32_t* cw_scratch);
+// Signal-chain launchers, R = double (the reference's precision, default) or
+// float (fast mode); explicit instances in lte_kernels.hip.
+template <class R>
 int launch_ofdm_tx(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                   int enc_words, const int32_t* tx_map, float2* x, int B, float2* cap_syms = nullptr,
+                   int enc_words, const int32_t* tx_map, cx<R>* x, int B, cx<R>* cap_syms = nullptr,
                    int sc_fdm = 0);
-int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const float* gains_dev, const uint64_t* fid,
-                  uint64_t seed, const float* inj_ph, int64_t inj_stride, float* phases, float2* coef);
+template <class R>
+int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const R* gains_dev, const uint64_t* fid,
+                  uint64_t seed, const R* inj_ph, int64_t inj_stride, R* phases, cx<R>* coef);
+template <class R>
 int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh, int n_paths,
-                   const int32_t* delays_dev, const float* gains_dev, float fD, float fs, const float* phases,
-                   const float2* coef, const float2* x, float2* y, float* pow_part, int nblk, int max_delay);
-int launch_npow(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
-                float* npow);
+                   const int32_t* delays_dev, const R* gains_dev, R fD, R fs, const R* phases, const cx<R>* coef,
+                   const cx<R>* x, cx<R>* y, R* pow_part, int nblk, int max_delay);
+template <class R>
+int launch_npow(hipStream_t s, int B, int num_rx, const R* pow_part, int nblk, int L, const R* snr_lin, R* npow);
 int channel_nblk(int L);   // power partials per (frame, rx) written by launch_channel
 // OFDM TX with the static-tap multipath channel fused in (SISO, fD = 0, every
 // delay <= CP, N >= 512): k_ofdm_tx<.., CH> writes the received stream outside
@@ -77,36 +82,44 @@ int channel_nblk(int L);   // power partials per (frame, rx) written by launch_c
 // the power of the first max_delay samples, which need the previous symbol's
 // tail (kept per symbol in xh).  pow_part then holds n_sym partials per frame.
 constexpr int TXCH_MAXP = 8;
-struct TxChannel {
+template <class R>
+struct TxChannelT {
   int n_paths, max_delay;
   int delays[TXCH_MAXP];
-  const float2* coef;   // [B][n_paths]
-  float2* y;            // [B][L]
-  float2* xh;           // [B][n_sym][2 * max_delay]: first / last max_delay TX samples of each symbol
-  float* pow_part;      // [B][n_sym]
+  const cx<R>* coef;   // [B][n_paths]
+  cx<R>* y;            // [B][L]
+  cx<R>* xh;           // [B][n_sym][2 * max_delay]: first / last max_delay TX samples of each symbol
+  R* pow_part;         // [B][n_sym]
 };
 bool txch_supported(const Grid& g, int n_paths, int max_delay);
+template <class R>
 int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                      int enc_words, const int32_t* tx_map, int B, float2* cap_syms, const TxChannel& ch);
-int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannel& ch);
-int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const float2* y, int64_t y_rx_stride,
-                    int64_t y_frame_stride, const float* npow, const uint64_t* fid, uint64_t seed,
-                    const float* inj_z, int64_t inj_stride, float2* H, float* pstats);
-int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, int num_rx,
-                   const float2* y, int64_t y_rx_stride, int64_t y_frame_stride, const float2* H,
-                   const float* npow, const float* snr_lin, const uint64_t* fid, uint64_t seed,
-                   const float* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
-                   uint32_t* frame_err, float* llr, float2* cap_syms, uint8_t* cap_bits, int sc_fdm = 0,
-                   float* nv_out = nullptr);   // coded: nv_out set -> llr takes z (float2 per RE), nv_out sigma^2_eff
-// g0 / b0: first 64-frame group / first frame of a frame range [.., B) of the
-// plan's buffers (the pipelined chain runs the decoder side per chunk)
-int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
-                   const int64_t* rows, int C, int g0 = 0);
+                      int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch);
+template <class R>
+int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannelT<R>& ch);
+template <class R>
+int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>* y, int64_t y_rx_stride,
+                    int64_t y_frame_stride, const R* npow, const uint64_t* fid, uint64_t seed, const R* inj_z,
+                    int64_t inj_stride, cx<R>* H, R* pstats);
+// coded: nv_out set -> llr takes z (cx<R> per RE), nv_out sigma^2_eff
+template <class R>
+int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, int num_rx, const cx<R>* y,
+                   int64_t y_rx_stride, int64_t y_frame_stride, const cx<R>* H, const R* npow, const R* snr_lin,
+                   const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, const uint32_t* pw, int PW,
+                   int n_bits, uint32_t* frame_err, R* llr, cx<R>* cap_syms, uint8_t* cap_bits, int sc_fdm = 0,
+                   R* nv_out = nullptr);
+// Rate dematch into the decoder rows (rows of R: float / double).  rx_map
+// [n_layers][T]: layer 0 assigns, layers 1.. add in order (E > N_cb
+// repetition, rate_matching.py:433-436).  g0: first 64-frame group.
+template <class R>
+int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_map, int n_layers, R* const* blk,
+                   const int64_t* rows, int g0 = 0);
 // dematch with the soft demapper fused in: reads the equalised symbols z and
 // their noise variances ([B][n_re] each, from k_rx_data's nv_out mode) instead
 // of LLRs; same decoder rows as launch_dematch (bps 4 / 6)
-int launch_dematch_zn(hipStream_t s, const float2* z, const float* nv, int n_re, int bps, int B,
-                      const int32_t* rx_map, float* const* blk, const int64_t* rows, int g0 = 0);
+template <class R>
+int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int bps, int B, const int32_t* rx_map,
+                      int n_layers, R* const* blk, const int64_t* rows, int g0 = 0);
 // f64 != 0: the float64 decoder (bit-exact with the reference), blk / ckpt hold doubles
 int launch_turbo(hipStream_t s, void* blk, void* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
                  int G, int mode, int f64);
@@ -132,10 +145,14 @@ int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* cons
                      uint8_t* cap_bits, int b0 = 0);
 int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, int n_snr, const int32_t* snr_idx,
                       const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts);
-int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);
-int launch_dft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const float2* in, float2* out);
-int launch_llr(hipStream_t s, int bps, int64_t n, const float2* syms, const float* nv, float* llr);
-int launch_hard(hipStream_t s, int bps, int64_t n, const float2* syms, uint8_t* bits);
+template <class R>
+int launch_fft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const cx<R>* in, cx<R>* out);
+template <class R>
+int launch_dft(hipStream_t s, const Grid& g, int inverse, int64_t batch, const cx<R>* in, cx<R>* out);
+template <class R>
+int launch_llr(hipStream_t s, int bps, int64_t n, const cx<R>* syms, const R* nv, R* llr);
+template <class R>
+int launch_hard(hipStream_t s, int bps, int64_t n, const cx<R>* syms, uint8_t* bits);
 
 // ---------------------------------------------------------------- multi-antenna chains
 // SFBC 2xN (configs 4 / simulate_miso / simulate_mimo) and TM4 spatial
@@ -205,7 +222,7 @@ enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3, TM_FINAL = 4 };  // 
 // turbo geometry: rows of one (r, group) block = 4K+12:
 //   [0,K+3) LS (sys + sys1 tail) | [K+3,2K+6) LP1 | [2K+6,3K+9) LP2 | [3K+9,3K+12) LS2T | [3K+12,4K+12) LE
 __host__ __device__ inline int64_t turbo_rows(int K) { return 4LL * K + 12; }
-__host__ __device__ inline int turbo_nwin(int K) { return K / 4 + 1; }  // sized for windows >= 4
+__host__ __device__ inline int turbo_nwin(int K) { return K / 8 + 1; }  // checkpoint windows (>= 8 steps each)
 // alpha checkpoint rows per window: f32 states 1..7 (state 0 is 0 after
 // normalisation); f64 all 8 states (unnormalised, as the reference)
 constexpr int TURBO_CK_ROWS_F32 = 7;

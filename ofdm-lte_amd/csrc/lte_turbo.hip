@@ -11,93 +11,104 @@ namespace lte {
 constexpr int RS = TURBO_RS;   // decoder row stride (elements): 64 lanes
 
 // ---------------------------------------------------------------------------
-// RX rate-dematch + transpose into the decoder layout.
+// RX rate-dematch + transpose into the decoder layout, rows of R (double: the
+// default float64 chain; float: fast mode).
 // Replaces rate_dematching_turbo (rate_matching.py:374-489) composed with the
-// T/F de-interleaver (core/ofdm_core.py:1174-1207): rx_map[t] gives, for LLR t
-// of a frame in RE order, the destination (r<<24 | row) or -1.  A block loads
-// a [64 frames][256 t] tile (coalesced rows), then every wave writes whole
-// 256-B decoder rows.
+// T/F de-interleaver (core/ofdm_core.py:1174-1207): rx_map[layer][t] gives, for
+// LLR t of a frame in RE order, the destination (r<<24 | row) or -1.  Layer 0
+// writes 0.5 * (0 + llr) (the circular buffer starts at zero); layers 1.. hold
+// the repeats of E > N_cb and ADD in order (circular_buffer[pos] += llr[i],
+// rate_matching.py:433-436), one launch per layer so the sums keep the
+// reference's order.  Rows hold LLR/2: x/2 commutes with every rounded add.
+// A block loads a [64 frames][DM_CH t] tile (coalesced rows), then every wave
+// writes whole decoder rows (64 frames of one LLR).
 constexpr int DM_CH = 64;
-__global__ __launch_bounds__(256) void k_dematch(const float* __restrict__ llr, int T, int B,
-                                                 const int32_t* __restrict__ rx_map,
-                                                 float* const* __restrict__ blk, const int64_t* __restrict__ rows,
+template <class R>
+__device__ __forceinline__ void dm_store(R* dst, R v, bool add) {
+  if (add) *dst = *dst + (R)0.5 * v;
+  else *dst = (R)0.5 * ((R)0 + v);
+}
+
+template <class R>
+__global__ __launch_bounds__(256) void k_dematch(const R* __restrict__ llr, int T, int B,
+                                                 const int32_t* __restrict__ rx_map, int add,
+                                                 R* const* __restrict__ blk, const int64_t* __restrict__ rows,
                                                  int g0) {
-  __shared__ float tile[64][DM_CH + 1];   // [frame][t], +1: conflict-free column reads
+  __shared__ R tile[64][DM_CH + 1];   // [frame][t], +1: conflict-free column reads
   const int g = g0 + blockIdx.y;
   const int t0 = blockIdx.x * DM_CH;
   const int nt = min(DM_CH, T - t0);
-  // load: 16 lanes x float4 per frame row (256-B coalesced); scalar tail
+  // load: 16 lanes x 4 LLRs per frame row (coalesced); scalar tail
   const int c4 = (threadIdx.x & 15) * 4;
   for (int f = threadIdx.x >> 4; f < 64; f += 16) {
     const int b = g * 64 + f;
-    const float* src = llr + (size_t)b * T + t0;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const R* src = llr + (size_t)b * T + t0;
+    R v[4] = {(R)0, (R)0, (R)0, (R)0};
     if (b < B) {
-      if ((T & 3) == 0 && c4 + 3 < nt) v = *reinterpret_cast<const float4*>(src + c4);
-      else {
-        if (c4 + 0 < nt) v.x = src[c4 + 0];
-        if (c4 + 1 < nt) v.y = src[c4 + 1];
-        if (c4 + 2 < nt) v.z = src[c4 + 2];
-        if (c4 + 3 < nt) v.w = src[c4 + 3];
-      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c4 + e < nt) v[e] = src[c4 + e];
     }
-    tile[f][c4 + 0] = v.x;
-    tile[f][c4 + 1] = v.y;
-    tile[f][c4 + 2] = v.z;
-    tile[f][c4 + 3] = v.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[f][c4 + e] = v[e];
   }
   __syncthreads();
-  // store: each wave writes whole 256-B decoder rows (64 frames of one LLR)
+  // store: each wave writes whole decoder rows (64 frames of one LLR)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), f = threadIdx.x & 63;
   for (int c = wv; c < nt; c += 4) {
     const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
-    blk[r][((size_t)g * rows[r] + row) * RS + f] = 0.5f * tile[f][c];   // rows hold LLR/2 (exact)
+    dm_store(&blk[r][((size_t)g * rows[r] + row) * RS + f], tile[f][c], add != 0);
   }
 }
 
-int launch_dematch(hipStream_t s, const float* llr, int T, int B, const int32_t* rx_map, float* const* blk,
-                   const int64_t* rows, int C, int g0) {
-  (void)C;
+template <class R>
+int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_map, int n_layers, R* const* blk,
+                   const int64_t* rows, int g0) {
   const int G = (B + 63) / 64 - g0;   // groups g0 .. ceil(B/64)-1
-  if (G < 1 || G > 65535) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_dematch, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B, rx_map, blk, rows,
-                     g0);
-  return (int)hipGetLastError();
+  if (G < 1 || G > 65535 || n_layers < 1) return (int)hipErrorInvalidValue;
+  for (int k = 0; k < n_layers; ++k) {
+    hipLaunchKernelGGL(k_dematch<R>, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B,
+                       rx_map + (size_t)k * T, k > 0 ? 1 : 0, blk, rows, g0);
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+  }
+  return 0;
 }
 
 // Soft demap + dematch in one pass: a block covers DZ_RE resource elements of
-// 64 frames; it reads their equalised symbols and noise variances (12 B per RE
-// instead of 4 * bps B of LLRs), computes the max-log LLRs (soft_demap, the
-// function k_rx_data uses) into an LDS tile [frame][LLR], then writes whole
-// 256-B decoder rows exactly as k_dematch.
-constexpr int DZ_RE = 16;
-template <int BPS>
-__global__ __launch_bounds__(256) void k_dematch_zn(const float2* __restrict__ z, const float* __restrict__ nv,
-                                                    int n_re, int B, const int32_t* __restrict__ rx_map,
-                                                    float* const* __restrict__ blk,
-                                                    const int64_t* __restrict__ rows, int g0) {
-  constexpr int TC = DZ_RE * BPS, PER = 64 * DZ_RE / 256;
-  __shared__ float tile[64][TC + 1];
+// 64 frames; it reads their equalised symbols and noise variances (instead of
+// bps LLRs per RE), computes the max-log LLRs (soft_demap, the function
+// k_rx_data uses) into an LDS tile [frame][LLR], then writes whole decoder
+// rows exactly as k_dematch.  f64 covers 8 REs per block (49 KB tile at 16).
+template <class R> constexpr int dz_re() { return sizeof(R) == 8 ? 8 : 16; }
+template <class R, int BPS>
+__global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z, const R* __restrict__ nv, int n_re,
+                                                    int B, const int32_t* __restrict__ rx_map, int add,
+                                                    R* const* __restrict__ blk, const int64_t* __restrict__ rows,
+                                                    int g0) {
+  using V = cx<R>;
+  constexpr int DZ_RE = dz_re<R>(), TC = DZ_RE * BPS, PER = 64 * DZ_RE / 256;
+  __shared__ R tile[64][TC + 1];
   const int g = g0 + blockIdx.y;
   const int re0 = blockIdx.x * DZ_RE;
   const int nr = min(DZ_RE, n_re - re0);
   // every (z, nv) load of this thread issued before the demapping
-  float2 zv[PER];
-  float nvv[PER];
+  V zv[PER];
+  R nvv[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int e = threadIdx.x + k * 256, f = e / DZ_RE, r = e % DZ_RE, b = g * 64 + f;
     const bool ok = b < B && r < nr;
     const size_t i = (size_t)b * n_re + re0 + r;
-    zv[k] = ok ? z[i] : make_float2(0.f, 0.f);
-    nvv[k] = ok ? nv[i] : 1.f;
+    zv[k] = ok ? z[i] : mkc((R)0, (R)0);
+    nvv[k] = ok ? nv[i] : (R)1;
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int e = threadIdx.x + k * 256, f = e / DZ_RE, r = e % DZ_RE;
-    float o[BPS];
+    R o[BPS];
     soft_demap<BPS>(zv[k], nvv[k], o);
 #pragma unroll
     for (int m = 0; m < BPS; ++m) tile[f][r * BPS + m] = o[m];
@@ -109,19 +120,40 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const float2* __restrict__ z
     const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
-    blk[r][((size_t)g * rows[r] + row) * RS + f] = 0.5f * tile[f][c];   // rows hold LLR/2 (exact)
+    dm_store(&blk[r][((size_t)g * rows[r] + row) * RS + f], tile[f][c], add != 0);
   }
 }
 
-int launch_dematch_zn(hipStream_t s, const float2* z, const float* nv, int n_re, int bps, int B,
-                      const int32_t* rx_map, float* const* blk, const int64_t* rows, int g0) {
+template <class R>
+int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int bps, int B, const int32_t* rx_map,
+                      int n_layers, R* const* blk, const int64_t* rows, int g0) {
   const int G = (B + 63) / 64 - g0;
-  if (G < 1 || G > 65535 || (bps != 4 && bps != 6)) return (int)hipErrorInvalidValue;
-  const dim3 grid((n_re + DZ_RE - 1) / DZ_RE, G);
-  if (bps == 4) hipLaunchKernelGGL(k_dematch_zn<4>, grid, dim3(256), 0, s, z, nv, n_re, B, rx_map, blk, rows, g0);
-  else hipLaunchKernelGGL(k_dematch_zn<6>, grid, dim3(256), 0, s, z, nv, n_re, B, rx_map, blk, rows, g0);
-  return (int)hipGetLastError();
+  if (G < 1 || G > 65535 || (bps != 4 && bps != 6) || n_layers < 1) return (int)hipErrorInvalidValue;
+  constexpr int DZ = dz_re<R>();
+  const dim3 grid((n_re + DZ - 1) / DZ, G);
+  const int T = n_re * bps;
+  for (int k = 0; k < n_layers; ++k) {
+    const int32_t* mp = rx_map + (size_t)k * T;
+    if (bps == 4)
+      hipLaunchKernelGGL((k_dematch_zn<R, 4>), grid, dim3(256), 0, s, z, nv, n_re, B, mp, k > 0 ? 1 : 0, blk, rows,
+                         g0);
+    else
+      hipLaunchKernelGGL((k_dematch_zn<R, 6>), grid, dim3(256), 0, s, z, nv, n_re, B, mp, k > 0 ? 1 : 0, blk, rows,
+                         g0);
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+  }
+  return 0;
 }
+
+template int launch_dematch<float>(hipStream_t, const float*, int, int, const int32_t*, int, float* const*,
+                                   const int64_t*, int);
+template int launch_dematch<double>(hipStream_t, const double*, int, int, const int32_t*, int, double* const*,
+                                    const int64_t*, int);
+template int launch_dematch_zn<float>(hipStream_t, const float2*, const float*, int, int, int, const int32_t*, int,
+                                      float* const*, const int64_t*, int);
+template int launch_dematch_zn<double>(hipStream_t, const double2*, const double*, int, int, int, const int32_t*,
+                                       int, double* const*, const int64_t*, int);
 
 // ---------------------------------------------------------------------------
 // TX: CB construction (segmentation.py:212-247 + CRC-24B crc.py:162-184) and

@@ -21,6 +21,7 @@ CH_AWGN, CH_RAYLEIGH = 0, 1
 DET_MMSE, DET_ZF, DET_SIC, DET_MRC = 0, 1, 2, 3
 STAGE_TX, STAGE_CHANNEL, STAGE_RX, STAGE_ALL = 1, 2, 4, 7
 MAX_PATHS = 16
+PREC_DEFAULT, PREC_F32, PREC_F64 = 0, 32, 64
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 P = ctypes.POINTER
@@ -32,7 +33,7 @@ class PlanDesc(ctypes.Structure):
                 ('delays', c_i32 * MAX_PATHS), ('gains', c_f64 * MAX_PATHS), ('fD', c_f64), ('fs', c_f64),
                 ('n_bits', c_i32), ('turbo_iters', c_i32), ('max_frames', c_i32), ('cell_id', c_i32),
                 ('num_tx', c_i32), ('rank', c_i32), ('detector', c_i32), ('precoder', c_f64 * 32),
-                ('sc_fdm', c_i32), ('bf_adaptive', c_i32), ('no_equalization', c_i32)]
+                ('sc_fdm', c_i32), ('bf_adaptive', c_i32), ('no_equalization', c_i32), ('precision', c_i32)]
 
 
 class RunArgs(ctypes.Structure):
@@ -42,12 +43,12 @@ class RunArgs(ctypes.Structure):
                 ('phases', P(c_f64)), ('phases_stride', c_i64),
                 ('noise', P(c_f64)), ('noise_stride', c_i64),
                 ('counts', P(c_u64)), ('frame_errors', P(ctypes.c_uint32)), ('frame_crc_ok', P(ctypes.c_uint8)),
-                ('stages', c_i32), ('in_signal', P(ctypes.c_float)), ('in_signal_stride', c_i64),
-                ('cap_signal_tx', P(ctypes.c_float)), ('cap_signal_rx', P(ctypes.c_float)),
-                ('cap_data_syms', P(ctypes.c_float)), ('cap_H', P(ctypes.c_float)),
-                ('cap_pilot_stats', P(ctypes.c_float)), ('cap_bits_rx', P(ctypes.c_uint8)),
-                ('cap_llr', P(ctypes.c_float)), ('cap_noise_power', P(ctypes.c_float)),
-                ('cap_tx_syms', P(ctypes.c_float)),
+                ('stages', c_i32), ('in_signal', ctypes.c_void_p), ('in_signal_stride', c_i64),
+                ('cap_signal_tx', ctypes.c_void_p), ('cap_signal_rx', ctypes.c_void_p),
+                ('cap_data_syms', ctypes.c_void_p), ('cap_H', ctypes.c_void_p),
+                ('cap_pilot_stats', ctypes.c_void_p), ('cap_bits_rx', P(ctypes.c_uint8)),
+                ('cap_llr', ctypes.c_void_p), ('cap_noise_power', ctypes.c_void_p),
+                ('cap_tx_syms', ctypes.c_void_p),
                 ('link_noise', P(c_f64)), ('link_noise_stride', c_i64),
                 ('link_h', P(c_f64)), ('link_h_stride', c_i64),
                 ('cap_link_stats', P(ctypes.c_float)),
@@ -63,16 +64,21 @@ _SIGS = {
     'lte_plan_create': (ctypes.c_int, [P(PlanDesc), P(ctypes.c_void_p)]),
     'lte_plan_destroy': (ctypes.c_int, [ctypes.c_void_p]),
     'lte_plan_info': (ctypes.c_int, [ctypes.c_void_p, P(c_i64)]),
+    'lte_plan_precision': (ctypes.c_int, [ctypes.c_void_p]),
     'lte_run': (ctypes.c_int, [ctypes.c_void_p, P(RunArgs)]),
     'lte_timing_enable': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'lte_timing_read': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, P(c_f64), P(c_i64),
                                        ctypes.c_int]),
     'lte_timing_reset': (ctypes.c_int, [ctypes.c_void_p]),
     'lte_fft_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_fft_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(c_f64), P(c_f64)]),
     'lte_pilots': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P(c_f64)]),
     'lte_dft_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_dft_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(c_f64), P(c_f64)]),
     'lte_llr_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_llr_host64': (ctypes.c_int, [ctypes.c_int, c_i64, P(c_f64), P(c_f64), P(c_f64)]),
     'lte_hard_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_uint8)]),
+    'lte_hard_host64': (ctypes.c_int, [ctypes.c_int, c_i64, P(c_f64), P(ctypes.c_uint8)]),
     'lte_turbo_encode_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_uint8), P(ctypes.c_uint8)]),
     'lte_turbo_decode_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float),
                                              P(ctypes.c_uint8)]),
@@ -119,7 +125,7 @@ def load():
 PRECISIONS = ('f64', 'f32')
 
 
-def precision(p=None):
+def precision_of(p=None):
     """Arithmetic type of the GPU chains: 'f64' (the default -- the reference
     computes in float64 / complex128 throughout) or 'f32' (opt-in fast mode).
     LTE_PRECISION in the environment changes the default."""
@@ -160,25 +166,34 @@ def ptr(a, t):
 F32, U8, U32, U64, I32, F64 = ctypes.c_float, ctypes.c_uint8, ctypes.c_uint32, c_u64, c_i32, c_f64
 
 
-def fft(x, inverse=False):
-    """Batched N-point FFT/sqrt(N) (inverse: IFFT*sqrt(N)) on the GPU; x [..., N] complex."""
+def _cdtype(prec):
+    return (np.complex128, np.float64, F64) if prec == 'f64' else (np.complex64, np.float32, F32)
+
+
+def fft(x, inverse=False, precision=None):
+    """Batched N-point FFT/sqrt(N) (inverse: IFFT*sqrt(N)) on the GPU; x [..., N] complex.
+    precision 'f64' (default, complex128) or 'f32' (complex64)."""
     device_init()
-    x = np.ascontiguousarray(x, dtype=np.complex64)
+    prec = precision_of(precision)
+    cdt, rdt, ct = _cdtype(prec)
+    x = np.ascontiguousarray(x, dtype=cdt)
     N = x.shape[-1]
     out = np.empty_like(x)
-    check(load().lte_fft_host(N, 1 if inverse else 0, x.size // N, ptr(x.view(np.float32), F32),
-                              ptr(out.view(np.float32), F32)))
+    f = load().lte_fft_host64 if prec == 'f64' else load().lte_fft_host
+    check(f(N, 1 if inverse else 0, x.size // N, ptr(x.view(rdt), ct), ptr(out.view(rdt), ct)))
     return out
 
 
-def dft(x, inverse=False):
+def dft(x, inverse=False, precision=None):
     """SC-FDM DFT (inverse: IDFT) of size M = x.shape[-1], unitary (1/sqrt(M)), on the GPU."""
     device_init()
-    x = np.ascontiguousarray(x, dtype=np.complex64)
+    prec = precision_of(precision)
+    cdt, rdt, ct = _cdtype(prec)
+    x = np.ascontiguousarray(x, dtype=cdt)
     M = x.shape[-1]
     out = np.empty_like(x)
-    check(load().lte_dft_host(M, 1 if inverse else 0, x.size // M, ptr(x.view(np.float32), F32),
-                              ptr(out.view(np.float32), F32)))
+    f = load().lte_dft_host64 if prec == 'f64' else load().lte_dft_host
+    check(f(M, 1 if inverse else 0, x.size // M, ptr(x.view(rdt), ct), ptr(out.view(rdt), ct)))
     return out
 
 
@@ -210,3 +225,6 @@ def mimo_detect(det, y, H, sigma2, W, bps=0):
                                       ptr(H.view(np.float64), F64), ptr(W.view(np.float64), F64), float(sigma2),
                                       ptr(out.view(np.float64), F64)))
     return out
+
+
+precision = precision_of   # short alias used by the coding entry points

@@ -18,7 +18,7 @@ from . import _capi as C
 class Plan:
     def __init__(self, *, N, Nc, cp_len, bps, n_sym, chain, channel, num_rx=1, delays=(), gains=(), fD=0.0,
                  fs=0.0, n_bits, turbo_iters=8, max_frames=1, cell_id=0, num_tx=1, rank=0, detector=0,
-                 precoder=(), sc_fdm=0, bf_adaptive=0, no_equalization=0):
+                 precoder=(), sc_fdm=0, bf_adaptive=0, no_equalization=0, precision=None):
         C.device_init()
         d = C.PlanDesc()
         d.N, d.Nc, d.cp_len, d.bps, d.n_sym = N, Nc, cp_len, bps, n_sym
@@ -34,6 +34,11 @@ class Plan:
         d.num_tx = int(num_tx)
         d.rank, d.detector, d.sc_fdm, d.bf_adaptive = int(rank), int(detector), int(sc_fdm), int(bf_adaptive)
         d.no_equalization = int(no_equalization)
+        # SISO / SIMO chains: float64 (the reference's arithmetic) unless 'f32' is
+        # asked for; the multi-antenna / beamforming chains run float32
+        multi = chain >= C.CHAIN_SFBC
+        d.precision = C.PREC_DEFAULT if multi else (C.PREC_F64 if C.precision_of(precision) == 'f64'
+                                                     else C.PREC_F32)
         if rank and num_tx <= 4 and rank <= 4:   # W [num_tx][rank] -> the [4][4] table of lte_plan_desc.precoder
             #                                    (larger arrays: lte_plan_create rejects them, LTE_EUNSUP)
             W = np.asarray(precoder, dtype=np.complex128).reshape(int(num_tx), int(rank))
@@ -49,6 +54,10 @@ class Plan:
         C.check(C.load().lte_plan_info(h, C.ptr(info, C.c_i64)))
         self.L, self.n_sym, self.Nd, self.Np, self.n_grp, self.n_cb, self.coded_bits, self.n_re_bits = \
             (int(v) for v in info)
+        self.precision = 'f64' if C.load().lte_plan_precision(h) == C.PREC_F64 else 'f32'
+        # element types of in_signal and the real / complex captures
+        self.cdt = np.complex128 if self.precision == 'f64' else np.complex64
+        self.rdt = np.float64 if self.precision == 'f64' else np.float32
         self.num_rx, self.N, self.bps, self.n_bits, self.max_frames = num_rx, N, bps, int(n_bits), int(max_frames)
         self.chain = chain
         self.num_tx = int(num_tx)
@@ -128,32 +137,33 @@ class Plan:
             a.frame_crc_ok = C.ptr(crc, C.U8)
             out['crc_ok'] = crc
         a.stages = int(stages)
+        cdt, rdt = self.cdt, self.rdt
         if in_signal is not None:
-            xs = np.ascontiguousarray(in_signal, dtype=np.complex64).reshape(-1, self.L)
+            xs = np.ascontiguousarray(in_signal, dtype=cdt).reshape(-1, self.L)
             keep.append(xs)
-            a.in_signal = C.ptr(xs.view(np.float32), C.F32)
+            a.in_signal = xs.ctypes.data
             a.in_signal_stride = 0 if xs.shape[0] == 1 else 2 * self.L
         shapes = {
-            'signal_tx': ((B, self.L), np.complex64, 'cap_signal_tx', C.F32),
-            'signal_rx': ((B, self.num_rx, self.L), np.complex64, 'cap_signal_rx', C.F32),
-            'data_syms': ((B, self.n_sym * self.Nd), np.complex64, 'cap_data_syms', C.F32),
-            'H': ((B, self.num_rx, self.n_grp, self.N), np.complex64, 'cap_H', C.F32),
-            'pilot_stats': ((B, self.num_rx, self.n_grp, 2), np.float32, 'cap_pilot_stats', C.F32),
+            'signal_tx': ((B, self.L), cdt, 'cap_signal_tx', None),
+            'signal_rx': ((B, self.num_rx, self.L), cdt, 'cap_signal_rx', None),
+            'data_syms': ((B, self.n_sym * self.Nd), cdt, 'cap_data_syms', None),
+            'H': ((B, self.num_rx, self.n_grp, self.N), cdt, 'cap_H', None),
+            'pilot_stats': ((B, self.num_rx, self.n_grp, 2), rdt, 'cap_pilot_stats', None),
             'bits_rx': ((B, self.n_bits), np.uint8, 'cap_bits_rx', C.U8),
-            'llr': ((B, self.n_re_bits), np.float32, 'cap_llr', C.F32),
-            'noise_power': ((B, self.num_rx), np.float32, 'cap_noise_power', C.F32),
-            'tx_syms': ((B, self.n_sym * self.Nd), np.complex64, 'cap_tx_syms', C.F32),
+            'llr': ((B, self.n_re_bits), rdt, 'cap_llr', None),
+            'noise_power': ((B, self.num_rx), rdt, 'cap_noise_power', None),
+            'tx_syms': ((B, self.n_sym * self.Nd), cdt, 'cap_tx_syms', None),
         }
         if self.mimo:
             shapes.update({
-                'signal_tx': ((B, self.num_tx, self.L), np.complex64, 'cap_signal_tx', C.F32),
-                'data_syms': ((B, self.n_sym * self.res), np.complex64, 'cap_data_syms', C.F32),
-                'H': ((B, self.num_rx, self.n_est, self.num_tx, self.n_dsc), np.complex64, 'cap_H', C.F32),
+                'signal_tx': ((B, self.num_tx, self.L), cdt, 'cap_signal_tx', None),
+                'data_syms': ((B, self.n_sym * self.res), cdt, 'cap_data_syms', None),
+                'H': ((B, self.num_rx, self.n_est, self.num_tx, self.n_dsc), cdt, 'cap_H', None),
                 'link_stats': ((B, self.num_rx, self.num_tx, 4), np.float32, 'cap_link_stats', C.F32)})
             shapes.pop('pilot_stats')
             shapes.pop('tx_syms')
         if self.bf:
-            shapes.update({'H': ((B, self.num_rx, self.num_tx), np.complex64, 'cap_H', C.F32),
+            shapes.update({'H': ((B, self.num_rx, self.num_tx), cdt, 'cap_H', None),
                            'pmi': ((B,), np.int32, 'cap_pmi', C.I32),
                            'bf_gain': ((B,), np.float32, 'cap_bf_gain', C.F32)})
             for k in ('pilot_stats', 'tx_syms', 'signal_tx', 'signal_rx', 'llr', 'noise_power'):
@@ -161,8 +171,8 @@ class Plan:
         for name in capture:
             shp, dt, field, ct = shapes[name]
             arr = np.zeros(shp, dtype=dt)
-            view = arr.view(np.float32) if dt == np.complex64 else arr
-            setattr(a, field, C.ptr(view, ct))
+            # void* fields take the address; typed fields a ctypes pointer
+            setattr(a, field, arr.ctypes.data if ct is None else C.ptr(arr, ct))
             out[name] = arr
         C.check(C.load().lte_run(self.h, ctypes.byref(a)))
         del keep
@@ -189,6 +199,7 @@ _CACHE_MAX = 8
 
 
 def get_plan(**kw):
+    kw['precision'] = C.precision_of(kw.get('precision'))   # resolved now: part of the cache key
     key = tuple(sorted((k, tuple(v) if isinstance(v, (list, tuple, np.ndarray)) else v) for k, v in kw.items()))
     p = _CACHE.get(key)
     if p is None:

@@ -471,9 +471,13 @@ class OFDMSimulator:
 
     def __init__(self, config: Optional[LTEConfig] = None, channel_type: str = 'awgn', mode: str = 'lte',
                  enable_sc_fdm: bool = False, enable_equalization: bool = True, num_channels: int = 1,
-                 itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0.0):
+                 itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0.0,
+                 *, precision: Optional[str] = None):
+        """precision (not in the reference): arithmetic type of the SISO / SIMO GPU
+        chains, 'f64' (default; the reference's float64) or 'f32' (fast mode)."""
         if config is None:
             config = LTEConfig()
+        self.precision = C.precision_of(precision)
         self.config, self.channel_type, self.mode = config, channel_type, mode
         self.enable_sc_fdm, self.enable_equalization = enable_sc_fdm, enable_equalization
         self.itu_profile, self.frequency_ghz, self.velocity_kmh = itu_profile, frequency_ghz, velocity_kmh
@@ -508,7 +512,7 @@ class OFDMSimulator:
         return get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
                         chain=chain, channel=ch.kind, num_rx=num_rx, delays=tuple(ch.delays),
                         gains=tuple(ch.gains), fD=ch.fD, fs=cfg.fs, n_bits=n_bits, turbo_iters=iters,
-                        max_frames=max_frames, sc_fdm=sc, no_equalization=noeq)
+                        max_frames=max_frames, sc_fdm=sc, no_equalization=noeq, precision=self.precision)
 
     def _ref_draws(self, L, num_rx=1):
         """Exactly the global-RNG consumption of one reference simulate_* call:

@@ -90,8 +90,10 @@ def test_api_surface_matches_reference_signatures():
     import inspect
     import lte_phy
     sig = inspect.signature(lte_phy.OFDMSimulator.__init__)
+    # the reference's parameters, in order; then our keyword-only precision switch
     assert list(sig.parameters)[1:] == ['config', 'channel_type', 'mode', 'enable_sc_fdm', 'enable_equalization',
-                                        'num_channels', 'itu_profile', 'frequency_ghz', 'velocity_kmh']
+                                        'num_channels', 'itu_profile', 'frequency_ghz', 'velocity_kmh', 'precision']
+    assert sig.parameters['precision'].kind == inspect.Parameter.KEYWORD_ONLY
     assert sig.parameters['velocity_kmh'].default == 0.0
     s2 = inspect.signature(lte_phy.OFDMSimulator.simulate_simo)
     assert [p.default for p in list(s2.parameters.values())[2:]] == [10.0, 2, 'mrc', True]

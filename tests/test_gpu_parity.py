@@ -1,11 +1,13 @@
 """GPU parity: the HIP path (through the C ABI) against the oracle / golden
-vectors.  Tolerances: the GPU computes in float32, the reference in float64.
-  * FFT: relative L2 error <= 2e-6 (f32 round-off of a 2048-point transform)
+vectors.  The chains run in float64 by default (the reference's arithmetic);
+float32 is the opt-in fast mode.  Tolerances:
+  * FFT: relative L2 error <= 1e-14 (f64) / 2e-6 (f32) vs np.fft
   * integer/bit work (turbo encoder, CRC, packing): bit-exact
-  * decisions (hard bits, turbo decoded bits): exact except for points whose
-    float64 decision metric sits within f32 round-off of a boundary; counted
-    and bounded below
-  * BER at every SNR point: |BER_gpu - BER_ref| < 1e-3 (north_star tolerance)
+  * turbo decoder: f64 bit-exact with the reference; f32 bit-exact with its
+    float32 model (oracle turbo_decode_f32_model)
+  * end-to-end vs the reference's own outputs on its own random numbers: f64
+    bit errors and CRC verdicts equal; f32 |BER_gpu - BER_ref| < 1e-3 (the
+    north_star tolerance) where the reference decodes
 """
 import numpy as np
 import pytest
@@ -23,50 +25,74 @@ def C():
     return _capi
 
 
+TOL_FFT = {'f64': 1e-14, 'f32': 2e-6}
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('N', [128, 256, 512, 1024, 2048])
-def test_fft_matches_numpy(C, N):
+def test_fft_matches_numpy(C, N, prec):
     rs = np.random.RandomState(N)
-    x = (rs.randn(37, N) + 1j * rs.randn(37, N)).astype(np.complex64)
-    f = C.fft(x, inverse=False)
-    ref = np.fft.fft(x.astype(np.complex128), axis=1) / np.sqrt(N)
-    assert np.linalg.norm(f - ref) / np.linalg.norm(ref) < 2e-6
-    i = C.fft(x, inverse=True)
-    ref = np.fft.ifft(x.astype(np.complex128), axis=1) * np.sqrt(N)
-    assert np.linalg.norm(i - ref) / np.linalg.norm(ref) < 2e-6
+    x = rs.randn(37, N) + 1j * rs.randn(37, N)
+    if prec == 'f32':
+        x = x.astype(np.complex64).astype(np.complex128)
+    f = C.fft(x, inverse=False, precision=prec)
+    ref = np.fft.fft(x, axis=1) / np.sqrt(N)
+    assert np.linalg.norm(f - ref) / np.linalg.norm(ref) < TOL_FFT[prec]
+    i = C.fft(x, inverse=True, precision=prec)
+    ref = np.fft.ifft(x, axis=1) * np.sqrt(N)
+    assert np.linalg.norm(i - ref) / np.linalg.norm(ref) < TOL_FFT[prec]
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mod', MODS)
-def test_hard_decision(C, golden, oracle, mod):
+def test_hard_decision(C, golden, oracle, mod, prec):
     pts = golden[f'qam_{mod}_pts']
     bps = oracle.BPS[mod]
-    x = pts.astype(np.complex64)
-    out = np.zeros(len(x) * bps, dtype=np.uint8)
-    C.check(C.load().lte_hard_host(bps, len(x), C.ptr(x.view(np.float32), C.F32), C.ptr(out, C.U8)))
+    out = np.zeros(len(pts) * bps, dtype=np.uint8)
+    if prec == 'f64':
+        x = np.ascontiguousarray(pts, dtype=np.complex128)
+        C.check(C.load().lte_hard_host64(bps, len(x), C.ptr(x.view(np.float64), C.F64), C.ptr(out, C.U8)))
+    else:
+        x = pts.astype(np.complex64)
+        C.check(C.load().lte_hard_host(bps, len(x), C.ptr(x.view(np.float32), C.F32), C.ptr(out, C.U8)))
     ref = golden[f'qam_{mod}_hard']
     # exact away from decision boundaries (the golden set deliberately puts a
-    # third of its points ON boundaries, where f32 and f64 round differently)
+    # third of its points ON boundaries, where the reference's argmin of
+    # hypot distances and a per-axis slicer may round a tie differently)
     nl = {2: 2, 4: 4, 6: 8}[bps]
     sc = {2: np.sqrt(2), 4: np.sqrt(10), 6: np.sqrt(42)}[bps]
     bnd = np.array([0.0]) if bps == 2 else (np.arange(1, nl) * 2 - nl) / sc
     far = np.ones(len(pts), bool)
     for v in (pts.real, pts.imag):
-        far &= np.min(np.abs(v[:, None] - bnd[None, :]), axis=1) > 1e-5
+        far &= np.min(np.abs(v[:, None] - bnd[None, :]), axis=1) > (1e-12 if prec == 'f64' else 1e-5)
     far_bits = np.repeat(far, bps)
     assert far.sum() > len(pts) // 2
     assert np.array_equal(out[far_bits], ref[far_bits])
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mod', MODS)
-def test_llr(C, golden, oracle, mod):
+def test_llr(C, golden, oracle, mod, prec):
     pts, nv = golden['llr_pts'], golden['llr_nv']
     bps = oracle.BPS[mod]
-    x = pts.astype(np.complex64)
-    n32 = nv.astype(np.float32)
-    out = np.zeros(len(x) * bps, dtype=np.float32)
-    C.check(C.load().lte_llr_host(bps, len(x), C.ptr(x.view(np.float32), C.F32), C.ptr(n32, C.F32),
-                                  C.ptr(out, C.F32)))
     ref = golden[f'llr_{mod}']
-    assert np.max(np.abs(out - ref) / (1 + np.abs(ref))) < 1e-4
+    if prec == 'f64':
+        # float64 max-log LLRs; the reference takes min |y - c|^2 over the 2-D
+        # constellation (np.abs = hypot), the kernel the separable per-axis
+        # minimum (the other axis' term cancels): equal up to f64 round-off
+        x = np.ascontiguousarray(pts, dtype=np.complex128)
+        n64 = np.ascontiguousarray(nv, dtype=np.float64)
+        out = np.zeros(len(x) * bps)
+        C.check(C.load().lte_llr_host64(bps, len(x), C.ptr(x.view(np.float64), C.F64), C.ptr(n64, C.F64),
+                                        C.ptr(out, C.F64)))
+        assert np.max(np.abs(out - ref) / (1 + np.abs(ref))) < 1e-12
+    else:
+        x = pts.astype(np.complex64)
+        n32 = nv.astype(np.float32)
+        out = np.zeros(len(x) * bps, dtype=np.float32)
+        C.check(C.load().lte_llr_host(bps, len(x), C.ptr(x.view(np.float32), C.F32), C.ptr(n32, C.F32),
+                                      C.ptr(out, C.F32)))
+        assert np.max(np.abs(out - ref) / (1 + np.abs(ref))) < 1e-4
 
 
 @pytest.mark.parametrize('K', [40, 1024, 5568, 5632, 6144])
@@ -166,39 +192,46 @@ def test_turbo_decode_batch_vs_oracle(C, oracle, K, n, snr):
         assert np.array_equal(dec[i], oracle.turbo_decode_f32_model(l32[i], K, 8)), i
 
 
-def _sim(bw, mod, chan):
+def _sim(bw, mod, chan, prec=None, **kw):
     import lte_phy
-    return lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type=chan)
+    return lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type=chan,
+                                 precision=prec, **kw)
 
 
 def _state_head():
     return np.array(np.random.get_state()[1][:8], dtype=np.uint32)
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('name,bw,mod,chan,snrs', [
     ('e2e_c1', 1.25, 'QPSK', 'awgn', [0, 5, 10]),
     ('e2e_c1odd', 1.25, 'QPSK', 'awgn', [3]),
     ('e2e_c2', 20.0, '64-QAM', 'rayleigh_mp', [0, 10, 20, 30]),
     ('e2e_c2awgn', 20.0, '16-QAM', 'awgn', [12])])
-def test_simulate_siso_ref_compat(C, golden, name, bw, mod, chan, snrs):
-    """Drop-in OFDMSimulator.simulate_siso == the reference's own output (frozen RNG)."""
-    sim = _sim(bw, mod, chan)
+def test_simulate_siso_ref_compat(C, golden, name, bw, mod, chan, snrs, prec):
+    """Drop-in OFDMSimulator.simulate_siso == the reference's own output (frozen
+    RNG).  f64: identical received bits; f32: within the north-star 1e-3."""
+    sim = _sim(bw, mod, chan, prec)
     nb = int(golden[name + '_nbits'][0])
     bits = unpack(golden[name + '_bits'], nb).astype(np.int64)
     for snr in snrs:
         k = f'{name}_snr{snr}'
         r = sim.simulate_siso(bits, snr)
         ref_err = int(golden[k + '_errors'][0])
-        assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
         diff = np.mean(r['bits_received_array'] != unpack(golden[k + '_rx'], nb))
-        assert diff < 1e-3, (k, diff)
-        assert abs(r['papr_db'] - golden[k + '_papr'][0]) < 1e-3
+        if prec == 'f64':
+            assert r['bit_errors'] == ref_err and diff == 0, (k, r['bit_errors'], ref_err, diff)
+        else:
+            assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
+            assert diff < 1e-3, (k, diff)
+        assert abs(r['papr_db'] - golden[k + '_papr'][0]) < (1e-9 if prec == 'f64' else 1e-3)
         assert np.array_equal(_state_head(), golden[k + '_state']), 'global RNG side effects differ'
 
 
-def test_simulate_siso_signals_vs_oracle(C, oracle, golden):
+@pytest.mark.parametrize('prec,tol', [('f64', 1e-13), ('f32', 1e-5)])
+def test_simulate_siso_signals_vs_oracle(C, oracle, golden, prec, tol):
     """Sample-level parity of the captured TX / RX streams (config 2)."""
-    sim = _sim(20.0, '64-QAM', 'rayleigh_mp')
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
     nb = int(golden['e2e_c2_nbits'][0])
     bits = unpack(golden['e2e_c2_bits'], nb).astype(np.int64)
     r = sim.simulate_siso(bits, 20)
@@ -206,23 +239,27 @@ def test_simulate_siso_signals_vs_oracle(C, oracle, golden):
     o = oracle.simulate_siso(num, bits, 20, 'rayleigh_mp')
     for key in ['signal_tx', 'signal_rx']:
         a, b = r[key], o[key]
-        assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-5, key
+        assert np.linalg.norm(a - b) / np.linalg.norm(b) < tol, key
     a, b = r['symbols_rx'], o['symbols_rx']
-    assert np.median(np.abs(a - b)) < 1e-4
+    assert np.median(np.abs(a - b)) < (1e-12 if prec == 'f64' else 1e-4)
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('name,bw,mod,chan,snrs,nrx', [
     ('e2e_c3', 10.0, '16-QAM', 'rayleigh_mp', [5, 15], 4),
     ('e2e_c1simo', 1.25, 'QPSK', 'awgn', [2], 2)])
-def test_simulate_simo_ref_compat(C, golden, name, bw, mod, chan, snrs, nrx):
-    sim = _sim(bw, mod, chan)
+def test_simulate_simo_ref_compat(C, golden, name, bw, mod, chan, snrs, nrx, prec):
+    sim = _sim(bw, mod, chan, prec)
     nb = int(golden[name + '_nbits'][0])
     bits = unpack(golden[name + '_bits'], nb).astype(np.int64)
     for snr in snrs:
         k = f'{name}_snr{snr}'
         r = sim.simulate_simo(bits, snr, num_rx=nrx, parallel=False)
         ref_err = int(golden[k + '_errors'][0])
-        assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
+        if prec == 'f64':
+            assert r['bit_errors'] == ref_err, (k, r['bit_errors'], ref_err)
+        else:
+            assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
         assert np.array_equal(_state_head(), golden[k + '_state'])
 
 
@@ -231,15 +268,34 @@ def test_simulate_simo_ref_compat(C, golden, name, bw, mod, chan, snrs, nrx):
     ('e2e_cod_c2s', 20.0, '64-QAM', 'rayleigh_mp', [8, 20]),
     ('e2e_cod_c2', 20.0, '64-QAM', 'rayleigh_mp', [20])])
 def test_simulate_siso_coded_ref_compat(C, golden, name, bw, mod, chan, snrs):
-    """Headline chain (TX coding -> Rayleigh -> RX + turbo) vs the reference.
-    Frames the reference decodes cleanly must decode cleanly with identical
-    CRC.  Where the reference's decoder fails (BER ~0.4: past the turbo
-    cliff, f32 round-off changes which wrong bits come out) the GPU must fail
-    too, with BER within 0.1; the decoder itself is pinned bit-exact against
-    its f32 model by test_coded_rx_decode_vs_oracle_on_philox_frames."""
-    sim = _sim(bw, mod, chan)
+    """Headline chain (TX coding -> Rayleigh -> RX + turbo) in float64 vs the
+    reference's own output on its own random numbers: identical bit errors,
+    CRC verdict, measured SNR and noise variance, and global-RNG state --
+    including the frames the reference fails to decode (past the turbo cliff)."""
+    sim = _sim(bw, mod, chan, 'f64')
     if name + '_nbits' not in golden:
         pytest.skip('slow golden vector absent')
+    nb = int(golden[name + '_nbits'][0])
+    bits = unpack(golden[name + '_bits'], nb).astype(np.int64)
+    for snr in snrs:
+        k = f'{name}_snr{snr}'
+        r = sim.simulate_siso_coded(bits, snr)
+        ref_err = int(golden[k + '_errors'][0])
+        assert r['bit_errors'] == ref_err, (k, r['bit_errors'], ref_err)
+        assert bool(r['crc_pass']) == bool(int(golden[k + '_crc'][0])), k
+        assert abs(r['channel_snr_db'] - golden[k + '_chsnr'][0]) < 1e-9
+        assert abs(r['noise_var_mean'] / golden[k + '_nvmean'][0] - 1) < 1e-12
+        assert np.array_equal(_state_head(), golden[k + '_state'])
+
+
+@pytest.mark.parametrize('name,bw,mod,chan,snrs', [
+    ('e2e_cod_small', 1.25, 'QPSK', 'awgn', [0, 6]),
+    ('e2e_cod_c2s', 20.0, '64-QAM', 'rayleigh_mp', [8, 20])])
+def test_simulate_siso_coded_ref_compat_f32(C, golden, name, bw, mod, chan, snrs):
+    """f32 fast mode on the same vectors: frames the reference decodes decode
+    cleanly with identical CRC; past the turbo cliff f32 round-off changes which
+    wrong bits come out, so only the CRC verdict is compared there."""
+    sim = _sim(bw, mod, chan, 'f32')
     nb = int(golden[name + '_nbits'][0])
     bits = unpack(golden[name + '_bits'], nb).astype(np.int64)
     for snr in snrs:
@@ -250,9 +306,6 @@ def test_simulate_siso_coded_ref_compat(C, golden, name, bw, mod, chan, snrs):
             assert r['bit_errors'] == 0 and r['crc_pass'] and int(golden[k + '_crc'][0]) == 1, k
         else:
             assert not r['crc_pass'] and int(golden[k + '_crc'][0]) == 0, k
-            assert abs(r['ber'] - ref_err / nb) < 0.1, (k, r['ber'], ref_err / nb)
-        assert abs(r['channel_snr_db'] - golden[k + '_chsnr'][0]) < 1e-3
-        assert abs(r['noise_var_mean'] / golden[k + '_nvmean'][0] - 1) < 1e-4
         assert np.array_equal(_state_head(), golden[k + '_state'])
 
 
@@ -270,9 +323,10 @@ def test_run_ber_sweep_matches_reference_semantics(C, golden):
         assert res['papr_values'][i] == np.mean([one['papr_db']] * 3)
 
 
-def test_run_grid_sharding_invariant(C):
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+def test_run_grid_sharding_invariant(C, prec):
     """Philox keyed by global frame id: 2-way sharded counts sum to the unsharded counts."""
-    sim = _sim(20.0, '64-QAM', 'rayleigh_mp')
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
     a = sim.run_grid([5.0, 15.0], 40, seed=7)
     b0 = sim.run_grid([5.0, 15.0], 40, seed=7, rank=0, world_size=2)
     b1 = sim.run_grid([5.0, 15.0], 40, seed=7, rank=1, world_size=2)
@@ -303,16 +357,18 @@ def test_run_grid_statistics_vs_oracle(C, oracle):
         assert abs(p_gpu - p_ref) <= 0.35 * p_ref + 2e-3, (snr, p_gpu, p_ref)
 
 
-def test_coded_rx_decode_vs_oracle_on_philox_frames(C, oracle):
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+def test_coded_rx_decode_vs_oracle_on_philox_frames(C, oracle, prec):
     """RX decode path (T/F de-interleave + rate dematch + turbo + desegment +
     CRC) on realistic Philox frames: feed the GPU's own LLRs (captured) to the
-    oracle's RX decode chain.  With the f32 decoder model: decoded TB bits and
-    CRC verdicts bit-exact; with the float64 reference decoder: bit-exact on
-    every frame the reference decodes (CRC pass)."""
-    sim = _sim(20.0, '64-QAM', 'rayleigh_mp')
+    oracle's RX decode chain.  f64: the reference's float64 decoder gives the
+    GPU's decoded TB bits and CRC verdicts on every frame; f32: its float32
+    decoder model does."""
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
     plan = sim._plan(C.CHAIN_CODED, 0, 27760, max_frames=8)
     snrs = np.array([6, 9, 12, 15, 18, 21, 24, 30], dtype=np.float64)
     r = plan.run(snrs, seed=11, capture=('llr', 'bits_rx'))
+    assert r['llr'].dtype == (np.float64 if prec == 'f64' else np.float32)
     num = oracle.Numerology(bandwidth=20.0, modulation='64-QAM')
     bps, Nd = 6, num.Nd
     coded = plan.coded_bits
@@ -327,26 +383,23 @@ def test_coded_rx_decode_vs_oracle_on_philox_frames(C, oracle):
     for b in range(len(snrs)):
         L_re = r['llr'][b].astype(np.float64).reshape(-1, bps)
         L = L_re[src_re].reshape(-1)[:coded]
-        dec, ok = oracle.coded_rx_decode(L, seg_plan, rm, 8, f32_model=True)
+        dec, ok = oracle.coded_rx_decode(L, seg_plan, rm, 8, f32_model=(prec == 'f32'))
         assert np.array_equal(dec, r['bits_rx'][b]) and bool(ok) == bool(r['crc_ok'][b]), b
-        dec64, ok64 = oracle.coded_rx_decode(L, seg_plan, rm, 8)
-        if ok64:
-            n_ok += 1
-            assert np.array_equal(dec64, r['bits_rx'][b]) and r['crc_ok'][b] == 1, b
-    assert n_ok >= 2
+        n_ok += int(ok)
+    assert 2 <= n_ok < len(snrs)   # decoded and failed frames both covered
 
 
+@pytest.mark.parametrize('prec,tol', [('f64', 1e-12), ('f32', 1e-4)])
 @pytest.mark.parametrize('bw,mod', [(20.0, '64-QAM'), (5.0, '16-QAM'), (1.25, 'QPSK')])
-def test_coded_chain_llrs_vs_oracle(C, oracle, bw, mod):
+def test_coded_chain_llrs_vs_oracle(C, oracle, bw, mod, prec, tol):
     """In-chain soft demapper: the LLRs k_rx_data writes == the oracle's max-log
     LLRs (core/ofdm_core.py:791-923) of the same equalised symbols with the
     same per-RE noise variance (ofdm_core.py:1224-1243)."""
-    sim = _sim(bw, mod, 'rayleigh_mp')
+    sim = _sim(bw, mod, 'rayleigh_mp', prec)
     plan = sim._plan(C.CHAIN_CODED, 0, 2000, max_frames=3)
     snrs = np.array([3.0, 12.0, 25.0])
     r = plan.run(snrs, seed=5, capture=('llr', 'data_syms', 'H'))
     num = oracle.Numerology(bandwidth=bw, modulation=mod)
-    bps = oracle.BPS[mod]
     for b, snr in enumerate(snrs):
         sy = r['data_syms'][b].astype(np.complex128)
         Hs = r['H'][b, 0].astype(np.complex128)
@@ -354,37 +407,18 @@ def test_coded_chain_llrs_vs_oracle(C, oracle, bw, mod):
         nv = oracle.noise_var_per_symbol(Hd, snr, 'rayleigh_mp')
         ref = oracle.llrs(sy, nv, mod)
         got = r['llr'][b].astype(np.float64)[:len(ref)]
-        assert np.max(np.abs(got - ref) / (1 + np.abs(ref))) < 1e-4, (b, snr)
+        assert np.max(np.abs(got - ref) / (1 + np.abs(ref))) < tol, (b, snr)
 
 
-@pytest.mark.parametrize('chunks', [2, 3])
-def test_pipelined_chain_matches_unpipelined(C, monkeypatch, chunks):
-    """The coded chain cut into chunks of 64-frame groups (front end of chunk
-    c+1 overlapping the decoder of chunk c on a second stream) gives the same
-    per-frame bit errors and CRC flags as the one-pass chain (ragged chunks:
-    5 groups, last group partial)."""
-    sim = _sim(20.0, '64-QAM', 'rayleigh_mp')
-    B = 4 * 64 + 37
-    plan = sim._plan(C.CHAIN_CODED, 0, 27760, max_frames=B)
-    snr = np.tile(np.arange(8.0, 24.0, 2.0), B)[:B]
-    monkeypatch.setenv('LTE_PIPELINE_CHUNKS', '1')
-    a = plan.run(snr, seed=0x5EED, frame_id0=1000)
-    monkeypatch.setenv('LTE_PIPELINE_CHUNKS', str(chunks))
-    b = plan.run(snr, seed=0x5EED, frame_id0=1000)
-    assert np.array_equal(a['frame_errors'], b['frame_errors'])
-    assert np.array_equal(a['crc_ok'], b['crc_ok'])
-    assert np.array_equal(a['counts'], b['counts'])
-    assert 0 < int(np.sum(a['crc_ok'])) < B   # both failing and passing frames at these SNRs
-
-
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('chain', ['coded', 'uncoded'])
-def test_fused_tx_channel_matches_separate_kernels(C, monkeypatch, chain):
+def test_fused_tx_channel_matches_separate_kernels(C, monkeypatch, chain, prec):
     """TX with the static-tap channel fused in (k_ofdm_tx<.., CH> + k_chan_fix)
     vs the separate TX and channel kernels, on the same Philox frames: noise
     power (the measured-power SNR, Q5), channel estimates and LLRs agree to
-    float32 round-off (the power is summed per symbol instead of per 2048-sample
+    round-off (the power is summed per symbol instead of per 2048-sample
     block); decisions agree up to that round-off."""
-    sim = _sim(20.0, '64-QAM', 'rayleigh_mp')
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
     B = 3 * 64 + 5
     coded = chain == 'coded'
     plan = sim._plan(C.CHAIN_CODED, 0, 27760, max_frames=B) if coded else \
@@ -395,25 +429,27 @@ def test_fused_tx_channel_matches_separate_kernels(C, monkeypatch, chain):
     a = plan.run(snr, seed=0x5EED, frame_id0=77, capture=cap)
     monkeypatch.setenv('LTE_TXCH_FUSE', '1')
     b = plan.run(snr, seed=0x5EED, frame_id0=77, capture=cap)
-    assert np.max(np.abs(b['noise_power'] / a['noise_power'] - 1)) < 2e-6
-    assert np.max(np.abs(b['H'] - a['H'])) < 1e-4 * np.max(np.abs(a['H']))
+    f64 = prec == 'f64'
+    assert np.max(np.abs(b['noise_power'] / a['noise_power'] - 1)) < (1e-13 if f64 else 2e-6)
+    assert np.max(np.abs(b['H'] - a['H'])) < (1e-12 if f64 else 1e-4) * np.max(np.abs(a['H']))
     if coded:
         # LLR = d^2 difference / (2 sigma^2_eff): at 30 dB a 1e-7 change of the
-        # received sample moves it by ~1e-4 (measured 2e-4 at most)
-        assert np.max(np.abs(b['llr'] - a['llr']) / (1 + np.abs(a['llr']))) < 1e-3
-        assert int(np.sum(a['crc_ok'] != b['crc_ok'])) <= 1
+        # received sample moves it by ~1e-4 (measured 2e-4 at most) in f32
+        assert np.max(np.abs(b['llr'] - a['llr']) / (1 + np.abs(a['llr']))) < (1e-9 if f64 else 1e-3)
+        assert int(np.sum(a['crc_ok'] != b['crc_ok'])) <= (0 if f64 else 1)
     ea, eb = int(a['counts'][:, 0].sum()), int(b['counts'][:, 0].sum())
-    assert abs(ea - eb) <= 1e-3 * ea + 5, (ea, eb)
+    assert abs(ea - eb) <= (2 if f64 else 1e-3 * ea + 5), (ea, eb)
     assert np.array_equal(a['counts'][:, 1], b['counts'][:, 1])
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mod', ['16-QAM', '64-QAM'])
-def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod):
+def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
     """k_rx_data handing (z, sigma^2_eff) per RE to k_dematch_zn, which runs the
     same max-log demapper while it builds the decoder rows, decodes exactly
     like the LLR round trip (k_rx_data LLRs -> k_dematch): identical per-frame
     bit errors and CRC flags on the same Philox frames."""
-    sim = _sim(20.0, mod, 'rayleigh_mp')
+    sim = _sim(20.0, mod, 'rayleigh_mp', prec)
     B = 2 * 64 + 9
     plan = sim._plan(C.CHAIN_CODED, 0, 27760 if mod == '64-QAM' else 18000, max_frames=B)
     snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]

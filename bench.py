@@ -1,18 +1,25 @@
 """Headline benchmark: LTE subframes/s through the full coded chain
 (config 2: 20 MHz, 64-QAM, Rayleigh ITU Pedestrian-A, turbo max-log-MAP x8,
-TB 27 760 bits = 5 code blocks = 14 OFDM symbols), BER sweep SNR 0:2:30 dB.
+TB 27 760 bits = 5 code blocks = 14 OFDM symbols), BER sweep SNR 0:2:30 dB,
+in float64 (the reference's arithmetic; `--precision f32` is the fast mode).
 
 One step = one batch of `--frames` subframes per GPU pushed TX -> channel ->
 RX + turbo; all inputs (Philox bits / fading / noise) are generated on the
 device.  N>1: one process per GPU (torch.distributed, RCCL); frames are
 partitioned by global frame id (weak scaling, no data-path collective); the
-only collective is the SUM of the BER counters (and MAX of the step time).
+only collectives are the SUM of the BER counters and the MAX of the step time.
 
-usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F]
+`python bench.py --gpus N` with no launcher environment starts N ranks itself
+(torch.distributed.run on 127.0.0.1, before anything touches the GPU) and
+exits with their status; under a launcher WORLD_SIZE must equal --gpus.
+
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--precision f64|f32]
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,15 +35,19 @@ SNRS = np.arange(0, 31, 2, dtype=np.float64)
 TB = 27760
 HBM_PEAK_GBS = 8000.0
 # compulsory stage-boundary bytes of one config-2 coded subframe
-# (TX map+IFFT, channel, FFT, estimation/equalisation/LLR, dematch+decode, CRC)
-B_SF = 2_116_904
+# (TX map+IFFT, channel, FFT, estimation/equalisation/LLR, dematch+decode, CRC),
+# quoted for 4-B reals; the f64 chain moves 8-B reals at the same boundaries
+B_SF_F32 = 2_116_904
 # turbo work per subframe = sum(K+3) x 17 passes x ~100 ops
 TURBO_OPS_SF = 27_919 * 17 * 100
-# VALU issue peak of one MI355X for the decoder's instruction mix (v_add_f32 /
-# v_sub_f32 / v_max_f32 / v_max3_f32, non-packed): one wave64 instruction per 4
-# cycles per SIMD (16 lanes, MI355X_MICROARCH.md "vector-instruction ISSUE
-# cost"), 1024 SIMDs at 2.4 GHz = 39.3 T lane-ops/s
-VALU_PEAK_OPS = 256 * 4 * 16 * 2.4e9
+# Non-packed vector ALU peaks of one MI355X (add / max, 1 op per lane per
+# instruction; 256 CUs x 4 SIMD-32 x 2.4 GHz):
+#  * f32: a wave64 instruction every 2 cycles per SIMD with several waves
+#    resident (MI355X_MICROARCH.md: SIMD-32, 2 cycles per wave64 VALU op)
+#    = 32 lane-ops/cycle/SIMD -> 78.6 T op/s (half the 157.3 TFLOPS FMA spec)
+#  * f64: 16 lane-ops/cycle/SIMD (the 78.6 TFLOPS f64 vector FMA spec / 2)
+#    -> 39.3 T op/s; scripts/valu_peak_bench.hip measures both on the box
+VALU_PEAK_OPS = {'f32': 256 * 4 * 32 * 2.4e9, 'f64': 256 * 4 * 16 * 2.4e9}
 
 
 def _cpu_worker(job):
@@ -81,10 +92,8 @@ def cpu_baseline(seconds=15.0, procs=None):
                       f'process each (oracle: NumPy + C, float64)'}
 
 
-def load_traffic(name='pmc_turbo_traffic.json'):
-    """Per-frame counters of the turbo kernel from a committed rocprofv3 --pmc
-    summary (HBM bytes: pmc_turbo_traffic.json; SQ instruction counts:
-    pmc_turbo_sq.json)."""
+def load_profile(name):
+    """A committed rocprofv3 --pmc summary (profiles/<name>), or None."""
     p = os.path.join(ROOT, 'profiles', name)
     if os.path.exists(p):
         try:
@@ -94,140 +103,204 @@ def load_traffic(name='pmc_turbo_traffic.json'):
     return None
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """--gpus N without a launcher: run N ranks under torch.distributed.run as a
+    child process (this process never touches the GPU) and return its status."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.call(cmd, env=env)
+
+
+def roofline(prec, tim, steps, F, el, value, world):
+    """Dominant kernel (the turbo decoder) against its roofline, from the HIP
+    event times of the timed launches: the VALU view (SURVEY §8(d)'s turbo
+    work: sum(K+3) x 17 passes x 100 add/max ops per subframe, against the
+    non-packed vector peak of the decode's arithmetic type) as the headline,
+    the HBM view (algorithmic bytes: the rate-dematched input LLRs and the
+    decoded bits) beside it with the measured traffic / algorithmic ratio."""
+    from lte_phy.channel_coding import segmentation_sizes
+    t_ms, t_n = tim.get('turbo', (0.0, 0))
+    avg_s = t_ms / max(t_n, 1) * 1e-3
+    Fp = ((F + 63) // 64) * 64            # frames padded to whole 64-frame decoder groups
+    esz = 8 if prec == 'f64' else 4
+    alg_bytes = sum(Fp * ((3 * K + 12) * esz + K / 8) for K in segmentation_sizes(TB + 24))
+    peak = VALU_PEAK_OPS[prec]
+    ops = TURBO_OPS_SF * F
+    achieved_T = ops / avg_s / 1e12 if t_n else 0.0
+    traffic = load_profile(f'pmc_turbo_traffic_{prec}.json')
+    sq = load_profile(f'pmc_turbo_sq_{prec}.json')
+    hbm_alg = alg_bytes / avg_s / 1e9 if t_n else 0.0
+    tr = traffic['bytes_per_frame'] * Fp if traffic else None
+    roof = {'bound': 'valu', 'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo',
+            'achieved': round(achieved_T, 3), 'peak': round(peak / 1e12, 2), 'unit': 'Top/s',
+            'frac': round(achieved_T * 1e12 / peak, 4),
+            'ops_per_subframe': TURBO_OPS_SF, 'frames_per_launch': F,
+            # HBM bytes per launch from the committed PMC passes (per-frame bytes,
+            # gfx950-corrected, scaled to this launch's frames)
+            'traffic': round(tr) if tr else None,
+            'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': t_n,
+            'hbm': {'alg_bytes_per_launch': int(alg_bytes), 'achieved_GBs': round(hbm_alg, 2),
+                    'peak_GBs': HBM_PEAK_GBS, 'frac': round(hbm_alg / HBM_PEAK_GBS, 5),
+                    'traffic_over_alg': round(tr / alg_bytes, 1) if tr else None,
+                    'traffic_GBs': round(tr / avg_s / 1e9, 1) if tr and t_n else None},
+            'issued_valu': ({'wave_instr_per_frame': sq['valu_wave_instr_per_frame'],
+                             'busy_frac': round(sq['valu_wave_instr_per_frame'] * Fp * sq['issue_cycles_per_instr']
+                                                / (avg_s * 2.4e9 * 1024), 4)} if sq and t_n else None),
+            'turbo_share_of_step': round(t_ms / (el * 1e3) if el > 0 else 0, 3),
+            'kernel_ms_per_step': {k: round(v[0] / steps, 3) for k, v in tim.items() if v[1]},
+            # SURVEY §8(d)'s whole-chain view: compulsory stage-boundary bytes per subframe
+            'pipeline_hbm': {'bytes_per_subframe': B_SF_F32 * esz // 4,
+                             'achieved_GBs': round(B_SF_F32 * esz / 4 * value / world / 1e9, 2),
+                             'frac': round(B_SF_F32 * esz / 4 * value / world / 1e9 / HBM_PEAK_GBS, 5)}}
+    return roof
+
+
+def dry_run_counts(ids, S):
+    """--dry-run: a deterministic per-frame statistic in place of the GPU chain
+    (exercises the launcher, sharding and reductions without a device)."""
+    from lte_phy import dist as D
+    si = D.snr_index(ids, S)
+    c = np.zeros((S, 4), dtype=np.uint64)
+    np.add.at(c[:, 0], si, ids % np.uint64(7))
+    np.add.at(c[:, 1], si, np.uint64(TB))
+    np.add.at(c[:, 2], si, (ids % np.uint64(3) == 0).astype(np.uint64))
+    np.add.at(c[:, 3], si, np.uint64(1))
+    return c
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--frames', type=int, default=65536, help='subframes per step per GPU (65536: 5120 turbo waves, 1.7 generations at 3 waves per SIMD; '
-                         '39296 / 65536 / 78592 measured within 2 %% per frame)')
+    ap.add_argument('--frames', type=int, default=65536, help='subframes per step per GPU')
     ap.add_argument('--iters', type=int, default=8)
+    ap.add_argument('--precision', choices=('f64', 'f32'), default='f64')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--dry-run', action='store_true', help='no GPU: launcher / sharding / reductions only (gloo)')
+    argv = sys.argv[1:]
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     # the CPU baseline runs first, in spawned worker processes, before anything
     # initialises the GPU (rank 0 of a 1-GPU run only)
-    cpu = cpu_baseline(args.cpu_seconds) if world == 1 and rank == 0 and not args.no_cpu else None
+    cpu = (cpu_baseline(args.cpu_seconds) if world == 1 and rank == 0 and not args.no_cpu and not args.dry_run
+           else None)
     import torch
     dist = None
     # LTE_BENCH_BACKEND=gloo: rehearse the N>1 path with several ranks sharing
     # the visible GPUs (device = LOCAL_RANK mod device count); the default is
     # RCCL ('nccl') with one rank per GPU
-    backend = os.environ.get('LTE_BENCH_BACKEND', 'nccl')
-    if backend == 'gloo':
+    backend = 'gloo' if args.dry_run else os.environ.get('LTE_BENCH_BACKEND', 'nccl')
+    if backend == 'gloo' and not args.dry_run:
         local = local % max(1, torch.cuda.device_count())
         os.environ['LTE_DEVICE'] = str(local)   # the device lte_phy plans bind to
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         if backend == 'nccl':
+            torch.cuda.set_device(local)
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
-            dist.init_process_group(backend)
-    else:
+            if not args.dry_run:
+                torch.cuda.set_device(local)
+            dist.init_process_group('gloo')
+    elif not args.dry_run:
         torch.cuda.set_device(local)
 
-    import lte_phy
-    from lte_phy import _capi as C
     from lte_phy import dist as D
-    C.device_init(local)
-    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=20.0, modulation='64-QAM'),
-                                channel_type='rayleigh_mp', itu_profile='Pedestrian_A')
-    F = int(args.frames)
-    plan = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=F, iters=args.iters)
     S = len(SNRS)
+    F = int(args.frames)
     counts = np.zeros((S, 4), dtype=np.uint64)
+    if args.dry_run:
+        plan = None
+        dev_id = f'rank{rank}'
+        step = lambda k: dry_run_counts(D.frame_ids(k, rank, world, F), S)   # noqa: E731
+        prec = args.precision
+    else:
+        import lte_phy
+        from lte_phy import _capi as C
+        C.device_init(local)
+        props = torch.cuda.get_device_properties(local)
+        dev_id = f"{getattr(props, 'pci_bus_id', '')}:{getattr(props, 'uuid', local)}"
+        sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=20.0, modulation='64-QAM'),
+                                    channel_type='rayleigh_mp', itu_profile='Pedestrian_A',
+                                    precision=args.precision)
+        plan = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=F, iters=args.iters)
+        prec = plan.precision
 
-    def step(k):
-        ids = D.frame_ids(k, rank, world, F)
-        si = D.snr_index(ids, S)
-        r = plan.run(SNRS[si], snr_index=si, n_snr=S, seed=0x5EED, frame_ids=ids)
-        return r['counts']
+        def step(k):
+            ids = D.frame_ids(k, rank, world, F)
+            si = D.snr_index(ids, S)
+            return plan.run(SNRS[si], snr_index=si, n_snr=S, seed=0x5EED, frame_ids=ids)['counts']
 
     def barrier():
-        torch.cuda.synchronize()
+        if not args.dry_run:
+            torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        if not args.dry_run:
+            torch.cuda.synchronize()
 
     for w in range(args.warmup):
         step(10_000 + w)
-    plan.timing_reset()
-    plan.timing(True)
+    if plan is not None:
+        plan.timing_reset()
+        plan.timing(True)
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
         counts += step(k)
     barrier()
     el = time.perf_counter() - t0
-    plan.timing(False)
-    tim = plan.timing_read()
+    tim = {}
+    if plan is not None:
+        plan.timing(False)
+        tim = plan.timing_read()
 
     el = D.allreduce_max(el, dist)
     counts = D.allreduce_counts(counts, dist)
+    # distinct devices that took part (not the rank count)
+    devs = [dev_id]
+    if dist is not None:
+        devs = [None] * world
+        dist.all_gather_object(devs, dev_id)
+    n_dev = len(set(devs))
 
     total = F * args.steps * world
     value = total / el
-    # dominant kernel: turbo decoder.  Algorithmic bytes per launch (SURVEY §8d
-    # per-CB figure x CBs per launch): its compulsory input = the rate-dematched
-    # f32 LLRs (3K+12 per CB) + output = K decoded bits per CB.
-    t_ms, t_n = tim.get('turbo', (0.0, 0))
-    from lte_phy.channel_coding import segmentation_sizes
-    cb_K = segmentation_sizes(TB + 24)
-    Fp = ((F + 63) // 64) * 64
-    alg_bytes_total = sum(Fp * ((3 * K + 12) * 4 + K / 8) for K in cb_K) * args.steps
-    avg_launch_ms = t_ms / max(t_n, 1)
-    alg_per_launch = alg_bytes_total / max(t_n, 1)
-    achieved = alg_per_launch / (avg_launch_ms * 1e-3) / 1e9 if t_n else 0.0
-    traffic = load_traffic()
-    sq = load_traffic('pmc_turbo_sq.json')
-    roof = {'bound': 'hbm', 'kernel': 'k_turbo', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-            # HBM bytes per launch from the committed PMC passes (profiles/pmc_turbo_traffic.json:
-            # per-frame bytes, gfx950-corrected, scaled to this launch's frames)
-            'traffic': (round(traffic['bytes_per_frame'] * Fp) if traffic else None),
-            # the same measured bytes over the measured launch time: how close the decoder's
-            # real stream (17 passes x fwd + bwd sweeps per code block) runs to the HBM peak
-            'traffic_GBs': (round(traffic['bytes_per_frame'] * Fp / (avg_launch_ms * 1e-3) / 1e9, 1)
-                            if traffic and t_n else None),
-            'traffic_frac': (round(traffic['bytes_per_frame'] * Fp / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                             if traffic and t_n else None),
-            'avg_launch_ms': round(avg_launch_ms, 3), 'launches': t_n,
-            'alg_bytes_per_launch': int(alg_per_launch),
-            'turbo_share_of_step': round(t_ms / (el * 1e3) if el > 0 else 0, 3),
-            'kernel_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in tim.items() if v[1]},
-            # SURVEY §8(d) asks for both views: the whole chain against HBM (compulsory
-            # stage-boundary bytes) and the turbo kernel against the f32 VALU peak
-            'pipeline_hbm': {'bytes_per_subframe': B_SF,
-                             'achieved_GBs': round(B_SF * value / world / 1e9, 2),
-                             'frac': round(B_SF * value / world / 1e9 / HBM_PEAK_GBS, 5)},
-            'turbo_valu': {'ops_per_subframe': TURBO_OPS_SF,
-                           'achieved_Tops': round(TURBO_OPS_SF * F / (avg_launch_ms * 1e-3) / 1e12, 3)
-                           if t_n else 0.0,
-                           'peak_Tops': round(VALU_PEAK_OPS / 1e12, 2),
-                           'frac': round(TURBO_OPS_SF * F / (avg_launch_ms * 1e-3) / VALU_PEAK_OPS, 4)
-                           if t_n else 0.0,
-                           # issued VALU lane-ops per subframe from the committed SQ_INSTS_VALU pass
-                           # (profiles/pmc_turbo_sq.json): what the SIMDs actually execute
-                           'issued_ops_per_subframe': round(sq['valu_wave_instr_per_frame'] * 64) if sq else None,
-                           'issued_frac': round(sq['valu_wave_instr_per_frame'] * 64 * Fp / (avg_launch_ms * 1e-3)
-                                                / VALU_PEAK_OPS, 4) if sq and t_n else None}}
     ber = (counts[:, 0] / np.maximum(counts[:, 1], 1)).tolist()
     bler = (counts[:, 2] / np.maximum(counts[:, 3], 1)).tolist()
-    out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'subframes/s', 'n_gpus': world,
+    out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'subframes/s', 'n_gpus': n_dev,
            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el * 1e3 / args.steps, 3),
-           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': prec,
            'data': 'synthetic (Philox4x32-10 payload bits, Jakes phases and AWGN generated on the GPU)',
            'config': {'workload': 'config 2: SISO 20 MHz (N=2048) 64-QAM, Rayleigh ITU Pedestrian-A, '
                                   'turbo max-log-MAP 8 it., TB 27760 (5 CBs, 14 OFDM symbols), SNR 0:2:30 dB',
                       'frames_per_step_per_gpu': F, 'global_batch': F * world, 'parallelism': f'dp{world}',
-                      'snr_db': SNRS.tolist()},
-           'roofline': roof,
+                      'ranks': world, 'snr_db': SNRS.tolist()},
+           'roofline': roofline(prec, tim, args.steps, F, el, value, world) if plan is not None else None,
            'ber': [float(f'{b:.4e}') for b in ber], 'bler': [float(f'{b:.4e}') for b in bler]}
+    if args.dry_run:
+        out['dry_run'] = True
+        out['counts'] = counts.tolist()
     if rank == 0:
         out['cpu_baseline'] = cpu
         print(json.dumps(out), flush=True)

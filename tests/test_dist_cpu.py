@@ -67,3 +67,43 @@ def test_single_process_reductions_are_identity():
     c = np.arange(8, dtype=np.uint64).reshape(2, 4)
     assert D.allreduce_counts(c) is c
     assert D.allreduce_max(3.0) == 3.0
+
+
+def _bench(args, env=None):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(root, 'bench.py')] + args, env=e, capture_output=True,
+                          text=True, timeout=300)
+
+
+def test_bench_self_launches_ranks_dry_run():
+    """`bench.py --gpus 2` with no launcher starts 2 ranks itself (torch.distributed.run,
+    gloo in --dry-run), shards frames by global id and reports the distinct
+    devices (here: ranks) and the summed counters of both ranks."""
+    import json
+    from lte_phy import dist as D
+    F, steps = 64, 2
+    r = _bench(['--gpus', '2', '--dry-run', '--steps', str(steps), '--warmup', '0', '--frames', str(F)])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(line) == 1, r.stdout          # one JSON line, rank 0 only
+    out = json.loads(line[0])
+    assert out['n_gpus'] == 2 and out['config']['ranks'] == 2 and out['config']['global_batch'] == 2 * F
+    ids = np.concatenate([D.frame_ids(k, rk, 2, F) for k in range(steps) for rk in range(2)])
+    si = D.snr_index(ids, 16)
+    ref = np.zeros((16, 4), dtype=np.uint64)
+    np.add.at(ref[:, 0], si, ids % np.uint64(7))
+    np.add.at(ref[:, 1], si, np.uint64(27760))
+    np.add.at(ref[:, 2], si, (ids % np.uint64(3) == 0).astype(np.uint64))
+    np.add.at(ref[:, 3], si, np.uint64(1))
+    assert np.array_equal(np.array(out['counts'], dtype=np.uint64), ref)
+
+
+def test_bench_rejects_world_size_mismatch():
+    r = _bench(['--gpus', '2', '--dry-run', '--steps', '1', '--warmup', '0'], env={'WORLD_SIZE': '1'})
+    assert r.returncode == 2 and 'WORLD_SIZE' in r.stderr

@@ -16,6 +16,8 @@ GOLDEN_TM4 = os.path.join(ROOT, 'tests', 'golden', 'golden_tm4.npz')
 GOLDEN_SCFDM = os.path.join(ROOT, 'tests', 'golden', 'golden_scfdm.npz')
 GOLDEN_IMAGE = os.path.join(ROOT, 'tests', 'golden', 'golden_image.npz')
 GOLDEN_BF = os.path.join(ROOT, 'tests', 'golden', 'golden_bf.npz')
+GOLDEN_R2 = os.path.join(ROOT, 'tests', 'golden', 'golden_r2.npz')
+FIXTURE_CURVE = os.path.join(ROOT, 'tests', 'golden', 'fixture_ber_curve.npz')
 
 
 def pytest_configure(config):
@@ -67,6 +69,16 @@ def golden_image():
 @pytest.fixture(scope='session')
 def golden_bf():
     return np.load(GOLDEN_BF, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def golden_r2():
+    return np.load(GOLDEN_R2, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def fixture_curve():
+    return np.load(FIXTURE_CURVE, allow_pickle=False)
 
 
 @pytest.fixture(scope='session')

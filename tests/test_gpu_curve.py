@@ -1,0 +1,184 @@
+"""GPU: the headline chain's BER curve and the round-2 reference goldens.
+
+  * cod_curve (tests/golden/golden_r2.npz, the REFERENCE's own
+    simulate_siso_coded on config 2 at every SNR of 0:2:30 dB): the float64
+    chain gives identical bit errors, received bits, CRC verdicts, measured
+    SNR, noise variance and RNG state at every point.
+  * fixture_ber_curve (the float64 oracle on 32 RandomState-seeded injected
+    frames per SNR point, 512 frames): the float64 chain is identical frame by
+    frame; the f32 fast mode's per-point |dBER| is reported (north_star: BER
+    match within 1e-3) and bounded where the reference decodes.
+  * c3veha: config 3 as BASELINE states it (SIMO 1x4 MRC, 10 MHz 16-QAM,
+    Vehicular-A: 6 paths, delays to 39 samples -- the channel kernel's LDS
+    delay halo beyond PedA's 13).
+  * sweep: run_ber_sweep against the reference's own output.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, unpack
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def C():
+    from lte_phy import _capi
+    _capi.device_init()
+    return _capi
+
+
+def _sim(bw, mod, chan, prec, **kw):
+    import lte_phy
+    return lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type=chan,
+                                 precision=prec, **kw)
+
+
+def _state_head():
+    return np.array(np.random.get_state()[1][:8], dtype=np.uint32)
+
+
+def _report(name, obj):
+    d = os.path.join(ROOT, 'gpurun_out')
+    if os.path.isdir(d):
+        with open(os.path.join(d, name), 'w') as f:
+            json.dump(obj, f, indent=1)
+
+
+def test_coded_ber_curve_vs_reference(C, golden_r2):
+    """Config 2 coded, SNR 0:2:30 dB, float64: every point equal to the reference."""
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', 'f64')
+    nb = int(golden_r2['cod_curve_nbits'][0])
+    bits = unpack(golden_r2['cod_curve_bits'], nb).astype(np.int64)
+    for snr in golden_r2['cod_curve_snrs'].astype(int):
+        k = f'cod_curve_snr{snr}'
+        r = sim.simulate_siso_coded(bits, float(snr))
+        assert r['bit_errors'] == int(golden_r2[k + '_errors'][0]), (k, r['bit_errors'])
+        assert np.array_equal(r['bits_received_array'], unpack(golden_r2[k + '_rx'], nb)), k
+        assert bool(r['crc_pass']) == bool(golden_r2[k + '_crc'][0]), k
+        assert abs(r['channel_snr_db'] - golden_r2[k + '_chsnr'][0]) < 1e-9, k
+        assert abs(r['noise_var_mean'] / golden_r2[k + '_nvmean'][0] - 1) < 1e-12, k
+        assert np.array_equal(_state_head(), golden_r2[k + '_state']), k
+
+
+def test_coded_ber_curve_vs_reference_f32(C, golden_r2):
+    """The same curve in the f32 fast mode: identical CRC verdicts at every
+    point and |BER - BER_ref| < 1e-3 wherever the reference decodes."""
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', 'f32')
+    nb = int(golden_r2['cod_curve_nbits'][0])
+    bits = unpack(golden_r2['cod_curve_bits'], nb).astype(np.int64)
+    rep = {}
+    for snr in golden_r2['cod_curve_snrs'].astype(int):
+        k = f'cod_curve_snr{snr}'
+        r = sim.simulate_siso_coded(bits, float(snr))
+        ref = int(golden_r2[k + '_errors'][0])
+        rep[int(snr)] = {'ber': r['ber'], 'ber_ref': ref / nb, 'dber': r['ber'] - ref / nb}
+        assert bool(r['crc_pass']) == bool(golden_r2[k + '_crc'][0]), k
+        if golden_r2[k + '_crc'][0]:
+            assert abs(r['ber'] - ref / nb) < 1e-3, k
+    _report('ber_curve_ref_f32.json', rep)
+
+
+def _curve_draws(fx, L):
+    """The fixture's injected draws (tests/golden/make_fixture_ber_curve.py)."""
+    snrs, F, seed0, TB = fx['snrs'], int(fx['frames'][0]), int(fx['seed0'][0]), int(fx['tb'][0])
+    n = len(snrs) * F
+    bits = np.zeros((n, TB), dtype=np.uint8)
+    ph = np.zeros((n, 1, 4, 16))
+    z = np.zeros((n, 1, 2, L))
+    snr = np.zeros(n)
+    for s in range(len(snrs)):
+        for f in range(F):
+            i = s * F + f
+            rs = np.random.RandomState(seed0 + 1000 * s + f)
+            bits[i] = rs.randint(0, 2, TB)
+            ph[i, 0] = 2 * np.pi * rs.rand(4, 16)
+            z[i, 0, 0] = rs.randn(L)
+            z[i, 0, 1] = rs.randn(L)
+            snr[i] = snrs[s]
+    return bits, ph, z, snr
+
+
+@pytest.fixture(scope='module')
+def curve_runs(C, fixture_curve):
+    out = {}
+    draws = None
+    for prec in ('f64', 'f32'):
+        sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
+        TB = int(fixture_curve['tb'][0])
+        n = fixture_curve['bit_errors'].size
+        plan = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=n)
+        if draws is None:
+            draws = _curve_draws(fixture_curve, plan.L)
+        bits, ph, z, snr = draws
+        r = plan.run(snr, bits=bits, phases=ph, noise=z)
+        out[prec] = (r['frame_errors'].astype(np.int64).reshape(fixture_curve['bit_errors'].shape),
+                     r['crc_ok'].reshape(fixture_curve['crc_ok'].shape))
+    return out
+
+
+def test_coded_ber_curve_fixture_f64_exact(curve_runs, fixture_curve):
+    """512 injected frames over SNR 0:2:30 dB: the float64 GPU chain == the
+    float64 oracle frame by frame (bit errors and CRC)."""
+    err, crc = curve_runs['f64']
+    assert np.array_equal(err, fixture_curve['bit_errors'])
+    assert np.array_equal(crc, fixture_curve['crc_ok'])
+
+
+def test_coded_ber_curve_fixture_f32_fast_mode(curve_runs, fixture_curve):
+    """f32 fast mode on the same 512 frames: |BER - BER_oracle| per SNR point
+    reported (gpurun_out/ber_curve_fixture_f32.json); < 1e-3 wherever the
+    float64 chain decodes every frame, and the CRC verdicts agree on >= 95 % of
+    frames overall (past the turbo cliff f32 round-off picks different wrong
+    bits)."""
+    err, crc = curve_runs['f32']
+    TB = int(fixture_curve['tb'][0])
+    F = err.shape[1]
+    ref_err, ref_crc = fixture_curve['bit_errors'], fixture_curve['crc_ok']
+    dber = (err.sum(1) - ref_err.sum(1)) / (F * TB)
+    _report('ber_curve_fixture_f32.json', {
+        'snr_db': fixture_curve['snrs'].tolist(), 'dber': dber.tolist(),
+        'ber_ref': (ref_err.sum(1) / (F * TB)).tolist(), 'crc_agree': float(np.mean(crc == ref_crc))})
+    clean = ref_crc.all(axis=1)
+    assert np.all(np.abs(dber[clean]) < 1e-3), dber
+    assert np.mean(crc == ref_crc) >= 0.95
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+def test_simulate_simo_config3_vehicular_a(C, golden_r2, prec):
+    """Config 3 as BASELINE states it: SIMO 1x4 MRC, 10 MHz 16-QAM, Vehicular-A."""
+    sim = _sim(10.0, '16-QAM', 'rayleigh_mp', prec, itu_profile='Vehicular_A')
+    nb = int(golden_r2['c3veha_nbits'][0])
+    bits = unpack(golden_r2['c3veha_bits'], nb).astype(np.int64)
+    for snr in [5, 15]:
+        k = f'c3veha_snr{snr}'
+        r = sim.simulate_simo(bits, snr, num_rx=4, parallel=False)
+        ref = int(golden_r2[k + '_errors'][0])
+        comb = np.asarray(r['symbols_rx_combined'])
+        g = golden_r2[k + '_comb']
+        if prec == 'f64':
+            assert r['bit_errors'] == ref, (k, r['bit_errors'], ref)
+            assert np.array_equal(r['bits_received_array'], unpack(golden_r2[k + '_rx'], nb)), k
+            assert np.linalg.norm(comb[:len(g)] - g) / np.linalg.norm(g) < 1e-12
+        else:
+            assert abs(r['bit_errors'] - ref) / nb < 1e-3, (k, r['bit_errors'], ref)
+            assert np.linalg.norm(comb[:len(g)] - g) / np.linalg.norm(g) < 1e-5
+        assert np.array_equal(_state_head(), golden_r2[k + '_state']), k
+
+
+def test_run_ber_sweep_vs_reference(C, golden_r2):
+    """OFDMModule.run_ber_sweep (ofdm_module.py:173-198 -> core/ofdm_core.py:
+    1795-1846) on config 1, np.random.seed(0), 3 trials at 0 / 5 / 10 dB: the
+    reference's own ber_mean / ber_values / papr_values and RNG state."""
+    import lte_phy
+    m = lte_phy.OFDMModule(lte_phy.LTEConfig(bandwidth=1.25, modulation='QPSK'))
+    np.random.seed(0)
+    res = m.run_ber_sweep(14 * 62 * 2, np.array([0, 5, 10]), num_trials=3)
+    assert np.array_equal(np.asarray(res['snr_db'], dtype=np.float64), golden_r2['sweep_snr'])
+    assert np.array_equal(res['ber_mean'], golden_r2['sweep_ber_mean'])
+    assert np.array_equal(res['ber_values'], golden_r2['sweep_ber_values'])
+    assert np.max(np.abs(res['papr_values'] - golden_r2['sweep_papr'])) < 1e-9
+    assert np.array_equal(_state_head(), golden_r2['sweep_state'])

@@ -309,20 +309,6 @@ def test_simulate_siso_coded_ref_compat_f32(C, golden, name, bw, mod, chan, snrs
         assert np.array_equal(_state_head(), golden[k + '_state'])
 
 
-def test_run_ber_sweep_matches_reference_semantics(C, golden):
-    """run_ber_sweep (frozen RNG => identical trials) == per-SNR simulate_siso."""
-    import lte_phy
-    m = lte_phy.OFDMModule(lte_phy.LTEConfig(bandwidth=1.25, modulation='QPSK'))
-    np.random.seed(0)
-    res = m.run_ber_sweep(14 * 62 * 2, np.array([0, 5, 10]), num_trials=3)
-    np.random.seed(0)
-    bits = np.random.randint(0, 2, 14 * 62 * 2)
-    for i, snr in enumerate([0, 5, 10]):
-        one = m.transmit(bits, snr)
-        assert res['ber_mean'][i] == np.mean([one['ber']] * 3)   # ofdm_core.py:1838
-        assert res['papr_values'][i] == np.mean([one['papr_db']] * 3)
-
-
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
 def test_run_grid_sharding_invariant(C, prec):
     """Philox keyed by global frame id: 2-way sharded counts sum to the unsharded counts."""

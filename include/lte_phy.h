@@ -218,7 +218,9 @@ int lte_turbo_decode_host64(int K, int iters, int64_t ncb, const double *llr /*[
 /* float64 single BCJR pass of any length n, a-posteriori output for every step:
  * LogMAPDecoder.decode (turbo_decoder.py:181-278) with return_extrinsic=False. */
 int lte_bcjr_host64(int n, int64_t ncb, const double *ls, const double *lp, const double *la, double *app);
-/* CRC: _calculate_crc core/channel_coding/crc.py:89-134 (MSB-first, zero init) */
+/* CRC: _calculate_crc core/channel_coding/crc.py:89-134 (MSB-first, zero init);
+ * poly 0x1864CFB (CRC-24A, calculate_crc24a :137-159) or 0x1800063 (CRC-24B,
+ * calculate_crc24b :162-184), len 24 */
 int lte_crc_host(int64_t n, const uint8_t *bits, uint32_t poly, int len, uint32_t *crc);
 /* Channel on an arbitrary-length stream: ChannelSimulator.transmit (core/channel.py:
  * 334-345) = RayleighChannel.filter (rayleighchannel.py:44-58) + measured-power
@@ -254,6 +256,21 @@ int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps
 /* Rate dematching map: rate_dematching_turbo core/channel_coding/rate_matching.py:374-489
  * src[j] = index into the E rate-matched LLRs feeding output j of [3K+12], -1 = zero. */
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t *src);
+/* rate_dematching_turbo (core/channel_coding/rate_matching.py:374-489) for any
+ * E, on the device: llr [ncb][E] float64 -> out [ncb][3K+12]; punctured
+ * positions 0.0, repeats (E > N_cb) summed in order onto 0.0 (:433-436). */
+int lte_rate_dematch_host64(int K, int E, int rv_idx, int64_t ncb, const double *llr, double *out);
+/* QPP interleaver pi(i) = (f1 i + f2 i^2) mod K: qpp_interleave
+ * core/channel_coding/turbo_encoder.py:76-103 (out[i] = in[perm[i]]). */
+int lte_qpp_perm(int K, int32_t *perm);
+/* Sub-block interleaver index map (32 columns, <NULL>s removed):
+ * sub_block_interleaver core/channel_coding/rate_matching.py:25-94 (out[i] = in[perm[i]]). */
+int lte_subblock_perm(int n, int32_t *perm);
+/* set_decoder_mode (core/channel_coding/turbo_decoder.py:35-54): 1 = max-log-MAP
+ * (the reference default), 0 = exact log-MAP (log_sum_exp max*, :64-88) for
+ * every float64 decode (entry points and f64 plans); float32 decoders refuse
+ * exact log-MAP with LTE_EUNSUP. */
+int lte_set_decoder_mode(int use_max_log_map);
 
 #ifdef __cplusplus
 }

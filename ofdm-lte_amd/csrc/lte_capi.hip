@@ -711,15 +711,19 @@ int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps
   return rc;
 }
 
-int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t* src) {
+// Output position j of [3K+12] (turbo_encode order) fed by rate-matched index
+// i (E <= N_cb) -- rate_dematching_turbo's de-collection + sub-block
+// de-interleave + re-interleave (rate_matching.py:428-489) as one map.
+static int dematch_first_map(int K, int E, int rv_idx, int32_t* src, bool* repeats) {
   int f1, f2;
   if (!qpp_lookup(K, &f1, &f2)) return fail(LTE_EINVAL, "Invalid interleaver size K=" + std::to_string(K));
   if (E <= 0 || !src) return fail(LTE_EINVAL, "bad E");
+  const int Ncb = 3 * (K + 6);
   std::vector<RmSrc> rs;
-  rm_source(K, rv_idx, E, rs);
+  rm_source(K, rv_idx, std::min(E, Ncb), rs);
   const int n = 3 * K + 12;
   for (int j = 0; j < n; ++j) src[j] = -1;
-  for (int i = 0; i < E; ++i) {
+  for (int i = 0; i < (int)rs.size(); ++i) {
     const RmSrc s = rs[i];
     if (s.stream < 0) continue;
     int j;
@@ -732,9 +736,57 @@ int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t* src) {
     } else {
       j = s.idx < K ? 3 * s.idx + 2 : 3 * K + 9 + (s.idx - K);
     }
-    if (src[j] >= 0) return fail(LTE_EUNSUP, "rate-dematch repetition (E > N_cb) not supported by the map form");
     src[j] = i;
   }
+  if (repeats) *repeats = E > Ncb;
+  return LTE_OK;
+}
+
+int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t* src) {
+  bool rep = false;
+  const int rc = dematch_first_map(K, E, rv_idx, src, &rep);
+  if (rc != LTE_OK) return rc;
+  if (rep) return fail(LTE_EUNSUP, "E > N_cb repeats LLRs: use lte_rate_dematch_host64 (sums the repeats)");
+  return LTE_OK;
+}
+
+int lte_rate_dematch_host64(int K, int E, int rv_idx, int64_t ncb, const double* llr, double* out) {
+  if (ncb < 0 || (ncb > 0 && (!llr || !out))) return fail(LTE_EINVAL, "bad arguments");
+  std::vector<int32_t> src(3 * (size_t)K + 12);
+  const int rc = dematch_first_map(K, E, rv_idx, src.data(), nullptr);
+  if (rc != LTE_OK || ncb == 0) return rc;
+  const int n = 3 * K + 12;
+  DBuf<double> dl, dout;
+  DBuf<int32_t> dsrc;
+  if (dl.alloc((size_t)ncb * E) || dout.alloc((size_t)ncb * n) || upload(dsrc, src))
+    return fail(LTE_ENOMEM, "dematch buffers");
+  int r = LTE_OK;
+  if (hipMemcpy(dl.p, llr, (size_t)ncb * E * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_rate_dematch(nullptr, dl.p, E, 3 * (K + 6), n, dsrc.p, ncb, dout.p) ||
+      hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, dout.p, (size_t)ncb * n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    r = fail(LTE_EHIP, std::string("rate dematch failed: ") + hipGetErrorString(hipGetLastError()));
+  dl.release(); dout.release(); dsrc.release();
+  return r;
+}
+
+int lte_qpp_perm(int K, int32_t* perm) {
+  int f1, f2;
+  if (!qpp_lookup(K, &f1, &f2)) return fail(LTE_EINVAL, "Invalid interleaver size K=" + std::to_string(K));
+  if (!perm) return fail(LTE_EINVAL, "null perm");
+  for (int64_t i = 0; i < K; ++i) perm[i] = (int32_t)((f1 * i + f2 * i * i) % K);   // turbo_encoder.py:76-103
+  return LTE_OK;
+}
+
+int lte_subblock_perm(int n, int32_t* perm) {
+  if (n < 0 || (n > 0 && !perm)) return fail(LTE_EINVAL, "bad arguments");
+  const std::vector<int> p = subblock_perm(n);   // rate_matching.py:25-94, <NULL>s removed
+  std::copy(p.begin(), p.end(), perm);
+  return LTE_OK;
+}
+
+int lte_set_decoder_mode(int use_max_log_map) {
+  set_logmap(use_max_log_map ? 0 : 1);
   return LTE_OK;
 }
 
@@ -1282,7 +1334,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   {
     Timer t(p, KN_PAYLOAD);
-    LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
+    LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? CRC24A_POLY : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
   }
   if (coded) {
     Timer t(p, KN_ENCODE);
@@ -1611,7 +1663,7 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   const bool fuse = do_tx && do_ch && txch_fusable(p, a, coded);
   if (do_tx || a->bits) {
     Timer t(p, KN_PAYLOAD);
-    LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? 1 : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
+    LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? CRC24A_POLY : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
   }
   if (!fuse && c.x.alloc((size_t)d.max_frames * p->L)) return fail(LTE_ENOMEM, "TX signal buffer");
   if (do_tx) {
@@ -1810,6 +1862,8 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   const int stages = a->stages ? a->stages : LTE_STAGE_ALL;
   if (!(stages & LTE_STAGE_TX) && !a->in_signal) return fail(LTE_EINVAL, "in_signal required when the TX stage is skipped");
   p->evuse.clear();
+  if (logmap_on() && (d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED) && !p->f64)
+    return fail(LTE_EUNSUP, "exact log-MAP decoding runs in float64 plans only");
   if (!p->mimo && !p->bf) {
     const int e = p->f64 ? run_siso<double>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride)
                          : run_siso<float>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride);
@@ -1974,7 +2028,8 @@ int lte_hard_host64(int bps, int64_t n, const double* syms, uint8_t* bits) {
 
 int lte_crc_host(int64_t n, const uint8_t* bits, uint32_t poly, int len, uint32_t* crc) {
   if (n < 0 || !crc || (n && !bits)) return fail(LTE_EINVAL, "bad crc arguments");
-  if (poly != 0x1864CFBu || len != 24) return fail(LTE_EUNSUP, "only CRC-24A runs on the device path");
+  if ((poly != 0x1864CFBu && poly != 0x1800063u) || len != 24)
+    return fail(LTE_EUNSUP, "the device CRC path computes CRC-24A / CRC-24B");
   const int nw = (int)((n + 24 + 31) / 32) + 1;
   std::vector<uint32_t> w(nw, 0);
   pack_bits(bits, (int)n, w.data(), nw);
@@ -1985,7 +2040,7 @@ int lte_crc_host(int64_t n, const uint8_t* bits, uint32_t poly, int len, uint32_
   std::vector<uint32_t> o(nw);
   if (hipMemcpy(dinj.p, w.data(), nw * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(dfid.p, 0, 8) != hipSuccess ||
-      launch_payload(nullptr, dpw.p, nw, (int)n, 1, dfid.p, 0, 1, dinj.p, 0) ||
+      launch_payload(nullptr, dpw.p, nw, (int)n, (int)(poly & 0xFFFFFFu), dfid.p, 0, 1, dinj.p, 0) ||
       hipMemcpy(o.data(), dpw.p, nw * 4, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "crc failed");
   if (rc == LTE_OK) {
@@ -2117,6 +2172,7 @@ extern "C" {
 
 int lte_turbo_decode_host(int K, int iters, int64_t ncb, const float* llr, uint8_t* bits) {
   if (iters < 0 || (ncb > 0 && (!llr || !bits))) return fail(LTE_EINVAL, "bad arguments");
+  if (logmap_on()) return fail(LTE_EUNSUP, "exact log-MAP runs in float64 only (the f32 decoder is max-log)");
   return turbo_host_run<float>(K, iters, ncb, llr, nullptr, nullptr, nullptr, TM_DEC1, bits, nullptr);
 }
 
@@ -2127,6 +2183,7 @@ int lte_turbo_decode_host64(int K, int iters, int64_t ncb, const double* llr, ui
 
 int lte_bcjr_host(int K, int64_t ncb, const float* ls, const float* lp, const float* la, float* app) {
   if (ncb > 0 && (!ls || !lp || !la || !app)) return fail(LTE_EINVAL, "bad arguments");
+  if (logmap_on()) return fail(LTE_EUNSUP, "exact log-MAP runs in float64 only (the f32 decoder is max-log)");
   return turbo_host_run<float>(K, 0, ncb, nullptr, ls, lp, la, TM_APP, nullptr, app);
 }
 

@@ -27,6 +27,10 @@
 #include "lte_common.h"
 #include "lte_internal.h"
 
+// the exact log-MAP instance (k_turbo64_logmap, an exactness mode, not a hot
+// path) is too large for the requested full unrolls; it runs correctly rolled
+#pragma clang diagnostic ignored "-Wpass-failed"
+
 #ifndef LTE_TURBO_SUB
 #define LTE_TURBO_SUB 2
 #endif
@@ -61,6 +65,21 @@ template <> struct TurboT<double> {
 __device__ __forceinline__ float vmax(float a, float b) { return fmaxf(a, b); }
 __device__ __forceinline__ double vmax(double a, double b) { return fmax(a, b); }
 
+// max* of the recursions: LM = false max-log-MAP (max), LM = true the exact
+// log-MAP of set_decoder_mode(False): log_sum_exp (turbo_decoder.py:64-88) --
+// -inf operands return the other one, else max + log1p(exp(-|a - b|)) in the
+// reference's branch order (float64 only).
+template <bool LM, class T>
+__device__ __forceinline__ T mstar(T a, T b) {
+  if constexpr (!LM) {
+    return vmax(a, b);
+  } else {
+    if (a == -__builtin_inf()) return b;
+    if (b == -__builtin_inf()) return a;
+    return a > b ? a + log1p(exp(b - a)) : b + log1p(exp(a - b));
+  }
+}
+
 // gamma for (fb, par, u); c = {g(0,0,0), g(0,0,1), g(0,1,0), g(0,1,1)}.  The
 // other four are exact negations (turbo_decoder.py:305-333 sums +/-L/2 terms,
 // and round-to-nearest is symmetric: fl(-x - y) = -fl(x + y)).
@@ -90,14 +109,14 @@ __device__ __forceinline__ void gam(T hs, T hp, T ha, T c[4]) {
 // State s = 4*s0 + 2*s1 + s2; next = 4*fb + 2*s0 + s1, fb = u^s1^s2,
 // par = fb^s0^s2.  Predecessors of ns=(f,a,b): (a,b,0) with u=f^b, par=f^a and
 // (a,b,1) with u=f^b^1, par=f^a^1.
-template <class T>
+template <class T, bool LM = false>
 __device__ __forceinline__ void fwd(const T a[8], const T c[4], T o[8]) {
 #pragma unroll
   for (int ns = 0; ns < 8; ++ns) {
     const int f = ns >> 2, s0 = (ns >> 1) & 1, s1 = ns & 1;
     const T v0 = a[4 * s0 + 2 * s1] + gsel(c, f, f ^ s0, f ^ s1);
     const T v1 = a[4 * s0 + 2 * s1 + 1] + gsel(c, f, f ^ s0 ^ 1, f ^ s1 ^ 1);
-    o[ns] = vmax(v0, v1);
+    o[ns] = mstar<LM>(v0, v1);
   }
   if constexpr (TurboT<T>::NORM) {
     const T n0 = o[0];
@@ -110,7 +129,7 @@ __device__ __forceinline__ void fwd(const T a[8], const T c[4], T o[8]) {
 // backward recursion only (trellis-termination steps, turbo_decoder.py:
 // 238-245): beta(s) = max(beta[next(s,0)] + g(s,0), beta[next(s,1)] + g(s,1)),
 // g(s,1) = -g(s,0), next(s,1) = next(s,0) ^ 4.
-template <class T>
+template <class T, bool LM = false>
 __device__ __forceinline__ void bonly(T b[8], const T c[4]) {
   T bn[8];
 #pragma unroll
@@ -118,7 +137,7 @@ __device__ __forceinline__ void bonly(T b[8], const T c[4]) {
     const int s0 = s >> 2, s1 = (s >> 1) & 1, s2 = s & 1;
     const int fb = s1 ^ s2, par = fb ^ s0 ^ s2, ns = 4 * fb + 2 * s0 + s1;
     const T g = gsel(c, fb, par, 0);
-    bn[s] = vmax(b[ns] + g, b[ns ^ 4] - g);
+    bn[s] = mstar<LM>(b[ns] + g, b[ns ^ 4] - g);
   }
   if constexpr (TurboT<T>::NORM) {
     const T n0 = bn[0];
@@ -136,7 +155,7 @@ __device__ __forceinline__ void bonly(T b[8], const T c[4]) {
 // 250-266) in one loop.  f64: each term is (alpha + gamma) + beta, the
 // reference's order (:257); f32: alpha + (beta + gamma), its C model's order.
 // Returns L and advances beta in place.
-template <class T>
+template <class T, bool LM = false>
 __device__ __forceinline__ T bstep(T b[8], const T c[4], const T a[8]) {
   T bn[8], m0 = (T)0, m1 = (T)0;
 #pragma unroll
@@ -157,10 +176,10 @@ __device__ __forceinline__ T bstep(T b[8], const T c[4], const T a[8]) {
       m0 = u0;
       m1 = u1;
     } else {
-      m0 = vmax(m0, u0);
-      m1 = vmax(m1, u1);
+      m0 = mstar<LM>(m0, u0);
+      m1 = mstar<LM>(m1, u1);
     }
-    bn[s] = vmax(t0, t1);
+    bn[s] = mstar<LM>(t0, t1);
   }
   if constexpr (TurboT<T>::NORM) {
     const T n0 = bn[0];
@@ -234,7 +253,7 @@ struct RowPtr {
 // MODE TM_FINAL: the decoder-1 a-posteriori pass that ends a decode; it also
 // packs the hard decisions L < 0 MSB-first into `bo` (words [kw][64 lanes]),
 // storing each word as the backward sweep reaches its bit 0 (no re-read pass).
-template <class T, int MODE>
+template <class T, int MODE, bool LM = false>
 __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__ wck, int lane, int K, int f1,
                                           int f2, bool first, uint32_t* __restrict__ bo = nullptr) {
   using TT = TurboT<T>;
@@ -280,7 +299,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
     for (int j = 0; j < TW; ++j) {
       T c[4], o[8];
       gam(ls[j], lp[j], la[j], c);
-      fwd(a, c, o);
+      fwd<T, LM>(a, c, o);
 #pragma unroll
       for (int s = 0; s < 8; ++s) a[s] = o[s];
     }
@@ -300,7 +319,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
     const T lp = LP.ld(k);
     T c[4];
     gam(ls, lp, (T)0, c);
-    bonly(b, c);
+    bonly<T, LM>(b, c);
   }
   // pi/d are now at k = K (decoder 2); each super-window steps them back to
   // its start, walks forward while loading and back again while storing
@@ -344,7 +363,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
           const int i = (m - 1) * TW + j;
           T c[4], o[8];
           gam(ls[i], lp[i], la[i], c);
-          fwd(cks[m], c, o);
+          fwd<T, LM>(cks[m], c, o);
 #pragma unroll
           for (int s = 0; s < 8; ++s) cks[m][s] = o[s];
         }
@@ -374,7 +393,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
             const int i = m * TW + j;
             T c[4], o[8];
             gam(ls[i], lp[i], la[i], c);
-            fwd(A[0], c, o);
+            fwd<T, LM>(A[0], c, o);
 #pragma unroll
             for (int s = 0; s < 8; ++s) A[0][s] = o[s];
           }
@@ -384,7 +403,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
           const int i = m * TW + h * TH + j;
           T c[4];
           gam(ls[i], lp[i], la[i], c);
-          fwd(A[j], c, A[j + 1]);
+          fwd<T, LM>(A[j], c, A[j + 1]);
         }
         // gamma is 6 VALU ops: recompute it below rather than keep the
         // recompute's gamma vectors live next to the inputs
@@ -399,7 +418,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
           const int k = k0 + i;
           T c[4];
           gam(ls[i], lp[i], la[i], c);
-          const T L = bstep(b, c, A[j]);
+          const T L = bstep<T, LM>(b, c, A[j]);
           if (MODE == TM_DEC1) {
             LE.st(k, ((T)0.5 * L - la[i]) - ls[i]);
           } else if (MODE == TM_DEC2) {
@@ -431,7 +450,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
 // One launch decodes every code-block slot of the batch: wave w -> job r
 // (CB slot, i.e. one K) and frame group g.  256-thread blocks = 4 independent
 // waves (no LDS, no barriers).
-template <class T>
+template <class T, bool LM = false>
 __device__ __forceinline__ void turbo_body(const TurboJobs& jobs, int iters, int mode) {
   const int wg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -445,16 +464,16 @@ __device__ __forceinline__ void turbo_body(const TurboJobs& jobs, int iters, int
   T* ck = reinterpret_cast<T*>(jb.ck) + (size_t)g * (turbo_nwin(K) * TurboT<T>::CK) * RS;
   uint32_t* bo = jb.bits + (size_t)g * turbo_kw(K) * RS;
   if (mode == TM_APP) {
-    half_pass<T, TM_APP>(base, ck, lane, K, jb.f1, jb.f2, false);
+    half_pass<T, TM_APP, LM>(base, ck, lane, K, jb.f1, jb.f2, false);
     return;
   }
   for (int it = 0; it < iters; ++it) {
-    half_pass<T, TM_DEC1>(base, ck, lane, K, jb.f1, jb.f2, it == 0);
-    half_pass<T, TM_DEC2>(base, ck, lane, K, jb.f1, jb.f2, false);
+    half_pass<T, TM_DEC1, LM>(base, ck, lane, K, jb.f1, jb.f2, it == 0);
+    half_pass<T, TM_DEC2, LM>(base, ck, lane, K, jb.f1, jb.f2, false);
   }
   // final pass = decoder 1 a-posteriori LLRs (turbo_decoder.py:440-447) and
   // the hard decisions L < 0 (:276), packed MSB-first
-  half_pass<T, TM_FINAL>(base, ck, lane, K, jb.f1, jb.f2, iters == 0, bo);
+  half_pass<T, TM_FINAL, LM>(base, ck, lane, K, jb.f1, jb.f2, iters == 0, bo);
 }
 
 __global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mode) {
@@ -465,6 +484,17 @@ __global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mo
 __global__ __launch_bounds__(256, 2) void k_turbo64(TurboJobs jobs, int iters, int mode) {
   turbo_body<double>(jobs, iters, mode);
 }
+
+// f64 exact log-MAP (set_decoder_mode(False)); not a hot path
+__global__ __launch_bounds__(256, 1) void k_turbo64_logmap(TurboJobs jobs, int iters, int mode) {
+  turbo_body<double, true>(jobs, iters, mode);
+}
+
+// decoder arithmetic of the f64 entry points and chains: max-log-MAP (the
+// reference's default, USE_MAX_LOG_MAP = True) or exact log-MAP
+static int g_logmap = 0;
+void set_logmap(int on) { g_logmap = on ? 1 : 0; }
+int logmap_on() { return g_logmap; }
 
 int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode, int f64) {
   for (int o = 0; o < n; o += TURBO_MAX_JOBS) {
@@ -477,7 +507,8 @@ int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int
     }
     const int waves = J.prefix[J.n];
     if (waves == 0) continue;
-    if (f64) hipLaunchKernelGGL(k_turbo64, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
+    if (f64 && g_logmap) hipLaunchKernelGGL(k_turbo64_logmap, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
+    else if (f64) hipLaunchKernelGGL(k_turbo64, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
     else hipLaunchKernelGGL(k_turbo, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
     const int e = (int)hipGetLastError();
     if (e) return e;
@@ -498,6 +529,7 @@ int launch_turbo(hipStream_t s, void* blk, void* ckpt, uint32_t* bits, int K, in
 // per code block; alpha of every step kept in a scratch [n][8][lanes] (f64,
 // the reference's unnormalised metrics), then the backward sweep.  Not a hot
 // path (the chain runs k_turbo64); the reference's operation order.
+template <bool LM>
 __global__ __launch_bounds__(64) void k_bcjr64(const double* __restrict__ ls, const double* __restrict__ lp,
                                                const double* __restrict__ la, int n, int ncb,
                                                double* __restrict__ alpha, double* __restrict__ app) {
@@ -515,7 +547,7 @@ __global__ __launch_bounds__(64) void k_bcjr64(const double* __restrict__ ls, co
     for (int s = 0; s < 8; ++s) al[k * st + s] = a[s];
     double cc[4], o[8];
     gam(0.5 * S[k], 0.5 * P[k], 0.5 * A[k], cc);   // x / 2.0 == 0.5 * x (exact)
-    fwd(a, cc, o);
+    fwd<double, LM>(a, cc, o);
     for (int s = 0; s < 8; ++s) a[s] = o[s];
   }
   double b[8];
@@ -525,14 +557,17 @@ __global__ __launch_bounds__(64) void k_bcjr64(const double* __restrict__ ls, co
     double cc[4], ak[8];
     gam(0.5 * S[k], 0.5 * P[k], 0.5 * A[k], cc);
     for (int s = 0; s < 8; ++s) ak[s] = al[k * st + s];
-    app[(size_t)c * n + k] = bstep(b, cc, ak);
+    app[(size_t)c * n + k] = bstep<double, LM>(b, cc, ak);
   }
 }
 
 int launch_bcjr64(hipStream_t s, const double* ls, const double* lp, const double* la, int n, int ncb,
                   double* alpha_scratch, double* app) {
   if (n < 1 || ncb < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bcjr64, dim3((ncb + 63) / 64), dim3(64), 0, s, ls, lp, la, n, ncb, alpha_scratch, app);
+  if (g_logmap)
+    hipLaunchKernelGGL(k_bcjr64<true>, dim3((ncb + 63) / 64), dim3(64), 0, s, ls, lp, la, n, ncb, alpha_scratch, app);
+  else
+    hipLaunchKernelGGL(k_bcjr64<false>, dim3((ncb + 63) / 64), dim3(64), 0, s, ls, lp, la, n, ncb, alpha_scratch, app);
   return (int)hipGetLastError();
 }
 

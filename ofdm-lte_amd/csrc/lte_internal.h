@@ -53,6 +53,8 @@ template <> struct GridT<double> {
 };
 
 // launchers (return hipError_t as int)
+constexpr int CRC24A_POLY = 0x864CFB, CRC24B_POLY = 0x800063;   // crc.py polynomials without x^24
+// crc: CRC polynomial to append (0: none)
 int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, const uint64_t* fid,
                    uint64_t seed, int B, const uint32_t* inj, int64_t inj_stride);
 // cw_scratch: encode_scratch_words(KWmax, C, B) words (the code blocks as [wave][word][lane])
@@ -136,6 +138,12 @@ struct TurboJobs {
   int prefix[TURBO_MAX_JOBS + 1];
 };
 int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int mode, int f64);
+// rate_dematching_turbo for any E (repeats summed in order): llr [ncb][E] -> out [ncb][n_out]
+int launch_rate_dematch(hipStream_t s, const double* llr, int E, int Ncb, int n_out, const int32_t* src0, int64_t ncb,
+                        double* out);
+// exact log-MAP (set_decoder_mode(False)) for the float64 decoders; default max-log-MAP
+void set_logmap(int on);
+int logmap_on();
 // one float64 BCJR pass of any length n (LogMAPDecoder.decode): app [ncb][n];
 // alpha_scratch n * ncb * 8 doubles
 int launch_bcjr64(hipStream_t s, const double* ls, const double* lp, const double* la, int n, int ncb,

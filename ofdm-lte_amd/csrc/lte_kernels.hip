@@ -12,7 +12,9 @@ namespace lte {
 constexpr int WG = 256;
 
 // ---------------------------------------------------------------------------
-// Payload bits (+ CRC-24A, crc.py:212-233) : one lane per frame.
+// Payload bits (+ CRC-24, crc.py:89-134: CRC-24A attach crc.py:212-233, or
+// CRC-24B for the stage entry, crc.py:162-184): one lane per frame.  crc = the
+// 24-bit polynomial without its x^24 term (0: no CRC).
 __device__ __forceinline__ uint32_t crc24_entry(uint32_t i, uint32_t poly) {
   uint32_t r = i << 16;
   for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? ((r << 1) ^ poly) : (r << 1);
@@ -23,7 +25,8 @@ __global__ __launch_bounds__(WG) void k_payload(uint32_t* __restrict__ pw, int P
                                                 const uint64_t* __restrict__ fid, uint64_t seed, int B,
                                                 const uint32_t* __restrict__ inj, int64_t inj_stride) {
   __shared__ uint32_t T[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_entry(i, 0x864CFBu);
+  const uint32_t poly = (uint32_t)crc & 0xFFFFFFu;
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_entry(i, poly);
   __syncthreads();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -50,7 +53,7 @@ __global__ __launch_bounds__(WG) void k_payload(uint32_t* __restrict__ pw, int P
         for (; k < dbits; ++k) {
           const uint32_t msb = (c >> 23) & 1u;
           c = (c << 1) & 0xFFFFFFu;
-          if (msb ^ ((v >> (31 - k)) & 1u)) c ^= 0x864CFBu;
+          if (msb ^ ((v >> (31 - k)) & 1u)) c ^= poly;
         }
       }
     }

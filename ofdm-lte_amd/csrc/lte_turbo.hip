@@ -156,6 +156,34 @@ template int launch_dematch_zn<double>(hipStream_t, const double2*, const double
                                        int, double* const*, const int64_t*, int);
 
 // ---------------------------------------------------------------------------
+// Stage entry: rate_dematching_turbo (rate_matching.py:374-489) for any E,
+// repetition included.  One thread per (code block, output j of [3K+12]):
+// src0[j] is the first rate-matched index feeding j (-1: punctured, stays
+// 0.0); the repeats i0 + m N_cb (m >= 1, E > N_cb) are summed in order of i
+// onto 0.0, exactly as circular_buffer[pos] += llr[i] (:433-436).
+__global__ __launch_bounds__(256) void k_rate_dematch(const double* __restrict__ llr, int E, int Ncb, int n_out,
+                                                      const int32_t* __restrict__ src0, int64_t ncb,
+                                                      double* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= ncb * n_out) return;
+  const int64_t c = t / n_out;
+  const int j = (int)(t - c * n_out);
+  double v = 0.0;
+  const double* l = llr + c * E;
+  for (int i = src0[j]; i >= 0 && i < E; i += Ncb) v = v + l[i];
+  out[t] = v;
+}
+
+int launch_rate_dematch(hipStream_t s, const double* llr, int E, int Ncb, int n_out, const int32_t* src0, int64_t ncb,
+                        double* out) {
+  const int64_t n = ncb * n_out;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_rate_dematch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, llr, E, Ncb, n_out, src0, ncb,
+                     out);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // TX: CB construction (segmentation.py:212-247 + CRC-24B crc.py:162-184) and
 // turbo encoding (turbo_encoder.py:137-313).  One lane = one (CB slot, frame).
 struct BitWriter {   // MSB-first stream writer; one store per completed word

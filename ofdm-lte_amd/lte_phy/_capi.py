@@ -91,6 +91,10 @@ _SIGS = {
     'lte_mimo_detect_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             c_i64, P(c_f64), P(c_f64), P(c_f64), c_f64, P(c_f64)]),
     'lte_rate_dematch_map': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32)]),
+    'lte_rate_dematch_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, P(c_f64), P(c_f64)]),
+    'lte_qpp_perm': (ctypes.c_int, [ctypes.c_int, P(c_i32)]),
+    'lte_subblock_perm': (ctypes.c_int, [ctypes.c_int, P(c_i32)]),
+    'lte_set_decoder_mode': (ctypes.c_int, [ctypes.c_int]),
     'lte_channel_host': (ctypes.c_int, [c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32), P(c_f64),
                                         c_f64, c_f64, c_f64, c_u64, P(ctypes.c_float), P(c_f64), P(c_f64),
                                         P(ctypes.c_float), P(ctypes.c_float)]),

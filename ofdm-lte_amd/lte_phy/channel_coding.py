@@ -1,9 +1,18 @@
-"""Channel-coding API (drop-in names of core/channel_coding/__init__.py:15-40).
+"""Channel-coding API: every name of core/channel_coding/__init__.py:15-40.
 
-The compute-heavy functions (turbo encode / decode, CRC-24A, one BCJR pass)
-run on the GPU through liblte_hip.so; segmentation and rate (de)matching are
-index bookkeeping built from the library's native tables.
+The compute-heavy functions run on the GPU through liblte_hip.so:
+  * CRC-24A / CRC-24B (the payload kernel's CRC, crc.py:89-347),
+  * turbo encode (turbo_encoder.py:214-313),
+  * turbo decode and LogMAPDecoder.decode (float64 max-log-MAP by default,
+    bit-exact with the reference; exact log-MAP after set_decoder_mode(False);
+    float32 fast mode on request),
+  * rate_dematching_turbo for any E (repeats summed on the device).
+Segmentation, the QPP / sub-block permutations and rate matching are index
+bookkeeping; their permutations come from the library's native tables
+(lte_qpp_perm, lte_subblock_perm, lte_rate_dematch_map).
 """
+from typing import List, Tuple
+
 import numpy as np
 
 from . import _capi as C
@@ -12,51 +21,174 @@ CRC24A_POLYNOMIAL = 0x1864CFB
 CRC24B_POLYNOMIAL = 0x1800063
 USE_MAX_LOG_MAP = True
 
+__all__ = ['calculate_crc24a', 'calculate_crc24b', 'attach_crc24a', 'attach_crc24b', 'check_crc24a', 'check_crc24b',
+           'segment_code_blocks', 'desegment_code_blocks', 'get_segmentation_info', 'turbo_encode', 'turbo_decode',
+           'LogMAPDecoder', 'qpp_interleave', 'qpp_deinterleave', 'rate_match_turbo', 'rate_dematching_turbo',
+           'sub_block_interleaver', 'sub_block_deinterleaver']
 
-_TURBO_SIZES = ([40 + 8 * i for i in range(60)] + [528 + 16 * i for i in range(32)] +
-                [1056 + 32 * i for i in range(32)] + [2112 + 64 * i for i in range(64)])
-
-
-def segmentation_sizes(B):
-    """Code-block sizes of segment_code_blocks (segmentation.py:74-263) for a
-    transport block of B bits (CRC-24A included)."""
-    Z, L = 6144, 24
-    if B <= Z:
-        return [next(k for k in _TURBO_SIZES if k >= B)]
-    C_ = -(-B // (Z - L))
-    Bp = B + C_ * L
-    Kp = next(k for k in _TURBO_SIZES if k >= -(-Bp // C_))
-    i = _TURBO_SIZES.index(Kp)
-    Km = _TURBO_SIZES[i - 1] if i > 0 else Kp
-    Cm = (C_ * Kp - Bp) // (Kp - Km) if Kp > Km else 0
-    return [Km] * Cm + [Kp] * (C_ - Cm)
+# segmentation.py:32-51 (TS 36.212 Table 5.1.3-3)
+TURBO_INTERLEAVER_SIZES = ([40 + 8 * i for i in range(60)] + [528 + 16 * i for i in range(32)] +
+                           [1056 + 32 * i for i in range(32)] + [2112 + 64 * i for i in range(64)])
+_TURBO_SIZES = TURBO_INTERLEAVER_SIZES
 
 
-def set_decoder_mode(use_max_log_map: bool = True):
-    """turbo_decoder.py:35-54.  Only max-log-MAP (the reference default) runs on the GPU."""
-    if not use_max_log_map:
-        raise NotImplementedError("exact log-MAP is not on the GPU path (the reference defaults to max-log)")
+def find_interleaver_size(min_size: int) -> int:
+    """segmentation.py:53-71."""
+    for size in TURBO_INTERLEAVER_SIZES:
+        if size >= min_size:
+            return size
+    raise ValueError(f"No valid interleaver size found for min_size={min_size}")
 
 
-def calculate_crc24a(data_bits):
-    """crc.py:137-159 on the GPU (same kernel that attaches the TB CRC)."""
+# ---------------------------------------------------------------- CRC (GPU)
+def _crc(data_bits, poly):
     C.device_init()
-    b = np.ascontiguousarray(np.asarray(data_bits), dtype=np.uint8)
+    b = np.ascontiguousarray(np.asarray(data_bits), dtype=np.uint8) & 1
     out = np.zeros(1, dtype=np.uint32)
-    C.check(C.load().lte_crc_host(len(b), C.ptr(b, C.U8), CRC24A_POLYNOMIAL, 24, C.ptr(out, C.U32)))
+    C.check(C.load().lte_crc_host(len(b), C.ptr(b, C.U8), poly, 24, C.ptr(out, C.U32)))
     v = int(out[0])
     return np.array([(v >> (23 - i)) & 1 for i in range(24)], dtype=np.uint8)
 
 
-def attach_crc24a(data_bits):
-    return np.concatenate([np.asarray(data_bits), calculate_crc24a(data_bits)])
+def calculate_crc24a(data_bits: np.ndarray) -> np.ndarray:
+    """crc.py:137-159 on the GPU."""
+    return _crc(data_bits, CRC24A_POLYNOMIAL)
 
 
-def check_crc24a(data_with_crc):
+def calculate_crc24b(data_bits: np.ndarray) -> np.ndarray:
+    """crc.py:162-184 on the GPU."""
+    return _crc(data_bits, CRC24B_POLYNOMIAL)
+
+
+def attach_crc24a(data_bits: np.ndarray) -> np.ndarray:
+    """crc.py:212-233."""
+    return np.concatenate([data_bits, calculate_crc24a(data_bits)])
+
+
+def attach_crc24b(data_bits: np.ndarray) -> np.ndarray:
+    """crc.py:236-257."""
+    return np.concatenate([data_bits, calculate_crc24b(data_bits)])
+
+
+def check_crc24a(data_with_crc: np.ndarray) -> bool:
+    """crc.py:277-307."""
     d = np.asarray(data_with_crc)
     if len(d) < 24:
         return False
     return bool(np.array_equal(d[-24:], calculate_crc24a(d[:-24])))
+
+
+def check_crc24b(data_with_crc: np.ndarray) -> bool:
+    """crc.py:310-347."""
+    d = np.asarray(data_with_crc)
+    if len(d) < 24:
+        return False
+    return bool(np.array_equal(d[-24:], calculate_crc24b(d[:-24])))
+
+
+# ---------------------------------------------------------------- segmentation
+def _seg_params(B):
+    """C, K-, K+, C-, C+, F of segmentation.py:147-187 (B > Z)."""
+    Z, L = 6144, 24
+    Cn = int(np.ceil(B / (Z - L)))
+    Bp = B + Cn * L
+    Kp = find_interleaver_size(int(np.ceil(Bp / Cn)))
+    i = TURBO_INTERLEAVER_SIZES.index(Kp) - 1
+    Km = TURBO_INTERLEAVER_SIZES[i] if i >= 0 else Kp
+    dK = Kp - Km
+    Cm = (Cn * Kp - Bp) // dK if dK > 0 else 0
+    return Cn, Km, Kp, Cm, Cn - Cm, Cn * Kp - Bp + Cm * (Kp - Km)
+
+
+def _bits_per_block(B, sizes):
+    """Information bits of each code block (segmentation.py:193-214, 303-316)."""
+    out, rem, Cn = [], B, len(sizes)
+    for r, K in enumerate(sizes):
+        n = rem if r == Cn - 1 else min(K - 24, rem // (Cn - r))
+        out.append(n)
+        rem -= n
+    return out
+
+
+def segmentation_sizes(B):
+    """Code-block sizes of segment_code_blocks for a transport block of B bits
+    (CRC-24A included)."""
+    if B <= 6144:
+        return [find_interleaver_size(B)]
+    Cn, Km, Kp, Cm, Cp, _ = _seg_params(B)
+    return [Km] * Cm + [Kp] * Cp
+
+
+def segment_code_blocks(transport_block_with_crc: np.ndarray) -> Tuple[List[np.ndarray], dict]:
+    """segmentation.py:74-263: fillers (zeros) first, then the information
+    bits; CRC-24B (on the GPU) per block when C > 1."""
+    tb = np.asarray(transport_block_with_crc)
+    B = len(tb)
+    if B <= 6144:
+        K = find_interleaver_size(B)
+        F = K - B
+        cb = np.zeros(K, dtype=np.uint8)
+        cb[F:] = tb
+        return [cb], {'num_blocks': 1, 'block_sizes': [K], 'num_filler_bits': F,
+                      'filler_positions': list(range(F)) if F > 0 else [], 'filler_per_block': [F],
+                      'original_size': B, 'segmented': False}
+    Cn, Km, Kp, Cm, Cp, F = _seg_params(B)
+    sizes = [Km] * Cm + [Kp] * Cp
+    info = _bits_per_block(B, sizes)
+    blocks, fill, fpos, pos = [], [], [], 0
+    for K, n in zip(sizes, info):
+        cb = np.zeros(K - 24, dtype=np.uint8)
+        Fr = (K - 24) - n
+        fill.append(Fr)
+        if n > 0:
+            cb[Fr:Fr + n] = tb[pos:pos + n]
+        if Fr > 0:
+            fpos.extend(range(len(fpos), len(fpos) + Fr))
+        pos += n
+        blocks.append(attach_crc24b(cb))
+    return blocks, {'num_blocks': Cn, 'block_sizes': sizes, 'num_filler_bits': F, 'filler_positions': fpos,
+                    'filler_per_block': fill, 'original_size': B, 'segmented': True, 'K_plus': Kp,
+                    'K_minus': Km, 'C_plus': Cp, 'C_minus': Cm}
+
+
+def desegment_code_blocks(code_blocks: List[np.ndarray], metadata: dict) -> np.ndarray:
+    """segmentation.py:266-359: drop CRC-24B and fillers, concatenate."""
+    B = metadata['original_size']
+    if not metadata['segmented']:
+        F = metadata['num_filler_bits']
+        return code_blocks[0][F:F + B]
+    sizes = metadata['block_sizes']
+    out = []
+    for cb, K, n in zip(code_blocks, sizes, _bits_per_block(B, sizes)):
+        Fr = (K - 24) - n
+        out.append(cb[:-24][Fr:Fr + n])
+    return np.concatenate(out)
+
+
+def get_segmentation_info(transport_block_size: int) -> dict:
+    """segmentation.py:362-420."""
+    sizes = segmentation_sizes(transport_block_size)
+    return {'num_blocks': len(sizes), 'block_sizes': sizes, 'total_coded_bits': sum(3 * K + 12 for K in sizes)}
+
+
+# ---------------------------------------------------------------- turbo encode (GPU)
+def _qpp(K):
+    perm = np.empty(int(K), dtype=np.int32)
+    C.check(C.load().lte_qpp_perm(int(K), C.ptr(perm, C.I32)))
+    return perm
+
+
+def qpp_interleave(data: np.ndarray, K: int) -> np.ndarray:
+    """turbo_encoder.py:76-103: out[i] = data[(f1 i + f2 i^2) mod K]."""
+    return np.asarray(data)[_qpp(K)]
+
+
+def qpp_deinterleave(data: np.ndarray, K: int) -> np.ndarray:
+    """turbo_encoder.py:105-134 (inverse permutation)."""
+    perm = _qpp(K)
+    inv = np.zeros(int(K), dtype=int)
+    inv[perm] = np.arange(int(K))
+    return np.asarray(data)[inv]
 
 
 def turbo_encode(input_bits):
@@ -69,9 +201,20 @@ def turbo_encode(input_bits):
     return out
 
 
+# ---------------------------------------------------------------- turbo decode (GPU)
+def set_decoder_mode(use_max_log_map: bool = True):
+    """turbo_decoder.py:35-54: True = max-log-MAP (default), False = exact
+    log-MAP (log_sum_exp max*), for every float64 decode on the GPU."""
+    global USE_MAX_LOG_MAP
+    USE_MAX_LOG_MAP = bool(use_max_log_map)
+    C.check(C.load().lte_set_decoder_mode(1 if use_max_log_map else 0))
+    mode = "Max-Log-MAP (fast)" if use_max_log_map else "True Log-MAP (exact)"
+    print(f"Turbo Decoder mode set to: {mode}")
+
+
 def turbo_decode(llr_encoded, K, num_iterations=5, debug=False, precision=None):
-    """turbo_decoder.py:338-450 on the GPU (max-log BCJR).  precision 'f64'
-    (default, bit-exact with the reference) or 'f32' (fast mode)."""
+    """turbo_decoder.py:338-450 on the GPU.  precision 'f64' (default,
+    bit-exact with the reference) or 'f32' (fast mode, max-log only)."""
     return turbo_decode_batch(np.asarray(llr_encoded)[None], K, num_iterations, precision)[0]
 
 
@@ -91,6 +234,78 @@ def turbo_decode_batch(llrs, K, num_iterations=8, precision=None):
     return out
 
 
+class LogMAPDecoder:
+    """turbo_decoder.py:118-335: one BCJR pass of the 8-state RSC over any
+    length (tail steps included), float64 on the GPU (lte_bcjr_host64), max*
+    per set_decoder_mode.  The trellis tables mirror _build_trellis."""
+
+    def __init__(self):
+        self.num_states = 8
+        self.num_memory = 3
+        self._build_trellis()
+
+    def _build_trellis(self):
+        self.next_state = np.zeros((8, 2), dtype=int)
+        self.output_systematic = np.zeros((8, 2), dtype=int)
+        self.output_parity = np.zeros((8, 2), dtype=int)
+        for s in range(8):
+            s0, s1, s2 = (s >> 2) & 1, (s >> 1) & 1, s & 1
+            for u in range(2):
+                fb = (u + s1 + s2) % 2
+                self.next_state[s, u] = (fb << 2) | (s0 << 1) | s1
+                self.output_systematic[s, u] = fb
+                self.output_parity[s, u] = (fb + s0 + s2) % 2
+
+    def decode(self, llr_systematic: np.ndarray, llr_parity: np.ndarray, llr_apriori: np.ndarray = None,
+               return_extrinsic: bool = True) -> Tuple[np.ndarray, np.ndarray]:
+        ls = np.ascontiguousarray(llr_systematic, dtype=np.float64)
+        K = len(ls)
+        lp = np.ascontiguousarray(llr_parity, dtype=np.float64)[:K]
+        la = np.zeros(K) if llr_apriori is None else np.ascontiguousarray(llr_apriori, dtype=np.float64)[:K]
+        if len(lp) < K or len(la) < K:
+            raise ValueError("llr_parity / llr_apriori shorter than llr_systematic")
+        C.device_init()
+        app = np.zeros(K)
+        C.check(C.load().lte_bcjr_host64(K, 1, C.ptr(ls, C.F64), C.ptr(np.ascontiguousarray(lp), C.F64),
+                                         C.ptr(np.ascontiguousarray(la), C.F64), C.ptr(app, C.F64)))
+        out = (app - la - ls) if return_extrinsic else app
+        return (app < 0).astype(np.uint8), out
+
+
+# ---------------------------------------------------------------- rate matching
+def _sbi(n):
+    perm = np.empty(int(n), dtype=np.int32)
+    C.check(C.load().lte_subblock_perm(int(n), C.ptr(perm, C.I32)))
+    return perm
+
+
+def sub_block_interleaver(input_bits: np.ndarray, D: int = 32) -> np.ndarray:
+    """rate_matching.py:25-94 (D = 32 columns; <NULL>s removed)."""
+    if D != 32:
+        raise ValueError("the LTE sub-block interleaver has D = 32 columns")
+    x = np.asarray(input_bits)
+    if len(x) == 0:
+        return np.array([], dtype=np.uint8)
+    return x[_sbi(len(x))].astype(np.uint8)
+
+
+def sub_block_deinterleaver(input_bits: np.ndarray, original_length: int, D: int = 32) -> np.ndarray:
+    """rate_matching.py:97-190: the inverse permutation; like the reference
+    the output is uint8 (its int matrix truncates), and missing input leaves
+    its positions out."""
+    if D != 32:
+        raise ValueError("the LTE sub-block interleaver has D = 32 columns")
+    n = int(original_length)
+    if n == 0:
+        return np.array([], dtype=np.uint8)
+    x = np.asarray(input_bits)
+    perm = _sbi(n)
+    m = min(len(x), n)
+    out = np.full(n, -1, dtype=np.int64)
+    out[perm[:m]] = np.asarray(x[:m]).astype(np.int64)
+    return out[out != -1].astype(np.uint8)
+
+
 def rate_match_turbo(encoded_bits, E, K, rv_idx=0):
     """rate_matching.py:193-297 via the native dematch map (its inverse)."""
     enc = np.asarray(encoded_bits)
@@ -105,10 +320,10 @@ def rate_match_turbo(encoded_bits, E, K, rv_idx=0):
 
 
 def rate_dematching_turbo(rate_matched_llrs, K, rv_idx=0, debug=False):
-    """rate_matching.py:374-489 (no repetition: E <= N_cb)."""
-    llr = np.asarray(rate_matched_llrs, dtype=np.float64)
-    src = C.rate_dematch_map(K, len(llr), rv_idx)
+    """rate_matching.py:374-489 on the GPU for any E: punctured positions 0.0,
+    repeats (E > N_cb) summed in order onto 0.0."""
+    C.device_init()
+    llr = np.ascontiguousarray(rate_matched_llrs, dtype=np.float64)
     out = np.zeros(3 * K + 12)
-    m = src >= 0
-    out[m] = llr[src[m]]
+    C.check(C.load().lte_rate_dematch_host64(int(K), len(llr), int(rv_idx), 1, C.ptr(llr, C.F64), C.ptr(out, C.F64)))
     return out

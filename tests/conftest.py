@@ -18,6 +18,7 @@ GOLDEN_IMAGE = os.path.join(ROOT, 'tests', 'golden', 'golden_image.npz')
 GOLDEN_BF = os.path.join(ROOT, 'tests', 'golden', 'golden_bf.npz')
 GOLDEN_R2 = os.path.join(ROOT, 'tests', 'golden', 'golden_r2.npz')
 FIXTURE_CURVE = os.path.join(ROOT, 'tests', 'golden', 'fixture_ber_curve.npz')
+GOLDEN_CODING_R2 = os.path.join(ROOT, 'tests', 'golden', 'golden_coding_r2.npz')
 
 
 def pytest_configure(config):
@@ -74,6 +75,13 @@ def golden_bf():
 @pytest.fixture(scope='session')
 def golden_r2():
     return np.load(GOLDEN_R2, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def golden_coding():
+    import json
+    meta = json.load(open(GOLDEN_CODING_R2.replace('.npz', '_meta.json')))
+    return np.load(GOLDEN_CODING_R2, allow_pickle=False), meta
 
 
 @pytest.fixture(scope='session')

@@ -230,6 +230,10 @@ int lte_crc_host(int64_t n, const uint8_t *bits, uint32_t poly, int len, uint32_
 int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int32_t *delays, const double *gains,
                      double fD, double fs, double snr_db, uint64_t seed, const float *x, const double *phases,
                      const double *noise, float *y, float *noise_power);
+/* the same in float64: x [L] complex128 -> y [num_rx][L] complex128 */
+int lte_channel_host64(int64_t L, int num_rx, int channel, int n_paths, const int32_t *delays, const double *gains,
+                       double fD, double fs, double snr_db, uint64_t seed, const double *x, const double *phases,
+                       const double *noise, double *y, double *noise_power);
 /* Multi-antenna channel on arbitrary streams.
  * mode 0: OFDMChannel.transmit_mimo (core/ofdm_core.py:434-543) -- AWGN links
  *   h = exp(j tx pi/2); Rayleigh links each a 100 dB ChannelSimulator (fading +

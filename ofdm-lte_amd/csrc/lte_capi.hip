@@ -529,18 +529,23 @@ int lte_pilots(int cell_id, int n, double* out) {
   return LTE_OK;
 }
 
-int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int32_t* delays, const double* gains,
-                     double fD, double fs, double snr_db, uint64_t seed, const float* x, const double* phases,
-                     const double* noise, float* y, float* noise_power) {
+}  // extern "C"
+
+// OFDMChannel.transmit on an arbitrary stream in precision R (lte_channel_host / _host64).
+template <class R>
+static int channel_host(int64_t L, int num_rx, int channel, int n_paths, const int32_t* delays, const double* gains,
+                        double fD, double fs, double snr_db, uint64_t seed, const R* x, const double* phases,
+                        const double* noise, R* y, R* noise_power) {
+  using V = cx<R>;
   if (L < 1 || L > (1LL << 30) || num_rx < 1 || !x || !y) return fail(LTE_EINVAL, "bad channel arguments");
   const bool ray = channel == LTE_CH_RAYLEIGH;
   if (!ray && channel != LTE_CH_AWGN) return fail(LTE_EINVAL, "Tipo de canal desconocido");
   if (ray && (n_paths < 1 || n_paths > LTE_MAX_PATHS || !delays || !gains)) return fail(LTE_EINVAL, "bad paths");
   Grid g{};
   g.L = (int)L;
-  const int nblk = (int)((L + 255) / 256);
-  DBuf<float2> dx, dy, dcoef, dout;
-  DBuf<float> dph, dpp, dsl, dnp, dz, dgain, dinj;
+  const int nblk = channel_nblk((int)L);
+  DBuf<V> dx, dy, dcoef, dout;
+  DBuf<R> dph, dpp, dsl, dnp, dz, dgain, dinj;
   DBuf<int32_t> ddel;
   DBuf<uint64_t> dfid;
   int rc = LTE_OK;
@@ -554,43 +559,57 @@ int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int3
     cleanup();
     return fail(LTE_ENOMEM, "channel buffers");
   }
-  const float sl = (float)std::pow(10.0, snr_db / 10.0);
+  const R sl = (R)std::pow(10.0, snr_db / 10.0);
   const uint64_t fid0 = 0;
-  std::vector<float> hz, hp, hg;
-  bool ok = hipMemcpy(dx.p, x, L * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess &&
-            hipMemcpy(dsl.p, &sl, 4, hipMemcpyHostToDevice) == hipSuccess &&
+  bool ok = hipMemcpy(dx.p, x, L * sizeof(V), hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dsl.p, &sl, sizeof(R), hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(dfid.p, &fid0, 8, hipMemcpyHostToDevice) == hipSuccess;
   if (ok && ray) {
     std::vector<int32_t> dl(delays, delays + n_paths);
-    hg.assign(gains, gains + n_paths);
+    std::vector<R> hg(gains, gains + n_paths);
     ok = upload(ddel, dl) == 0 && upload(dgain, hg) == 0;
     if (ok && phases) {
-      hp.assign(phases, phases + (size_t)num_rx * n_paths * 16);
+      std::vector<R> hp(phases, phases + (size_t)num_rx * n_paths * 16);
       ok = upload(dinj, hp) == 0;
     }
-    ok = ok && launch_fading(nullptr, 1, num_rx, n_paths, dgain.p, dfid.p, seed, phases ? dinj.p : nullptr, 0,
-                             dph.p, dcoef.p) == 0;
+    ok = ok && launch_fading<R>(nullptr, 1, num_rx, n_paths, dgain.p, dfid.p, seed, phases ? dinj.p : nullptr, 0,
+                                dph.p, dcoef.p) == 0;
   }
   if (ok && noise) {
-    hz.assign(noise, noise + (size_t)num_rx * 2 * L);
+    std::vector<R> hz(noise, noise + (size_t)num_rx * 2 * L);
     ok = upload(dz, hz) == 0;
   }
-  ok = ok && launch_channel(nullptr, g, 1, num_rx, ray ? 1 : 0, n_paths, ddel.p, dgain.p, (float)fD, (float)fs,
-                            dph.p, dcoef.p, dx.p, dy.p, dpp.p, channel_nblk((int)L),
-                            ray ? *std::max_element(delays, delays + n_paths) : 0) == 0;
-  ok = ok && launch_npow(nullptr, 1, num_rx, dpp.p, channel_nblk((int)L), (int)L, dsl.p, dnp.p) == 0;
+  ok = ok && launch_channel<R>(nullptr, g, 1, num_rx, ray ? 1 : 0, n_paths, ddel.p, dgain.p, (R)fD, (R)fs, dph.p,
+                               dcoef.p, dx.p, dy.p, dpp.p, nblk, ray ? *std::max_element(delays, delays + n_paths) : 0) == 0;
+  ok = ok && launch_npow<R>(nullptr, 1, num_rx, dpp.p, nblk, (int)L, dsl.p, dnp.p) == 0;
   if (ok) {
-    const float2* ys = ray ? dy.p : dx.p;
-    hipLaunchKernelGGL(k_cap_rx<float>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
+    const V* ys = ray ? dy.p : dx.p;
+    hipLaunchKernelGGL(k_cap_rx<R>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
                        1, ys, ray ? L : 0, ray ? (int64_t)num_rx * L : L, dnp.p, dfid.p, seed,
                        noise ? dz.p : nullptr, 0, dout.p);
     ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
-         hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(float2), hipMemcpyDeviceToHost) == hipSuccess &&
-         (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess);
+         hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(V), hipMemcpyDeviceToHost) == hipSuccess &&
+         (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(R), hipMemcpyDeviceToHost) == hipSuccess);
   }
   if (!ok) rc = fail(LTE_EHIP, std::string("channel failed: ") + hipGetErrorString(hipGetLastError()));
   cleanup();
   return rc;
+}
+
+extern "C" {
+
+int lte_channel_host(int64_t L, int num_rx, int channel, int n_paths, const int32_t* delays, const double* gains,
+                     double fD, double fs, double snr_db, uint64_t seed, const float* x, const double* phases,
+                     const double* noise, float* y, float* noise_power) {
+  return channel_host<float>(L, num_rx, channel, n_paths, delays, gains, fD, fs, snr_db, seed, x, phases, noise, y,
+                             noise_power);
+}
+
+int lte_channel_host64(int64_t L, int num_rx, int channel, int n_paths, const int32_t* delays, const double* gains,
+                       double fD, double fs, double snr_db, uint64_t seed, const double* x, const double* phases,
+                       const double* noise, double* y, double* noise_power) {
+  return channel_host<double>(L, num_rx, channel, n_paths, delays, gains, fD, fs, snr_db, seed, x, phases, noise, y,
+                              noise_power);
 }
 
 int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,

@@ -98,6 +98,9 @@ _SIGS = {
     'lte_channel_host': (ctypes.c_int, [c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32), P(c_f64),
                                         c_f64, c_f64, c_f64, c_u64, P(ctypes.c_float), P(c_f64), P(c_f64),
                                         P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_channel_host64': (ctypes.c_int, [c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32), P(c_f64),
+                                          c_f64, c_f64, c_f64, c_u64, P(c_f64), P(c_f64), P(c_f64),
+                                          P(c_f64), P(c_f64)]),
     'lte_channel_mimo_host': (ctypes.c_int, [c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, P(c_i32), P(c_f64), c_f64, c_f64, c_f64, c_u64,
                                              P(ctypes.c_float), P(c_f64), P(c_f64), P(c_f64), P(c_f64),

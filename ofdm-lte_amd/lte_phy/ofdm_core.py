@@ -310,20 +310,25 @@ class OFDMChannel:
         return ph, z
 
     def _apply(self, signal, num_rx):
+        """Channel on an arbitrary stream on the GPU (lte_channel_host64; float32
+        lte_channel_host when LTE_PRECISION=f32)."""
         C.device_init()
-        x = np.ascontiguousarray(signal, dtype=np.complex64)
+        f64 = C.precision_of() == 'f64'
+        cdt, rdt, ct = (np.complex128, np.float64, C.F64) if f64 else (np.complex64, np.float32, C.F32)
+        x = np.ascontiguousarray(signal, dtype=cdt)
         L = len(x)
         ph, z = self.draw(L, num_rx)
-        y = np.zeros((num_rx, L), dtype=np.complex64)
-        npow = np.zeros(num_rx, dtype=np.float32)
+        y = np.zeros((num_rx, L), dtype=cdt)
+        npow = np.zeros(num_rx, dtype=rdt)
         P = len(self.delays)
         dl = np.array(self.delays, dtype=np.int32)
         g = np.array(self.gains, dtype=np.float64)
-        C.check(C.load().lte_channel_host(L, num_rx, self.kind, P, C.ptr(dl, C.I32) if P else None,
-                                          C.ptr(g, C.F64) if P else None, float(self.fD), float(self.fs or 0.0),
-                                          float(self.snr_db), 0, C.ptr(x.view(np.float32), C.F32),
-                                          C.ptr(ph, C.F64) if P else None, C.ptr(z, C.F64),
-                                          C.ptr(y.view(np.float32), C.F32), C.ptr(npow, C.F32)))
+        fn = C.load().lte_channel_host64 if f64 else C.load().lte_channel_host
+        C.check(fn(L, num_rx, self.kind, P, C.ptr(dl, C.I32) if P else None,
+                   C.ptr(g, C.F64) if P else None, float(self.fD), float(self.fs or 0.0),
+                   float(self.snr_db), 0, C.ptr(x.view(rdt), ct),
+                   C.ptr(ph, C.F64) if P else None, C.ptr(z, C.F64),
+                   C.ptr(y.view(rdt), ct), C.ptr(npow, ct)))
         return y.astype(np.complex128)
 
     def transmit(self, signal: np.ndarray) -> np.ndarray:

@@ -446,3 +446,26 @@ def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
     assert np.array_equal(a['frame_errors'], b['frame_errors'])
     assert np.array_equal(a['crc_ok'], b['crc_ok'])
     assert 0 < int(np.sum(a['crc_ok'])) < B
+
+
+@pytest.mark.parametrize('prec,tol', [('f64', 1e-13), ('f32', 1e-5)])
+@pytest.mark.parametrize('chan,profile', [('awgn', 'Pedestrian_A'), ('rayleigh_mp', 'Pedestrian_A'),
+                                          ('rayleigh_mp', 'Vehicular_A')])
+def test_ofdm_channel_transmit_vs_oracle(C, oracle, monkeypatch, chan, profile, prec, tol):
+    """OFDMChannel.transmit (ChannelSimulator.transmit, core/channel.py:334-345)
+    on an arbitrary stream through lte_channel_host64 / lte_channel_host: the
+    same global-RNG draws as the reference (phases per path, then the two
+    normal(L) vectors), output equal to the oracle to round-off."""
+    import lte_phy
+    monkeypatch.setenv('LTE_PRECISION', prec)
+    num = oracle.Numerology(bandwidth=20.0, modulation='64-QAM')
+    rs = np.random.RandomState(4)
+    x = (rs.randn(20000) + 1j * rs.randn(20000)) / np.sqrt(2)
+    ch = lte_phy.OFDMChannel(chan, 12.0, num.fs, itu_profile=profile)
+    np.random.seed(99)
+    y = ch.transmit(x)
+    st = _state_head()
+    np.random.seed(99)
+    ref = oracle.channel_transmit(num, x, chan, 12.0, profile)
+    assert np.array_equal(st, _state_head())
+    assert np.linalg.norm(y - ref) / np.linalg.norm(ref) < tol

@@ -181,8 +181,11 @@ __device__ __forceinline__ void dft8_inplace(V (&v)[8]) {
 // NC > 0: a kernel instance for one transform size (NC = N): pass count,
 // strides, swizzle predicates and twiddle strides fold and the passes unroll
 // (ofdm_tx / rx_data / rx_chest at N = 2048: -2..-15 % time).  NC = 0: runtime N.
-template <bool INV, int NC = 0, class V>
-__device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __restrict__ tw, int tid, bool active) {
+// SC: the last pass multiplies its outputs by osc (an output scale folded into
+// the final store instead of a separate LDS pass).
+template <bool INV, int NC = 0, bool SC = false, class V>
+__device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __restrict__ tw, int tid, bool active,
+                                        re_t<V> osc = (re_t<V>)1) {
   const int N = NC ? NC : N_;
   const int log2N = NC ? __builtin_ctz(NC) : log2N_;
   const int T = N >> 3;
@@ -215,7 +218,7 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int i = idx + r * Ns;
-          buf[wsw ? fft_sw(i) : i] = v[r];
+          buf[wsw ? fft_sw(i) : i] = (SC && !wsw) ? cscale(v[r], osc) : v[r];
         }
       }
       __syncthreads();
@@ -246,7 +249,7 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int i = idx + r * Ns;
-          buf[wsw ? fft_sw(i) : i] = v[r];
+          buf[wsw ? fft_sw(i) : i] = (SC && !wsw) ? cscale(v[r], osc) : v[r];
         }
       }
       __syncthreads();
@@ -274,7 +277,7 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
       for (int q = 0; q < 2; ++q) {
         const int j = tid + q * T;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) buf[j + r * q4] = v[q][r];
+        for (int r = 0; r < 4; ++r) buf[j + r * q4] = SC ? cscale(v[q][r], osc) : v[q][r];
       }
     }
     __syncthreads();
@@ -295,8 +298,8 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = tid + q * T;
-        buf[j] = v[q][0];
-        buf[j + h] = v[q][1];
+        buf[j] = SC ? cscale(v[q][0], osc) : v[q][0];
+        buf[j + h] = SC ? cscale(v[q][1], osc) : v[q][1];
       }
     }
     __syncthreads();

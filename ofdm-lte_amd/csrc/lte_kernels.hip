@@ -106,8 +106,9 @@ __device__ __forceinline__ R rx_scale(int N) {
 // max_delay every delayed tap stays inside the symbol); stores m >= cp only
 // and sums |y|^2 over m >= max_delay per slot in a fixed order.  Called by
 // every thread of the block.  f32 folds the output scale into the taps; f64
-// scales the symbol first (x = ifft * sqrt(N) as the reference forms it) and
-// applies the taps (gain * fading) * x in the reference's order.
+// receives the symbol already scaled by the IFFT's last pass (x = ifft *
+// sqrt(N) as the reference forms it) and applies the taps (gain * fading) * x
+// in the reference's order.
 template <class R>
 __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxChannelT<R>& ch, int b, int l, int slot,
                                            int tid, int T, bool active, R sc) {
@@ -115,11 +116,6 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
   __shared__ R red[WG / 64];
   constexpr bool F64 = sizeof(R) == 8;
   const int N = g.N, cp = g.cp, S = N + cp, D = ch.max_delay;
-  if constexpr (F64) {
-    if (active)
-      for (int k = tid; k < N; k += T) buf[k] = cscale(buf[k], sc);
-    __syncthreads();
-  }
   R pw = (R)0;
   if (active) {
     if (D > 0) {   // the TX samples x at both ends of the symbol
@@ -255,8 +251,9 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
       for (int j = tid; j < g.Nd; j += T) buf[g.data_idx[j]] = pre[j];
   }
   __syncthreads();
-  fft_lds<true, NC>(buf, N, g.log2N, G::tw(g), tid, active);
   const R sc = tx_scale<R>(N);
+  // f64 + channel: the IFFT's last pass applies the output scale
+  fft_lds<true, NC, CH && sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
   if constexpr (CH) {
     tx_channel<R>(buf, g, ch, b, l, slot, tid, T, active, sc);
   } else if (active) {
@@ -266,10 +263,15 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   }
 }
 
-// LDS bytes of the coded stream staged per slot (0: not staged)
+// LDS bytes of the coded stream staged per slot (0: not staged).
+// LTE_TX_STAGE=0 gathers the coded bits through L1 / L2 instead (A/B knob).
 static size_t tx_enc_shm(int coded, int spw, int enc_words) {
   const size_t e = (size_t)spw * enc_words * sizeof(uint32_t);
-  return coded && e <= 32768 ? e : 0;
+  static const int on = [] {
+    const char* v = std::getenv("LTE_TX_STAGE");
+    return v ? std::atoi(v) : 1;
+  }();
+  return coded && on && e <= 32768 ? e : 0;
 }
 
 template <class R>

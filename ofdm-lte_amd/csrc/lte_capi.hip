@@ -1646,6 +1646,14 @@ static R* zn_nv(lte_plan* p) {
   return cbuf<R>(p).llr.p + 2 * (size_t)p->d.max_frames * (p->n_re_bits / p->d.bps);
 }
 
+// Fused SISO receiver (k_rx_frame): one RX, coded or uncoded, no SC-FDM.
+// LTE_RX_FUSE=0 selects k_rx_chest + k_rx_data (A/B and parity tests).
+static bool rx_fusable(const lte_plan* p, const lte_plan_desc& d) {
+  if (const char* e = std::getenv("LTE_RX_FUSE"))
+    if (std::atoi(e) == 0) return false;
+  return rx_frame_supported(p->grid, d.chain, d.num_rx, (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0);
+}
+
 // SISO / SIMO chains (uncoded, coded, MRC) in precision R.
 template <class R>
 static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const std::vector<double>& snr_lin,
@@ -1728,7 +1736,9 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                            ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0));
     LCHK(launch_npow<R>(s, B, rx, c.pow_part.p, channel_nblk(p->L), p->L, c.snr_lin.p, c.npow.p));
   }
-  if (do_rx) {
+  // SISO receiver fused (estimation + data path per frame) unless LTE_RX_FUSE=0
+  const bool rxf = do_rx && rx_fusable(p, d);
+  if (do_rx && !rxf) {
     Timer t(p, KN_RX_CHEST);
     LCHK(launch_rx_chest<R>(s, g, B, rx, ysrc, yrs, yfs, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.H.p,
                             c.pstats.p));
@@ -1745,7 +1755,14 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   const bool zn = demap_in_dematch(p, a);
   if (coded && !zn && c.llr.alloc((size_t)d.max_frames * p->n_re_bits)) return fail(LTE_ENOMEM, "LLR buffer");
-  if (do_rx) {
+  if (rxf) {
+    Timer t(p, KN_RX_DATA);
+    LCHK(launch_rx_frame<R>(s, g, d.chain, ray ? 1 : 0, B, ysrc, yfs, c.npow.p, c.snr_lin.p, p->fid.p, a->seed, inj_z,
+                            inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+                            zn ? reinterpret_cast<R*>(zn_z<R>(p)) : c.llr.p, cap_syms_dev,
+                            coded ? nullptr : cap_bits_dev, zn ? zn_nv<R>(p) : nullptr,
+                            a->cap_H ? c.H.p : nullptr, a->cap_pilot_stats ? c.pstats.p : nullptr));
+  } else if (do_rx) {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_data<R>(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, c.H.p, c.npow.p, c.snr_lin.p, p->fid.p,
                            a->seed, inj_z, inj_z_stride, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
@@ -1759,7 +1776,7 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     {
       Timer t(p, KN_DEMATCH);
       if (zn)
-        LCHK(launch_dematch_zn<R>(s, zn_z<R>(p), zn_nv<R>(p), p->n_re_bits / d.bps, d.bps, B, p->rx_map.p,
+        LCHK(launch_dematch_zn<R>(s, zn_z<R>(p), zn_nv<R>(p), p->n_re_bits / d.bps, p->Nd, d.bps, B, p->rx_map.p,
                                   p->n_layers, c.blk_ptrs.p, p->rows_dev.p));
       else
         LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p));

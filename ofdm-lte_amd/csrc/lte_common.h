@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "lte_bm_tables.h"
 
 #define LTE_NEG_BIG (-1.0e30f)
 
@@ -73,9 +74,47 @@ __device__ __forceinline__ double2 box_muller64(uint32_t a, uint32_t b) {
   sincospi(2.0 * v, &s, &c);
   return make_double2(r * c, r * s);
 }
+// Table-driven float64 Box-Muller: the same (a, b) -> (r cos t, r sin t) as
+// box_muller64 on the same uniforms, with ln u and the angle's sin / cos from
+// correctly rounded float64 tables (lte_bm_tables.h) plus short polynomials
+// on |x| < 2^-8: about 40 % of the VALU work of OCML's log and sincospi, and
+// within a few float64 ulps of them (scripts/rx_parts_bench.hip measures both).
+//  ln u, u = (a + 0.5) 2^-32: u = 2^e m, m in [1, 2); m = c_i (1 + r) with c_i
+//  the centre of m's 1/128 bucket, ln u = e ln 2 + ln c_i + log1p(r); for u in
+//  [1 - 2^-8, 1) log1p(-(1 - u)) directly (keeps the relative precision near 1).
+//  angle 2 pi (b + 0.5) 2^-32 = 2 pi (i + 0.5) / 256 + x, |x| < 2 pi 2^-9.
+__device__ __forceinline__ double log1p_small(double r) {   // |r| <= 2^-8, error < 2^-60
+  return r * (1.0 + r * (-0.5 + r * (0x1.5555555555555p-2 + r * (-0.25 + r * (0.2 + r * (-0x1.5555555555555p-3 +
+                                                                                          r * 0x1.2492492492492p-3))))));
+}
+__device__ __forceinline__ double ln_u32(uint32_t a) {
+  const double x = (double)a + 0.5;   // exact
+  const uint64_t bx = (uint64_t)__double_as_longlong(x);
+  const int e = (int)(bx >> 52) - 1023 - 32;
+  const int i = (int)(bx >> 45) & 127;
+  const double m = __longlong_as_double((long long)((bx & 0xFFFFFFFFFFFFFull) | 0x3FF0000000000000ull));
+  const double c = 1.0 + ((double)i + 0.5) * 0.0078125;   // exact
+  const double2 t = BM_LG[i];
+  const bool near1 = a >= 0xFF000000u;
+  const double d = ((double)(0xFFFFFFFFu - a) + 0.5) * 0x1p-32;   // 1 - u, exact
+  const double r = near1 ? -d : (m - c) * t.x;                    // m - c exact
+  const double p = log1p_small(r);
+  const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
+  return near1 ? p : (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
+}
+__device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b) {
+  const double r = sqrt(-2.0 * ln_u32(a));
+  const double2 T = BM_SC[b >> 24];
+  const double x = ((double)((int)(b & 0xFFFFFFu) - 0x800000) + 0.5) * 0x1p-32 * 0x1.921fb54442d18p+2;
+  const double x2 = x * x;
+  const double sx = x + x * x2 * (-0x1.5555555555555p-3 + x2 * (0x1.1111111111111p-7 + x2 * -0x1.a01a01a01a01ap-13));
+  const double cx = 1.0 + x2 * (-0.5 + x2 * (0x1.5555555555555p-5 + x2 * -0x1.6c16c16c16c17p-10));
+  const double c = T.x * cx - T.y * sx, s = T.y * cx + T.x * sx;
+  return make_double2(r * c, r * s);
+}
 template <class R> __device__ __forceinline__ cx<R> gauss2(uint32_t a, uint32_t b);
 template <> __device__ __forceinline__ float2 gauss2<float>(uint32_t a, uint32_t b) { return box_muller(a, b); }
-template <> __device__ __forceinline__ double2 gauss2<double>(uint32_t a, uint32_t b) { return box_muller64(a, b); }
+template <> __device__ __forceinline__ double2 gauss2<double>(uint32_t a, uint32_t b) { return box_muller64t(a, b); }
 
 // ---------------------------------------------------------------- complex
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }

@@ -110,18 +110,28 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                    const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, const uint32_t* pw, int PW,
                    int n_bits, uint32_t* frame_err, R* llr, cx<R>* cap_syms, uint8_t* cap_bits, int sc_fdm = 0,
                    R* nv_out = nullptr);
+// Fused SISO receiver (estimation + data path, one slot per frame): coded or
+// uncoded, one RX, no SC-FDM.  nv_out set: llr takes z per RE and nv_out
+// sigma^2_eff per (frame, group, data subcarrier); H / pstats: optional captures.
+bool rx_frame_supported(const Grid& g, int chain, int num_rx, int sc_fdm);
+template <class R>
+int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, const cx<R>* y,
+                    int64_t y_frame_stride, const R* npow, const R* snr_lin, const uint64_t* fid, uint64_t seed,
+                    const R* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits, R* nv_out, cx<R>* H, R* pstats);
 // Rate dematch into the decoder rows (rows of R: float / double).  rx_map
 // [n_layers][T]: layer 0 assigns, layers 1.. add in order (E > N_cb
 // repetition, rate_matching.py:433-436).  g0: first 64-frame group.
 template <class R>
 int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_map, int n_layers, R* const* blk,
                    const int64_t* rows, int g0 = 0);
-// dematch with the soft demapper fused in: reads the equalised symbols z and
-// their noise variances ([B][n_re] each, from k_rx_data's nv_out mode) instead
-// of LLRs; same decoder rows as launch_dematch (bps 4 / 6)
+// dematch with the soft demapper fused in: reads the equalised symbols z
+// ([B][n_re]) and their noise variances ([B][n_grp][nd] per data subcarrier,
+// from the receivers' nv_out mode) instead of LLRs; same decoder rows as
+// launch_dematch (bps 4 / 6)
 template <class R>
-int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int bps, int B, const int32_t* rx_map,
-                      int n_layers, R* const* blk, const int64_t* rows, int g0 = 0);
+int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int nd, int bps, int B,
+                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int g0 = 0);
 // f64 != 0: the float64 decoder (bit-exact with the reference), blk / ckpt hold doubles
 int launch_turbo(hipStream_t s, void* blk, void* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
                  int G, int mode, int f64);

@@ -804,9 +804,9 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
       const R s2 = (R)1 / snr_lin[b];
       R nv = s2;
       if (rayleigh) nv = fmax(s2 / fmin(fmax(den[q], (R)1e-6), (R)1e6), s2 / (R)4);
-      if (nvo) {   // demap in k_dematch_zn: hand over the equalised symbol and its noise variance
+      if (nvo) {   // demap in k_dematch_zn: the equalised symbol and sigma^2_eff per (group, subcarrier)
         reinterpret_cast<V*>(llr)[fre + re] = z;
-        nvo[fre + re] = nv;
+        nvo[((size_t)b * g.n_grp + grp) * g.Nd + j] = nv;
         continue;
       }
       R o[BPS];
@@ -834,6 +834,233 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
   }
   // one atomic per frame per wave (all lanes reach this point; inactive lanes carry 0)
   if constexpr (CHAIN != LTE_CHAIN_CODED) frame_err_add(frame_err, b, errs);
+}
+
+// ---------------------------------------------------------------------------
+// Fused SISO receiver: one slot per frame walks its OFDM symbols in order; the
+// first symbol of each 14-symbol group also yields the group's LS estimate
+// (k_rx_chest's work on the FFT the data path needs anyway), and the per-
+// subcarrier equaliser terms -- NumPy's complex division by H + 1e-6 reduced
+// to its per-subcarrier ratio / scale (ZfCoef), and sigma^2_eff -- are formed
+// once per group in registers for the thread's data subcarriers instead of per
+// RE.  H is never re-read from HBM (written only for a capture).  Same
+// arithmetic per RE as k_rx_chest + k_rx_data (parity test
+// test_fused_receiver_matches_separate_kernels).
+template <class R> struct ZfCoef;
+template <> struct ZfCoef<double> {   // cdiv(y, h) (Smith, lte_common.h) with the h-only terms precomputed
+  double rat, sre, sim;
+  bool swp;
+  __device__ __forceinline__ void set(double2 h) {
+    swp = !(fabs(h.x) >= fabs(h.y));
+    if (!swp) {
+      rat = (h.x == 0.0 && h.y == 0.0) ? 0.0 : h.y / h.x;   // h = 0: a / 0 as cdiv
+      sre = sim = (h.x == 0.0 && h.y == 0.0) ? 1.0 / h.x : 1.0 / (h.x + h.y * rat);
+    } else {
+      rat = h.x / h.y;
+      sre = 1.0 / (h.y + h.x * rat);
+      sim = -sre;
+    }
+  }
+  // !swp: ((a.x + a.y rat) s, (a.y - a.x rat) s); swp: ((a.x rat + a.y) s, (a.y rat - a.x) s)
+  __device__ __forceinline__ double2 apply(double2 a) const {
+    const double u = swp ? a.x : a.y, v = swp ? a.y : a.x;
+    return make_double2((v + u * rat) * sre, (u - v * rat) * sim);
+  }
+};
+template <> struct ZfCoef<float> {    // zf_div(y, h): y conj(h) / |h|^2
+  float2 h;
+  float r;
+  __device__ __forceinline__ void set(float2 hh) {
+    h = hh;
+    r = 1.0f / (hh.x * hh.x + hh.y * hh.y);
+  }
+  __device__ __forceinline__ float2 apply(float2 y) const {
+    return make_float2((y.x * h.x + y.y * h.y) * r, (y.y * h.x - y.x * h.y) * r);
+  }
+};
+
+// linear interpolation of the pilot LS estimates hp at subcarrier k with edge
+// hold (lte_receiver.py:114-133), as k_rx_chest forms it
+template <class R>
+__device__ __forceinline__ cx<R> chest_interp(const Grid& g, const cx<R>* hp, int k) {
+  using V = cx<R>;
+  const int sidx = g.seg[k];
+  if (sidx < 0) return hp[0];
+  if (sidx >= g.Np - 1) return hp[g.Np - 1];
+  const V v0 = hp[sidx], v1 = hp[sidx + 1];
+  const R fk = (R)(k - g.pilot_idx[sidx]);
+  const R ig = GridT<R>::inv_gap(g)[sidx];
+  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+}
+
+#ifndef RXF_EXP
+#define RXF_EXP 0
+#endif
+#ifndef RXF_WAVES
+#define RXF_WAVES 3
+#endif
+template <class R, int CHAIN, int BPS, int NC = 0>
+__global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh, int B, const cx<R>* __restrict__ y,
+                                                 int64_t y_frame_stride, const R* __restrict__ npow,
+                                                 const R* __restrict__ snr_lin, const uint64_t* __restrict__ fid,
+                                                 uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride,
+                                                 const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                 uint32_t* __restrict__ frame_err, R* __restrict__ llr,
+                                                 cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits,
+                                                 R* __restrict__ nvo, cx<R>* __restrict__ H, R* __restrict__ pstats) {
+  using V = cx<R>;
+  using G = GridT<R>;
+  V* sm = dyn_lds<V>();
+  const int N = NC ? NC : g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
+  const int b = blockIdx.x * spw + slot;
+  const bool active = slot < spw && b < B;
+  V* buf = sm + slot * (N + g.Np);
+  V* hp = buf + N;
+  const R sc = rx_scale<R>(N);
+  constexpr R QS = (R)qam_norm<BPS>();
+  constexpr int QM = 4;   // data REs per thread (Nd < N/2 for every LTE profile)
+  const R sigma = active ? sqrt(npow[b] / (R)2) : (R)0;
+  const R s2 = active ? (R)1 / snr_lin[b] : (R)1;
+  const uint64_t fr = active ? fid[b] : 0ull;
+  const R* zf = (inj_z && active) ? inj_z + (size_t)b * inj_stride : nullptr;
+  const V* yf = y + (size_t)(active ? b : 0) * y_frame_stride;
+  const uint32_t* fb = pw + (size_t)(active ? b : 0) * PW;
+  const size_t fre = (size_t)(active ? b : 0) * g.n_sym * g.Nd;
+  int kpos[QM];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int j = tid0 + q * T;
+    kpos[q] = (active && j < g.Nd) ? g.data_idx[j] : 0;
+  }
+  ZfCoef<R> zc[QM];
+  R nvq[QM];
+  uint32_t errs = 0;
+  for (int l = 0; l < g.n_sym; ++l) {
+    // tid made opaque per symbol: the FFT / loader address arithmetic derived
+    // from it is recomputed each symbol instead of hoisted and held live
+    // across the loop (which took the kernel to 255 VGPRs)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    if (active) load_symbol_noisy2(buf, yf, N, g.cp, l, sigma, seed, fr, 0, zf, g.L, tid, T);
+    __syncthreads();
+    fft_lds<false, NC>(buf, N, g.log2N, G::tw(g), tid, active);
+    if (l % 14 == 0) {   // group estimate from its first symbol (lte_receiver.py:360-411)
+      const int grp = l / 14;
+      if (active)
+        for (int p = tid; p < g.Np; p += T) {
+          const V Y = cscale(buf[g.pilot_idx[p]], sc);
+          hp[p] = cdiv(Y, G::pilots(g)[p]);
+          buf[g.pilot_idx[p]] = Y;   // scaled pilots for the SNR stats
+        }
+      __syncthreads();
+      if (active) {
+        if (RXF_EXP != 1 && H) {
+          V* Hf = H + ((size_t)b * g.n_grp + grp) * N;
+          for (int k = tid; k < N; k += T) Hf[k] = chest_interp<R>(g, hp, k);
+        }
+#pragma unroll
+        for (int q = 0; q < QM; ++q) {
+          const int j = tid + q * T;
+          if (j < g.Nd) {
+            const V h = chest_interp<R>(g, hp, kpos[q]);
+            zc[q].set(mkc(h.x + (R)1e-6, h.y));
+            const R den = abs2_ref(h);
+            nvq[q] = rayleigh ? fmax(s2 / fmin(fmax(den, (R)1e-6), (R)1e6), s2 / (R)4) : s2;
+            if (nvo) nvo[((size_t)b * g.n_grp + grp) * g.Nd + j] = nvq[q];
+          }
+        }
+        if (RXF_EXP != 1 && pstats && tid == 0) {
+          R pp = (R)0, en = (R)0;
+          for (int p = 0; p < g.Np; ++p) {
+            const V Yp = buf[g.pilot_idx[p]], X = G::pilots(g)[p];
+            pp += Yp.x * Yp.x + Yp.y * Yp.y;
+            const V d = csub(Yp, X);
+            en += d.x * d.x + d.y * d.y;
+          }
+          R* st = pstats + ((size_t)b * g.n_grp + grp) * 2;
+          st[0] = pp / (R)g.Np;
+          st[1] = en / (R)g.Np;
+        }
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) {
+        const int j = tid + q * T;
+        if (j >= g.Nd) continue;
+        const int re = l * g.Nd + j;
+        const V Y = cscale(buf[kpos[q]], sc);
+        const V z = (CHAIN == LTE_CHAIN_UNCODED && g.no_eq) ? Y : zc[q].apply(Y);
+        if (cap_syms) cap_syms[fre + re] = z;
+        if constexpr (CHAIN == LTE_CHAIN_CODED) {
+          if (nvo) {   // demap in k_dematch_zn: the equalised symbol (sigma^2_eff per subcarrier in nvo)
+            reinterpret_cast<V*>(llr)[fre + re] = z;
+            continue;
+          }
+          R o[BPS];
+          soft_demap<BPS>(z, nvq[q], o);
+          R* lo = llr + (fre + re) * BPS;
+          if constexpr (BPS == 4 && sizeof(R) == 4) {
+            *reinterpret_cast<float4*>(lo) = make_float4(o[0], o[1], o[2], o[3]);
+          } else {
+#pragma unroll
+            for (int m = 0; m < BPS; m += 2) *reinterpret_cast<V*>(lo + m) = mkc(o[m], o[m + 1]);
+          }
+        } else {
+          const int idx = hard_index(z, BPS, QS);
+          const int64_t pb0 = (int64_t)re * BPS;
+#pragma unroll
+          for (int m = 0; m < BPS; ++m) {
+            const int64_t pbit = pb0 + m;
+            if (pbit < n_bits) {
+              const uint32_t bit = (idx >> (BPS - 1 - m)) & 1;
+              errs += bit ^ getbit(fb, pbit);
+              if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();   // every read of buf done before the next symbol lands in it
+  }
+  if constexpr (CHAIN != LTE_CHAIN_CODED) frame_err_add(frame_err, b, errs);
+}
+
+bool rx_frame_supported(const Grid& g, int chain, int num_rx, int sc_fdm) {
+  return num_rx == 1 && !sc_fdm && (chain == LTE_CHAIN_CODED || chain == LTE_CHAIN_UNCODED) &&
+         (g.bps == 2 || g.bps == 4 || g.bps == 6) && 2 * g.Nd < g.N;
+}
+
+template <class R>
+int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, const cx<R>* y,
+                    int64_t y_frame_stride, const R* npow, const R* snr_lin, const uint64_t* fid, uint64_t seed,
+                    const R* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits, R* nv_out, cx<R>* H, R* pstats) {
+  if (!rx_frame_supported(g, chain, 1, 0) || (nv_out && chain != LTE_CHAIN_CODED)) return (int)hipErrorInvalidValue;
+  const int spw = WG / (g.N >> 3);
+  const int blocks = (B + spw - 1) / spw;
+  const size_t shm = (size_t)spw * (g.N + g.Np) * sizeof(cx<R>);
+#define LTE_RXF(CH_, BPS_, NC_)                                                                                      \
+  hipLaunchKernelGGL((k_rx_frame<R, CH_, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, y,             \
+                     y_frame_stride, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,    \
+                     cap_syms, cap_bits, nv_out, H, pstats)
+#define LTE_RXF_BPS(CH_, NC_)                                                                                        \
+  do {                                                                                                               \
+    if (g.bps == 2) LTE_RXF(CH_, 2, NC_);                                                                            \
+    else if (g.bps == 4) LTE_RXF(CH_, 4, NC_);                                                                       \
+    else LTE_RXF(CH_, 6, NC_);                                                                                       \
+  } while (0)
+  if (chain == LTE_CHAIN_CODED) {
+    if (g.N == 2048) LTE_RXF_BPS(LTE_CHAIN_CODED, 2048);   // the headline chain
+    else LTE_RXF_BPS(LTE_CHAIN_CODED, 0);
+  } else {
+    if (g.N == 2048) LTE_RXF_BPS(LTE_CHAIN_UNCODED, 2048);
+    else LTE_RXF_BPS(LTE_CHAIN_UNCODED, 0);
+  }
+#undef LTE_RXF_BPS
+#undef LTE_RXF
+  return (int)hipGetLastError();
 }
 
 template <class R, int CHAIN, bool SCF = false, int NC = 0>
@@ -897,7 +1124,10 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                                   const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, R*);                        \
   template int launch_rx_data<R>(hipStream_t, const Grid&, int, int, int, int, const cx<R>*, int64_t, int64_t,       \
                                  const cx<R>*, const R*, const R*, const uint64_t*, uint64_t, const R*, int64_t,    \
-                                 const uint32_t*, int, int, uint32_t*, R*, cx<R>*, uint8_t*, int, R*);
+                                 const uint32_t*, int, int, uint32_t*, R*, cx<R>*, uint8_t*, int, R*);              \
+  template int launch_rx_frame<R>(hipStream_t, const Grid&, int, int, int, const cx<R>*, int64_t, const R*, const R*, \
+                                  const uint64_t*, uint64_t, const R*, int64_t, const uint32_t*, int, int, uint32_t*, \
+                                  R*, cx<R>*, uint8_t*, R*, cx<R>*, R*);
 LTE_INST(float)
 LTE_INST(double)
 #undef LTE_INST

@@ -82,10 +82,13 @@ int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_
 // bps LLRs per RE), computes the max-log LLRs (soft_demap, the function
 // k_rx_data uses) into an LDS tile [frame][LLR], then writes whole decoder
 // rows exactly as k_dematch.  f64 covers 8 REs per block (49 KB tile at 16).
+// The noise variance is per (frame, 14-symbol group, data subcarrier): RE re =
+// l * nd + j of a frame reads nv[b * n_nv + (l / 14) * nd + j].
 template <class R> constexpr int dz_re() { return sizeof(R) == 8 ? 8 : 16; }
 template <class R, int BPS>
 __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z, const R* __restrict__ nv, int n_re,
-                                                    int B, const int32_t* __restrict__ rx_map, int add,
+                                                    int nd, int n_nv, int B, const int32_t* __restrict__ rx_map,
+                                                    int add,
                                                     R* const* __restrict__ blk, const int64_t* __restrict__ rows,
                                                     int g0) {
   using V = cx<R>;
@@ -102,8 +105,9 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
     const int e = threadIdx.x + k * 256, f = e / DZ_RE, r = e % DZ_RE, b = g * 64 + f;
     const bool ok = b < B && r < nr;
     const size_t i = (size_t)b * n_re + re0 + r;
+    const int l = (re0 + r) / nd, j = re0 + r - l * nd;
     zv[k] = ok ? z[i] : mkc((R)0, (R)0);
-    nvv[k] = ok ? nv[i] : (R)1;
+    nvv[k] = ok ? nv[(size_t)b * n_nv + (l / 14) * nd + j] : (R)1;
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -125,21 +129,22 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
 }
 
 template <class R>
-int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int bps, int B, const int32_t* rx_map,
-                      int n_layers, R* const* blk, const int64_t* rows, int g0) {
+int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int nd, int bps, int B,
+                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int g0) {
   const int G = (B + 63) / 64 - g0;
-  if (G < 1 || G > 65535 || (bps != 4 && bps != 6) || n_layers < 1) return (int)hipErrorInvalidValue;
+  if (G < 1 || G > 65535 || (bps != 4 && bps != 6) || n_layers < 1 || nd < 1) return (int)hipErrorInvalidValue;
+  const int n_nv = ((n_re / nd + 13) / 14) * nd;   // groups x data subcarriers per frame
   constexpr int DZ = dz_re<R>();
   const dim3 grid((n_re + DZ - 1) / DZ, G);
   const int T = n_re * bps;
   for (int k = 0; k < n_layers; ++k) {
     const int32_t* mp = rx_map + (size_t)k * T;
     if (bps == 4)
-      hipLaunchKernelGGL((k_dematch_zn<R, 4>), grid, dim3(256), 0, s, z, nv, n_re, B, mp, k > 0 ? 1 : 0, blk, rows,
-                         g0);
+      hipLaunchKernelGGL((k_dematch_zn<R, 4>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, B, mp, k > 0 ? 1 : 0,
+                         blk, rows, g0);
     else
-      hipLaunchKernelGGL((k_dematch_zn<R, 6>), grid, dim3(256), 0, s, z, nv, n_re, B, mp, k > 0 ? 1 : 0, blk, rows,
-                         g0);
+      hipLaunchKernelGGL((k_dematch_zn<R, 6>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, B, mp, k > 0 ? 1 : 0,
+                         blk, rows, g0);
     const int e = (int)hipGetLastError();
     if (e) return e;
   }
@@ -150,10 +155,10 @@ template int launch_dematch<float>(hipStream_t, const float*, int, int, const in
                                    const int64_t*, int);
 template int launch_dematch<double>(hipStream_t, const double*, int, int, const int32_t*, int, double* const*,
                                     const int64_t*, int);
-template int launch_dematch_zn<float>(hipStream_t, const float2*, const float*, int, int, int, const int32_t*, int,
-                                      float* const*, const int64_t*, int);
-template int launch_dematch_zn<double>(hipStream_t, const double2*, const double*, int, int, int, const int32_t*,
-                                       int, double* const*, const int64_t*, int);
+template int launch_dematch_zn<float>(hipStream_t, const float2*, const float*, int, int, int, int, const int32_t*,
+                                      int, float* const*, const int64_t*, int);
+template int launch_dematch_zn<double>(hipStream_t, const double2*, const double*, int, int, int, int,
+                                       const int32_t*, int, double* const*, const int64_t*, int);
 
 // ---------------------------------------------------------------------------
 // Stage entry: rate_dematching_turbo (rate_matching.py:374-489) for any E,

@@ -429,6 +429,44 @@ def test_fused_tx_channel_matches_separate_kernels(C, monkeypatch, chain, prec):
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('chain,bw,mod', [('coded', 20.0, '64-QAM'), ('coded', 5.0, '16-QAM'),
+                                          ('uncoded', 20.0, '64-QAM'), ('uncoded', 1.25, 'QPSK')])
+def test_fused_receiver_matches_separate_kernels(C, monkeypatch, chain, bw, mod, prec):
+    """The fused SISO receiver (k_rx_frame: estimation on each group's first
+    symbol + data path, per-subcarrier equaliser terms) vs k_rx_chest +
+    k_rx_data on the same Philox frames: channel estimates, pilot statistics,
+    equalised symbols and LLRs to round-off (same operations; the per-
+    subcarrier terms are formed once instead of per RE), identical decisions
+    and counts; and without captures (the demap-in-dematch path) identical
+    per-frame bit errors and CRC verdicts."""
+    sim = _sim(bw, mod, 'rayleigh_mp', prec)
+    B = 64 + 7
+    coded = chain == 'coded'
+    plan = sim._plan(C.CHAIN_CODED, 0, 27760 if bw == 20.0 else 3000, max_frames=B) if coded else \
+        sim._plan(C.CHAIN_UNCODED, 14, 14 * sim.Nd * sim.config.bits_per_symbol, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('H', 'pilot_stats', 'data_syms') + (('llr',) if coded else ('bits_rx',))
+    runs = {}
+    for fuse in ('0', '1'):
+        monkeypatch.setenv('LTE_RX_FUSE', fuse)
+        runs[fuse] = (plan.run(snr, seed=0x5EED, frame_id0=3, capture=cap),
+                      plan.run(snr, seed=0x5EED, frame_id0=3))
+    (a, a0), (b, b0) = runs['0'], runs['1']
+    tol = 1e-13 if prec == 'f64' else 1e-5
+    for k in ('H', 'pilot_stats', 'data_syms'):
+        assert np.max(np.abs(b[k] - a[k])) <= tol * np.max(np.abs(a[k])), k
+    if coded:
+        assert np.max(np.abs(b['llr'] - a['llr']) / (1 + np.abs(a['llr']))) < (1e-10 if prec == 'f64' else 1e-3)
+        assert np.array_equal(a['crc_ok'], b['crc_ok'])
+        assert np.array_equal(a0['frame_errors'], b0['frame_errors']) and np.array_equal(a0['crc_ok'], b0['crc_ok'])
+        assert 0 < int(np.sum(b0['crc_ok'])) < B
+    else:
+        assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 2
+    assert abs(int(a0['counts'][:, 0].sum()) - int(b0['counts'][:, 0].sum())) <= (0 if coded else 2)
+    assert np.array_equal(a0['counts'][:, 1], b0['counts'][:, 1])
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mod', ['16-QAM', '64-QAM'])
 def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
     """k_rx_data handing (z, sigma^2_eff) per RE to k_dematch_zn, which runs the

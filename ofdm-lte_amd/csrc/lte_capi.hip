@@ -1593,6 +1593,17 @@ static int upload_inj(DBuf<R>& dst, const double* src, int64_t stride, int B, si
   return LTE_OK;
 }
 
+// Coded TX + channel with one slot per frame (k_ofdm_txf) when its LDS fits
+// (coded streams staged once per frame); LTE_TX_FRAME=0 keeps one slot per
+// OFDM symbol (k_ofdm_tx<.., CH>, A/B and parity tests).
+static bool tx_per_frame(const lte_plan* p) {
+  if (const char* e = std::getenv("LTE_TX_FRAME"))
+    if (std::atoi(e) == 0) return false;
+  const int spw = 256 / (p->grid.N >> 3);
+  const size_t el = p->f64 ? 16 : 8;
+  return (size_t)spw * (p->grid.N * el + (size_t)p->enc_words * 4) <= 65536;
+}
+
 // Fading taps, fused TX + channel, first-samples power fix-up and noise power.
 template <class R>
 static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bool coded, const R* inj_ph,
@@ -1616,8 +1627,11 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
   ch.pow_part = c.pow_part.p;
   {
     Timer t(p, KN_OFDM_TX, s);
-    LCHK(launch_ofdm_tx_ch<R>(s, p->grid, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, B,
-                              cap_tx_syms, ch));
+    if (coded && tx_per_frame(p))
+      LCHK(launch_ofdm_txf<R>(s, p->grid, p->enc.p, p->enc_words, p->tx_map.p, B, cap_tx_syms, ch));
+    else
+      LCHK(launch_ofdm_tx_ch<R>(s, p->grid, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, B,
+                                cap_tx_syms, ch));
   }
   {
     Timer t(p, KN_CHANNEL, s);

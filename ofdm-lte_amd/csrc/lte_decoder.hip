@@ -480,8 +480,17 @@ __global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mo
   turbo_body<float>(jobs, iters, mode);
 }
 
-// f64: at most 256 VGPRs (2 waves per SIMD)
-__global__ __launch_bounds__(256, 2) void k_turbo64(TurboJobs jobs, int iters, int mode) {
+// f64: one wave per SIMD (LTE_TURBO64_ONE_WAVE, default on; 0: up to 256
+// VGPRs, two waves).  The decoder streams HBM slightly faster with one
+// resident wave per SIMD than with two (A/B on one MI355X: 358 / 359 ms vs
+// 367 / 368 ms per 65 536 frames); the cap is set by reserving 32 AGPRs.
+#ifndef LTE_TURBO64_ONE_WAVE
+#define LTE_TURBO64_ONE_WAVE 1
+#endif
+__global__ __launch_bounds__(256, LTE_TURBO64_ONE_WAVE ? 1 : 2) void k_turbo64(TurboJobs jobs, int iters, int mode) {
+#if LTE_TURBO64_ONE_WAVE
+  asm volatile("" ::: "a31");
+#endif
   turbo_body<double>(jobs, iters, mode);
 }
 

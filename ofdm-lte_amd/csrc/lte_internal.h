@@ -99,6 +99,11 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
                       int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch);
 template <class R>
 int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannelT<R>& ch);
+// coded TX + channel with one slot per frame (the frame's coded streams staged
+// in LDS once); same outputs as launch_ofdm_tx_ch(coded = 1)
+template <class R>
+int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map, int B,
+                    cx<R>* cap_syms, const TxChannelT<R>& ch);
 template <class R>
 int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>* y, int64_t y_rx_stride,
                     int64_t y_frame_stride, const R* npow, const uint64_t* fid, uint64_t seed, const R* inj_z,

@@ -333,6 +333,98 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
   return (int)hipGetLastError();
 }
 
+// Coded OFDM TX + static-tap channel, one slot per frame walking its OFDM
+// symbols in order: the frame's coded streams are staged in LDS once (instead
+// of once per symbol), then per symbol the same work as k_ofdm_tx<.., CH>: RE
+// mapping through tx_map, pilots, IFFT (f64: output scale in the last pass),
+// taps, received stream and per-symbol power.  Identical arithmetic per
+// sample (test_frame_tx_matches_symbol_tx).
+#ifndef TXF_WAVES
+#define TXF_WAVES 1
+#endif
+template <class R, int BPS, int NC = 0>
+__global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32_t* __restrict__ enc, int enc_words,
+                                                          const int32_t* __restrict__ tx_map, int B,
+                                                          cx<R>* __restrict__ cap_syms, TxChannelT<R> ch) {
+  using V = cx<R>;
+  using G = GridT<R>;
+  V* sm = dyn_lds<V>();
+  const int N = NC ? NC : g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
+  const int b = blockIdx.x * spw + slot;
+  const bool active = slot < spw && b < B;
+  V* buf = sm + slot * N;
+  uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
+  if (active) {
+    const uint32_t* fe = enc + (size_t)b * enc_words;
+    for (int i = tid0; i < enc_words; i += T) es[i] = fe[i];
+  }
+  const R sc = tx_scale<R>(N);
+  constexpr int QM = 4;   // Nd < N/2 = QM * T for every LTE profile
+  for (int l = 0; l < g.n_sym; ++l) {
+    int tid = tid0;   // opaque per symbol: address arithmetic is not hoisted out of the loop
+    asm volatile("" : "+v"(tid));
+    int srcs[QM][BPS];
+    int kpos[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = tid + q * T;
+      const bool ok = active && j < g.Nd;
+      const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
+#pragma unroll
+      for (int m = 0; m < BPS; ++m) srcs[q][m] = ok ? tx_map[t0 + m] : -1;
+      kpos[q] = ok ? g.data_idx[j] : 0;
+    }
+    if (active)
+      for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
+    __syncthreads();   // (first symbol: also the staged streams)
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) {
+        const int j = tid + q * T;
+        if (j >= g.Nd) break;
+        int idx = 0;
+        bool zero = false;
+#pragma unroll
+        for (int m = 0; m < BPS; ++m) {
+          zero |= srcs[q][m] == -2;
+          const uint32_t bit = srcs[q][m] >= 0 ? getbit(es, srcs[q][m]) : 0u;
+          idx = (idx << 1) | (int)bit;
+        }
+        const V sym = zero ? mkc((R)0, (R)0) : qam_point<BPS, R>(idx);
+        buf[kpos[q]] = sym;
+        if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + j] = sym;
+      }
+      for (int p = tid; p < g.Np; p += T) buf[g.pilot_idx[p]] = G::pilots(g)[p];
+    }
+    __syncthreads();
+    fft_lds<true, NC, sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
+    // every read of buf in tx_channel precedes its reduction barrier, so the
+    // next symbol may overwrite buf after it
+    tx_channel<R>(buf, g, ch, b, l, slot, tid, T, active, sc);
+  }
+}
+
+template <class R>
+int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map, int B,
+                    cx<R>* cap_syms, const TxChannelT<R>& ch) {
+  const int spw = WG / (g.N >> 3);
+  if (!txch_supported(g, ch.n_paths, ch.max_delay) || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
+  const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + (size_t)spw * enc_words * sizeof(uint32_t);
+  if (shm > 65536) return (int)hipErrorInvalidValue;
+  const int blocks = (B + spw - 1) / spw;
+#define LTE_TXF(BPS_, NC_)                                                                                      \
+  hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, tx_map, B, \
+                     cap_syms, ch)
+  if (g.N == 2048) {
+    if (g.bps == 2) LTE_TXF(2, 2048); else if (g.bps == 4) LTE_TXF(4, 2048); else LTE_TXF(6, 2048);
+  } else {
+    if (g.bps == 2) LTE_TXF(2, 0); else if (g.bps == 4) LTE_TXF(4, 0); else LTE_TXF(6, 0);
+  }
+#undef LTE_TXF
+  return (int)hipGetLastError();
+}
+
 // Power of each symbol's first max_delay channel-output samples (their delayed
 // taps reach into the previous symbol's tail, or the zero prefix of symbol 0),
 // added to the symbol's partial.  16 lanes per (frame, symbol), one sample
@@ -1115,6 +1207,8 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
   template int launch_ofdm_tx_ch<R>(hipStream_t, const Grid&, int, const uint32_t*, int, const uint32_t*, int,       \
                                     const int32_t*, int, cx<R>*, const TxChannelT<R>&);                             \
   template int launch_chan_fix<R>(hipStream_t, const Grid&, int, const TxChannelT<R>&);                             \
+  template int launch_ofdm_txf<R>(hipStream_t, const Grid&, const uint32_t*, int, const int32_t*, int, cx<R>*,      \
+                                  const TxChannelT<R>&);                                                             \
   template int launch_fading<R>(hipStream_t, int, int, int, const R*, const uint64_t*, uint64_t, const R*, int64_t, \
                                 R*, cx<R>*);                                                                         \
   template int launch_channel<R>(hipStream_t, const Grid&, int, int, int, int, const int32_t*, const R*, R, R,       \

@@ -467,6 +467,27 @@ def test_fused_receiver_matches_separate_kernels(C, monkeypatch, chain, bw, mod,
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('bw,mod', [(20.0, '64-QAM'), (5.0, '16-QAM'), (10.0, 'QPSK')])
+def test_frame_tx_matches_symbol_tx(C, monkeypatch, bw, mod, prec):
+    """Coded TX + channel with one slot per frame (k_ofdm_txf, coded streams
+    staged once per frame) vs one slot per OFDM symbol (k_ofdm_tx<.., CH>):
+    the same operations per sample, so noise powers, transmitted symbols and
+    LLRs are identical."""
+    sim = _sim(bw, mod, 'rayleigh_mp', prec)
+    B = 64 + 3
+    plan = sim._plan(C.CHAIN_CODED, 0, 27760 if bw == 20.0 else 4000, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('noise_power', 'tx_syms', 'llr')
+    monkeypatch.setenv('LTE_TX_FRAME', '0')
+    a = plan.run(snr, seed=0x5EED, frame_id0=21, capture=cap)
+    monkeypatch.setenv('LTE_TX_FRAME', '1')
+    b = plan.run(snr, seed=0x5EED, frame_id0=21, capture=cap)
+    for k in cap:
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a['crc_ok'], b['crc_ok']) and np.array_equal(a['counts'], b['counts'])
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mod', ['16-QAM', '64-QAM'])
 def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
     """k_rx_data handing (z, sigma^2_eff) per RE to k_dematch_zn, which runs the

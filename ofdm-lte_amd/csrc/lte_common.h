@@ -222,7 +222,11 @@ __device__ __forceinline__ void dft8_inplace(V (&v)[8]) {
 // (ofdm_tx / rx_data / rx_chest at N = 2048: -2..-15 % time).  NC = 0: runtime N.
 // SC: the last pass multiplies its outputs by osc (an output scale folded into
 // the final store instead of a separate LDS pass).
-template <bool INV, int NC = 0, bool SC = false, class V>
+// TWR (default for a compile-time N): the twiddles of a butterfly, w^(r ks)
+// for r >= 2, formed from w^ks by complex products -- one table load per
+// butterfly instead of 7 (radix 8) / 3 (radix 4), a few ulp each; the f64
+// N = 2048 transform runs 22 % faster (scripts/rx_parts_bench.hip).
+template <bool INV, int NC = 0, bool SC = false, bool TWR = (NC > 0), class V>
 __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __restrict__ tw, int tid, bool active,
                                         re_t<V> osc = (re_t<V>)1) {
   const int N = NC ? NC : N_;
@@ -246,8 +250,21 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
         }
         if (s > 0) {
           const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));   // k * N / (8 Ns)
+          if constexpr (TWR) {
+            V w[8];
+            w[1] = twid<INV>(tw, ks);
+            w[2] = cmul(w[1], w[1]);
+            w[3] = cmul(w[2], w[1]);
+            w[4] = cmul(w[2], w[2]);
+            w[5] = cmul(w[4], w[1]);
+            w[6] = cmul(w[3], w[3]);
+            w[7] = cmul(w[4], w[3]);
 #pragma unroll
-          for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], twid<INV>(tw, r * ks));
+            for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], w[r]);
+          } else {
+#pragma unroll
+            for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], twid<INV>(tw, r * ks));
+          }
         }
         dft8_inplace<INV>(v);
       }
@@ -305,8 +322,15 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
         const int j = tid + q * T;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[q][r] = buf[fft_sw(j + r * q4)];
+        if constexpr (TWR) {
+          const V w1 = twid<INV>(tw, j), w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+          v[q][1] = cmul(v[q][1], w1);
+          v[q][2] = cmul(v[q][2], w2);
+          v[q][3] = cmul(v[q][3], w3);
+        } else {
 #pragma unroll
-        for (int r = 1; r < 4; ++r) v[q][r] = cmul(v[q][r], twid<INV>(tw, j * r));
+          for (int r = 1; r < 4; ++r) v[q][r] = cmul(v[q][r], twid<INV>(tw, j * r));
+        }
         dft4_inplace<INV>(v[q][0], v[q][1], v[q][2], v[q][3]);
       }
     }

@@ -38,7 +38,7 @@
 #define LTE_TURBO_HALVES 2
 #endif
 #ifndef LTE_TURBO64_SUB
-#define LTE_TURBO64_SUB 2
+#define LTE_TURBO64_SUB 3   // f64: 24-step super-windows (A/B on MI355X: 2 / 3 / 4 -> 352 / 341 / 377 ms)
 #endif
 #ifndef LTE_TURBO64_HALVES
 #define LTE_TURBO64_HALVES 2
@@ -249,7 +249,7 @@ struct RowPtr {
 // only 8 / HALVES alpha vectors are ever live.  Recomputed alphas are
 // bit-identical to the forward pass (same operations, same order).  HBM rows
 // per step: 3 input loads x 2 passes + 1 extrinsic store + 2 CK/SW checkpoint
-// rows (f32 TSUB = 2: 7.875 rows of 4 B; f64 TSUB = 2: 8 rows of 8 B).
+// rows (f32 TSUB = 2: 7.875 rows of 4 B; f64 TSUB = 3: 7.67 rows of 8 B).
 // MODE TM_FINAL: the decoder-1 a-posteriori pass that ends a decode; it also
 // packs the hard decisions L < 0 MSB-first into `bo` (words [kw][64 lanes]),
 // storing each word as the backward sweep reaches its bit 0 (no re-read pass).

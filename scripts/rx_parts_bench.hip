@@ -40,15 +40,22 @@ __global__ __launch_bounds__(256) void k_noise(double* out, uint64_t seed) {
   out[t] = acc + (double)xacc;
 }
 
-template <class R>
+template <class R, bool TWR = false, int REP = 1>
 __global__ __launch_bounds__(256) void k_fft(const cx<R>* __restrict__ tw, double* out) {
   extern __shared__ double2 lds_raw[];
   cx<R>* buf = reinterpret_cast<cx<R>*>(lds_raw);
-  const int tid = threadIdx.x;
-  for (int k = tid; k < N; k += 256) buf[k] = mkc((R)(k ^ blockIdx.x), (R)(k - (int)blockIdx.x));
-  __syncthreads();
-  fft_lds<false, N>(buf, N, 11, tw, tid, true);
-  out[(size_t)blockIdx.x * 256 + tid] = (double)buf[tid].x;
+  const int tid0 = threadIdx.x;
+  double acc = 0.0;
+  for (int rep = 0; rep < REP; ++rep) {   // REP FFTs per block in sequence (the per-frame kernels' shape)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    for (int k = tid; k < N; k += 256) buf[k] = mkc((R)(k ^ (blockIdx.x + rep)), (R)(k - (int)blockIdx.x));
+    __syncthreads();
+    fft_lds<false, N, false, TWR>(buf, N, 11, tw, tid, true);
+    acc += (double)buf[tid].x;
+    __syncthreads();
+  }
+  out[(size_t)blockIdx.x * 256 + tid0] = acc;
 }
 
 __global__ __launch_bounds__(256) void k_cdiv(const double2* __restrict__ h, double* out, int per) {
@@ -128,6 +135,15 @@ int main() {
   auto f32 = [](void* a) {
     hipLaunchKernelGGL(k_fft<float>, dim3(FRAMES * NSYM / 8), dim3(256), N * sizeof(float2), 0, ((Ctx*)a)->tw32, ((Ctx*)a)->out);
   };
+  auto f64t = [](void* a) {
+    hipLaunchKernelGGL((k_fft<double, true>), dim3(FRAMES * NSYM / 8), dim3(256), N * sizeof(double2), 0, ((Ctx*)a)->tw64, ((Ctx*)a)->out);
+  };
+  auto f64r = [](void* a) {   // 14 FFTs per block (one frame's symbols)
+    hipLaunchKernelGGL((k_fft<double, false, 14>), dim3(FRAMES / 8), dim3(256), N * sizeof(double2), 0, ((Ctx*)a)->tw64, ((Ctx*)a)->out);
+  };
+  auto f64rt = [](void* a) {
+    hipLaunchKernelGGL((k_fft<double, true, 14>), dim3(FRAMES / 8), dim3(256), N * sizeof(double2), 0, ((Ctx*)a)->tw64, ((Ctx*)a)->out);
+  };
   auto cd = [](void* a) {
     hipLaunchKernelGGL(k_cdiv, dim3(FRAMES * 14 / 256), dim3(256), 0, 0, ((Ctx*)a)->h, ((Ctx*)a)->out, 999 / 8);
   };
@@ -135,6 +151,7 @@ int main() {
   const float t0 = timeit(p0, &c), t1 = timeit(p1, &c), t2 = timeit(p2, &c);
   // FFTs: 1/8 of the subframes' FFTs timed, scaled by 8
   const float t3 = 8 * timeit(f64, &c), t4 = 8 * timeit(f32, &c);
+  const float t3t = 8 * timeit(f64t, &c), t3r = 8 * timeit(f64r, &c), t3rt = 8 * timeit(f64rt, &c);
   // divisions: FRAMES*14/256 blocks * 256 threads * 124 = 1/8 of 13 986 per subframe, scaled by 8
   const float t5 = 8 * timeit(cd, &c);
   printf("{\"part\": \"philox\", \"ms_per_65536_subframes\": %.3f}\n", t0);
@@ -142,6 +159,9 @@ int main() {
   printf("{\"part\": \"bm64_table\", \"ms_per_65536_subframes\": %.3f}\n", t2);
   printf("{\"part\": \"fft64\", \"ms_per_65536_subframes\": %.3f}\n", t3);
   printf("{\"part\": \"fft32\", \"ms_per_65536_subframes\": %.3f}\n", t4);
+  printf("{\"part\": \"fft64_twr\", \"ms_per_65536_subframes\": %.3f}\n", t3t);
+  printf("{\"part\": \"fft64_14_per_block\", \"ms_per_65536_subframes\": %.3f}\n", t3r);
+  printf("{\"part\": \"fft64_14_per_block_twr\", \"ms_per_65536_subframes\": %.3f}\n", t3rt);
   printf("{\"part\": \"cdiv64\", \"ms_per_65536_subframes\": %.3f}\n", t5);
   const int n = 1 << 22;
   hipLaunchKernelGGL(k_acc, dim3(n / 256), dim3(256), 0, 0, c.out, n);

@@ -919,9 +919,9 @@ static int plan_coded_maps(lte_plan* p) {
       const int K = p->cbs[r].K;
       const RmSrc s = rs[r][i];
       int row = -1;
-      if (s.stream == 0) row = s.idx < K + 3 ? s.idx : 3 * K + 9 + (s.idx - K - 3);
-      else if (s.stream == 1) row = K + 3 + s.idx;
-      else if (s.stream == 2) row = 2 * K + 6 + s.idx;
+      if (s.stream == 0) row = (int)(s.idx < K + 3 ? trow_ls(K, s.idx) : trow_ls2t(K, s.idx - K - 3));
+      else if (s.stream == 1) row = (int)trow_lp(K, 1, s.idx);
+      else if (s.stream == 2) row = (int)trow_lp(K, 2, s.idx);
       if (row >= 0) rxm[(size_t)(i / (3 * (K + 6))) * p->n_re_bits + (size_t)re * bps + m] = (r << 24) | row;
     }
     (void)base;
@@ -2169,20 +2169,20 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const T* llr, const T* 
       const T* s = ls + c * (K + 3);
       const T* q = lp + c * (K + 3);
       const T* A = la + c * (K + 3);
-      for (int k = 0; k < K + 3; ++k) { at(c, k) = s[k]; at(c, K + 3 + k) = q[k]; }
-      for (int k = 0; k < K; ++k) at(c, 3 * K + 12 + k) = A[k];
+      for (int k = 0; k < K + 3; ++k) { at(c, trow_ls(K, k)) = s[k]; at(c, trow_lp(K, 1, k)) = q[k]; }
+      for (int k = 0; k < K; ++k) at(c, trow_le(K, k)) = A[k];
     } else {
       const T* l = llr + c * (3 * K + 12);
       for (int k = 0; k < K; ++k) {
-        at(c, k) = l[3 * k];
-        at(c, K + 3 + k) = l[3 * k + 1];
-        at(c, 2 * K + 6 + k) = l[3 * k + 2];
+        at(c, trow_ls(K, k)) = l[3 * k];
+        at(c, trow_lp(K, 1, k)) = l[3 * k + 1];
+        at(c, trow_lp(K, 2, k)) = l[3 * k + 2];
       }
       for (int t = 0; t < 3; ++t) {
-        at(c, K + t) = l[3 * K + t];
-        at(c, 2 * K + 3 + t) = l[3 * K + 3 + t];
-        at(c, 3 * K + 9 + t) = l[3 * K + 6 + t];
-        at(c, 3 * K + 6 + t) = l[3 * K + 9 + t];
+        at(c, trow_ls(K, K + t)) = l[3 * K + t];
+        at(c, trow_lp(K, 1, K + t)) = l[3 * K + 3 + t];
+        at(c, trow_ls2t(K, t)) = l[3 * K + 6 + t];
+        at(c, trow_lp(K, 2, K + t)) = l[3 * K + 9 + t];
       }
     }
   }
@@ -2204,7 +2204,7 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const T* llr, const T* 
       if (hipMemcpy(h.data(), db.p, h.size() * sizeof(T), hipMemcpyDeviceToHost) != hipSuccess)
         rc = fail(LTE_EHIP, "copy");
       for (int64_t c = 0; c < ncb && rc == LTE_OK; ++c)
-        for (int k = 0; k < K; ++k) app[c * K + k] = at(c, 3 * K + 12 + k);
+        for (int k = 0; k < K; ++k) app[c * K + k] = at(c, trow_le(K, k));
     } else {
       if (hipMemcpy(hb.data(), dbits.p, hb.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(LTE_EHIP, "copy");
       for (int64_t c = 0; c < ncb && rc == LTE_OK; ++c)

@@ -40,6 +40,9 @@
 #ifndef LTE_TURBO64_SUB
 #define LTE_TURBO64_SUB 3   // f64: 24-step super-windows (A/B on MI355X: 2 / 3 / 4 -> 352 / 341 / 377 ms)
 #endif
+#ifndef LTE_TURBO64_FWD_PF
+#define LTE_TURBO64_FWD_PF 0
+#endif
 #ifndef LTE_TURBO64_HALVES
 #define LTE_TURBO64_HALVES 2
 #endif
@@ -52,6 +55,7 @@ template <> struct TurboT<float> {
   static constexpr int CK = TURBO_CK_ROWS_F32;   // checkpointed states 1..7 (state 0 is 0)
   static constexpr int TSUB = LTE_TURBO_SUB;     // 8-step sub-windows per checkpoint
   static constexpr int HALVES = LTE_TURBO_HALVES;
+  static constexpr bool FWD_PF = false;
   __device__ static constexpr float neg() { return LTE_NEG_BIG; }
 };
 template <> struct TurboT<double> {
@@ -59,6 +63,7 @@ template <> struct TurboT<double> {
   static constexpr int CK = TURBO_CK_ROWS_F64;   // all 8 states
   static constexpr int TSUB = LTE_TURBO64_SUB;
   static constexpr int HALVES = LTE_TURBO64_HALVES;
+  static constexpr bool FWD_PF = LTE_TURBO64_FWD_PF;
   __device__ static constexpr double neg() { return -__builtin_inf(); }
 };
 
@@ -218,8 +223,9 @@ struct RowPtr {
   __amdgpu_buffer_rsrc_t r;
   int row0;   // first row of this sub-array inside the block
   int voff;   // sizeof(T) * lane
+  int rstr = 1;   // row stride of the sub-array (2: interleaved LS / LE)
   __device__ __forceinline__ T ld(int row) const {
-    const int so = (row0 + row) * (RS * (int)sizeof(T));
+    const int so = (row0 + row * rstr) * (RS * (int)sizeof(T));
     if constexpr (sizeof(T) == 8) {
       return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, voff, so, 0));
     } else {
@@ -227,7 +233,7 @@ struct RowPtr {
     }
   }
   __device__ __forceinline__ void st(int row, T v) const {
-    const int so = (row0 + row) * (RS * (int)sizeof(T));
+    const int so = (row0 + row * rstr) * (RS * (int)sizeof(T));
     if constexpr (sizeof(T) == 8) {
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, voff, so, 0);
     } else {
@@ -261,10 +267,15 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
   constexpr int TH = TW / TT::HALVES;
   const int vo = lane * (int)sizeof(T);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * sizeof(T)));
-  const RowPtr<T> LS{rb, 0, vo};
-  const RowPtr<T> LP{rb, ((MODE == TM_DEC2) ? 2 : 1) * (K + 3), vo};
-  const RowPtr<T> LS2T{rb, 3 * K + 9, vo};
-  const RowPtr<T> LE{rb, 3 * K + 12, vo};
+  // rows of step k < K: base + k * stride (lte_internal.h trow_*); tails separately
+  constexpr int IST = LTE_TURBO_ILV == 3 ? 4 : LTE_TURBO_ILV == 2 ? 3 : LTE_TURBO_ILV == 1 ? 2 : 1;
+  constexpr int DEC = (MODE == TM_DEC2) ? 2 : 1;
+  const RowPtr<T> LS{rb, 0, vo, IST};
+  const RowPtr<T> LS1T{rb, (int)trow_ls(K, K), vo};   // decoder 1's systematic tail
+  const RowPtr<T> LP{rb, (int)trow_lp(K, DEC, 0), vo, LTE_TURBO_ILV == 3 ? 4 : (DEC == 1 && LTE_TURBO_ILV == 2) ? 3 : 1};
+  const RowPtr<T> LPT{rb, (int)trow_lp(K, DEC, K), vo};   // parity tail
+  const RowPtr<T> LS2T{rb, (int)trow_ls2t(K, 0), vo};
+  const RowPtr<T> LE{rb, (int)trow_le(K, 0), vo, IST};
   const RowPtr<T> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * CK * RS * sizeof(T))), 0, vo};
   const int nsub = K / TW;   // every LTE K is a multiple of 8
   const int tf2 = (2 * f2) % K;
@@ -279,13 +290,8 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
 #pragma unroll
   for (int s = 1; s < 8; ++s) a[s] = TT::neg();
   int pi = 0, d = (f1 + f2) % K;
-#pragma unroll 1
-  for (int w = 0; w < nsub; ++w) {
-    if (w % TSUB == 0) {
-#pragma unroll
-      for (int s = CK0; s < 8; ++s) ck.st((w / TSUB) * CK + s - CK0, a[s]);
-    }
-    T ls[TW], lp[TW], la[TW];
+  // window w's inputs (pi / d advance in window order)
+  auto ldwin = [&](int w, T (&ls)[TW], T (&lp)[TW], T (&la)[TW]) {
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
       const int k = w * TW + j;
@@ -295,6 +301,12 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
       la[j] = use_la ? LE.ld(p) : (T)0;
       if (MODE == TM_DEC2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
     }
+  };
+  auto stepwin = [&](int w, const T (&ls)[TW], const T (&lp)[TW], const T (&la)[TW]) {
+    if (w % TSUB == 0) {
+#pragma unroll
+      for (int s = CK0; s < 8; ++s) ck.st((w / TSUB) * CK + s - CK0, a[s]);
+    }
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
       T c[4], o[8];
@@ -302,6 +314,28 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
       fwd<T, LM>(a, c, o);
 #pragma unroll
       for (int s = 0; s < 8; ++s) a[s] = o[s];
+    }
+  };
+  if constexpr (TT::FWD_PF) {
+    // software-pipelined: window w + 1's loads are in flight while window w
+    // is computed (one resident wave per SIMD has no other wave to overlap)
+    T x0[TW], y0[TW], z0[TW], x1[TW], y1[TW], z1[TW];
+    ldwin(0, x0, y0, z0);
+#pragma unroll 1
+    for (int w = 0; w < nsub; w += 2) {
+      if (w + 1 < nsub) ldwin(w + 1, x1, y1, z1);
+      stepwin(w, x0, y0, z0);
+      if (w + 1 < nsub) {
+        if (w + 2 < nsub) ldwin(w + 2, x0, y0, z0);
+        stepwin(w + 1, x1, y1, z1);
+      }
+    }
+  } else {
+#pragma unroll 1
+    for (int w = 0; w < nsub; ++w) {
+      T ls[TW], lp[TW], la[TW];
+      ldwin(w, ls, lp, la);
+      stepwin(w, ls, lp, la);
     }
   }
 
@@ -314,9 +348,8 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
   // their a priori is 0, turbo_decoder.py:406, 428)
 #pragma unroll
   for (int j = 2; j >= 0; --j) {
-    const int k = K + j;
-    const T ls = (MODE == TM_DEC2) ? LS2T.ld(j) : LS.ld(k);
-    const T lp = LP.ld(k);
+    const T ls = (MODE == TM_DEC2) ? LS2T.ld(j) : LS1T.ld(j);
+    const T lp = LPT.ld(j);
     T c[4];
     gam(ls, lp, (T)0, c);
     bonly<T, LM>(b, c);

@@ -242,9 +242,40 @@ int launch_bf(hipStream_t s, int B, int n_sym, int Nd, int bps, int num_tx, int 
 
 // turbo modes
 enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3, TM_FINAL = 4 };  // TM_DECODE: full decode (iterations + decisions)
-// turbo geometry: rows of one (r, group) block = 4K+12:
-//   [0,K+3) LS (sys + sys1 tail) | [K+3,2K+6) LP1 | [2K+6,3K+9) LP2 | [3K+9,3K+12) LS2T | [3K+12,4K+12) LE
+// turbo geometry: rows of one (r, group) block = 4K+12: LS (sys + sys1 tail,
+// K + 3), LP1 (K + 3), LP2 (K + 3), LS2T (decoder 2's sys tail, 3), LE (K);
+// placement: trow_* below
 __host__ __device__ inline int64_t turbo_rows(int K) { return 4LL * K + 12; }
+// Row of each decoder input / the extrinsic within a block (LTE_TURBO_ILV):
+//  3: all four rows of step k side by side -- [4k] LS, [4k+1] LE, [4k+2] LP1,
+//    [4k+3] LP2 -- then the LS, LP1, LP2 tails and LS2T (3 each);
+//  2 (default): decoder 1's three rows of step k side by side -- [3k] LS(k),
+//    [3k+1] LE(k), [3k+2] LP1(k) for k < K -- so its step reads one contiguous
+//    1.5 KB span (f64) and decoder 2's step at pi(k) a 1 KB LS / LE span;
+//    then LS tail (3), LP1 tail (3), LP2 (K + 3), LS2T (3);
+//  1: [2k] LS(k), [2k+1] LE(k); LS tail, LP1, LP2, LS2T;
+//  0: sequential LS, LP1, LP2, LS2T, LE.
+// A/B on MI355X (f64 decoder, 65 536 frames): see DESIGN.md §5.
+#ifndef LTE_TURBO_ILV
+#define LTE_TURBO_ILV 1
+#endif
+__host__ __device__ inline int64_t trow_ls(int K, int k) {   // k in [0, K + 3)
+  if (LTE_TURBO_ILV == 3) return k < K ? 4LL * k : 4LL * K + (k - K);
+  if (LTE_TURBO_ILV == 2) return k < K ? 3LL * k : 3LL * K + (k - K);
+  if (LTE_TURBO_ILV == 1) return k < K ? 2LL * k : (int64_t)K + k;
+  return k;
+}
+__host__ __device__ inline int64_t trow_le(int K, int k) {   // k in [0, K)
+  return LTE_TURBO_ILV == 3 ? 4LL * k + 1 : LTE_TURBO_ILV == 2 ? 3LL * k + 1 : LTE_TURBO_ILV == 1 ? 2LL * k + 1
+                                                                                           : 3LL * K + 12 + k;
+}
+__host__ __device__ inline int64_t trow_lp(int K, int dec, int k) {   // dec 1 / 2, k in [0, K + 3)
+  if (LTE_TURBO_ILV == 3) return k < K ? 4LL * k + 1 + dec : 4LL * K + 3 * dec + (k - K);
+  if (LTE_TURBO_ILV == 2) return dec == 1 ? (k < K ? 3LL * k + 2 : 3LL * K + 3 + (k - K)) : 3LL * K + 6 + k;
+  if (LTE_TURBO_ILV == 1) return (dec == 1 ? 2LL * K + 3 : 3LL * K + 6) + k;
+  return (dec == 1 ? (int64_t)K + 3 : 2LL * K + 6) + k;
+}
+__host__ __device__ inline int64_t trow_ls2t(int K, int j) { return (LTE_TURBO_ILV ? 4LL * K + 9 : 3LL * K + 9) + j; }
 __host__ __device__ inline int turbo_nwin(int K) { return K / 8 + 1; }  // checkpoint windows (>= 8 steps each)
 // alpha checkpoint rows per window: f32 states 1..7 (state 0 is 0 after
 // normalisation); f64 all 8 states (unnormalised, as the reference)

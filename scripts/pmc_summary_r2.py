@@ -90,7 +90,9 @@ def main(prec='f64', frames=8192, src=os.path.join(ROOT, 'gpurun_out')):
     tk_name = 'k_turbo64' if prec == 'f64' else 'k_turbo'
     t = out[tk_name]
     esz = 8 if prec == 'f64' else 4
-    ckrows = (8 if prec == 'f64' else 7) / 16.0
+    # checkpoint rows stored (and loaded) per step: 8 (f64) / 7 (f32) states per
+    # super-window of 24 (f64, LTE_TURBO64_SUB = 3) / 16 (f32) steps
+    ckrows = (8 / 24.0) if prec == 'f64' else (7 / 16.0)
     model = STEPS * PASSES * esz * (6 + 1 + 2 * ckrows)
     with open(os.path.join(ROOT, 'profiles', f'pmc_turbo_traffic_{prec}.json'), 'w') as f:
         json.dump({'kernel': tk_name, 'frames_per_launch': frames, 'command': meta['command'],

@@ -509,7 +509,17 @@ __device__ __forceinline__ void turbo_body(const TurboJobs& jobs, int iters, int
   half_pass<T, TM_FINAL, LM>(base, ck, lane, K, jb.f1, jb.f2, iters == 0, bo);
 }
 
-__global__ __launch_bounds__(256) void k_turbo(TurboJobs jobs, int iters, int mode) {
+// f32 fast mode: 134 VGPRs = 3 waves per SIMD; LTE_TURBO32_WAVES = 2 / 1 caps
+// the resident waves with reserved AGPRs (A/B knob, as k_turbo64)
+#ifndef LTE_TURBO32_WAVES
+#define LTE_TURBO32_WAVES 3
+#endif
+__global__ __launch_bounds__(256, LTE_TURBO32_WAVES == 3 ? 2 : 1) void k_turbo(TurboJobs jobs, int iters, int mode) {
+#if LTE_TURBO32_WAVES == 2
+  asm volatile("" ::: "a47");
+#elif LTE_TURBO32_WAVES == 1
+  asm volatile("" ::: "a127");
+#endif
   turbo_body<float>(jobs, iters, mode);
 }
 

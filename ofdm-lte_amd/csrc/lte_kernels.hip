@@ -342,6 +342,9 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
 #ifndef TXF_WAVES
 #define TXF_WAVES 1
 #endif
+#ifndef TXF_STAGE   // 1: the frame's coded streams staged in LDS; 0: bit gathers through L1 / L2
+#define TXF_STAGE 1
+#endif
 template <class R, int BPS, int NC = 0>
 __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32_t* __restrict__ enc, int enc_words,
                                                           const int32_t* __restrict__ tx_map, int B,
@@ -354,11 +357,15 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
   const int b = blockIdx.x * spw + slot;
   const bool active = slot < spw && b < B;
   V* buf = sm + slot * N;
+#if TXF_STAGE
   uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
   if (active) {
     const uint32_t* fe = enc + (size_t)b * enc_words;
     for (int i = tid0; i < enc_words; i += T) es[i] = fe[i];
   }
+#else
+  const uint32_t* es = enc + (size_t)(active ? b : 0) * enc_words;
+#endif
   const R sc = tx_scale<R>(N);
   constexpr int QM = 4;   // Nd < N/2 = QM * T for every LTE profile
   for (int l = 0; l < g.n_sym; ++l) {
@@ -410,7 +417,7 @@ int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_w
                     cx<R>* cap_syms, const TxChannelT<R>& ch) {
   const int spw = WG / (g.N >> 3);
   if (!txch_supported(g, ch.n_paths, ch.max_delay) || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
-  const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + (size_t)spw * enc_words * sizeof(uint32_t);
+  const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + (TXF_STAGE ? (size_t)spw * enc_words * sizeof(uint32_t) : 0);
   if (shm > 65536) return (int)hipErrorInvalidValue;
   const int blocks = (B + spw - 1) / spw;
 #define LTE_TXF(BPS_, NC_)                                                                                      \

@@ -157,12 +157,42 @@ def roofline(prec, tim, steps, F, el, value, world):
                              'busy_frac': round(sq['valu_wave_instr_per_frame'] * Fp * sq['issue_cycles_per_instr']
                                                 / (avg_s * 2.4e9 * 1024), 4)} if sq and t_n else None),
             'turbo_share_of_step': round(t_ms / (el * 1e3) if el > 0 else 0, 3),
+            'front_end': front_end(prec, tim, F),
             'kernel_ms_per_step': {k: round(v[0] / steps, 3) for k, v in tim.items() if v[1]},
             # SURVEY §8(d)'s whole-chain view: compulsory stage-boundary bytes per subframe
             'pipeline_hbm': {'bytes_per_subframe': B_SF_F32 * esz // 4,
                              'achieved_GBs': round(B_SF_F32 * esz / 4 * value / world / 1e9, 2),
                              'frac': round(B_SF_F32 * esz / 4 * value / world / 1e9 / HBM_PEAK_GBS, 5)}}
     return roof
+
+
+# front-end stages (bench timers) -> their kernels in the committed PMC summary
+FE_KERNELS = {'payload': ['k_payload'], 'encode': ['k_encode', 'k_encode2'], 'ofdm_tx': ['k_ofdm_txf'],
+              'rx_data': ['k_rx_frame'], 'dematch': ['k_dematch_zn'], 'crc_count': ['k_crc_count']}
+
+
+def front_end(prec, tim, F):
+    """Per front-end stage: its HIP-event time per launch, the HBM bytes per
+    frame its kernels move (profiles/r2_pmc_<prec>.json, rocprofv3 FETCH_SIZE /
+    WRITE_SIZE, gfx950-corrected) and the resulting rate against the 8 TB/s
+    peak, plus the VALU / LDS shares of active issue from the same PMC passes
+    (what bounds the FFT / noise kernels, which are not HBM-bound)."""
+    pmc = load_profile(f'r2_pmc_{prec}.json')
+    if not pmc:
+        return None
+    ks = pmc['kernels']
+    out = {}
+    for stage, names in FE_KERNELS.items():
+        t_ms, n = tim.get(stage, (0.0, 0))
+        if not n or not all(k in ks for k in names):
+            continue
+        b = sum(ks[k]['hbm_bytes_per_frame'] for k in names)
+        gbs = b * F / (t_ms / n * 1e-3) / 1e9
+        share = ks[names[0]].get('share_of_active_issue', {})
+        out[stage] = {'kernels': names, 'ms': round(t_ms / n, 3), 'hbm_bytes_per_frame': round(b),
+                      'achieved_GBs': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 3),
+                      'valu_share': share.get('valu'), 'lds_share': share.get('lds')}
+    return out
 
 
 def dry_run_counts(ids, S):

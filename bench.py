@@ -13,7 +13,7 @@ only collectives are the SUM of the BER counters and the MAX of the step time.
 (torch.distributed.run on 127.0.0.1, before anything touches the GPU) and
 exits with their status; under a launcher WORLD_SIZE must equal --gpus.
 
-usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--precision f64|f32]
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--precision f64|f32] [--velocity KMH]
 """
 import argparse
 import json
@@ -112,50 +112,93 @@ def _free_port():
 
 
 def launch_ranks(args, argv):
-    """--gpus N without a launcher: run N ranks under torch.distributed.run as a
-    child process (this process never touches the GPU) and return its status."""
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
-           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + argv
+    """--gpus N without a launcher: time the CPU baseline here (this process
+    never touches the GPU), then run N ranks under torch.distributed.run as a
+    child process and return its status.  Rank 0 reads the baseline from
+    LTE_BENCH_CPU_JSON, so the N > 1 line carries it too."""
     env = dict(os.environ)
     env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    if not args.no_cpu:
+        env['LTE_BENCH_CPU_JSON'] = json.dumps(cpu_baseline(args.cpu_seconds))
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + argv
     return subprocess.call(cmd, env=env)
 
 
-def roofline(prec, tim, steps, F, el, value, world):
-    """Dominant kernel (the turbo decoder) against its roofline, from the HIP
-    event times of the timed launches: the VALU view (SURVEY §8(d)'s turbo
-    work: sum(K+3) x 17 passes x 100 add/max ops per subframe, against the
-    non-packed vector peak of the decode's arithmetic type) as the headline,
-    the HBM view (algorithmic bytes: the rate-dematched input LLRs and the
-    decoded bits) beside it with the measured traffic / algorithmic ratio."""
+def decoder_row_bytes(K, esz, iters):
+    """Compulsory HBM bytes of one code block through the exact lane-per-code-
+    block decoder (k_turbo64 / k_turbo): a step of the unnormalised
+    recursion needs the three rows (Ls, Lp, La) of its step in the forward
+    sweep and again in the backward sweep (beta at k depends on every input
+    after k, the LLR on alpha and beta; a code block's working set cannot stay
+    on chip), plus the extrinsic store: 7 rows of esz bytes per step and pass.
+    The first pass has no a priori (5 rows), the final a-posteriori pass stores
+    packed decisions instead of an extrinsic (6 rows + K/8 B).  The two tail
+    rows (Ls, Lp) of the 3 termination steps are read once per pass.  The alpha
+    checkpoint rows are NOT counted: they are this implementation's choice (its
+    measured traffic shows them)."""
+    passes = 2 * iters + 1
+    rows = 5 + (passes - 2) * 7 + 6 if iters >= 1 else 6
+    return K * rows * esz + 3 * 2 * passes * esz + K / 8
+
+
+def roofline(prec, tim, steps, F, el, value, world, iters=8):
+    """Dominant kernel (the turbo decoder, ~87 % of a step) against the roofline
+    that bounds it.  The exact decoder streams its rows: `achieved` = the
+    compulsory row bytes of the exact recursion (decoder_row_bytes) per launch
+    / the kernel's mean launch time (HIP events on the plan's stream; the max
+    over ranks), against the 8 TB/s HBM peak; `traffic` = the PMC-measured HBM
+    bytes per launch (profiles/pmc_turbo_traffic_<prec>.json, gfx950-corrected),
+    with `shape_ceiling` = the measured streaming rate of the same access shape
+    without the arithmetic (profiles/r3_turbo_shape_microbench.json).  Beside
+    it: SURVEY §8(d)'s stage-boundary bytes (input LLRs + decoded bits) and its
+    VALU view (sum(K+3) x 17 passes x 100 add/max ops per subframe against the
+    non-packed vector peak), and the SQ-counted VALU issue occupancy.  `bound`
+    is the larger of the measured HBM and VALU occupancies."""
     from lte_phy.channel_coding import segmentation_sizes
     t_ms, t_n = tim.get('turbo', (0.0, 0))
     avg_s = t_ms / max(t_n, 1) * 1e-3
     Fp = ((F + 63) // 64) * 64            # frames padded to whole 64-frame decoder groups
     esz = 8 if prec == 'f64' else 4
-    alg_bytes = sum(Fp * ((3 * K + 12) * esz + K / 8) for K in segmentation_sizes(TB + 24))
+    Ks = segmentation_sizes(TB + 24)
+    row_bytes = sum(Fp * decoder_row_bytes(K, esz, iters) for K in Ks)
+    stage_bytes = sum(Fp * ((3 * K + 12) * esz + K / 8) for K in Ks)
     peak = VALU_PEAK_OPS[prec]
     ops = TURBO_OPS_SF * F
     achieved_T = ops / avg_s / 1e12 if t_n else 0.0
     traffic = load_profile(f'pmc_turbo_traffic_{prec}.json')
     sq = load_profile(f'pmc_turbo_sq_{prec}.json')
-    hbm_alg = alg_bytes / avg_s / 1e9 if t_n else 0.0
+    shape = load_profile('r3_turbo_shape_microbench.json')
+    gbs = row_bytes / avg_s / 1e9 if t_n else 0.0
     tr = traffic['bytes_per_frame'] * Fp if traffic else None
-    roof = {'bound': 'valu', 'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo',
-            'achieved': round(achieved_T, 3), 'peak': round(peak / 1e12, 2), 'unit': 'Top/s',
-            'frac': round(achieved_T * 1e12 / peak, 4),
-            'ops_per_subframe': TURBO_OPS_SF, 'frames_per_launch': F,
+    tr_gbs = tr / avg_s / 1e9 if tr and t_n else None
+    busy = (sq['valu_wave_instr_per_frame'] * Fp * sq['issue_cycles_per_instr'] / (avg_s * 2.4e9 * 1024)
+            if sq and t_n else None)
+    hbm_occ = (tr_gbs if tr_gbs else gbs) / HBM_PEAK_GBS
+    ceil = shape.get(f'ceiling_GBs_{prec}') if shape else None
+    roof = {'bound': 'hbm' if busy is None or hbm_occ >= busy else 'valu',
+            'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo',
+            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4),
             # HBM bytes per launch from the committed PMC passes (per-frame bytes,
             # gfx950-corrected, scaled to this launch's frames)
             'traffic': round(tr) if tr else None,
-            'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': t_n,
-            'hbm': {'alg_bytes_per_launch': int(alg_bytes), 'achieved_GBs': round(hbm_alg, 2),
-                    'peak_GBs': HBM_PEAK_GBS, 'frac': round(hbm_alg / HBM_PEAK_GBS, 5),
-                    'traffic_over_alg': round(tr / alg_bytes, 1) if tr else None,
-                    'traffic_GBs': round(tr / avg_s / 1e9, 1) if tr and t_n else None},
-            'issued_valu': ({'wave_instr_per_frame': sq['valu_wave_instr_per_frame'],
-                             'busy_frac': round(sq['valu_wave_instr_per_frame'] * Fp * sq['issue_cycles_per_instr']
-                                                / (avg_s * 2.4e9 * 1024), 4)} if sq and t_n else None),
+            'alg_bytes_per_launch': int(row_bytes),
+            'alg_bytes': 'exact-recursion row stream: per code-block step 7 rows (Ls, Lp, La forward and '
+                         'backward + extrinsic store) x esz B x 17 passes (first pass 5, final 6 + K/8 B decisions)',
+            'traffic_over_alg': round(tr / row_bytes, 3) if tr else None,
+            'traffic_GBs': round(tr_gbs, 1) if tr_gbs else None,
+            'traffic_frac': round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs else None,
+            'shape_ceiling': ({'GBs': ceil, 'traffic_frac_of_ceiling': round(tr_gbs / ceil, 4) if tr_gbs else None,
+                               'source': 'profiles/r3_turbo_shape_microbench.json'} if ceil else None),
+            'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': t_n, 'frames_per_launch': F,
+            'stage_bytes': {'bytes_per_launch': int(stage_bytes), 'achieved_GBs': round(stage_bytes / avg_s / 1e9, 2)
+                            if t_n else 0.0, 'frac': round(stage_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if t_n else 0.0,
+                            'what': 'SURVEY §8(d) stage boundary: rate-dematched input LLRs + decoded bits'},
+            'valu': {'achieved_Tops': round(achieved_T, 3), 'peak_Tops': round(peak / 1e12, 2),
+                     'frac': round(achieved_T * 1e12 / peak, 4), 'ops_per_subframe': TURBO_OPS_SF,
+                     'issued_busy_frac': round(busy, 4) if busy is not None else None,
+                     'wave_instr_per_frame': sq['valu_wave_instr_per_frame'] if sq else None},
             'turbo_share_of_step': round(t_ms / (el * 1e3) if el > 0 else 0, 3),
             'front_end': front_end(prec, tim, F),
             'kernel_ms_per_step': {k: round(v[0] / steps, 3) for k, v in tim.items() if v[1]},
@@ -164,6 +207,17 @@ def roofline(prec, tim, steps, F, el, value, world):
                              'achieved_GBs': round(B_SF_F32 * esz / 4 * value / world / 1e9, 2),
                              'frac': round(B_SF_F32 * esz / 4 * value / world / 1e9 / HBM_PEAK_GBS, 5)}}
     return roof
+
+
+def merge_timers(all_tim):
+    """Per stage, the rank whose mean launch time is the largest (the roofline
+    prices the slowest rank's kernels, like the step time)."""
+    out = {}
+    for tim in all_tim:
+        for k, (ms, n) in (tim or {}).items():
+            if n and (k not in out or ms / n > out[k][0] / out[k][1]):
+                out[k] = (ms, n)
+    return out
 
 
 # front-end stages (bench timers) -> their kernels in the committed PMC summary
@@ -216,6 +270,9 @@ def main():
     ap.add_argument('--frames', type=int, default=65536, help='subframes per step per GPU')
     ap.add_argument('--iters', type=int, default=8)
     ap.add_argument('--precision', choices=('f64', 'f32'), default='f64')
+    ap.add_argument('--velocity', type=float, default=0.0,
+                    help='UE speed in km/h (fD = v fc / c at 2 GHz); 0 = the OFDMSimulator default (static taps), '
+                         '3 = the GUI default (Jakes fading over the subframe): a secondary line, not the headline')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--dry-run', action='store_true', help='no GPU: launcher / sharding / reductions only (gloo)')
@@ -231,9 +288,13 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     # the CPU baseline runs first, in spawned worker processes, before anything
-    # initialises the GPU (rank 0 of a 1-GPU run only)
-    cpu = (cpu_baseline(args.cpu_seconds) if world == 1 and rank == 0 and not args.no_cpu and not args.dry_run
-           else None)
+    # initialises the GPU: on rank 0 (under an external launcher the other ranks
+    # wait for it in the rendezvous), or in the self-launching parent, which
+    # hands it over in LTE_BENCH_CPU_JSON
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = (json.loads(os.environ['LTE_BENCH_CPU_JSON']) if os.environ.get('LTE_BENCH_CPU_JSON')
+               else cpu_baseline(args.cpu_seconds))
     import torch
     dist = None
     # LTE_BENCH_BACKEND=gloo: rehearse the N>1 path with several ranks sharing
@@ -272,7 +333,7 @@ def main():
         dev_id = f"{getattr(props, 'pci_bus_id', '')}:{getattr(props, 'uuid', local)}"
         sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=20.0, modulation='64-QAM'),
                                     channel_type='rayleigh_mp', itu_profile='Pedestrian_A',
-                                    precision=args.precision)
+                                    velocity_kmh=args.velocity, precision=args.precision)
         plan = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=F, iters=args.iters)
         prec = plan.precision
 
@@ -304,9 +365,18 @@ def main():
     if plan is not None:
         plan.timing(False)
         tim = plan.timing_read()
+    elif args.dry_run:
+        # --dry-run: synthetic per-rank kernel timers (exercise the roofline
+        # gather; the line is marked dry_run)
+        tim = {'turbo': (0.8 * el * 1e3 * (1 + 0.01 * rank), args.steps)}
 
     el = D.allreduce_max(el, dist)
     counts = D.allreduce_counts(counts, dist)
+    # kernel timers of every rank: the roofline prices the slowest one
+    if dist is not None:
+        all_tim = [None] * world
+        dist.all_gather_object(all_tim, tim)
+        tim = merge_timers(all_tim)
     # distinct devices that took part (not the rank count)
     devs = [dev_id]
     if dist is not None:
@@ -318,15 +388,18 @@ def main():
     value = total / el
     ber = (counts[:, 0] / np.maximum(counts[:, 1], 1)).tolist()
     bler = (counts[:, 2] / np.maximum(counts[:, 3], 1)).tolist()
+    workload = ('config 2: SISO 20 MHz (N=2048) 64-QAM, Rayleigh ITU Pedestrian-A, '
+                'turbo max-log-MAP 8 it., TB 27760 (5 CBs, 14 OFDM symbols), SNR 0:2:30 dB')
+    if args.velocity:
+        workload += f' -- SECONDARY line: UE at {args.velocity:g} km/h (Jakes fading over the subframe)'
     out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'subframes/s', 'n_gpus': n_dev,
            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el * 1e3 / args.steps, 3),
            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': prec,
            'data': 'synthetic (Philox4x32-10 payload bits, Jakes phases and AWGN generated on the GPU)',
-           'config': {'workload': 'config 2: SISO 20 MHz (N=2048) 64-QAM, Rayleigh ITU Pedestrian-A, '
-                                  'turbo max-log-MAP 8 it., TB 27760 (5 CBs, 14 OFDM symbols), SNR 0:2:30 dB',
+           'config': {'workload': workload, 'velocity_kmh': args.velocity,
                       'frames_per_step_per_gpu': F, 'global_batch': F * world, 'parallelism': f'dp{world}',
                       'ranks': world, 'snr_db': SNRS.tolist()},
-           'roofline': roofline(prec, tim, args.steps, F, el, value, world) if plan is not None else None,
+           'roofline': roofline(prec, tim, args.steps, F, el, value, world, args.iters) if tim else None,
            'ber': [float(f'{b:.4e}') for b in ber], 'bler': [float(f'{b:.4e}') for b in bler]}
     if args.dry_run:
         out['dry_run'] = True

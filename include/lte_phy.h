@@ -159,8 +159,9 @@ typedef struct {
   const double *link_h; int64_t link_h_stride;
   /* multi-antenna capture: per link [n_frames][num_rx][num_tx][4] = mean|x_tx|^2,
    * mean|y_link|^2, Re and Im of mean(y_link conj(x_tx)) -- the statistics
-   * transmit_mimo reports its channel_matrix from (core/ofdm_core.py:505-516) */
-  float *cap_link_stats;
+   * transmit_mimo reports its channel_matrix from (core/ofdm_core.py:505-516);
+   * real, the plan's arithmetic type */
+  void *cap_link_stats;
   /* beamforming capture: per frame PMI (CSIFeedback) and beamforming gain (dB);
    * cap_H holds H [n_frames][num_rx][num_tx] for this chain */
   int32_t *cap_pmi;
@@ -250,6 +251,14 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
                           uint64_t seed, const float *x, const double *phases, const double *link_noise,
                           const double *link_h, const double *noise, float *y, float *link_stats,
                           float *noise_power);
+/* the same in float64 (complex128 streams; fD != 0 evaluates the Jakes sum of
+ * rayleighchannel.py:20-42 exactly per sample instead of the float32 path's
+ * per-symbol expansion) */
+int lte_channel_mimo_host64(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,
+                            const int32_t *delays, const double *gains, double fD, double fs, double snr_db,
+                            uint64_t seed, const double *x, const double *phases, const double *link_noise,
+                            const double *link_h, const double *noise, double *y, double *link_stats,
+                            double *noise_power);
 /* TM4 detection: MIMODetector.detect (core/mimo_detector.py:55-369) per
  * subcarrier, float64 on the device.  y [num_rx][n_sc] complex128, H
  * [num_rx][num_tx][n_sc] complex128, W [num_tx][rank] complex128 (row-major),

@@ -350,12 +350,18 @@ template <class R>
 struct ChainBufs {
   DBuf<cx<R>> x, y, coef, H, capbuf, captx, xh;
   DBuf<R> gains, phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
+  // multi-antenna chains: received data SCs [B][n_sym][num_rx][n_dsc] (H holds
+  // the estimates [B][num_rx][n_est][num_tx][n_dsc]), transmit_mimo's link
+  // power partials / noise sigmas, link injections
+  DBuf<cx<R>> Ym;
+  DBuf<R> link_part, link_sigma, inj_lz, inj_lh;
   std::vector<DBuf<R>> blk, ckpt;
   DBuf<R*> blk_ptrs;
   void release() {
     x.release(); y.release(); coef.release(); H.release(); capbuf.release(); captx.release(); xh.release();
     gains.release(); phases.release(); pow_part.release(); pstats.release(); npow.release(); llr.release();
     snr_lin.release(); inj_ph.release(); inj_z.release();
+    Ym.release(); link_part.release(); link_sigma.release(); inj_lz.release(); inj_lh.release();
     for (auto& b : blk) b.release();
     for (auto& b : ckpt) b.release();
     blk_ptrs.release();
@@ -410,14 +416,14 @@ struct lte_plan {
   TableSet tabs;
   Grid grid;
   hipStream_t stream = nullptr;
-  int f64 = 0;                       // signal chain + decoder in float64 (SISO / SIMO chains)
+  int f64 = 0;                       // signal chain + decoder in float64 (every chain but beamforming)
   int n_layers = 1;                  // rx_map layers (> 1: rate-matching repetition, E > N_cb)
   std::vector<CbInfo> cbs;
   // device
   DBuf<CbInfo> cbi;
   DBuf<int32_t> tx_map, rx_map, delays;
   DBuf<uint32_t> pw, enc, enc_cw, inj_bits;
-  ChainBufs<float> c32;              // f32 plans (and every multi-antenna chain)
+  ChainBufs<float> c32;              // f32 plans (and the beamforming chain)
   ChainBufs<double> c64;             // f64 plans
   DBuf<uint32_t> frame_err, frame_crc;
   DBuf<int32_t> snr_idx;
@@ -438,9 +444,10 @@ struct lte_plan {
   int res = 0;                       // QAM symbols per OFDM symbol (= Nd for SISO / SIMO)
   MimoGrid mg{};
   DBuf<int32_t> m_np, m_ppos, m_pseg;
-  DBuf<float2> m_pval, Ym, Hm;
-  DBuf<float> m_pig, link_part, link_sigma, inj_lz, inj_lh;
-  DBuf<double> m_W;
+  DBuf<float2> m_pval;
+  DBuf<double2> m_pval64;
+  DBuf<float> m_pig, inj_lh;
+  DBuf<double> m_pig64, m_W;
   // timing
   bool timing = false;
   double kms[KN_COUNT] = {0};
@@ -612,18 +619,23 @@ int lte_channel_host64(int64_t L, int num_rx, int channel, int n_paths, const in
                               noise_power);
 }
 
-int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,
-                          const int32_t* delays, const double* gains, double fD, double fs, double snr_db,
-                          uint64_t seed, const float* x, const double* phases, const double* link_noise,
-                          const double* link_h, const double* noise, float* y, float* link_stats,
-                          float* noise_power) {
+}  // extern "C"
+
+// Multi-antenna channel on arbitrary streams in precision R (lte_channel_mimo_host / _host64).
+template <class R>
+static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,
+                             const int32_t* delays, const double* gains, double fD, double fs, double snr_db,
+                             uint64_t seed, const R* x, const double* phases, const double* link_noise,
+                             const double* link_h, const double* noise, R* y, R* link_stats, R* noise_power) {
+  using V = cx<R>;
   if (L < 1 || L > (1LL << 28) || num_tx < 1 || num_tx > 8 || num_rx < 1 || num_rx > 16 || !x || !y)
     return fail(LTE_EINVAL, "bad channel arguments");
   if (mode != 0 && mode != 1) return fail(LTE_EINVAL, "mode must be 0 (transmit_mimo) or 1 (spatial)");
   const bool ray = channel == LTE_CH_RAYLEIGH;
   if (!ray && channel != LTE_CH_AWGN) return fail(LTE_EINVAL, "Tipo de canal desconocido");
   if (ray && (n_paths < 1 || n_paths > LTE_MAX_PATHS || !delays || !gains)) return fail(LTE_EINVAL, "bad paths");
-  // an arbitrary stream is cut into 1024-sample chunks for the fD != 0 expansion
+  // an arbitrary stream is cut into 1024-sample chunks for the f32 fD != 0
+  // expansion; f64 evaluates the Jakes sum exactly per sample
   const int chunk = 1024;
   Grid g{};
   g.N = chunk;
@@ -633,36 +645,38 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
   m.mode = mode == 0 ? MIMO_SFBC : MIMO_SPATIAL;
   m.num_tx = num_tx;
   m.num_rx = num_rx;
-  m.n_cs = (ray && fD != 0.0) ? (int)((L + chunk - 1) / chunk) : 1;
+  m.exact_jakes = sizeof(R) == 8 && ray && fD != 0.0;
+  for (int k = 0; k < 16; ++k) m.jw[k] = 6.283185307179586 * fD * std::cos(6.283185307179586 * (k + 1) / 16.0);
+  m.n_cs = (ray && fD != 0.0 && !m.exact_jakes) ? (int)((L + chunk - 1) / chunk) : 1;
   const int np = ray ? n_paths : 1;
   // partial-sum slots: 256-sample blocks (link stats) or OFDM-symbol blocks (channel), whichever is more
   const int nblk = std::max((int)((L + 255) / 256), mimo_channel_nblk((int)L, g.N + g.cp));
   const size_t links = (size_t)num_rx * num_tx;
   const bool link_noise_on = mode == 0 && ray;
-  DBuf<float2> dx, dy, dcoef, dout;
-  DBuf<float> dgain, dph, dlz, dlh, dz, dpp, dlp, dls, dsl, dnp, dstp, dst;
+  DBuf<V> dx, dy, dcoef, dout;
+  DBuf<R> dgain, dph, dlz, dlh, dz, dpp, dlp, dls, dsl, dnp, dstp, dst, dphs;
   DBuf<int32_t> ddel;
   DBuf<uint64_t> dfid;
   auto cleanup = [&]() {
     dx.release(); dy.release(); dcoef.release(); dout.release(); dgain.release(); dph.release(); dlz.release();
     dlh.release(); dz.release(); dpp.release(); dlp.release(); dls.release(); dsl.release(); dnp.release();
-    dstp.release(); dst.release(); ddel.release(); dfid.release();
+    dstp.release(); dst.release(); dphs.release(); ddel.release(); dfid.release();
   };
   if (dx.alloc((size_t)num_tx * L) || dy.alloc((size_t)num_rx * L) || dout.alloc((size_t)num_rx * L) ||
       dcoef.alloc(links * np * m.n_cs * 3) || dpp.alloc((size_t)num_rx * nblk) || dsl.alloc(1) ||
-      dnp.alloc(num_rx) || dfid.alloc(1) ||
+      dnp.alloc(num_rx) || dfid.alloc(1) || (m.exact_jakes && dphs.alloc(links * np * 16)) ||
       (link_noise_on && (dlp.alloc(links * nblk) || dls.alloc(links)))) {
     cleanup();
     return fail(LTE_ENOMEM, "channel buffers");
   }
-  auto up = [&](DBuf<float>& d, const double* src, size_t n) {
-    std::vector<float> h(src, src + n);
+  auto up = [&](DBuf<R>& d, const double* src, size_t n) {
+    std::vector<R> h(src, src + n);
     return upload(d, h) == 0;
   };
-  const float sl = (float)std::pow(10.0, snr_db / 10.0);
+  const R sl = (R)std::pow(10.0, snr_db / 10.0);
   const uint64_t fid0 = 0;
-  bool ok = hipMemcpy(dx.p, x, (size_t)num_tx * L * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess &&
-            hipMemcpy(dsl.p, &sl, 4, hipMemcpyHostToDevice) == hipSuccess &&
+  bool ok = hipMemcpy(dx.p, x, (size_t)num_tx * L * sizeof(V), hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dsl.p, &sl, sizeof(R), hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(dfid.p, &fid0, 8, hipMemcpyHostToDevice) == hipSuccess;
   if (ok && ray) {
     std::vector<int32_t> dl(delays, delays + n_paths);
@@ -672,33 +686,53 @@ int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int chann
   if (ok && link_noise_on && link_noise) ok = up(dlz, link_noise, links * 2 * L);
   if (ok && !ray && mode == 1 && link_h) ok = up(dlh, link_h, links * 2);
   if (ok && noise) ok = up(dz, noise, (size_t)num_rx * 2 * L);
-  ok = ok && launch_fading_mimo(nullptr, g, m, 1, ray ? 1 : 0, n_paths, dgain.p, fD, fs, dfid.p, seed,
-                                (ray && phases) ? dph.p : nullptr, 0, (!ray && mode == 1 && link_h) ? dlh.p : nullptr,
-                                0, dcoef.p) == 0;
-  ok = ok && launch_channel_mimo(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dx.p, dy.p,
-                                 link_noise_on ? 1 : 0, dfid.p, seed, (link_noise_on && link_noise) ? dlz.p : nullptr,
-                                 0, dlp.p, dls.p, dpp.p, nblk) == 0;
-  ok = ok && launch_npow_mimo(nullptr, 1, num_rx, dpp.p, mimo_channel_nblk((int)L, g.N + g.cp), (int)L, dsl.p,
-                              mode == 0 ? 1.0f / num_tx : 1.0f,
-                              dnp.p) == 0;
+  ok = ok && launch_fading_mimo<R>(nullptr, g, m, 1, ray ? 1 : 0, n_paths, dgain.p, fD, fs, dfid.p, seed,
+                                   (ray && phases) ? dph.p : nullptr, 0,
+                                   (!ray && mode == 1 && link_h) ? dlh.p : nullptr, 0, dcoef.p, dphs.p) == 0;
+  const R* lz = (link_noise_on && link_noise) ? dlz.p : nullptr;
+  ok = ok && launch_channel_mimo<R>(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dphs.p, dgain.p, fs, dx.p,
+                                    dy.p, link_noise_on ? 1 : 0, dfid.p, seed, lz, 0, dlp.p, dls.p, dpp.p, nblk) == 0;
+  ok = ok && launch_npow_mimo<R>(nullptr, 1, num_rx, dpp.p, mimo_channel_nblk((int)L, g.N + g.cp), (int)L, dsl.p,
+                                 mode == 0 ? (double)num_tx : 1.0, dnp.p) == 0;
   if (ok) {
-    hipLaunchKernelGGL(k_cap_rx<float>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
+    hipLaunchKernelGGL(k_cap_rx<R>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
                        dy.p, (int64_t)L, (int64_t)num_rx * L, dnp.p, dfid.p, seed, noise ? dz.p : nullptr, 0,
                        dout.p);
     ok = hipGetLastError() == hipSuccess;
   }
   if (ok && link_stats) {
     ok = dstp.alloc(links * 4 * nblk) == 0 && dst.alloc(links * 4) == 0 &&
-         launch_link_stats(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dx.p, dstp.p, nblk, dst.p) == 0;
+         launch_link_stats<R>(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dphs.p, dgain.p, fs, dx.p,
+                              link_noise_on ? dls.p : nullptr, dfid.p, seed, lz, 0, dstp.p, nblk, dst.p) == 0;
   }
   ok = ok && hipDeviceSynchronize() == hipSuccess &&
-       hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(float2), hipMemcpyDeviceToHost) == hipSuccess &&
-       (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess) &&
-       (!link_stats || hipMemcpy(link_stats, dst.p, links * 4 * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess);
+       hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(V), hipMemcpyDeviceToHost) == hipSuccess &&
+       (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(R), hipMemcpyDeviceToHost) == hipSuccess) &&
+       (!link_stats || hipMemcpy(link_stats, dst.p, links * 4 * sizeof(R), hipMemcpyDeviceToHost) == hipSuccess);
   int rc = LTE_OK;
   if (!ok) rc = fail(LTE_EHIP, std::string("mimo channel failed: ") + hipGetErrorString(hipGetLastError()));
   cleanup();
   return rc;
+}
+
+extern "C" {
+
+int lte_channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,
+                          const int32_t* delays, const double* gains, double fD, double fs, double snr_db,
+                          uint64_t seed, const float* x, const double* phases, const double* link_noise,
+                          const double* link_h, const double* noise, float* y, float* link_stats,
+                          float* noise_power) {
+  return channel_mimo_host<float>(L, num_tx, num_rx, mode, channel, n_paths, delays, gains, fD, fs, snr_db, seed, x,
+                                  phases, link_noise, link_h, noise, y, link_stats, noise_power);
+}
+
+int lte_channel_mimo_host64(int64_t L, int num_tx, int num_rx, int mode, int channel, int n_paths,
+                            const int32_t* delays, const double* gains, double fD, double fs, double snr_db,
+                            uint64_t seed, const double* x, const double* phases, const double* link_noise,
+                            const double* link_h, const double* noise, double* y, double* link_stats,
+                            double* noise_power) {
+  return channel_mimo_host<double>(L, num_tx, num_rx, mode, channel, n_paths, delays, gains, fD, fs, snr_db, seed, x,
+                                   phases, link_noise, link_h, noise, y, link_stats, noise_power);
 }
 
 int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps, int64_t n_sc, const double* y,
@@ -948,6 +982,8 @@ static int plan_mimo_tables(lte_plan* p) {
   std::vector<int32_t> np(nt), ppos((size_t)nt * maxP, 0), pseg((size_t)nt * nd, -1);
   std::vector<float2> pval((size_t)nt * maxP, make_float2(0.f, 0.f));
   std::vector<float> pig((size_t)nt * maxP, 0.f);
+  std::vector<double2> pval64((size_t)nt * maxP, make_double2(0.0, 0.0));
+  std::vector<double> pig64((size_t)nt * maxP, 0.0);
   for (int t = 0; t < nt; ++t) {
     const int n = (int)sub[t].size();
     if (n < 1) return fail(LTE_EUNSUP, "no pilots for a TX antenna");
@@ -957,7 +993,12 @@ static int plan_mimo_tables(lte_plan* p) {
     for (int i = 0; i < n; ++i) {
       ppos[(size_t)t * maxP + i] = sub[t][i];
       pval[(size_t)t * maxP + i] = make_float2((float)pr[2 * i], (float)pr[2 * i + 1]);
-      if (i + 1 < n) pig[(size_t)t * maxP + i] = (float)(1.0 * (1.0 / (sub[t][i + 1] - sub[t][i])));
+      pval64[(size_t)t * maxP + i] = make_double2(pr[2 * i], pr[2 * i + 1]);
+      // np.linspace's step: delta * (1 / gap) (complex / int divides by Smith's rule)
+      if (i + 1 < n) {
+        pig64[(size_t)t * maxP + i] = 1.0 / (double)(sub[t][i + 1] - sub[t][i]);
+        pig[(size_t)t * maxP + i] = (float)pig64[(size_t)t * maxP + i];
+      }
     }
     int sidx = -1;
     for (int j = 0; j < nd; ++j) {
@@ -967,13 +1008,15 @@ static int plan_mimo_tables(lte_plan* p) {
     }
   }
   if (upload(p->m_np, np) || upload(p->m_ppos, ppos) || upload(p->m_pseg, pseg) || upload(p->m_pval, pval) ||
-      upload(p->m_pig, pig))
+      upload(p->m_pig, pig) || upload(p->m_pval64, pval64) || upload(p->m_pig64, pig64))
     return fail(LTE_ENOMEM, "mimo table upload failed");
   p->mg.maxP = maxP;
   p->mg.np_tx = p->m_np.p;
   p->mg.ppos = p->m_ppos.p;
   p->mg.pval = p->m_pval.p;
   p->mg.pig = p->m_pig.p;
+  p->mg.pval64 = p->m_pval64.p;
+  p->mg.pig64 = p->m_pig64.p;
   p->mg.pseg = p->m_pseg.p;
   return LTE_OK;
 }
@@ -1023,6 +1066,51 @@ static bool alloc_siso(lte_plan* p, bool coded) {
   return !bad;
 }
 
+// Device workspace of the multi-antenna chains in precision R.
+template <class R>
+static bool alloc_mimo(lte_plan* p, bool coded) {
+  const lte_plan_desc& d = p->d;
+  ChainBufs<R>& c = cbuf<R>(p);
+  const size_t B = (size_t)d.max_frames;
+  const int G = (int)((B + 63) / 64);
+  const bool ray = d.channel == LTE_CH_RAYLEIGH;
+  const MimoGrid& m = p->mg;
+  const size_t links = (size_t)m.num_rx * m.num_tx;
+  bool bad = false;
+  bad |= c.x.alloc(B * m.num_tx * p->L) != 0;
+  bad |= c.y.alloc(B * m.num_rx * p->L) != 0;
+  bad |= c.coef.alloc(B * links * (ray ? d.n_paths : 1) * m.n_cs * 3) != 0;
+  if (ray && m.exact_jakes) bad |= c.phases.alloc(B * links * d.n_paths * 16) != 0;
+  if (ray && d.chain != LTE_CHAIN_SPATIAL) {
+    bad |= c.link_part.alloc(B * links * p->nblk) != 0;
+    bad |= c.link_sigma.alloc(B * links) != 0;
+  }
+  bad |= c.Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
+  bad |= c.H.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
+  if (ray) {
+    std::vector<R> gh(d.gains, d.gains + d.n_paths);
+    bad |= upload(c.gains, gh) != 0;
+  }
+  bad |= c.pow_part.alloc(B * m.num_rx * p->nblk) != 0;
+  bad |= c.npow.alloc(B * m.num_rx) != 0;
+  bad |= c.snr_lin.alloc(B) != 0;
+  if (coded) {
+    bad |= c.llr.alloc(B * p->n_re_bits) != 0;
+    c.blk.resize(p->C);
+    c.ckpt.resize(p->C);
+    std::vector<R*> bp(p->C);
+    for (int r = 0; r < p->C; ++r) {
+      const int K = p->cbs[r].K;
+      bad |= c.blk[r].alloc((size_t)G * turbo_rows(K) * 64) != 0;
+      bad |= c.ckpt[r].alloc((size_t)G * turbo_nwin(K) * turbo_ck_rows(sizeof(R) == 8) * 64) != 0;
+      if (!bad && hipMemset(c.blk[r].p, 0, c.blk[r].n * sizeof(R)) != hipSuccess) bad = true;
+      bp[r] = c.blk[r].p;
+    }
+    if (!bad) bad |= upload(c.blk_ptrs, bp) != 0;
+  }
+  return !bad;
+}
+
 extern "C" {
 
 static int plan_alloc(lte_plan* p) {
@@ -1030,48 +1118,17 @@ static int plan_alloc(lte_plan* p) {
   const size_t B = (size_t)d.max_frames;
   const int G = (int)((B + 63) / 64);
   const int rx = d.num_rx;
-  const bool ray = d.channel == LTE_CH_RAYLEIGH;
   const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
   bool bad = false;
   bad |= p->pw.alloc(B * p->PW) != 0;
-  if (p->mimo || p->bf) {   // float32 chains
+  if (p->mimo) {
+    bad |= !(p->f64 ? alloc_mimo<double>(p, coded) : alloc_mimo<float>(p, coded));
+  } else if (p->bf) {   // float32 chain
     ChainBufs<float>& c = p->c32;
-    if (p->mimo) {
-      const MimoGrid& m = p->mg;
-      const size_t links = (size_t)m.num_rx * m.num_tx;
-      bad |= c.x.alloc(B * m.num_tx * p->L) != 0;
-      bad |= c.y.alloc(B * m.num_rx * p->L) != 0;
-      bad |= c.coef.alloc(B * links * (ray ? d.n_paths : 1) * m.n_cs * 3) != 0;
-      if (ray && d.chain != LTE_CHAIN_SPATIAL) {
-        bad |= p->link_part.alloc(B * links * p->nblk) != 0;
-        bad |= p->link_sigma.alloc(B * links) != 0;
-      }
-      bad |= p->Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
-      bad |= p->Hm.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
-      if (ray) {
-        std::vector<float> gh(d.gains, d.gains + d.n_paths);
-        bad |= upload(c.gains, gh) != 0;
-      }
-    } else {
-      bad |= p->bf_fr.alloc(B) != 0;
-    }
+    bad |= p->bf_fr.alloc(B) != 0;
     bad |= c.pow_part.alloc(B * rx * p->nblk) != 0;
     bad |= c.npow.alloc(B * rx) != 0;
     bad |= c.snr_lin.alloc(B) != 0;
-    if (coded) {
-      bad |= c.llr.alloc(B * p->n_re_bits) != 0;
-      c.blk.resize(p->C);
-      c.ckpt.resize(p->C);
-      std::vector<float*> bp(p->C);
-      for (int r = 0; r < p->C; ++r) {
-        const int K = p->cbs[r].K;
-        bad |= c.blk[r].alloc((size_t)G * turbo_rows(K) * 64) != 0;
-        bad |= c.ckpt[r].alloc((size_t)G * turbo_nwin(K) * TURBO_CK_ROWS_F32 * 64) != 0;
-        if (!bad) HIPCHK(hipMemset(c.blk[r].p, 0, c.blk[r].n * sizeof(float)));
-        bp[r] = c.blk[r].p;
-      }
-      if (!bad) bad |= upload(c.blk_ptrs, bp) != 0;
-    }
   } else {
     bad |= !(p->f64 ? alloc_siso<double>(p, coded) : alloc_siso<float>(p, coded));
   }
@@ -1137,15 +1194,15 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
   if (d.n_bits < 1) return fail(LTE_EINVAL, "Bits array cannot be empty");
   if (d.precision != LTE_PREC_DEFAULT && d.precision != LTE_PREC_F32 && d.precision != LTE_PREC_F64)
     return fail(LTE_EINVAL, "precision must be LTE_PREC_DEFAULT, LTE_PREC_F32 or LTE_PREC_F64");
-  // float64 (the reference's arithmetic) is the default of the SISO / SIMO
-  // chains; the multi-antenna and beamforming chains compute in float32
-  if ((mimo || bf) && d.precision == LTE_PREC_F64)
-    return fail(LTE_EUNSUP, "the multi-antenna and beamforming chains compute in float32 (LTE_PREC_F32)");
+  // float64 (the reference's arithmetic) is the default of every chain but
+  // beamforming, which computes in float32
+  if (bf && d.precision == LTE_PREC_F64)
+    return fail(LTE_EUNSUP, "the beamforming chain computes in float32 (LTE_PREC_F32)");
   lte_plan* p = new lte_plan();
   p->d = d;
   p->d.num_tx = num_tx;
   p->mimo = mimo;
-  p->f64 = !(mimo || bf) && d.precision != LTE_PREC_F32;
+  p->f64 = !bf && d.precision != LTE_PREC_F32;
   const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
   if (coded && d.turbo_iters < 0) { delete p; return fail(LTE_EINVAL, "bad turbo_iters"); }
   int rc = plan_tables(p);
@@ -1200,7 +1257,11 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
     m.det = d.detector;
     m.n_dsc = sfbc ? p->res : (p->Nd + rank - 1) / rank;   // layers fill the first ceil(Nd/rank) data SCs (Q20)
     m.n_est = sfbc ? p->n_grp : p->n_sym;
-    m.n_cs = (d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0) ? p->n_sym : 1;
+    // fD != 0: f64 evaluates the Jakes sum exactly per sample (jw[m] = (2 pi
+    // fD) cos(alpha_m), rayleighchannel.py:28-38); f32 expands it per symbol
+    m.exact_jakes = p->f64 && d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0;
+    for (int k = 0; k < 16; ++k) m.jw[k] = 6.283185307179586 * d.fD * std::cos(6.283185307179586 * (k + 1) / 16.0);
+    m.n_cs = (d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0 && !m.exact_jakes) ? p->n_sym : 1;
     rc = plan_mimo_tables(p);
     if (rc) { p->tabs.release(); delete p; return rc; }
     if (!sfbc) {   // precoder W [num_tx][rank] in a [4][4] table; rank 0 in the descriptor -> identity
@@ -1252,9 +1313,9 @@ int lte_plan_destroy(lte_plan* p) {
   p->cap_bits.release();
   for (auto& b : p->decb) b.release();
   p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
-  p->m_np.release(); p->m_ppos.release(); p->m_pseg.release(); p->m_pval.release(); p->Ym.release();
-  p->Hm.release(); p->m_pig.release(); p->link_part.release(); p->link_sigma.release(); p->inj_lz.release();
-  p->inj_lh.release(); p->m_W.release(); p->bf_cb.release(); p->bf_fr.release();
+  p->m_np.release(); p->m_ppos.release(); p->m_pseg.release(); p->m_pval.release(); p->m_pval64.release();
+  p->m_pig.release(); p->m_pig64.release(); p->inj_lh.release(); p->m_W.release(); p->bf_cb.release();
+  p->bf_fr.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -1309,47 +1370,65 @@ static void pack_bits(const uint8_t* bits, int n, uint32_t* w, int nw) {
     if (bits[i] & 1) w[i >> 5] |= 1u << (31 - (i & 31));
 }
 
-// Multi-antenna chains (SFBC 2xN, uncoded / coded; TM4 spatial multiplexing).
-static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const uint32_t* inj_bits,
-                    int64_t inj_bits_stride, const float* inj_ph, int64_t inj_ph_stride, const float* inj_z,
-                    int64_t inj_z_stride) {
+}  // extern "C"
+
+// Host injection (float64 from the caller) -> device buffer of R, frames
+// [0, nf) of `per` values each; synchronous (the host copy is a temporary).
+template <class R>
+static int upload_inj(DBuf<R>& dst, const double* src, int64_t stride, int B, size_t per, hipStream_t s,
+                      const R** out, int64_t* out_stride) {
+  const int nf = stride ? B : 1;
+  std::vector<R> h((size_t)nf * per);
+  for (int f = 0; f < nf; ++f)
+    for (size_t i = 0; i < per; ++i) h[f * per + i] = (R)src[(size_t)f * stride + i];
+  if (dst.alloc(h.size())) return fail(LTE_ENOMEM, "injection buffer");
+  HIPCHK(hipMemcpyAsync(dst.p, h.data(), h.size() * sizeof(R), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *out = dst.p;
+  *out_stride = stride ? (int64_t)per : 0;
+  return LTE_OK;
+}
+
+// Multi-antenna chains (SFBC 2xN, uncoded / coded; TM4 spatial multiplexing)
+// in precision R.
+template <class R>
+static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const std::vector<double>& snr_lin,
+                    const uint32_t* inj_bits, int64_t inj_bits_stride) {
+  using V = cx<R>;
   const lte_plan_desc& d = p->d;
   const Grid& g = p->grid;
   const MimoGrid& m = p->mg;
+  ChainBufs<R>& c = cbuf<R>(p);
   hipStream_t s = p->stream;
   const bool coded = d.chain == LTE_CHAIN_SFBC_CODED;
   const bool ray = d.channel == LTE_CH_RAYLEIGH;
   const bool sfbc = m.mode == MIMO_SFBC;
   const bool link_noise = sfbc && ray;  // transmit_mimo's per-link 100 dB ChannelSimulator (core/ofdm_core.py:490-503)
   const size_t links = (size_t)m.num_rx * m.num_tx;
-  // link injections
-  const float* inj_lz = nullptr;
-  int64_t inj_lz_stride = 0;
-  std::vector<float> hlz;
-  if (a->link_noise && link_noise) {
-    const int nf = a->link_noise_stride ? B : 1;
-    const size_t per = links * 2 * p->L;
-    hlz.resize(nf * per);
-    for (int f = 0; f < nf; ++f)
-      for (size_t i = 0; i < per; ++i) hlz[f * per + i] = (float)a->link_noise[(size_t)f * a->link_noise_stride + i];
-    if (p->inj_lz.alloc(hlz.size())) return fail(LTE_ENOMEM, "inj link noise");
-    HIPCHK(hipMemcpyAsync(p->inj_lz.p, hlz.data(), hlz.size() * 4, hipMemcpyHostToDevice, s));
-    inj_lz = p->inj_lz.p;
-    inj_lz_stride = a->link_noise_stride ? (int64_t)per : 0;
+  std::vector<R> sl(B);
+  for (int b = 0; b < B; ++b) sl[b] = (R)snr_lin[b];
+  HIPCHK(hipMemcpyAsync(c.snr_lin.p, sl.data(), B * sizeof(R), hipMemcpyHostToDevice, s));
+  // injections (the reference's own draws, ref-compat mode)
+  const R *inj_ph = nullptr, *inj_z = nullptr, *inj_lz = nullptr, *inj_lh = nullptr;
+  int64_t inj_ph_stride = 0, inj_z_stride = 0, inj_lz_stride = 0, inj_lh_stride = 0;
+  if (a->phases && ray) {
+    const int e = upload_inj<R>(c.inj_ph, a->phases, a->phases_stride, B, links * d.n_paths * 16, s, &inj_ph,
+                                &inj_ph_stride);
+    if (e != LTE_OK) return e;
   }
-  const float* inj_lh = nullptr;
-  int64_t inj_lh_stride = 0;
-  std::vector<float> hlh;
+  if (a->noise) {
+    const int e = upload_inj<R>(c.inj_z, a->noise, a->noise_stride, B, (size_t)m.num_rx * 2 * p->L, s, &inj_z,
+                                &inj_z_stride);
+    if (e != LTE_OK) return e;
+  }
+  if (a->link_noise && link_noise) {
+    const int e = upload_inj<R>(c.inj_lz, a->link_noise, a->link_noise_stride, B, links * 2 * p->L, s, &inj_lz,
+                                &inj_lz_stride);
+    if (e != LTE_OK) return e;
+  }
   if (a->link_h && !ray && !sfbc) {
-    const int nf = a->link_h_stride ? B : 1;
-    const size_t per = links * 2;
-    hlh.resize(nf * per);
-    for (int f = 0; f < nf; ++f)
-      for (size_t i = 0; i < per; ++i) hlh[f * per + i] = (float)a->link_h[(size_t)f * a->link_h_stride + i];
-    if (p->inj_lh.alloc(hlh.size())) return fail(LTE_ENOMEM, "inj link gains");
-    HIPCHK(hipMemcpyAsync(p->inj_lh.p, hlh.data(), hlh.size() * 4, hipMemcpyHostToDevice, s));
-    inj_lh = p->inj_lh.p;
-    inj_lh_stride = a->link_h_stride ? (int64_t)per : 0;
+    const int e = upload_inj<R>(c.inj_lh, a->link_h, a->link_h_stride, B, links * 2, s, &inj_lh, &inj_lh_stride);
+    if (e != LTE_OK) return e;
   }
   {
     Timer t(p, KN_PAYLOAD);
@@ -1361,32 +1440,33 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   {
     Timer t(p, KN_OFDM_TX);
-    LCHK(launch_ofdm_tx_mimo(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, p->c32.x.p, B));
+    LCHK(launch_ofdm_tx_mimo<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, c.x.p, B));
   }
   const int np = ray ? d.n_paths : 1;
+  R* phases = (ray && m.exact_jakes) ? c.phases.p : nullptr;
   {
     Timer t(p, KN_FADING);
-    LCHK(launch_fading_mimo(s, g, m, B, ray ? 1 : 0, d.n_paths, p->c32.gains.p, d.fD, d.fs, p->fid.p, a->seed, inj_ph,
-                            inj_ph_stride, inj_lh, inj_lh_stride, p->c32.coef.p));
+    LCHK(launch_fading_mimo<R>(s, g, m, B, ray ? 1 : 0, d.n_paths, c.gains.p, d.fD, d.fs, p->fid.p, a->seed, inj_ph,
+                               inj_ph_stride, inj_lh, inj_lh_stride, c.coef.p, phases));
   }
   {
     Timer t(p, KN_CHANNEL);
-    LCHK(launch_channel_mimo(s, g, m, B, np, ray ? p->delays.p : nullptr, p->c32.coef.p, p->c32.x.p, p->c32.y.p,
-                             link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, p->link_part.p,
-                             p->link_sigma.p, p->c32.pow_part.p, p->nblk));
+    LCHK(launch_channel_mimo<R>(s, g, m, B, np, ray ? p->delays.p : nullptr, c.coef.p, phases, c.gains.p, d.fs, c.x.p,
+                                c.y.p, link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, c.link_part.p,
+                                c.link_sigma.p, c.pow_part.p, p->nblk));
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
-    LCHK(launch_npow_mimo(s, B, m.num_rx, p->c32.pow_part.p, mimo_channel_nblk(p->L, g.N + g.cp), p->L, p->c32.snr_lin.p,
-                          sfbc ? 1.0f / (float)m.num_tx : 1.0f, p->c32.npow.p));
+    LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, mimo_channel_nblk(p->L, g.N + g.cp), p->L, c.snr_lin.p,
+                             sfbc ? (double)m.num_tx : 1.0, c.npow.p));
   }
   {
     Timer t(p, KN_RX_CHEST);
-    LCHK(launch_rx_fft_mimo(s, g, m, B, p->c32.y.p, p->c32.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, p->Ym.p, p->Hm.p));
+    LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p));
   }
-  float2* cap_syms_dev = nullptr;
+  V* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
   if (a->cap_data_syms) {
-    if (p->c32.capbuf.alloc((size_t)B * p->n_sym * m.res)) return fail(LTE_ENOMEM, "capture");
-    cap_syms_dev = p->c32.capbuf.p;
+    if (c.capbuf.alloc((size_t)B * p->n_sym * m.res)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = c.capbuf.p;
   }
   if (a->cap_bits_rx) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
@@ -1395,26 +1475,26 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   {
     Timer t(p, KN_RX_DATA);
     if (sfbc)
-      LCHK(launch_det_sfbc(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, p->Ym.p, p->Hm.p, p->c32.snr_lin.p, p->pw.p, p->PW,
-                           d.n_bits, p->frame_err.p, p->c32.llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev));
+      LCHK(launch_det_sfbc<R>(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, c.Ym.p, c.H.p, c.snr_lin.p, p->pw.p, p->PW,
+                              d.n_bits, p->frame_err.p, c.llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev));
     else
-      LCHK(launch_det_spatial(s, g, m, B, p->Ym.p, p->Hm.p, p->c32.snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
-                              cap_syms_dev, cap_bits_dev));
+      LCHK(launch_det_spatial<R>(s, g, m, B, c.Ym.p, c.H.p, c.snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+                                 cap_syms_dev, cap_bits_dev));
   }
   if (coded) {
     {
       Timer t(p, KN_DEMATCH);
-      LCHK(launch_dematch(s, p->c32.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, p->c32.blk_ptrs.p, p->rows_dev.p));
+      LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p));
     }
     const int G = (B + 63) / 64;
     std::vector<TurboJob> jobs(p->C);
     for (int r = 0; r < p->C; ++r) {
-      const CbInfo& c = p->cbs[r];
-      jobs[r] = TurboJob{p->c32.blk[r].p, p->c32.ckpt[r].p, p->decb[r].p, c.K, c.f1, c.f2, G};
+      const CbInfo& cb = p->cbs[r];
+      jobs[r] = TurboJob{c.blk[r].p, c.ckpt[r].p, p->decb[r].p, cb.K, cb.f1, cb.f2, G};
     }
     {
       Timer t(p, KN_TURBO);
-      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1, 0));
+      LCHK(launch_turbo_jobs(s, jobs.data(), p->C, d.turbo_iters, TM_DEC1, sizeof(R) == 8 ? 1 : 0));
     }
     {
       Timer t(p, KN_CRC);
@@ -1436,47 +1516,45 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     HIPCHK(hipMemcpyAsync(crc.data(), p->frame_crc.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   }
   if (a->cap_signal_tx)
-    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, p->c32.x.p, (size_t)B * m.num_tx * p->L * sizeof(float2),
-                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_signal_tx, c.x.p, (size_t)B * m.num_tx * p->L * sizeof(V), hipMemcpyDeviceToHost, s));
   if (a->cap_signal_rx) {
-    DBuf<float2> tmp;
+    DBuf<V> tmp;
     if (tmp.alloc((size_t)B * m.num_rx * p->L)) return fail(LTE_ENOMEM, "capture");
     {
       Timer t(p, KN_CAP);
-      hipLaunchKernelGGL(k_cap_rx<float>, dim3(((p->L + 255) / 256) * B, m.num_rx), dim3(256), 0, s, p->L, m.num_rx, B,
-                         p->c32.y.p, (int64_t)p->L, (int64_t)m.num_rx * p->L, p->c32.npow.p, p->fid.p, a->seed, inj_z,
+      hipLaunchKernelGGL(k_cap_rx<R>, dim3(((p->L + 255) / 256) * B, m.num_rx), dim3(256), 0, s, p->L, m.num_rx, B,
+                         c.y.p, (int64_t)p->L, (int64_t)m.num_rx * p->L, c.npow.p, p->fid.p, a->seed, inj_z,
                          inj_z_stride, tmp.p);
       LCHK((int)hipGetLastError());
     }
-    HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * m.num_rx * p->L * sizeof(float2),
-                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * m.num_rx * p->L * sizeof(V), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     tmp.release();
   }
   if (a->cap_data_syms)
-    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->n_sym * m.res * sizeof(float2),
+    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->n_sym * m.res * sizeof(V),
                           hipMemcpyDeviceToHost, s));
   if (a->cap_H)   // multi-antenna layout [B][num_rx][n_est][num_tx][n_dsc]
-    HIPCHK(hipMemcpyAsync(a->cap_H, p->Hm.p, (size_t)B * m.num_rx * m.n_est * m.num_tx * m.n_dsc * sizeof(float2),
+    HIPCHK(hipMemcpyAsync(a->cap_H, c.H.p, (size_t)B * m.num_rx * m.n_est * m.num_tx * m.n_dsc * sizeof(V),
                           hipMemcpyDeviceToHost, s));
   if (a->cap_bits_rx)
     HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
   if (a->cap_llr && coded)
-    HIPCHK(hipMemcpyAsync(a->cap_llr, p->c32.llr.p, (size_t)B * p->n_re_bits * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_llr, c.llr.p, (size_t)B * p->n_re_bits * sizeof(R), hipMemcpyDeviceToHost, s));
   if (a->cap_noise_power)
-    HIPCHK(hipMemcpyAsync(a->cap_noise_power, p->c32.npow.p, (size_t)B * m.num_rx * sizeof(float), hipMemcpyDeviceToHost,
-                          s));
-  DBuf<float> lpart, lstats;
+    HIPCHK(hipMemcpyAsync(a->cap_noise_power, c.npow.p, (size_t)B * m.num_rx * sizeof(R), hipMemcpyDeviceToHost, s));
+  DBuf<R> lpart, lstats;
   if (a->cap_link_stats) {
-    if (lpart.alloc((size_t)B * links * 4 * p->nblk) || lstats.alloc((size_t)B * links * 4))
+    const int nb = (p->L + 255) / 256;
+    if (lpart.alloc((size_t)B * links * 4 * nb) || lstats.alloc((size_t)B * links * 4))
       return fail(LTE_ENOMEM, "capture");
     {
       Timer t(p, KN_CAP);
-      LCHK(launch_link_stats(s, g, m, B, np, ray ? p->delays.p : nullptr, p->c32.coef.p, p->c32.x.p, lpart.p, p->nblk,
-                             lstats.p));
+      LCHK(launch_link_stats<R>(s, g, m, B, np, ray ? p->delays.p : nullptr, c.coef.p, phases, c.gains.p, d.fs, c.x.p,
+                                link_noise ? c.link_sigma.p : nullptr, p->fid.p, a->seed, inj_lz, inj_lz_stride,
+                                lpart.p, nb, lstats.p));
     }
-    HIPCHK(hipMemcpyAsync(a->cap_link_stats, lstats.p, (size_t)B * links * 4 * sizeof(float), hipMemcpyDeviceToHost,
-                          s));
+    HIPCHK(hipMemcpyAsync(a->cap_link_stats, lstats.p, (size_t)B * links * 4 * sizeof(R), hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
   if (p->timing) collect_timing(p);
@@ -1486,6 +1564,8 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     for (int b = 0; b < B; ++b) a->frame_crc_ok[b] = (uint8_t)crc[b];
   return LTE_OK;
 }
+
+extern "C" {
 
 // Beamforming chain (frequency domain, flat H per frame).
 static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const uint32_t* inj_bits,
@@ -1576,22 +1656,6 @@ static bool txch_fusable(const lte_plan* p, const lte_run_args* a, bool coded) {
 }
 
 
-// Host injection (float64 from the caller) -> device buffer of R, frames
-// [0, nf) of `per` values each; synchronous (the host copy is a temporary).
-template <class R>
-static int upload_inj(DBuf<R>& dst, const double* src, int64_t stride, int B, size_t per, hipStream_t s,
-                      const R** out, int64_t* out_stride) {
-  const int nf = stride ? B : 1;
-  std::vector<R> h((size_t)nf * per);
-  for (int f = 0; f < nf; ++f)
-    for (size_t i = 0; i < per; ++i) h[f * per + i] = (R)src[(size_t)f * stride + i];
-  if (dst.alloc(h.size())) return fail(LTE_ENOMEM, "injection buffer");
-  HIPCHK(hipMemcpyAsync(dst.p, h.data(), h.size() * sizeof(R), hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));
-  *out = dst.p;
-  *out_stride = stride ? (int64_t)per : 0;
-  return LTE_OK;
-}
 
 // Coded TX + channel with one slot per frame (k_ofdm_txf) when its LDS fits
 // (coded streams staged once per frame); LTE_TX_FRAME=0 keeps one slot per
@@ -1920,19 +1984,15 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
     HIPCHK(hipStreamSynchronize(s));
     return e;
   }
-  // multi-antenna / beamforming chains: float32
   if (stages != LTE_STAGE_ALL) return fail(LTE_EUNSUP, "multi-antenna chains run all stages");
+  if (p->mimo)
+    return p->f64 ? run_mimo<double>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride)
+                  : run_mimo<float>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride);
+  // beamforming chain: float32
   ChainBufs<float>& c = p->c32;
   std::vector<float> slf(B);
   for (int b = 0; b < B; ++b) slf[b] = (float)sl[b];
   HIPCHK(hipMemcpyAsync(c.snr_lin.p, slf.data(), B * sizeof(float), hipMemcpyHostToDevice, s));
-  const float* inj_ph = nullptr;
-  int64_t inj_ph_stride = 0;
-  if (a->phases && d.channel == LTE_CH_RAYLEIGH) {
-    const int e = upload_inj<float>(c.inj_ph, a->phases, a->phases_stride, B, (size_t)rx * d.num_tx * d.n_paths * 16,
-                                    s, &inj_ph, &inj_ph_stride);
-    if (e != LTE_OK) return e;
-  }
   const float* inj_z = nullptr;
   int64_t inj_z_stride = 0;
   if (a->noise) {
@@ -1940,8 +2000,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
                                     &inj_z_stride);
     if (e != LTE_OK) return e;
   }
-  if (p->bf) return run_bf(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_z, inj_z_stride);
-  return run_mimo(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_ph, inj_ph_stride, inj_z, inj_z_stride);
+  return run_bf(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_z, inj_z_stride);
 }
 
 // ------------------------------------------------------------------ stage entry points

@@ -37,6 +37,21 @@ __device__ __forceinline__ cx<R> qam_point(int idx) {
   }
 }
 
+// TX output scale: f32 1/sqrt(N); f64 sqrt(N)/N, which for a power-of-two N
+// is exactly NumPy's ifft(.) * sqrt(N) (the 1/N is a power of two)
+template <class R>
+__device__ __forceinline__ R tx_scale(int N) {
+  if constexpr (sizeof(R) == 8) return sqrt((double)N) / (double)N;
+  else return rsqrtf((float)N);
+}
+// RX FFT scale: fft(.) / sqrt(N); NumPy's complex / real divide multiplies by
+// the reciprocal, so f64 uses 1.0 / sqrt(N)
+template <class R>
+__device__ __forceinline__ R rx_scale(int N) {
+  if constexpr (sizeof(R) == 8) return 1.0 / sqrt((double)N);
+  else return rsqrtf((float)N);
+}
+
 template <class R>
 __device__ __forceinline__ R block_sum(R v, R* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

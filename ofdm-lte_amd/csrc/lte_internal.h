@@ -187,7 +187,7 @@ struct MimoGrid {
   int n_dsc;               // data SCs that carry data: SFBC Nd&~1, spatial ceil(Nd/num_tx)
   int maxP;                // pilot stride of the per-TX tables
   int n_est;               // channel estimates per frame (SFBC: one per 14-symbol group; spatial: every symbol)
-  int n_cs;                // fading coefficient sets per link path (1 if fD == 0, else n_sym)
+  int n_cs;                // fading coefficient sets per link path (1 if fD == 0 or exact Jakes, else n_sym)
   const int32_t* np_tx;    // [num_tx] pilots of each TX
   const int32_t* ppos;     // [num_tx][maxP] pilot subcarriers of TX t
   const float2* pval;      // [num_tx][maxP] pilot symbols of TX t
@@ -195,32 +195,65 @@ struct MimoGrid {
   const int32_t* pseg;     // [num_tx][n_dsc] left pilot (within TX t's set) of data SC j; -1 / >= np-1: edge hold
   int rank, det;           // spatial: layers, LTE_DET_*
   const double* W;         // spatial: [4][4] complex (re, im) precoder, entry (t, c) at (t*4 + c)*2
+  // float64 plans: the pilot tables in float64, and for fD != 0 the exact
+  // Jakes sum per sample (jakes_fading, rayleighchannel.py:20-42): jw[m] =
+  // (2 pi fD) cos(alpha_m) as the reference forms it, the 16 phases of every
+  // link path in the channel kernels' `phases` buffer
+  const double2* pval64;
+  const double* pig64;
+  int exact_jakes;
+  double jw[16];
 };
+template <class R> struct MGT;
+template <> struct MGT<float> {
+  __host__ __device__ static const float2* pval(const MimoGrid& m) { return m.pval; }
+  __host__ __device__ static const float* pig(const MimoGrid& m) { return m.pig; }
+};
+template <> struct MGT<double> {
+  __host__ __device__ static const double2* pval(const MimoGrid& m) { return m.pval64; }
+  __host__ __device__ static const double* pig(const MimoGrid& m) { return m.pig64; }
+};
+// Multi-antenna launchers, R = double (the reference's complex128, default)
+// or float (fast mode); explicit instances in lte_mimo.hip.
+template <class R>
 int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
-                        const uint32_t* enc, int enc_words, const int32_t* tx_map, float2* x, int B);
-// per link path: h(n) = A + B d + C d^2 around the centre of n's OFDM symbol (fD != 0), or A (fD == 0)
+                        const uint32_t* enc, int enc_words, const int32_t* tx_map, cx<R>* x, int B);
+// per link path: f32 h(n) = A + B d + C d^2 around the centre of n's OFDM
+// symbol (fD != 0), or A (fD == 0); f64 A (fD == 0) or the phases (exact Jakes)
+template <class R>
 int launch_fading_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int rayleigh, int n_paths,
-                       const float* gains, double fD, double fs, const uint64_t* fid, uint64_t seed,
-                       const float* inj_ph, int64_t inj_ph_stride, const float* inj_h, int64_t inj_h_stride,
-                       float2* coef);
+                       const R* gains, double fD, double fs, const uint64_t* fid, uint64_t seed,
+                       const R* inj_ph, int64_t inj_ph_stride, const R* inj_h, int64_t inj_h_stride,
+                       cx<R>* coef, R* phases);
+// phases / gains: exact-Jakes mode (m.exact_jakes) only
+template <class R>
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
-                        const float2* coef, const float2* x, float2* y, int link_noise, const uint64_t* fid,
-                        uint64_t seed, const float* inj_lz, int64_t inj_lz_stride, float* link_part,
-                        float* link_sigma, float* pow_part, int nblk);
+                        const cx<R>* coef, const R* phases, const R* gains, double fs, const cx<R>* x, cx<R>* y,
+                        int link_noise, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
+                        R* link_part, R* link_sigma, R* pow_part, int nblk);
 int mimo_channel_nblk(int L, int sym_len);   // power partials per (frame, rx) written by launch_channel_mimo
+// per link [mean|x|^2, mean|y|^2, Re, Im mean(y conj x)] of the link's output
+// y (with its 100 dB link noise when link_sigma is set)
+template <class R>
 int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
-                      const float2* coef, const float2* x, float* part, int nblk, float* stats);
-int launch_npow_mimo(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
-                     float norm, float* npow);
-int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* y, const float* npow,
-                       const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride, float2* Y,
-                       float2* H);
-int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const float2* Y,
-                    const float2* H, const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                    float* llr, float2* cap_syms, uint8_t* cap_bits);
-int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
-                       const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                       float2* cap_syms, uint8_t* cap_bits);
+                      const cx<R>* coef, const R* phases, const R* gains, double fs, const cx<R>* x,
+                      const R* link_sigma, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
+                      R* part, int nblk, R* stats);
+// noise power per RX: ((P / div) / snr): div = num_tx (transmit_mimo) or 1 (spatial)
+template <class R>
+int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nblk, int L, const R* snr_lin,
+                     double div, R* npow);
+template <class R>
+int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
+                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H);
+template <class R>
+int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const cx<R>* Y,
+                    const cx<R>* H, const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits);
+template <class R>
+int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* Y, const cx<R>* H,
+                       const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                       cx<R>* cap_syms, uint8_t* cap_bits);
 int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int64_t n, const double* y,
                      const double* H, const double* W, double s2, double* out);
 

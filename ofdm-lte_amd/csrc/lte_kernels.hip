@@ -85,21 +85,6 @@ __device__ __forceinline__ V* dyn_lds() {
   return reinterpret_cast<V*>(lte_dyn_lds);
 }
 
-// TX output scale: f32 1/sqrt(N); f64 sqrt(N)/N, which for a power-of-two N
-// is exactly NumPy's ifft(.) * sqrt(N) (the 1/N is a power of two)
-template <class R>
-__device__ __forceinline__ R tx_scale(int N) {
-  if constexpr (sizeof(R) == 8) return sqrt((double)N) / (double)N;
-  else return rsqrtf((float)N);
-}
-// RX FFT scale: fft(.) / sqrt(N); NumPy's complex / real divide multiplies by
-// the reciprocal, so f64 uses 1.0 / sqrt(N)
-template <class R>
-__device__ __forceinline__ R rx_scale(int N) {
-  if constexpr (sizeof(R) == 8) return 1.0 / sqrt((double)N);
-  else return rsqrtf((float)N);
-}
-
 // Fused static-tap channel for one OFDM symbol held in LDS (TxChannelT): y[m] =
 // sum_p c_p x[m - d_p] over the CP-extended symbol, whose sample j is
 // buf[j < cp ? N - cp + j : j - cp] (rayleighchannel.py:44-58; for m >=

@@ -4,11 +4,17 @@
 //  * TM4 spatial multiplexing, 2 / 4 TX, 1-4 RX, rank 1-4, codebook precoder W,
 //    MMSE / ZF / SIC / MRC (simulate_spatial_multiplexing,
 //    core/ofdm_core.py:2489-2815; config 5 = 4x4 rank 4 MMSE).
+// Every kernel is one template over the arithmetic type R: double (the
+// default; the reference computes in complex128) or float (fast mode), V =
+// cx<R>.  The float64 instances follow the reference's operation order where
+// it is cheap to (NumPy scalar semantics in the SFBC combiner, the exact Jakes
+// sum per sample for fD != 0); the float32 ones keep their shortcuts.
 // Per frame:  TX  one slot per (frame, OFDM symbol, TX antenna): QAM map ->
 //                 SFBC pair coding / layer mapping -> per-TX CRS pilots -> IFFT + CP
-//             CH  per link path coefficients (Jakes, fD = 0 constant or a
-//                 per-symbol quadratic expansion when fD != 0), sum over TX,
-//                 measured-power noise per RX (transmit_mimo / _spatial_multiplexing)
+//             CH  per link path coefficients (Jakes: fD = 0 constant; fD != 0
+//                 f64 the exact sum per sample, f32 a per-symbol quadratic
+//                 expansion), sum over TX, measured-power noise per RX
+//                 (transmit_mimo / transmit_spatial_multiplexing)
 //             RX  one slot per (frame, RX, OFDM symbol): noise + CP removal + FFT;
 //                 on estimation symbols LS at each TX's pilot subset + linear
 //                 interpolation (MIMOChannelEstimatorPeriodic); data SCs to HBM
@@ -22,16 +28,22 @@ namespace lte {
 
 constexpr int MWG = 256;
 
+template <class V>
+__device__ __forceinline__ V* mimo_lds() {
+  extern __shared__ double2 lte_mimo_lds[];
+  return reinterpret_cast<V*>(lte_mimo_lds);
+}
+
 // ---------------------------------------------------------------------------
 // TX.  SFBCAlamouti.encode (core/sfbc_alamouti.py:45-78) + SFBCResourceMapper
 // (:213-256): data RE j of symbol l carries, for the pair (s0, s1) =
 // (q[l*res + (j&~1)], q[.. + 1]): TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)].
 // Spatial (core/ofdm_core.py:2596-2655): layer c = q[R j + c] on data SC j <
 // ceil(Nd/R) (Q20), x_t = sum_c W[t][c] layer_c.  Pilots: TX t at its subset
-// (cell t % 4).
-template <int CODED, int BPS>
-__device__ __forceinline__ float2 qam_at(int64_t q, const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fe,
-                                         const int32_t* __restrict__ tx_map) {
+// (cell t % 4).  x = ifft(grid) sqrt(N) (tx_scale), CP prepended.
+template <class R, int CODED, int BPS>
+__device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fe,
+                                        const int32_t* __restrict__ tx_map) {
   int idx = 0;
   bool zero = false;
   if constexpr (CODED) {
@@ -45,22 +57,23 @@ __device__ __forceinline__ float2 qam_at(int64_t q, const uint32_t* __restrict__
 #pragma unroll
     for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, q * BPS + m);
   }
-  return zero ? make_float2(0.f, 0.f) : qam_point<BPS>(idx);
+  return zero ? mkc((R)0, (R)0) : qam_point<BPS, R>(idx);
 }
 
-template <int MODE, int CODED, int BPS>
+template <class R, int MODE, int CODED, int BPS>
 __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                       const uint32_t* __restrict__ enc, int enc_words,
-                                                      const int32_t* __restrict__ tx_map, float2* __restrict__ x,
+                                                      const int32_t* __restrict__ tx_map, cx<R>* __restrict__ x,
                                                       int B, int stage_enc) {
-  extern __shared__ float2 sm[];
+  using V = cx<R>;
+  V* sm = mimo_lds<V>();
   const int N = g.N, T = N >> 3, spw = MWG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int per = g.n_sym * m.num_tx;
   const int gs = blockIdx.x * spw + slot;
   const int b = gs / per, r = gs - b * per, l = r / m.num_tx, t = r - l * m.num_tx;
   const bool active = slot < spw && b < B;
-  float2* buf = sm + slot * N;
+  V* buf = sm + slot * N;
   // coded: the frame's coded streams are staged in LDS (coalesced), so the
   // rate-match / interleaver bit gathers hit LDS (as in k_ofdm_tx)
   const uint32_t* fe = enc + (size_t)b * enc_words;
@@ -71,54 +84,56 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
     fe = es;
   }
   if (active)
-    for (int k = tid; k < N; k += T) buf[k] = make_float2(0.f, 0.f);
+    for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
   __syncthreads();
   if (active) {
     const uint32_t* fb = pw + (size_t)b * PW;
     const int64_t q0 = (int64_t)l * m.res;
     for (int j = tid; j < m.n_dsc; j += T) {
-      float2 v;
+      V v;
       if constexpr (MODE == MIMO_SFBC) {
         const int64_t qp = q0 + (j & ~1);
-        const float2 s0 = qam_at<CODED, BPS>(qp, fb, fe, tx_map), s1 = qam_at<CODED, BPS>(qp + 1, fb, fe, tx_map);
+        const V s0 = qam_at<R, CODED, BPS>(qp, fb, fe, tx_map), s1 = qam_at<R, CODED, BPS>(qp + 1, fb, fe, tx_map);
         if ((j & 1) == 0) v = t == 0 ? s0 : s1;
-        else v = t == 0 ? make_float2(-s1.x, s1.y) : make_float2(s0.x, -s0.y);   // -conj(s1) / conj(s0)
+        else v = t == 0 ? mkc(-s1.x, s1.y) : mkc(s0.x, -s0.y);   // -conj(s1) / conj(s0)
       } else {
-        v = make_float2(0.f, 0.f);
+        v = mkc((R)0, (R)0);
         for (int c = 0; c < m.rank; ++c) {
           const int qi = m.rank * j + c;
           if (qi >= m.res) break;
-          const float2 sq = qam_at<CODED, BPS>(q0 + qi, fb, fe, tx_map);
-          const float2 w = make_float2((float)m.W[(t * 4 + c) * 2], (float)m.W[(t * 4 + c) * 2 + 1]);
+          const V sq = qam_at<R, CODED, BPS>(q0 + qi, fb, fe, tx_map);
+          const V w = mkc((R)m.W[(t * 4 + c) * 2], (R)m.W[(t * 4 + c) * 2 + 1]);
           v = cadd(v, cmul(w, sq));
         }
       }
       buf[g.data_idx[j]] = v;
     }
     const int npt = m.np_tx[t];
-    for (int p = tid; p < npt; p += T) buf[m.ppos[t * m.maxP + p]] = m.pval[t * m.maxP + p];
+    const V* pv = MGT<R>::pval(m) + t * m.maxP;
+    for (int p = tid; p < npt; p += T) buf[m.ppos[t * m.maxP + p]] = pv[p];
   }
   __syncthreads();
-  fft_lds<true>(buf, N, g.log2N, g.tw, tid, active);
+  fft_lds<true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
   if (active) {
-    const float sc = rsqrtf((float)N);
-    float2* xo = x + ((size_t)b * m.num_tx + t) * g.L + (size_t)l * (N + g.cp);
+    const R sc = tx_scale<R>(N);
+    V* xo = x + ((size_t)b * m.num_tx + t) * g.L + (size_t)l * (N + g.cp);
     for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
     for (int k = tid; k < g.cp; k += T) xo[k] = cscale(buf[N - g.cp + k], sc);
   }
 }
 
+template <class R>
 int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
-                        const uint32_t* enc, int enc_words, const int32_t* tx_map, float2* x, int B) {
+                        const uint32_t* enc, int enc_words, const int32_t* tx_map, cx<R>* x, int B) {
   const int spw = MWG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym * m.num_tx;
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
   const int stage_enc = coded && enc_shm <= 32768;
-  const size_t shm = spw * g.N * sizeof(float2) + (stage_enc ? enc_shm : 0);
+  const size_t shm = spw * g.N * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
 #define LTE_TXM(M_, C_, B_)                                                                                          \
-  hipLaunchKernelGGL((k_ofdm_tx_mimo<M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words,   \
+  hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words, \
                      tx_map, x, B, stage_enc)
 #define LTE_TXM_BPS(M_, C_) \
   do { if (g.bps == 2) LTE_TXM(M_, C_, 2); else if (g.bps == 4) LTE_TXM(M_, C_, 4); else LTE_TXM(M_, C_, 6); } while (0)
@@ -135,41 +150,55 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
 // ---------------------------------------------------------------------------
 // Link fading.  One thread per (frame, rx, tx, path).  Rayleigh:
 // RayleighChannel.jakes_fading (core/rayleighchannel.py:20-42) with 16 phases
-// (injected, or Philox): h(n) = g sqrt(2/16) sum_m exp(j(w_m n + phi_m)),
-// w_m = 2 pi fD cos(2 pi (m+1)/16) / fs.  fD == 0: constant A.  Otherwise,
-// per OFDM symbol s with centre c_s, the exact second-order expansion
-// h(c_s + d) = A + B d + C d^2 (|w d| <= 1.3e-3 rad at 3 km/h, 20 MHz: the
-// truncation error ~1e-10 is far below float32), computed in float64.
+// (injected, or Philox): h(n) = g sqrt(2/16) sum_m exp(j(w_m n / fs + phi_m)),
+// w_m = (2 pi fD) cos(2 pi (m+1)/16).
+//  * fD == 0: the constant A = g (sqrt(2/16) sum_m exp(j phi_m)) -- f64 in the
+//    reference's order (phi_m is then exactly the argument);
+//  * fD != 0, f64 (exact Jakes): the phases are stored and the channel kernels
+//    evaluate the sum per sample (link_accumulate);
+//  * fD != 0, f32: per OFDM symbol s with centre c_s the exact second-order
+//    expansion h(c_s + d) = A + B d + C d^2 (|w d| <= 1.3e-3 rad at 3 km/h,
+//    20 MHz: truncation ~1e-10, far below float32), computed in float64.
 // AWGN links: SFBC h = exp(j t pi/2) (core/ofdm_core.py:476-487); spatial
 // h ~ CN(0,1) (core/channel.py:473-480), injected or Philox.
-// coef layout: [B][rx][tx][path][n_cs][3] (A, B, C).
+// coef layout: [B][rx][tx][path][n_cs][3] (A, B, C); phases [B][rx][tx][path][16].
+template <class R>
 __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_tx, int n_paths, int n_cs, int mode,
-                                                     int rayleigh, const float* __restrict__ gains, double fD,
-                                                     double fs, int sym_len, const uint64_t* __restrict__ fid,
-                                                     uint64_t seed, const float* __restrict__ inj_ph,
-                                                     int64_t inj_ph_stride, const float* __restrict__ inj_h,
-                                                     int64_t inj_h_stride, float2* __restrict__ coef) {
+                                                     int rayleigh, const R* __restrict__ gains, double fD, double fs,
+                                                     int sym_len, const uint64_t* __restrict__ fid, uint64_t seed,
+                                                     const R* __restrict__ inj_ph, int64_t inj_ph_stride,
+                                                     const R* __restrict__ inj_h, int64_t inj_h_stride,
+                                                     cx<R>* __restrict__ coef, R* __restrict__ phases) {
+  constexpr bool F64 = sizeof(R) == 8;
   const int per = num_rx * num_tx * n_paths;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * per) return;
   const int b = i / per, rem = i - b * per, link = rem / n_paths, p = rem - link * n_paths;
   const int rx = link / num_tx, tx = link - rx * num_tx;
-  float2* out = coef + (size_t)i * n_cs * 3;
+  cx<R>* out = coef + (size_t)i * n_cs * 3;
   if (!rayleigh) {
     double hr = 0.0, hi = 0.0;
     if (mode == MIMO_SFBC) {
       if (tx == 0) { hr = 1.0; hi = 0.0; }
-      else { hr = cos(tx * 1.5707963267948966); hi = sin(tx * 1.5707963267948966); }
+      else {   // np.exp(1j * (t * np.pi / 2))
+        const double a = ((double)tx * 3.141592653589793) / 2.0;
+        hr = cos(a); hi = sin(a);
+      }
     } else if (inj_h) {
-      const float* hh = inj_h + (size_t)b * inj_h_stride + (size_t)link * 2;
+      const R* hh = inj_h + (size_t)b * inj_h_stride + (size_t)link * 2;
       hr = hh[0]; hi = hh[1];
     } else {
       const u32x4 r = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, 0x7FFFFFFFu);
-      const float2 z = box_muller(r.x, r.y);
-      hr = z.x * 0.7071067811865476; hi = z.y * 0.7071067811865476;
+      if constexpr (F64) {
+        const double2 z = gauss2<double>(r.x, r.y);
+        hr = 0.7071067811865475 * z.x; hi = 0.7071067811865475 * z.y;   // normal(0, 1/np.sqrt(2))
+      } else {
+        const float2 z = box_muller(r.x, r.y);
+        hr = z.x * 0.7071067811865476; hi = z.y * 0.7071067811865476;
+      }
     }
-    out[0] = make_float2((float)hr, (float)hi);
-    out[1] = out[2] = make_float2(0.f, 0.f);
+    out[0] = mkc((R)hr, (R)hi);
+    out[1] = out[2] = mkc((R)0, (R)0);
     return;
   }
   double ph[16];
@@ -180,63 +209,119 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
       const u32x4 r = rng4(seed, fid[b], RNG_STREAM_MIMO_FADE + (uint32_t)rem, (uint32_t)(mm >> 2));
       const int q = mm & 3;
       const uint32_t u = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
-      ph[mm] = 6.283185307179586 * ((u >> 8) * (1.0 / 16777216.0));
+      ph[mm] = F64 ? 6.283185307179586 * (((double)u + 0.5) * 2.3283064365386962890625e-10)
+                   : 6.283185307179586 * ((u >> 8) * (1.0 / 16777216.0));
     }
   }
-  const double k = sqrt(2.0 / 16.0) * (double)gains[p];
-  // per sinusoid: phasor at the first symbol centre, then rotate by w * sym_len
-  // per symbol (float64 recurrence: 2 sincos per sinusoid instead of one per symbol)
-  double w[16], zr[16], zi[16], rr[16], ri[16];
-  const double c0 = fD == 0.0 ? 0.0 : 0.5 * (sym_len - 1);
-  for (int mm = 0; mm < 16; ++mm) {
-    w[mm] = fD == 0.0 ? 0.0 : 6.283185307179586 * fD * cos(6.283185307179586 * (mm + 1) / 16.0) / fs;
-    sincos(w[mm] * c0 + ph[mm], &zi[mm], &zr[mm]);
-    sincos(w[mm] * (double)sym_len, &ri[mm], &rr[mm]);
-  }
-  for (int sidx = 0; sidx < n_cs; ++sidx) {
-    double ar = 0, ai = 0, br = 0, bi = 0, cr = 0, ci = 0;
+  if constexpr (F64) {
+    double sr = 0.0, si = 0.0;
     for (int mm = 0; mm < 16; ++mm) {
-      const double cv = zr[mm], sv = zi[mm], wm = w[mm];
-      ar += cv; ai += sv;
-      br += -wm * sv; bi += wm * cv;                   // j w e^{j th}
-      cr += -0.5 * wm * wm * cv; ci += -0.5 * wm * wm * sv;
-      zr[mm] = cv * rr[mm] - sv * ri[mm];
-      zi[mm] = cv * ri[mm] + sv * rr[mm];
+      double sv, cv;
+      sincos(ph[mm], &sv, &cv);
+      sr += cv;
+      si += sv;
     }
-    out[sidx * 3 + 0] = make_float2((float)(ar * k), (float)(ai * k));
-    out[sidx * 3 + 1] = make_float2((float)(br * k), (float)(bi * k));
-    out[sidx * 3 + 2] = make_float2((float)(cr * k), (float)(ci * k));
+    const double k = sqrt(2.0 / 16.0), gn = gains[p];
+    out[0] = make_double2(gn * (sr * k), gn * (si * k));
+    out[1] = out[2] = make_double2(0.0, 0.0);
+    if (phases)
+      for (int mm = 0; mm < 16; ++mm) phases[(size_t)i * 16 + mm] = ph[mm];
+    return;
+  } else {
+    const double k = sqrt(2.0 / 16.0) * (double)gains[p];
+    // per sinusoid: phasor at the first symbol centre, then rotate by w * sym_len
+    // per symbol (float64 recurrence: 2 sincos per sinusoid instead of one per symbol)
+    double w[16], zr[16], zi[16], rr[16], ri[16];
+    const double c0 = fD == 0.0 ? 0.0 : 0.5 * (sym_len - 1);
+    for (int mm = 0; mm < 16; ++mm) {
+      w[mm] = fD == 0.0 ? 0.0 : 6.283185307179586 * fD * cos(6.283185307179586 * (mm + 1) / 16.0) / fs;
+      sincos(w[mm] * c0 + ph[mm], &zi[mm], &zr[mm]);
+      sincos(w[mm] * (double)sym_len, &ri[mm], &rr[mm]);
+    }
+    for (int sidx = 0; sidx < n_cs; ++sidx) {
+      double ar = 0, ai = 0, br = 0, bi = 0, cr = 0, ci = 0;
+      for (int mm = 0; mm < 16; ++mm) {
+        const double cv = zr[mm], sv = zi[mm], wm = w[mm];
+        ar += cv; ai += sv;
+        br += -wm * sv; bi += wm * cv;                   // j w e^{j th}
+        cr += -0.5 * wm * wm * cv; ci += -0.5 * wm * wm * sv;
+        zr[mm] = cv * rr[mm] - sv * ri[mm];
+        zi[mm] = cv * ri[mm] + sv * rr[mm];
+      }
+      out[sidx * 3 + 0] = make_float2((float)(ar * k), (float)(ai * k));
+      out[sidx * 3 + 1] = make_float2((float)(br * k), (float)(bi * k));
+      out[sidx * 3 + 2] = make_float2((float)(cr * k), (float)(ci * k));
+    }
   }
 }
 
+template <class R>
 int launch_fading_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int rayleigh, int n_paths,
-                       const float* gains, double fD, double fs, const uint64_t* fid, uint64_t seed,
-                       const float* inj_ph, int64_t inj_ph_stride, const float* inj_h, int64_t inj_h_stride,
-                       float2* coef) {
+                       const R* gains, double fD, double fs, const uint64_t* fid, uint64_t seed, const R* inj_ph,
+                       int64_t inj_ph_stride, const R* inj_h, int64_t inj_h_stride, cx<R>* coef, R* phases) {
   const int np = rayleigh ? n_paths : 1;
   const int n = B * m.num_rx * m.num_tx * np;
-  hipLaunchKernelGGL(k_fading_mimo, dim3((n + MWG - 1) / MWG), dim3(MWG), 0, s, B, m.num_rx, m.num_tx, np, m.n_cs,
+  if (rayleigh && m.exact_jakes && !phases) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fading_mimo<R>, dim3((n + MWG - 1) / MWG), dim3(MWG), 0, s, B, m.num_rx, m.num_tx, np, m.n_cs,
                      m.mode, rayleigh, gains, fD, fs, g.N + g.cp, fid, seed, inj_ph, inj_ph_stride, inj_h,
-                     inj_h_stride, coef);
+                     inj_h_stride, coef, (rayleigh && m.exact_jakes) ? phases : nullptr);
   return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// Channel.  y_rx[n] = sum_tx sum_p h_{rx,tx,p}(n) x_tx[n - d_p] (stream-level
-// delay with a zero prefix, Q4) + (transmit_mimo Rayleigh only) the link noise
-// of each link's own 100 dB ChannelSimulator (core/ofdm_core.py:490-503:
-// sigma^2 = P_link / 1e10, still drawn).  Power partials -> noise per RX:
-// SFBC (P_rx / num_tx) / SNR (:524-534), spatial P_rx / SNR (channel.py:457-467).
-__device__ __forceinline__ float2 link_sample(const float2* __restrict__ cf, int n_cs, int np, int n, int sym_len,
-                                              const int32_t* __restrict__ delays, const float2* __restrict__ xf) {
+// Channel.  y_rx[n] = sum_tx y_link[n], y_link[n] = sum_p h_{rx,tx,p}(n)
+// x_tx[n - d_p] (stream-level delay with a zero prefix, Q4) + (transmit_mimo
+// Rayleigh only) the link noise of each link's own 100 dB ChannelSimulator
+// (core/ofdm_core.py:490-503: sigma^2 = P_link / 1e10, still drawn).  Power
+// partials -> noise per RX: SFBC (P_rx / num_tx) / SNR (:524-534), spatial
+// P_rx / SNR (channel.py:457-467).  The f64 instances sum each link from zero
+// and then add it to the RX stream, as the reference accumulates signals_rx.
+
+// exact jakes_fading at sample n of a link path (f64): g (sqrt(2/16) sum_m
+// exp(j (w_m t + phi_m))), t = n / fs, in the reference's operation order
+__device__ __noinline__ double2 jakes_exact(const MimoGrid& m, const double (&ph)[16], double gn, int n, double fs) {
+  const double t = (double)n / fs;
+  double sr = 0.0, si = 0.0;
+#pragma unroll
+  for (int mm = 0; mm < 16; ++mm) {
+    double sv, cv;
+    sincos(m.jw[mm] * t + ph[mm], &sv, &cv);
+    sr += cv;
+    si += sv;
+  }
+  const double k = 0.3535533905932738;   // np.sqrt(2 / 16)
+  return make_double2(gn * (sr * k), gn * (si * k));
+}
+
+// one link's output at a single sample n (link_sample: coefficient triples of
+// n's symbol; f64 exact Jakes when ph is set)
+template <class R>
+__device__ __forceinline__ cx<R> link_value(int n, const cx<R>* __restrict__ cf, int n_cs, int np, int sym_len,
+                                            const int32_t* __restrict__ delays, const cx<R>* __restrict__ xf,
+                                            const R* __restrict__ ph, const R* __restrict__ gains, const MimoGrid& m,
+                                            double fs) {
+  using V = cx<R>;
+  V acc = mkc((R)0, (R)0);
+  if constexpr (sizeof(R) == 8) {
+    if (ph) {
+      for (int p = 0; p < np; ++p) {
+        const int src = n - (delays ? delays[p] : 0);
+        if (src < 0) continue;
+        double phv[16];
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
+        acc = cadd(acc, cmul(jakes_exact(m, phv, gains[p], n, fs), xf[src]));
+      }
+      return acc;
+    }
+  }
   const int sidx = n_cs > 1 ? n / sym_len : 0;
-  const float d = n_cs > 1 ? (float)(n - sidx * sym_len) - 0.5f * (float)(sym_len - 1) : 0.f;
-  float2 acc = make_float2(0.f, 0.f);
+  const R d = n_cs > 1 ? (R)(n - sidx * sym_len) - (R)0.5 * (R)(sym_len - 1) : (R)0;
   for (int p = 0; p < np; ++p) {
     const int src = n - (delays ? delays[p] : 0);
     if (src < 0) continue;
-    const float2* c = cf + ((size_t)p * n_cs + sidx) * 3;
-    float2 h = c[0];
+    const V* c = cf + ((size_t)p * n_cs + sidx) * 3;
+    V h = c[0];
     if (n_cs > 1) {   // A + B d + C d^2
       h.x += d * (c[1].x + d * c[2].x);
       h.y += d * (c[1].y + d * c[2].y);
@@ -265,28 +350,42 @@ struct SymSpan {
   }
 };
 
-// acc[j] += sum_p h_p(d_j) x[n_j - delay_p] for one link (cs: the link's
-// coefficients at this symbol, stride n_cs*3 per path)
-template <int J>
-__device__ __forceinline__ void link_accumulate(float2 (&acc)[J], const SymSpan<J>& sp, const float2* __restrict__ cs,
+// acc[j] += sum_p h_p(n_j) x[n_j - delay_p] for one link (cs: the link's
+// coefficients at this symbol, stride n_cs*3 per path; ph: f64 exact Jakes)
+template <class R, int J>
+__device__ __forceinline__ void link_accumulate(cx<R> (&acc)[J], const SymSpan<J>& sp, const cx<R>* __restrict__ cs,
                                                 int n_cs, int np, const int32_t* __restrict__ delays,
-                                                const float2* __restrict__ xf) {
+                                                const cx<R>* __restrict__ xf, const R* __restrict__ ph,
+                                                const R* __restrict__ gains, const MimoGrid& m, double fs) {
+  using V = cx<R>;
   for (int p = 0; p < np; ++p) {
     const int dl = delays ? delays[p] : 0;
-    float2 xs[J];
+    V xs[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int src = sp.n[j] - dl;
-      xs[j] = (sp.ok[j] && src >= 0) ? xf[src] : make_float2(0.f, 0.f);
+      xs[j] = (sp.ok[j] && src >= 0) ? xf[src] : mkc((R)0, (R)0);
     }
-    const float2* c = cs + (size_t)p * n_cs * 3;
-    const float2 c0 = c[0];
+    if constexpr (sizeof(R) == 8) {
+      if (ph) {
+        double phv[16];
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
+        const double gn = gains[p];
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (sp.ok[j] && sp.n[j] >= dl) acc[j] = cadd(acc[j], cmul(jakes_exact(m, phv, gn, sp.n[j], fs), xs[j]));
+        continue;
+      }
+    }
+    const V* c = cs + (size_t)p * n_cs * 3;
+    const V c0 = c[0];
     if (n_cs > 1) {   // A + B d + C d^2
-      const float2 c1 = c[1], c2 = c[2];
+      const V c1 = c[1], c2 = c[2];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        const float dj = sp.d[j];
-        const float2 h = make_float2(c0.x + dj * (c1.x + dj * c2.x), c0.y + dj * (c1.y + dj * c2.y));
+        const R dj = (R)sp.d[j];
+        const V h = mkc(c0.x + dj * (c1.x + dj * c2.x), c0.y + dj * (c1.y + dj * c2.y));
         acc[j] = cadd(acc[j], cmul(h, xs[j]));
       }
     } else {
@@ -296,43 +395,62 @@ __device__ __forceinline__ void link_accumulate(float2 (&acc)[J], const SymSpan<
   }
 }
 
+// the link's 100 dB noise: y + (s z_re + j s z_im) (injected [2][L] or Philox)
+template <class R>
+__device__ __forceinline__ cx<R> link_noise_at(int n, R sg, const R* __restrict__ zf, int L, uint64_t seed,
+                                               uint64_t frame, int link, cx<R> v) {
+  cx<R> z;
+  if (zf) {
+    z = mkc(zf[n], zf[L + n]);
+  } else {
+    const u32x4 rr = rng4(seed, frame, RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
+    z = (n & 1) ? gauss2<R>(rr.z, rr.w) : gauss2<R>(rr.x, rr.y);
+  }
+  return mkc(v.x + sg * z.x, v.y + sg * z.y);
+}
+
 // pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
 // one block per (frame, OFDM symbol, link)
-template <int J>
+template <class R, int J>
 __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
-                                                    const int32_t* __restrict__ delays,
-                                                    const float2* __restrict__ coef, const float2* __restrict__ x,
-                                                    float* __restrict__ part, int nblk) {
-  __shared__ float red[MWG / 64];
+                                                    const int32_t* __restrict__ delays, const cx<R>* __restrict__ coef,
+                                                    const R* __restrict__ phases, const R* __restrict__ gains,
+                                                    double fs, MimoGrid m, const cx<R>* __restrict__ x,
+                                                    R* __restrict__ part, int nblk) {
+  using V = cx<R>;
+  __shared__ R red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
   const int link = blockIdx.y, tx = link % num_tx;
   const int sidx = n_cs > 1 ? blk : 0;
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
   const float dc = 0.5f * (float)(sym_len - 1);
-  const float2* cs = coef + ((size_t)b * num_rx * num_tx + link) * np * n_cs * 3 + (size_t)sidx * 3;
-  const float2* xf = x + ((size_t)b * num_tx + tx) * L;
-  float v = 0.f;
+  const size_t lk = (size_t)b * num_rx * num_tx + link;
+  const V* cs = coef + lk * np * n_cs * 3 + (size_t)sidx * 3;
+  const R* ph = phases ? phases + lk * np * 16 : nullptr;
+  const V* xf = x + ((size_t)b * num_tx + tx) * L;
+  R v = (R)0;
   for (int base = nbeg; base < nend; base += J * MWG) {
     const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
-    float2 acc[J];
+    V acc[J];
 #pragma unroll
-    for (int j = 0; j < J; ++j) acc[j] = make_float2(0.f, 0.f);
-    link_accumulate<J>(acc, sp, cs, n_cs, np, delays, xf);
+    for (int j = 0; j < J; ++j) acc[j] = mkc((R)0, (R)0);
+    link_accumulate<R, J>(acc, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
 #pragma unroll
     for (int j = 0; j < J; ++j)
       if (sp.ok[j]) v += acc[j].x * acc[j].x + acc[j].y * acc[j].y;
   }
-  const float t = block_sum(v, red);
-  if (threadIdx.x == 0) part[((size_t)b * num_rx * num_tx + link) * nblk + blk] = t;
+  const R t = block_sum(v, red);
+  if (threadIdx.x == 0) part[lk * nblk + blk] = t;
 }
 
-__global__ void k_link_sigma(int n_links_total, const float* __restrict__ part, int nblk, int L,
-                             float* __restrict__ sigma) {
+// sigma of the link noise: sqrt((mean|y0|^2 / 10^(100/10)) / 2)
+template <class R>
+__global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int nblk, int L, R* __restrict__ sigma) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_links_total) return;
   double acc = 0.0;
   for (int k = 0; k < nblk; ++k) acc += part[(size_t)i * nblk + k];
-  sigma[i] = (float)sqrt(acc / L / 1e10 * 0.5);
+  sigma[i] = (R)sqrt(((acc / L) / 1e10) / 2.0);
 }
 
 // One block per (frame, OFDM symbol): the symbol index -- hence every link
@@ -344,56 +462,65 @@ __global__ void k_link_sigma(int n_links_total, const float* __restrict__ part, 
 constexpr int MC_MAXRX = 8;   // receive antennas per launch
 constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the transmit streams
 
-template <int J>
+template <class R, int J>
 __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
-                                                      const float2* __restrict__ coef, const float2* __restrict__ x,
-                                                      float2* __restrict__ y, const float* __restrict__ link_sigma,
+                                                      const cx<R>* __restrict__ coef, const R* __restrict__ phases,
+                                                      const R* __restrict__ gains, double fs, MimoGrid m,
+                                                      const cx<R>* __restrict__ x, cx<R>* __restrict__ y,
+                                                      const R* __restrict__ link_sigma,
                                                       const uint64_t* __restrict__ fid, uint64_t seed,
-                                                      const float* __restrict__ inj_lz, int64_t inj_lz_stride,
-                                                      float* __restrict__ pow_part, int nblk) {
-  __shared__ float red[MWG / 64];
+                                                      const R* __restrict__ inj_lz, int64_t inj_lz_stride,
+                                                      R* __restrict__ pow_part, int nblk) {
+  using V = cx<R>;
+  constexpr bool F64 = sizeof(R) == 8;
+  __shared__ R red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;   // blk = OFDM symbol (block of sym_len samples)
   const int sidx = n_cs > 1 ? blk : 0;
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
   const float dc = 0.5f * (float)(sym_len - 1);
   const size_t nl = (size_t)num_rx * num_tx;
   for (int rg = 0; rg < num_rx; rg += MC_RXG) {
-    float pw[MC_RXG];
+    R pw[MC_RXG];
 #pragma unroll
-    for (int q = 0; q < MC_RXG; ++q) pw[q] = 0.f;
+    for (int q = 0; q < MC_RXG; ++q) pw[q] = (R)0;
     for (int base = nbeg; base < nend; base += J * MWG) {
       const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
-      float2 v[MC_RXG][J];
+      V v[MC_RXG][J];
 #pragma unroll
       for (int q = 0; q < MC_RXG; ++q)
 #pragma unroll
-        for (int j = 0; j < J; ++j) v[q][j] = make_float2(0.f, 0.f);
+        for (int j = 0; j < J; ++j) v[q][j] = mkc((R)0, (R)0);
       for (int tx = 0; tx < num_tx; ++tx) {
-        const float2* xf = x + ((size_t)b * num_tx + tx) * L;
+        const V* xf = x + ((size_t)b * num_tx + tx) * L;
 #pragma unroll
         for (int q = 0; q < MC_RXG; ++q) {
           const int r = rg + q;
           if (r >= num_rx) break;
-          const size_t link = (size_t)r * num_tx + tx;
-          link_accumulate<J>(v[q], sp, coef + ((size_t)b * nl + link) * np * n_cs * 3 + (size_t)sidx * 3, n_cs, np,
-                             delays, xf);
-          if (link_sigma) {   // the link's own ChannelSimulator noise
-            const float sg = link_sigma[(size_t)b * nl + link];
+          const size_t link = (size_t)r * num_tx + tx, lk = (size_t)b * nl + link;
+          const V* cs = coef + lk * np * n_cs * 3 + (size_t)sidx * 3;
+          const R* ph = phases ? phases + lk * np * 16 : nullptr;
+          const R* zf = inj_lz ? inj_lz + (size_t)b * inj_lz_stride + link * 2 * L : nullptr;
+          if constexpr (F64) {   // y_link from zero, then signals_rx += y_link
+            V vl[J];
 #pragma unroll
-            for (int j = 0; j < J; ++j) {
-              const int n = sp.n[j];
-              float2 z = make_float2(0.f, 0.f);
-              if (sp.ok[j]) {
-                if (inj_lz) {
-                  const float* zf = inj_lz + (size_t)b * inj_lz_stride + link * 2 * L;
-                  z = make_float2(zf[n], zf[L + n]);
-                } else {
-                  const u32x4 rr = rng4(seed, fid[b], RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
-                  z = (n & 1) ? box_muller(rr.z, rr.w) : box_muller(rr.x, rr.y);
-                }
-              }
-              v[q][j] = make_float2(v[q][j].x + sg * z.x, v[q][j].y + sg * z.y);
+            for (int j = 0; j < J; ++j) vl[j] = mkc((R)0, (R)0);
+            link_accumulate<R, J>(vl, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
+            if (link_sigma) {
+              const R sg = link_sigma[lk];
+#pragma unroll
+              for (int j = 0; j < J; ++j)
+                if (sp.ok[j]) vl[j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], (int)link, vl[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) v[q][j] = cadd(v[q][j], vl[j]);
+          } else {
+            link_accumulate<R, J>(v[q], sp, cs, n_cs, np, delays, xf, nullptr, gains, m, fs);
+            if (link_sigma) {
+              const R sg = link_sigma[lk];
+#pragma unroll
+              for (int j = 0; j < J; ++j)
+                if (sp.ok[j]) v[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], (int)link, v[q][j]);
             }
           }
         }
@@ -414,7 +541,7 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
     for (int q = 0; q < MC_RXG; ++q) {
       const int r = rg + q;
       if (r >= num_rx) break;
-      const float t = block_sum(pw[q], red);
+      const R t = block_sum(pw[q], red);
       if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
       __syncthreads();
     }
@@ -423,29 +550,33 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
 
 int mimo_channel_nblk(int L, int sym_len) { return (L + sym_len - 1) / sym_len; }
 
+template <class R>
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
-                        const float2* coef, const float2* x, float2* y, int link_noise, const uint64_t* fid,
-                        uint64_t seed, const float* inj_lz, int64_t inj_lz_stride, float* link_part,
-                        float* link_sigma, float* pow_part, int nblk) {
+                        const cx<R>* coef, const R* phases, const R* gains, double fs, const cx<R>* x, cx<R>* y,
+                        int link_noise, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
+                        R* link_part, R* link_sigma, R* pow_part, int nblk) {
   const int sym_len = g.N + g.cp;
   if (m.num_rx > MC_MAXRX) return (int)hipErrorInvalidValue;
   const int nch = mimo_channel_nblk(g.L, sym_len);
   if (nch > nblk) return (int)hipErrorInvalidValue;   // partial buffers are sized for nblk blocks
+  const R* ph = m.exact_jakes ? phases : nullptr;
+  if (m.exact_jakes && (!phases || !gains)) return (int)hipErrorInvalidValue;
   // samples per thread per pass: the smallest instantiated J covering one symbol (larger symbols loop)
   const int jn = (sym_len + MWG - 1) / MWG;
   const int J = jn <= 1 ? 1 : jn <= 2 ? 2 : jn <= 3 ? 3 : jn <= 5 ? 5 : jn <= 7 ? 7 : 9;
 #define LTE_CHM(J_)                                                                                                 \
   do {                                                                                                             \
     if (link_noise) {                                                                                              \
-      hipLaunchKernelGGL(k_link_power<J_>, dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx,     \
-                         m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, x, link_part, nch);                     \
+      hipLaunchKernelGGL((k_link_power<R, J_>), dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L,          \
+                         m.num_rx, m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x,          \
+                         link_part, nch);                                                                          \
       const int nl = B * m.num_rx * m.num_tx;                                                                      \
-      hipLaunchKernelGGL(k_link_sigma, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L,          \
+      hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L,        \
                          link_sigma);                                                                              \
     }                                                                                                              \
-    hipLaunchKernelGGL(k_channel_mimo<J_>, dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths,       \
-                       m.n_cs, sym_len, delays, coef, x, y, link_noise ? link_sigma : nullptr, fid, seed, inj_lz,  \
-                       inj_lz_stride, pow_part, nch);                                                              \
+    hipLaunchKernelGGL((k_channel_mimo<R, J_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths,  \
+                       m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x, y, link_noise ? link_sigma : nullptr,   \
+                       fid, seed, inj_lz, inj_lz_stride, pow_part, nch);                                           \
   } while (0)
   switch (J) {
     case 1: LTE_CHM(1); break;
@@ -460,65 +591,86 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
 }
 
 // Per-link statistics for the reported channel matrix (transmit_mimo,
-// core/ofdm_core.py:505-516): mean|x|^2, mean|y_link|^2, mean(y_link conj(x)).
+// core/ofdm_core.py:505-516): mean|x|^2, mean|y_link|^2, mean(y_link conj(x)),
+// y_link with its link noise when link_sigma is set (the reference's y).
+template <class R>
 __global__ __launch_bounds__(MWG) void k_link_stats_part(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                          const int32_t* __restrict__ delays,
-                                                         const float2* __restrict__ coef,
-                                                         const float2* __restrict__ x, float* __restrict__ part,
-                                                         int nblk) {
-  __shared__ float red[MWG / 64];
+                                                         const cx<R>* __restrict__ coef, const R* __restrict__ phases,
+                                                         const R* __restrict__ gains, double fs, MimoGrid m,
+                                                         const cx<R>* __restrict__ x,
+                                                         const R* __restrict__ link_sigma,
+                                                         const uint64_t* __restrict__ fid, uint64_t seed,
+                                                         const R* __restrict__ inj_lz, int64_t inj_lz_stride,
+                                                         R* __restrict__ part, int nblk) {
+  using V = cx<R>;
+  __shared__ R red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
   const int link = blockIdx.y, rx = link / num_tx, tx = link - rx * num_tx;
   const int n = blk * MWG + threadIdx.x;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  const size_t lk = ((size_t)b * num_rx + rx) * num_tx + tx;
+  R v[4] = {(R)0, (R)0, (R)0, (R)0};
   if (n < L) {
-    const float2* xf = x + ((size_t)b * num_tx + tx) * L;
-    const float2* cf = coef + (((size_t)b * num_rx + rx) * num_tx + tx) * np * n_cs * 3;
-    const float2 yv = link_sample(cf, n_cs, np, n, sym_len, delays, xf), xv = xf[n];
+    const V* xf = x + ((size_t)b * num_tx + tx) * L;
+    const V* cf = coef + lk * np * n_cs * 3;
+    V yv = link_value<R>(n, cf, n_cs, np, sym_len, delays, xf, phases ? phases + lk * np * 16 : nullptr, gains, m, fs);
+    if (link_sigma) {
+      const R* zf = inj_lz ? inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L : nullptr;
+      yv = link_noise_at<R>(n, link_sigma[lk], zf, L, seed, fid[b], link, yv);
+    }
+    const V xv = xf[n];
     v[0] = xv.x * xv.x + xv.y * xv.y;
     v[1] = yv.x * yv.x + yv.y * yv.y;
-    const float2 c = cmulc(yv, xv);
+    const V c = cmulc(yv, xv);
     v[2] = c.x;
     v[3] = c.y;
   }
   for (int q = 0; q < 4; ++q) {
-    const float t = block_sum(v[q], red);
+    const R t = block_sum(v[q], red);
     if (threadIdx.x == 0) part[((((size_t)b * num_rx * num_tx) + link) * 4 + q) * nblk + blk] = t;
     __syncthreads();
   }
 }
 
-__global__ void k_link_stats_fin(int n, const float* __restrict__ part, int nblk, int L, float* __restrict__ stats) {
+template <class R>
+__global__ void k_link_stats_fin(int n, const R* __restrict__ part, int nblk, int L, R* __restrict__ stats) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double acc = 0.0;
   for (int k = 0; k < nblk; ++k) acc += part[(size_t)i * nblk + k];
-  stats[i] = (float)(acc / L);
+  stats[i] = (R)(acc / L);
 }
 
+template <class R>
 int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
-                      const float2* coef, const float2* x, float* part, int nblk, float* stats) {
-  hipLaunchKernelGGL(k_link_stats_part, dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx,
-                     m.num_tx, n_paths, m.n_cs, g.N + g.cp, delays, coef, x, part, nblk);
+                      const cx<R>* coef, const R* phases, const R* gains, double fs, const cx<R>* x,
+                      const R* link_sigma, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
+                      R* part, int nblk, R* stats) {
+  if (nblk < (g.L + MWG - 1) / MWG) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_link_stats_part<R>, dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx,
+                     m.num_tx, n_paths, m.n_cs, g.N + g.cp, delays, coef, m.exact_jakes ? phases : nullptr, gains, fs,
+                     m, x, link_sigma, fid, seed, inj_lz, inj_lz_stride, part, nblk);
   const int n = B * m.num_rx * m.num_tx * 4;
-  hipLaunchKernelGGL(k_link_stats_fin, dim3((n + 255) / 256), dim3(256), 0, s, n, part, nblk, g.L, stats);
+  hipLaunchKernelGGL(k_link_stats_fin<R>, dim3((n + 255) / 256), dim3(256), 0, s, n, part, nblk, g.L, stats);
   return (int)hipGetLastError();
 }
 
-__global__ void k_npow_mimo(int n, const float* __restrict__ pow_part, int nblk, int L, const float* __restrict__ snr_lin,
-                            int num_rx, float norm, float* __restrict__ npow) {
+template <class R>
+__global__ void k_npow_mimo(int n, const R* __restrict__ pow_part, int nblk, int L, const R* __restrict__ snr_lin,
+                            int num_rx, double div, R* __restrict__ npow) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double acc = 0.0;
   for (int k = 0; k < nblk; ++k) acc += pow_part[(size_t)i * nblk + k];
-  npow[i] = (float)(acc / L * norm / snr_lin[i / num_rx]);
+  npow[i] = (R)(((acc / L) / div) / (double)snr_lin[i / num_rx]);
 }
 
-int launch_npow_mimo(hipStream_t s, int B, int num_rx, const float* pow_part, int nblk, int L, const float* snr_lin,
-                     float norm, float* npow) {
+template <class R>
+int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nblk, int L, const R* snr_lin,
+                     double div, R* npow) {
   const int n = B * num_rx;
-  hipLaunchKernelGGL(k_npow_mimo, dim3((n + 255) / 256), dim3(256), 0, s, n, pow_part, nblk, L, snr_lin, num_rx,
-                     norm, npow);
+  hipLaunchKernelGGL(k_npow_mimo<R>, dim3((n + 255) / 256), dim3(256), 0, s, n, pow_part, nblk, L, snr_lin, num_rx,
+                     div, npow);
   return (int)hipGetLastError();
 }
 
@@ -529,56 +681,60 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const float* pow_part, in
 // Y[b][l][rx][n_dsc].  On estimation symbols (SFBC: first of each 14-symbol
 // group, :195-234; spatial: every symbol, core/ofdm_core.py:2752) LS at each
 // TX's pilot subset + linear interpolation with edge hold (:108-185 +
-// lte_receiver.py:98-133) at the data SCs -> H[b][rx][e][tx][n_dsc].
-__global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const float2* __restrict__ y,
-                                                     const float* __restrict__ npow, const uint64_t* __restrict__ fid,
-                                                     uint64_t seed, const float* __restrict__ inj_z,
-                                                     int64_t inj_stride, float2* __restrict__ Y,
-                                                     float2* __restrict__ H) {
-  extern __shared__ float2 sm[];
+// lte_receiver.py:98-133: np.linspace, k (delta / gap) + start) at the data
+// SCs -> H[b][rx][e][tx][n_dsc].
+template <class R>
+__global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
+                                                     const R* __restrict__ npow, const uint64_t* __restrict__ fid,
+                                                     uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride,
+                                                     cx<R>* __restrict__ Y, cx<R>* __restrict__ H) {
+  using V = cx<R>;
+  V* sm = mimo_lds<V>();
   const int N = g.N, T = N >> 3, spw = MWG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int per = m.num_rx * g.n_sym;
   const int gs = blockIdx.x * spw + slot;
   const int b = gs / per, r = gs - b * per, rx = r / g.n_sym, l = r - rx * g.n_sym;
   const bool active = slot < spw && b < B;
-  float2* buf = sm + slot * N;
-  float2* hp = sm + spw * N + slot * (m.num_tx * m.maxP);
+  V* buf = sm + slot * N;
+  V* hp = sm + spw * N + slot * (m.num_tx * m.maxP);
   if (active) {
-    const float sigma = sqrtf(npow[(size_t)b * m.num_rx + rx] * 0.5f);
-    const float* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+    const R sigma = sqrt(npow[(size_t)b * m.num_rx + rx] * (R)0.5);
+    const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
     load_symbol_noisy2(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf, g.L, tid,
                        T);
   }
   __syncthreads();
-  fft_lds<false>(buf, N, g.log2N, g.tw, tid, active);
+  fft_lds<false>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
   const int e = m.mode == MIMO_SFBC ? l / 14 : l;
   const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
-  const float sc = rsqrtf((float)N);
+  const R sc = rx_scale<R>(N);
+  const V* pv = MGT<R>::pval(m);
   if (active && est) {
     for (int t = 0; t < m.num_tx; ++t)
       for (int p = tid; p < m.np_tx[t]; p += T)
-        hp[t * m.maxP + p] = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), m.pval[t * m.maxP + p]);
+        hp[t * m.maxP + p] = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), pv[t * m.maxP + p]);
   }
   __syncthreads();
   if (active) {
-    float2* Yo = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
+    V* Yo = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
     for (int j = tid; j < m.n_dsc; j += T) Yo[j] = cscale(buf[g.data_idx[j]], sc);
     if (est) {
+      const R* pig = MGT<R>::pig(m);
       for (int t = 0; t < m.num_tx; ++t) {
-        const float2* hpt = hp + t * m.maxP;
+        const V* hpt = hp + t * m.maxP;
         const int npt = m.np_tx[t];
-        float2* Ho = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + t) * m.n_dsc;
+        V* Ho = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + t) * m.n_dsc;
         for (int j = tid; j < m.n_dsc; j += T) {
           const int sidx = m.pseg[t * m.n_dsc + j];
-          float2 h;
+          V h;
           if (sidx < 0) h = hpt[0];
           else if (sidx >= npt - 1) h = hpt[npt - 1];
           else {
-            const float2 v0 = hpt[sidx], v1 = hpt[sidx + 1];
-            const float fk = (float)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
-            const float ig = m.pig[t * m.maxP + sidx];
-            h = make_float2(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+            const V v0 = hpt[sidx], v1 = hpt[sidx + 1];
+            const R fk = (R)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
+            const R ig = pig[t * m.maxP + sidx];
+            h = mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
           }
           Ho[j] = h;
         }
@@ -587,15 +743,15 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
   }
 }
 
-int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* y, const float* npow,
-                       const uint64_t* fid, uint64_t seed, const float* inj_z, int64_t inj_stride, float2* Y,
-                       float2* H) {
+template <class R>
+int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
+                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H) {
   const int spw = MWG / (g.N >> 3);
   const int64_t total = (int64_t)B * m.num_rx * g.n_sym;
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
-  const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(float2);
-  hipLaunchKernelGGL(k_rx_fft_mimo, dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z, inj_stride,
+  const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(cx<R>);
+  hipLaunchKernelGGL(k_rx_fft_mimo<R>, dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z, inj_stride,
                      Y, H);
   return (int)hipGetLastError();
 }
@@ -603,18 +759,24 @@ int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, c
 // ---------------------------------------------------------------------------
 // SFBC detection.  One thread per (frame, OFDM symbol, SC pair).
 // SFBCAlamouti.decode (core/sfbc_alamouti.py:80-163) per RX with that RX's
-// slot estimate, averaged over RX (core/ofdm_core.py:2204, Q17).  Uncoded:
+// slot estimate, averaged over RX (core/ofdm_core.py:2204, Q17).  f64 in the
+// reference's NumPy complex128 scalar semantics: s0 = conj(h0k) rk + h1k1
+// conj(rk1), norm = |avg(h0)|**2 + |avg(h1)|**2 + 1e-10 with |z| = hypot,
+// s / norm = s * (1 / norm) (complex / real divides by Smith's rule with a
+// zero imaginary part), the RX mean (sum_r d_r) * (1 / num_rx).  Uncoded:
 // nearest-point hard bits vs the payload (bit errors).  Coded (config 4):
 // max-log LLRs (core/ofdm_core.py:791-923) with the per-RE noise variance of
 // the combined estimate, sigma^2 / R^2 * sum_r 1 / clip(norm_r, 1e-6, 1e6),
 // floored at sigma^2 / 4 as in the SISO rule (ofdm_core.py:1224-1243) -- the
 // reference has no coded SFBC chain; DESIGN.md documents this composition.
-template <int CODED, int BPS>
-__global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, const float2* __restrict__ Y,
-                                                  const float2* __restrict__ H, const float* __restrict__ snr_lin,
+template <class R, int CODED, int BPS>
+__global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
+                                                  const cx<R>* __restrict__ H, const R* __restrict__ snr_lin,
                                                   const uint32_t* __restrict__ pw, int PW, int n_bits,
-                                                  uint32_t* __restrict__ frame_err, float* __restrict__ llr,
-                                                  float2* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+                                                  uint32_t* __restrict__ frame_err, R* __restrict__ llr,
+                                                  cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+  using V = cx<R>;
+  constexpr bool F64 = sizeof(R) == 8;
   const int npair = m.n_dsc >> 1;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t per = (int64_t)g.n_sym * npair;
@@ -624,37 +786,46 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
   const int b = act ? (int)(i / per) : B - 1;
   const int rem = act ? (int)(i - (int64_t)b * per) : 0, l = rem / npair, pr = rem - l * npair, j = 2 * pr;
   const int e = l / 14;
-  float2 z0 = make_float2(0.f, 0.f), z1 = make_float2(0.f, 0.f);
-  float inv_g = 0.f;
+  V z0 = mkc((R)0, (R)0), z1 = mkc((R)0, (R)0);
+  R inv_g = (R)0;
   for (int rx = 0; rx < m.num_rx; ++rx) {
-    const float2* Yr = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
-    const float2* H0 = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + 0) * m.n_dsc;
-    const float2* H1 = H0 + m.n_dsc;
-    const float2 rk = Yr[j], rk1 = Yr[j + 1];
-    const float2 h0k = H0[j], h1k = H1[j], h0k1 = H0[j + 1], h1k1 = H1[j + 1];
-    const float2 rc = make_float2(rk1.x, -rk1.y);
-    const float2 s0 = cadd(cmulc(rk, h0k), cmul(h1k1, rc));      // conj(h0k) rk + h1k1 conj(rk1)
-    const float2 s1 = csub(cmulc(rk, h1k), cmul(h0k1, rc));      // conj(h1k) rk - h0k1 conj(rk1)
-    const float2 a0 = make_float2(0.5f * (h0k.x + h0k1.x), 0.5f * (h0k.y + h0k1.y));
-    const float2 a1 = make_float2(0.5f * (h1k.x + h1k1.x), 0.5f * (h1k.y + h1k1.y));
-    const float nrm = (a0.x * a0.x + a0.y * a0.y) + (a1.x * a1.x + a1.y * a1.y) + 1e-10f;
-    z0 = make_float2(z0.x + s0.x / nrm, z0.y + s0.y / nrm);
-    z1 = make_float2(z1.x + s1.x / nrm, z1.y + s1.y / nrm);
-    inv_g += 1.0f / fminf(fmaxf(nrm, 1e-6f), 1e6f);
+    const V* Yr = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
+    const V* H0 = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + 0) * m.n_dsc;
+    const V* H1 = H0 + m.n_dsc;
+    const V rk = Yr[j], rk1 = Yr[j + 1];
+    const V h0k = H0[j], h1k = H1[j], h0k1 = H0[j + 1], h1k1 = H1[j + 1];
+    const V rc = mkc(rk1.x, -rk1.y);
+    const V s0 = cadd(cmulc(rk, h0k), cmul(h1k1, rc));      // conj(h0k) rk + h1k1 conj(rk1)
+    const V s1 = csub(cmulc(rk, h1k), cmul(h0k1, rc));      // conj(h1k) rk - h0k1 conj(rk1)
+    const V a0 = mkc((R)0.5 * (h0k.x + h0k1.x), (R)0.5 * (h0k.y + h0k1.y));
+    const V a1 = mkc((R)0.5 * (h1k.x + h1k1.x), (R)0.5 * (h1k.y + h1k1.y));
+    if constexpr (F64) {
+      const double n0 = hypot(a0.x, a0.y), n1 = hypot(a1.x, a1.y);
+      const double nrm = (n0 * n0 + n1 * n1) + 1e-10;
+      const double rn = 1.0 / nrm;
+      z0 = cadd(z0, make_double2(s0.x * rn, s0.y * rn));
+      z1 = cadd(z1, make_double2(s1.x * rn, s1.y * rn));
+      inv_g += 1.0 / fmin(fmax(nrm, 1e-6), 1e6);
+    } else {
+      const float nrm = (a0.x * a0.x + a0.y * a0.y) + (a1.x * a1.x + a1.y * a1.y) + 1e-10f;
+      z0 = make_float2(z0.x + s0.x / nrm, z0.y + s0.y / nrm);
+      z1 = make_float2(z1.x + s1.x / nrm, z1.y + s1.y / nrm);
+      inv_g += 1.0f / fminf(fmaxf(nrm, 1e-6f), 1e6f);
+    }
   }
-  const float ir = 1.0f / (float)m.num_rx;
-  z0 = make_float2(z0.x * ir, z0.y * ir);
-  z1 = make_float2(z1.x * ir, z1.y * ir);
+  const R ir = (R)1 / (R)m.num_rx;
+  z0 = mkc(z0.x * ir, z0.y * ir);
+  z1 = mkc(z1.x * ir, z1.y * ir);
   const int64_t re = (int64_t)l * m.res + j;
   if (cap_syms && act) {
     cap_syms[(size_t)b * g.n_sym * m.res + re] = z0;
     cap_syms[(size_t)b * g.n_sym * m.res + re + 1] = z1;
   }
   if constexpr (CODED) {
-    const float s2 = 1.0f / snr_lin[b];
-    const float nv = fmaxf(s2 * ir * ir * inv_g, s2 * 0.25f);
-    float o[BPS];
-    float* lo = llr + ((size_t)b * g.n_sym * m.res + re) * BPS;
+    const R s2 = (R)1 / snr_lin[b];
+    const R nv = F64 ? fmax((s2 / (R)(m.num_rx * m.num_rx)) * inv_g, s2 / (R)4) : fmax(s2 * ir * ir * inv_g, s2 * (R)0.25);
+    R o[BPS];
+    R* lo = llr + ((size_t)b * g.n_sym * m.res + re) * BPS;
     if (!act) return;
     soft_demap<BPS>(z0, nv, o);
 #pragma unroll
@@ -666,7 +837,7 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
     const uint32_t* fb = pw + (size_t)b * PW;
     uint32_t errs = 0;
     for (int h = 0; h < 2; ++h) {
-      const int idx = hard_index(h ? z1 : z0, BPS, (float)qam_norm<BPS>());
+      const int idx = hard_index(h ? z1 : z0, BPS, (R)qam_norm<BPS>());
 #pragma unroll
       for (int q = 0; q < BPS; ++q) {
         const int64_t pbit = (re + h) * BPS + q;
@@ -681,15 +852,16 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
   }
 }
 
-int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const float2* Y,
-                    const float2* H, const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                    float* llr, float2* cap_syms, uint8_t* cap_bits) {
+template <class R>
+int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const cx<R>* Y,
+                    const cx<R>* H, const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits) {
   (void)rayleigh;
   const int64_t n = (int64_t)B * g.n_sym * (m.n_dsc >> 1);
   const dim3 grid((unsigned)((n + MWG - 1) / MWG));
 #define LTE_DS(C_, B_) \
-  hipLaunchKernelGGL((k_det_sfbc<C_, B_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits, frame_err, \
-                     llr, cap_syms, cap_bits)
+  hipLaunchKernelGGL((k_det_sfbc<R, C_, B_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits, \
+                     frame_err, llr, cap_syms, cap_bits)
   if (coded) {
     if (g.bps == 2) LTE_DS(1, 2); else if (g.bps == 4) LTE_DS(1, 4); else LTE_DS(1, 6);
   } else {
@@ -890,12 +1062,13 @@ __device__ __forceinline__ void detect_sc(const dc (&He)[DMAX][DMAX], const dc (
     if (l >= R) sv[l] = {0.0, 0.0};
 }
 
-template <int BPS, bool SIC_ON>
-__global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, const float2* __restrict__ Y,
-                                                     const float2* __restrict__ H, const float* __restrict__ snr_lin,
+template <class R, int BPS, bool SIC_ON>
+__global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
+                                                     const cx<R>* __restrict__ H, const R* __restrict__ snr_lin,
                                                      const uint32_t* __restrict__ pw, int PW, int n_bits,
-                                                     uint32_t* __restrict__ frame_err, float2* __restrict__ cap_syms,
+                                                     uint32_t* __restrict__ frame_err, cx<R>* __restrict__ cap_syms,
                                                      uint8_t* __restrict__ cap_bits) {
+  using V = cx<R>;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t per = (int64_t)g.n_sym * m.n_dsc;
   // lanes past the batch stay in the wave (convergent error reduction) and
@@ -903,7 +1076,7 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
   const bool act = i < (int64_t)B * per;
   const int b = act ? (int)(i / per) : B - 1;
   const int rem = act ? (int)(i - (int64_t)b * per) : 0, l = rem / m.n_dsc, j = rem - l * m.n_dsc;
-  const int NR = m.num_rx, NT = m.num_tx, R = m.rank;
+  const int NR = m.num_rx, NT = m.num_tx, R_ = m.rank;
   dc He[DMAX][DMAX], yv[DMAX];
 #pragma unroll
   for (int r = 0; r < DMAX; ++r) {
@@ -911,30 +1084,30 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
 #pragma unroll
     for (int c = 0; c < DMAX; ++c) He[r][c] = {0.0, 0.0};
     if (r < NR) {
-      const float2 v = Y[(((size_t)b * g.n_sym + l) * NR + r) * m.n_dsc + j];
-      yv[r] = {v.x, v.y};
-      const float2* Hr = H + (((size_t)b * NR + r) * m.n_est + l) * NT * m.n_dsc + j;
+      const V v = Y[(((size_t)b * g.n_sym + l) * NR + r) * m.n_dsc + j];
+      yv[r] = {(double)v.x, (double)v.y};
+      const V* Hr = H + (((size_t)b * NR + r) * m.n_est + l) * NT * m.n_dsc + j;
       for (int t = 0; t < NT; ++t) {                 // He[r][c] = sum_t H[r][t] W[t][c]
-        const float2 hv = Hr[(size_t)t * m.n_dsc];
-        const dc h = {hv.x, hv.y};
+        const V hv = Hr[(size_t)t * m.n_dsc];
+        const dc h = {(double)hv.x, (double)hv.y};
 #pragma unroll
         for (int c = 0; c < DMAX; ++c)
-          if (c < R) He[r][c] = dadd(He[r][c], dmul(h, dc{m.W[(t * DMAX + c) * 2], m.W[(t * DMAX + c) * 2 + 1]}));
+          if (c < R_) He[r][c] = dadd(He[r][c], dmul(h, dc{m.W[(t * DMAX + c) * 2], m.W[(t * DMAX + c) * 2 + 1]}));
       }
     }
   }
   dc sv[DMAX];
-  detect_sc<SIC_ON>(He, yv, R, m.det, 1.0 / (double)snr_lin[b], BPS, sv);
+  detect_sc<SIC_ON>(He, yv, R_, m.det, 1.0 / (double)snr_lin[b], BPS, sv);
   const uint32_t* fb = pw + (size_t)b * PW;
   uint32_t errs = 0;
 #pragma unroll
   for (int t = 0; t < DMAX; ++t) {
-    const int qi = R * j + t;
-    if (t >= R || qi >= m.res) break;
-    const float2 z = make_float2((float)sv[t].x, (float)sv[t].y);
+    const int qi = R_ * j + t;
+    if (t >= R_ || qi >= m.res) break;
+    const V z = mkc((R)sv[t].x, (R)sv[t].y);
     const int64_t re = (int64_t)l * m.res + qi;
     if (cap_syms && act) cap_syms[(size_t)b * g.n_sym * m.res + re] = z;
-    const int idx = hard_index(z, BPS, (float)qam_norm<BPS>());
+    const int idx = hard_index(z, BPS, (R)qam_norm<BPS>());
 #pragma unroll
     for (int q = 0; q < BPS; ++q) {
       const int64_t pbit = re * BPS + q;
@@ -948,16 +1121,17 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
   frame_err_add(frame_err, b, errs);
 }
 
-int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const float2* Y, const float2* H,
-                       const float* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                       float2* cap_syms, uint8_t* cap_bits) {
+template <class R>
+int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* Y, const cx<R>* H,
+                       const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                       cx<R>* cap_syms, uint8_t* cap_bits) {
   if (m.num_tx < 1 || m.num_tx > DMAX || m.num_rx < 1 || m.num_rx > DMAX || m.rank < 1 || m.rank > m.num_rx ||
       m.rank > m.num_tx || !m.W)
     return (int)hipErrorInvalidValue;
   const int64_t n = (int64_t)B * g.n_sym * m.n_dsc;
   const dim3 grid((unsigned)((n + MWG - 1) / MWG));
 #define LTE_DSP(B_, S_)                                                                                            \
-  hipLaunchKernelGGL((k_det_spatial<B_, S_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits,        \
+  hipLaunchKernelGGL((k_det_spatial<R, B_, S_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits,     \
                      frame_err, cap_syms, cap_bits)
   const bool sic = m.det == LTE_DET_SIC;
   if (g.bps == 2) { if (sic) LTE_DSP(2, true); else LTE_DSP(2, false); }
@@ -1006,5 +1180,30 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
                      H, W, s2, out);
   return (int)hipGetLastError();
 }
+
+// explicit instances: float (fast mode) and double (the reference's precision)
+#define LTE_MIMO_INST(R)                                                                                           \
+  template int launch_ofdm_tx_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,       \
+                                      const uint32_t*, int, const int32_t*, cx<R>*, int);                          \
+  template int launch_fading_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const R*, double,   \
+                                     double, const uint64_t*, uint64_t, const R*, int64_t, const R*, int64_t,      \
+                                     cx<R>*, R*);                                                                  \
+  template int launch_channel_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const int32_t*,         \
+                                      const cx<R>*, const R*, const R*, double, const cx<R>*, cx<R>*, int,         \
+                                      const uint64_t*, uint64_t, const R*, int64_t, R*, R*, R*, int);              \
+  template int launch_link_stats<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const int32_t*,           \
+                                    const cx<R>*, const R*, const R*, double, const cx<R>*, const R*,              \
+                                    const uint64_t*, uint64_t, const R*, int64_t, R*, int, R*);                    \
+  template int launch_npow_mimo<R>(hipStream_t, int, int, const R*, int, int, const R*, double, R*);               \
+  template int launch_rx_fft_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const R*,       \
+                                     const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*);                \
+  template int launch_det_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const cx<R>*,          \
+                                  const cx<R>*, const R*, const uint32_t*, int, int, uint32_t*, R*, cx<R>*,        \
+                                  uint8_t*);                                                                       \
+  template int launch_det_spatial<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const cx<R>*,   \
+                                     const R*, const uint32_t*, int, int, uint32_t*, cx<R>*, uint8_t*);
+LTE_MIMO_INST(float)
+LTE_MIMO_INST(double)
+#undef LTE_MIMO_INST
 
 }  // namespace lte

@@ -51,7 +51,7 @@ class RunArgs(ctypes.Structure):
                 ('cap_tx_syms', ctypes.c_void_p),
                 ('link_noise', P(c_f64)), ('link_noise_stride', c_i64),
                 ('link_h', P(c_f64)), ('link_h_stride', c_i64),
-                ('cap_link_stats', P(ctypes.c_float)),
+                ('cap_link_stats', ctypes.c_void_p),
                 ('cap_pmi', P(c_i32)), ('cap_bf_gain', P(ctypes.c_float))]
 
 
@@ -105,6 +105,10 @@ _SIGS = {
                                              ctypes.c_int, P(c_i32), P(c_f64), c_f64, c_f64, c_f64, c_u64,
                                              P(ctypes.c_float), P(c_f64), P(c_f64), P(c_f64), P(c_f64),
                                              P(ctypes.c_float), P(ctypes.c_float), P(ctypes.c_float)]),
+    'lte_channel_mimo_host64': (ctypes.c_int, [c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, P(c_i32), P(c_f64), c_f64, c_f64, c_f64, c_u64,
+                                               P(c_f64), P(c_f64), P(c_f64), P(c_f64), P(c_f64),
+                                               P(c_f64), P(c_f64), P(c_f64)]),
 }
 
 _lib = None

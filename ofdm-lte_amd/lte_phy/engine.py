@@ -34,11 +34,10 @@ class Plan:
         d.num_tx = int(num_tx)
         d.rank, d.detector, d.sc_fdm, d.bf_adaptive = int(rank), int(detector), int(sc_fdm), int(bf_adaptive)
         d.no_equalization = int(no_equalization)
-        # SISO / SIMO chains: float64 (the reference's arithmetic) unless 'f32' is
-        # asked for; the multi-antenna / beamforming chains run float32
-        multi = chain >= C.CHAIN_SFBC
-        d.precision = C.PREC_DEFAULT if multi else (C.PREC_F64 if C.precision_of(precision) == 'f64'
-                                                     else C.PREC_F32)
+        # float64 (the reference's arithmetic) unless 'f32' is asked for; the
+        # beamforming chain runs float32
+        bf = chain == C.CHAIN_BEAMFORMING
+        d.precision = C.PREC_DEFAULT if bf else (C.PREC_F64 if C.precision_of(precision) == 'f64' else C.PREC_F32)
         if rank and num_tx <= 4 and rank <= 4:   # W [num_tx][rank] -> the [4][4] table of lte_plan_desc.precoder
             #                                    (larger arrays: lte_plan_create rejects them, LTE_EUNSUP)
             W = np.asarray(precoder, dtype=np.complex128).reshape(int(num_tx), int(rank))
@@ -159,7 +158,7 @@ class Plan:
                 'signal_tx': ((B, self.num_tx, self.L), cdt, 'cap_signal_tx', None),
                 'data_syms': ((B, self.n_sym * self.res), cdt, 'cap_data_syms', None),
                 'H': ((B, self.num_rx, self.n_est, self.num_tx, self.n_dsc), cdt, 'cap_H', None),
-                'link_stats': ((B, self.num_rx, self.num_tx, 4), np.float32, 'cap_link_stats', C.F32)})
+                'link_stats': ((B, self.num_rx, self.num_tx, 4), rdt, 'cap_link_stats', None)})
             shapes.pop('pilot_stats')
             shapes.pop('tx_syms')
         if self.bf:

@@ -276,7 +276,11 @@ class OFDMChannel:
     'rayleigh_mp' is AWGN, as in the reference (:322-332)."""
 
     def __init__(self, channel_type: str = 'awgn', snr_db: float = 10.0, fs: float = 15.36e6,
-                 itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0):
+                 itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0,
+                 *, precision: Optional[str] = None):
+        """precision (not in the reference): arithmetic type of the device channel,
+        'f64' (default, LTE_PRECISION when unset) or 'f32'; OFDMSimulator passes its own."""
+        self.precision = C.precision_of(precision)
         self.channel_type, self.snr_db, self.fs = channel_type, snr_db, fs
         self.profile, self.frequency_ghz, self.velocity_kmh = itu_profile, frequency_ghz, velocity_kmh
         self.rayleigh = channel_type == 'rayleigh_mp'
@@ -311,9 +315,9 @@ class OFDMChannel:
 
     def _apply(self, signal, num_rx):
         """Channel on an arbitrary stream on the GPU (lte_channel_host64; float32
-        lte_channel_host when LTE_PRECISION=f32)."""
+        lte_channel_host in an f32 channel)."""
         C.device_init()
-        f64 = C.precision_of() == 'f64'
+        f64 = self.precision == 'f64'
         cdt, rdt, ct = (np.complex128, np.float64, C.F64) if f64 else (np.complex64, np.float32, C.F32)
         x = np.ascontiguousarray(signal, dtype=cdt)
         L = len(x)
@@ -358,7 +362,9 @@ class OFDMChannel:
             if len(sg) != L:
                 raise ValueError(f"TX signal {t} length mismatch")
         C.device_init()
-        x = np.ascontiguousarray(np.stack([np.asarray(sg) for sg in signals_tx]), dtype=np.complex64)
+        f64 = self.precision == 'f64'
+        cdt, rdt, ct = (np.complex128, np.float64, C.F64) if f64 else (np.complex64, np.float32, C.F32)
+        x = np.ascontiguousarray(np.stack([np.asarray(sg) for sg in signals_tx]), dtype=cdt)
         P = len(self.delays)
         ph = np.zeros((num_rx, num_tx, max(P, 1), 16))
         lz = np.zeros((num_rx, num_tx, 2, L))
@@ -372,16 +378,17 @@ class OFDMChannel:
                     lz[r, t, 1] = np.random.normal(0, 1.0, L)
             z[r, 0] = np.random.normal(0, 1.0, L)
             z[r, 1] = np.random.normal(0, 1.0, L)
-        y = np.zeros((num_rx, L), dtype=np.complex64)
-        st = np.zeros((num_rx, num_tx, 4), dtype=np.float32)
+        y = np.zeros((num_rx, L), dtype=cdt)
+        st = np.zeros((num_rx, num_tx, 4), dtype=rdt)
         dl = np.array(self.delays, dtype=np.int32)
         g = np.array(self.gains, dtype=np.float64)
         ray = self.rayleigh
-        C.check(C.load().lte_channel_mimo_host(
+        fn = C.load().lte_channel_mimo_host64 if f64 else C.load().lte_channel_mimo_host
+        C.check(fn(
             L, num_tx, num_rx, 0, self.kind, P, C.ptr(dl, C.I32) if P else None, C.ptr(g, C.F64) if P else None,
-            float(self.fD), float(self.fs or 0.0), float(self.snr_db), 0, C.ptr(x.view(np.float32), C.F32),
+            float(self.fD), float(self.fs or 0.0), float(self.snr_db), 0, C.ptr(x.view(rdt), ct),
             C.ptr(ph, C.F64) if ray else None, C.ptr(lz, C.F64) if ray else None, None, C.ptr(z, C.F64),
-            C.ptr(y.view(np.float32), C.F32), C.ptr(st, C.F32) if ray else None, None))
+            C.ptr(y.view(rdt), ct), C.ptr(st, ct) if ray else None, None))
         return list(y.astype(np.complex128)), _link_matrix(st, ray)
 
     def get_config(self) -> Dict:
@@ -399,14 +406,14 @@ class ChannelSimulator:
     The fD rule and gain conversions are the reference's (doppler(), Q2)."""
 
     def __init__(self, channel_type='awgn', snr_db=10.0, fs=None, itu_profile='Vehicular_A', frequency_ghz=None,
-                 velocity_kmh=None, verbose=True):
+                 velocity_kmh=None, verbose=True, *, precision: Optional[str] = None):
         if channel_type == 'fading':
             raise NotImplementedError("FadingChannel is outside the GPU path (SURVEY §8)")
         if channel_type not in ('awgn', 'rayleigh_mp'):
             raise ValueError(f"Tipo de canal desconocido: {channel_type}")
         self.channel_type, self.fs, self.itu_profile = channel_type, fs, itu_profile
         self.frequency_ghz, self.velocity_kmh = frequency_ghz, velocity_kmh
-        self._ch = OFDMChannel(channel_type, snr_db, fs, itu_profile, frequency_ghz, velocity_kmh)
+        self._ch = OFDMChannel(channel_type, snr_db, fs, itu_profile, frequency_ghz, velocity_kmh, precision=precision)
 
     @property
     def snr_db(self):
@@ -432,7 +439,9 @@ class ChannelSimulator:
         ch = self._ch
         ray = ch.rayleigh
         C.device_init()
-        x = np.ascontiguousarray(np.stack([np.asarray(sg)[:L] for sg in tx_signals]), dtype=np.complex64)
+        f64 = ch.precision == 'f64'
+        cdt, rdt, ct = (np.complex128, np.float64, C.F64) if f64 else (np.complex64, np.float32, C.F32)
+        x = np.ascontiguousarray(np.stack([np.asarray(sg)[:L] for sg in tx_signals]), dtype=cdt)
         if ray:
             delays, gains = itu_paths(self.itu_profile, self.fs, spatial=True)
         else:
@@ -458,14 +467,15 @@ class ChannelSimulator:
         for r in range(num_rx):
             z[r, 0] = np.random.normal(0, 1.0, L)
             z[r, 1] = np.random.normal(0, 1.0, L)
-        y = np.zeros((num_rx, L), dtype=np.complex64)
+        y = np.zeros((num_rx, L), dtype=cdt)
         dl = np.array(delays, dtype=np.int32)
         g = np.array(gains, dtype=np.float64)
-        C.check(C.load().lte_channel_mimo_host(
+        fn = C.load().lte_channel_mimo_host64 if f64 else C.load().lte_channel_mimo_host
+        C.check(fn(
             L, num_tx, num_rx, 1, ch.kind, P, C.ptr(dl, C.I32) if P else None, C.ptr(g, C.F64) if P else None,
-            float(ch.fD), float(self.fs or 0.0), float(ch.snr_db), 0, C.ptr(x.view(np.float32), C.F32),
+            float(ch.fD), float(self.fs or 0.0), float(ch.snr_db), 0, C.ptr(x.view(rdt), ct),
             C.ptr(ph, C.F64) if ray else None, None, None if ray else C.ptr(lh, C.F64), C.ptr(z, C.F64),
-            C.ptr(y.view(np.float32), C.F32), None, None))
+            C.ptr(y.view(rdt), ct), None, None))
         return list(y.astype(np.complex128)), Hm
 
 
@@ -478,8 +488,10 @@ class OFDMSimulator:
                  enable_sc_fdm: bool = False, enable_equalization: bool = True, num_channels: int = 1,
                  itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0.0,
                  *, precision: Optional[str] = None):
-        """precision (not in the reference): arithmetic type of the SISO / SIMO GPU
-        chains, 'f64' (default; the reference's float64) or 'f32' (fast mode)."""
+        """precision (not in the reference): arithmetic type of the GPU chains
+        (SISO, SIMO, SFBC, spatial multiplexing; beamforming is float32) and of
+        this simulator's channels, 'f64' (default; the reference's float64) or
+        'f32' (fast mode)."""
         if config is None:
             config = LTEConfig()
         self.precision = C.precision_of(precision)
@@ -493,9 +505,10 @@ class OFDMSimulator:
         self.channels = []
         for _ in range(num_channels):
             if channel_type == 'rayleigh_mp':
-                ch = OFDMChannel('rayleigh_mp', 10.0, fs, itu_profile, frequency_ghz, velocity_kmh)
+                ch = OFDMChannel('rayleigh_mp', 10.0, fs, itu_profile, frequency_ghz, velocity_kmh,
+                                 precision=self.precision)
             else:
-                ch = OFDMChannel('awgn', snr_db=10.0, fs=fs)
+                ch = OFDMChannel('awgn', snr_db=10.0, fs=fs, precision=self.precision)
             self.channels.append(ch)
         self.grid = ResourceGrid(config.N, config.Nc)
         self.last_results = None
@@ -660,7 +673,7 @@ class OFDMSimulator:
         return get_plan(N=cfg.N, Nc=cfg.Nc, cp_len=cfg.cp_length, bps=cfg.bits_per_symbol, n_sym=n_sym,
                         chain=C.CHAIN_SFBC_CODED if coded else C.CHAIN_SFBC, channel=ch.kind, num_rx=num_rx,
                         num_tx=2, delays=tuple(ch.delays), gains=tuple(ch.gains), fD=ch.fD, fs=cfg.fs,
-                        n_bits=n_bits, turbo_iters=iters, max_frames=max_frames)
+                        n_bits=n_bits, turbo_iters=iters, max_frames=max_frames, precision=self.precision)
 
     def _simulate_sfbc(self, bits, snr_db, num_rx, mode):
         """simulate_miso (core/ofdm_core.py:1850-2047) / simulate_mimo (:2049-2258)
@@ -819,7 +832,7 @@ class OFDMSimulator:
             plan = _spatial_plan(cfg, ctype, ch.profile, velocity_kmh, frequency_ghz,
                                  int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol))), nb, frames_per_call,
                                  num_tx=sp['num_tx'], num_rx=sp['num_rx'], rank=sp['rank'],
-                                 detector=DETECTORS[sp['detector'].upper()], W=W)[0]
+                                 detector=DETECTORS[sp['detector'].upper()], W=W, precision=self.precision)[0]
         elif mimo == 'beamforming':
             from .beamforming import bf_plan
             bfo = {'num_tx': 4, 'num_rx': 1, 'update_mode': 'adaptive'}
@@ -852,7 +865,7 @@ class OFDMSimulator:
 
 
 def _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n_bits, max_frames=1,
-                  num_tx=4, num_rx=4, rank=4, detector=C.DET_MMSE, W=None):
+                  num_tx=4, num_rx=4, rank=4, detector=C.DET_MMSE, W=None, precision=None):
     ch = {'awgn': C.CH_AWGN, 'rayleigh_mp': C.CH_RAYLEIGH}.get(channel_type)
     if ch is None:
         raise ValueError(f"Tipo de canal desconocido: {channel_type}")
@@ -869,14 +882,14 @@ def _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz
     return get_plan(N=config.N, Nc=config.Nc, cp_len=config.cp_length, bps=config.bits_per_symbol, n_sym=n_sym,
                     chain=C.CHAIN_SPATIAL, channel=ch, num_rx=num_rx, num_tx=num_tx, delays=tuple(delays),
                     gains=tuple(gains), fD=fD, fs=config.fs, n_bits=n_bits, max_frames=max_frames, rank=rank,
-                    detector=detector, precoder=Wt), gains, fD
+                    detector=detector, precoder=Wt, precision=precision), gains, fD
 
 
 def simulate_spatial_multiplexing(bits, num_tx=4, num_rx=2, rank='adaptive', detector_type='MMSE',
                                   modulation='64-QAM', snr_db=15, config=None, channel_type='awgn',
                                   itu_profile='Pedestrian_A', velocity_kmh=3, frequency_ghz=2.0,
                                   enable_csi_feedback=True, coherence_time_symbols=None, enable_parallel=False,
-                                  codebook_type='TM4'):
+                                  codebook_type='TM4', *, precision: Optional[str] = None):
     """simulate_spatial_multiplexing (core/ofdm_core.py:2489-2815): TM4 with
     2 / 4 TX, 1-4 RX, rank 1-4 -- one GPU call.  Host: H_initial (:2573-2574,
     drawn even at fixed rank) -> RankAdaptation.get_feedback on it for
@@ -918,7 +931,8 @@ def simulate_spatial_multiplexing(bits, num_tx=4, num_rx=2, rank='adaptive', det
     if det == C.DET_MRC and rank_used != 1:
         raise ValueError("MRC solo soporta num_layers=1 (rank-1)")
     plan, gains, fD = _spatial_plan(config, channel_type, itu_profile, velocity_kmh, frequency_ghz, n_sym, n0,
-                                    num_tx=num_tx, num_rx=num_rx, rank=rank_used, detector=det, W=W)
+                                    num_tx=num_tx, num_rx=num_rx, rank=rank_used, detector=det, W=W,
+                                    precision=precision)
     L = plan.L
     ray = channel_type == 'rayleigh_mp'
     step = num_tx if num_tx <= 4 else 4

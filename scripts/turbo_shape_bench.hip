@@ -1,0 +1,208 @@
+// Microbenchmark: the f64 turbo decoder's HBM access shape with the
+// arithmetic removed -- the measured ceiling of k_turbo64's row stream.
+//
+// Same geometry as k_turbo64 (lte_decoder.hip, LTE_TURBO_ILV = 1): one wave
+// per SIMD (a 256-thread block holds 96 KB of LDS, so one block = 4 waves per
+// CU), a wave = 64 code blocks of one K, 512-B rows [row][64 lanes] f64, LS /
+// LE interleaved ([2k] LS, [2k+1] LE), LP1 / LP2 after them; per half
+// iteration a forward sweep of 8-step windows (3 rows per step: LS, LP, LE;
+// decoder 2 at the QPP address pi(k), wave-uniform), an alpha checkpoint of 8
+// rows stored every 24 steps, then a backward sweep of 24-step super-windows
+// (8 checkpoint rows + 3 x 24 input rows loaded, 24 extrinsic rows stored);
+// 8 iterations + the final pass; the first pass skips the LE loads.  Config 2
+// at 65 536 frames: 5 jobs (K = 5568 x 4, 5632), 1 024 waves each.
+//
+// The loaded values are folded with XOR into what is stored, so no load can be
+// dropped.  Prints bytes moved per launch and GB/s, for the decoder's shape
+// with and without the checkpoint rows, and with two waves per SIMD.
+// Build: hipcc -O3 --offload-arch=gfx950 -o scripts/turbo_shape_bench scripts/turbo_shape_bench.hip
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ uint64_t ld(__amdgpu_buffer_rsrc_t r, int vo, int row) {
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, vo, row * 512, 0));
+}
+__device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, int vo, int row, uint64_t v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, vo, row * 512, 0);
+}
+
+struct Job {
+  uint64_t* blk;
+  uint64_t* ck;
+  int K, f1, f2, G;
+};
+struct Jobs {
+  Job j[5];
+  int prefix[6];
+  int n;
+};
+
+__device__ __forceinline__ int modadd(int a, int b, int K) { a += b; return a >= K ? a - K : a; }
+__device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 0 ? a + K : a; }
+
+template <bool CKPT, bool dec2, bool first>
+__device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int vo, int K, int f1, int f2,
+                     uint64_t& acc) {
+  const int nsub = K / 8, tf2 = (2 * f2) % K;
+  const int lp0 = dec2 ? 3 * K + 6 : 2 * K + 3;
+  int pi = 0, d = (f1 + f2) % K;
+#pragma unroll 1
+  for (int w = 0; w < nsub; ++w) {
+    if (CKPT && w % 3 == 0) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) st(rc, vo, (w / 3) * 8 + s, acc + s);
+    }
+    uint64_t xs[8], xp[8], xe[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // the window's loads first (as the decoder's ldwin), then the fold
+      const int k = w * 8 + j, p = dec2 ? pi : k;
+      xs[j] = ld(rb, vo, 2 * p);
+      xp[j] = ld(rb, vo, lp0 + k);
+      xe[j] = first ? 0 : ld(rb, vo, 2 * p + 1);
+      if (dec2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
+    }
+    uint64_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x ^= xs[j] ^ xp[j] ^ xe[j];
+    acc = acc * 3 + x;
+  }
+  // tails: 3 termination steps (2 rows each)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) acc ^= ld(rb, vo, 2 * K + j) ^ ld(rb, vo, lp0 + K + j);
+  const int nsw = (nsub + 2) / 3;
+#pragma unroll 1
+  for (int q = nsw - 1; q >= 0; --q) {
+    const int ns = min(3, nsub - q * 3), n = ns * 8, k0 = q * 24;
+    if (dec2) {
+#pragma unroll 1
+      for (int j = 0; j < n; ++j) { d = modsub(d, tf2, K); pi = modsub(pi, d, K); }
+    }
+    uint64_t v[24], vp[24], ve[24];
+    int pp = pi, dd = d;
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      if (i < n) {
+        const int k = k0 + i, p = dec2 ? pp : k;
+        v[i] = ld(rb, vo, 2 * p);
+        vp[i] = ld(rb, vo, lp0 + k);
+        ve[i] = first ? 0 : ld(rb, vo, 2 * p + 1);
+        if (dec2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 24; ++i) v[i] ^= vp[i] ^ ve[i];
+    if (CKPT) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc ^= ld(rc, vo, q * 8 + s);
+    }
+#pragma unroll
+    for (int i = 23; i >= 0; --i) {
+      if (i < n) {
+        const int k = k0 + i;
+        int p = k;
+        if (dec2) { dd = modsub(dd, tf2, K); pp = modsub(pp, dd, K); p = pp; }
+        st(rb, vo, 2 * p + 1, v[i] + acc);
+      }
+    }
+    if (dec2) { pi = pp; d = dd; }
+  }
+}
+
+template <bool CKPT>
+__global__ __launch_bounds__(256) void k_shape(Jobs J, int iters) {
+  extern __shared__ uint64_t lds_pad[];
+  const int wg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wg >= J.prefix[J.n]) return;
+  int r = 0;
+  while (wg >= J.prefix[r + 1]) ++r;
+  const Job jb = J.j[r];
+  const int g = wg - J.prefix[r], K = jb.K, lane = threadIdx.x & 63, vo = lane * 8;
+  const size_t rows = 4 * (size_t)K + 12, ckrows = (size_t)(K / 8 + 1) * 8;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(jb.blk + (size_t)g * rows * 64, (uint32_t)(rows * 512));
+  const __amdgpu_buffer_rsrc_t rc = rsrc(jb.ck + (size_t)g * ckrows * 64, (uint32_t)(ckrows * 512));
+  uint64_t acc = lane;
+  for (int it = 0; it < iters; ++it) {
+    if (it == 0) pass<CKPT, false, true>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+    else pass<CKPT, false, false>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+    pass<CKPT, true, false>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+  }
+  pass<CKPT, false, false>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+  if (acc == 0x123456789abcdefull) lds_pad[0] = acc;   // never true; keeps the LDS request
+}
+
+// bytes one wave moves (the loop structure above, counted on the host)
+static double wave_bytes(int K, int iters, bool ckpt) {
+  const int nsub = K / 8, nsw = (nsub + 2) / 3;
+  double rows = 0;
+  for (int p = 0; p < 2 * iters + 1; ++p) {
+    const bool first = p == 0;
+    const double per = first ? 2 : 3;
+    rows += per * K * 2 + 6 + K;   // fwd + bwd loads, tails, extrinsic stores
+    if (ckpt) rows += (double)((nsub + 2) / 3) * 8 + nsw * 8;
+  }
+  return rows * 512;
+}
+
+int main(int argc, char** argv) {
+  const int F = argc > 1 ? atoi(argv[1]) : 65536, iters = 8, G = F / 64;
+  const int Ks[5] = {5568, 5568, 5568, 5568, 5632}, f1s[5] = {43, 43, 43, 43, 45}, f2s[5] = {174, 174, 174, 174, 176};
+  Jobs J{};
+  J.n = 5;
+  std::vector<void*> bufs;
+  double bytes_ck = 0, bytes_nock = 0;
+  for (int r = 0; r < 5; ++r) {
+    const size_t rows = 4 * (size_t)Ks[r] + 12, ckrows = (size_t)(Ks[r] / 8 + 1) * 8;
+    void *b, *c;
+    if (hipMalloc(&b, rows * 512 * G) || hipMalloc(&c, ckrows * 512 * G)) {
+      printf("alloc failed\n");
+      return 1;
+    }
+    (void)hipMemset(b, 0, rows * 512 * G);
+    (void)hipMemset(c, 0, ckrows * 512 * G);
+    bufs.push_back(b);
+    bufs.push_back(c);
+    J.j[r] = Job{(uint64_t*)b, (uint64_t*)c, Ks[r], f1s[r], f2s[r], G};
+    J.prefix[r + 1] = J.prefix[r] + G;
+    bytes_ck += wave_bytes(Ks[r], iters, true) * G;
+    bytes_nock += wave_bytes(Ks[r], iters, false) * G;
+  }
+  const int waves = J.prefix[5];
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  auto run = [&](bool ck, size_t lds) {
+    auto k = ck ? k_shape<true> : k_shape<false>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3((waves + 3) / 4), dim3(256), lds, 0, J, iters);   // warm
+    (void)hipEventRecord(a, 0);
+    for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k, dim3((waves + 3) / 4), dim3(256), lds, 0, J, iters);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms / 3.0;
+  };
+  const double m1 = run(true, 96 * 1024), m0 = run(false, 96 * 1024), m2 = run(true, 64 * 1024),
+               m3 = run(true, 0);
+  if (hipDeviceSynchronize() != hipSuccess) {
+    printf("kernel failed\n");
+    return 1;
+  }
+  printf("{\"frames\": %d, \"waves\": %d, \"bytes_per_launch_ckpt\": %.0f, \"bytes_per_launch_nockpt\": %.0f, "
+         "\"ms_1wps_ckpt\": %.3f, \"GBs_1wps_ckpt\": %.1f, \"ms_1wps_nockpt\": %.3f, \"GBs_1wps_nockpt\": %.1f, "
+         "\"ms_2wps_ckpt\": %.3f, \"GBs_2wps_ckpt\": %.1f, \"ms_free_ckpt\": %.3f, \"GBs_free_ckpt\": %.1f}\n",
+         F, waves, bytes_ck, bytes_nock, m1, bytes_ck / (m1 * 1e-3) / 1e9, m0, bytes_nock / (m0 * 1e-3) / 1e9, m2,
+         bytes_ck / (m2 * 1e-3) / 1e9, m3, bytes_ck / (m3 * 1e-3) / 1e9);
+  for (void* p : bufs) (void)hipFree(p);
+  return 0;
+}

@@ -88,7 +88,8 @@ def test_bench_self_launches_ranks_dry_run():
     import json
     from lte_phy import dist as D
     F, steps = 64, 2
-    r = _bench(['--gpus', '2', '--dry-run', '--steps', str(steps), '--warmup', '0', '--frames', str(F)])
+    r = _bench(['--gpus', '2', '--dry-run', '--steps', str(steps), '--warmup', '0', '--frames', str(F),
+                '--cpu-seconds', '0.5'])
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
     assert len(line) == 1, r.stdout          # one JSON line, rank 0 only
@@ -102,6 +103,28 @@ def test_bench_self_launches_ranks_dry_run():
     np.add.at(ref[:, 2], si, (ids % np.uint64(3) == 0).astype(np.uint64))
     np.add.at(ref[:, 3], si, np.uint64(1))
     assert np.array_equal(np.array(out['counts'], dtype=np.uint64), ref)
+    # the N > 1 line carries the CPU baseline (timed by the launching parent,
+    # before any rank starts) and a roofline priced on the slowest rank's timers
+    cpu = out['cpu_baseline']
+    assert cpu and cpu['value'] > 0 and cpu['cores'] >= 1 and cpu['kind'] == 'port'
+    roof = out['roofline']
+    assert roof['bound'] in ('hbm', 'valu') and roof['unit'] == 'GB/s' and roof['peak'] == 8000.0
+    for k in ('achieved', 'frac', 'traffic', 'alg_bytes_per_launch', 'avg_launch_ms', 'valu', 'stage_bytes'):
+        assert k in roof, k
+    # rank 1's synthetic timer is 1 % slower: the merged timer is the max
+    assert abs(roof['avg_launch_ms'] - 0.8 * out['ms_per_step'] * 1.01) < 0.05 * out['ms_per_step']
+
+
+def test_merge_timers_takes_slowest_rank():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location('bench_mod', os.path.join(root, 'bench.py'))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    m = b.merge_timers([{'turbo': (10.0, 5), 'dematch': (1.0, 5)}, {'turbo': (12.0, 5), 'dematch': (0.5, 5)}, None])
+    assert m == {'turbo': (12.0, 5), 'dematch': (1.0, 5)}
+    # the exact decoder's row model: 116 rows of 8 B per step over 8 iterations
+    assert b.decoder_row_bytes(5568, 8, 8) == 5568 * 116 * 8 + 3 * 2 * 17 * 8 + 5568 / 8
 
 
 def test_bench_rejects_world_size_mismatch():

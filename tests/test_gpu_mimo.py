@@ -2,10 +2,13 @@
 configs 4 and 5) against the reference's own outputs (tests/golden/
 golden_mimo.npz, frozen global RNG) and the oracle (oracle/mimo_oracle.py).
 
-Bars: BER |dBER| < 1e-3 absolute vs the reference (north_star tolerance);
-identical global-RNG side effects; channel matrices to float32 precision;
-coded SFBC: in-chain LLRs vs the oracle's max-log demapper (1e-4 relative) and
-decoding bit-exact vs the decoder's float32 model."""
+Bars, float64 (the default, the reference's complex128): identical bit
+errors and received bits, identical global-RNG side effects, channel matrices
+to 1e-12 relative, received streams to 1e-12 relative; coded SFBC: in-chain
+LLRs vs the oracle's max-log demapper to 1e-12 and decoding bit-exact vs the
+float64 reference decoder.  float32 fast mode: |dBER| < 1e-3 absolute (the
+north_star tolerance), matrices / streams to float32 precision, decoding
+bit-exact vs the decoder's float32 model."""
 import numpy as np
 import pytest
 
@@ -25,40 +28,56 @@ def _state():
     return np.array(np.random.get_state()[1][:8], dtype=np.uint32)
 
 
-def _sim(bw, mod, chan):
+def _sim(bw, mod, chan, precision='f64'):
     import lte_phy
-    return lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type=chan)
+    return lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type=chan,
+                                 precision=precision)
 
 
-@pytest.mark.parametrize('name,bw,mod,chan,snrs,nrx', [
-    ('sfbc_c1', 1.25, 'QPSK', 'awgn', [4], 2),
-    ('sfbc_c1miso', 1.25, 'QPSK', 'rayleigh_mp', [10], 1),
-    ('sfbc_c4', 20.0, '64-QAM', 'rayleigh_mp', [10, 20, 30], 2)])
-def test_sfbc_ref_compat(C, golden_mimo, name, bw, mod, chan, snrs, nrx):
+SFBC_CASES = [('sfbc_c1', 1.25, 'QPSK', 'awgn', [4], 2),
+              ('sfbc_c1miso', 1.25, 'QPSK', 'rayleigh_mp', [10], 1),
+              ('sfbc_c4', 20.0, '64-QAM', 'rayleigh_mp', [10, 20, 30], 2)]
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('name,bw,mod,chan,snrs,nrx', SFBC_CASES)
+def test_sfbc_ref_compat(C, golden_mimo, name, bw, mod, chan, snrs, nrx, prec):
     """simulate_miso / simulate_mimo (with the Q19 estimator fix) == the fixed
-    reference: bit errors, global RNG state, channel matrix, per-TX PAPR."""
-    sim = _sim(bw, mod, chan)
+    reference: bit errors, received bits, global RNG state, channel matrix,
+    per-TX PAPR.  f64: identical decisions; f32: within the north_star 1e-3."""
+    sim = _sim(bw, mod, chan, prec)
     nb = int(golden_mimo[name + '_nbits'][0])
     bits = unpack(golden_mimo[name + '_bits'], nb).astype(np.int64)
     for snr in snrs:
         k = f'{name}_snr{snr}'
         r = sim.simulate_miso(bits, snr) if nrx == 1 else sim.simulate_mimo(bits, snr, num_rx=nrx)
         ref_err = int(golden_mimo[k + '_errors'][0])
-        assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
-        assert np.mean(r['bits_received_array'] != unpack(golden_mimo[k + '_rx'], nb)) < 1e-3
-        assert np.array_equal(_state(), golden_mimo[k + '_state'])
+        ref_rx = unpack(golden_mimo[k + '_rx'], nb)
         H = golden_mimo[k + '_H']
-        assert np.max(np.abs(r['channel_matrix'] - H)) < 1e-4 * (1 + np.max(np.abs(H))), k
         p = golden_mimo[k + '_papr']
-        assert np.allclose([r['papr_db_tx0'], r['papr_db_tx1'], r['papr_db']], p, atol=1e-3), k
+        assert np.array_equal(_state(), golden_mimo[k + '_state'])
+        if prec == 'f64':
+            assert r['bit_errors'] == ref_err, (k, r['bit_errors'], ref_err)
+            assert np.array_equal(r['bits_received_array'], ref_rx), k
+            assert np.max(np.abs(r['channel_matrix'] - H)) < 1e-12 * (1 + np.max(np.abs(H))), k
+            assert np.allclose([r['papr_db_tx0'], r['papr_db_tx1'], r['papr_db']], p, rtol=0, atol=1e-9), k
+        else:
+            assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
+            assert np.mean(r['bits_received_array'] != ref_rx) < 1e-3
+            assert np.max(np.abs(r['channel_matrix'] - H)) < 1e-4 * (1 + np.max(np.abs(H))), k
+            assert np.allclose([r['papr_db_tx0'], r['papr_db_tx1'], r['papr_db']], p, atol=1e-3), k
 
 
-@pytest.mark.parametrize('name,bw,mod,chan,snrs', [
-    ('sm_c1', 1.25, 'QPSK', 'awgn', [15]),
-    ('sm_c5awgn', 20.0, '64-QAM', 'awgn', [25]),
-    ('sm_c5ray', 20.0, '64-QAM', 'rayleigh_mp', [25, 35])])
-def test_spatial_ref_compat(C, golden_mimo, name, bw, mod, chan, snrs):
-    """simulate_spatial_multiplexing 4x4 rank 4 MMSE == the reference."""
+SM_CASES = [('sm_c1', 1.25, 'QPSK', 'awgn', [15]),
+            ('sm_c5awgn', 20.0, '64-QAM', 'awgn', [25]),
+            ('sm_c5ray', 20.0, '64-QAM', 'rayleigh_mp', [25, 35])]
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('name,bw,mod,chan,snrs', SM_CASES)
+def test_spatial_ref_compat(C, golden_mimo, name, bw, mod, chan, snrs, prec):
+    """simulate_spatial_multiplexing 4x4 rank 4 MMSE == the reference (f64:
+    identical bit errors and received bits; f32: within 1e-3)."""
     import lte_phy
     nb = int(golden_mimo[name + '_nbits'][0])
     bits = unpack(golden_mimo[name + '_bits'], nb).astype(np.int64)
@@ -68,10 +87,15 @@ def test_spatial_ref_compat(C, golden_mimo, name, bw, mod, chan, snrs):
         r = lte_phy.simulate_spatial_multiplexing(bits, num_tx=4, num_rx=4, rank=4, detector_type='MMSE',
                                                   modulation=mod, snr_db=snr, config=c, channel_type=chan,
                                                   itu_profile='Pedestrian_A', velocity_kmh=3,
-                                                  enable_csi_feedback=False)
+                                                  enable_csi_feedback=False, precision=prec)
         ref_err = int(golden_mimo[k + '_errors'][0])
-        assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
-        assert np.mean(r['bits_received_array'] != unpack(golden_mimo[k + '_rx'], nb)) < 1e-3
+        ref_rx = unpack(golden_mimo[k + '_rx'], nb)
+        if prec == 'f64':
+            assert r['bit_errors'] == ref_err, (k, r['bit_errors'], ref_err)
+            assert np.array_equal(r['bits_received_array'], ref_rx), k
+        else:
+            assert abs(r['bit_errors'] - ref_err) / nb < 1e-3, (k, r['bit_errors'], ref_err)
+            assert np.mean(r['bits_received_array'] != ref_rx) < 1e-3
         assert np.array_equal(_state(), golden_mimo[k + '_state'])
         assert np.array_equal(r['channel_matrix'], golden_mimo[k + '_H'])
         assert np.array_equal(r['precoder_matrix'], golden_mimo[k + '_W'])
@@ -92,14 +116,16 @@ def test_spatial_vs_oracle_awgn_high_snr(C, oracle, mimo_oracle):
     assert np.array_equal(r['channel_matrix'], o['channel_matrix'])
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('chan', ['awgn', 'rayleigh_mp'])
-def test_sfbc_coded_llrs_and_decoding(C, oracle, chan):
+def test_sfbc_coded_llrs_and_decoding(C, oracle, chan, prec):
     """Config 4 chain on Philox frames: the LLRs k_det_sfbc writes equal the
     oracle's max-log LLRs of the same combined symbols with the documented
-    noise-variance rule, and the GPU decoder's output equals the float32
-    decoder model run on those LLRs (T/F de-interleave with cols = Nd & ~1,
-    rate dematch, turbo, CRC)."""
-    sim = _sim(20.0, '64-QAM', chan)
+    noise-variance rule (f64 1e-12, f32 1e-4), and the GPU decoder's output
+    equals the float64 reference decoder (f64) / the float32 decoder model
+    (f32) run on those LLRs (T/F de-interleave with cols = Nd & ~1, rate
+    dematch, turbo, CRC)."""
+    sim = _sim(20.0, '64-QAM', chan, prec)
     plan = sim._sfbc_plan(0, 27760, 2, coded=True, max_frames=4)
     snrs = np.array([8.0, 14.0, 20.0, 30.0])
     r = plan.run(snrs, seed=9, capture=('llr', 'data_syms', 'H', 'bits_rx'))
@@ -117,31 +143,34 @@ def test_sfbc_coded_llrs_and_decoding(C, oracle, chan):
     for b, snr in enumerate(snrs):
         z = r['data_syms'][b].astype(np.complex128)
         H = r['H'][b].astype(np.complex128)
-        s2 = 10 ** (-snr / 10)
+        s2 = 1.0 / 10 ** (snr / 10)
         nv = np.zeros(len(z))
         for l in range(plan.n_sym):
             e = l // 14
             inv_g = np.zeros(res // 2)
             for a in range(2):
                 h0, h1 = H[a, e, 0], H[a, e, 1]
-                nrm = np.abs((h0[0::2] + h0[1::2]) / 2) ** 2 + np.abs((h1[0::2] + h1[1::2]) / 2) ** 2 + 1e-10
+                a0, a1 = (h0[0::2] + h0[1::2]) / 2, (h1[0::2] + h1[1::2]) / 2
+                nrm = (np.hypot(a0.real, a0.imag) ** 2 + np.hypot(a1.real, a1.imag) ** 2) + 1e-10
                 inv_g += 1.0 / np.clip(nrm, 1e-6, 1e6)
             v = np.maximum(s2 / 4.0 * inv_g, s2 / 4.0)   # s2 / R^2 * sum 1/norm, R = 2
             nv[l * res:(l + 1) * res] = np.repeat(v, 2)
         ref = oracle.llrs(z, nv, '64-QAM')
         got = r['llr'][b].astype(np.float64)[:len(ref)]
-        assert np.max(np.abs(got - ref) / (1 + np.abs(ref))) < 1e-4, (chan, snr)
+        tol = 1e-12 if prec == 'f64' else 1e-4
+        assert np.max(np.abs(got - ref) / (1 + np.abs(ref))) < tol, (chan, snr)
         L = got.reshape(-1, bps)[src].reshape(-1)[:coded]
-        dec, ok = oracle.coded_rx_decode(L, seg_plan, rm, 8, f32_model=True)
+        dec, ok = oracle.coded_rx_decode(L, seg_plan, rm, 8, f32_model=prec == 'f32')
         assert np.array_equal(dec, r['bits_rx'][b]) and bool(ok) == bool(r['crc_ok'][b]), (chan, snr)
     if chan == 'awgn':
         assert r['crc_ok'][-1] == 1 and r['frame_errors'][-1] == 0
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mimo,coded,chan', [('sfbc', True, 'rayleigh_mp'), ('spatial', False, 'rayleigh_mp'),
                                             ('spatial', False, 'awgn')])
-def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan):
-    sim = _sim(20.0, '64-QAM', chan)
+def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan, prec):
+    sim = _sim(20.0, '64-QAM', chan, prec)
     kw = dict(mimo=mimo, coded=coded, num_rx=2 if mimo == 'sfbc' else 4)
     a = sim.run_grid([10.0, 25.0], 24, seed=5, **kw)
     b0 = sim.run_grid([10.0, 25.0], 24, seed=5, rank=0, world_size=2, **kw)
@@ -150,32 +179,37 @@ def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan):
     assert a['ber'][1] <= a['ber'][0] + 1e-12
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('chan', ['awgn', 'rayleigh_mp'])
-def test_transmit_mimo_stage(C, golden_mimo, chan):
+def test_transmit_mimo_stage(C, golden_mimo, chan, prec):
     """OFDMChannel.transmit_mimo (a12) == the reference on the same seed:
-    received streams to float32 precision, channel matrix, RNG state."""
+    received streams (f64 1e-12, f32 1e-5 relative), channel matrix, RNG state."""
     import lte_phy
     x = [golden_mimo['txmimo_x0'], golden_mimo['txmimo_x1']]
-    ch = lte_phy.OFDMChannel(channel_type=chan, snr_db=12.0, fs=30.72e6, itu_profile='Pedestrian_A')
+    ch = lte_phy.OFDMChannel(channel_type=chan, snr_db=12.0, fs=30.72e6, itu_profile='Pedestrian_A', precision=prec)
     np.random.seed(123)
     ys, Hm = ch.transmit_mimo(x, num_rx=2)
     ref = golden_mimo[f'txmimo_{chan}_y']
-    assert np.max(np.abs(np.array(ys) - ref)) < 1e-5 * (1 + np.max(np.abs(ref)))
-    assert np.allclose(Hm, golden_mimo[f'txmimo_{chan}_H'], rtol=1e-5, atol=1e-6)
+    tol = 1e-12 if prec == 'f64' else 1e-5
+    assert np.max(np.abs(np.array(ys) - ref)) < tol * (1 + np.max(np.abs(ref)))
+    assert np.allclose(Hm, golden_mimo[f'txmimo_{chan}_H'], rtol=tol, atol=tol * 0.1)
     assert np.array_equal(_state(), golden_mimo[f'txmimo_{chan}_state'])
 
 
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('chan', ['awgn', 'rayleigh_mp'])
-def test_transmit_spatial_multiplexing_stage(C, golden_mimo, chan):
+def test_transmit_spatial_multiplexing_stage(C, golden_mimo, chan, prec):
     """ChannelSimulator.transmit_spatial_multiplexing (a13), 4x4, PedA 3 km/h
-    (time-varying Jakes) == the reference on the same seed."""
+    (time-varying Jakes: f64 the exact sum per sample) == the reference on the
+    same seed (streams f64 1e-12, f32 1e-5 relative)."""
     import lte_phy
     cs = lte_phy.ChannelSimulator(channel_type=chan, snr_db=18.0, fs=30.72e6, itu_profile='Pedestrian_A',
-                                  frequency_ghz=2.0, velocity_kmh=3, verbose=False)
+                                  frequency_ghz=2.0, velocity_kmh=3, verbose=False, precision=prec)
     np.random.seed(321)
     ys, Hm = cs.transmit_spatial_multiplexing(list(golden_mimo['txsm_x']), num_rx=4)
     ref = golden_mimo[f'txsm_{chan}_y']
-    assert np.max(np.abs(np.array(ys) - ref)) < 1e-5 * (1 + np.max(np.abs(ref)))
+    tol = 1e-12 if prec == 'f64' else 1e-5
+    assert np.max(np.abs(np.array(ys) - ref)) < tol * (1 + np.max(np.abs(ref)))
     assert np.allclose(Hm, golden_mimo[f'txsm_{chan}_H'], rtol=1e-9, atol=1e-12)
     assert np.array_equal(_state(), golden_mimo[f'txsm_{chan}_state'])
 

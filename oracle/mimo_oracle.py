@@ -13,8 +13,10 @@ from __future__ import annotations
 
 import numpy as np
 
-from .lte_oracle import (BPS, ITU_CHANNEL_MODELS, Numerology, bits_to_symbols, constellation, doppler_hz,
-                         interp_channel, itu_paths, jakes, multipath, nearest_indices, indices_to_bits, pilots)
+from .lte_oracle import (BPS, ITU_CHANNEL_MODELS, Numerology, attach_crc24a, bits_to_symbols, coded_rx_decode,
+                         constellation, doppler_hz, interp_channel, itu_paths, jakes, llrs, multipath,
+                         nearest_indices, indices_to_bits, pilots, rate_match, segment, tf_interleave_perm,
+                         turbo_encode)
 
 
 # --------------------------------------------------------------------------
@@ -384,3 +386,82 @@ def simulate_spatial(num: Numerology, bits, snr_db, num_tx=4, num_rx=4, rank=4, 
     err = int(np.sum(bits[:n0] != rxb))
     return {'bits_received_array': rxb, 'bit_errors': err, 'ber': err / n0, 'channel_matrix': Hm,
             'precoder_matrix': W, 'signals_rx': ys}
+
+
+# --------------------------------------------------------------------------
+# Config 4: SFBC 2 x num_rx + the coding chain (the build's composition; the
+# reference has no function that composes them, SURVEY §8c / DESIGN.md §3a)
+def simulate_sfbc_coded(num: Numerology, bits, snr_db, num_rx=2, channel='rayleigh_mp', profile='Pedestrian_A',
+                        draws=None, iters=8):
+    """simulate_siso_coded's coding chain (core/ofdm_core.py:925-1338: CRC-24A,
+    segmentation, turbo, rate matching, QAM, T/F interleaver) with cols = the
+    SFBC REs per OFDM symbol (Nd & ~1, Q18) around simulate_mimo's SFBC link
+    (core/ofdm_core.py:2049-2258 with the Q19 estimator fix): per OFDM symbol
+    SFBC encode + grid (cells 0 / 1) + IFFT/CP; transmit_mimo; per RX FFT +
+    slot-0 estimate; per-RX SFBCAlamouti.decode averaged over RX.  Soft
+    output: max-log LLRs (core/ofdm_core.py:791-923) with sigma^2_eff =
+    max((sigma^2 / R^2) sum_r 1 / clip(norm_r, 1e-6, 1e6), sigma^2 / 4) per SC
+    pair, sigma^2 = 1 / 10^(SNR/10) -- the SISO rule (:1224-1243) applied to the
+    combined estimate; T/F de-interleave; dematch; the float64 reference turbo
+    decoder (8 iterations); CRC-24A."""
+    bits = np.asarray(bits)
+    n0 = len(bits)
+    tbc = attach_crc24a(bits)
+    cbs, plan = segment(tbc)
+    rms = []
+    for cb in cbs:
+        enc = turbo_encode(cb)
+        rms.append(rate_match(enc, len(enc), len(cb), 0))
+    coded = np.concatenate(rms)
+    qam = bits_to_symbols(coded, num.modulation)
+    d_idx = sfbc_data_idx(num)
+    res = len(d_idx)
+    perm, rows, total = tf_interleave_perm(len(qam), res)
+    padded = np.pad(qam, (0, total - len(qam))) if len(qam) < total else qam[:total]
+    inter = padded[perm]
+    n_sym = rows
+    s0, s1 = [], []
+    for i in range(n_sym):
+        t0, t1 = sfbc_encode(inter[i * res:(i + 1) * res])
+        g0, g1 = sfbc_map_grid(num, t0, t1)
+        s0.append(_ofdm_time(num, g0))
+        s1.append(_ofdm_time(num, g1))
+    ys, Hm = transmit_mimo(num, [np.concatenate(s0), np.concatenate(s1)], num_rx, channel, snr_db, profile, draws)
+    grids, H0s, H1s = [], [], []
+    for r in range(num_rx):
+        gr = _fft_symbols(num, ys[r], n_sym)
+        h0l, h1l = [], []
+        for st in range(0, len(gr), 14):
+            H = mimo_estimate(num, gr[st], 2)
+            for _ in range(min(14, len(gr) - st)):
+                h0l.append(H[0, 0])
+                h1l.append(H[0, 1])
+        grids.append(gr)
+        H0s.append(h0l)
+        H1s.append(h1l)
+    s2 = 1.0 / (10 ** (snr_db / 10))
+    z_all, nv_all = [], []
+    for i in range(n_sym):
+        dec, inv_g = [], np.zeros(res // 2)
+        for r in range(num_rx):
+            h0, h1 = H0s[r][i][d_idx], H1s[r][i][d_idx]
+            dec.append(sfbc_decode(grids[r][i][d_idx], h0, h1))
+            a0, a1 = (h0[0::2] + h0[1::2]) / 2, (h1[0::2] + h1[1::2]) / 2
+            nrm = np.abs(a0) ** 2 + np.abs(a1) ** 2 + 1e-10
+            inv_g += 1.0 / np.clip(nrm, 1e-6, 1e6)
+        z_all.append(np.mean(dec, axis=0))
+        nv_all.append(np.repeat(np.maximum((s2 / num_rx ** 2) * inv_g, s2 / 4.0), 2))
+    z = np.concatenate(z_all)
+    nv = np.concatenate(nv_all)
+    ncs = len(coded) // num.bps
+    rows_rx = int(np.ceil(ncs / res))
+    tot = rows_rx * res
+    sd = z[:tot].reshape(res, rows_rx).T.reshape(-1)[:ncs]
+    nd = nv[:tot].reshape(res, rows_rx).T.reshape(-1)[:ncs]
+    L = llrs(sd, nd, num.modulation)
+    L = np.pad(L, (0, len(coded) - len(L))) if len(L) < len(coded) else L[:len(coded)]
+    dec, ok = coded_rx_decode(L, plan, [len(r) for r in rms], iters)
+    dec = np.pad(dec, (0, n0 - len(dec))) if len(dec) < n0 else dec[:n0]
+    err = int(np.sum(bits != dec))
+    return {'bits_received_array': dec, 'bit_errors': err, 'ber': err / n0, 'crc_pass': bool(ok),
+            'channel_matrix': Hm, 'symbols_rx': sd, 'noise_var': nd, 'llrs': L}

@@ -17,7 +17,9 @@ GOLDEN_SCFDM = os.path.join(ROOT, 'tests', 'golden', 'golden_scfdm.npz')
 GOLDEN_IMAGE = os.path.join(ROOT, 'tests', 'golden', 'golden_image.npz')
 GOLDEN_BF = os.path.join(ROOT, 'tests', 'golden', 'golden_bf.npz')
 GOLDEN_R2 = os.path.join(ROOT, 'tests', 'golden', 'golden_r2.npz')
+GOLDEN_R3 = os.path.join(ROOT, 'tests', 'golden', 'golden_r3.npz')
 FIXTURE_CURVE = os.path.join(ROOT, 'tests', 'golden', 'fixture_ber_curve.npz')
+FIXTURE_CURVE_C4 = os.path.join(ROOT, 'tests', 'golden', 'fixture_ber_curve_c4.npz')
 GOLDEN_CODING_R2 = os.path.join(ROOT, 'tests', 'golden', 'golden_coding_r2.npz')
 
 
@@ -85,8 +87,18 @@ def golden_coding():
 
 
 @pytest.fixture(scope='session')
+def golden_r3():
+    return np.load(GOLDEN_R3, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
 def fixture_curve():
     return np.load(FIXTURE_CURVE, allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def fixture_curve_c4():
+    return np.load(FIXTURE_CURVE_C4, allow_pickle=False)
 
 
 @pytest.fixture(scope='session')

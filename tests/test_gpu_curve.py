@@ -8,6 +8,10 @@
     frames per SNR point, 512 frames): the float64 chain is identical frame by
     frame; the f32 fast mode's per-point |dBER| is reported (north_star: BER
     match within 1e-3) and bounded where the reference decodes.
+  * fixture_ber_curve_c4 (config 4 as BASELINE states it, "BER sweep": the
+    float64 oracle's SFBC 2x2 + turbo composition on 32 RandomState-seeded
+    injected frames per SNR point of 0:2:30 dB): the float64 GPU chain is
+    identical frame by frame; the f32 fast mode's |dBER| is reported.
   * c3veha: config 3 as BASELINE states it (SIMO 1x4 MRC, 10 MHz 16-QAM,
     Vehicular-A: 6 paths, delays to 39 samples -- the channel kernel's LDS
     delay halo beyond PedA's 13).
@@ -145,6 +149,74 @@ def test_coded_ber_curve_fixture_f32_fast_mode(curve_runs, fixture_curve):
     clean = ref_crc.all(axis=1)
     assert np.all(np.abs(dber[clean]) < 1e-3), dber
     assert np.mean(crc == ref_crc) >= 0.95
+
+
+def _c4_draws(fx, s, f, L, num_rx):
+    """tests/golden/make_fixture_ber_curve.py draws_c4: bits, then transmit_mimo's
+    draws (per RX: per TX link phases [4][16] + link noise re / im; RX noise)."""
+    rs = np.random.RandomState(int(fx['seed0'][0]) + 1000 * s + f)
+    bits = rs.randint(0, 2, int(fx['tb'][0]))
+    ph = np.zeros((num_rx, 2, 4, 16))
+    lz = np.zeros((num_rx, 2, 2, L))
+    z = np.zeros((num_rx, 2, L))
+    for r in range(num_rx):
+        for t in range(2):
+            for p in range(4):
+                ph[r, t, p] = 2 * np.pi * rs.rand(16)
+            lz[r, t, 0] = rs.randn(L)
+            lz[r, t, 1] = rs.randn(L)
+        z[r, 0] = rs.randn(L)
+        z[r, 1] = rs.randn(L)
+    return bits, ph, lz, z
+
+
+@pytest.fixture(scope='module')
+def curve_runs_c4(C, fixture_curve_c4):
+    fx = fixture_curve_c4
+    snrs, F, TB, nrx = fx['snrs'], int(fx['frames'][0]), int(fx['tb'][0]), int(fx['num_rx'][0])
+    chunk = 128
+    out = {}
+    for prec in ('f64', 'f32'):
+        sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
+        plan = sim._sfbc_plan(0, TB, nrx, coded=True, max_frames=chunk)
+        jobs = [(s, f) for s in range(len(snrs)) for f in range(F)]
+        err = np.zeros(len(jobs), dtype=np.int64)
+        crc = np.zeros(len(jobs), dtype=np.uint8)
+        for c0 in range(0, len(jobs), chunk):
+            part = jobs[c0:c0 + chunk]
+            d = [_c4_draws(fx, s, f, plan.L, nrx) for s, f in part]
+            r = plan.run(np.array([snrs[s] for s, _ in part]), bits=np.stack([x[0] for x in d]).astype(np.uint8),
+                         phases=np.stack([x[1] for x in d]), link_noise=np.stack([x[2] for x in d]),
+                         noise=np.stack([x[3] for x in d]))
+            err[c0:c0 + len(part)] = r['frame_errors']
+            crc[c0:c0 + len(part)] = r['crc_ok']
+        out[prec] = (err.reshape(len(snrs), F), crc.reshape(len(snrs), F))
+    return out
+
+
+def test_sfbc_coded_ber_curve_fixture_f64_exact(curve_runs_c4, fixture_curve_c4):
+    """Config 4 (SFBC 2x2 + turbo, 20 MHz 64-QAM PedA), 512 injected frames over
+    0:2:30 dB: the float64 GPU chain == the float64 oracle composition frame by
+    frame (bit errors and CRC verdicts)."""
+    err, crc = curve_runs_c4['f64']
+    assert np.array_equal(err, fixture_curve_c4['bit_errors'])
+    assert np.array_equal(crc, fixture_curve_c4['crc_ok'])
+
+
+def test_sfbc_coded_ber_curve_fixture_f32_fast_mode(curve_runs_c4, fixture_curve_c4):
+    """The same 512 frames in the f32 fast mode: per-point |dBER| reported
+    (gpurun_out/ber_curve_c4_f32.json), < 1e-3 wherever the f64 chain decodes
+    every frame of the point."""
+    err, crc = curve_runs_c4['f32']
+    TB = int(fixture_curve_c4['tb'][0])
+    F = err.shape[1]
+    ref_err, ref_crc = fixture_curve_c4['bit_errors'], fixture_curve_c4['crc_ok']
+    dber = (err.sum(1) - ref_err.sum(1)) / (F * TB)
+    _report('ber_curve_c4_f32.json', {'snr_db': fixture_curve_c4['snrs'].tolist(), 'dber': dber.tolist(),
+                                      'ber_ref': (ref_err.sum(1) / (F * TB)).tolist(),
+                                      'crc_agree': float(np.mean(crc == ref_crc))})
+    clean = ref_crc.all(axis=1)
+    assert np.all(np.abs(dber[clean]) < 1e-3), dber
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])

@@ -121,3 +121,18 @@ def test_simulate_spatial(golden_mimo, oracle, mimo_oracle, name, bw, mod, chan,
         assert np.array_equal(r['channel_matrix'], golden_mimo[k + '_H'])
         assert np.array_equal(r['precoder_matrix'], golden_mimo[k + '_W'])
         assert np.array_equal(np.array(np.random.get_state()[1][:8], dtype=np.uint32), golden_mimo[k + '_state'])
+
+
+def test_sfbc_coded_fixture_frames(oracle, mimo_oracle, fixture_curve_c4):
+    """The config-4 composition (simulate_sfbc_coded) regenerates the committed
+    fixture's verdicts for one frame past the cliff and one clean frame (the
+    fixture's draws are RandomState-seeded, tests/golden/make_fixture_ber_curve.py)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        'mkfx', os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'make_fixture_ber_curve.py'))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    for s, f in [(8, 3), (12, 0)]:
+        _, _, err, crc = mk.one_c4((s, f))
+        assert err == int(fixture_curve_c4['bit_errors'][s, f]) and crc == int(fixture_curve_c4['crc_ok'][s, f])

@@ -217,7 +217,8 @@ int lte_bcjr_host(int K, int64_t ncb, const float *ls, const float *lp, const fl
  * the reference's unnormalised max-log recursion in its own operation order. */
 int lte_turbo_decode_host64(int K, int iters, int64_t ncb, const double *llr /*[ncb][3K+12]*/, uint8_t *bits);
 /* float64 single BCJR pass of any length n, a-posteriori output for every step:
- * LogMAPDecoder.decode (turbo_decoder.py:181-278) with return_extrinsic=False. */
+ * LogMAPDecoder.decode (turbo_decoder.py:181-278) with return_extrinsic=False.
+ * n = 0 is valid (nothing written), like the reference's zero-step recursion. */
 int lte_bcjr_host64(int n, int64_t ncb, const double *ls, const double *lp, const double *la, double *app);
 /* CRC: _calculate_crc core/channel_coding/crc.py:89-134 (MSB-first, zero init);
  * poly 0x1864CFB (CRC-24A, calculate_crc24a :137-159) or 0x1800063 (CRC-24B,
@@ -271,7 +272,8 @@ int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t *src);
 /* rate_dematching_turbo (core/channel_coding/rate_matching.py:374-489) for any
  * E, on the device: llr [ncb][E] float64 -> out [ncb][3K+12]; punctured
- * positions 0.0, repeats (E > N_cb) summed in order onto 0.0 (:433-436). */
+ * positions 0.0, repeats (E > N_cb) summed in order onto 0.0 (:433-436).
+ * E = 0 (all punctured) writes zeros without a launch, as the reference returns. */
 int lte_rate_dematch_host64(int K, int E, int rv_idx, int64_t ncb, const double *llr, double *out);
 /* QPP interleaver pi(i) = (f1 i + f2 i^2) mod K: qpp_interleave
  * core/channel_coding/turbo_encoder.py:76-103 (out[i] = in[perm[i]]). */

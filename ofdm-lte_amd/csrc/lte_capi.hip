@@ -804,6 +804,11 @@ int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t* src) {
 }
 
 int lte_rate_dematch_host64(int K, int E, int rv_idx, int64_t ncb, const double* llr, double* out) {
+  if (E == 0) {   // nothing received: every position punctured, zeros(3K + 12) like the reference
+    if (K < 0 || ncb < 0 || (ncb > 0 && !out)) return fail(LTE_EINVAL, "bad arguments");
+    std::fill(out, out + (size_t)ncb * (3 * (size_t)K + 12), 0.0);
+    return LTE_OK;
+  }
   if (ncb < 0 || (ncb > 0 && (!llr || !out))) return fail(LTE_EINVAL, "bad arguments");
   std::vector<int32_t> src(3 * (size_t)K + 12);
   const int rc = dematch_first_map(K, E, rv_idx, src.data(), nullptr);
@@ -2297,8 +2302,8 @@ int lte_bcjr_host(int K, int64_t ncb, const float* ls, const float* lp, const fl
 }
 
 int lte_bcjr_host64(int n, int64_t ncb, const double* ls, const double* lp, const double* la, double* app) {
-  if (n < 1 || ncb < 0 || (ncb > 0 && (!ls || !lp || !la || !app))) return fail(LTE_EINVAL, "bad arguments");
-  if (ncb == 0) return LTE_OK;
+  if (n < 0 || ncb < 0 || (n > 0 && ncb > 0 && (!ls || !lp || !la || !app))) return fail(LTE_EINVAL, "bad arguments");
+  if (ncb == 0 || n == 0) return LTE_OK;   // K = 0: empty decisions and LLRs, like the reference
   const size_t sz = (size_t)ncb * n;
   DBuf<double> dls, dlp, dla, dal, dapp;
   if (dls.alloc(sz) || dlp.alloc(sz) || dla.alloc(sz) || dal.alloc(sz * 8) || dapp.alloc(sz))

@@ -162,11 +162,11 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 // butterfly per thread per pass, every pass register-staged (read -> barrier
 // -> write -> barrier), so several transforms of the same N can share a
 // workgroup.  Between passes the data lives in an XOR-swizzled layout
-// (fft_sw) that makes the strided Stockham stores conflict-free for
-// ds_write_b64 (16-lane groups, banks mod 32); the caller's layout (input and
-// output) is the natural one.  tw[e] = exp(-2*pi*i*e/N), e in [0, N).
-// V = float2 or double2 (the chain precision; fft_sw's swizzle is tuned for
-// the 8-B float2 element).
+// (fft_sw<V>) that makes the strided Stockham stores and the unit-stride loads
+// conflict-free for the element's LDS instructions; the output layout is the
+// natural one, the input layout natural or (ISW) swizzled.
+// tw[e] = exp(-2*pi*i*e/N), e in [0, N).  V = float2 or double2 (the chain
+// precision).
 // Unscaled.  N in [128, 2048].  All threads of the workgroup must call it (it
 // contains __syncthreads).
 template <bool INV, class V>
@@ -175,8 +175,23 @@ __device__ __forceinline__ V twid(const V* __restrict__ tw, int e) {
   return INV ? mkc(w.x, -w.y) : w;
 }
 
-// logical -> physical float2 index between passes (bijection on each 128-block)
-__device__ __forceinline__ int fft_sw(int i) { return i ^ (((i >> 4) & 7) | ((i >> 3) & 8)); }
+// logical -> physical element index between passes (a bijection on each
+// 128-element block).  The bank rules (MI355X_MICROARCH.md, LDS):
+// * float2 (8 B): ds_write_b64 serves 16 contiguous lanes per cycle on banks
+//   (a/4) mod 32, i.e. element mod 16; ds_read_b64 32 lanes, element mod 32.
+//   The radix-8 store 8j + r needs bits 4..6 folded into bits 0..3.
+// * double2 (16 B): ds_write_b128 serves 8 contiguous lanes per cycle
+//   (element mod 8 must differ), ds_read_b128 the 16-lane groups
+//   {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31} (element mod 16).  Folding bits
+//   3..5 into bits 0..2 makes the first pass's stride-8 store (lanes j, element
+//   8j + r: low bits r ^ (j & 7)) and every unit-stride load conflict-free; the
+//   float2 fold above leaves the stride-8 store 2-way and some loads 2-way.
+// (scripts/lds_bank_model.py checks both against every pass of N = 128..2048.)
+template <class V>
+__device__ __forceinline__ int fft_sw(int i) {
+  if constexpr (sizeof(V) == 16) return i ^ ((i >> 3) & 7);
+  else return i ^ (((i >> 4) & 7) | ((i >> 3) & 8));
+}
 
 // x * -j (forward) or x * +j (inverse)
 template <bool INV, class V>
@@ -226,7 +241,10 @@ __device__ __forceinline__ void dft8_inplace(V (&v)[8]) {
 // for r >= 2, formed from w^ks by complex products -- one table load per
 // butterfly instead of 7 (radix 8) / 3 (radix 4), a few ulp each; the f64
 // N = 2048 transform runs 22 % faster (scripts/rx_parts_bench.hip).
-template <bool INV, int NC = 0, bool SC = false, bool TWR = (NC > 0), class V>
+// ISW: the input is in the swizzled layout (written through fft_sw<V> by a
+// loader whose natural pattern would conflict, e.g. load_symbol_noisy2's
+// stride-2 sample pairs).
+template <bool INV, int NC = 0, bool SC = false, bool TWR = (NC > 0), bool ISW = false, class V>
 __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __restrict__ tw, int tid, bool active,
                                         re_t<V> osc = (re_t<V>)1) {
   const int N = NC ? NC : N_;
@@ -239,14 +257,14 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
   if constexpr (NC > 0) {
 #pragma unroll
     for (int s = 0; s < n8; ++s) {
-      const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
+      const bool rsw = s > 0 || ISW, wsw = !(s == n8 - 1 && rem == 0);
       V v[8];
       const int j = tid;
       if (active) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int i = j + r * T;
-          v[r] = buf[rsw ? fft_sw(i) : i];
+          v[r] = buf[rsw ? fft_sw<V>(i) : i];
         }
         if (s > 0) {
           const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));   // k * N / (8 Ns)
@@ -274,7 +292,7 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int i = idx + r * Ns;
-          buf[wsw ? fft_sw(i) : i] = (SC && !wsw) ? cscale(v[r], osc) : v[r];
+          buf[wsw ? fft_sw<V>(i) : i] = (SC && !wsw) ? cscale(v[r], osc) : v[r];
         }
       }
       __syncthreads();
@@ -283,14 +301,14 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
     }
   } else {
     for (int s = 0; s < n8; ++s) {
-      const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
+      const bool rsw = s > 0 || ISW, wsw = !(s == n8 - 1 && rem == 0);
       V v[8];
       const int j = tid;
       if (active) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int i = j + r * T;
-          v[r] = buf[rsw ? fft_sw(i) : i];
+          v[r] = buf[rsw ? fft_sw<V>(i) : i];
         }
         if (s > 0) {
           const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));   // k * N / (8 Ns)
@@ -305,7 +323,7 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int i = idx + r * Ns;
-          buf[wsw ? fft_sw(i) : i] = (SC && !wsw) ? cscale(v[r], osc) : v[r];
+          buf[wsw ? fft_sw<V>(i) : i] = (SC && !wsw) ? cscale(v[r], osc) : v[r];
         }
       }
       __syncthreads();
@@ -321,7 +339,7 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
       for (int q = 0; q < 2; ++q) {
         const int j = tid + q * T;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[q][r] = buf[fft_sw(j + r * q4)];
+        for (int r = 0; r < 4; ++r) v[q][r] = buf[fft_sw<V>(j + r * q4)];
         if constexpr (TWR) {
           const V w1 = twid<INV>(tw, j), w2 = cmul(w1, w1), w3 = cmul(w2, w1);
           v[q][1] = cmul(v[q][1], w1);
@@ -351,7 +369,7 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = tid + q * T;
-        const V a = buf[fft_sw(j)], b = cmul(buf[fft_sw(j + h)], twid<INV>(tw, j));
+        const V a = buf[fft_sw<V>(j)], b = cmul(buf[fft_sw<V>(j + h)], twid<INV>(tw, j));
         v[q][0] = cadd(a, b);
         v[q][1] = csub(a, b);
       }
@@ -367,6 +385,43 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
     }
     __syncthreads();
   }
+}
+
+// ---------------------------------------------------------------- CRC-24 algebra
+// The LTE CRCs (crc.py:89-184: zero initial register, no reflection, no final
+// XOR) are linear over GF(2): crc(M) = M(x) x^24 mod P.  A message split into
+// blocks B_0 .. B_{n-1} of lengths l_i therefore has
+//   crc(M) = sum_i crc(B_i) * x^(l_{i+1} + ... + l_{n-1})  mod P,
+// which lets lanes (or waves) form the CRCs of their blocks independently and
+// combine them with a few multiplications.  Appending z zero bits multiplies the
+// CRC by x^z, so a message zero-padded to a convenient length is corrected by
+// x^(-z) (x is invertible mod P: both LTE polynomials have a constant term).
+// poly = P without its x^24 term; all values are 24-bit.
+__host__ __device__ __forceinline__ uint32_t gf24_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t r = 0u;
+#pragma unroll
+  for (int i = 23; i >= 0; --i) {
+    r = ((r << 1) & 0xFFFFFFu) ^ ((r & 0x800000u) ? poly : 0u);   // r * x mod P
+    r ^= ((a >> i) & 1u) ? b : 0u;
+  }
+  return r;
+}
+// x^e mod P (e >= 0); inv: x^(-e) mod P
+__host__ __device__ inline uint32_t gf24_xpow(uint64_t e, uint32_t poly, bool inv = false) {
+  uint32_t base = inv ? (((poly ^ 1u) >> 1) | 0x800000u) : 2u;   // x^-1 = (P + 1) / x
+  uint32_t r = 1u;
+  while (e) {
+    if (e & 1u) r = gf24_mul(r, base, poly);
+    base = gf24_mul(base, base, poly);
+    e >>= 1;
+  }
+  return r;
+}
+// one byte of CRC register update through a 256-entry table (crc24_byte_table)
+__host__ __device__ __forceinline__ uint32_t crc24_table_entry(uint32_t i, uint32_t poly) {
+  uint32_t r = i << 16;
+  for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? (((r << 1) ^ poly) & 0xFFFFFFu) : ((r << 1) & 0xFFFFFFu);
+  return r & 0xFFFFFFu;
 }
 
 // ---------------------------------------------------------------- bits

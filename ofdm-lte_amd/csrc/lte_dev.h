@@ -67,7 +67,9 @@ __device__ __forceinline__ R block_sum(R v, R* red) {
 
 // Load one OFDM symbol (CP removed) of (frame, rx) into LDS adding AWGN:
 // noise = sigma * z, sigma = sqrt(P/SNR/2) (channel.py:52-60).
-template <class V>
+// SW: samples land in the FFT's swizzled layout (fft_sw<V>, read by
+// fft_lds<.., ISW = true>).
+template <bool SW = false, class V>
 __device__ __forceinline__ void load_symbol_noisy(V* buf, const V* __restrict__ yf, int N, int cp, int l,
                                                   re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
                                                   const re_t<V>* __restrict__ zf /*inj: [2][L] or null*/, int L,
@@ -84,7 +86,7 @@ __device__ __forceinline__ void load_symbol_noisy(V* buf, const V* __restrict__ 
       z = (n & 1) ? gauss2<R>(r.z, r.w) : gauss2<R>(r.x, r.y);
     }
     const V v = yf[n];
-    buf[k] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
+    buf[SW ? fft_sw<V>(k) : k] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
   }
 }
 
@@ -169,15 +171,17 @@ __device__ __forceinline__ double2 zf_eq(double2 y, double2 h) { return cdiv(y, 
 
 // Noise-add for one OFDM symbol into LDS, one Philox call per pair of
 // samples (sample n uses half (n&1) of counter n>>1 -- same draws as
-// load_symbol_noisy, at half the generator cost).
-template <class V>
+// load_symbol_noisy, at half the generator cost).  Lane t stores samples 2t
+// and 2t + 1 (a stride-2 ds_write pattern, 2-way on 16-B and 8-B elements);
+// SW = true stores them swizzled (conflict-free) for fft_lds<.., ISW = true>.
+template <bool SW = false, class V>
 __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__ yf, int N, int cp, int l,
                                                    re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
                                                    const re_t<V>* __restrict__ zf, int L, int tid, int T) {
   using R = re_t<V>;
   const int off = l * (N + cp) + cp;
   if (zf) {
-    load_symbol_noisy(buf, yf, N, cp, l, sigma, seed, frame, rx, zf, L, tid, T);
+    load_symbol_noisy<SW>(buf, yf, N, cp, l, sigma, seed, frame, rx, zf, L, tid, T);
     return;
   }
   const int p0 = off >> 1, p1 = (off + N - 1) >> 1;
@@ -199,11 +203,11 @@ __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__
     const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
     if (n0 >= off) {
       const V z = gauss2<R>(r.x, r.y);
-      buf[n0 - off] = mkc(va[i].x + sigma * z.x, va[i].y + sigma * z.y);
+      buf[SW ? fft_sw<V>(n0 - off) : n0 - off] = mkc(va[i].x + sigma * z.x, va[i].y + sigma * z.y);
     }
     if (n0 + 1 < off + N) {
       const V z = gauss2<R>(r.z, r.w);
-      buf[n0 + 1 - off] = mkc(vb[i].x + sigma * z.x, vb[i].y + sigma * z.y);
+      buf[SW ? fft_sw<V>(n0 + 1 - off) : n0 + 1 - off] = mkc(vb[i].x + sigma * z.x, vb[i].y + sigma * z.y);
     }
   }
 }

@@ -13,64 +13,94 @@ constexpr int WG = 256;
 
 // ---------------------------------------------------------------------------
 // Payload bits (+ CRC-24, crc.py:89-134: CRC-24A attach crc.py:212-233, or
-// CRC-24B for the stage entry, crc.py:162-184): one lane per frame.  crc = the
-// 24-bit polynomial without its x^24 term (0: no CRC).
-__device__ __forceinline__ uint32_t crc24_entry(uint32_t i, uint32_t poly) {
-  uint32_t r = i << 16;
-  for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? ((r << 1) ^ poly) : (r << 1);
-  return r & 0xFFFFFFu;
+// CRC-24B for the stage entry, crc.py:162-184): one wave per frame.  The frame's
+// PW words are cut into 128-bit groups (Philox counter g = group g, words
+// 4g..4g+3: the draws of the one-lane-per-frame kernel this replaces), and lane
+// l owns the KG consecutive groups [l KG, (l+1) KG): it draws and stores them
+// and runs the CRC register over them (a byte-table step per 8 bits, starting
+// from 0).  The 64 chunk CRCs are combined by the linearity of the CRC
+// (gf24_mul, lte_common.h): a 6-level tree with the multipliers
+// x^(128 KG 2^s), then x^(-pad) for the zero bits the chunks hold past n_bits.
+// crc = the polynomial without its x^24 term (0: no CRC); CrcTree is formed on
+// the host (crc_tree).
+struct CrcTree {
+  uint32_t poly, corr;   // corr = x^-(64 KG 128 - n_bits) mod P
+  uint32_t xl[6];        // x^(128 KG 2^s) mod P
+};
+
+static CrcTree crc_tree(uint32_t poly, int KG, int n_bits) {
+  CrcTree t{};
+  t.poly = poly;
+  if (!poly) return t;
+  t.corr = gf24_xpow((uint64_t)64 * KG * 128 - (uint64_t)n_bits, poly, true);
+  for (int s = 0; s < 6; ++s) t.xl[s] = gf24_xpow((uint64_t)128 * KG << s, poly);
+  return t;
 }
 
-__global__ __launch_bounds__(WG) void k_payload(uint32_t* __restrict__ pw, int PW, int n_bits, int crc,
+__global__ __launch_bounds__(WG) void k_payload(uint32_t* __restrict__ pw, int PW, int n_bits, int KG, CrcTree ct,
                                                 const uint64_t* __restrict__ fid, uint64_t seed, int B,
                                                 const uint32_t* __restrict__ inj, int64_t inj_stride) {
   __shared__ uint32_t T[256];
-  const uint32_t poly = (uint32_t)crc & 0xFFFFFFu;
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_entry(i, poly);
+  const uint32_t poly = ct.poly;
+  if (poly)
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_table_entry(i, poly);
   __syncthreads();
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (WG / 64) + (threadIdx.x >> 6);
+  if (b >= B) return;   // whole waves; no barrier below
   uint32_t* w = pw + (size_t)b * PW;
   const int nwd = (n_bits + 31) >> 5;
-  u32x4 rv{0, 0, 0, 0};
-  uint32_t c = 0;
-  for (int i = 0; i < PW; ++i) {
-    uint32_t v = 0;
-    if (i < nwd) {
-      if (inj) {
-        v = inj[(size_t)b * inj_stride + i];
-      } else {
-        if ((i & 3) == 0) rv = rng4(seed, fid[b], RNG_STREAM_BITS, (uint32_t)(i >> 2));
-        const int q = i & 3;
-        v = q == 0 ? rv.x : q == 1 ? rv.y : q == 2 ? rv.z : rv.w;
+  // the (at most two) words holding the CRC bits [n_bits, n_bits + 24) are
+  // stored after the CRC is known, by the lane that drew them
+  const int c0 = n_bits >> 5, c1 = (n_bits + 23) >> 5;
+  uint32_t h0 = 0u, h1 = 0u;
+  const uint64_t f = inj ? 0ull : fid[b];
+  uint32_t c = 0u;
+  for (int k = 0; k < KG; ++k) {
+    const int g = lane * KG + k;
+    u32x4 rv{0u, 0u, 0u, 0u};
+    if (!inj && 4 * g < nwd) rv = rng4(seed, f, RNG_STREAM_BITS, (uint32_t)g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 4 * g + q;
+      uint32_t v = 0u;
+      if (i < nwd) {
+        v = inj ? inj[(size_t)b * inj_stride + i] : (q == 0 ? rv.x : q == 1 ? rv.y : q == 2 ? rv.z : rv.w);
+        const int rem = n_bits - 32 * i;
+        if (rem < 32) v &= ~(0xFFFFFFFFu >> rem);
       }
-      const int rem = n_bits - 32 * i;
-      if (rem < 32) v &= ~(0xFFFFFFFFu >> rem);
-      if (crc) {
-        const int dbits = min(32, rem);
-        int k = 0;
-        for (; k + 8 <= dbits; k += 8) c = ((c << 8) & 0xFFFFFFu) ^ T[((c >> 16) ^ (v >> (24 - k))) & 0xFFu];
-        for (; k < dbits; ++k) {
-          const uint32_t msb = (c >> 23) & 1u;
-          c = (c << 1) & 0xFFFFFFu;
-          if (msb ^ ((v >> (31 - k)) & 1u)) c ^= poly;
-        }
+      if (poly) {
+#pragma unroll
+        for (int k8 = 0; k8 < 4; ++k8) c = ((c << 8) & 0xFFFFFFu) ^ T[((c >> 16) ^ (v >> (24 - 8 * k8))) & 0xFFu];
+        if (i == c0) { h0 = v; continue; }
+        if (i == c1) { h1 = v; continue; }
       }
+      if (i < PW) w[i] = v;
     }
-    w[i] = v;
   }
-  if (crc) {  // append the 24 CRC bits MSB-first at [n_bits, n_bits+24)
-    for (int t = 0; t < 24; ++t) {
-      const int p = n_bits + t;
-      if ((c >> (23 - t)) & 1u) w[p >> 5] |= 1u << (31 - (p & 31));
+  if (poly) {
+    // lane l's chunk sits 64 - 1 - l chunks before the end: merge neighbours,
+    // the left one shifted past the right one's 128 KG 2^s bits
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const uint32_t r = __shfl_down(c, 1 << s);
+      c = gf24_mul(c, ct.xl[s], poly) ^ r;
     }
+    const uint32_t crc = gf24_mul(__shfl(c, 0), ct.corr, poly);
+    const uint32_t L = crc << 8, o = (uint32_t)(n_bits & 31);   // CRC left-aligned, MSB-first at bit n_bits
+    if (lane == ((c0 >> 2) / KG) && c0 < PW) w[c0] = h0 | (L >> o);
+    if (c1 != c0 && lane == ((c1 >> 2) / KG) && c1 < PW) w[c1] = h1 | (L << (32 - o));
   }
 }
 
 int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, const uint64_t* fid, uint64_t seed,
                    int B, const uint32_t* inj, int64_t inj_stride) {
-  hipLaunchKernelGGL(k_payload, dim3((B + WG - 1) / WG), dim3(WG), 0, s, pw, PW, n_bits, crc, fid, seed, B, inj,
-                     inj_stride);
+  const uint32_t poly = (uint32_t)crc & 0xFFFFFFu;
+  if (PW < 1 || n_bits < 0 || (poly && (!(poly & 1u) || PW * 32 < n_bits + 24))) return (int)hipErrorInvalidValue;
+  const int KG = ((PW + 3) / 4 + 63) / 64;   // 128-bit groups per lane
+  const int fpb = WG / 64;
+  hipLaunchKernelGGL(k_payload, dim3((B + fpb - 1) / fpb), dim3(WG), 0, s, pw, PW, n_bits, KG,
+                     crc_tree(poly, KG, n_bits), fid, seed, B, inj, inj_stride);
   return (int)hipGetLastError();
 }
 
@@ -327,6 +357,9 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
 #ifndef TXF_WAVES
 #define TXF_WAVES 1
 #endif
+#ifndef LTE_LDS_PROBE   // timing probes of the per-RE LDS accesses (A/B builds only)
+#define LTE_LDS_PROBE 0
+#endif
 #ifndef TXF_STAGE   // 1: the frame's coded streams staged in LDS; 0: bit gathers through L1 / L2
 #define TXF_STAGE 1
 #endif
@@ -366,6 +399,13 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
 #pragma unroll
       for (int m = 0; m < BPS; ++m) srcs[q][m] = ok ? tx_map[t0 + m] : -1;
       kpos[q] = ok ? g.data_idx[j] : 0;
+#if LTE_LDS_PROBE & 1   // timing probe only (wrong outputs): conflict-free RE positions
+      kpos[q] = ok ? N / 2 - 512 + j : 0;
+#endif
+#if LTE_LDS_PROBE & 2   // timing probe only (wrong outputs): conflict-free bit gathers
+#pragma unroll
+      for (int m = 0; m < BPS; ++m) srcs[q][m] = ok ? 32 * ((j + 41 * m) % 300) + 5 : -1;
+#endif
     }
     if (active)
       for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
@@ -826,11 +866,11 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
     if (active) {
       const R sigma = sqrt(npow[(size_t)b * num_rx + rx] / (R)2);
       const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-      load_symbol_noisy2(buf, y + b * y_frame_stride + rx * y_rx_stride, N, g.cp, l, sigma, seed, fid[b], rx, zf,
-                         g.L, tid, T);
+      load_symbol_noisy2<true>(buf, y + b * y_frame_stride + rx * y_rx_stride, N, g.cp, l, sigma, seed, fid[b], rx,
+                               zf, g.L, tid, T);
     }
     __syncthreads();
-    fft_lds<false, NC>(buf, N, g.log2N, G::tw(g), tid, active);
+    fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, G::tw(g), tid, active);
     if (active) {
       const V* Hf = H + (((size_t)b * num_rx + rx) * g.n_grp + grp) * N;
 #pragma unroll
@@ -1016,6 +1056,9 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh
   for (int q = 0; q < QM; ++q) {
     const int j = tid0 + q * T;
     kpos[q] = (active && j < g.Nd) ? g.data_idx[j] : 0;
+#if LTE_LDS_PROBE & 1   // timing probe only (wrong outputs): conflict-free RE positions
+    kpos[q] = (active && j < g.Nd) ? N / 2 - 512 + j : 0;
+#endif
   }
   ZfCoef<R> zc[QM];
   R nvq[QM];
@@ -1026,9 +1069,9 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh
     // across the loop (which took the kernel to 255 VGPRs)
     int tid = tid0;
     asm volatile("" : "+v"(tid));
-    if (active) load_symbol_noisy2(buf, yf, N, g.cp, l, sigma, seed, fr, 0, zf, g.L, tid, T);
+    if (active) load_symbol_noisy2<true>(buf, yf, N, g.cp, l, sigma, seed, fr, 0, zf, g.L, tid, T);
     __syncthreads();
-    fft_lds<false, NC>(buf, N, g.log2N, G::tw(g), tid, active);
+    fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, G::tw(g), tid, active);
     if (l % 14 == 0) {   // group estimate from its first symbol (lte_receiver.py:360-411)
       const int grp = l / 14;
       if (active)

@@ -701,11 +701,11 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
   if (active) {
     const R sigma = sqrt(npow[(size_t)b * m.num_rx + rx] * (R)0.5);
     const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-    load_symbol_noisy2(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf, g.L, tid,
-                       T);
+    load_symbol_noisy2<true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf,
+                             g.L, tid, T);
   }
   __syncthreads();
-  fft_lds<false>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
+  fft_lds<false, 0, false, false, true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
   const int e = m.mode == MIMO_SFBC ? l / 14 : l;
   const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
   const R sc = rx_scale<R>(N);

@@ -209,11 +209,6 @@ struct BitWriter {   // MSB-first stream writer; one store per completed word
 };
 
 // CRC-24 byte table (MSB-first, zero init; poly without the x^24 term)
-__device__ __forceinline__ uint32_t crc24_table_entry(uint32_t i, uint32_t poly) {
-  uint32_t r = i << 16;
-  for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? ((r << 1) ^ poly) : (r << 1);
-  return r & 0xFFFFFFu;
-}
 
 // RSC code (turbo_encoder.py:137-211) 32 bits at a time, in closed form.  The
 // feedback ("systematic", Q13) sequence obeys a_k = u_k ^ a_{k-2} ^ a_{k-3}, i.e.
@@ -447,7 +442,7 @@ int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t
 // ---------------------------------------------------------------------------
 // CRC-24A / desegmentation / bit-error count.  One lane per frame; lanes of a
 // wave are 64 consecutive frames = one decoder group, so the decoded-word
-// reads are coalesced rows.  Replaces desegment_code_blocks
+// reads are coalesced rows; CRC_SEG waves split the frame's words.  Replaces desegment_code_blocks
 // (segmentation.py:266-359), check_crc24a (crc.py:277-307) and the BER count
 // (core/ofdm_core.py:1304-1311).
 
@@ -462,23 +457,38 @@ __device__ __forceinline__ uint32_t get32s(const uint32_t* w, int64_t st, int64_
   return (a << o) | (b >> (32 - o));
 }
 
-__global__ __launch_bounds__(256) void k_crc_count(const CbInfo* __restrict__ cbi, int C,
-                                                   uint32_t* const* __restrict__ dec, const int* __restrict__ KW,
-                                                   int B, const uint32_t* __restrict__ pw, int PW, int n_bits,
-                                                   uint32_t* __restrict__ frame_err, uint32_t* __restrict__ frame_crc,
-                                                   uint8_t* __restrict__ cap_bits, int b0) {
+// CRC_SEG waves per 64 frames: wave s walks TB words [s SW, (s+1) SW) of the
+// 64 frames (lanes), so a frame's word chain is CRC_SEG times shorter and the
+// chip holds CRC_SEG times more waves.  Each wave runs the CRC register from 0
+// over its data bits; the frame's CRC is sum_s crc_s * x^(data bits after
+// segment s) mod P (lte_common.h CRC-24 algebra, multipliers from the host),
+// formed by wave 0 from the per-wave results parked in LDS.
+constexpr int CRC_SEG = 8;
+struct CrcSeg { uint32_t x[CRC_SEG]; };
+
+__global__ __launch_bounds__(64 * CRC_SEG) void k_crc_count(const CbInfo* __restrict__ cbi, int C,
+                                                            uint32_t* const* __restrict__ dec,
+                                                            const int* __restrict__ KW, int B,
+                                                            const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                            int SW, CrcSeg xs, uint32_t* __restrict__ frame_err,
+                                                            uint32_t* __restrict__ frame_crc,
+                                                            uint8_t* __restrict__ cap_bits, int b0) {
   __shared__ uint32_t T[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_table_entry(i, 0x864CFBu);
+  __shared__ uint32_t part[3][CRC_SEG][64];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_table_entry(i, (uint32_t)CRC24A_POLY);
   __syncthreads();
-  const int b = b0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int g = b >> 6, lane = b & 63;
-  const uint32_t* tx = pw + (size_t)b * PW;
+  const int lane = threadIdx.x & 63, seg = threadIdx.x >> 6;
+  const int b = b0 + blockIdx.x * 64 + lane;
+  const bool act = b < B;
+  const int bb = act ? b : b0;
+  const int g = bb >> 6, gl = bb & 63;
+  const uint32_t* tx = pw + (size_t)bb * PW;
   const int Btb = n_bits + 24;
   const int nw = (Btb + 31) >> 5;
+  const int w0 = seg * SW, w1 = min(nw, w0 + SW);
   uint32_t crc = 0, err = 0, rx_crc = 0;
   int r = 0;
-  for (int w = 0; w < nw; ++w) {
+  for (int w = w0; w < w1; ++w) {
     // assemble TB word w (bits 32w .. 32w+31) from the decoded code blocks
     uint32_t word = 0;
     int got = 0;
@@ -489,7 +499,7 @@ __global__ __launch_bounds__(256) void k_crc_count(const CbInfo* __restrict__ cb
       const CbInfo ci = cbi[r];
       const int avail = min(want - got, ci.off + ci.info - j);
       const int64_t pcb = (int64_t)ci.F + (j - ci.off);
-      const uint32_t* base = dec[r] + (size_t)g * KW[r] * 64 + lane;
+      const uint32_t* base = dec[r] + (size_t)g * KW[r] * 64 + gl;
       const uint32_t v = get32s(base, 64, pcb, KW[r]);
       const uint32_t m = avail >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> avail);
       word |= (v & m) >> got;
@@ -506,28 +516,49 @@ __global__ __launch_bounds__(256) void k_crc_count(const CbInfo* __restrict__ cb
       const uint32_t bit = (word >> (31 - k)) & 1u;
       const uint32_t msb = (crc >> 23) & 1u;
       crc = (crc << 1) & 0xFFFFFFu;
-      if (msb ^ bit) crc ^= 0x864CFBu;
+      if (msb ^ bit) crc ^= (uint32_t)CRC24A_POLY;
     }
-    // received CRC bits [n_bits, n_bits+24)
-    for (int q = max(0, n_bits - 32 * w); q < want; ++q) rx_crc = (rx_crc << 1) | ((word >> (31 - q)) & 1u);
+    // received CRC bits [n_bits, n_bits+24), placed at their CRC bit position
+    for (int q = max(0, n_bits - 32 * w); q < want; ++q)
+      rx_crc |= ((word >> (31 - q)) & 1u) << (23 - (32 * w + q - n_bits));
     if (dbits > 0) {
       const uint32_t m = dbits >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> dbits);
       err += __popc((word ^ tx[w]) & m);
     }
-    if (cap_bits) {
+    if (cap_bits && act) {
       for (int q = 0; q < dbits; ++q) cap_bits[(size_t)b * n_bits + 32 * w + q] = (word >> (31 - q)) & 1u;
     }
   }
-  frame_err[b] = err;
-  frame_crc[b] = (crc == rx_crc) ? 1u : 0u;
+  part[0][seg][lane] = gf24_mul(crc, xs.x[seg], (uint32_t)CRC24A_POLY);
+  part[1][seg][lane] = err;
+  part[2][seg][lane] = rx_crc;
+  __syncthreads();
+  if (seg == 0 && act) {
+    uint32_t c = 0, e = 0, rc = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < CRC_SEG; ++s2) {
+      c ^= part[0][s2][lane];
+      e += part[1][s2][lane];
+      rc |= part[2][s2][lane];
+    }
+    frame_err[b] = e;
+    frame_crc[b] = (c == rc) ? 1u : 0u;
+  }
 }
 
 int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
                      const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
                      uint8_t* cap_bits, int b0) {
-  if (b0 < 0 || b0 >= B) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_crc_count, dim3((B - b0 + 255) / 256), dim3(256), 0, s, cbi_dev, C, dec, KW, B, pw, PW, n_bits,
-                     frame_err, frame_crc, cap_bits, b0);
+  if (b0 < 0 || b0 >= B || n_bits < 0) return (int)hipErrorInvalidValue;
+  const int nw = (n_bits + 24 + 31) >> 5;
+  const int SW = (nw + CRC_SEG - 1) / CRC_SEG;
+  CrcSeg xs{};
+  for (int sg = 0; sg < CRC_SEG; ++sg) {
+    const int end = std::min(32 * (sg + 1) * SW, n_bits);   // data bits up to the segment's end
+    xs.x[sg] = gf24_xpow((uint64_t)(n_bits - std::max(end, 0)), (uint32_t)CRC24A_POLY);
+  }
+  hipLaunchKernelGGL(k_crc_count, dim3((B - b0 + 63) / 64), dim3(64 * CRC_SEG), 0, s, cbi_dev, C, dec, KW, B, pw, PW,
+                     n_bits, SW, xs, frame_err, frame_crc, cap_bits, b0);
   return (int)hipGetLastError();
 }
 

@@ -264,6 +264,8 @@ class LogMAPDecoder:
         la = np.zeros(K) if llr_apriori is None else np.ascontiguousarray(llr_apriori, dtype=np.float64)[:K]
         if len(lp) < K or len(la) < K:
             raise ValueError("llr_parity / llr_apriori shorter than llr_systematic")
+        if K == 0:   # the reference's recursions run zero steps: empty decisions and LLRs
+            return np.zeros(0, dtype=np.uint8), np.zeros(0)
         C.device_init()
         app = np.zeros(K)
         C.check(C.load().lte_bcjr_host64(K, 1, C.ptr(ls, C.F64), C.ptr(np.ascontiguousarray(lp), C.F64),
@@ -322,8 +324,10 @@ def rate_match_turbo(encoded_bits, E, K, rv_idx=0):
 def rate_dematching_turbo(rate_matched_llrs, K, rv_idx=0, debug=False):
     """rate_matching.py:374-489 on the GPU for any E: punctured positions 0.0,
     repeats (E > N_cb) summed in order onto 0.0."""
-    C.device_init()
     llr = np.ascontiguousarray(rate_matched_llrs, dtype=np.float64)
     out = np.zeros(3 * K + 12)
+    if len(llr) == 0:   # E = 0: every position punctured (the reference returns zeros(3K + 12))
+        return out
+    C.device_init()
     C.check(C.load().lte_rate_dematch_host64(int(K), len(llr), int(rv_idx), 1, C.ptr(llr, C.F64), C.ptr(out, C.F64)))
     return out

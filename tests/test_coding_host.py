@@ -53,3 +53,23 @@ def test_single_block_segmentation(golden_coding, B):
     assert md == meta[f'seg{B}']
     assert np.array_equal(np.concatenate(blocks), g[f'seg{B}_blocks'])
     assert np.array_equal(cc.desegment_code_blocks(blocks, md), g[f'seg{B}_back'])
+
+
+@pytest.mark.parametrize('K', [40, 1024, 5568])
+def test_empty_inputs_like_the_reference(K):
+    """rate_dematching_turbo on E = 0 LLRs returns zeros(3K + 12) (every
+    position punctured, rate_matching.py:422-489 with an empty loop) and
+    LogMAPDecoder.decode on K = 0 returns empty decisions / LLRs
+    (turbo_decoder.py:181-278 with zero recursion steps), in the drop-in and in
+    the C-ABI (neither touches the device)."""
+    import ctypes
+    from lte_phy import _capi as C
+    from lte_phy import channel_coding as cc
+    out = cc.rate_dematching_turbo(np.zeros(0), K, 0)
+    assert out.dtype == np.float64 and out.shape == (3 * K + 12,) and not out.any()
+    b, llr = cc.LogMAPDecoder().decode(np.zeros(0), np.zeros(0), return_extrinsic=True)
+    assert b.shape == (0,) and b.dtype == np.uint8 and llr.shape == (0,)
+    buf = np.full(2 * (3 * K + 12), 7.0)
+    assert C.load().lte_rate_dematch_host64(K, 0, 0, 2, None, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double))) == 0
+    assert not buf.any()
+    assert C.load().lte_bcjr_host64(0, 3, None, None, None, None) == 0

@@ -94,3 +94,51 @@ def test_rate_dematching_punct_and_repeat(cc, golden, K):
 def test_rate_dematching_triple_repetition(cc, golden_coding, K):
     g, _ = golden_coding
     assert np.array_equal(cc.rate_dematching_turbo(g[f'dmrep{K}_in'], K, 1), g[f'dmrep{K}_out'])
+
+
+@pytest.mark.parametrize('bw,mod,n_bits', [(20.0, '64-QAM', 6230), (5.0, '16-QAM', 1000)])
+def test_exact_log_map_coded_chain(cc, bw, mod, n_bits):
+    """set_decoder_mode(False) on a whole coded float64 plan (k_turbo64_logmap
+    in the chain): 96 frames = two 64-frame decoder groups; a 6230-bit TB (two
+    code blocks of different sizes, K = 3136 and 3200, in one launch) and a
+    1000-bit TB (one code block).  The chain's decoded TB bits and CRC verdicts
+    equal the host entry points in the same mode (rate_dematching_turbo +
+    turbo_decode, both pinned to the reference's log-MAP goldens above) on the
+    chain's own captured LLRs.  One turbo iteration: the exact log-MAP kernel
+    (exp / log1p per max*) is far slower than the max-log hot path."""
+    import lte_phy
+    from lte_phy import _capi as C
+    from oracle import lte_oracle as O
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type='rayleigh_mp',
+                                precision='f64')
+    its = 1
+    try:
+        cc.set_decoder_mode(False)
+        plan = sim._plan(C.CHAIN_CODED, 0, n_bits, max_frames=96, iters=its)
+        snrs = np.linspace(0.0, 30.0, 96)
+        r = plan.run(snrs, seed=19, capture=('llr', 'bits_rx'))
+        num = O.Numerology(bandwidth=bw, modulation=mod)
+        bps, Nd = num.bps, num.Nd
+        coded = plan.coded_bits
+        ncs = coded // bps
+        rows = -(-ncs // Nd)
+        _, seg_plan = O.segment(O.attach_crc24a(np.zeros(n_bits, dtype=np.uint8)))
+        assert len({p[0] for p in seg_plan}) == (2 if n_bits > 6120 else 1)
+        q = np.arange(ncs)
+        src_re = (q % Nd) * rows + q // Nd
+        L = np.stack([r['llr'][b].reshape(-1, bps)[src_re].reshape(-1)[:coded] for b in range(len(snrs))])
+        off, blocks = 0, []
+        for (K, F, info, o, crc) in seg_plan:   # every frame's code block r in one batched host decode
+            E = 3 * K + 12
+            dm = np.stack([cc.rate_dematching_turbo(L[b, off:off + E], K, 0) for b in range(len(snrs))])
+            off += E
+            blocks.append(cc.turbo_decode_batch(dm, K, its))
+        n_ok = 0
+        for b in range(len(snrs)):
+            tbc = O.desegment([blk[b] for blk in blocks], seg_plan)
+            ok = O.check_crc24a(tbc)
+            assert np.array_equal(tbc[:-24], r['bits_rx'][b]) and bool(ok) == bool(r['crc_ok'][b]), b
+            n_ok += int(ok)
+        assert 4 <= n_ok < len(snrs)   # decoded and failed frames both covered
+    finally:
+        cc.set_decoder_mode(True)

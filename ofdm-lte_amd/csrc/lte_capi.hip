@@ -422,7 +422,9 @@ struct lte_plan {
   // device
   DBuf<CbInfo> cbi;
   DBuf<int32_t> tx_map, rx_map, delays;
-  DBuf<uint32_t> pw, enc, enc_cw, inj_bits;
+  DBuf<uint32_t> pw, enc, inj_bits;
+  DBuf<uint16_t> enc_qmask;   // encoder 2's per-bit segment-state contributions (encode_qmask)
+  int qstride = 0;
   ChainBufs<float> c32;              // f32 plans (and the beamforming chain)
   ChainBufs<double> c64;             // f64 plans
   DBuf<uint32_t> frame_err, frame_crc;
@@ -965,7 +967,10 @@ static int plan_coded_maps(lte_plan* p) {
     }
     (void)base;
   }
-  if (upload(p->tx_map, txm) || upload(p->rx_map, rxm) || upload(p->cbi, p->cbs))
+  p->qstride = Kmax + 32;
+  std::vector<uint16_t> qm((size_t)p->C * p->qstride, 0);
+  encode_qmask(p->cbs.data(), p->C, p->qstride, qm.data());
+  if (upload(p->tx_map, txm) || upload(p->rx_map, rxm) || upload(p->cbi, p->cbs) || upload(p->enc_qmask, qm))
     return fail(LTE_ENOMEM, "map upload failed");
   return LTE_OK;
 }
@@ -1143,7 +1148,6 @@ static int plan_alloc(lte_plan* p) {
   bad |= p->frame_crc.alloc(B) != 0;
   if (coded) {
     bad |= p->enc.alloc(B * p->enc_words) != 0;
-    bad |= p->enc_cw.alloc(encode_scratch_words(p->KWmax, p->C, (int)B)) != 0;
     p->decb.resize(p->C);
     std::vector<int64_t> rows(p->C);
     std::vector<uint32_t*> dp(p->C);
@@ -1312,7 +1316,7 @@ int lte_plan_destroy(lte_plan* p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   p->tabs.release();
   p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release();
-  p->pw.release(); p->enc.release(); p->enc_cw.release(); p->inj_bits.release();
+  p->pw.release(); p->enc.release(); p->inj_bits.release(); p->enc_qmask.release();
   p->c32.release(); p->c64.release();
   p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->fid.release(); p->counts.release();
   p->cap_bits.release();
@@ -1441,7 +1445,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   if (coded) {
     Timer t(p, KN_ENCODE);
-    LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_cw.p));
+    LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_qmask.p, p->qstride));
   }
   {
     Timer t(p, KN_OFDM_TX);
@@ -1504,7 +1508,8 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     {
       Timer t(p, KN_CRC);
       LCHK(launch_crc_count(s, p->cbi.p, p->C, p->dec_ptrs.p, p->kw_dev.p, B, p->pw.p, p->PW, d.n_bits,
-                            p->frame_err.p, p->frame_crc.p, cap_bits_dev));
+                            p->frame_err.p, p->frame_crc.p, cap_bits_dev, 0, inj_bits ? nullptr : p->fid.p,
+                            a->seed));
     }
   }
   {
@@ -1779,7 +1784,7 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   if (do_tx) {
     if (coded) {
       Timer t(p, KN_ENCODE);
-      LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_cw.p));
+      LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_qmask.p, p->qstride));
     }
     V* cts = nullptr;
     if (a->cap_tx_syms) {
@@ -1877,7 +1882,8 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     {
       Timer t(p, KN_CRC);
       LCHK(launch_crc_count(s, p->cbi.p, p->C, p->dec_ptrs.p, p->kw_dev.p, B, p->pw.p, p->PW, d.n_bits,
-                            p->frame_err.p, p->frame_crc.p, cap_bits_dev));
+                            p->frame_err.p, p->frame_crc.p, cap_bits_dev, 0, inj_bits ? nullptr : p->fid.p,
+                            a->seed));
     }
   }
   if (do_rx) {
@@ -2178,18 +2184,20 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out)
   std::vector<uint32_t> w((size_t)ncb * PW);
   for (int64_t c = 0; c < ncb; ++c) pack_bits(bits + c * K, K, &w[c * PW], PW);
   CbInfo ci{K, 0, K, 0, 0, f1, f2, 3 * K + 12};
-  DBuf<uint32_t> dpw, denc, dcw;
+  DBuf<uint32_t> dpw, denc;
   DBuf<CbInfo> dci;
+  DBuf<uint16_t> dqm;
   std::vector<CbInfo> vci{ci};
-  if (dpw.alloc(w.size()) || denc.alloc((size_t)ncb * 3 * EW) || dcw.alloc(encode_scratch_words(KW, 1, (int)ncb)) ||
-      upload(dci, vci)) {
-    dpw.release(); denc.release(); dcw.release(); dci.release();
+  std::vector<uint16_t> qm(K + 32);
+  encode_qmask(&ci, 1, K + 32, qm.data());
+  if (dpw.alloc(w.size()) || denc.alloc((size_t)ncb * 3 * EW) || upload(dci, vci) || upload(dqm, qm)) {
+    dpw.release(); denc.release(); dci.release(); dqm.release();
     return fail(LTE_ENOMEM, "buffers");
   }
   std::vector<uint32_t> e((size_t)ncb * 3 * EW);
   int rc = LTE_OK;
   if (hipMemcpy(dpw.p, w.data(), w.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      launch_encode(nullptr, dpw.p, PW, KW, denc.p, EW, dci.p, 1, (int)ncb, dcw.p) ||
+      launch_encode(nullptr, dpw.p, PW, KW, denc.p, EW, dci.p, 1, (int)ncb, dqm.p, K + 32) ||
       hipMemcpy(e.data(), denc.p, e.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(LTE_EHIP, "encode failed");
   if (rc == LTE_OK) {
@@ -2208,7 +2216,7 @@ int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t* bits, uint8_t* out)
       }
     }
   }
-  dpw.release(); denc.release(); dcw.release(); dci.release();
+  dpw.release(); denc.release(); dci.release(); dqm.release();
   return rc;
 }
 

@@ -423,6 +423,25 @@ __host__ __device__ __forceinline__ uint32_t crc24_table_entry(uint32_t i, uint3
   for (int k = 0; k < 8; ++k) r = (r & 0x800000u) ? (((r << 1) ^ poly) & 0xFFFFFFu) : ((r << 1) & 0xFFFFFFu);
   return r & 0xFFFFFFu;
 }
+// Slice-by-4 tables T[k][b] = b x^(8k) x^24 mod P (k = 0: the byte table), so
+// 32 message bits x update the register c in one step of four independent
+// lookups: with v = (c << 8) ^ x, c' = T3[v >> 24] ^ T2[v >> 16] ^ T1[v >> 8] ^
+// T0[v] (bytes).  Fill: every thread of the block calls it, then a barrier.
+__device__ __forceinline__ void crc24_slice4_fill(uint32_t* T, uint32_t poly) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = crc24_table_entry((uint32_t)i, poly);
+    T[i] = c;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {   // one more zero byte: c x^8 mod P
+      c = ((c << 8) & 0xFFFFFFu) ^ crc24_table_entry(c >> 16, poly);
+      T[k * 256 + i] = c;
+    }
+  }
+}
+__device__ __forceinline__ uint32_t crc24_slice4(const uint32_t* T, uint32_t c, uint32_t x) {
+  const uint32_t v = (c << 8) ^ x;
+  return T[768 + (v >> 24)] ^ T[512 + ((v >> 16) & 0xFFu)] ^ T[256 + ((v >> 8) & 0xFFu)] ^ T[v & 0xFFu];
+}
 
 // ---------------------------------------------------------------- bits
 // Packed bit streams are MSB-first: bit i of a stream lives in word i>>5 at

@@ -57,10 +57,11 @@ constexpr int CRC24A_POLY = 0x864CFB, CRC24B_POLY = 0x800063;   // crc.py polyno
 // crc: CRC polynomial to append (0: none)
 int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, const uint64_t* fid,
                    uint64_t seed, int B, const uint32_t* inj, int64_t inj_stride);
-// cw_scratch: encode_scratch_words(KWmax, C, B) words (the code blocks as [wave][word][lane])
-size_t encode_scratch_words(int KWmax, int C, int B);
+// qmask: encode_qmask(cbs, C, qstride) on the host, C x qstride uint16, qstride >= max K + 32 and a
+// multiple of 2 (the kernel reads whole 32-entry rows as uint32 pairs; entries past K are zero)
+void encode_qmask(const CbInfo* cbs, int C, int qstride, uint16_t* out);
 int launch_encode(hipStream_t s, const uint32_t* pw, int PW, int KWmax, uint32_t* enc, int EW,
-                  const CbInfo* cbi_dev, int C, int B, uint32_t* cw_scratch);
+                  const CbInfo* cbi_dev, int C, int B, const uint16_t* qmask, int qstride);
 // Signal-chain launchers, R = double (the reference's precision, default) or
 // float (fast mode); explicit instances in lte_kernels.hip.
 template <class R>
@@ -165,7 +166,8 @@ int launch_bcjr64(hipStream_t s, const double* ls, const double* lp, const doubl
                   double* alpha_scratch, double* app);
 int launch_crc_count(hipStream_t s, const CbInfo* cbi_dev, int C, uint32_t* const* dec, const int* KW, int B,
                      const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err, uint32_t* frame_crc,
-                     uint8_t* cap_bits, int b0 = 0);
+                     uint8_t* cap_bits, int b0 = 0, const uint64_t* fid = nullptr, uint64_t seed = 0);
+// (fid given: the transmitted words are re-drawn from k_payload's Philox counters instead of read from pw)
 int launch_accumulate(hipStream_t s, int B, int coded, int n_bits, int n_snr, const int32_t* snr_idx,
                       const uint32_t* frame_err, const uint32_t* frame_crc, unsigned long long* counts);
 template <class R>

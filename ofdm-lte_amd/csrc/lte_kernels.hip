@@ -17,10 +17,11 @@ constexpr int WG = 256;
 // PW words are cut into 128-bit groups (Philox counter g = group g, words
 // 4g..4g+3: the draws of the one-lane-per-frame kernel this replaces), and lane
 // l owns the KG consecutive groups [l KG, (l+1) KG): it draws and stores them
-// and runs the CRC register over them (a byte-table step per 8 bits, starting
-// from 0).  The 64 chunk CRCs are combined by the linearity of the CRC
-// (gf24_mul, lte_common.h): a 6-level tree with the multipliers
-// x^(128 KG 2^s), then x^(-pad) for the zero bits the chunks hold past n_bits.
+// and runs the CRC register over them (slice-by-4 tables, starting from 0).
+// The 64 chunk CRCs are combined by the linearity of the CRC (lte_common.h): a
+// 6-level tree with the multipliers x^(128 KG 2^s), then x^(-pad) for the zero
+// bits the chunks hold past n_bits (products through per-block nibble tables).
+// Waves loop over frames so the tables are built once per block.
 // crc = the polynomial without its x^24 term (0: no CRC); CrcTree is formed on
 // the host (crc_tree).
 struct CrcTree {
@@ -37,59 +38,73 @@ static CrcTree crc_tree(uint32_t poly, int KG, int n_bits) {
   return t;
 }
 
+// c * X_k mod P through nibble tables NT[k][j][v] = (v x^(4j)) X_k mod P
+__device__ __forceinline__ uint32_t gf24_mul_nt(const uint32_t* NT, int k, uint32_t c) {
+  const uint32_t* t = NT + k * 96;
+  uint32_t r = 0u;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) r ^= t[j * 16 + ((c >> (4 * j)) & 15u)];
+  return r;
+}
+
 __global__ __launch_bounds__(WG) void k_payload(uint32_t* __restrict__ pw, int PW, int n_bits, int KG, CrcTree ct,
                                                 const uint64_t* __restrict__ fid, uint64_t seed, int B,
                                                 const uint32_t* __restrict__ inj, int64_t inj_stride) {
-  __shared__ uint32_t T[256];
+  __shared__ uint32_t T[1024];      // slice-by-4 CRC tables
+  __shared__ uint32_t NT[7 * 96];   // nibble tables of the 6 tree multipliers and x^-pad
   const uint32_t poly = ct.poly;
-  if (poly)
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) T[i] = crc24_table_entry(i, poly);
+  if (poly) {
+    crc24_slice4_fill(T, poly);
+    for (int i = threadIdx.x; i < 7 * 96; i += blockDim.x) {
+      const int k = i / 96, j = (i % 96) >> 4, v = i & 15;
+      NT[i] = gf24_mul((uint32_t)v << (4 * j), k < 6 ? ct.xl[k] : ct.corr, poly);
+    }
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * (WG / 64) + (threadIdx.x >> 6);
-  if (b >= B) return;   // whole waves; no barrier below
-  uint32_t* w = pw + (size_t)b * PW;
   const int nwd = (n_bits + 31) >> 5;
   // the (at most two) words holding the CRC bits [n_bits, n_bits + 24) are
   // stored after the CRC is known, by the lane that drew them
   const int c0 = n_bits >> 5, c1 = (n_bits + 23) >> 5;
-  uint32_t h0 = 0u, h1 = 0u;
-  const uint64_t f = inj ? 0ull : fid[b];
-  uint32_t c = 0u;
-  for (int k = 0; k < KG; ++k) {
-    const int g = lane * KG + k;
-    u32x4 rv{0u, 0u, 0u, 0u};
-    if (!inj && 4 * g < nwd) rv = rng4(seed, f, RNG_STREAM_BITS, (uint32_t)g);
+  for (int b = blockIdx.x * (WG / 64) + (threadIdx.x >> 6); b < B; b += gridDim.x * (WG / 64)) {   // whole waves
+    uint32_t* w = pw + (size_t)b * PW;
+    uint32_t h0 = 0u, h1 = 0u;
+    const uint64_t f = inj ? 0ull : fid[b];
+    uint32_t c = 0u;
+    for (int k = 0; k < KG; ++k) {
+      const int g = lane * KG + k;
+      u32x4 rv{0u, 0u, 0u, 0u};
+      if (!inj && 4 * g < nwd) rv = rng4(seed, f, RNG_STREAM_BITS, (uint32_t)g);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = 4 * g + q;
-      uint32_t v = 0u;
-      if (i < nwd) {
-        v = inj ? inj[(size_t)b * inj_stride + i] : (q == 0 ? rv.x : q == 1 ? rv.y : q == 2 ? rv.z : rv.w);
-        const int rem = n_bits - 32 * i;
-        if (rem < 32) v &= ~(0xFFFFFFFFu >> rem);
+      for (int q = 0; q < 4; ++q) {
+        const int i = 4 * g + q;
+        uint32_t v = 0u;
+        if (i < nwd) {
+          v = inj ? inj[(size_t)b * inj_stride + i] : (q == 0 ? rv.x : q == 1 ? rv.y : q == 2 ? rv.z : rv.w);
+          const int rem = n_bits - 32 * i;
+          if (rem < 32) v &= ~(0xFFFFFFFFu >> rem);
+        }
+        if (poly) {
+          c = crc24_slice4(T, c, v);
+          if (i == c0) { h0 = v; continue; }
+          if (i == c1) { h1 = v; continue; }
+        }
+        if (i < PW) w[i] = v;
       }
-      if (poly) {
+    }
+    if (poly) {
+      // lane l's chunk sits 64 - 1 - l chunks before the end: merge neighbours,
+      // the left one shifted past the right one's 128 KG 2^s bits
 #pragma unroll
-        for (int k8 = 0; k8 < 4; ++k8) c = ((c << 8) & 0xFFFFFFu) ^ T[((c >> 16) ^ (v >> (24 - 8 * k8))) & 0xFFu];
-        if (i == c0) { h0 = v; continue; }
-        if (i == c1) { h1 = v; continue; }
+      for (int s = 0; s < 6; ++s) {
+        const uint32_t r = __shfl_down(c, 1 << s);
+        c = gf24_mul_nt(NT, s, c) ^ r;
       }
-      if (i < PW) w[i] = v;
+      const uint32_t crc = gf24_mul_nt(NT, 6, __shfl(c, 0));
+      const uint32_t L = crc << 8, o = (uint32_t)(n_bits & 31);   // CRC left-aligned, MSB-first at bit n_bits
+      if (lane == ((c0 >> 2) / KG) && c0 < PW) w[c0] = h0 | (L >> o);
+      if (c1 != c0 && lane == ((c1 >> 2) / KG) && c1 < PW) w[c1] = h1 | (L << (32 - o));
     }
-  }
-  if (poly) {
-    // lane l's chunk sits 64 - 1 - l chunks before the end: merge neighbours,
-    // the left one shifted past the right one's 128 KG 2^s bits
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const uint32_t r = __shfl_down(c, 1 << s);
-      c = gf24_mul(c, ct.xl[s], poly) ^ r;
-    }
-    const uint32_t crc = gf24_mul(__shfl(c, 0), ct.corr, poly);
-    const uint32_t L = crc << 8, o = (uint32_t)(n_bits & 31);   // CRC left-aligned, MSB-first at bit n_bits
-    if (lane == ((c0 >> 2) / KG) && c0 < PW) w[c0] = h0 | (L >> o);
-    if (c1 != c0 && lane == ((c1 >> 2) / KG) && c1 < PW) w[c1] = h1 | (L << (32 - o));
   }
 }
 
@@ -99,7 +114,8 @@ int launch_payload(hipStream_t s, uint32_t* pw, int PW, int n_bits, int crc, con
   if (PW < 1 || n_bits < 0 || (poly && (!(poly & 1u) || PW * 32 < n_bits + 24))) return (int)hipErrorInvalidValue;
   const int KG = ((PW + 3) / 4 + 63) / 64;   // 128-bit groups per lane
   const int fpb = WG / 64;
-  hipLaunchKernelGGL(k_payload, dim3((B + fpb - 1) / fpb), dim3(WG), 0, s, pw, PW, n_bits, KG,
+  const int blocks = std::max(1, std::min((B + fpb - 1) / fpb, 1024));   // waves loop over frames (tables amortised)
+  hipLaunchKernelGGL(k_payload, dim3(blocks), dim3(WG), 0, s, pw, PW, n_bits, KG,
                      crc_tree(poly, KG, n_bits), fid, seed, B, inj, inj_stride);
   return (int)hipGetLastError();
 }

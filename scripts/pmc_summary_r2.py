@@ -4,11 +4,11 @@ MI355X_MICROARCH.md's gfx950 correction for wide streaming reads -- and
 WRITE_SIZE x 1024 for writes), SQ instruction / wait counters per frame, and
 derived VALU / LDS / VMEM shares.  Writes
 
-  profiles/r2_pmc_<prec>.json            every kernel
+  profiles/<tag>_pmc_<prec>.json         every kernel (tag r2 by default)
   profiles/pmc_turbo_traffic_<prec>.json  the decoder's bytes (bench.py roofline.traffic)
   profiles/pmc_turbo_sq_<prec>.json       the decoder's VALU instruction count
 
-usage: python scripts/pmc_summary_r2.py [prec] [frames] [src_dir]
+usage: python scripts/pmc_summary_r2.py [prec] [frames] [src_dir] [tag: output profiles/<tag>_pmc_<prec>.json]
 """
 import csv
 import json
@@ -47,7 +47,7 @@ def kernel_time(path):
     return t
 
 
-def main(prec='f64', frames=8192, src=os.path.join(ROOT, 'gpurun_out')):
+def main(prec='f64', frames=8192, src=os.path.join(ROOT, 'gpurun_out'), tag='r2'):
     frames = int(frames)
     d = lambda n: os.path.join(src, f'pmc_{prec}_{n}')   # noqa: E731
     fk, _ = per_kernel(os.path.join(d('FETCH_SIZE'), 'run_counter_collection.csv'))
@@ -85,7 +85,7 @@ def main(prec='f64', frames=8192, src=os.path.join(ROOT, 'gpurun_out')):
             'correction': 'MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE reports 1/2 of wide streaming-read '
                           'bytes -> read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 exact',
             'kernels': out}
-    with open(os.path.join(ROOT, 'profiles', f'r2_pmc_{prec}.json'), 'w') as f:
+    with open(os.path.join(ROOT, 'profiles', f'{tag}_pmc_{prec}.json'), 'w') as f:
         json.dump(meta, f, indent=1)
     tk_name = 'k_turbo64' if prec == 'f64' else 'k_turbo'
     t = out[tk_name]

@@ -221,17 +221,17 @@ def merge_timers(all_tim):
 
 
 # front-end stages (bench timers) -> their kernels in the committed PMC summary
-FE_KERNELS = {'payload': ['k_payload'], 'encode': ['k_encode', 'k_encode2'], 'ofdm_tx': ['k_ofdm_txf'],
+FE_KERNELS = {'payload': ['k_payload'], 'encode': ['k_encode'], 'ofdm_tx': ['k_ofdm_txf'],
               'rx_data': ['k_rx_frame'], 'dematch': ['k_dematch_zn'], 'crc_count': ['k_crc_count']}
 
 
 def front_end(prec, tim, F):
     """Per front-end stage: its HIP-event time per launch, the HBM bytes per
-    frame its kernels move (profiles/r2_pmc_<prec>.json, rocprofv3 FETCH_SIZE /
+    frame its kernels move (profiles/r3_pmc_<prec>.json, rocprofv3 FETCH_SIZE /
     WRITE_SIZE, gfx950-corrected) and the resulting rate against the 8 TB/s
     peak, plus the VALU / LDS shares of active issue from the same PMC passes
     (what bounds the FFT / noise kernels, which are not HBM-bound)."""
-    pmc = load_profile(f'r2_pmc_{prec}.json')
+    pmc = load_profile(f'r3_pmc_{prec}.json') or load_profile(f'r2_pmc_{prec}.json')
     if not pmc:
         return None
     ks = pmc['kernels']

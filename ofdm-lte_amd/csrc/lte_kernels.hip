@@ -608,6 +608,20 @@ __device__ __forceinline__ cx<R> jakes_coef(const R* __restrict__ ph, R gain, R 
   }
 }
 
+// Time-varying taps (fD != 0) by a Taylor expansion of the Jakes sum: over a
+// sub-interval of SL samples centred at t_c the sum is
+//   sum_m a_m exp(j w_m tau) = sum_k c_k tau^k,  a_m = exp(j (w_m t_c + phi_m)),
+//   c_k = sum_m a_m (j w_m)^k / k!,  tau = t - t_c,
+// with a_m formed exactly as jakes_coef forms one sample (the reference's
+// argument order).  The host picks SL (a power of two, >= 64) so that
+// |w tau| <= 2.7e-3 on it: the degree-5 remainder is below 16 (2.7e-3)^6 / 720
+// ~ 9e-18, under float64 rounding, and the per-sample cost drops from 16 sincos
+// to 5 complex Horner steps per path (3 km/h at 20 MHz: one interval per 2048
+// samples; SL = 64 covers fD <= ~420 Hz).  Larger fD, or more than CH_MAXP
+// paths, keep the per-sample sum (SL = 0).
+constexpr int JK_DEG = 5;
+constexpr int JK_MINSL = 64;
+
 // Rayleigh with every delay <= CH_HALO: the chunk plus its delay halo is staged
 // in LDS once, so the n_paths delayed taps read LDS instead of re-fetching x
 // through L1/L2 (the kernel was latency bound at ~2.2 TB/s); otherwise the
@@ -621,10 +635,11 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
                                                 R fD, R fs, const R* __restrict__ phases,
                                                 const cx<R>* __restrict__ coef, const cx<R>* __restrict__ x,
                                                 cx<R>* __restrict__ y, R* __restrict__ pow_part, int nblk,
-                                                int staged) {
+                                                int staged, int SL) {
   using V = cx<R>;
   __shared__ R red[WG / 64];
   __shared__ V xs[CH_CHUNK + CH_HALO];
+  V* jc = dyn_lds<V>();   // Taylor coefficients [sub-interval][path][degree] (SL > 0; sized by the launch)
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
   const int rx = blockIdx.y;
   const V* xf = x + (size_t)b * L;
@@ -632,6 +647,48 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
   const size_t cb = ((size_t)b * num_rx + rx) * n_paths;
   const int n0 = blk * CH_CHUNK;
   R pw = (R)0;
+  if (rayleigh && SL > 0) {
+    // time-varying taps: the Taylor coefficients first, overlapping the staging
+    // loads below (one barrier for both): one lane per (sub-interval, path,
+    // m), the 16 m of a (sub-interval, path) on 16 consecutive lanes, summed
+    // by an xor butterfly
+    const int nsub = CH_CHUNK / SL, items = nsub * n_paths * 16;
+    for (int e0 = 0; e0 < items; e0 += WG) {   // uniform trip count: every lane reaches the shuffles
+      const int e = e0 + threadIdx.x, grp = e >> 4, m = e & 15;
+      const bool ok = e < items;
+      const int sb = ok ? grp / n_paths : 0, p = ok ? grp - sb * n_paths : 0;
+      V t = mkc((R)0, (R)0);
+      R w = (R)0;
+      if (ok) {
+        const R tc = (R)(n0 + sb * SL + SL / 2) / fs;
+        R arg;
+        if constexpr (sizeof(R) == 8) {
+          const double al = 6.283185307179586 * (double)(m + 1) / 16.0;
+          w = 6.283185307179586 * fD * cos(al);
+          arg = w * tc + phases[(cb + p) * 16 + m];
+        } else {
+          const float al = 6.2831853071795864f * (float)(m + 1) / 16.0f;
+          w = 6.2831853071795864f * fD * cosf(al);
+          arg = w * tc + phases[(cb + p) * 16 + m];
+        }
+        R sv, cv;
+        if constexpr (sizeof(R) == 8) sincos(arg, &sv, &cv);
+        else sincosf(arg, &sv, &cv);
+        t = mkc(cv, sv);   // a_m, then a_m (j w_m)^k / k!
+      }
+#pragma unroll
+      for (int k = 0; k <= JK_DEG; ++k) {
+        V c = t;
+        t = mkc(-t.y * (w / (R)(k + 1)), t.x * (w / (R)(k + 1)));
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          c.x += __shfl_xor(c.x, o);
+          c.y += __shfl_xor(c.y, o);
+        }
+        if (ok && m == 0) jc[(sb * CH_MAXP + p) * (JK_DEG + 1) + k] = c;
+      }
+    }
+  }
   if (rayleigh && staged) {
     if constexpr (sizeof(R) == 4) {   // 16-B pairs of samples (L even)
       const float4* x4 = reinterpret_cast<const float4*>(xf);
@@ -649,6 +706,8 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
         xs[e] = (n >= 0 && n < L) ? xf[n] : make_double2(0.0, 0.0);
       }
     }
+    __syncthreads();
+  } else if (rayleigh && SL > 0) {
     __syncthreads();
   }
   if (rayleigh && staged && fD == (R)0 && n_paths <= CH_MAXP) {
@@ -670,6 +729,33 @@ __global__ __launch_bounds__(WG) void k_channel(int L, int num_rx, int rayleigh,
 #pragma unroll
       for (int p = 0; p < CH_MAXP; ++p)
         if (p < n_paths) v = cadd(v, cmul(cf[p], xs[n - dl[p] - n0 + CH_HALO]));
+      yf[n] = v;
+      pw += v.x * v.x + v.y * v.y;
+    }
+    const R t = block_sum(pw, red);
+    if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rx) * nblk + blk] = t;
+    return;
+  }
+  if (rayleigh && SL > 0) {
+    const R k2 = sizeof(R) == 8 ? (R)sqrt(2.0 / 16.0) : sqrtf(2.0f / 16.0f);
+#pragma unroll
+    for (int i = 0; i < CH_PER; ++i) {
+      const int n = n0 + i * WG + threadIdx.x;
+      if (n >= L) break;
+      const int sb = (n - n0) / SL;
+      const R tau = (R)(n - (n0 + sb * SL + SL / 2)) / fs;
+      V v = mkc((R)0, (R)0);
+      for (int p = 0; p < n_paths; ++p) {
+        const int src = n - delays[p];
+        if (src < 0) continue;
+        const V* cc = jc + (sb * CH_MAXP + p) * (JK_DEG + 1);
+        V H = cc[JK_DEG];
+#pragma unroll
+        for (int k = JK_DEG - 1; k >= 0; --k) H = mkc(H.x * tau + cc[k].x, H.y * tau + cc[k].y);
+        const R gn = gains[p];
+        const V hc = sizeof(R) == 8 ? mkc(gn * (H.x * k2), gn * (H.y * k2)) : mkc(H.x * (k2 * gn), H.y * (k2 * gn));
+        v = cadd(v, cmul(hc, staged ? xs[src - n0 + CH_HALO] : xf[src]));
+      }
       yf[n] = v;
       pw += v.x * v.x + v.y * v.y;
     }
@@ -708,8 +794,15 @@ int launch_channel(hipStream_t s, const Grid& g, int B, int num_rx, int rayleigh
   if (nblk != channel_nblk(g.L)) return (int)hipErrorInvalidValue;
   // f32 staging uses 16-B pairs: every frame's stream must start 16-B aligned (L even)
   const int staged = rayleigh && max_delay >= 0 && max_delay <= CH_HALO && (sizeof(R) == 8 || (g.L & 1) == 0);
-  hipLaunchKernelGGL(k_channel<R>, dim3(nblk * B, num_rx), dim3(WG), 0, s, g.L, num_rx, rayleigh, n_paths,
-                     delays_dev, gains_dev, fD, fs, phases, coef, x, y, pow_part, nblk, staged);
+  int SL = 0;   // Taylor sub-interval of the time-varying taps (0: the per-sample sum)
+  if (rayleigh && fD != (R)0 && n_paths <= CH_MAXP && phases) {
+    SL = CH_CHUNK;
+    while (SL >= JK_MINSL && 6.283185307179586 * std::fabs((double)fD) * (SL / 2) / (double)fs > 2.7e-3) SL /= 2;
+    if (SL < JK_MINSL) SL = 0;
+  }
+  const size_t shm = SL ? (size_t)(CH_CHUNK / SL) * CH_MAXP * (JK_DEG + 1) * sizeof(cx<R>) : 0;
+  hipLaunchKernelGGL(k_channel<R>, dim3(nblk * B, num_rx), dim3(WG), shm, s, g.L, num_rx, rayleigh, n_paths,
+                     delays_dev, gains_dev, fD, fs, phases, coef, x, y, pow_part, nblk, staged, SL);
   return (int)hipGetLastError();
 }
 

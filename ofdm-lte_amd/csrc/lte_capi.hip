@@ -636,8 +636,9 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
   const bool ray = channel == LTE_CH_RAYLEIGH;
   if (!ray && channel != LTE_CH_AWGN) return fail(LTE_EINVAL, "Tipo de canal desconocido");
   if (ray && (n_paths < 1 || n_paths > LTE_MAX_PATHS || !delays || !gains)) return fail(LTE_EINVAL, "bad paths");
-  // an arbitrary stream is cut into 1024-sample chunks for the f32 fD != 0
-  // expansion; f64 evaluates the Jakes sum exactly per sample
+  // an arbitrary stream is cut into 1024-sample chunks for the fD != 0
+  // expansion (f32: second order; f64: degree 5, or the per-sample sum past
+  // mimo_taylor_ok)
   const int chunk = 1024;
   Grid g{};
   g.N = chunk;
@@ -647,7 +648,7 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
   m.mode = mode == 0 ? MIMO_SFBC : MIMO_SPATIAL;
   m.num_tx = num_tx;
   m.num_rx = num_rx;
-  m.exact_jakes = sizeof(R) == 8 && ray && fD != 0.0;
+  m.exact_jakes = sizeof(R) == 8 && ray && fD != 0.0 && !mimo_taylor_ok(fD, fs, chunk);
   for (int k = 0; k < 16; ++k) m.jw[k] = 6.283185307179586 * fD * std::cos(6.283185307179586 * (k + 1) / 16.0);
   m.n_cs = (ray && fD != 0.0 && !m.exact_jakes) ? (int)((L + chunk - 1) / chunk) : 1;
   const int np = ray ? n_paths : 1;
@@ -665,7 +666,7 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
     dstp.release(); dst.release(); dphs.release(); ddel.release(); dfid.release();
   };
   if (dx.alloc((size_t)num_tx * L) || dy.alloc((size_t)num_rx * L) || dout.alloc((size_t)num_rx * L) ||
-      dcoef.alloc(links * np * m.n_cs * 3) || dpp.alloc((size_t)num_rx * nblk) || dsl.alloc(1) ||
+      dcoef.alloc(links * np * m.n_cs * mimo_ncf<R>()) || dpp.alloc((size_t)num_rx * nblk) || dsl.alloc(1) ||
       dnp.alloc(num_rx) || dfid.alloc(1) || (m.exact_jakes && dphs.alloc(links * np * 16)) ||
       (link_noise_on && (dlp.alloc(links * nblk) || dls.alloc(links)))) {
     cleanup();
@@ -1089,7 +1090,7 @@ static bool alloc_mimo(lte_plan* p, bool coded) {
   bool bad = false;
   bad |= c.x.alloc(B * m.num_tx * p->L) != 0;
   bad |= c.y.alloc(B * m.num_rx * p->L) != 0;
-  bad |= c.coef.alloc(B * links * (ray ? d.n_paths : 1) * m.n_cs * 3) != 0;
+  bad |= c.coef.alloc(B * links * (ray ? d.n_paths : 1) * m.n_cs * (p->f64 ? mimo_ncf<double>() : mimo_ncf<float>())) != 0;
   if (ray && m.exact_jakes) bad |= c.phases.alloc(B * links * d.n_paths * 16) != 0;
   if (ray && d.chain != LTE_CHAIN_SPATIAL) {
     bad |= c.link_part.alloc(B * links * p->nblk) != 0;
@@ -1266,9 +1267,11 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
     m.det = d.detector;
     m.n_dsc = sfbc ? p->res : (p->Nd + rank - 1) / rank;   // layers fill the first ceil(Nd/rank) data SCs (Q20)
     m.n_est = sfbc ? p->n_grp : p->n_sym;
-    // fD != 0: f64 evaluates the Jakes sum exactly per sample (jw[m] = (2 pi
-    // fD) cos(alpha_m), rayleighchannel.py:28-38); f32 expands it per symbol
-    m.exact_jakes = p->f64 && d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0;
+    // fD != 0: the Jakes sum expanded per OFDM symbol (f32 second order, f64
+    // degree 5); past mimo_taylor_ok f64 evaluates it per sample (jw[m] = (2 pi
+    // fD) cos(alpha_m), rayleighchannel.py:28-38)
+    m.exact_jakes = p->f64 && d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0 &&
+                    !mimo_taylor_ok(d.fD, d.fs, d.N + d.cp_len);
     for (int k = 0; k < 16; ++k) m.jw[k] = 6.283185307179586 * d.fD * std::cos(6.283185307179586 * (k + 1) / 16.0);
     m.n_cs = (d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0 && !m.exact_jakes) ? p->n_sym : 1;
     rc = plan_mimo_tables(p);

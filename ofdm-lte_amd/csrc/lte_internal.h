@@ -183,6 +183,14 @@ int launch_hard(hipStream_t s, int bps, int64_t n, const cx<R>* syms, uint8_t* b
 // SFBC 2xN (configs 4 / simulate_miso / simulate_mimo) and TM4 spatial
 // multiplexing (config 5 and its generalisation).  lte_mimo.hip.
 enum { MIMO_SFBC = 0, MIMO_SPATIAL = 1 };
+// terms per fading coefficient set: h(c + d) = sum_k c_k d^k, d in samples from
+// the set's centre (f32: degree 2; f64: degree 5, remainder under float64 rounding)
+template <class R> constexpr int mimo_ncf() { return sizeof(R) == 8 ? 6 : 3; }
+// f64 expands the Jakes sum per coefficient set when |w_max| * half-span <= 2.7e-3
+// (degree-5 remainder < 1e-17); otherwise it evaluates it per sample (exact_jakes)
+inline bool mimo_taylor_ok(double fD, double fs, int span) {
+  return 6.283185307179586 * (fD < 0 ? -fD : fD) / fs * (0.5 * span) <= 2.7e-3;
+}
 struct MimoGrid {
   int mode, num_tx, num_rx;
   int res;                 // QAM symbols per OFDM symbol: SFBC Nd&~1, spatial Nd
@@ -190,6 +198,7 @@ struct MimoGrid {
   int maxP;                // pilot stride of the per-TX tables
   int n_est;               // channel estimates per frame (SFBC: one per 14-symbol group; spatial: every symbol)
   int n_cs;                // fading coefficient sets per link path (1 if fD == 0 or exact Jakes, else n_sym)
+                           // each of mimo_ncf<R>() terms: f32 A + B d + C d^2, f64 the degree-5 Taylor
   const int32_t* np_tx;    // [num_tx] pilots of each TX
   const int32_t* ppos;     // [num_tx][maxP] pilot subcarriers of TX t
   const float2* pval;      // [num_tx][maxP] pilot symbols of TX t

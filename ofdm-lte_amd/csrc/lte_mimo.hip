@@ -154,14 +154,17 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
 // w_m = (2 pi fD) cos(2 pi (m+1)/16).
 //  * fD == 0: the constant A = g (sqrt(2/16) sum_m exp(j phi_m)) -- f64 in the
 //    reference's order (phi_m is then exactly the argument);
-//  * fD != 0, f64 (exact Jakes): the phases are stored and the channel kernels
-//    evaluate the sum per sample (link_accumulate);
-//  * fD != 0, f32: per OFDM symbol s with centre c_s the exact second-order
-//    expansion h(c_s + d) = A + B d + C d^2 (|w d| <= 1.3e-3 rad at 3 km/h,
-//    20 MHz: truncation ~1e-10, far below float32), computed in float64.
+//  * fD != 0, f64: per OFDM symbol s with centre c_s the degree-5 Taylor
+//    expansion h(c_s + d) = sum_k c_k d^k, c_k = g sqrt(2/16) sum_m a_m
+//    (j W_m)^k / k!, a_m = exp(j (w_m t_c + phi_m)) formed like one reference
+//    sample, W_m = w_m / fs (|W d| <= 1.3e-3 rad at 3 km/h, 20 MHz: remainder
+//    < 1e-17, under float64 rounding); past mimo_taylor_ok the phases are stored
+//    and the channel kernels evaluate the sum per sample (exact_jakes);
+//  * fD != 0, f32: the same expansion to second order, A + B d + C d^2
+//    (truncation ~1e-10, far below float32), computed in float64.
 // AWGN links: SFBC h = exp(j t pi/2) (core/ofdm_core.py:476-487); spatial
 // h ~ CN(0,1) (core/channel.py:473-480), injected or Philox.
-// coef layout: [B][rx][tx][path][n_cs][3] (A, B, C); phases [B][rx][tx][path][16].
+// coef layout: [B][rx][tx][path][n_cs][mimo_ncf<R>()]; phases [B][rx][tx][path][16].
 template <class R>
 __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_tx, int n_paths, int n_cs, int mode,
                                                      int rayleigh, const R* __restrict__ gains, double fD, double fs,
@@ -175,7 +178,8 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
   if (i >= B * per) return;
   const int b = i / per, rem = i - b * per, link = rem / n_paths, p = rem - link * n_paths;
   const int rx = link / num_tx, tx = link - rx * num_tx;
-  cx<R>* out = coef + (size_t)i * n_cs * 3;
+  constexpr int NCF = mimo_ncf<R>();
+  cx<R>* out = coef + (size_t)i * n_cs * NCF;
   if (!rayleigh) {
     double hr = 0.0, hi = 0.0;
     if (mode == MIMO_SFBC) {
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
       }
     }
     out[0] = mkc((R)hr, (R)hi);
-    out[1] = out[2] = mkc((R)0, (R)0);
+    for (int k = 1; k < NCF; ++k) out[k] = mkc((R)0, (R)0);
     return;
   }
   double ph[16];
@@ -214,6 +218,30 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
     }
   }
   if constexpr (F64) {
+    const double k = sqrt(2.0 / 16.0), gn = gains[p];
+    if (n_cs > 1) {   // the Taylor sets (fD != 0)
+      for (int sidx = 0; sidx < n_cs; ++sidx) {
+        const double tc = ((double)sidx * sym_len + 0.5 * (sym_len - 1)) / fs;
+        double cr[NCF], ci[NCF];
+        for (int kk = 0; kk < NCF; ++kk) cr[kk] = ci[kk] = 0.0;
+        for (int mm = 0; mm < 16; ++mm) {
+          const double w = 6.283185307179586 * fD * cos(6.283185307179586 * (double)(mm + 1) / 16.0);
+          double sv, cv;
+          sincos(w * tc + ph[mm], &sv, &cv);
+          const double W = w / fs;
+#pragma unroll
+          for (int kk = 0; kk < NCF; ++kk) {   // a_m (j W)^k / k!
+            cr[kk] += cv;
+            ci[kk] += sv;
+            const double nr = -sv * (W / (kk + 1)), ni = cv * (W / (kk + 1));
+            cv = nr;
+            sv = ni;
+          }
+        }
+        for (int kk = 0; kk < NCF; ++kk) out[sidx * NCF + kk] = make_double2(gn * (cr[kk] * k), gn * (ci[kk] * k));
+      }
+      return;
+    }
     double sr = 0.0, si = 0.0;
     for (int mm = 0; mm < 16; ++mm) {
       double sv, cv;
@@ -221,9 +249,8 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
       sr += cv;
       si += sv;
     }
-    const double k = sqrt(2.0 / 16.0), gn = gains[p];
     out[0] = make_double2(gn * (sr * k), gn * (si * k));
-    out[1] = out[2] = make_double2(0.0, 0.0);
+    for (int kk = 1; kk < NCF; ++kk) out[kk] = make_double2(0.0, 0.0);
     if (phases)
       for (int mm = 0; mm < 16; ++mm) phases[(size_t)i * 16 + mm] = ph[mm];
     return;
@@ -294,37 +321,38 @@ __device__ __noinline__ double2 jakes_exact(const MimoGrid& m, const double (&ph
 }
 
 // one link's output at a single sample n (link_sample: coefficient triples of
-// n's symbol; f64 exact Jakes when ph is set)
-template <class R>
+// n's symbol; EX: f64 exact Jakes from the phases ph)
+template <class R, bool EX>
 __device__ __forceinline__ cx<R> link_value(int n, const cx<R>* __restrict__ cf, int n_cs, int np, int sym_len,
                                             const int32_t* __restrict__ delays, const cx<R>* __restrict__ xf,
                                             const R* __restrict__ ph, const R* __restrict__ gains, const MimoGrid& m,
                                             double fs) {
   using V = cx<R>;
   V acc = mkc((R)0, (R)0);
-  if constexpr (sizeof(R) == 8) {
-    if (ph) {
-      for (int p = 0; p < np; ++p) {
-        const int src = n - (delays ? delays[p] : 0);
-        if (src < 0) continue;
-        double phv[16];
+  if constexpr (EX) {
+    static_assert(sizeof(R) == 8, "exact Jakes is the float64 path");
+    for (int p = 0; p < np; ++p) {
+      const int src = n - (delays ? delays[p] : 0);
+      if (src < 0) continue;
+      double phv[16];
 #pragma unroll
-        for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
-        acc = cadd(acc, cmul(jakes_exact(m, phv, gains[p], n, fs), xf[src]));
-      }
-      return acc;
+      for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
+      acc = cadd(acc, cmul(jakes_exact(m, phv, gains[p], n, fs), xf[src]));
     }
+    return acc;
   }
+  constexpr int NCF = mimo_ncf<R>();
   const int sidx = n_cs > 1 ? n / sym_len : 0;
   const R d = n_cs > 1 ? (R)(n - sidx * sym_len) - (R)0.5 * (R)(sym_len - 1) : (R)0;
   for (int p = 0; p < np; ++p) {
     const int src = n - (delays ? delays[p] : 0);
     if (src < 0) continue;
-    const V* c = cf + ((size_t)p * n_cs + sidx) * 3;
+    const V* c = cf + ((size_t)p * n_cs + sidx) * NCF;
     V h = c[0];
-    if (n_cs > 1) {   // A + B d + C d^2
-      h.x += d * (c[1].x + d * c[2].x);
-      h.y += d * (c[1].y + d * c[2].y);
+    if (n_cs > 1) {   // sum_k c_k d^k (Horner)
+      h = c[NCF - 1];
+#pragma unroll
+      for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * d + c[k].x, h.y * d + c[k].y);
     }
     acc = cadd(acc, cmul(h, xf[src]));
   }
@@ -351,8 +379,10 @@ struct SymSpan {
 };
 
 // acc[j] += sum_p h_p(n_j) x[n_j - delay_p] for one link (cs: the link's
-// coefficients at this symbol, stride n_cs*3 per path; ph: f64 exact Jakes)
-template <class R, int J>
+// coefficients at this symbol, stride n_cs * mimo_ncf per path; EX: f64 exact
+// Jakes from the phases ph -- a separate instance, so that its sincos calls do
+// not set the register budget of the coefficient path)
+template <class R, int J, bool EX>
 __device__ __forceinline__ void link_accumulate(cx<R> (&acc)[J], const SymSpan<J>& sp, const cx<R>* __restrict__ cs,
                                                 int n_cs, int np, const int32_t* __restrict__ delays,
                                                 const cx<R>* __restrict__ xf, const R* __restrict__ ph,
@@ -366,26 +396,30 @@ __device__ __forceinline__ void link_accumulate(cx<R> (&acc)[J], const SymSpan<J
       const int src = sp.n[j] - dl;
       xs[j] = (sp.ok[j] && src >= 0) ? xf[src] : mkc((R)0, (R)0);
     }
-    if constexpr (sizeof(R) == 8) {
-      if (ph) {
-        double phv[16];
+    if constexpr (EX) {
+      static_assert(sizeof(R) == 8, "exact Jakes is the float64 path");
+      double phv[16];
 #pragma unroll
-        for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
-        const double gn = gains[p];
+      for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
+      const double gn = gains[p];
 #pragma unroll
-        for (int j = 0; j < J; ++j)
-          if (sp.ok[j] && sp.n[j] >= dl) acc[j] = cadd(acc[j], cmul(jakes_exact(m, phv, gn, sp.n[j], fs), xs[j]));
-        continue;
-      }
+      for (int j = 0; j < J; ++j)
+        if (sp.ok[j] && sp.n[j] >= dl) acc[j] = cadd(acc[j], cmul(jakes_exact(m, phv, gn, sp.n[j], fs), xs[j]));
+      continue;
     }
-    const V* c = cs + (size_t)p * n_cs * 3;
+    constexpr int NCF = mimo_ncf<R>();
+    const V* c = cs + (size_t)p * n_cs * NCF;
     const V c0 = c[0];
-    if (n_cs > 1) {   // A + B d + C d^2
-      const V c1 = c[1], c2 = c[2];
+    if (n_cs > 1) {   // sum_k c_k d^k (Horner; f32: A + B d + C d^2)
+      V cc[NCF];
+#pragma unroll
+      for (int k = 0; k < NCF; ++k) cc[k] = c[k];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const R dj = (R)sp.d[j];
-        const V h = mkc(c0.x + dj * (c1.x + dj * c2.x), c0.y + dj * (c1.y + dj * c2.y));
+        V h = cc[NCF - 1];
+#pragma unroll
+        for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * dj + cc[k].x, h.y * dj + cc[k].y);
         acc[j] = cadd(acc[j], cmul(h, xs[j]));
       }
     } else {
@@ -411,7 +445,7 @@ __device__ __forceinline__ cx<R> link_noise_at(int n, R sg, const R* __restrict_
 
 // pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
 // one block per (frame, OFDM symbol, link)
-template <class R, int J>
+template <class R, int J, bool EX>
 __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                     const int32_t* __restrict__ delays, const cx<R>* __restrict__ coef,
                                                     const R* __restrict__ phases, const R* __restrict__ gains,
@@ -425,7 +459,7 @@ __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_t
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
   const float dc = 0.5f * (float)(sym_len - 1);
   const size_t lk = (size_t)b * num_rx * num_tx + link;
-  const V* cs = coef + lk * np * n_cs * 3 + (size_t)sidx * 3;
+  const V* cs = coef + lk * np * n_cs * mimo_ncf<R>() + (size_t)sidx * mimo_ncf<R>();
   const R* ph = phases ? phases + lk * np * 16 : nullptr;
   const V* xf = x + ((size_t)b * num_tx + tx) * L;
   R v = (R)0;
@@ -434,7 +468,7 @@ __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_t
     V acc[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j] = mkc((R)0, (R)0);
-    link_accumulate<R, J>(acc, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
+    link_accumulate<R, J, EX>(acc, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
 #pragma unroll
     for (int j = 0; j < J; ++j)
       if (sp.ok[j]) v += acc[j].x * acc[j].x + acc[j].y * acc[j].y;
@@ -462,7 +496,7 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
 constexpr int MC_MAXRX = 8;   // receive antennas per launch
 constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the transmit streams
 
-template <class R, int J>
+template <class R, int J, bool EX>
 __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
                                                       const cx<R>* __restrict__ coef, const R* __restrict__ phases,
@@ -498,14 +532,14 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
           const int r = rg + q;
           if (r >= num_rx) break;
           const size_t link = (size_t)r * num_tx + tx, lk = (size_t)b * nl + link;
-          const V* cs = coef + lk * np * n_cs * 3 + (size_t)sidx * 3;
+          const V* cs = coef + lk * np * n_cs * mimo_ncf<R>() + (size_t)sidx * mimo_ncf<R>();
           const R* ph = phases ? phases + lk * np * 16 : nullptr;
           const R* zf = inj_lz ? inj_lz + (size_t)b * inj_lz_stride + link * 2 * L : nullptr;
           if constexpr (F64) {   // y_link from zero, then signals_rx += y_link
             V vl[J];
 #pragma unroll
             for (int j = 0; j < J; ++j) vl[j] = mkc((R)0, (R)0);
-            link_accumulate<R, J>(vl, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
+            link_accumulate<R, J, EX>(vl, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
             if (link_sigma) {
               const R sg = link_sigma[lk];
 #pragma unroll
@@ -515,7 +549,7 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
 #pragma unroll
             for (int j = 0; j < J; ++j) v[q][j] = cadd(v[q][j], vl[j]);
           } else {
-            link_accumulate<R, J>(v[q], sp, cs, n_cs, np, delays, xf, nullptr, gains, m, fs);
+            link_accumulate<R, J, false>(v[q], sp, cs, n_cs, np, delays, xf, nullptr, gains, m, fs);
             if (link_sigma) {
               const R sg = link_sigma[lk];
 #pragma unroll
@@ -561,22 +595,33 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   if (nch > nblk) return (int)hipErrorInvalidValue;   // partial buffers are sized for nblk blocks
   const R* ph = m.exact_jakes ? phases : nullptr;
   if (m.exact_jakes && (!phases || !gains)) return (int)hipErrorInvalidValue;
-  // samples per thread per pass: the smallest instantiated J covering one symbol (larger symbols loop)
+  // samples per thread per pass: the smallest instantiated J covering one symbol
+  // (larger symbols loop); float64 at most 3 -- its accumulators v[MC_RXG][J]
+  // take 16 J VGPRs, and J = 9 spilled to scratch at one wave per SIMD
   const int jn = (sym_len + MWG - 1) / MWG;
-  const int J = jn <= 1 ? 1 : jn <= 2 ? 2 : jn <= 3 ? 3 : jn <= 5 ? 5 : jn <= 7 ? 7 : 9;
-#define LTE_CHM(J_)                                                                                                 \
+  int J = jn <= 1 ? 1 : jn <= 2 ? 2 : jn <= 3 ? 3 : jn <= 5 ? 5 : jn <= 7 ? 7 : 9;
+  if (sizeof(R) == 8 && J > 3) J = 3;
+#define LTE_CHM_EX(J_, EX_)                                                                                         \
   do {                                                                                                             \
     if (link_noise) {                                                                                              \
-      hipLaunchKernelGGL((k_link_power<R, J_>), dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L,          \
+      hipLaunchKernelGGL((k_link_power<R, J_, EX_>), dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L,     \
                          m.num_rx, m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x,          \
                          link_part, nch);                                                                          \
       const int nl = B * m.num_rx * m.num_tx;                                                                      \
       hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L,        \
                          link_sigma);                                                                              \
     }                                                                                                              \
-    hipLaunchKernelGGL((k_channel_mimo<R, J_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, n_paths,  \
+    hipLaunchKernelGGL((k_channel_mimo<R, J_, EX_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx,      \
+                       n_paths,                                                                                    \
                        m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x, y, link_noise ? link_sigma : nullptr,   \
                        fid, seed, inj_lz, inj_lz_stride, pow_part, nch);                                           \
+  } while (0)
+#define LTE_CHM(J_)                                                                                                 \
+  do {                                                                                                             \
+    if constexpr (sizeof(R) == 8) {                                                                                \
+      if (m.exact_jakes) { LTE_CHM_EX(J_, true); break; }                                                          \
+    }                                                                                                              \
+    LTE_CHM_EX(J_, false);                                                                                         \
   } while (0)
   switch (J) {
     case 1: LTE_CHM(1); break;
@@ -587,13 +632,14 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
     default: LTE_CHM(9); break;
   }
 #undef LTE_CHM
+#undef LTE_CHM_EX
   return (int)hipGetLastError();
 }
 
 // Per-link statistics for the reported channel matrix (transmit_mimo,
 // core/ofdm_core.py:505-516): mean|x|^2, mean|y_link|^2, mean(y_link conj(x)),
 // y_link with its link noise when link_sigma is set (the reference's y).
-template <class R>
+template <class R, bool EX>
 __global__ __launch_bounds__(MWG) void k_link_stats_part(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                          const int32_t* __restrict__ delays,
                                                          const cx<R>* __restrict__ coef, const R* __restrict__ phases,
@@ -612,8 +658,8 @@ __global__ __launch_bounds__(MWG) void k_link_stats_part(int L, int num_rx, int 
   R v[4] = {(R)0, (R)0, (R)0, (R)0};
   if (n < L) {
     const V* xf = x + ((size_t)b * num_tx + tx) * L;
-    const V* cf = coef + lk * np * n_cs * 3;
-    V yv = link_value<R>(n, cf, n_cs, np, sym_len, delays, xf, phases ? phases + lk * np * 16 : nullptr, gains, m, fs);
+    const V* cf = coef + lk * np * n_cs * mimo_ncf<R>();
+    V yv = link_value<R, EX>(n, cf, n_cs, np, sym_len, delays, xf, EX ? phases + lk * np * 16 : nullptr, gains, m, fs);
     if (link_sigma) {
       const R* zf = inj_lz ? inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L : nullptr;
       yv = link_noise_at<R>(n, link_sigma[lk], zf, L, seed, fid[b], link, yv);
@@ -647,9 +693,17 @@ int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, in
                       const R* link_sigma, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
                       R* part, int nblk, R* stats) {
   if (nblk < (g.L + MWG - 1) / MWG) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_link_stats_part<R>, dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L, m.num_rx,
-                     m.num_tx, n_paths, m.n_cs, g.N + g.cp, delays, coef, m.exact_jakes ? phases : nullptr, gains, fs,
-                     m, x, link_sigma, fid, seed, inj_lz, inj_lz_stride, part, nblk);
+  if (m.exact_jakes && !phases) return (int)hipErrorInvalidValue;
+#define LTE_LSP(EX_)                                                                                                 \
+  hipLaunchKernelGGL((k_link_stats_part<R, EX_>), dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L,         \
+                     m.num_rx, m.num_tx, n_paths, m.n_cs, g.N + g.cp, delays, coef, phases, gains, fs, m, x,          \
+                     link_sigma, fid, seed, inj_lz, inj_lz_stride, part, nblk)
+  bool done = false;
+  if constexpr (sizeof(R) == 8) {
+    if (m.exact_jakes) { LTE_LSP(true); done = true; }
+  }
+  if (!done) LTE_LSP(false);
+#undef LTE_LSP
   const int n = B * m.num_rx * m.num_tx * 4;
   hipLaunchKernelGGL(k_link_stats_fin<R>, dim3((n + 255) / 256), dim3(256), 0, s, n, part, nblk, g.L, stats);
   return (int)hipGetLastError();

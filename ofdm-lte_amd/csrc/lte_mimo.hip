@@ -378,16 +378,24 @@ struct SymSpan {
   }
 };
 
-// acc[j] += sum_p h_p(n_j) x[n_j - delay_p] for one link (cs: the link's
-// coefficients at this symbol, stride n_cs * mimo_ncf per path; EX: f64 exact
-// Jakes from the phases ph -- a separate instance, so that its sincos calls do
-// not set the register budget of the coefficient path)
+constexpr int MC_MAXRX = 8;   // receive antennas per launch
+constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the transmit streams
+
+// acc[q][j] += sum_p h_{rx q, tx, p}(n_j) x_tx[n_j - delay_p] for the nq <=
+// MC_RXG receive antennas of a group and one transmit stream: each delayed TX
+// sample is loaded once for all of them (the group's links share the TX
+// stream).  cs: the first link's coefficients at this symbol (stride n_cs *
+// mimo_ncf per path, cs_q per receive antenna); EX: f64 exact Jakes from the
+// phases ph (ph_q per receive antenna) -- a separate instance, so that its
+// sincos calls do not set the register budget of the coefficient path.
 template <class R, int J, bool EX>
-__device__ __forceinline__ void link_accumulate(cx<R> (&acc)[J], const SymSpan<J>& sp, const cx<R>* __restrict__ cs,
-                                                int n_cs, int np, const int32_t* __restrict__ delays,
-                                                const cx<R>* __restrict__ xf, const R* __restrict__ ph,
-                                                const R* __restrict__ gains, const MimoGrid& m, double fs) {
+__device__ __forceinline__ void links_accumulate(cx<R> (&acc)[MC_RXG][J], int nq, const SymSpan<J>& sp,
+                                                 const cx<R>* __restrict__ cs, size_t cs_q, int n_cs, int np,
+                                                 const int32_t* __restrict__ delays, const cx<R>* __restrict__ xf,
+                                                 const R* __restrict__ ph, size_t ph_q, const R* __restrict__ gains,
+                                                 const MimoGrid& m, double fs) {
   using V = cx<R>;
+  constexpr int NCF = mimo_ncf<R>();
   for (int p = 0; p < np; ++p) {
     const int dl = delays ? delays[p] : 0;
     V xs[J];
@@ -396,35 +404,39 @@ __device__ __forceinline__ void link_accumulate(cx<R> (&acc)[J], const SymSpan<J
       const int src = sp.n[j] - dl;
       xs[j] = (sp.ok[j] && src >= 0) ? xf[src] : mkc((R)0, (R)0);
     }
-    if constexpr (EX) {
-      static_assert(sizeof(R) == 8, "exact Jakes is the float64 path");
-      double phv[16];
 #pragma unroll
-      for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
-      const double gn = gains[p];
+    for (int q = 0; q < MC_RXG; ++q) {
+      if (q >= nq) break;
+      if constexpr (EX) {
+        static_assert(sizeof(R) == 8, "exact Jakes is the float64 path");
+        double phv[16];
 #pragma unroll
-      for (int j = 0; j < J; ++j)
-        if (sp.ok[j] && sp.n[j] >= dl) acc[j] = cadd(acc[j], cmul(jakes_exact(m, phv, gn, sp.n[j], fs), xs[j]));
-      continue;
-    }
-    constexpr int NCF = mimo_ncf<R>();
-    const V* c = cs + (size_t)p * n_cs * NCF;
-    const V c0 = c[0];
-    if (n_cs > 1) {   // sum_k c_k d^k (Horner; f32: A + B d + C d^2)
-      V cc[NCF];
+        for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[q * ph_q + p * 16 + mm];
+        const double gn = gains[p];
 #pragma unroll
-      for (int k = 0; k < NCF; ++k) cc[k] = c[k];
+        for (int j = 0; j < J; ++j)
+          if (sp.ok[j] && sp.n[j] >= dl)
+            acc[q][j] = cadd(acc[q][j], cmul(jakes_exact(m, phv, gn, sp.n[j], fs), xs[j]));
+      } else {
+        const V* c = cs + q * cs_q + (size_t)p * n_cs * NCF;
+        if (n_cs > 1) {   // sum_k c_k d^k (Horner; f32: A + B d + C d^2)
+          V cc[NCF];
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const R dj = (R)sp.d[j];
-        V h = cc[NCF - 1];
+          for (int k = 0; k < NCF; ++k) cc[k] = c[k];
 #pragma unroll
-        for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * dj + cc[k].x, h.y * dj + cc[k].y);
-        acc[j] = cadd(acc[j], cmul(h, xs[j]));
+          for (int j = 0; j < J; ++j) {
+            const R dj = (R)sp.d[j];
+            V h = cc[NCF - 1];
+#pragma unroll
+            for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * dj + cc[k].x, h.y * dj + cc[k].y);
+            acc[q][j] = cadd(acc[q][j], cmul(h, xs[j]));
+          }
+        } else {
+          const V c0 = c[0];
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[q][j] = cadd(acc[q][j], cmul(c0, xs[j]));
+        }
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < J; ++j) acc[j] = cadd(acc[j], cmul(c0, xs[j]));
     }
   }
 }
@@ -444,7 +456,7 @@ __device__ __forceinline__ cx<R> link_noise_at(int n, R sg, const R* __restrict_
 }
 
 // pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
-// one block per (frame, OFDM symbol, link)
+// one block per (frame, OFDM symbol, TX stream), the receive antennas in groups
 template <class R, int J, bool EX>
 __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                     const int32_t* __restrict__ delays, const cx<R>* __restrict__ coef,
@@ -452,29 +464,45 @@ __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_t
                                                     double fs, MimoGrid m, const cx<R>* __restrict__ x,
                                                     R* __restrict__ part, int nblk) {
   using V = cx<R>;
+  constexpr int NCF = mimo_ncf<R>();
   __shared__ R red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
-  const int link = blockIdx.y, tx = link % num_tx;
+  const int tx = blockIdx.y;
   const int sidx = n_cs > 1 ? blk : 0;
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
   const float dc = 0.5f * (float)(sym_len - 1);
-  const size_t lk = (size_t)b * num_rx * num_tx + link;
-  const V* cs = coef + lk * np * n_cs * mimo_ncf<R>() + (size_t)sidx * mimo_ncf<R>();
-  const R* ph = phases ? phases + lk * np * 16 : nullptr;
   const V* xf = x + ((size_t)b * num_tx + tx) * L;
-  R v = (R)0;
-  for (int base = nbeg; base < nend; base += J * MWG) {
-    const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
-    V acc[J];
+  const size_t cs_q = (size_t)num_tx * np * n_cs * NCF, ph_q = (size_t)num_tx * np * 16;
+  for (int rg = 0; rg < num_rx; rg += MC_RXG) {
+    const int nq = min(MC_RXG, num_rx - rg);
+    const size_t lk0 = ((size_t)b * num_rx + rg) * num_tx + tx;
+    const V* cs = coef + lk0 * np * n_cs * NCF + (size_t)sidx * NCF;
+    const R* ph = EX ? phases + lk0 * np * 16 : nullptr;
+    R pw[MC_RXG];
 #pragma unroll
-    for (int j = 0; j < J; ++j) acc[j] = mkc((R)0, (R)0);
-    link_accumulate<R, J, EX>(acc, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
+    for (int q = 0; q < MC_RXG; ++q) pw[q] = (R)0;
+    for (int base = nbeg; base < nend; base += J * MWG) {
+      const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
+      V acc[MC_RXG][J];
 #pragma unroll
-    for (int j = 0; j < J; ++j)
-      if (sp.ok[j]) v += acc[j].x * acc[j].x + acc[j].y * acc[j].y;
+      for (int q = 0; q < MC_RXG; ++q)
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[q][j] = mkc((R)0, (R)0);
+      links_accumulate<R, J, EX>(acc, nq, sp, cs, cs_q, n_cs, np, delays, xf, ph, ph_q, gains, m, fs);
+#pragma unroll
+      for (int q = 0; q < MC_RXG; ++q)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (sp.ok[j]) pw[q] += acc[q][j].x * acc[q][j].x + acc[q][j].y * acc[q][j].y;
+    }
+#pragma unroll
+    for (int q = 0; q < MC_RXG; ++q) {
+      if (q >= nq) break;
+      const R t = block_sum(pw[q], red);
+      if (threadIdx.x == 0) part[(lk0 + (size_t)q * num_tx) * nblk + blk] = t;
+      __syncthreads();
+    }
   }
-  const R t = block_sum(v, red);
-  if (threadIdx.x == 0) part[lk * nblk + blk] = t;
 }
 
 // sigma of the link noise: sqrt((mean|y0|^2 / 10^(100/10)) / 2)
@@ -488,14 +516,10 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
 }
 
 // One block per (frame, OFDM symbol): the symbol index -- hence every link
-// path's fading coefficients (A, B, C) -- is uniform over the block, so they
-// are scalar loads; the sample offset d from the symbol centre is per lane.
-// All RX of the frame per block: each TX stream sample is loaded once for
-// every RX (the [rx][tx] link loop runs on registers), one power reduction
-// per RX.
-constexpr int MC_MAXRX = 8;   // receive antennas per launch
-constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the transmit streams
-
+// path's fading coefficients -- is uniform over the block, so they are scalar
+// loads; the sample offset d from the symbol centre is per lane.  All RX of
+// the frame per block: each delayed TX sample is loaded once for a group of
+// MC_RXG receive antennas (links_accumulate), one power reduction per RX.
 template <class R, int J, bool EX>
 __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
@@ -508,13 +532,16 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
                                                       R* __restrict__ pow_part, int nblk) {
   using V = cx<R>;
   constexpr bool F64 = sizeof(R) == 8;
+  constexpr int NCF = mimo_ncf<R>();
   __shared__ R red[MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;   // blk = OFDM symbol (block of sym_len samples)
   const int sidx = n_cs > 1 ? blk : 0;
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
   const float dc = 0.5f * (float)(sym_len - 1);
   const size_t nl = (size_t)num_rx * num_tx;
+  const size_t cs_q = (size_t)num_tx * np * n_cs * NCF, ph_q = (size_t)num_tx * np * 16;
   for (int rg = 0; rg < num_rx; rg += MC_RXG) {
+    const int nq = min(MC_RXG, num_rx - rg);
     R pw[MC_RXG];
 #pragma unroll
     for (int q = 0; q < MC_RXG; ++q) pw[q] = (R)0;
@@ -527,42 +554,41 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
         for (int j = 0; j < J; ++j) v[q][j] = mkc((R)0, (R)0);
       for (int tx = 0; tx < num_tx; ++tx) {
         const V* xf = x + ((size_t)b * num_tx + tx) * L;
+        const size_t lk0 = (size_t)b * nl + (size_t)rg * num_tx + tx;
+        const V* cs = coef + lk0 * np * n_cs * NCF + (size_t)sidx * NCF;
+        const R* ph = EX ? phases + lk0 * np * 16 : nullptr;
+        // f64: each link's y from zero, then signals_rx += y_link (the
+        // reference's order); f32 accumulates into the RX sums directly
+        V vl[MC_RXG][J];
+        V (&acc)[MC_RXG][J] = F64 ? vl : v;
+        if constexpr (F64) {
+#pragma unroll
+          for (int q = 0; q < MC_RXG; ++q)
+#pragma unroll
+            for (int j = 0; j < J; ++j) vl[q][j] = mkc((R)0, (R)0);
+        }
+        links_accumulate<R, J, EX>(acc, nq, sp, cs, cs_q, n_cs, np, delays, xf, ph, ph_q, gains, m, fs);
 #pragma unroll
         for (int q = 0; q < MC_RXG; ++q) {
-          const int r = rg + q;
-          if (r >= num_rx) break;
-          const size_t link = (size_t)r * num_tx + tx, lk = (size_t)b * nl + link;
-          const V* cs = coef + lk * np * n_cs * mimo_ncf<R>() + (size_t)sidx * mimo_ncf<R>();
-          const R* ph = phases ? phases + lk * np * 16 : nullptr;
-          const R* zf = inj_lz ? inj_lz + (size_t)b * inj_lz_stride + link * 2 * L : nullptr;
-          if constexpr (F64) {   // y_link from zero, then signals_rx += y_link
-            V vl[J];
+          if (q >= nq) break;
+          const int link = (rg + q) * num_tx + tx;
+          if (link_sigma) {
+            const R sg = link_sigma[(size_t)b * nl + link];
+            const R* zf = inj_lz ? inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L : nullptr;
 #pragma unroll
-            for (int j = 0; j < J; ++j) vl[j] = mkc((R)0, (R)0);
-            link_accumulate<R, J, EX>(vl, sp, cs, n_cs, np, delays, xf, ph, gains, m, fs);
-            if (link_sigma) {
-              const R sg = link_sigma[lk];
+            for (int j = 0; j < J; ++j)
+              if (sp.ok[j]) acc[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, acc[q][j]);
+          }
+          if constexpr (F64) {
 #pragma unroll
-              for (int j = 0; j < J; ++j)
-                if (sp.ok[j]) vl[j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], (int)link, vl[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < J; ++j) v[q][j] = cadd(v[q][j], vl[j]);
-          } else {
-            link_accumulate<R, J, false>(v[q], sp, cs, n_cs, np, delays, xf, nullptr, gains, m, fs);
-            if (link_sigma) {
-              const R sg = link_sigma[lk];
-#pragma unroll
-              for (int j = 0; j < J; ++j)
-                if (sp.ok[j]) v[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], (int)link, v[q][j]);
-            }
+            for (int j = 0; j < J; ++j) v[q][j] = cadd(v[q][j], vl[q][j]);
           }
         }
       }
 #pragma unroll
       for (int q = 0; q < MC_RXG; ++q) {
+        if (q >= nq) break;
         const int r = rg + q;
-        if (r >= num_rx) break;
 #pragma unroll
         for (int j = 0; j < J; ++j)
           if (sp.ok[j]) {
@@ -573,10 +599,9 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
     }
 #pragma unroll
     for (int q = 0; q < MC_RXG; ++q) {
-      const int r = rg + q;
-      if (r >= num_rx) break;
+      if (q >= nq) break;
       const R t = block_sum(pw[q], red);
-      if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
+      if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rg + q) * nblk + blk] = t;
       __syncthreads();
     }
   }
@@ -595,16 +620,19 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   if (nch > nblk) return (int)hipErrorInvalidValue;   // partial buffers are sized for nblk blocks
   const R* ph = m.exact_jakes ? phases : nullptr;
   if (m.exact_jakes && (!phases || !gains)) return (int)hipErrorInvalidValue;
-  // samples per thread per pass: the smallest instantiated J covering one symbol
-  // (larger symbols loop); float64 at most 3 -- its accumulators v[MC_RXG][J]
-  // take 16 J VGPRs, and J = 9 spilled to scratch at one wave per SIMD
+  // samples per thread per pass: the smallest instantiated J covering one
+  // symbol, at most 2 (f64) / 3 (f32) -- larger symbols loop.  The RX-group
+  // accumulators take 4 MC_RXG J VGPRs per component pair (f64: v and the
+  // per-link vl); measured J = 1 / 2 / 3 / 5 at 20 MHz, f64 config 5 channel
+  // 6.0 / 6.0 / 6.8 / 11.2 ms and 3 km/h 26.9 / 19.3 / 27.1 / 41.9 ms per 8192
+  // frames; f32 4.2 / 3.1 / 3.0 / 3.2 and 15.9 / 11.0 / 9.6 / 11.3 ms
   const int jn = (sym_len + MWG - 1) / MWG;
-  int J = jn <= 1 ? 1 : jn <= 2 ? 2 : jn <= 3 ? 3 : jn <= 5 ? 5 : jn <= 7 ? 7 : 9;
-  if (sizeof(R) == 8 && J > 3) J = 3;
+  const int jmax = sizeof(R) == 8 ? 2 : 3;
+  const int J = jn <= 1 ? 1 : jn <= 2 || jmax == 2 ? 2 : 3;
 #define LTE_CHM_EX(J_, EX_)                                                                                         \
   do {                                                                                                             \
     if (link_noise) {                                                                                              \
-      hipLaunchKernelGGL((k_link_power<R, J_, EX_>), dim3(nch * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L,     \
+      hipLaunchKernelGGL((k_link_power<R, J_, EX_>), dim3(nch * B, m.num_tx), dim3(MWG), 0, s, g.L,               \
                          m.num_rx, m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x,          \
                          link_part, nch);                                                                          \
       const int nl = B * m.num_rx * m.num_tx;                                                                      \
@@ -626,10 +654,7 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   switch (J) {
     case 1: LTE_CHM(1); break;
     case 2: LTE_CHM(2); break;
-    case 3: LTE_CHM(3); break;
-    case 5: LTE_CHM(5); break;
-    case 7: LTE_CHM(7); break;
-    default: LTE_CHM(9); break;
+    default: LTE_CHM(3); break;
   }
 #undef LTE_CHM
 #undef LTE_CHM_EX

@@ -200,7 +200,7 @@ def test_transmit_mimo_stage(C, golden_mimo, chan, prec):
 @pytest.mark.parametrize('chan', ['awgn', 'rayleigh_mp'])
 def test_transmit_spatial_multiplexing_stage(C, golden_mimo, chan, prec):
     """ChannelSimulator.transmit_spatial_multiplexing (a13), 4x4, PedA 3 km/h
-    (time-varying Jakes: f64 the exact sum per sample) == the reference on the
+    (time-varying Jakes: f64 degree-5 Taylor sets per OFDM symbol) == the reference on the
     same seed (streams f64 1e-12, f32 1e-5 relative)."""
     import lte_phy
     cs = lte_phy.ChannelSimulator(channel_type=chan, snr_db=18.0, fs=30.72e6, itu_profile='Pedestrian_A',

@@ -118,3 +118,53 @@ def test_run_grid_3kmh_sharding_invariant(C, prec):
     b1 = sim.run_grid([10.0, 24.0], 24, seed=7, coded=True, rank=1, world_size=2)
     assert np.array_equal(a['counts'], b0['counts'] + b1['counts'])
     assert a['ber'][1] <= a['ber'][0]
+
+
+# Faster UEs than the 3 km/h goldens cover: the channel stages against the
+# oracle's per-sample Jakes sum (oracle/lte_oracle.py multipath / jakes,
+# core/rayleighchannel.py:20-58) on the same global-RNG draws.  20 MHz,
+# fs = 30.72 MHz, 2 GHz: 30 km/h (fD 55.6 Hz), 120 km/h (222 Hz) and 500 km/h
+# (926 Hz).  SISO: the Taylor sub-intervals shrink to 64 samples by 120 km/h
+# and give way to the per-sample sum past ~227 km/h (k_channel); the 4x4
+# spatial links take the per-symbol Taylor sets up to ~6.5 km/h, the
+# per-sample exact sum beyond (k_channel_mimo<.., EX>).  float32 keeps its
+# per-symbol quadratic at every speed (truncation (|W| S / 2)^3 / 6: ~2e-5 at
+# 120 km/h), so it is held to 1e-5 up to 120 km/h only.
+@pytest.mark.parametrize('prec,tol', [('f64', 1e-12), ('f32', 1e-5)])
+@pytest.mark.parametrize('kmh', [30.0, 120.0, 500.0])
+def test_ofdm_channel_transmit_moving_vs_oracle(C, oracle, kmh, prec, tol):
+    import lte_phy
+    num = oracle.Numerology(bandwidth=20.0, modulation='64-QAM')
+    rs = np.random.RandomState(5)
+    x = (rs.randn(30000) + 1j * rs.randn(30000)) / np.sqrt(2)
+    ch = lte_phy.OFDMChannel('rayleigh_mp', 15.0, num.fs, itu_profile='Pedestrian_A', frequency_ghz=2.0,
+                             velocity_kmh=kmh, precision=prec)
+    np.random.seed(1234)
+    y = ch.transmit(x)
+    st = _state_head()
+    np.random.seed(1234)
+    assert ch.fD == oracle.doppler_hz(2.0, kmh)
+    ref = oracle.channel_transmit(num, x, 'rayleigh_mp', 15.0, 'Pedestrian_A', fD=ch.fD)
+    assert np.array_equal(st, _state_head())
+    assert np.linalg.norm(y - ref) / np.linalg.norm(ref) < tol
+
+
+@pytest.mark.parametrize('prec,tol,kmh', [('f64', 1e-12, 30.0), ('f64', 1e-12, 120.0), ('f64', 1e-12, 500.0),
+                                          ('f32', 1e-5, 30.0), ('f32', 1e-5, 120.0)])
+def test_spatial_multiplexing_channel_moving_vs_oracle(C, mimo_oracle, oracle, kmh, prec, tol):
+    import lte_phy
+    num = oracle.Numerology(bandwidth=20.0, modulation='64-QAM')
+    rs = np.random.RandomState(6)
+    xs = [(rs.randn(8 * 2192) + 1j * rs.randn(8 * 2192)) / np.sqrt(2) for _ in range(4)]
+    cs = lte_phy.ChannelSimulator(channel_type='rayleigh_mp', snr_db=18.0, fs=num.fs, itu_profile='Pedestrian_A',
+                                  frequency_ghz=2.0, velocity_kmh=kmh, verbose=False, precision=prec)
+    np.random.seed(4321)
+    ys, Hm = cs.transmit_spatial_multiplexing(list(xs), num_rx=4)
+    st = _state_head()
+    np.random.seed(4321)
+    ref, Href = mimo_oracle.transmit_sm(num, xs, 4, 'rayleigh_mp', 18.0, 'Pedestrian_A',
+                                        fD=oracle.doppler_hz(2.0, kmh))
+    assert np.array_equal(st, _state_head())
+    for r in range(4):
+        assert np.linalg.norm(ys[r] - ref[r]) / np.linalg.norm(ref[r]) < tol, r
+    assert np.allclose(Hm, Href, rtol=1e-9 if prec == 'f64' else 1e-5, atol=1e-12 if prec == 'f64' else 1e-6)

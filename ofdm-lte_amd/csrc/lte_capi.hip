@@ -348,7 +348,7 @@ struct TableSet {  // device copies of the static grid tables for one N (f64 cop
 // per-precision device buffers of the signal chains (R = float / double)
 template <class R>
 struct ChainBufs {
-  DBuf<cx<R>> x, y, coef, H, capbuf, captx, xh;
+  DBuf<cx<R>> x, y, coef, H, capbuf, captx, xh, tcoef;
   DBuf<R> gains, phases, pow_part, pstats, npow, llr, snr_lin, inj_ph, inj_z;
   // multi-antenna chains: received data SCs [B][n_sym][num_rx][n_dsc] (H holds
   // the estimates [B][num_rx][n_est][num_tx][n_dsc]), transmit_mimo's link
@@ -359,6 +359,7 @@ struct ChainBufs {
   DBuf<R*> blk_ptrs;
   void release() {
     x.release(); y.release(); coef.release(); H.release(); capbuf.release(); captx.release(); xh.release();
+    tcoef.release();
     gains.release(); phases.release(); pow_part.release(); pstats.release(); npow.release(); llr.release();
     snr_lin.release(); inj_ph.release(); inj_z.release();
     Ym.release(); link_part.release(); link_sigma.release(); inj_lz.release(); inj_lh.release();
@@ -1656,12 +1657,15 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
 
 }  // extern "C"
 
-// TX with the static-tap channel fused in (TxChannelT): SISO Rayleigh with
-// fD = 0, delays within the CP, no TX / RX stream capture.  LTE_TXCH_FUSE=0
-// selects the separate TX and channel kernels (A/B and parity tests).
+// TX with the channel fused in (TxChannelT): SISO Rayleigh, delays within the
+// CP, no TX / RX stream capture; static taps (fD = 0) or per-symbol Taylor
+// sets while mimo_taylor_ok (3 km/h at 20 MHz: |w| S / 2 = 1.2e-3).
+// LTE_TXCH_FUSE=0 selects the separate TX and channel kernels (A/B and
+// parity tests).
 static bool txch_fusable(const lte_plan* p, const lte_run_args* a, bool coded) {
   const lte_plan_desc& d = p->d;
-  if (d.channel != LTE_CH_RAYLEIGH || d.fD != 0.0 || d.num_rx != 1 || p->mimo || p->bf) return false;
+  if (d.channel != LTE_CH_RAYLEIGH || d.num_rx != 1 || p->mimo || p->bf) return false;
+  if (d.fD != 0.0 && !mimo_taylor_ok(d.fD, d.fs, d.N + d.cp_len)) return false;
   if ((d.sc_fdm && !coded) || a->in_signal || a->cap_signal_tx || a->cap_signal_rx) return false;
   if (const char* e = std::getenv("LTE_TXCH_FUSE"))
     if (std::atoi(e) == 0) return false;
@@ -1689,12 +1693,19 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
   ChainBufs<R>& c = cbuf<R>(p);
   const int maxd = *std::max_element(d.delays, d.delays + d.n_paths);
   if (c.xh.alloc((size_t)d.max_frames * p->n_sym * 2 * std::max(maxd, 1))) return fail(LTE_ENOMEM, "tx channel");
+  const bool tv = d.fD != 0.0;   // time-varying taps: per-symbol Taylor sets
+  if (tv && c.tcoef.alloc((size_t)d.max_frames * d.n_paths * p->n_sym * mimo_ncf<R>()))
+    return fail(LTE_ENOMEM, "tx channel");
   {
     Timer t(p, KN_FADING, s);
     LCHK(launch_fading<R>(s, B, 1, d.n_paths, c.gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, c.phases.p,
                           c.coef.p));
+    if (tv)
+      LCHK(launch_jakes_sets<R>(s, B, d.n_paths, p->n_sym, d.N + d.cp_len, c.phases.p, c.gains.p, d.fD, d.fs,
+                                c.tcoef.p));
   }
   TxChannelT<R> ch{};
+  ch.tcoef = tv ? c.tcoef.p : nullptr;
   ch.n_paths = d.n_paths;
   ch.max_delay = maxd;
   for (int i = 0; i < d.n_paths; ++i) ch.delays[i] = d.delays[i];

@@ -253,4 +253,68 @@ __device__ __forceinline__ void frame_err_add(uint32_t* __restrict__ frame_err, 
   }
 }
 
+// Per-OFDM-symbol Taylor sets of one path's Jakes sum (jakes_fading,
+// core/rayleighchannel.py:20-42): for symbol s with centre c_s (samples
+// s * sym_len + (sym_len - 1) / 2), h(c_s + d) = sum_k c_k d^k with
+//  * f64: degree 5, c_k = g sqrt(2/16) sum_m a_m (j W_m)^k / k!, a_m =
+//    exp(j (w_m t_c + phi_m)) formed like one reference sample, W_m = w_m / fs
+//    (valid while mimo_taylor_ok: remainder under float64 rounding);
+//  * f32: A + B d + C d^2 computed in float64 (truncation ~1e-10 at 3 km/h),
+//    each sinusoid's phasor rotated from symbol to symbol.
+// out: n_cs sets of mimo_ncf<R>() terms.  Shared by k_fading_mimo (the
+// multi-antenna links) and k_jakes_sets (the fused SISO TX channel).
+template <class R>
+__device__ __forceinline__ void jakes_symbol_sets(const double (&ph)[16], double gain, double fD, double fs,
+                                                  int sym_len, int n_cs, cx<R>* __restrict__ out) {
+  constexpr int NCF = mimo_ncf<R>();
+  if constexpr (sizeof(R) == 8) {
+    const double k = sqrt(2.0 / 16.0), gn = gain;
+    for (int sidx = 0; sidx < n_cs; ++sidx) {
+      const double tc = ((double)sidx * sym_len + 0.5 * (sym_len - 1)) / fs;
+      double cr[NCF], ci[NCF];
+      for (int kk = 0; kk < NCF; ++kk) cr[kk] = ci[kk] = 0.0;
+      for (int mm = 0; mm < 16; ++mm) {
+        const double w = 6.283185307179586 * fD * cos(6.283185307179586 * (double)(mm + 1) / 16.0);
+        double sv, cv;
+        sincos(w * tc + ph[mm], &sv, &cv);
+        const double W = w / fs;
+#pragma unroll
+        for (int kk = 0; kk < NCF; ++kk) {   // a_m (j W)^k / k!
+          cr[kk] += cv;
+          ci[kk] += sv;
+          const double nr = -sv * (W / (kk + 1)), ni = cv * (W / (kk + 1));
+          cv = nr;
+          sv = ni;
+        }
+      }
+      for (int kk = 0; kk < NCF; ++kk) out[sidx * NCF + kk] = make_double2(gn * (cr[kk] * k), gn * (ci[kk] * k));
+    }
+  } else {
+    const double k = sqrt(2.0 / 16.0) * gain;
+    // per sinusoid: phasor at the first symbol centre, then rotate by w * sym_len
+    // per symbol (float64 recurrence: 2 sincos per sinusoid instead of one per symbol)
+    double w[16], zr[16], zi[16], rr[16], ri[16];
+    const double c0 = fD == 0.0 ? 0.0 : 0.5 * (sym_len - 1);
+    for (int mm = 0; mm < 16; ++mm) {
+      w[mm] = fD == 0.0 ? 0.0 : 6.283185307179586 * fD * cos(6.283185307179586 * (mm + 1) / 16.0) / fs;
+      sincos(w[mm] * c0 + ph[mm], &zi[mm], &zr[mm]);
+      sincos(w[mm] * (double)sym_len, &ri[mm], &rr[mm]);
+    }
+    for (int sidx = 0; sidx < n_cs; ++sidx) {
+      double ar = 0, ai = 0, br = 0, bi = 0, cr = 0, ci = 0;
+      for (int mm = 0; mm < 16; ++mm) {
+        const double cv = zr[mm], sv = zi[mm], wm = w[mm];
+        ar += cv; ai += sv;
+        br += -wm * sv; bi += wm * cv;                   // j w e^{j th}
+        cr += -0.5 * wm * wm * cv; ci += -0.5 * wm * wm * sv;
+        zr[mm] = cv * rr[mm] - sv * ri[mm];
+        zi[mm] = cv * ri[mm] + sv * rr[mm];
+      }
+      out[sidx * 3 + 0] = make_float2((float)(ar * k), (float)(ai * k));
+      out[sidx * 3 + 1] = make_float2((float)(br * k), (float)(bi * k));
+      out[sidx * 3 + 2] = make_float2((float)(cr * k), (float)(ci * k));
+    }
+  }
+}
+
 }  // namespace lte

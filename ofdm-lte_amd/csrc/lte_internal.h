@@ -93,8 +93,16 @@ struct TxChannelT {
   cx<R>* y;            // [B][L]
   cx<R>* xh;           // [B][n_sym][2 * max_delay]: first / last max_delay TX samples of each symbol
   R* pow_part;         // [B][n_sym]
+  // fD != 0: per-symbol Taylor sets of every path [B][n_paths][n_sym][mimo_ncf<R>()]
+  // (k_jakes_sets); null for static taps (coef)
+  const cx<R>* tcoef;
 };
 bool txch_supported(const Grid& g, int n_paths, int max_delay);
+// per-OFDM-symbol Taylor sets of the SISO paths from k_fading's phases (the
+// fused TX channel at fD != 0): [B][n_paths][n_sym][mimo_ncf<R>()]
+template <class R>
+int launch_jakes_sets(hipStream_t s, int B, int n_paths, int n_sym, int sym_len, const R* phases, const R* gains,
+                      double fD, double fs, cx<R>* tcoef);
 template <class R>
 int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
                       int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch);

@@ -140,7 +140,14 @@ __device__ __forceinline__ V* dyn_lds() {
 // receives the symbol already scaled by the IFFT's last pass (x = ifft *
 // sqrt(N) as the reference forms it) and applies the taps (gain * fading) * x
 // in the reference's order.
-template <class R>
+//
+// TV, time-varying taps (ch.tcoef, fD != 0): tap p at sample m of the symbol is
+// the Horner value of the symbol's Taylor set at d = m - (S - 1) / 2
+// (jakes_symbol_sets, as the multi-antenna links form it).  A wave belongs to
+// one slot (T >= 64), so the set's address is wave-uniform (scalar loads);
+// paths outer, the thread's samples (at most TXCH_MAXS) inner.
+constexpr int TXCH_MAXS = 10;   // samples per thread per symbol: S <= 1.25 N (cp <= N / 4), T = N / 8
+template <class R, bool TV>
 __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxChannelT<R>& ch, int b, int l, int slot,
                                            int tid, int T, bool active, R sc) {
   using V = cx<R>;
@@ -148,7 +155,48 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
   constexpr bool F64 = sizeof(R) == 8;
   const int N = g.N, cp = g.cp, S = N + cp, D = ch.max_delay;
   R pw = (R)0;
-  if (active) {
+  if (TV && active) {
+    constexpr int NCF = mimo_ncf<R>();
+    if (D > 0) {   // the TX samples x at both ends of the symbol
+      V* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
+      for (int i = tid; i < 2 * D; i += T) {
+        const int j = i < D ? i : S - 2 * D + i;
+        const V v = buf[(j - cp) & (N - 1)];
+        xh[i] = F64 ? v : cscale(v, sc);
+      }
+    }
+    const int bu = __builtin_amdgcn_readfirstlane(b), lu = __builtin_amdgcn_readfirstlane(l);
+    const V* tc = ch.tcoef + ((size_t)bu * ch.n_paths * g.n_sym + lu) * NCF;
+    const R dc = (R)0.5 * (R)(S - 1);
+    V v[TXCH_MAXS];
+#pragma unroll
+    for (int i = 0; i < TXCH_MAXS; ++i) v[i] = mkc((R)0, (R)0);
+    for (int p = 0; p < ch.n_paths; ++p) {
+      const V* c = tc + (size_t)p * g.n_sym * NCF;
+      V cc[NCF];
+#pragma unroll
+      for (int k = 0; k < NCF; ++k) cc[k] = F64 ? c[k] : cscale(c[k], sc);
+      const int off = ch.delays[p] + cp;
+#pragma unroll
+      for (int i = 0; i < TXCH_MAXS; ++i) {
+        const int m = D + tid + i * T;
+        if (m >= S) break;
+        const R d = (R)m - dc;
+        V h = cc[NCF - 1];
+#pragma unroll
+        for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * d + cc[k].x, h.y * d + cc[k].y);
+        v[i] = cadd(v[i], cmul(h, buf[(m - off) & (N - 1)]));
+      }
+    }
+    V* yo = ch.y + (size_t)b * g.L + (size_t)l * S;
+#pragma unroll
+    for (int i = 0; i < TXCH_MAXS; ++i) {
+      const int m = D + tid + i * T;
+      if (m >= S) break;
+      if (m >= cp) yo[m] = v[i];
+      pw += v[i].x * v[i].x + v[i].y * v[i].y;
+    }
+  } else if (!TV && active) {
     if (D > 0) {   // the TX samples x at both ends of the symbol
       V* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
       for (int i = tid; i < 2 * D; i += T) {
@@ -286,7 +334,8 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   // f64 + channel: the IFFT's last pass applies the output scale
   fft_lds<true, NC, CH && sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
   if constexpr (CH) {
-    tx_channel<R>(buf, g, ch, b, l, slot, tid, T, active, sc);
+    if (ch.tcoef) tx_channel<R, true>(buf, g, ch, b, l, slot, tid, T, active, sc);
+    else tx_channel<R, false>(buf, g, ch, b, l, slot, tid, T, active, sc);
   } else if (active) {
     V* xo = x + (size_t)b * g.L + (size_t)l * (N + g.cp);
     for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
@@ -379,7 +428,7 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
 #ifndef TXF_STAGE   // 1: the frame's coded streams staged in LDS; 0: bit gathers through L1 / L2
 #define TXF_STAGE 1
 #endif
-template <class R, int BPS, int NC = 0>
+template <class R, int BPS, int NC = 0, bool TV = false>
 __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32_t* __restrict__ enc, int enc_words,
                                                           const int32_t* __restrict__ tx_map, int B,
                                                           cx<R>* __restrict__ cap_syms, TxChannelT<R> ch) {
@@ -449,7 +498,7 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
     fft_lds<true, NC, sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
     // every read of buf in tx_channel precedes its reduction barrier, so the
     // next symbol may overwrite buf after it
-    tx_channel<R>(buf, g, ch, b, l, slot, tid, T, active, sc);
+    tx_channel<R, TV>(buf, g, ch, b, l, slot, tid, T, active, sc);
   }
 }
 
@@ -462,8 +511,14 @@ int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_w
   if (shm > 65536) return (int)hipErrorInvalidValue;
   const int blocks = (B + spw - 1) / spw;
 #define LTE_TXF(BPS_, NC_)                                                                                      \
-  hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, tx_map, B, \
-                     cap_syms, ch)
+  do {                                                                                                          \
+    if (ch.tcoef)                                                                                               \
+      hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_, true>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words,   \
+                         tx_map, B, cap_syms, ch);                                                              \
+    else                                                                                                        \
+      hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, tx_map, \
+                         B, cap_syms, ch);                                                                      \
+  } while (0)
   if (g.N == 2048) {
     if (g.bps == 2) LTE_TXF(2, 2048); else if (g.bps == 4) LTE_TXF(4, 2048); else LTE_TXF(6, 2048);
   } else {
@@ -490,12 +545,24 @@ __global__ __launch_bounds__(WG) void k_chan_fix(Grid g, int B, TxChannelT<R> ch
     const int D = ch.max_delay;
     const V* hd = ch.xh + (size_t)i * 2 * D;   // this symbol's head; hd[-D..-1] = previous symbol's tail
     const V* cb = ch.coef + (size_t)b * ch.n_paths;
+    constexpr int NCF = mimo_ncf<R>();
+    const R dc = (R)0.5 * (R)(g.N + g.cp - 1);
     for (int m = lane; m < D; m += CHF_LANES) {
       V v = mkc((R)0, (R)0);
       for (int p = 0; p < ch.n_paths; ++p) {
         const int j = m - ch.delays[p];
         const V xv = (j >= 0 || l > 0) ? hd[j] : mkc((R)0, (R)0);
-        v = cadd(v, cmul(cb[p], xv));
+        V h;
+        if (ch.tcoef) {   // the symbol's Taylor set at d = m - (S - 1) / 2 (tx_channel)
+          const V* c = ch.tcoef + (((size_t)b * ch.n_paths + p) * g.n_sym + l) * NCF;
+          const R d = (R)m - dc;
+          h = c[NCF - 1];
+#pragma unroll
+          for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * d + c[k].x, h.y * d + c[k].y);
+        } else {
+          h = cb[p];
+        }
+        v = cadd(v, cmul(h, xv));
       }
       pw += v.x * v.x + v.y * v.y;
     }
@@ -564,6 +631,31 @@ int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const R* gains_
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_fading<R>, dim3((n + WG - 1) / WG), dim3(WG), 0, s, B, num_rx, n_paths, gains_dev, fid, seed,
                      inj_ph, inj_stride, phases, coef);
+  return (int)hipGetLastError();
+}
+
+// Per-symbol Taylor sets of the SISO paths (fD != 0, the fused TX channel):
+// one thread per (frame, path) from k_fading's 16 phases (jakes_symbol_sets).
+template <class R>
+__global__ __launch_bounds__(WG) void k_jakes_sets(int B, int n_paths, int n_sym, int sym_len,
+                                                   const R* __restrict__ phases, const R* __restrict__ gains,
+                                                   double fD, double fs, cx<R>* __restrict__ tcoef) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * n_paths) return;
+  const int p = i % n_paths;
+  double ph[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) ph[m] = phases[(size_t)i * 16 + m];
+  jakes_symbol_sets<R>(ph, (double)gains[p], fD, fs, sym_len, n_sym, tcoef + (size_t)i * n_sym * mimo_ncf<R>());
+}
+
+template <class R>
+int launch_jakes_sets(hipStream_t s, int B, int n_paths, int n_sym, int sym_len, const R* phases, const R* gains,
+                      double fD, double fs, cx<R>* tcoef) {
+  const int n = B * n_paths;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_jakes_sets<R>, dim3((n + WG - 1) / WG), dim3(WG), 0, s, B, n_paths, n_sym, sym_len, phases,
+                     gains, fD, fs, tcoef);
   return (int)hipGetLastError();
 }
 
@@ -1355,6 +1447,7 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                                   const TxChannelT<R>&);                                                             \
   template int launch_fading<R>(hipStream_t, int, int, int, const R*, const uint64_t*, uint64_t, const R*, int64_t, \
                                 R*, cx<R>*);                                                                         \
+  template int launch_jakes_sets<R>(hipStream_t, int, int, int, int, const R*, const R*, double, double, cx<R>*);     \
   template int launch_channel<R>(hipStream_t, const Grid&, int, int, int, int, const int32_t*, const R*, R, R,       \
                                  const R*, const cx<R>*, const cx<R>*, cx<R>*, R*, int, int);                       \
   template int launch_npow<R>(hipStream_t, int, int, const R*, int, int, const R*, R*);                             \

@@ -218,30 +218,12 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
     }
   }
   if constexpr (F64) {
-    const double k = sqrt(2.0 / 16.0), gn = gains[p];
+    const double gn = gains[p];
     if (n_cs > 1) {   // the Taylor sets (fD != 0)
-      for (int sidx = 0; sidx < n_cs; ++sidx) {
-        const double tc = ((double)sidx * sym_len + 0.5 * (sym_len - 1)) / fs;
-        double cr[NCF], ci[NCF];
-        for (int kk = 0; kk < NCF; ++kk) cr[kk] = ci[kk] = 0.0;
-        for (int mm = 0; mm < 16; ++mm) {
-          const double w = 6.283185307179586 * fD * cos(6.283185307179586 * (double)(mm + 1) / 16.0);
-          double sv, cv;
-          sincos(w * tc + ph[mm], &sv, &cv);
-          const double W = w / fs;
-#pragma unroll
-          for (int kk = 0; kk < NCF; ++kk) {   // a_m (j W)^k / k!
-            cr[kk] += cv;
-            ci[kk] += sv;
-            const double nr = -sv * (W / (kk + 1)), ni = cv * (W / (kk + 1));
-            cv = nr;
-            sv = ni;
-          }
-        }
-        for (int kk = 0; kk < NCF; ++kk) out[sidx * NCF + kk] = make_double2(gn * (cr[kk] * k), gn * (ci[kk] * k));
-      }
+      jakes_symbol_sets<R>(ph, gn, fD, fs, sym_len, n_cs, out);
       return;
     }
+    const double k = sqrt(2.0 / 16.0);
     double sr = 0.0, si = 0.0;
     for (int mm = 0; mm < 16; ++mm) {
       double sv, cv;
@@ -255,30 +237,7 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
       for (int mm = 0; mm < 16; ++mm) phases[(size_t)i * 16 + mm] = ph[mm];
     return;
   } else {
-    const double k = sqrt(2.0 / 16.0) * (double)gains[p];
-    // per sinusoid: phasor at the first symbol centre, then rotate by w * sym_len
-    // per symbol (float64 recurrence: 2 sincos per sinusoid instead of one per symbol)
-    double w[16], zr[16], zi[16], rr[16], ri[16];
-    const double c0 = fD == 0.0 ? 0.0 : 0.5 * (sym_len - 1);
-    for (int mm = 0; mm < 16; ++mm) {
-      w[mm] = fD == 0.0 ? 0.0 : 6.283185307179586 * fD * cos(6.283185307179586 * (mm + 1) / 16.0) / fs;
-      sincos(w[mm] * c0 + ph[mm], &zi[mm], &zr[mm]);
-      sincos(w[mm] * (double)sym_len, &ri[mm], &rr[mm]);
-    }
-    for (int sidx = 0; sidx < n_cs; ++sidx) {
-      double ar = 0, ai = 0, br = 0, bi = 0, cr = 0, ci = 0;
-      for (int mm = 0; mm < 16; ++mm) {
-        const double cv = zr[mm], sv = zi[mm], wm = w[mm];
-        ar += cv; ai += sv;
-        br += -wm * sv; bi += wm * cv;                   // j w e^{j th}
-        cr += -0.5 * wm * wm * cv; ci += -0.5 * wm * wm * sv;
-        zr[mm] = cv * rr[mm] - sv * ri[mm];
-        zi[mm] = cv * ri[mm] + sv * rr[mm];
-      }
-      out[sidx * 3 + 0] = make_float2((float)(ar * k), (float)(ai * k));
-      out[sidx * 3 + 1] = make_float2((float)(br * k), (float)(bi * k));
-      out[sidx * 3 + 2] = make_float2((float)(cr * k), (float)(ci * k));
-    }
+    jakes_symbol_sets<R>(ph, (double)gains[p], fD, fs, sym_len, n_cs, out);
   }
 }
 

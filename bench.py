@@ -18,6 +18,7 @@ usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--preci
 import argparse
 import json
 import os
+import platform
 import socket
 import subprocess
 import sys
@@ -70,6 +71,17 @@ def _cpu_worker(job):
             return n, el
 
 
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or 'unknown'
+
+
 def cpu_baseline(seconds=15.0, procs=None):
     """Time the oracle (float64 CPU restatement: NumPy front end + C turbo
     decoder, bit-exact with the reference) on this host's cores on a bounded
@@ -86,7 +98,7 @@ def cpu_baseline(seconds=15.0, procs=None):
     n = sum(r[0] for r in res)
     value = sum(r[0] / r[1] for r in res)
     return {'value': value, 'unit': 'subframes/s', 'cores': procs, 'kind': 'port',
-            'per_core': value / procs,
+            'per_core': value / procs, 'cpu_model': _cpu_model(),
             'sample': f'{n} config-2 coded subframes (TB {TB}, 8 it.) over SNR 0:2:30 dB, '
                       f'{max(r[1] for r in res):.1f} s on {procs} host cores, one single-threaded '
                       f'process each (oracle: NumPy + C, float64)'}

@@ -1664,7 +1664,7 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
 // parity tests).
 static bool txch_fusable(const lte_plan* p, const lte_run_args* a, bool coded) {
   const lte_plan_desc& d = p->d;
-  if (d.channel != LTE_CH_RAYLEIGH || d.num_rx != 1 || p->mimo || p->bf) return false;
+  if (d.channel != LTE_CH_RAYLEIGH || d.num_rx < 1 || p->mimo || p->bf) return false;
   if (d.fD != 0.0 && !mimo_taylor_ok(d.fD, d.fs, d.N + d.cp_len)) return false;
   if ((d.sc_fdm && !coded) || a->in_signal || a->cap_signal_tx || a->cap_signal_rx) return false;
   if (const char* e = std::getenv("LTE_TXCH_FUSE"))
@@ -1693,19 +1693,21 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
   ChainBufs<R>& c = cbuf<R>(p);
   const int maxd = *std::max_element(d.delays, d.delays + d.n_paths);
   if (c.xh.alloc((size_t)d.max_frames * p->n_sym * 2 * std::max(maxd, 1))) return fail(LTE_ENOMEM, "tx channel");
+  const int rx = d.num_rx;
   const bool tv = d.fD != 0.0;   // time-varying taps: per-symbol Taylor sets
-  if (tv && c.tcoef.alloc((size_t)d.max_frames * d.n_paths * p->n_sym * mimo_ncf<R>()))
+  if (tv && c.tcoef.alloc((size_t)d.max_frames * rx * d.n_paths * p->n_sym * mimo_ncf<R>()))
     return fail(LTE_ENOMEM, "tx channel");
   {
     Timer t(p, KN_FADING, s);
-    LCHK(launch_fading<R>(s, B, 1, d.n_paths, c.gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, c.phases.p,
+    LCHK(launch_fading<R>(s, B, rx, d.n_paths, c.gains.p, p->fid.p, a->seed, inj_ph, inj_ph_stride, c.phases.p,
                           c.coef.p));
-    if (tv)
-      LCHK(launch_jakes_sets<R>(s, B, d.n_paths, p->n_sym, d.N + d.cp_len, c.phases.p, c.gains.p, d.fD, d.fs,
+    if (tv)   // one (frame, RX) at a time: phases / sets are [B][rx][path]
+      LCHK(launch_jakes_sets<R>(s, B * rx, d.n_paths, p->n_sym, d.N + d.cp_len, c.phases.p, c.gains.p, d.fD, d.fs,
                                 c.tcoef.p));
   }
   TxChannelT<R> ch{};
   ch.tcoef = tv ? c.tcoef.p : nullptr;
+  ch.num_rx = rx;
   ch.n_paths = d.n_paths;
   ch.max_delay = maxd;
   for (int i = 0; i < d.n_paths; ++i) ch.delays[i] = d.delays[i];
@@ -1724,7 +1726,7 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
   {
     Timer t(p, KN_CHANNEL, s);
     LCHK(launch_chan_fix<R>(s, p->grid, B, ch));
-    LCHK(launch_npow<R>(s, B, 1, ch.pow_part, p->n_sym, p->L, c.snr_lin.p, c.npow.p));
+    LCHK(launch_npow<R>(s, B, rx, ch.pow_part, p->n_sym, p->L, c.snr_lin.p, c.npow.p));
   }
   return LTE_OK;
 }

@@ -88,12 +88,13 @@ constexpr int TXCH_MAXP = 8;
 template <class R>
 struct TxChannelT {
   int n_paths, max_delay;
+  int num_rx;          // receive antennas (SIMO: independent taps per RX, y / coef / pow_part per RX)
   int delays[TXCH_MAXP];
-  const cx<R>* coef;   // [B][n_paths]
-  cx<R>* y;            // [B][L]
+  const cx<R>* coef;   // [B][num_rx][n_paths]
+  cx<R>* y;            // [B][num_rx][L]
   cx<R>* xh;           // [B][n_sym][2 * max_delay]: first / last max_delay TX samples of each symbol
-  R* pow_part;         // [B][n_sym]
-  // fD != 0: per-symbol Taylor sets of every path [B][n_paths][n_sym][mimo_ncf<R>()]
+  R* pow_part;         // [B][num_rx][n_sym]
+  // fD != 0: per-symbol Taylor sets of every path [B][num_rx][n_paths][n_sym][mimo_ncf<R>()]
   // (k_jakes_sets); null for static taps (coef)
   const cx<R>* tcoef;
 };

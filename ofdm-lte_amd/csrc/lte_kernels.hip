@@ -154,85 +154,85 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
   __shared__ R red[WG / 64];
   constexpr bool F64 = sizeof(R) == 8;
   const int N = g.N, cp = g.cp, S = N + cp, D = ch.max_delay;
-  R pw = (R)0;
-  if (TV && active) {
-    constexpr int NCF = mimo_ncf<R>();
-    if (D > 0) {   // the TX samples x at both ends of the symbol
-      V* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
-      for (int i = tid; i < 2 * D; i += T) {
-        const int j = i < D ? i : S - 2 * D + i;
-        const V v = buf[(j - cp) & (N - 1)];
-        xh[i] = F64 ? v : cscale(v, sc);
-      }
+  if (active && D > 0) {   // the TX samples x at both ends of the symbol (every RX's taps read them)
+    V* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
+    for (int i = tid; i < 2 * D; i += T) {
+      const int j = i < D ? i : S - 2 * D + i;
+      const V v = buf[(j - cp) & (N - 1)];
+      xh[i] = F64 ? v : cscale(v, sc);
     }
-    const int bu = __builtin_amdgcn_readfirstlane(b), lu = __builtin_amdgcn_readfirstlane(l);
-    const V* tc = ch.tcoef + ((size_t)bu * ch.n_paths * g.n_sym + lu) * NCF;
-    const R dc = (R)0.5 * (R)(S - 1);
-    V v[TXCH_MAXS];
+  }
+  // SIMO: each RX its own taps, stream and power partial (transmit_simo,
+  // core/ofdm_core.py:361-412); the symbol in LDS is read once per RX
+  for (int r = 0; r < ch.num_rx; ++r) {
+    const size_t br = (size_t)b * ch.num_rx + r;
+    R pw = (R)0;
+    if (TV && active) {
+      constexpr int NCF = mimo_ncf<R>();
+      const int bu = __builtin_amdgcn_readfirstlane(b), lu = __builtin_amdgcn_readfirstlane(l);
+      const V* tc = ch.tcoef + (((size_t)bu * ch.num_rx + r) * ch.n_paths * g.n_sym + lu) * NCF;
+      const R dc = (R)0.5 * (R)(S - 1);
+      V v[TXCH_MAXS];
 #pragma unroll
-    for (int i = 0; i < TXCH_MAXS; ++i) v[i] = mkc((R)0, (R)0);
-    for (int p = 0; p < ch.n_paths; ++p) {
-      const V* c = tc + (size_t)p * g.n_sym * NCF;
-      V cc[NCF];
+      for (int i = 0; i < TXCH_MAXS; ++i) v[i] = mkc((R)0, (R)0);
+      for (int p = 0; p < ch.n_paths; ++p) {
+        const V* c = tc + (size_t)p * g.n_sym * NCF;
+        V cc[NCF];
 #pragma unroll
-      for (int k = 0; k < NCF; ++k) cc[k] = F64 ? c[k] : cscale(c[k], sc);
-      const int off = ch.delays[p] + cp;
+        for (int k = 0; k < NCF; ++k) cc[k] = F64 ? c[k] : cscale(c[k], sc);
+        const int off = ch.delays[p] + cp;
+#pragma unroll
+        for (int i = 0; i < TXCH_MAXS; ++i) {
+          const int m = D + tid + i * T;
+          if (m < S) {
+            const R d = (R)m - dc;
+            V h = cc[NCF - 1];
+#pragma unroll
+            for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * d + cc[k].x, h.y * d + cc[k].y);
+            v[i] = cadd(v[i], cmul(h, buf[(m - off) & (N - 1)]));
+          }
+        }
+      }
+      V* yo = ch.y + br * g.L + (size_t)l * S;
 #pragma unroll
       for (int i = 0; i < TXCH_MAXS; ++i) {
         const int m = D + tid + i * T;
-        if (m >= S) break;
-        const R d = (R)m - dc;
-        V h = cc[NCF - 1];
+        if (m < S) {
+          if (m >= cp) yo[m] = v[i];
+          pw += v[i].x * v[i].x + v[i].y * v[i].y;
+        }
+      }
+    } else if (!TV && active) {
+      // sample j of the CP-extended symbol is buf[(j - cp) mod N] (N a power of 2)
+      V cf[TXCH_MAXP];
+      int off[TXCH_MAXP];
 #pragma unroll
-        for (int k = NCF - 2; k >= 0; --k) h = mkc(h.x * d + cc[k].x, h.y * d + cc[k].y);
-        v[i] = cadd(v[i], cmul(h, buf[(m - off) & (N - 1)]));
+      for (int p = 0; p < TXCH_MAXP; ++p) {
+        const V c = p < ch.n_paths ? ch.coef[br * ch.n_paths + p] : mkc((R)0, (R)0);
+        cf[p] = F64 ? c : cscale(c, sc);
+        off[p] = ch.delays[p] + cp;
+      }
+      V* yo = ch.y + br * g.L + (size_t)l * S;
+      for (int m = D + tid; m < S; m += T) {
+        V v = mkc((R)0, (R)0);
+#pragma unroll
+        for (int p = 0; p < TXCH_MAXP; ++p)
+          if (p < ch.n_paths) v = cadd(v, cmul(cf[p], buf[(m - off[p]) & (N - 1)]));
+        if (m >= cp) yo[m] = v;
+        pw += v.x * v.x + v.y * v.y;
       }
     }
-    V* yo = ch.y + (size_t)b * g.L + (size_t)l * S;
-#pragma unroll
-    for (int i = 0; i < TXCH_MAXS; ++i) {
-      const int m = D + tid + i * T;
-      if (m >= S) break;
-      if (m >= cp) yo[m] = v[i];
-      pw += v[i].x * v[i].x + v[i].y * v[i].y;
+    // per-slot sum in a fixed order: T >= 64 threads = T / 64 whole waves per slot
+    for (int o = 32; o > 0; o >>= 1) pw += __shfl_xor(pw, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pw;
+    __syncthreads();
+    if (active && tid == 0) {
+      const int wps = T >> 6;
+      R t = (R)0;
+      for (int w = 0; w < wps; ++w) t += red[slot * wps + w];
+      ch.pow_part[br * g.n_sym + l] = t;
     }
-  } else if (!TV && active) {
-    if (D > 0) {   // the TX samples x at both ends of the symbol
-      V* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
-      for (int i = tid; i < 2 * D; i += T) {
-        const int j = i < D ? i : S - 2 * D + i;
-        const V v = buf[(j - cp) & (N - 1)];
-        xh[i] = F64 ? v : cscale(v, sc);
-      }
-    }
-    // sample j of the CP-extended symbol is buf[(j - cp) mod N] (N a power of 2)
-    V cf[TXCH_MAXP];
-    int off[TXCH_MAXP];
-#pragma unroll
-    for (int p = 0; p < TXCH_MAXP; ++p) {
-      const V c = p < ch.n_paths ? ch.coef[(size_t)b * ch.n_paths + p] : mkc((R)0, (R)0);
-      cf[p] = F64 ? c : cscale(c, sc);
-      off[p] = ch.delays[p] + cp;
-    }
-    V* yo = ch.y + (size_t)b * g.L + (size_t)l * S;
-    for (int m = D + tid; m < S; m += T) {
-      V v = mkc((R)0, (R)0);
-#pragma unroll
-      for (int p = 0; p < TXCH_MAXP; ++p)
-        if (p < ch.n_paths) v = cadd(v, cmul(cf[p], buf[(m - off[p]) & (N - 1)]));
-      if (m >= cp) yo[m] = v;
-      pw += v.x * v.x + v.y * v.y;
-    }
-  }
-  // per-slot sum in a fixed order: T >= 64 threads = T / 64 whole waves per slot
-  for (int o = 32; o > 0; o >>= 1) pw += __shfl_xor(pw, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pw;
-  __syncthreads();
-  if (active && tid == 0) {
-    const int wps = T >> 6;
-    R t = (R)0;
-    for (int w = 0; w < wps; ++w) t += red[slot * wps + w];
-    ch.pow_part[(size_t)b * g.n_sym + l] = t;
+    if (r + 1 < ch.num_rx) __syncthreads();   // red is rewritten by the next RX
   }
 }
 
@@ -243,8 +243,9 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
 // 181-223), ifft*sqrt(N) + CP (modulator.py:242-248).
 // SCF (SC-FDM, uncoded chains): the Nd QAM symbols of the OFDM symbol are
 // DFT-precoded (M = Nd, core/modulator.py:232-236) in a second LDS buffer first.
-// CH: the channel applied in place (tx_channel); NC: compile-time N (fft_lds).
-template <class R, int CODED, int BPS, bool SCF = false, bool CH = false, int NC = 0>
+// CH: the channel applied in place (tx_channel: 1 static taps, 2 time-varying);
+// NC: compile-time N (fft_lds).
+template <class R, int CODED, int BPS, bool SCF = false, int CH = 0, int NC = 0>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
                                                 const int32_t* __restrict__ tx_map, cx<R>* __restrict__ x, int B,
@@ -332,10 +333,9 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   __syncthreads();
   const R sc = tx_scale<R>(N);
   // f64 + channel: the IFFT's last pass applies the output scale
-  fft_lds<true, NC, CH && sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
-  if constexpr (CH) {
-    if (ch.tcoef) tx_channel<R, true>(buf, g, ch, b, l, slot, tid, T, active, sc);
-    else tx_channel<R, false>(buf, g, ch, b, l, slot, tid, T, active, sc);
+  fft_lds<true, NC, CH != 0 && sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
+  if constexpr (CH != 0) {
+    tx_channel<R, CH == 2>(buf, g, ch, b, l, slot, tid, T, active, sc);
   } else if (active) {
     V* xo = x + (size_t)b * g.L + (size_t)l * (N + g.cp);
     for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
@@ -397,19 +397,24 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
   const size_t enc_shm = tx_enc_shm(coded, spw, enc_words);
   const int stage_enc = enc_shm > 0;
   const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + enc_shm;
-#define LTE_TXC(C_, B_)                                                                                          \
+#define LTE_TXC2(C_, B_, CH_)                                                                                     \
   if (g.N == 2048)                                                                                                 \
-    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, false, true, 2048>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,  \
+    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, false, CH_, 2048>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,   \
                        enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch);                             \
   else                                                                                                             \
-    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, false, true>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,         \
+    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, false, CH_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,          \
                        enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch)
+#define LTE_TXC(C_, B_)                                                                                          \
+  do {                                                                                                             \
+    if (ch.tcoef) { LTE_TXC2(C_, B_, 2); } else { LTE_TXC2(C_, B_, 1); }                                           \
+  } while (0)
   if (coded) {
     if (g.bps == 2) LTE_TXC(1, 2); else if (g.bps == 4) LTE_TXC(1, 4); else LTE_TXC(1, 6);
   } else {
     if (g.bps == 2) LTE_TXC(0, 2); else if (g.bps == 4) LTE_TXC(0, 4); else LTE_TXC(0, 6);
   }
 #undef LTE_TXC
+#undef LTE_TXC2
   return (int)hipGetLastError();
 }
 
@@ -536,15 +541,17 @@ constexpr int CHF_LANES = 16;
 template <class R>
 __global__ __launch_bounds__(WG) void k_chan_fix(Grid g, int B, TxChannelT<R> ch) {
   using V = cx<R>;
-  const int64_t i = ((int64_t)blockIdx.x * WG + threadIdx.x) / CHF_LANES;
+  const int64_t i = ((int64_t)blockIdx.x * WG + threadIdx.x) / CHF_LANES;   // (frame, RX, symbol)
   const int lane = threadIdx.x % CHF_LANES;
-  const bool ok = i < (int64_t)B * g.n_sym;
+  const bool ok = i < (int64_t)B * ch.num_rx * g.n_sym;
   R pw = (R)0;
   if (ok) {
-    const int l = (int)(i % g.n_sym), b = (int)(i / g.n_sym);
+    const int l = (int)(i % g.n_sym);
+    const int64_t br = i / g.n_sym;
+    const int b = (int)(br / ch.num_rx);
     const int D = ch.max_delay;
-    const V* hd = ch.xh + (size_t)i * 2 * D;   // this symbol's head; hd[-D..-1] = previous symbol's tail
-    const V* cb = ch.coef + (size_t)b * ch.n_paths;
+    const V* hd = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;   // this symbol's head; hd[-D..-1] = previous symbol's tail
+    const V* cb = ch.coef + (size_t)br * ch.n_paths;
     constexpr int NCF = mimo_ncf<R>();
     const R dc = (R)0.5 * (R)(g.N + g.cp - 1);
     for (int m = lane; m < D; m += CHF_LANES) {
@@ -554,7 +561,7 @@ __global__ __launch_bounds__(WG) void k_chan_fix(Grid g, int B, TxChannelT<R> ch
         const V xv = (j >= 0 || l > 0) ? hd[j] : mkc((R)0, (R)0);
         V h;
         if (ch.tcoef) {   // the symbol's Taylor set at d = m - (S - 1) / 2 (tx_channel)
-          const V* c = ch.tcoef + (((size_t)b * ch.n_paths + p) * g.n_sym + l) * NCF;
+          const V* c = ch.tcoef + (((size_t)br * ch.n_paths + p) * g.n_sym + l) * NCF;
           const R d = (R)m - dc;
           h = c[NCF - 1];
 #pragma unroll
@@ -574,7 +581,7 @@ __global__ __launch_bounds__(WG) void k_chan_fix(Grid g, int B, TxChannelT<R> ch
 
 template <class R>
 int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannelT<R>& ch) {
-  const int64_t n = (int64_t)B * g.n_sym * CHF_LANES;
+  const int64_t n = (int64_t)B * ch.num_rx * g.n_sym * CHF_LANES;
   if (ch.max_delay == 0 || n == 0) return 0;
   hipLaunchKernelGGL(k_chan_fix<R>, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, g, B, ch);
   return (int)hipGetLastError();

@@ -1757,6 +1757,12 @@ static bool rx_fusable(const lte_plan* p, const lte_plan_desc& d) {
     if (std::atoi(e) == 0) return false;
   return rx_frame_supported(p->grid, d.chain, d.num_rx, (d.sc_fdm && d.chain == LTE_CHAIN_UNCODED) ? 1 : 0);
 }
+// Fused SIMO MRC receiver (k_rx_frame_simo), same switch.
+static bool rx_simo_fusable(const lte_plan* p, const lte_plan_desc& d) {
+  if (const char* e = std::getenv("LTE_RX_FUSE"))
+    if (std::atoi(e) == 0) return false;
+  return d.chain == LTE_CHAIN_SIMO && rx_frame_simo_supported(p->grid, d.num_rx);
+}
 
 // SISO / SIMO chains (uncoded, coded, MRC) in precision R.
 template <class R>
@@ -1842,7 +1848,8 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   // SISO receiver fused (estimation + data path per frame) unless LTE_RX_FUSE=0
   const bool rxf = do_rx && rx_fusable(p, d);
-  if (do_rx && !rxf) {
+  const bool rxs = do_rx && !rxf && rx_simo_fusable(p, d);
+  if (do_rx && !rxf && !rxs) {
     Timer t(p, KN_RX_CHEST);
     LCHK(launch_rx_chest<R>(s, g, B, rx, ysrc, yrs, yfs, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.H.p,
                             c.pstats.p));
@@ -1866,6 +1873,11 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                             zn ? reinterpret_cast<R*>(zn_z<R>(p)) : c.llr.p, cap_syms_dev,
                             coded ? nullptr : cap_bits_dev, zn ? zn_nv<R>(p) : nullptr,
                             a->cap_H ? c.H.p : nullptr, a->cap_pilot_stats ? c.pstats.p : nullptr));
+  } else if (rxs) {
+    Timer t(p, KN_RX_DATA);
+    LCHK(launch_rx_frame_simo<R>(s, g, B, rx, ysrc, yrs, yfs, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride,
+                                 p->pw.p, p->PW, d.n_bits, p->frame_err.p, cap_syms_dev, cap_bits_dev,
+                                 a->cap_H ? c.H.p : nullptr, a->cap_pilot_stats ? c.pstats.p : nullptr));
   } else if (do_rx) {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_data<R>(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, c.H.p, c.npow.p, c.snr_lin.p, p->fid.p,

@@ -134,6 +134,16 @@ int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B
                     int64_t y_frame_stride, const R* npow, const R* snr_lin, const uint64_t* fid, uint64_t seed,
                     const R* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
                     R* llr, cx<R>* cap_syms, uint8_t* cap_bits, R* nv_out, cx<R>* H, R* pstats);
+// Fused SIMO MRC receiver (uncoded, 2..RXS_MAXRX RX): one slot per frame walks
+// its symbols, every RX's estimate in registers; H / pstats: optional captures
+// [B][num_rx][n_grp][N] / [B][num_rx][n_grp][2].
+constexpr int RXS_MAXRX = 4;
+bool rx_frame_simo_supported(const Grid& g, int num_rx);
+template <class R>
+int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>* y, int64_t y_rx_stride,
+                         int64_t y_frame_stride, const R* npow, const uint64_t* fid, uint64_t seed, const R* inj_z,
+                         int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                         cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats);
 // Rate dematch into the decoder rows (rows of R: float / double).  rx_map
 // [n_layers][T]: layer 0 assigns, layers 1.. add in order (E > N_cb
 // repetition, rate_matching.py:433-436).  g0: first 64-frame group.

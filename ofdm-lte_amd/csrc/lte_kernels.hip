@@ -1398,6 +1398,181 @@ int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B
   return (int)hipGetLastError();
 }
 
+// Fused SIMO MRC receiver (simulate_simo, core/ofdm_core.py:1405-1534): one
+// slot per frame walks its OFDM symbols; per symbol every RX in turn is loaded
+// with its noise, FFT'd and folded into the MRC sums sum_r conj(H_r) Y_r /
+// (sum_r |H_r|^2 + 1e-10), RX 0 first as k_rx_data sums them.  The first symbol
+// of each 14-symbol group also yields every RX's LS estimate (k_rx_chest's
+// work on the FFT the data path needs anyway), kept in registers for the
+// thread's data subcarriers (hq[r][q], selected by an unrolled compare so the
+// FFT itself is not duplicated per RX).  Same arithmetic per RE as k_rx_chest
+// + k_rx_data<SIMO> (test_fused_simo_receiver_matches_separate_kernels).
+template <class R, int BPS, int NC = 0>
+__global__ __launch_bounds__(WG, sizeof(R) == 8 ? 2 : RXF_WAVES) void k_rx_frame_simo(
+    Grid g, int B, int num_rx, const cx<R>* __restrict__ y, int64_t y_rx_stride, int64_t y_frame_stride,
+    const R* __restrict__ npow, const uint64_t* __restrict__ fid, uint64_t seed, const R* __restrict__ inj_z,
+    int64_t inj_stride, const uint32_t* __restrict__ pw, int PW, int n_bits, uint32_t* __restrict__ frame_err,
+    cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits, cx<R>* __restrict__ H, R* __restrict__ pstats) {
+  using V = cx<R>;
+  using G = GridT<R>;
+  V* sm = dyn_lds<V>();
+  const int N = NC ? NC : g.N, T = N >> 3, spw = WG / T;
+  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
+  const int b = blockIdx.x * spw + slot;
+  const bool active = slot < spw && b < B;
+  V* buf = sm + slot * (N + g.Np);
+  V* hp = buf + N;
+  const R sc = rx_scale<R>(N);
+  constexpr R QS = (R)qam_norm<BPS>();
+  constexpr int QM = 4;   // data REs per thread (Nd < N/2 for every LTE profile)
+  const uint64_t fr = active ? fid[b] : 0ull;
+  const V* yf = y + (size_t)(active ? b : 0) * y_frame_stride;
+  const uint32_t* fb = pw + (size_t)(active ? b : 0) * PW;
+  const size_t fre = (size_t)(active ? b : 0) * g.n_sym * g.Nd;
+  int kpos[QM];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int j = tid0 + q * T;
+    kpos[q] = (active && j < g.Nd) ? g.data_idx[j] : 0;
+  }
+  V hq[RXS_MAXRX][QM];
+  R den[QM];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    den[q] = (R)0;
+#pragma unroll
+    for (int r = 0; r < RXS_MAXRX; ++r) hq[r][q] = mkc((R)0, (R)0);
+  }
+  uint32_t errs = 0;
+  for (int l = 0; l < g.n_sym; ++l) {
+    const bool est = l % 14 == 0;
+    const int grp = l / 14;
+    V num[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) num[q] = mkc((R)0, (R)0);
+    if (est) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) den[q] = (R)0;
+    }
+    for (int rx = 0; rx < num_rx; ++rx) {
+      int tid = tid0;   // opaque per pass (see k_rx_frame)
+      asm volatile("" : "+v"(tid));
+      if (active) {
+        const R sigma = sqrt(npow[(size_t)b * num_rx + rx] / (R)2);
+        const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+        load_symbol_noisy2<true>(buf, yf + rx * y_rx_stride, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T);
+      }
+      __syncthreads();
+      fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, G::tw(g), tid, active);
+      if (est) {   // this RX's group estimate from the group's first symbol (lte_receiver.py:360-411)
+        if (active)
+          for (int p = tid; p < g.Np; p += T) {
+            const V Y = cscale(buf[g.pilot_idx[p]], sc);
+            hp[p] = cdiv(Y, G::pilots(g)[p]);
+            buf[g.pilot_idx[p]] = Y;   // scaled pilots for the SNR stats
+          }
+        __syncthreads();
+        if (active) {
+          const size_t hr = ((size_t)b * num_rx + rx) * g.n_grp + grp;
+          if (H) {
+            V* Hf = H + hr * N;
+            for (int k = tid; k < N; k += T) Hf[k] = chest_interp<R>(g, hp, k);
+          }
+#pragma unroll
+          for (int q = 0; q < QM; ++q) {
+            const int j = tid + q * T;
+            if (j < g.Nd) {
+              const V h = chest_interp<R>(g, hp, kpos[q]);
+              den[q] += abs2_ref(h);
+#pragma unroll
+              for (int r = 0; r < RXS_MAXRX; ++r)
+                if (r == rx) hq[r][q] = h;
+            }
+          }
+          if (pstats && tid == 0) {
+            R pp = (R)0, en = (R)0;
+            for (int p = 0; p < g.Np; ++p) {
+              const V Yp = buf[g.pilot_idx[p]], X = G::pilots(g)[p];
+              pp += Yp.x * Yp.x + Yp.y * Yp.y;
+              const V d = csub(Yp, X);
+              en += d.x * d.x + d.y * d.y;
+            }
+            pstats[hr * 2] = pp / (R)g.Np;
+            pstats[hr * 2 + 1] = en / (R)g.Np;
+          }
+        }
+      }
+      if (active) {
+#pragma unroll
+        for (int q = 0; q < QM; ++q) {
+          const int j = tid + q * T;
+          if (j < g.Nd) {
+            V h = hq[0][q];
+#pragma unroll
+            for (int r = 1; r < RXS_MAXRX; ++r)
+              if (r == rx) h = hq[r][q];
+            num[q] = cadd(num[q], cmulc(cscale(buf[kpos[q]], sc), h));
+          }
+        }
+      }
+      __syncthreads();   // every read of buf done before the next RX / symbol lands in it
+    }
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) {
+        const int j = tid0 + q * T;
+        if (j >= g.Nd) continue;
+        const int re = l * g.Nd + j;
+        const R rr = (R)1 / (den[q] + (R)1e-10);
+        const V z = mkc(num[q].x * rr, num[q].y * rr);
+        if (cap_syms) cap_syms[fre + re] = z;
+        const int idx = hard_index(z, BPS, QS);
+        const int64_t pb0 = (int64_t)re * BPS;
+#pragma unroll
+        for (int m = 0; m < BPS; ++m) {
+          const int64_t pbit = pb0 + m;
+          if (pbit < n_bits) {
+            const uint32_t bit = (idx >> (BPS - 1 - m)) & 1;
+            errs += bit ^ getbit(fb, pbit);
+            if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
+          }
+        }
+      }
+    }
+  }
+  frame_err_add(frame_err, b, errs);
+}
+
+bool rx_frame_simo_supported(const Grid& g, int num_rx) {
+  return num_rx >= 2 && num_rx <= RXS_MAXRX && (g.bps == 2 || g.bps == 4 || g.bps == 6) && 2 * g.Nd < g.N;
+}
+
+template <class R>
+int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>* y, int64_t y_rx_stride,
+                         int64_t y_frame_stride, const R* npow, const uint64_t* fid, uint64_t seed, const R* inj_z,
+                         int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                         cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats) {
+  if (!rx_frame_simo_supported(g, num_rx)) return (int)hipErrorInvalidValue;
+  const int spw = WG / (g.N >> 3);
+  const int blocks = (B + spw - 1) / spw;
+  const size_t shm = (size_t)spw * (g.N + g.Np) * sizeof(cx<R>);
+#define LTE_RXS(BPS_, NC_)                                                                                           \
+  hipLaunchKernelGGL((k_rx_frame_simo<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, B, num_rx, y, y_rx_stride,  \
+                     y_frame_stride, npow, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, cap_syms,        \
+                     cap_bits, H, pstats)
+#define LTE_RXS_BPS(NC_)                                                                                             \
+  do {                                                                                                               \
+    if (g.bps == 2) LTE_RXS(2, NC_);                                                                                 \
+    else if (g.bps == 4) LTE_RXS(4, NC_);                                                                            \
+    else LTE_RXS(6, NC_);                                                                                            \
+  } while (0)
+  if (g.N == 1024) LTE_RXS_BPS(1024);   // config 3 (10 MHz)
+  else LTE_RXS_BPS(0);
+#undef LTE_RXS_BPS
+#undef LTE_RXS
+  return (int)hipGetLastError();
+}
+
 template <class R, int CHAIN, bool SCF = false, int NC = 0>
 static void rx_data_bps(int bps, hipStream_t s, int blocks, size_t shm, const Grid& g, int rayleigh, int B,
                         int num_rx, const cx<R>* y, int64_t y_rx_stride, int64_t y_frame_stride, const cx<R>* H,
@@ -1463,6 +1638,9 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
   template int launch_rx_data<R>(hipStream_t, const Grid&, int, int, int, int, const cx<R>*, int64_t, int64_t,       \
                                  const cx<R>*, const R*, const R*, const uint64_t*, uint64_t, const R*, int64_t,    \
                                  const uint32_t*, int, int, uint32_t*, R*, cx<R>*, uint8_t*, int, R*);              \
+  template int launch_rx_frame_simo<R>(hipStream_t, const Grid&, int, int, const cx<R>*, int64_t, int64_t, const R*,  \
+                                       const uint64_t*, uint64_t, const R*, int64_t, const uint32_t*, int, int,       \
+                                       uint32_t*, cx<R>*, uint8_t*, cx<R>*, R*);                                     \
   template int launch_rx_frame<R>(hipStream_t, const Grid&, int, int, int, const cx<R>*, int64_t, const R*, const R*, \
                                   const uint64_t*, uint64_t, const R*, int64_t, const uint32_t*, int, int, uint32_t*, \
                                   R*, cx<R>*, uint8_t*, R*, cx<R>*, R*);

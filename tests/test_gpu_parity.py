@@ -467,6 +467,38 @@ def test_fused_receiver_matches_separate_kernels(C, monkeypatch, chain, bw, mod,
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('bw,mod,nrx,prof', [(10.0, '16-QAM', 4, 'Vehicular_A'), (20.0, '64-QAM', 2, 'Pedestrian_A'),
+                                             (1.25, 'QPSK', 3, 'Pedestrian_A')])
+def test_fused_simo_receiver_matches_separate_kernels(C, monkeypatch, bw, mod, nrx, prof, prec):
+    """The fused SIMO MRC receiver (k_rx_frame_simo: every RX's estimate on
+    each group's first symbol, kept per data subcarrier, MRC over the RX in
+    order) vs k_rx_chest + k_rx_data<SIMO> on the same Philox frames: channel
+    estimates, pilot statistics and combined symbols to round-off, decisions
+    and counts identical."""
+    import lte_phy
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=bw, modulation=mod), channel_type='rayleigh_mp',
+                                itu_profile=prof, precision=prec)
+    B = 64 + 5
+    bps = sim.config.bits_per_symbol
+    plan = sim._plan(C.CHAIN_SIMO, 14, 14 * sim.Nd * bps, num_rx=nrx, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('H', 'pilot_stats', 'data_syms', 'bits_rx')
+    runs = {}
+    for fuse in ('0', '1'):
+        monkeypatch.setenv('LTE_RX_FUSE', fuse)
+        runs[fuse] = (plan.run(snr, seed=0x5EED, frame_id0=11, capture=cap),
+                      plan.run(snr, seed=0x5EED, frame_id0=11))
+    (a, a0), (b, b0) = runs['0'], runs['1']
+    tol = 1e-13 if prec == 'f64' else 1e-5
+    for k in ('H', 'pilot_stats', 'data_syms'):
+        assert np.max(np.abs(b[k] - a[k])) <= tol * np.max(np.abs(a[k])), k
+    assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 2
+    assert abs(int(a0['counts'][:, 0].sum()) - int(b0['counts'][:, 0].sum())) <= 2
+    assert np.array_equal(a0['counts'][:, 1], b0['counts'][:, 1])
+    assert 0 < int(b0['counts'][:, 0].sum())
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('bw,mod', [(20.0, '64-QAM'), (5.0, '16-QAM'), (10.0, 'QPSK')])
 def test_frame_tx_matches_symbol_tx(C, monkeypatch, bw, mod, prec):
     """Coded TX + channel with one slot per frame (k_ofdm_txf, coded streams

@@ -14,7 +14,8 @@
 //
 // The loaded values are folded with XOR into what is stored, so no load can be
 // dropped.  Prints bytes moved per launch and GB/s, for the decoder's shape
-// with and without the checkpoint rows, and with two waves per SIMD.
+// with and without the checkpoint rows, and with two waves per SIMD; _seq:
+// decoder 2 addressed in natural order (what a QPP-free layout would reach).
 // Build: hipcc -O3 --offload-arch=gfx950 -o scripts/turbo_shape_bench scripts/turbo_shape_bench.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -50,7 +51,7 @@ struct Jobs {
 __device__ __forceinline__ int modadd(int a, int b, int K) { a += b; return a >= K ? a - K : a; }
 __device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 0 ? a + K : a; }
 
-template <bool CKPT, bool dec2, bool first>
+template <bool CKPT, bool dec2, bool first, bool SEQ = false>
 __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int vo, int K, int f1, int f2,
                      uint64_t& acc) {
   const int nsub = K / 8, tf2 = (2 * f2) % K;
@@ -65,7 +66,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
     uint64_t xs[8], xp[8], xe[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {   // the window's loads first (as the decoder's ldwin), then the fold
-      const int k = w * 8 + j, p = dec2 ? pi : k;
+      const int k = w * 8 + j, p = (dec2 && !SEQ) ? pi : k;
       xs[j] = ld(rb, vo, 2 * p);
       xp[j] = ld(rb, vo, lp0 + k);
       xe[j] = first ? 0 : ld(rb, vo, 2 * p + 1);
@@ -92,7 +93,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
 #pragma unroll
     for (int i = 0; i < 24; ++i) {
       if (i < n) {
-        const int k = k0 + i, p = dec2 ? pp : k;
+        const int k = k0 + i, p = (dec2 && !SEQ) ? pp : k;
         v[i] = ld(rb, vo, 2 * p);
         vp[i] = ld(rb, vo, lp0 + k);
         ve[i] = first ? 0 : ld(rb, vo, 2 * p + 1);
@@ -110,7 +111,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
       if (i < n) {
         const int k = k0 + i;
         int p = k;
-        if (dec2) { dd = modsub(dd, tf2, K); pp = modsub(pp, dd, K); p = pp; }
+        if (dec2) { dd = modsub(dd, tf2, K); pp = modsub(pp, dd, K); p = SEQ ? k : pp; }
         st(rb, vo, 2 * p + 1, v[i] + acc);
       }
     }
@@ -118,7 +119,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
   }
 }
 
-template <bool CKPT>
+template <bool CKPT, bool SEQ = false>
 __global__ __launch_bounds__(256) void k_shape(Jobs J, int iters) {
   extern __shared__ uint64_t lds_pad[];
   const int wg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -132,9 +133,9 @@ __global__ __launch_bounds__(256) void k_shape(Jobs J, int iters) {
   const __amdgpu_buffer_rsrc_t rc = rsrc(jb.ck + (size_t)g * ckrows * 64, (uint32_t)(ckrows * 512));
   uint64_t acc = lane;
   for (int it = 0; it < iters; ++it) {
-    if (it == 0) pass<CKPT, false, true>(rb, rc, vo, K, jb.f1, jb.f2, acc);
-    else pass<CKPT, false, false>(rb, rc, vo, K, jb.f1, jb.f2, acc);
-    pass<CKPT, true, false>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+    if (it == 0) pass<CKPT, false, true, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+    else pass<CKPT, false, false, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+    pass<CKPT, true, false, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc);
   }
   pass<CKPT, false, false>(rb, rc, vo, K, jb.f1, jb.f2, acc);
   if (acc == 0x123456789abcdefull) lds_pad[0] = acc;   // never true; keeps the LDS request
@@ -180,8 +181,8 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  auto run = [&](bool ck, size_t lds) {
-    auto k = ck ? k_shape<true> : k_shape<false>;
+  auto run = [&](bool ck, size_t lds, bool seq = false) {
+    auto k = seq ? k_shape<true, true> : ck ? k_shape<true> : k_shape<false>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3((waves + 3) / 4), dim3(256), lds, 0, J, iters);   // warm
     (void)hipEventRecord(a, 0);
@@ -193,7 +194,7 @@ int main(int argc, char** argv) {
     return ms / 3.0;
   };
   const double m1 = run(true, 96 * 1024), m0 = run(false, 96 * 1024), m2 = run(true, 64 * 1024),
-               m3 = run(true, 0);
+               m3 = run(true, 0), m4 = run(true, 96 * 1024, true), m5 = run(true, 0, true);
   if (hipDeviceSynchronize() != hipSuccess) {
     printf("kernel failed\n");
     return 1;
@@ -203,6 +204,8 @@ int main(int argc, char** argv) {
          "\"ms_2wps_ckpt\": %.3f, \"GBs_2wps_ckpt\": %.1f, \"ms_free_ckpt\": %.3f, \"GBs_free_ckpt\": %.1f}\n",
          F, waves, bytes_ck, bytes_nock, m1, bytes_ck / (m1 * 1e-3) / 1e9, m0, bytes_nock / (m0 * 1e-3) / 1e9, m2,
          bytes_ck / (m2 * 1e-3) / 1e9, m3, bytes_ck / (m3 * 1e-3) / 1e9);
+  printf("{\"ms_1wps_ckpt_seq\": %.3f, \"GBs_1wps_ckpt_seq\": %.1f, \"ms_free_ckpt_seq\": %.3f, \"GBs_free_ckpt_seq\": %.1f}\n",
+         m4, bytes_ck / (m4 * 1e-3) / 1e9, m5, bytes_ck / (m5 * 1e-3) / 1e9);
   for (void* p : bufs) (void)hipFree(p);
   return 0;
 }

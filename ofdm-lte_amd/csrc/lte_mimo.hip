@@ -60,14 +60,14 @@ __device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ 
   return zero ? mkc((R)0, (R)0) : qam_point<BPS, R>(idx);
 }
 
-template <class R, int MODE, int CODED, int BPS>
+template <class R, int MODE, int CODED, int BPS, int NC = 0>
 __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                       const uint32_t* __restrict__ enc, int enc_words,
                                                       const int32_t* __restrict__ tx_map, cx<R>* __restrict__ x,
                                                       int B, int stage_enc) {
   using V = cx<R>;
   V* sm = mimo_lds<V>();
-  const int N = g.N, T = N >> 3, spw = MWG / T;
+  const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int per = g.n_sym * m.num_tx;
   const int gs = blockIdx.x * spw + slot;
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
     for (int p = tid; p < npt; p += T) buf[m.ppos[t * m.maxP + p]] = pv[p];
   }
   __syncthreads();
-  fft_lds<true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
+  fft_lds<true, NC>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
   if (active) {
     const R sc = tx_scale<R>(N);
     V* xo = x + ((size_t)b * m.num_tx + t) * g.L + (size_t)l * (N + g.cp);
@@ -133,8 +133,14 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
   const int stage_enc = coded && enc_shm <= 32768;
   const size_t shm = spw * g.N * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
 #define LTE_TXM(M_, C_, B_)                                                                                          \
-  hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words, \
-                     tx_map, x, B, stage_enc)
+  do {                                                                                                               \
+    if (g.N == 2048)   /* 20 MHz: compile-time N (unrolled passes, twiddle recurrence) */                            \
+      hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc,  \
+                         enc_words, tx_map, x, B, stage_enc);                                                        \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc,        \
+                         enc_words, tx_map, x, B, stage_enc);                                                        \
+  } while (0)
 #define LTE_TXM_BPS(M_, C_) \
   do { if (g.bps == 2) LTE_TXM(M_, C_, 2); else if (g.bps == 4) LTE_TXM(M_, C_, 4); else LTE_TXM(M_, C_, 6); } while (0)
   if (m.mode == MIMO_SFBC) {
@@ -721,14 +727,14 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
 // TX's pilot subset + linear interpolation with edge hold (:108-185 +
 // lte_receiver.py:98-133: np.linspace, k (delta / gap) + start) at the data
 // SCs -> H[b][rx][e][tx][n_dsc].
-template <class R>
+template <class R, int NC = 0>
 __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
                                                      const R* __restrict__ npow, const uint64_t* __restrict__ fid,
                                                      uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride,
                                                      cx<R>* __restrict__ Y, cx<R>* __restrict__ H) {
   using V = cx<R>;
   V* sm = mimo_lds<V>();
-  const int N = g.N, T = N >> 3, spw = MWG / T;
+  const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int per = m.num_rx * g.n_sym;
   const int gs = blockIdx.x * spw + slot;
@@ -743,7 +749,7 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
                              g.L, tid, T);
   }
   __syncthreads();
-  fft_lds<false, 0, false, false, true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
+  fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
   const int e = m.mode == MIMO_SFBC ? l / 14 : l;
   const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
   const R sc = rx_scale<R>(N);
@@ -789,8 +795,12 @@ int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, c
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(cx<R>);
-  hipLaunchKernelGGL(k_rx_fft_mimo<R>, dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z, inj_stride,
-                     Y, H);
+  if (g.N == 2048)   // 20 MHz: compile-time N (unrolled passes, twiddle recurrence)
+    hipLaunchKernelGGL((k_rx_fft_mimo<R, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
+                       inj_stride, Y, H);
+  else
+    hipLaunchKernelGGL((k_rx_fft_mimo<R>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
+                       inj_stride, Y, H);
   return (int)hipGetLastError();
 }
 

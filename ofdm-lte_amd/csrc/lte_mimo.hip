@@ -420,6 +420,36 @@ __device__ __forceinline__ cx<R> link_noise_at(int n, R sg, const R* __restrict_
   return mkc(v.x + sg * z.x, v.y + sg * z.y);
 }
 
+// The link noise of a SymSpan's J samples (Philox path; the same values as
+// link_noise_at per sample).  With an even base, lane pair (2k, 2k+1) holds
+// sample pairs (n, n + 1) that share one Philox draw (counter n >> 1): the
+// even lane draws for sample j, the odd lane for sample j + 1, and each hands
+// its partner the other half through one xor-1 shuffle -- one draw per lane
+// per two samples instead of one per sample.
+template <class R, int J>
+__device__ __forceinline__ void link_noise_span(cx<R> (&acc)[J], const SymSpan<J>& sp, R sg, uint64_t seed,
+                                                uint64_t frame, int link, bool even_base) {
+  if (!even_base) {
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (sp.ok[j]) acc[j] = link_noise_at<R>(sp.n[j], sg, nullptr, 0, seed, frame, link, acc[j]);
+    return;
+  }
+  const bool odd = threadIdx.x & 1;
+#pragma unroll
+  for (int j = 0; j < J; j += 2) {
+    const int jo = j + 1 < J ? j + 1 : j;
+    const u32x4 r = rng4(seed, frame, RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(sp.n[odd ? jo : j] >> 1));
+    const uint32_t g0 = __shfl_xor(odd ? r.x : r.z, 1), g1 = __shfl_xor(odd ? r.y : r.w, 1);
+    // even lane: sample j (even n) its own (x, y), sample jo (even n) the partner's (x, y);
+    // odd lane: sample j (odd n) the partner's (z, w), sample jo (odd n) its own (z, w)
+    const cx<R> zj = gauss2<R>(odd ? g0 : r.x, odd ? g1 : r.y);
+    const cx<R> zo = gauss2<R>(odd ? r.z : g0, odd ? r.w : g1);
+    if (sp.ok[j]) acc[j] = mkc(acc[j].x + sg * zj.x, acc[j].y + sg * zj.y);
+    if (jo != j && sp.ok[jo]) acc[jo] = mkc(acc[jo].x + sg * zo.x, acc[jo].y + sg * zo.y);
+  }
+}
+
 // pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
 // one block per (frame, OFDM symbol, TX stream), the receive antennas in groups
 template <class R, int J, bool EX>
@@ -539,10 +569,14 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
           const int link = (rg + q) * num_tx + tx;
           if (link_sigma) {
             const R sg = link_sigma[(size_t)b * nl + link];
-            const R* zf = inj_lz ? inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L : nullptr;
+            if (inj_lz) {
+              const R* zf = inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L;
 #pragma unroll
-            for (int j = 0; j < J; ++j)
-              if (sp.ok[j]) acc[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, acc[q][j]);
+              for (int j = 0; j < J; ++j)
+                if (sp.ok[j]) acc[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, acc[q][j]);
+            } else {
+              link_noise_span<R, J>(acc[q], sp, sg, seed, fid[b], link, (nbeg & 1) == 0);
+            }
           }
           if constexpr (F64) {
 #pragma unroll

@@ -1657,16 +1657,17 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
 
 }  // extern "C"
 
-// TX with the channel fused in (TxChannelT): SISO Rayleigh, delays within the
-// CP, no TX / RX stream capture; static taps (fD = 0) or per-symbol Taylor
-// sets while mimo_taylor_ok (3 km/h at 20 MHz: |w| S / 2 = 1.2e-3).
+// TX with the channel fused in (TxChannelT): SISO / SIMO Rayleigh (SC-FDM
+// precoding included), delays within the CP, no TX / RX stream capture; static
+// taps (fD = 0) or per-symbol Taylor sets while mimo_taylor_ok (3 km/h at
+// 20 MHz: |w| S / 2 = 1.2e-3).
 // LTE_TXCH_FUSE=0 selects the separate TX and channel kernels (A/B and
 // parity tests).
 static bool txch_fusable(const lte_plan* p, const lte_run_args* a, bool coded) {
   const lte_plan_desc& d = p->d;
   if (d.channel != LTE_CH_RAYLEIGH || d.num_rx < 1 || p->mimo || p->bf) return false;
   if (d.fD != 0.0 && !mimo_taylor_ok(d.fD, d.fs, d.N + d.cp_len)) return false;
-  if ((d.sc_fdm && !coded) || a->in_signal || a->cap_signal_tx || a->cap_signal_rx) return false;
+  if (a->in_signal || a->cap_signal_tx || a->cap_signal_rx) return false;
   if (const char* e = std::getenv("LTE_TXCH_FUSE"))
     if (std::atoi(e) == 0) return false;
   return txch_supported(p->grid, d.n_paths, *std::max_element(d.delays, d.delays + d.n_paths));
@@ -1721,7 +1722,7 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
       LCHK(launch_ofdm_txf<R>(s, p->grid, p->enc.p, p->enc_words, p->tx_map.p, B, cap_tx_syms, ch));
     else
       LCHK(launch_ofdm_tx_ch<R>(s, p->grid, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, B,
-                                cap_tx_syms, ch));
+                                cap_tx_syms, ch, (d.sc_fdm && !coded) ? 1 : 0));
   }
   {
     Timer t(p, KN_CHANNEL, s);

@@ -106,7 +106,8 @@ int launch_jakes_sets(hipStream_t s, int B, int n_paths, int n_sym, int sym_len,
                       double fD, double fs, cx<R>* tcoef);
 template <class R>
 int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                      int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch);
+                      int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch,
+                      int sc_fdm = 0);
 template <class R>
 int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannelT<R>& ch);
 // coded TX + channel with one slot per frame (the frame's coded streams staged

@@ -387,31 +387,36 @@ bool txch_supported(const Grid& g, int n_paths, int max_delay) {
 
 template <class R>
 int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
-                      int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch) {
+                      int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch,
+                      int sc_fdm) {
   const int spw = WG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym;
+  if (sc_fdm && (coded || !GridT<R>::chirp(g) || !GridT<R>::bhat(g) || 2 * g.Nd > g.N))
+    return (int)hipErrorInvalidValue;
   if (!txch_supported(g, ch.n_paths, ch.max_delay) || total > 0x7FFFFFFF - spw ||
       (g.bps != 2 && g.bps != 4 && g.bps != 6))
     return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t enc_shm = tx_enc_shm(coded, spw, enc_words);
   const int stage_enc = enc_shm > 0;
-  const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + enc_shm;
-#define LTE_TXC2(C_, B_, CH_)                                                                                     \
+  const size_t shm = (sc_fdm ? 2 : 1) * (size_t)spw * g.N * sizeof(cx<R>) + enc_shm;
+#define LTE_TXC2(C_, B_, S_, CH_)                                                                                 \
   if (g.N == 2048)                                                                                                 \
-    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, false, CH_, 2048>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,   \
+    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, S_, CH_, 2048>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,      \
                        enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch);                             \
   else                                                                                                             \
-    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, false, CH_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,          \
+    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, S_, CH_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,             \
                        enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch)
-#define LTE_TXC(C_, B_)                                                                                          \
+#define LTE_TXC(C_, B_, S_)                                                                                      \
   do {                                                                                                             \
-    if (ch.tcoef) { LTE_TXC2(C_, B_, 2); } else { LTE_TXC2(C_, B_, 1); }                                           \
+    if (ch.tcoef) { LTE_TXC2(C_, B_, S_, 2); } else { LTE_TXC2(C_, B_, S_, 1); }                                   \
   } while (0)
   if (coded) {
-    if (g.bps == 2) LTE_TXC(1, 2); else if (g.bps == 4) LTE_TXC(1, 4); else LTE_TXC(1, 6);
+    if (g.bps == 2) LTE_TXC(1, 2, false); else if (g.bps == 4) LTE_TXC(1, 4, false); else LTE_TXC(1, 6, false);
+  } else if (sc_fdm) {   // SC-FDM (uncoded SISO / SIMO transmitters): DFT precoding, then the same channel
+    if (g.bps == 2) LTE_TXC(0, 2, true); else if (g.bps == 4) LTE_TXC(0, 4, true); else LTE_TXC(0, 6, true);
   } else {
-    if (g.bps == 2) LTE_TXC(0, 2); else if (g.bps == 4) LTE_TXC(0, 4); else LTE_TXC(0, 6);
+    if (g.bps == 2) LTE_TXC(0, 2, false); else if (g.bps == 4) LTE_TXC(0, 4, false); else LTE_TXC(0, 6, false);
   }
 #undef LTE_TXC
 #undef LTE_TXC2
@@ -1623,7 +1628,7 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
   template int launch_ofdm_tx<R>(hipStream_t, const Grid&, int, const uint32_t*, int, const uint32_t*, int,          \
                                  const int32_t*, cx<R>*, int, cx<R>*, int);                                         \
   template int launch_ofdm_tx_ch<R>(hipStream_t, const Grid&, int, const uint32_t*, int, const uint32_t*, int,       \
-                                    const int32_t*, int, cx<R>*, const TxChannelT<R>&);                             \
+                                    const int32_t*, int, cx<R>*, const TxChannelT<R>&, int);                        \
   template int launch_chan_fix<R>(hipStream_t, const Grid&, int, const TxChannelT<R>&);                             \
   template int launch_ofdm_txf<R>(hipStream_t, const Grid&, const uint32_t*, int, const int32_t*, int, cx<R>*,      \
                                   const TxChannelT<R>&);                                                             \

@@ -649,7 +649,7 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
   m.mode = mode == 0 ? MIMO_SFBC : MIMO_SPATIAL;
   m.num_tx = num_tx;
   m.num_rx = num_rx;
-  m.exact_jakes = sizeof(R) == 8 && ray && fD != 0.0 && !mimo_taylor_ok(fD, fs, chunk);
+  m.exact_jakes = ray && fD != 0.0 && !mimo_taylor_ok_prec(sizeof(R) == 8, fD, fs, chunk);
   for (int k = 0; k < 16; ++k) m.jw[k] = 6.283185307179586 * fD * std::cos(6.283185307179586 * (k + 1) / 16.0);
   m.n_cs = (ray && fD != 0.0 && !m.exact_jakes) ? (int)((L + chunk - 1) / chunk) : 1;
   const int np = ray ? n_paths : 1;
@@ -1271,8 +1271,8 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
     // fD != 0: the Jakes sum expanded per OFDM symbol (f32 second order, f64
     // degree 5); past mimo_taylor_ok f64 evaluates it per sample (jw[m] = (2 pi
     // fD) cos(alpha_m), rayleighchannel.py:28-38)
-    m.exact_jakes = p->f64 && d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0 &&
-                    !mimo_taylor_ok(d.fD, d.fs, d.N + d.cp_len);
+    m.exact_jakes = d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0 &&
+                    !mimo_taylor_ok_prec(p->f64, d.fD, d.fs, d.N + d.cp_len);
     for (int k = 0; k < 16; ++k) m.jw[k] = 6.283185307179586 * d.fD * std::cos(6.283185307179586 * (k + 1) / 16.0);
     m.n_cs = (d.channel == LTE_CH_RAYLEIGH && d.fD != 0.0 && !m.exact_jakes) ? p->n_sym : 1;
     rc = plan_mimo_tables(p);

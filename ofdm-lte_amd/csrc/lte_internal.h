@@ -211,6 +211,12 @@ template <class R> constexpr int mimo_ncf() { return sizeof(R) == 8 ? 6 : 3; }
 inline bool mimo_taylor_ok(double fD, double fs, int span) {
   return 6.283185307179586 * (fD < 0 ? -fD : fD) / fs * (0.5 * span) <= 2.7e-3;
 }
+// f32's per-symbol quadratic: truncation (|w| S / 2)^3 / 6 under float32's
+// half ulp (6e-8) while |w| S / 2 <= 7e-3 (~20 km/h at 20 MHz); past it the
+// per-sample sum (exact_jakes) in float64 arithmetic, rounded to float
+inline bool mimo_taylor_ok_prec(bool f64, double fD, double fs, int span) {
+  return f64 ? mimo_taylor_ok(fD, fs, span) : 6.283185307179586 * (fD < 0 ? -fD : fD) / fs * (0.5 * span) <= 7e-3;
+}
 struct MimoGrid {
   int mode, num_tx, num_rx;
   int res;                 // QAM symbols per OFDM symbol: SFBC Nd&~1, spatial Nd

@@ -167,7 +167,8 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
 //    < 1e-17, under float64 rounding); past mimo_taylor_ok the phases are stored
 //    and the channel kernels evaluate the sum per sample (exact_jakes);
 //  * fD != 0, f32: the same expansion to second order, A + B d + C d^2
-//    (truncation ~1e-10, far below float32), computed in float64.
+//    (truncation ~1e-10 at 3 km/h, far below float32), computed in float64,
+//    while mimo_taylor_ok_prec; past it the per-sample sum, rounded to float.
 // AWGN links: SFBC h = exp(j t pi/2) (core/ofdm_core.py:476-487); spatial
 // h ~ CN(0,1) (core/channel.py:473-480), injected or Philox.
 // coef layout: [B][rx][tx][path][n_cs][mimo_ncf<R>()]; phases [B][rx][tx][path][16].
@@ -244,6 +245,8 @@ __global__ __launch_bounds__(MWG) void k_fading_mimo(int B, int num_rx, int num_
     return;
   } else {
     jakes_symbol_sets<R>(ph, (double)gains[p], fD, fs, sym_len, n_cs, out);
+    if (phases)   // past the quadratic's bound: the per-sample sum (exact_jakes)
+      for (int mm = 0; mm < 16; ++mm) phases[(size_t)i * 16 + mm] = (R)ph[mm];
   }
 }
 
@@ -284,6 +287,13 @@ __device__ __noinline__ double2 jakes_exact(const MimoGrid& m, const double (&ph
   const double k = 0.3535533905932738;   // np.sqrt(2 / 16)
   return make_double2(gn * (sr * k), gn * (si * k));
 }
+// the exact value in the chain's type (float: rounded once)
+template <class R>
+__device__ __forceinline__ cx<R> jakes_exact_r(const MimoGrid& m, const double (&ph)[16], double gn, int n,
+                                               double fs) {
+  const double2 h = jakes_exact(m, ph, gn, n, fs);
+  return mkc((R)h.x, (R)h.y);
+}
 
 // one link's output at a single sample n (link_sample: coefficient triples of
 // n's symbol; EX: f64 exact Jakes from the phases ph)
@@ -295,14 +305,13 @@ __device__ __forceinline__ cx<R> link_value(int n, const cx<R>* __restrict__ cf,
   using V = cx<R>;
   V acc = mkc((R)0, (R)0);
   if constexpr (EX) {
-    static_assert(sizeof(R) == 8, "exact Jakes is the float64 path");
     for (int p = 0; p < np; ++p) {
       const int src = n - (delays ? delays[p] : 0);
       if (src < 0) continue;
       double phv[16];
 #pragma unroll
       for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[p * 16 + mm];
-      acc = cadd(acc, cmul(jakes_exact(m, phv, gains[p], n, fs), xf[src]));
+      acc = cadd(acc, cmul(jakes_exact_r<R>(m, phv, (double)gains[p], n, fs), xf[src]));
     }
     return acc;
   }
@@ -373,15 +382,14 @@ __device__ __forceinline__ void links_accumulate(cx<R> (&acc)[MC_RXG][J], int nq
     for (int q = 0; q < MC_RXG; ++q) {
       if (q >= nq) break;
       if constexpr (EX) {
-        static_assert(sizeof(R) == 8, "exact Jakes is the float64 path");
-        double phv[16];
+          double phv[16];
 #pragma unroll
         for (int mm = 0; mm < 16; ++mm) phv[mm] = ph[q * ph_q + p * 16 + mm];
         const double gn = gains[p];
 #pragma unroll
         for (int j = 0; j < J; ++j)
           if (sp.ok[j] && sp.n[j] >= dl)
-            acc[q][j] = cadd(acc[q][j], cmul(jakes_exact(m, phv, gn, sp.n[j], fs), xs[j]));
+            acc[q][j] = cadd(acc[q][j], cmul(jakes_exact_r<R>(m, phv, gn, sp.n[j], fs), xs[j]));
       } else {
         const V* c = cs + q * cs_q + (size_t)p * n_cs * NCF;
         if (n_cs > 1) {   // sum_k c_k d^k (Horner; f32: A + B d + C d^2)
@@ -645,9 +653,7 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   } while (0)
 #define LTE_CHM(J_)                                                                                                 \
   do {                                                                                                             \
-    if constexpr (sizeof(R) == 8) {                                                                                \
-      if (m.exact_jakes) { LTE_CHM_EX(J_, true); break; }                                                          \
-    }                                                                                                              \
+    if (m.exact_jakes) { LTE_CHM_EX(J_, true); break; }                                                            \
     LTE_CHM_EX(J_, false);                                                                                         \
   } while (0)
   switch (J) {
@@ -722,11 +728,8 @@ int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, in
   hipLaunchKernelGGL((k_link_stats_part<R, EX_>), dim3(nblk * B, m.num_rx * m.num_tx), dim3(MWG), 0, s, g.L,         \
                      m.num_rx, m.num_tx, n_paths, m.n_cs, g.N + g.cp, delays, coef, phases, gains, fs, m, x,          \
                      link_sigma, fid, seed, inj_lz, inj_lz_stride, part, nblk)
-  bool done = false;
-  if constexpr (sizeof(R) == 8) {
-    if (m.exact_jakes) { LTE_LSP(true); done = true; }
-  }
-  if (!done) LTE_LSP(false);
+  if (m.exact_jakes) LTE_LSP(true);
+  else LTE_LSP(false);
 #undef LTE_LSP
   const int n = B * m.num_rx * m.num_tx * 4;
   hipLaunchKernelGGL(k_link_stats_fin<R>, dim3((n + 255) / 256), dim3(256), 0, s, n, part, nblk, g.L, stats);

@@ -424,6 +424,7 @@ struct lte_plan {
   DBuf<CbInfo> cbi;
   DBuf<int32_t> tx_map, rx_map, delays;
   DBuf<uint32_t> pw, enc, inj_bits;
+  DBuf<uint8_t> inj_bytes;   // the caller's payload bits as given (packed on the device)
   DBuf<uint16_t> enc_qmask;   // encoder 2's per-bit segment-state contributions (encode_qmask)
   int qstride = 0;
   ChainBufs<float> c32;              // f32 plans (and the beamforming chain)
@@ -1320,7 +1321,7 @@ int lte_plan_destroy(lte_plan* p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   p->tabs.release();
   p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release();
-  p->pw.release(); p->enc.release(); p->inj_bits.release(); p->enc_qmask.release();
+  p->pw.release(); p->enc.release(); p->inj_bits.release(); p->inj_bytes.release(); p->enc_qmask.release();
   p->c32.release(); p->c64.release();
   p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->fid.release(); p->counts.release();
   p->cap_bits.release();
@@ -1391,11 +1392,15 @@ template <class R>
 static int upload_inj(DBuf<R>& dst, const double* src, int64_t stride, int B, size_t per, hipStream_t s,
                       const R** out, int64_t* out_stride) {
   const int nf = stride ? B : 1;
-  std::vector<R> h((size_t)nf * per);
-  for (int f = 0; f < nf; ++f)
-    for (size_t i = 0; i < per; ++i) h[f * per + i] = (R)src[(size_t)f * stride + i];
-  if (dst.alloc(h.size())) return fail(LTE_ENOMEM, "injection buffer");
-  HIPCHK(hipMemcpyAsync(dst.p, h.data(), h.size() * sizeof(R), hipMemcpyHostToDevice, s));
+  if (dst.alloc((size_t)nf * per)) return fail(LTE_ENOMEM, "injection buffer");
+  if (sizeof(R) == 8 && (!stride || (size_t)stride == per)) {   // float64, dense: straight from the caller
+    HIPCHK(hipMemcpyAsync(dst.p, src, (size_t)nf * per * sizeof(R), hipMemcpyHostToDevice, s));
+  } else {
+    std::vector<R> h((size_t)nf * per);
+    for (int f = 0; f < nf; ++f)
+      for (size_t i = 0; i < per; ++i) h[f * per + i] = (R)src[(size_t)f * stride + i];
+    HIPCHK(hipMemcpyAsync(dst.p, h.data(), h.size() * sizeof(R), hipMemcpyHostToDevice, s));
+  }
   HIPCHK(hipStreamSynchronize(s));
   *out = dst.p;
   *out_stride = stride ? (int64_t)per : 0;
@@ -2000,14 +2005,13 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   // payload injection (packed MSB-first)
   const uint32_t* inj_bits = nullptr;
   int64_t inj_bits_stride = 0;
-  std::vector<uint32_t> hb;
-  if (a->bits) {
+  if (a->bits) {   // one uint8 per bit from the caller, packed MSB-first on the device
     const int nf = a->bits_stride ? B : 1;
     const int nwd = (d.n_bits + 31) / 32;
-    hb.assign((size_t)nf * nwd, 0);
-    for (int f = 0; f < nf; ++f) pack_bits(a->bits + (size_t)f * a->bits_stride, d.n_bits, &hb[(size_t)f * nwd], nwd);
-    if (p->inj_bits.alloc(hb.size())) return fail(LTE_ENOMEM, "inj bits");
-    HIPCHK(hipMemcpyAsync(p->inj_bits.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, s));
+    const size_t nb = a->bits_stride ? (size_t)(nf - 1) * a->bits_stride + d.n_bits : (size_t)d.n_bits;
+    if (p->inj_bytes.alloc(nb) || p->inj_bits.alloc((size_t)nf * nwd)) return fail(LTE_ENOMEM, "inj bits");
+    HIPCHK(hipMemcpyAsync(p->inj_bytes.p, a->bits, nb, hipMemcpyHostToDevice, s));
+    LCHK(launch_pack_bits(s, p->inj_bytes.p, a->bits_stride, d.n_bits, nwd, nf, p->inj_bits.p));
     inj_bits = p->inj_bits.p;
     inj_bits_stride = a->bits_stride ? nwd : 0;
   }

@@ -99,6 +99,9 @@ struct TxChannelT {
   const cx<R>* tcoef;
 };
 bool txch_supported(const Grid& g, int n_paths, int max_delay);
+// host payload bits (one uint8 per bit, frames `stride` bytes apart) already on
+// the device -> packed MSB-first words [nf][nwd]
+int launch_pack_bits(hipStream_t s, const uint8_t* bits, int64_t stride, int n_bits, int nwd, int nf, uint32_t* out);
 // per-OFDM-symbol Taylor sets of the SISO paths from k_fading's phases (the
 // fused TX channel at fD != 0): [B][n_paths][n_sym][mimo_ncf<R>()]
 template <class R>

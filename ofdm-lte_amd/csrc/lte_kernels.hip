@@ -646,6 +646,29 @@ int launch_fading(hipStream_t s, int B, int num_rx, int n_paths, const R* gains_
   return (int)hipGetLastError();
 }
 
+// Host payload injection: the caller's uint8 bits (copied to the device as
+// they are) packed MSB-first into 32-bit words, one word per thread (the
+// lanes of a wave read 64 consecutive 32-byte runs: coalesced).
+__global__ __launch_bounds__(WG) void k_pack_bits(const uint8_t* __restrict__ bits, int64_t stride, int n_bits,
+                                                  int nwd, int nf, uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (i >= (int64_t)nf * nwd) return;
+  const int f = (int)(i / nwd), w = (int)(i - (int64_t)f * nwd);
+  const uint8_t* src = bits + f * stride + (int64_t)w * 32;
+  const int n = min(32, n_bits - w * 32);
+  uint32_t v = 0;
+  for (int k = 0; k < n; ++k) v |= (uint32_t)(src[k] & 1) << (31 - k);
+  out[i] = v;
+}
+
+int launch_pack_bits(hipStream_t s, const uint8_t* bits, int64_t stride, int n_bits, int nwd, int nf, uint32_t* out) {
+  const int64_t n = (int64_t)nf * nwd;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, bits, stride, n_bits, nwd, nf,
+                     out);
+  return (int)hipGetLastError();
+}
+
 // Per-symbol Taylor sets of the SISO paths (fD != 0, the fused TX channel):
 // one thread per (frame, path) from k_fading's 16 phases (jakes_symbol_sets).
 template <class R>

@@ -1430,13 +1430,22 @@ int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B
 // slot per frame walks its OFDM symbols; per symbol every RX in turn is loaded
 // with its noise, FFT'd and folded into the MRC sums sum_r conj(H_r) Y_r /
 // (sum_r |H_r|^2 + 1e-10), RX 0 first as k_rx_data sums them.  The first symbol
-// of each 14-symbol group also yields every RX's LS estimate (k_rx_chest's
-// work on the FFT the data path needs anyway), kept in registers for the
-// thread's data subcarriers (hq[r][q], selected by an unrolled compare so the
-// FFT itself is not duplicated per RX).  Same arithmetic per RE as k_rx_chest
-// + k_rx_data<SIMO> (test_fused_simo_receiver_matches_separate_kernels).
+// of each 14-symbol group also yields every RX's LS pilot estimates, kept in
+// LDS per RX (k_rx_chest's work on the FFT the data path needs anyway); each
+// RE's estimate is interpolated from them per symbol with the thread's
+// per-subcarrier segment / offset / 1-over-gap held in registers (chest_interp's
+// expression), so no per-RX estimate occupies registers.  Same arithmetic per
+// RE as k_rx_chest + k_rx_data<SIMO> (test_fused_simo_receiver_matches_separate_kernels).
+template <class R>
+__device__ __forceinline__ cx<R> interp_seg(const cx<R>* hp, int np, int sidx, R fk, R ig) {
+  if (sidx < 0) return hp[0];
+  if (sidx >= np - 1) return hp[np - 1];
+  const cx<R> v0 = hp[sidx], v1 = hp[sidx + 1];
+  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+}
+
 template <class R, int BPS, int NC = 0>
-__global__ __launch_bounds__(WG, sizeof(R) == 8 ? 2 : RXF_WAVES) void k_rx_frame_simo(
+__global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo(
     Grid g, int B, int num_rx, const cx<R>* __restrict__ y, int64_t y_rx_stride, int64_t y_frame_stride,
     const R* __restrict__ npow, const uint64_t* __restrict__ fid, uint64_t seed, const R* __restrict__ inj_z,
     int64_t inj_stride, const uint32_t* __restrict__ pw, int PW, int n_bits, uint32_t* __restrict__ frame_err,
@@ -1448,8 +1457,8 @@ __global__ __launch_bounds__(WG, sizeof(R) == 8 ? 2 : RXF_WAVES) void k_rx_frame
   const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
   const int b = blockIdx.x * spw + slot;
   const bool active = slot < spw && b < B;
-  V* buf = sm + slot * (N + g.Np);
-  V* hp = buf + N;
+  V* buf = sm + slot * (N + RXS_MAXRX * g.Np);
+  V* hpa = buf + N;   // [RXS_MAXRX][Np] pilot LS estimates of the current group
   const R sc = rx_scale<R>(N);
   constexpr R QS = (R)qam_norm<BPS>();
   constexpr int QM = 4;   // data REs per thread (Nd < N/2 for every LTE profile)
@@ -1457,20 +1466,20 @@ __global__ __launch_bounds__(WG, sizeof(R) == 8 ? 2 : RXF_WAVES) void k_rx_frame
   const V* yf = y + (size_t)(active ? b : 0) * y_frame_stride;
   const uint32_t* fb = pw + (size_t)(active ? b : 0) * PW;
   const size_t fre = (size_t)(active ? b : 0) * g.n_sym * g.Nd;
-  int kpos[QM];
+  int kpos[QM], sg[QM];
+  R fk[QM], ig[QM];
 #pragma unroll
-  for (int q = 0; q < QM; ++q) {
+  for (int q = 0; q < QM; ++q) {   // chest_interp's per-subcarrier terms
     const int j = tid0 + q * T;
     kpos[q] = (active && j < g.Nd) ? g.data_idx[j] : 0;
+    sg[q] = g.seg[kpos[q]];
+    const int sc_ = sg[q] < 0 ? 0 : (sg[q] >= g.Np - 1 ? g.Np - 1 : sg[q]);
+    fk[q] = (R)(kpos[q] - g.pilot_idx[sc_]);
+    ig[q] = GridT<R>::inv_gap(g)[sc_];
   }
-  V hq[RXS_MAXRX][QM];
   R den[QM];
 #pragma unroll
-  for (int q = 0; q < QM; ++q) {
-    den[q] = (R)0;
-#pragma unroll
-    for (int r = 0; r < RXS_MAXRX; ++r) hq[r][q] = mkc((R)0, (R)0);
-  }
+  for (int q = 0; q < QM; ++q) den[q] = (R)0;
   uint32_t errs = 0;
   for (int l = 0; l < g.n_sym; ++l) {
     const bool est = l % 14 == 0;
@@ -1492,6 +1501,7 @@ __global__ __launch_bounds__(WG, sizeof(R) == 8 ? 2 : RXF_WAVES) void k_rx_frame
       }
       __syncthreads();
       fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, G::tw(g), tid, active);
+      V* hp = hpa + rx * g.Np;
       if (est) {   // this RX's group estimate from the group's first symbol (lte_receiver.py:360-411)
         if (active)
           for (int p = tid; p < g.Np; p += T) {
@@ -1509,13 +1519,7 @@ __global__ __launch_bounds__(WG, sizeof(R) == 8 ? 2 : RXF_WAVES) void k_rx_frame
 #pragma unroll
           for (int q = 0; q < QM; ++q) {
             const int j = tid + q * T;
-            if (j < g.Nd) {
-              const V h = chest_interp<R>(g, hp, kpos[q]);
-              den[q] += abs2_ref(h);
-#pragma unroll
-              for (int r = 0; r < RXS_MAXRX; ++r)
-                if (r == rx) hq[r][q] = h;
-            }
+            if (j < g.Nd) den[q] += abs2_ref(interp_seg<R>(hp, g.Np, sg[q], fk[q], ig[q]));
           }
           if (pstats && tid == 0) {
             R pp = (R)0, en = (R)0;
@@ -1534,13 +1538,8 @@ __global__ __launch_bounds__(WG, sizeof(R) == 8 ? 2 : RXF_WAVES) void k_rx_frame
 #pragma unroll
         for (int q = 0; q < QM; ++q) {
           const int j = tid + q * T;
-          if (j < g.Nd) {
-            V h = hq[0][q];
-#pragma unroll
-            for (int r = 1; r < RXS_MAXRX; ++r)
-              if (r == rx) h = hq[r][q];
-            num[q] = cadd(num[q], cmulc(cscale(buf[kpos[q]], sc), h));
-          }
+          if (j < g.Nd)
+            num[q] = cadd(num[q], cmulc(cscale(buf[kpos[q]], sc), interp_seg<R>(hp, g.Np, sg[q], fk[q], ig[q])));
         }
       }
       __syncthreads();   // every read of buf done before the next RX / symbol lands in it
@@ -1583,7 +1582,7 @@ int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const 
   if (!rx_frame_simo_supported(g, num_rx)) return (int)hipErrorInvalidValue;
   const int spw = WG / (g.N >> 3);
   const int blocks = (B + spw - 1) / spw;
-  const size_t shm = (size_t)spw * (g.N + g.Np) * sizeof(cx<R>);
+  const size_t shm = (size_t)spw * (g.N + RXS_MAXRX * g.Np) * sizeof(cx<R>);
 #define LTE_RXS(BPS_, NC_)                                                                                           \
   hipLaunchKernelGGL((k_rx_frame_simo<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, B, num_rx, y, y_rx_stride,  \
                      y_frame_stride, npow, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, cap_syms,        \

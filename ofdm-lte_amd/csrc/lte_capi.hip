@@ -1069,8 +1069,8 @@ static bool alloc_siso(lte_plan* p, bool coded) {
     std::vector<R*> bp(p->C);
     for (int r = 0; r < p->C; ++r) {
       const int K = p->cbs[r].K;
-      bad |= c.blk[r].alloc((size_t)G * turbo_rows(K) * 64) != 0;
-      bad |= c.ckpt[r].alloc((size_t)G * turbo_nwin(K) * turbo_ck_rows(sizeof(R) == 8) * 64) != 0;
+      bad |= c.blk[r].alloc((size_t)turbo_galloc(G) * turbo_rows(K) * 64) != 0;
+      bad |= c.ckpt[r].alloc((size_t)turbo_galloc(G) * turbo_nwin(K) * turbo_ck_rows(sizeof(R) == 8) * 64) != 0;
       if (!bad && hipMemset(c.blk[r].p, 0, c.blk[r].n * sizeof(R)) != hipSuccess) bad = true;
       bp[r] = c.blk[r].p;
     }
@@ -1114,8 +1114,8 @@ static bool alloc_mimo(lte_plan* p, bool coded) {
     std::vector<R*> bp(p->C);
     for (int r = 0; r < p->C; ++r) {
       const int K = p->cbs[r].K;
-      bad |= c.blk[r].alloc((size_t)G * turbo_rows(K) * 64) != 0;
-      bad |= c.ckpt[r].alloc((size_t)G * turbo_nwin(K) * turbo_ck_rows(sizeof(R) == 8) * 64) != 0;
+      bad |= c.blk[r].alloc((size_t)turbo_galloc(G) * turbo_rows(K) * 64) != 0;
+      bad |= c.ckpt[r].alloc((size_t)turbo_galloc(G) * turbo_nwin(K) * turbo_ck_rows(sizeof(R) == 8) * 64) != 0;
       if (!bad && hipMemset(c.blk[r].p, 0, c.blk[r].n * sizeof(R)) != hipSuccess) bad = true;
       bp[r] = c.blk[r].p;
     }
@@ -2267,8 +2267,8 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const T* llr, const T* 
   const int f64 = sizeof(T) == 8;
   const int G = (int)((ncb + 63) / 64);
   const int64_t rows = turbo_rows(K);
-  std::vector<T> h((size_t)G * rows * 64, (T)0);
-  auto at = [&](int64_t c, int64_t row) -> T& { return h[((c / 64) * rows + row) * 64 + (c % 64)]; };
+  std::vector<T> h((size_t)turbo_galloc(G) * rows * 64, (T)0);
+  auto at = [&](int64_t c, int64_t row) -> T& { return h[turbo_elem(rows, c / 64, row) + (c % 64)]; };
   for (int64_t c = 0; c < ncb; ++c) {
     if (mode == TM_APP) {
       const T* s = ls + c * (K + 3);
@@ -2295,7 +2295,7 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const T* llr, const T* 
   DBuf<T> db, dck;
   DBuf<uint32_t> dbits;
   const int KW = turbo_kw(K);
-  if (db.alloc(h.size()) || dck.alloc((size_t)G * turbo_nwin(K) * turbo_ck_rows(f64) * 64) ||
+  if (db.alloc(h.size()) || dck.alloc((size_t)turbo_galloc(G) * turbo_nwin(K) * turbo_ck_rows(f64) * 64) ||
       dbits.alloc((size_t)G * KW * 64))
     return fail(LTE_ENOMEM, "turbo buffers");
   int rc = LTE_OK;

@@ -218,26 +218,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
-template <class T>
+// Cache-policy bits of the decoder's row loads / stores (buffer "aux"; gfx950:
+// 1 = sc0, 2 = nt, 16 = sc1).  Measured on the decoder's access shape
+// (scripts/turbo_shape_bench.hip): nt helps only together with
+// the wave-chunked layout (TURBO_CH).
+#ifndef LTE_TURBO_CPOL
+#define LTE_TURBO_CPOL 2
+#endif
+
+// RSB: bytes between consecutive rows (TURBO_CH groups of 64 lanes for the
+// decoder's block arrays); CP: cache-policy bits
+template <class T, int RSB = RS * (int)sizeof(T), int CP = 0>
 struct RowPtr {
   __amdgpu_buffer_rsrc_t r;
   int row0;   // first row of this sub-array inside the block
-  int voff;   // sizeof(T) * lane
+  int voff;   // sizeof(T) * lane (+ the group's slot within its chunk)
   int rstr = 1;   // row stride of the sub-array (2: interleaved LS / LE)
   __device__ __forceinline__ T ld(int row) const {
-    const int so = (row0 + row * rstr) * (RS * (int)sizeof(T));
+    const int so = (row0 + row * rstr) * RSB;
     if constexpr (sizeof(T) == 8) {
-      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, voff, so, 0));
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, voff, so, CP));
     } else {
-      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, voff, so, 0));
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, voff, so, CP));
     }
   }
   __device__ __forceinline__ void st(int row, T v) const {
-    const int so = (row0 + row * rstr) * (RS * (int)sizeof(T));
+    const int so = (row0 + row * rstr) * RSB;
     if constexpr (sizeof(T) == 8) {
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, voff, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, voff, so, CP);
     } else {
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, so, CP);
     }
   }
 };
@@ -260,23 +270,25 @@ struct RowPtr {
 // packs the hard decisions L < 0 MSB-first into `bo` (words [kw][64 lanes]),
 // storing each word as the backward sweep reaches its bit 0 (no re-read pass).
 template <class T, int MODE, bool LM = false>
-__device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__ wck, int lane, int K, int f1,
-                                          int f2, bool first, uint32_t* __restrict__ bo = nullptr) {
+__device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__ wck, int slot, int lane, int K,
+                                          int f1, int f2, bool first, uint32_t* __restrict__ bo = nullptr) {
   using TT = TurboT<T>;
+  using DRow = RowPtr<T, RS * TURBO_CH * (int)sizeof(T), LTE_TURBO_CPOL>;   // the block arrays' rows
   constexpr int TSUB = TT::TSUB, SW = TW * TSUB, CK = TT::CK, CK0 = 8 - CK;   // CK0: first stored state
   constexpr int TH = TW / TT::HALVES;
-  const int vo = lane * (int)sizeof(T);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * RS * sizeof(T)));
+  // wbase / wck: the group's chunk; slot: the group's place in it (turbo_elem)
+  const int vo = (slot * RS + lane) * (int)sizeof(T);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * TURBO_CH * RS * sizeof(T)));
   // rows of step k < K: base + k * stride (lte_internal.h trow_*); tails separately
   constexpr int IST = LTE_TURBO_ILV == 3 ? 4 : LTE_TURBO_ILV == 2 ? 3 : LTE_TURBO_ILV == 1 ? 2 : 1;
   constexpr int DEC = (MODE == TM_DEC2) ? 2 : 1;
-  const RowPtr<T> LS{rb, 0, vo, IST};
-  const RowPtr<T> LS1T{rb, (int)trow_ls(K, K), vo};   // decoder 1's systematic tail
-  const RowPtr<T> LP{rb, (int)trow_lp(K, DEC, 0), vo, LTE_TURBO_ILV == 3 ? 4 : (DEC == 1 && LTE_TURBO_ILV == 2) ? 3 : 1};
-  const RowPtr<T> LPT{rb, (int)trow_lp(K, DEC, K), vo};   // parity tail
-  const RowPtr<T> LS2T{rb, (int)trow_ls2t(K, 0), vo};
-  const RowPtr<T> LE{rb, (int)trow_le(K, 0), vo, IST};
-  const RowPtr<T> ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * CK * RS * sizeof(T))), 0, vo};
+  const DRow LS{rb, 0, vo, IST};
+  const DRow LS1T{rb, (int)trow_ls(K, K), vo};   // decoder 1's systematic tail
+  const DRow LP{rb, (int)trow_lp(K, DEC, 0), vo, LTE_TURBO_ILV == 3 ? 4 : (DEC == 1 && LTE_TURBO_ILV == 2) ? 3 : 1};
+  const DRow LPT{rb, (int)trow_lp(K, DEC, K), vo};   // parity tail
+  const DRow LS2T{rb, (int)trow_ls2t(K, 0), vo};
+  const DRow LE{rb, (int)trow_le(K, 0), vo, IST};
+  const DRow ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * CK * TURBO_CH * RS * sizeof(T))), 0, vo};
   const int nsub = K / TW;   // every LTE K is a multiple of 8
   const int tf2 = (2 * f2) % K;
   const bool use_la = !first;
@@ -493,20 +505,22 @@ __device__ __forceinline__ void turbo_body(const TurboJobs& jobs, int iters, int
   const TurboJob jb = jobs.j[r];
   const int g = wg - jobs.prefix[r];
   const int K = jb.K;
-  T* base = reinterpret_cast<T*>(jb.blk) + (size_t)g * turbo_rows(K) * RS;
-  T* ck = reinterpret_cast<T*>(jb.ck) + (size_t)g * (turbo_nwin(K) * TurboT<T>::CK) * RS;
+  // the group's chunk of the block arrays (turbo_elem: [chunk][row][TURBO_CH][64])
+  const int slot = g % TURBO_CH;
+  T* base = reinterpret_cast<T*>(jb.blk) + turbo_elem(turbo_rows(K), g - slot, 0);
+  T* ck = reinterpret_cast<T*>(jb.ck) + turbo_elem(turbo_nwin(K) * TurboT<T>::CK, g - slot, 0);
   uint32_t* bo = jb.bits + (size_t)g * turbo_kw(K) * RS;
   if (mode == TM_APP) {
-    half_pass<T, TM_APP, LM>(base, ck, lane, K, jb.f1, jb.f2, false);
+    half_pass<T, TM_APP, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, false);
     return;
   }
   for (int it = 0; it < iters; ++it) {
-    half_pass<T, TM_DEC1, LM>(base, ck, lane, K, jb.f1, jb.f2, it == 0);
-    half_pass<T, TM_DEC2, LM>(base, ck, lane, K, jb.f1, jb.f2, false);
+    half_pass<T, TM_DEC1, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, it == 0);
+    half_pass<T, TM_DEC2, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, false);
   }
   // final pass = decoder 1 a-posteriori LLRs (turbo_decoder.py:440-447) and
   // the hard decisions L < 0 (:276), packed MSB-first
-  half_pass<T, TM_FINAL, LM>(base, ck, lane, K, jb.f1, jb.f2, iters == 0, bo);
+  half_pass<T, TM_FINAL, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, iters == 0, bo);
 }
 
 // f32 fast mode: 134 VGPRs = 3 waves per SIMD; LTE_TURBO32_WAVES = 2 / 1 caps

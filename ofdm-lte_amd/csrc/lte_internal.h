@@ -356,6 +356,19 @@ constexpr int TURBO_CK_ROWS_F32 = 7;
 constexpr int TURBO_CK_ROWS_F64 = 8;
 __host__ __device__ inline int turbo_ck_rows(int f64) { return f64 ? TURBO_CK_ROWS_F64 : TURBO_CK_ROWS_F32; }
 constexpr int TURBO_RS = 64;   // decoder row stride (elements): 64 code blocks per wave
+// Block arrays (decoder rows, checkpoints) are chunked over frame groups:
+// [chunk][row][TURBO_CH groups][64 lanes], so the rows of TURBO_CH waves that
+// run side by side share DRAM pages and TLB entries (TURBO_CH = 1: one group's
+// block contiguous).  Jobs allocate whole chunks (turbo_galloc).
+#ifndef LTE_TURBO_CH
+#define LTE_TURBO_CH 32
+#endif
+constexpr int TURBO_CH = LTE_TURBO_CH;
+__host__ __device__ inline int64_t turbo_galloc(int64_t G) { return (G + TURBO_CH - 1) / TURBO_CH * TURBO_CH; }
+// element offset of lane 0 of (group g, row) in a block array of `rows` rows per group
+__host__ __device__ inline int64_t turbo_elem(int64_t rows, int64_t g, int64_t row) {
+  return (((g / TURBO_CH) * rows + row) * TURBO_CH + g % TURBO_CH) * TURBO_RS;
+}
 __host__ __device__ inline int turbo_kw(int K) { return (K + 31) / 32; }
 
 }  // namespace lte

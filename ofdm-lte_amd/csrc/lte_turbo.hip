@@ -8,7 +8,6 @@
 
 namespace lte {
 
-constexpr int RS = TURBO_RS;   // decoder row stride (elements): 64 lanes
 
 // ---------------------------------------------------------------------------
 // RX rate-dematch + transpose into the decoder layout, rows of R (double: the
@@ -59,7 +58,7 @@ __global__ __launch_bounds__(256) void k_dematch(const R* __restrict__ llr, int 
     const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
-    dm_store(&blk[r][((size_t)g * rows[r] + row) * RS + f], tile[f][c], add != 0);
+    dm_store(&blk[r][turbo_elem(rows[r], g, row) + f], tile[f][c], add != 0);
   }
 }
 
@@ -124,7 +123,7 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
     const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
-    dm_store(&blk[r][((size_t)g * rows[r] + row) * RS + f], tile[f][c], add != 0);
+    dm_store(&blk[r][turbo_elem(rows[r], g, row) + f], tile[f][c], add != 0);
   }
 }
 

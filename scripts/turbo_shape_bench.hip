@@ -30,11 +30,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
-__device__ __forceinline__ uint64_t ld(__amdgpu_buffer_rsrc_t r, int vo, int row) {
-  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, vo, row * 512, 0));
+// row stride in bytes: 512 (a wave's rows contiguous) or CH x 512 (rows of CH
+// consecutive waves side by side: [chunk][row][wave in chunk][lane])
+// cache-policy bits of the row loads / stores (LTE_SHAPE_AUX: 0 default, 1 glc,
+// 2 slc, 3 glc|slc); LTE_SHAPE_NOST: the extrinsic stores dropped (reads only)
+#ifndef LTE_SHAPE_AUX
+#define LTE_SHAPE_AUX 0
+#endif
+#ifndef LTE_SHAPE_AUXL
+#define LTE_SHAPE_AUXL LTE_SHAPE_AUX
+#endif
+#ifndef LTE_SHAPE_AUXS
+#define LTE_SHAPE_AUXS LTE_SHAPE_AUX
+#endif
+#ifndef LTE_SHAPE_NOST
+#define LTE_SHAPE_NOST 0
+#endif
+__device__ __forceinline__ uint64_t ld(__amdgpu_buffer_rsrc_t r, int vo, int row, int rs) {
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, vo, row * rs, LTE_SHAPE_AUXL));
 }
-__device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, int vo, int row, uint64_t v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, vo, row * 512, 0);
+__device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, int vo, int row, uint64_t v, int rs) {
+  if (LTE_SHAPE_NOST && v != 0x0123456789abcdefull) return;
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, vo, row * rs, LTE_SHAPE_AUXS);
 }
 
 struct Job {
@@ -53,7 +70,7 @@ __device__ __forceinline__ int modsub(int a, int b, int K) { a -= b; return a < 
 
 template <bool CKPT, bool dec2, bool first, bool SEQ = false>
 __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int vo, int K, int f1, int f2,
-                     uint64_t& acc) {
+                     uint64_t& acc, int rs) {
   const int nsub = K / 8, tf2 = (2 * f2) % K;
   const int lp0 = dec2 ? 3 * K + 6 : 2 * K + 3;
   int pi = 0, d = (f1 + f2) % K;
@@ -61,15 +78,15 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
   for (int w = 0; w < nsub; ++w) {
     if (CKPT && w % 3 == 0) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) st(rc, vo, (w / 3) * 8 + s, acc + s);
+      for (int s = 0; s < 8; ++s) st(rc, vo, (w / 3) * 8 + s, acc + s, rs);
     }
     uint64_t xs[8], xp[8], xe[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {   // the window's loads first (as the decoder's ldwin), then the fold
       const int k = w * 8 + j, p = (dec2 && !SEQ) ? pi : k;
-      xs[j] = ld(rb, vo, 2 * p);
-      xp[j] = ld(rb, vo, lp0 + k);
-      xe[j] = first ? 0 : ld(rb, vo, 2 * p + 1);
+      xs[j] = ld(rb, vo, 2 * p, rs);
+      xp[j] = ld(rb, vo, lp0 + k, rs);
+      xe[j] = first ? 0 : ld(rb, vo, 2 * p + 1, rs);
       if (dec2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
     }
     uint64_t x = 0;
@@ -79,7 +96,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
   }
   // tails: 3 termination steps (2 rows each)
 #pragma unroll
-  for (int j = 0; j < 3; ++j) acc ^= ld(rb, vo, 2 * K + j) ^ ld(rb, vo, lp0 + K + j);
+  for (int j = 0; j < 3; ++j) acc ^= ld(rb, vo, 2 * K + j, rs) ^ ld(rb, vo, lp0 + K + j, rs);
   const int nsw = (nsub + 2) / 3;
 #pragma unroll 1
   for (int q = nsw - 1; q >= 0; --q) {
@@ -94,9 +111,9 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
     for (int i = 0; i < 24; ++i) {
       if (i < n) {
         const int k = k0 + i, p = (dec2 && !SEQ) ? pp : k;
-        v[i] = ld(rb, vo, 2 * p);
-        vp[i] = ld(rb, vo, lp0 + k);
-        ve[i] = first ? 0 : ld(rb, vo, 2 * p + 1);
+        v[i] = ld(rb, vo, 2 * p, rs);
+        vp[i] = ld(rb, vo, lp0 + k, rs);
+        ve[i] = first ? 0 : ld(rb, vo, 2 * p + 1, rs);
         if (dec2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
       }
     }
@@ -104,7 +121,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
     for (int i = 0; i < 24; ++i) v[i] ^= vp[i] ^ ve[i];
     if (CKPT) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc ^= ld(rc, vo, q * 8 + s);
+      for (int s = 0; s < 8; ++s) acc ^= ld(rc, vo, q * 8 + s, rs);
     }
 #pragma unroll
     for (int i = 23; i >= 0; --i) {
@@ -112,7 +129,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
         const int k = k0 + i;
         int p = k;
         if (dec2) { dd = modsub(dd, tf2, K); pp = modsub(pp, dd, K); p = SEQ ? k : pp; }
-        st(rb, vo, 2 * p + 1, v[i] + acc);
+        st(rb, vo, 2 * p + 1, v[i] + acc, rs);
       }
     }
     if (dec2) { pi = pp; d = dd; }
@@ -120,7 +137,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
 }
 
 template <bool CKPT, bool SEQ = false>
-__global__ __launch_bounds__(256) void k_shape(Jobs J, int iters) {
+__global__ __launch_bounds__(256) void k_shape(Jobs J, int iters, int CH) {
   extern __shared__ uint64_t lds_pad[];
   const int wg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wg >= J.prefix[J.n]) return;
@@ -129,15 +146,17 @@ __global__ __launch_bounds__(256) void k_shape(Jobs J, int iters) {
   const Job jb = J.j[r];
   const int g = wg - J.prefix[r], K = jb.K, lane = threadIdx.x & 63, vo = lane * 8;
   const size_t rows = 4 * (size_t)K + 12, ckrows = (size_t)(K / 8 + 1) * 8;
-  const __amdgpu_buffer_rsrc_t rb = rsrc(jb.blk + (size_t)g * rows * 64, (uint32_t)(rows * 512));
-  const __amdgpu_buffer_rsrc_t rc = rsrc(jb.ck + (size_t)g * ckrows * 64, (uint32_t)(ckrows * 512));
+  const size_t ch = g / CH, gi = g % CH;   // CH = 1: the decoder's layout
+  const __amdgpu_buffer_rsrc_t rb = rsrc(jb.blk + (ch * rows * CH + gi) * 64, (uint32_t)(rows * 512 * CH));
+  const __amdgpu_buffer_rsrc_t rc = rsrc(jb.ck + (ch * ckrows * CH + gi) * 64, (uint32_t)(ckrows * 512 * CH));
   uint64_t acc = lane;
+  const int rs = 512 * CH;
   for (int it = 0; it < iters; ++it) {
-    if (it == 0) pass<CKPT, false, true, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc);
-    else pass<CKPT, false, false, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc);
-    pass<CKPT, true, false, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+    if (it == 0) pass<CKPT, false, true, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc, rs);
+    else pass<CKPT, false, false, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc, rs);
+    pass<CKPT, true, false, SEQ>(rb, rc, vo, K, jb.f1, jb.f2, acc, rs);
   }
-  pass<CKPT, false, false>(rb, rc, vo, K, jb.f1, jb.f2, acc);
+  pass<CKPT, false, false>(rb, rc, vo, K, jb.f1, jb.f2, acc, rs);
   if (acc == 0x123456789abcdefull) lds_pad[0] = acc;   // never true; keeps the LDS request
 }
 
@@ -181,12 +200,12 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  auto run = [&](bool ck, size_t lds, bool seq = false) {
+  auto run = [&](bool ck, size_t lds, bool seq = false, int CH = 1) {
     auto k = seq ? k_shape<true, true> : ck ? k_shape<true> : k_shape<false>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k, dim3((waves + 3) / 4), dim3(256), lds, 0, J, iters);   // warm
+    hipLaunchKernelGGL(k, dim3((waves + 3) / 4), dim3(256), lds, 0, J, iters, CH);   // warm
     (void)hipEventRecord(a, 0);
-    for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k, dim3((waves + 3) / 4), dim3(256), lds, 0, J, iters);
+    for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k, dim3((waves + 3) / 4), dim3(256), lds, 0, J, iters, CH);
     (void)hipEventRecord(b, 0);
     (void)hipEventSynchronize(b);
     float ms = 0.f;
@@ -206,6 +225,20 @@ int main(int argc, char** argv) {
          bytes_ck / (m2 * 1e-3) / 1e9, m3, bytes_ck / (m3 * 1e-3) / 1e9);
   printf("{\"ms_1wps_ckpt_seq\": %.3f, \"GBs_1wps_ckpt_seq\": %.1f, \"ms_free_ckpt_seq\": %.3f, \"GBs_free_ckpt_seq\": %.1f}\n",
          m4, bytes_ck / (m4 * 1e-3) / 1e9, m5, bytes_ck / (m5 * 1e-3) / 1e9);
+  // chunked layouts: rows of CH consecutive waves side by side (G = 1024 is a multiple of every CH)
+  const int chs[6] = {2, 4, 8, 16, 32, 64};
+  for (int c = 0; c < 6; ++c) {
+    const double m = run(true, 96 * 1024, false, chs[c]);
+    printf("{\"CH\": %d, \"ms_1wps_ckpt\": %.3f, \"GBs_1wps_ckpt\": %.1f}\n", chs[c], m, bytes_ck / (m * 1e-3) / 1e9);
+  }
+  {
+    const double m = run(true, 96 * 1024, false, 1);
+    printf("{\"CH\": 1, \"ms_1wps_ckpt\": %.3f, \"GBs_1wps_ckpt\": %.1f, \"repeat\": true}\n", m, bytes_ck / (m * 1e-3) / 1e9);
+  }
+  if (hipDeviceSynchronize() != hipSuccess) {
+    printf("kernel failed\n");
+    return 1;
+  }
   for (void* p : bufs) (void)hipFree(p);
   return 0;
 }

@@ -219,11 +219,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 // Cache-policy bits of the decoder's row loads / stores (buffer "aux"; gfx950:
-// 1 = sc0, 2 = nt, 16 = sc1).  Measured on the decoder's access shape
-// (scripts/turbo_shape_bench.hip): nt helps only together with
-// the wave-chunked layout (TURBO_CH).
+// 1 = sc0, 2 = nt, 16 = sc1).  nt helps only together with the wave-chunked
+// layout (TURBO_CH; scripts/turbo_shape_bench.hip).  Same-box A/B
+// of k_turbo64 at 65 536 frames: sc0|nt 320-324 ms, nt 322-324, none 339-346
+// (chunk 64), nt / sc1|nt / sc0 without chunking no better than none.
 #ifndef LTE_TURBO_CPOL
-#define LTE_TURBO_CPOL 2
+#define LTE_TURBO_CPOL 3
 #endif
 
 // RSB: bytes between consecutive rows (TURBO_CH groups of 64 lanes for the

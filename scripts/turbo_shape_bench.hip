@@ -17,6 +17,10 @@
 // with and without the checkpoint rows, and with two waves per SIMD; _seq:
 // decoder 2 addressed in natural order (what a QPP-free layout would reach).
 // Build: hipcc -O3 --offload-arch=gfx950 -o scripts/turbo_shape_bench scripts/turbo_shape_bench.hip
+// (-DLTE_SHAPE_AUX=3: the decoder's sc0|nt policy, LTE_TURBO_CPOL).  The
+// CH lines place the rows of CH consecutive waves side by side, as the decoder
+// does since round 3 (TURBO_CH = 32, lte_internal.h); "decoder_layout" is that
+// shape at one / two / three waves per SIMD.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -230,6 +234,13 @@ int main(int argc, char** argv) {
   for (int c = 0; c < 6; ++c) {
     const double m = run(true, 96 * 1024, false, chs[c]);
     printf("{\"CH\": %d, \"ms_1wps_ckpt\": %.3f, \"GBs_1wps_ckpt\": %.1f}\n", chs[c], m, bytes_ck / (m * 1e-3) / 1e9);
+  }
+  {   // the decoder's layout (TURBO_CH = 32 groups per chunk; build with -DLTE_SHAPE_AUX=3 for its policy)
+    const double a1 = run(true, 96 * 1024, false, 32), a2 = run(true, 64 * 1024, false, 32), a3 = run(true, 0, false, 32);
+    const double best = a1 < a2 ? (a1 < a3 ? a1 : a3) : (a2 < a3 ? a2 : a3);
+    printf("{\"decoder_layout\": {\"CH\": 32, \"aux\": %d, \"ms_1wps\": %.3f, \"ms_2wps\": %.3f, \"ms_free\": %.3f, "
+           "\"GBs_1wps\": %.1f, \"GBs_best\": %.1f}}\n", LTE_SHAPE_AUXL, a1, a2, a3, bytes_ck / (a1 * 1e-3) / 1e9,
+           bytes_ck / (best * 1e-3) / 1e9);
   }
   {
     const double m = run(true, 96 * 1024, false, 1);

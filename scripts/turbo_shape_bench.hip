@@ -50,6 +50,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 #ifndef LTE_SHAPE_NOST
 #define LTE_SHAPE_NOST 0
 #endif
+// LTE_SHAPE_SEPLE: LS rows [0, K), LE rows [K, 2K) (not interleaved);
+// LTE_SHAPE_XCD: a chunk's groups taken from blocks on one XCD (blocks are
+// dispatched round-robin over the 8 XCDs), within windows of 64 blocks
+#ifndef LTE_SHAPE_SEPLE
+#define LTE_SHAPE_SEPLE 0
+#endif
+#ifndef LTE_SHAPE_XCD
+#define LTE_SHAPE_XCD 0
+#endif
+// LTE_SHAPE_CKCH1: checkpoint rows of each group contiguous (not chunked);
+// LTE_SHAPE_SYNC: the block's 4 waves meet at a barrier every 24 steps
+#ifndef LTE_SHAPE_CKCH1
+#define LTE_SHAPE_CKCH1 0
+#endif
+#ifndef LTE_SHAPE_SYNC
+#define LTE_SHAPE_SYNC 0
+#endif
+#define RSC(rs) (LTE_SHAPE_CKCH1 ? 512 : (rs))
+#define ROW_LS(p) (LTE_SHAPE_SEPLE ? (p) : 2 * (p))
+#define ROW_LE(p) (LTE_SHAPE_SEPLE ? K + (p) : 2 * (p) + 1)
 __device__ __forceinline__ uint64_t ld(__amdgpu_buffer_rsrc_t r, int vo, int row, int rs) {
   return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, vo, row * rs, LTE_SHAPE_AUXL));
 }
@@ -80,17 +100,18 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
   int pi = 0, d = (f1 + f2) % K;
 #pragma unroll 1
   for (int w = 0; w < nsub; ++w) {
+    if (LTE_SHAPE_SYNC && w % 3 == 0) __syncthreads();
     if (CKPT && w % 3 == 0) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) st(rc, vo, (w / 3) * 8 + s, acc + s, rs);
+      for (int s = 0; s < 8; ++s) st(rc, vo, (w / 3) * 8 + s, acc + s, RSC(rs));
     }
     uint64_t xs[8], xp[8], xe[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {   // the window's loads first (as the decoder's ldwin), then the fold
       const int k = w * 8 + j, p = (dec2 && !SEQ) ? pi : k;
-      xs[j] = ld(rb, vo, 2 * p, rs);
+      xs[j] = ld(rb, vo, ROW_LS(p), rs);
       xp[j] = ld(rb, vo, lp0 + k, rs);
-      xe[j] = first ? 0 : ld(rb, vo, 2 * p + 1, rs);
+      xe[j] = first ? 0 : ld(rb, vo, ROW_LE(p), rs);
       if (dec2) { pi = modadd(pi, d, K); d = modadd(d, tf2, K); }
     }
     uint64_t x = 0;
@@ -104,6 +125,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
   const int nsw = (nsub + 2) / 3;
 #pragma unroll 1
   for (int q = nsw - 1; q >= 0; --q) {
+    if (LTE_SHAPE_SYNC) __syncthreads();
     const int ns = min(3, nsub - q * 3), n = ns * 8, k0 = q * 24;
     if (dec2) {
 #pragma unroll 1
@@ -115,9 +137,9 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
     for (int i = 0; i < 24; ++i) {
       if (i < n) {
         const int k = k0 + i, p = (dec2 && !SEQ) ? pp : k;
-        v[i] = ld(rb, vo, 2 * p, rs);
+        v[i] = ld(rb, vo, ROW_LS(p), rs);
         vp[i] = ld(rb, vo, lp0 + k, rs);
-        ve[i] = first ? 0 : ld(rb, vo, 2 * p + 1, rs);
+        ve[i] = first ? 0 : ld(rb, vo, ROW_LE(p), rs);
         if (dec2) { pp = modadd(pp, dd, K); dd = modadd(dd, tf2, K); }
       }
     }
@@ -125,7 +147,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
     for (int i = 0; i < 24; ++i) v[i] ^= vp[i] ^ ve[i];
     if (CKPT) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc ^= ld(rc, vo, q * 8 + s, rs);
+      for (int s = 0; s < 8; ++s) acc ^= ld(rc, vo, q * 8 + s, RSC(rs));
     }
 #pragma unroll
     for (int i = 23; i >= 0; --i) {
@@ -133,7 +155,7 @@ __device__ void pass(__amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rc, int v
         const int k = k0 + i;
         int p = k;
         if (dec2) { dd = modsub(dd, tf2, K); pp = modsub(pp, dd, K); p = SEQ ? k : pp; }
-        st(rb, vo, 2 * p + 1, v[i] + acc, rs);
+        st(rb, vo, ROW_LE(p), v[i] + acc, rs);
       }
     }
     if (dec2) { pi = pp; d = dd; }
@@ -150,9 +172,15 @@ __global__ __launch_bounds__(256) void k_shape(Jobs J, int iters, int CH) {
   const Job jb = J.j[r];
   const int g = wg - J.prefix[r], K = jb.K, lane = threadIdx.x & 63, vo = lane * 8;
   const size_t rows = 4 * (size_t)K + 12, ckrows = (size_t)(K / 8 + 1) * 8;
-  const size_t ch = g / CH, gi = g % CH;   // CH = 1: the decoder's layout
+  size_t gg = g;
+  if (LTE_SHAPE_XCD && CH == 32 && (J.prefix[r] % 256) == 0) {   // g = 4 (8 q + x) + w -> chunk (q / 8) * 8 + x
+    const int b = g >> 2, w = g & 3, x = b & 7, q = b >> 3;
+    if ((b | 63) < J.prefix[r + 1] / 4 - J.prefix[r] / 4) gg = (size_t)((q >> 3) * 8 + x) * 32 + (q & 7) * 4 + w;
+  }
+  const size_t ch = gg / CH, gi = gg % CH;   // CH = 1: each group's block contiguous
   const __amdgpu_buffer_rsrc_t rb = rsrc(jb.blk + (ch * rows * CH + gi) * 64, (uint32_t)(rows * 512 * CH));
-  const __amdgpu_buffer_rsrc_t rc = rsrc(jb.ck + (ch * ckrows * CH + gi) * 64, (uint32_t)(ckrows * 512 * CH));
+  const __amdgpu_buffer_rsrc_t rc = LTE_SHAPE_CKCH1 ? rsrc(jb.ck + gg * ckrows * 64, (uint32_t)(ckrows * 512))
+                                                    : rsrc(jb.ck + (ch * ckrows * CH + gi) * 64, (uint32_t)(ckrows * 512 * CH));
   uint64_t acc = lane;
   const int rs = 512 * CH;
   for (int it = 0; it < iters; ++it) {

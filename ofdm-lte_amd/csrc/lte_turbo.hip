@@ -22,9 +22,15 @@ namespace lte {
 // A block loads a [64 frames][DM_CH t] tile (coalesced rows), then every wave
 // writes whole decoder rows (64 frames of one LLR).
 constexpr int DM_CH = 64;
+// LTE_DM_NT (A/B): 1 = non-temporal decoder-row stores, 3 = also non-temporal
+// loads of the equalised symbols / noise variances (k_dematch_zn)
+#ifndef LTE_DM_NT
+#define LTE_DM_NT 0
+#endif
 template <class R>
 __device__ __forceinline__ void dm_store(R* dst, R v, bool add) {
   if (add) *dst = *dst + (R)0.5 * v;
+  else if (LTE_DM_NT & 1) __builtin_nontemporal_store((R)0.5 * ((R)0 + v), dst);
   else *dst = (R)0.5 * ((R)0 + v);
 }
 
@@ -105,8 +111,13 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
     const bool ok = b < B && r < nr;
     const size_t i = (size_t)b * n_re + re0 + r;
     const int l = (re0 + r) / nd, j = re0 + r - l * nd;
-    zv[k] = ok ? z[i] : mkc((R)0, (R)0);
-    nvv[k] = ok ? nv[(size_t)b * n_nv + (l / 14) * nd + j] : (R)1;
+    if (LTE_DM_NT & 2) {
+      zv[k] = ok ? mkc(__builtin_nontemporal_load(&z[i].x), __builtin_nontemporal_load(&z[i].y)) : mkc((R)0, (R)0);
+      nvv[k] = ok ? __builtin_nontemporal_load(&nv[(size_t)b * n_nv + (l / 14) * nd + j]) : (R)1;
+    } else {
+      zv[k] = ok ? z[i] : mkc((R)0, (R)0);
+      nvv[k] = ok ? nv[(size_t)b * n_nv + (l / 14) * nd + j] : (R)1;
+    }
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {

@@ -54,3 +54,29 @@ def test_bench_size_batch_invariance(C, prec):
     ref = small.run(snr[sel], snr_index=np.arange(64, dtype=np.int32), n_snr=64, seed=0x5EED,
                     frame_ids=ids[sel])['counts']
     assert np.array_equal(per_frame[sel], ref)
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+def test_decoder_partial_chunk_batch_invariance(C, prec):
+    """The decoder's block arrays are chunked over 32 frame groups (TURBO_CH,
+    lte_internal.h turbo_elem): a batch of 34 groups (one full chunk + a partial
+    one, 2 129 frames: the last group partial too) must give every frame the
+    per-frame counts it gets in 64-frame plans (one partial chunk each), around
+    the waterfall (14-22 dB) where the counts vary frame to frame."""
+    import lte_phy
+    from lte_phy import engine
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=20.0, modulation='64-QAM'), channel_type='rayleigh_mp',
+                                itu_profile='Pedestrian_A', precision=prec)
+    n = 33 * 64 + 17
+    ids = np.arange(n, dtype=np.uint64) + np.uint64(12345)
+    snr = (14.0 + 2.0 * (ids % np.uint64(5))).astype(np.float64)
+    big = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=n)
+    per_frame = big.run(snr, snr_index=np.arange(n, dtype=np.int32), n_snr=n, seed=0x5EED, frame_ids=ids)['counts']
+    del big
+    engine.clear_cache()
+    small = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=64)
+    ref = np.concatenate([small.run(snr[i:i + 64], snr_index=np.arange(min(64, n - i), dtype=np.int32),
+                                    n_snr=min(64, n - i), seed=0x5EED, frame_ids=ids[i:i + 64])['counts']
+                          for i in range(0, n, 64)])
+    assert per_frame[:, 0].sum() > 0 and np.any(per_frame[:, 2] == 0)   # errors and decoded blocks both present
+    assert np.array_equal(per_frame, ref)

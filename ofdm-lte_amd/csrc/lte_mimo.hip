@@ -354,6 +354,14 @@ struct SymSpan {
 
 constexpr int MC_MAXRX = 8;   // receive antennas per launch
 constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the transmit streams
+// (kernel template G: MC_RXG, or 2 when the plan has at most 2 receive antennas --
+// half the accumulator registers; LTE_CHM_G2 = 0 turns that off for A/B)
+#ifndef LTE_CHM_G2
+#define LTE_CHM_G2 1
+#endif
+#ifndef LTE_CHM_G2_WAVES   // f64 G = 2 channel kernel: minimum waves per SIMD asked of the register allocator
+#define LTE_CHM_G2_WAVES 5
+#endif
 
 // acc[q][j] += sum_p h_{rx q, tx, p}(n_j) x_tx[n_j - delay_p] for the nq <=
 // MC_RXG receive antennas of a group and one transmit stream: each delayed TX
@@ -362,8 +370,8 @@ constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the 
 // mimo_ncf per path, cs_q per receive antenna); EX: f64 exact Jakes from the
 // phases ph (ph_q per receive antenna) -- a separate instance, so that its
 // sincos calls do not set the register budget of the coefficient path.
-template <class R, int J, bool EX>
-__device__ __forceinline__ void links_accumulate(cx<R> (&acc)[MC_RXG][J], int nq, const SymSpan<J>& sp,
+template <class R, int J, bool EX, int G>
+__device__ __forceinline__ void links_accumulate(cx<R> (&acc)[G][J], int nq, const SymSpan<J>& sp,
                                                  const cx<R>* __restrict__ cs, size_t cs_q, int n_cs, int np,
                                                  const int32_t* __restrict__ delays, const cx<R>* __restrict__ xf,
                                                  const R* __restrict__ ph, size_t ph_q, const R* __restrict__ gains,
@@ -379,7 +387,7 @@ __device__ __forceinline__ void links_accumulate(cx<R> (&acc)[MC_RXG][J], int nq
       xs[j] = (sp.ok[j] && src >= 0) ? xf[src] : mkc((R)0, (R)0);
     }
 #pragma unroll
-    for (int q = 0; q < MC_RXG; ++q) {
+    for (int q = 0; q < G; ++q) {
       if (q >= nq) break;
       if constexpr (EX) {
           double phv[16];
@@ -460,7 +468,7 @@ __device__ __forceinline__ void link_noise_span(cx<R> (&acc)[J], const SymSpan<J
 
 // pass 1 (transmit_mimo Rayleigh): per-link power partials of the faded signal,
 // one block per (frame, OFDM symbol, TX stream), the receive antennas in groups
-template <class R, int J, bool EX>
+template <class R, int J, bool EX, int G>
 __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                     const int32_t* __restrict__ delays, const cx<R>* __restrict__ coef,
                                                     const R* __restrict__ phases, const R* __restrict__ gains,
@@ -476,30 +484,30 @@ __global__ __launch_bounds__(MWG) void k_link_power(int L, int num_rx, int num_t
   const float dc = 0.5f * (float)(sym_len - 1);
   const V* xf = x + ((size_t)b * num_tx + tx) * L;
   const size_t cs_q = (size_t)num_tx * np * n_cs * NCF, ph_q = (size_t)num_tx * np * 16;
-  for (int rg = 0; rg < num_rx; rg += MC_RXG) {
-    const int nq = min(MC_RXG, num_rx - rg);
+  for (int rg = 0; rg < num_rx; rg += G) {
+    const int nq = min(G, num_rx - rg);
     const size_t lk0 = ((size_t)b * num_rx + rg) * num_tx + tx;
     const V* cs = coef + lk0 * np * n_cs * NCF + (size_t)sidx * NCF;
     const R* ph = EX ? phases + lk0 * np * 16 : nullptr;
-    R pw[MC_RXG];
+    R pw[G];
 #pragma unroll
-    for (int q = 0; q < MC_RXG; ++q) pw[q] = (R)0;
+    for (int q = 0; q < G; ++q) pw[q] = (R)0;
     for (int base = nbeg; base < nend; base += J * MWG) {
       const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
-      V acc[MC_RXG][J];
+      V acc[G][J];
 #pragma unroll
-      for (int q = 0; q < MC_RXG; ++q)
+      for (int q = 0; q < G; ++q)
 #pragma unroll
         for (int j = 0; j < J; ++j) acc[q][j] = mkc((R)0, (R)0);
-      links_accumulate<R, J, EX>(acc, nq, sp, cs, cs_q, n_cs, np, delays, xf, ph, ph_q, gains, m, fs);
+      links_accumulate<R, J, EX, G>(acc, nq, sp, cs, cs_q, n_cs, np, delays, xf, ph, ph_q, gains, m, fs);
 #pragma unroll
-      for (int q = 0; q < MC_RXG; ++q)
+      for (int q = 0; q < G; ++q)
 #pragma unroll
         for (int j = 0; j < J; ++j)
           if (sp.ok[j]) pw[q] += acc[q][j].x * acc[q][j].x + acc[q][j].y * acc[q][j].y;
     }
 #pragma unroll
-    for (int q = 0; q < MC_RXG; ++q) {
+    for (int q = 0; q < G; ++q) {
       if (q >= nq) break;
       const R t = block_sum(pw[q], red);
       if (threadIdx.x == 0) part[(lk0 + (size_t)q * num_tx) * nblk + blk] = t;
@@ -523,8 +531,8 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
 // loads; the sample offset d from the symbol centre is per lane.  All RX of
 // the frame per block: each delayed TX sample is loaded once for a group of
 // MC_RXG receive antennas (links_accumulate), one power reduction per RX.
-template <class R, int J, bool EX>
-__global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
+template <class R, int J, bool EX, int G>
+__global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8) ? LTE_CHM_G2_WAVES : 1) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
                                                       const cx<R>* __restrict__ coef, const R* __restrict__ phases,
                                                       const R* __restrict__ gains, double fs, MimoGrid m,
@@ -543,16 +551,16 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
   const float dc = 0.5f * (float)(sym_len - 1);
   const size_t nl = (size_t)num_rx * num_tx;
   const size_t cs_q = (size_t)num_tx * np * n_cs * NCF, ph_q = (size_t)num_tx * np * 16;
-  for (int rg = 0; rg < num_rx; rg += MC_RXG) {
-    const int nq = min(MC_RXG, num_rx - rg);
-    R pw[MC_RXG];
+  for (int rg = 0; rg < num_rx; rg += G) {
+    const int nq = min(G, num_rx - rg);
+    R pw[G];
 #pragma unroll
-    for (int q = 0; q < MC_RXG; ++q) pw[q] = (R)0;
+    for (int q = 0; q < G; ++q) pw[q] = (R)0;
     for (int base = nbeg; base < nend; base += J * MWG) {
       const SymSpan<J> sp(base, nbeg, nend, dc, n_cs > 1);
-      V v[MC_RXG][J];
+      V v[G][J];
 #pragma unroll
-      for (int q = 0; q < MC_RXG; ++q)
+      for (int q = 0; q < G; ++q)
 #pragma unroll
         for (int j = 0; j < J; ++j) v[q][j] = mkc((R)0, (R)0);
       for (int tx = 0; tx < num_tx; ++tx) {
@@ -562,17 +570,17 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
         const R* ph = EX ? phases + lk0 * np * 16 : nullptr;
         // f64: each link's y from zero, then signals_rx += y_link (the
         // reference's order); f32 accumulates into the RX sums directly
-        V vl[MC_RXG][J];
-        V (&acc)[MC_RXG][J] = F64 ? vl : v;
+        V vl[G][J];
+        V (&acc)[G][J] = F64 ? vl : v;
         if constexpr (F64) {
 #pragma unroll
-          for (int q = 0; q < MC_RXG; ++q)
+          for (int q = 0; q < G; ++q)
 #pragma unroll
             for (int j = 0; j < J; ++j) vl[q][j] = mkc((R)0, (R)0);
         }
-        links_accumulate<R, J, EX>(acc, nq, sp, cs, cs_q, n_cs, np, delays, xf, ph, ph_q, gains, m, fs);
+        links_accumulate<R, J, EX, G>(acc, nq, sp, cs, cs_q, n_cs, np, delays, xf, ph, ph_q, gains, m, fs);
 #pragma unroll
-        for (int q = 0; q < MC_RXG; ++q) {
+        for (int q = 0; q < G; ++q) {
           if (q >= nq) break;
           const int link = (rg + q) * num_tx + tx;
           if (link_sigma) {
@@ -593,7 +601,7 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
         }
       }
 #pragma unroll
-      for (int q = 0; q < MC_RXG; ++q) {
+      for (int q = 0; q < G; ++q) {
         if (q >= nq) break;
         const int r = rg + q;
 #pragma unroll
@@ -605,7 +613,7 @@ __global__ __launch_bounds__(MWG) void k_channel_mimo(int L, int num_rx, int num
       }
     }
 #pragma unroll
-    for (int q = 0; q < MC_RXG; ++q) {
+    for (int q = 0; q < G; ++q) {
       if (q >= nq) break;
       const R t = block_sum(pw[q], red);
       if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rg + q) * nblk + blk] = t;
@@ -638,15 +646,20 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   const int J = jn <= 1 ? 1 : jn <= 2 || jmax == 2 ? 2 : 3;
 #define LTE_CHM_EX(J_, EX_)                                                                                         \
   do {                                                                                                             \
+    if (LTE_CHM_G2 && m.num_rx <= 2) LTE_CHM_EXG(J_, EX_, 2);                                                     \
+    else LTE_CHM_EXG(J_, EX_, MC_RXG);                                                                             \
+  } while (0)
+#define LTE_CHM_EXG(J_, EX_, G_)                                                                                    \
+  do {                                                                                                             \
     if (link_noise) {                                                                                              \
-      hipLaunchKernelGGL((k_link_power<R, J_, EX_>), dim3(nch * B, m.num_tx), dim3(MWG), 0, s, g.L,               \
+      hipLaunchKernelGGL((k_link_power<R, J_, EX_, G_>), dim3(nch * B, m.num_tx), dim3(MWG), 0, s, g.L,           \
                          m.num_rx, m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x,          \
                          link_part, nch);                                                                          \
       const int nl = B * m.num_rx * m.num_tx;                                                                      \
       hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L,        \
                          link_sigma);                                                                              \
     }                                                                                                              \
-    hipLaunchKernelGGL((k_channel_mimo<R, J_, EX_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx,      \
+    hipLaunchKernelGGL((k_channel_mimo<R, J_, EX_, G_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, \
                        n_paths,                                                                                    \
                        m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x, y, link_noise ? link_sigma : nullptr,   \
                        fid, seed, inj_lz, inj_lz_stride, pow_part, nch);                                           \
@@ -663,6 +676,7 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   }
 #undef LTE_CHM
 #undef LTE_CHM_EX
+#undef LTE_CHM_EXG
   return (int)hipGetLastError();
 }
 

@@ -532,7 +532,7 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
 // the frame per block: each delayed TX sample is loaded once for a group of
 // MC_RXG receive antennas (links_accumulate), one power reduction per RX.
 template <class R, int J, bool EX, int G>
-__global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8) ? LTE_CHM_G2_WAVES : 1) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
+__global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8 && !EX) ? LTE_CHM_G2_WAVES : 1) void k_channel_mimo(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                       const int32_t* __restrict__ delays,
                                                       const cx<R>* __restrict__ coef, const R* __restrict__ phases,
                                                       const R* __restrict__ gains, double fs, MimoGrid m,

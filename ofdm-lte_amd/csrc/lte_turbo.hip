@@ -89,7 +89,10 @@ int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_
 // rows exactly as k_dematch.  f64 covers 8 REs per block (49 KB tile at 16).
 // The noise variance is per (frame, 14-symbol group, data subcarrier): RE re =
 // l * nd + j of a frame reads nv[b * n_nv + (l / 14) * nd + j].
-template <class R> constexpr int dz_re() { return sizeof(R) == 8 ? 8 : 16; }
+#ifndef LTE_DZ_RE64   // REs per block for float64 (A/B: 16 = 256-B symbol spans per frame, 50 KB tile)
+#define LTE_DZ_RE64 8
+#endif
+template <class R> constexpr int dz_re() { return sizeof(R) == 8 ? LTE_DZ_RE64 : 16; }
 template <class R, int BPS>
 __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z, const R* __restrict__ nv, int n_re,
                                                     int nd, int n_nv, int B, const int32_t* __restrict__ rx_map,

@@ -2,18 +2,28 @@
 (config 2: 20 MHz, 64-QAM, Rayleigh ITU Pedestrian-A, turbo max-log-MAP x8,
 TB 27 760 bits = 5 code blocks = 14 OFDM symbols), BER sweep SNR 0:2:30 dB,
 in float64 (the reference's arithmetic; `--precision f32` is the fast mode).
+`--config 3|4|5` runs BASELINE.json's other GPU configs through the same
+harness (config 5 is the one BASELINE names for the 8-GPU sharded grid).
 
 One step = one batch of `--frames` subframes per GPU pushed TX -> channel ->
-RX + turbo; all inputs (Philox bits / fading / noise) are generated on the
+RX (+ turbo); all inputs (Philox bits / fading / noise) are generated on the
 device.  N>1: one process per GPU (torch.distributed, RCCL); frames are
 partitioned by global frame id (weak scaling, no data-path collective); the
 only collectives are the SUM of the BER counters and the MAX of the step time.
+
+BER match: the `cpu_baseline` leg runs the float64 oracle on the bench's own
+frames -- frame ids from both ends of rank 0's first timed step, with the
+oracle's restatement of the device's Philox draws (oracle/philox.py) -- and
+after the timed region rank 0 runs the same frame ids through the same plan:
+`ber_match` reports how many frames agree bit for bit and the largest BER gap
+over the sample's SNR points.
 
 `python bench.py --gpus N` with no launcher environment starts N ranks itself
 (torch.distributed.run on 127.0.0.1, before anything touches the GPU) and
 exits with their status; under a launcher WORLD_SIZE must equal --gpus.
 
-usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--precision f64|f32] [--velocity KMH]
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--frames F]
+                       [--precision f64|f32] [--velocity KMH] [--channel awgn|rayleigh_mp]
 """
 import argparse
 import json
@@ -33,14 +43,14 @@ for p in (ROOT, os.path.join(ROOT, 'ofdm-lte_amd')):
 
 METRIC = "LTE subframes/sec (20 MHz, 64-QAM, Rayleigh+turbo) at 1/2/4/8 GPU; BER match"
 SNRS = np.arange(0, 31, 2, dtype=np.float64)
+SEED = 0x5EED
 TB = 27760
 HBM_PEAK_GBS = 8000.0
+CPU_PER_GPU = 16     # host cores per GPU on the box (its CPU share)
 # compulsory stage-boundary bytes of one config-2 coded subframe
 # (TX map+IFFT, channel, FFT, estimation/equalisation/LLR, dematch+decode, CRC),
 # quoted for 4-B reals; the f64 chain moves 8-B reals at the same boundaries
 B_SF_F32 = 2_116_904
-# turbo work per subframe = sum(K+3) x 17 passes x ~100 ops
-TURBO_OPS_SF = 27_919 * 17 * 100
 # Non-packed vector ALU peaks of one MI355X (add / max, 1 op per lane per
 # instruction; 256 CUs x 4 SIMD-32 x 2.4 GHz):
 #  * f32: a wave64 instruction every 2 cycles per SIMD with several waves
@@ -50,25 +60,45 @@ TURBO_OPS_SF = 27_919 * 17 * 100
 #    -> 39.3 T op/s; scripts/valu_peak_bench.hip measures both on the box
 VALU_PEAK_OPS = {'f32': 256 * 4 * 32 * 2.4e9, 'f64': 256 * 4 * 16 * 2.4e9}
 
+# BASELINE.json's GPU configs: the workload, the default batch per GPU (sized to
+# the 288 GB of HBM and to fill the decoder's 1 024 resident waves several
+# times over), and the per-frame payload
+WORKLOADS = {
+    2: {'short': '20 MHz, 64-QAM, Rayleigh+turbo', 'frames': 65536, 'coded': True, 'n_bits': TB,
+        'desc': 'config 2: SISO 20 MHz (N=2048) 64-QAM, Rayleigh ITU Pedestrian-A, turbo max-log-MAP 8 it., '
+                'TB 27760 (5 CBs, 14 OFDM symbols), SNR 0:2:30 dB'},
+    3: {'short': 'config 3: SIMO 1x4 MRC, 10 MHz, 16-QAM, Rayleigh VehA', 'frames': 65536, 'coded': False,
+        'n_bits': 14 * 499 * 4,
+        'desc': 'config 3: SIMO 1x4 MRC, 10 MHz (N=1024) 16-QAM, Rayleigh ITU Vehicular-A per RX antenna, '
+                '14 OFDM symbols (27944 bits) uncoded, SNR 0:2:30 dB'},
+    4: {'short': 'config 4: SFBC 2x2 + turbo, 20 MHz, 64-QAM, Rayleigh', 'frames': 49152, 'coded': True,
+        'n_bits': TB,
+        'desc': 'config 4: Tx diversity 2x2 Alamouti SFBC + turbo max-log-MAP 8 it., 20 MHz 64-QAM, Rayleigh ITU '
+                'Pedestrian-A per link (transmit_mimo), TB 27760, SNR 0:2:30 dB'},
+    5: {'short': 'config 5: spatial 4x4 MMSE, 20 MHz, 64-QAM', 'frames': 32768, 'coded': False,
+        'n_bits': 14 * 999 * 6,
+        'desc': 'config 5: spatial multiplexing 4x4, rank 4, TM4 PMI 0 (W = I4), MMSE, 20 MHz 64-QAM, '
+                '14 OFDM symbols (83916 bits) uncoded, SNR 0:2:30 dB'},
+}
+
 
 def _cpu_worker(job):
-    """One host core: the oracle's config-2 coded chain on its own frames for
-    `seconds`; returns (subframes, elapsed)."""
-    seconds, seed = job
-    from oracle import lte_oracle as O
+    """One host core: the float64 oracle on the bench's own frames (its
+    restatement of the device's Philox draws), frame after frame from `ids`,
+    for `seconds`; returns ([(id, bit_errors, crc_ok)], elapsed)."""
+    config, seconds, ids, channel = job
+    from oracle import lte_oracle as O, philox as P
     O.lib()
-    num = O.Numerology(bandwidth=20.0, modulation='64-QAM')
-    L = 14 * (num.N + num.cp)
-    rs = np.random.RandomState(seed)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        bits = rs.randint(0, 2, TB)
-        d = [{'phases': [2 * np.pi * rs.rand(16) for _ in range(4)], 'z_re': rs.randn(L), 'z_im': rs.randn(L)}]
-        O.simulate_siso_coded(num, bits, float(SNRS[n % len(SNRS)]), 'rayleigh_mp', draws=d)
-        n += 1
+    f = P.BENCH_FRAMES[config]
+    kw = {'channel': channel} if config == 5 and channel else {}
+    res, t0 = [], time.perf_counter()
+    for i in ids:
+        e, c = f(int(i), **kw)
+        res.append((int(i), e, c))
         el = time.perf_counter() - t0
         if el >= seconds:
-            return n, el
+            break
+    return res, time.perf_counter() - t0
 
 
 def _cpu_model():
@@ -82,26 +112,79 @@ def _cpu_model():
     return platform.processor() or 'unknown'
 
 
-def cpu_baseline(seconds=15.0, procs=None):
+def sample_ids(F, procs):
+    """Frame ids of rank 0's first timed step ([0, F)) taken alternately from
+    both ends, dealt round-robin to the workers."""
+    h = (F + 1) // 2
+    order = np.empty(2 * h, dtype=np.int64)
+    order[0::2] = np.arange(h)
+    order[1::2] = F - 1 - np.arange(h)
+    order = order[:F]
+    return [order[i::procs].tolist() for i in range(procs)]
+
+
+def cpu_baseline(config=2, F=65536, seconds=15.0, procs=None, channel=None):
     """Time the oracle (float64 CPU restatement: NumPy front end + C turbo
     decoder, bit-exact with the reference) on this host's cores on a bounded
-    sample of the same workload (config-2 coded subframes cycling over SNRs):
-    one single-threaded worker process per core (frames are independent), the
-    box's CPU share at most (16 per GPU).  Runs before the GPU is initialised
-    (the workers are spawned processes)."""
+    sample of the bench's own frames: one single-threaded worker process per
+    core (frames are independent), the box's CPU share at most (16 cores per
+    GPU).  Runs before the GPU is initialised (spawned processes).  The
+    per-frame results feed `ber_match`."""
     import multiprocessing as mp
-    procs = procs or max(1, min(16, os.cpu_count() or 1))
+    procs = procs or max(1, min(CPU_PER_GPU, os.cpu_count() or 1))
     for v in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
         os.environ[v] = '1'
+    jobs = [(config, seconds, ids, channel) for ids in sample_ids(F, procs)]
     with mp.get_context('spawn').Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(seconds, 1234 + i) for i in range(procs)])
-    n = sum(r[0] for r in res)
-    value = sum(r[0] / r[1] for r in res)
+        res = pool.map(_cpu_worker, jobs)
+    n = sum(len(r[0]) for r in res)
+    value = sum(len(r[0]) / r[1] for r in res)
+    frames = sorted(x for r in res for x in r[0])
     return {'value': value, 'unit': 'subframes/s', 'cores': procs, 'kind': 'port',
             'per_core': value / procs, 'cpu_model': _cpu_model(),
-            'sample': f'{n} config-2 coded subframes (TB {TB}, 8 it.) over SNR 0:2:30 dB, '
-                      f'{max(r[1] for r in res):.1f} s on {procs} host cores, one single-threaded '
-                      f'process each (oracle: NumPy + C, float64)'}
+            'sample': f'{n} of the bench\'s own config-{config} frames (ids from both ends of rank 0\'s first '
+                      f'timed step, the oracle\'s restatement of the device Philox draws) over SNR 0:2:30 dB, '
+                      f'{max(r[1] for r in res):.1f} s on {procs} host cores, one single-threaded process each '
+                      f'(oracle: NumPy + C, float64)',
+            'frames': frames}
+
+
+def ber_match(plan, cpu, coded):
+    """Rank 0, after the timed region: the oracle's sample frames through the
+    bench's own plan (same seed, SNR by frame id); per-frame equality and the
+    largest |BER_gpu - BER_oracle| over the SNR points of the sample."""
+    fr = cpu.get('frames') if cpu else None
+    if not fr:
+        return None
+    ids = np.array([f[0] for f in fr], dtype=np.uint64)
+    e_or = np.array([f[1] for f in fr], dtype=np.int64)
+    S = len(SNRS)
+    e_gpu = np.zeros(len(ids), dtype=np.int64)
+    c_gpu = np.zeros(len(ids), dtype=bool)
+    for i in range(0, len(ids), plan.max_frames):
+        chunk = ids[i:i + plan.max_frames]
+        si = (chunk % np.uint64(S)).astype(np.int32)
+        out = plan.run(SNRS[si], snr_index=si, n_snr=S, seed=SEED, frame_ids=chunk)
+        e_gpu[i:i + len(chunk)] = out['frame_errors']
+        if coded:
+            c_gpu[i:i + len(chunk)] = out['crc_ok'].astype(bool)
+    si = (ids % np.uint64(S)).astype(np.int64)
+    nb = WORKLOADS[cpu['config']]['n_bits']
+    dber = 0.0
+    per = {}
+    for s in np.unique(si):
+        m = si == s
+        d = abs(e_gpu[m].sum() - e_or[m].sum()) / (m.sum() * nb)
+        per[f'{SNRS[s]:g}'] = int(m.sum())
+        dber = max(dber, float(d))
+    out = {'frames': int(len(ids)), 'frames_identical': int(np.sum(e_gpu == e_or)),
+           'max_abs_dber': dber, 'frames_per_snr_db': per,
+           'what': 'the oracle (float64, cpu_baseline leg) and the GPU plan on the same bench frame ids: per-frame '
+                   'bit-error equality and max over SNR points of |BER_gpu - BER_oracle| on the sample'}
+    if coded:
+        c_or = np.array([bool(f[2]) for f in fr])
+        out['crc_identical'] = int(np.sum(c_gpu == c_or))
+    return out
 
 
 def load_profile(name):
@@ -125,16 +208,38 @@ def _free_port():
 
 def launch_ranks(args, argv):
     """--gpus N without a launcher: time the CPU baseline here (this process
-    never touches the GPU), then run N ranks under torch.distributed.run as a
-    child process and return its status.  Rank 0 reads the baseline from
-    LTE_BENCH_CPU_JSON, so the N > 1 line carries it too."""
+    never touches the GPU; 16 host cores per GPU of the node), then run N ranks
+    under torch.distributed.run as a child process and return its status.
+    Rank 0 reads the baseline from LTE_BENCH_CPU_JSON (a file path), so the
+    N > 1 line carries it too."""
     env = dict(os.environ)
     env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
-    if not args.no_cpu:
-        env['LTE_BENCH_CPU_JSON'] = json.dumps(cpu_baseline(args.cpu_seconds))
+    if cpu_seconds(args) > 0:
+        procs = max(1, min(CPU_PER_GPU * args.gpus, os.cpu_count() or 1))
+        cpu = cpu_baseline(args.config, args.frames, cpu_seconds(args), procs, args.channel)
+        cpu['config'] = args.config
+        path = os.path.join(os.environ.get('TMPDIR', '/tmp'), f'lte_bench_cpu_{os.getpid()}.json')
+        with open(path, 'w') as f:
+            json.dump(cpu, f)
+        env['LTE_BENCH_CPU_JSON'] = path
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
            '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + argv
-    return subprocess.call(cmd, env=env)
+    rc = subprocess.call(cmd, env=env)
+    if env.get('LTE_BENCH_CPU_JSON'):
+        try:
+            os.remove(env['LTE_BENCH_CPU_JSON'])
+        except OSError:
+            pass
+    return rc
+
+
+def cpu_seconds(args):
+    """--cpu-seconds, or 15 s (0 under --dry-run unless given)."""
+    if args.no_cpu:
+        return 0.0
+    if args.cpu_seconds is not None:
+        return float(args.cpu_seconds)
+    return 0.0 if args.dry_run else 15.0
 
 
 def decoder_row_bytes(K, esz, iters):
@@ -154,30 +259,25 @@ def decoder_row_bytes(K, esz, iters):
     return K * rows * esz + 3 * 2 * passes * esz + K / 8
 
 
-def roofline(prec, tim, steps, F, el, value, world, iters=8):
-    """Dominant kernel (the turbo decoder, ~87 % of a step) against the roofline
-    that bounds it.  The exact decoder streams its rows: `achieved` = the
-    compulsory row bytes of the exact recursion (decoder_row_bytes) per launch
-    / the kernel's mean launch time (HIP events on the plan's stream; the max
-    over ranks), against the 8 TB/s HBM peak; `traffic` = the PMC-measured HBM
-    bytes per launch (profiles/pmc_turbo_traffic_<prec>.json, gfx950-corrected),
-    with `shape_ceiling` = the measured streaming rate of the same access shape
-    without the arithmetic (profiles/r3_turbo_shape_microbench.json).  Beside
-    it: SURVEY §8(d)'s stage-boundary bytes (input LLRs + decoded bits) and its
-    VALU view (sum(K+3) x 17 passes x 100 add/max ops per subframe against the
-    non-packed vector peak), and the SQ-counted VALU issue occupancy.  `bound`
-    is the larger of the measured HBM and VALU occupancies."""
+def turbo_roofline(prec, tim, F, iters=8):
+    """Turbo decoder (the dominant kernel of configs 2 and 4) against SURVEY
+    §8(d)'s roofline for it, K7: VALU, sum(K+3) x 17 passes x ~100 add/max ops
+    per subframe against the non-packed f64 (f32) vector peak -> `frac`.
+    Beside it the measured limiter: the exact recursion's HBM row stream
+    (`hbm_row_stream`: compulsory row bytes per launch / the mean launch time,
+    PMC traffic, the access-shape ceiling and what the stores cost), and the
+    SQ-counted VALU issue occupancy."""
     from lte_phy.channel_coding import segmentation_sizes
     t_ms, t_n = tim.get('turbo', (0.0, 0))
     avg_s = t_ms / max(t_n, 1) * 1e-3
     Fp = ((F + 63) // 64) * 64            # frames padded to whole 64-frame decoder groups
     esz = 8 if prec == 'f64' else 4
     Ks = segmentation_sizes(TB + 24)
+    ops_sf = sum(K + 3 for K in Ks) * (2 * iters + 1) * 100
     row_bytes = sum(Fp * decoder_row_bytes(K, esz, iters) for K in Ks)
     stage_bytes = sum(Fp * ((3 * K + 12) * esz + K / 8) for K in Ks)
     peak = VALU_PEAK_OPS[prec]
-    ops = TURBO_OPS_SF * F
-    achieved_T = ops / avg_s / 1e12 if t_n else 0.0
+    achieved_T = ops_sf * F / avg_s / 1e12 if t_n else 0.0
     traffic = load_profile(f'pmc_turbo_traffic_{prec}.json')
     sq = load_profile(f'pmc_turbo_sq_{prec}.json')
     shape = load_profile('r3_turbo_shape_microbench.json')
@@ -186,38 +286,103 @@ def roofline(prec, tim, steps, F, el, value, world, iters=8):
     tr_gbs = tr / avg_s / 1e9 if tr and t_n else None
     busy = (sq['valu_wave_instr_per_frame'] * Fp * sq['issue_cycles_per_instr'] / (avg_s * 2.4e9 * 1024)
             if sq and t_n else None)
-    hbm_occ = (tr_gbs if tr_gbs else gbs) / HBM_PEAK_GBS
     ceil = shape.get(f'ceiling_GBs_{prec}') if shape else None
-    roof = {'bound': 'hbm' if busy is None or hbm_occ >= busy else 'valu',
-            'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo',
-            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(gbs / HBM_PEAK_GBS, 4),
-            # HBM bytes per launch from the committed PMC passes (per-frame bytes,
-            # gfx950-corrected, scaled to this launch's frames)
+    return {'bound': 'valu', 'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo',
+            'achieved': round(achieved_T, 3), 'peak': round(peak / 1e12, 2), 'unit': 'Top/s',
+            'frac': round(achieved_T * 1e12 / peak, 4) if t_n else 0.0,
             'traffic': round(tr) if tr else None,
-            'alg_bytes_per_launch': int(row_bytes),
-            'alg_bytes': 'exact-recursion row stream: per code-block step 7 rows (Ls, Lp, La forward and '
-                         'backward + extrinsic store) x esz B x 17 passes (first pass 5, final 6 + K/8 B decisions)',
-            'traffic_over_alg': round(tr / row_bytes, 3) if tr else None,
-            'traffic_GBs': round(tr_gbs, 1) if tr_gbs else None,
-            'traffic_frac': round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs else None,
-            'shape_ceiling': ({'GBs': ceil, 'traffic_frac_of_ceiling': round(tr_gbs / ceil, 4) if tr_gbs else None,
-                               'source': 'profiles/r3_turbo_shape_microbench.json'} if ceil else None),
+            'what': 'SURVEY §8(d) K7: sum(K+3) x (2 it. + 1) passes x 100 add/max ops per subframe '
+                    f'({ops_sf} op) x frames / mean launch time, against the non-packed {prec} vector peak; '
+                    'traffic = PMC-measured HBM bytes per launch (gfx950-corrected)',
+            'ops_per_subframe': ops_sf,
             'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': t_n, 'frames_per_launch': F,
-            'stage_bytes': {'bytes_per_launch': int(stage_bytes), 'achieved_GBs': round(stage_bytes / avg_s / 1e9, 2)
-                            if t_n else 0.0, 'frac': round(stage_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if t_n else 0.0,
-                            'what': 'SURVEY §8(d) stage boundary: rate-dematched input LLRs + decoded bits'},
-            'valu': {'achieved_Tops': round(achieved_T, 3), 'peak_Tops': round(peak / 1e12, 2),
-                     'frac': round(achieved_T * 1e12 / peak, 4), 'ops_per_subframe': TURBO_OPS_SF,
-                     'issued_busy_frac': round(busy, 4) if busy is not None else None,
-                     'wave_instr_per_frame': sq['valu_wave_instr_per_frame'] if sq else None},
-            'turbo_share_of_step': round(t_ms / (el * 1e3) if el > 0 else 0, 3),
-            'front_end': front_end(prec, tim, F),
-            'kernel_ms_per_step': {k: round(v[0] / steps, 3) for k, v in tim.items() if v[1]},
+            'issued_valu_busy_frac': round(busy, 4) if busy is not None else None,
+            'valu_wave_instr_per_frame': sq['valu_wave_instr_per_frame'] if sq else None,
+            'measured_limiter': 'hbm' if busy is None or (tr_gbs or gbs) / HBM_PEAK_GBS >= busy else 'valu',
+            'hbm_row_stream': {
+                'achieved_GBs': round(gbs, 1), 'peak_GBs': HBM_PEAK_GBS,
+                'frac_row_stream': round(gbs / HBM_PEAK_GBS, 4),
+                'alg_bytes_per_launch': int(row_bytes),
+                'alg_bytes': 'exact-recursion row stream: per code-block step 7 rows (Ls, Lp, La forward and '
+                             'backward + extrinsic store) x esz B x 17 passes (first pass 5, final 6 + K/8 B decisions)',
+                'traffic_over_alg': round(tr / row_bytes, 3) if tr else None,
+                'traffic_GBs': round(tr_gbs, 1) if tr_gbs else None,
+                'traffic_frac': round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs else None,
+                'shape_ceiling': ({'GBs': ceil, 'traffic_frac_of_ceiling': round(tr_gbs / ceil, 4) if tr_gbs else None,
+                                   'source': 'profiles/r3_turbo_shape_microbench.json (another box: +-5 %)'}
+                                  if ceil else None),
+                # same box, same layout: the decoder's access shape with and
+                # without its stores (extrinsic + checkpoint rows, 17 % of the bytes)
+                'store_cost': {'shape_ms_full': 319.5, 'shape_ms_reads_only': 237.4,
+                               'store_share_of_time': round(1 - 237.4 / 319.5, 3), 'store_share_of_bytes': 0.17,
+                               'source': 'profiles/r3_turbo_shape_layouts.jsonl run shape4, variants aux3 / a3nost, '
+                                         'CH 32 (65 536 frames)'}},
+            'stage_bytes': {'bytes_per_launch': int(stage_bytes),
+                            'achieved_GBs': round(stage_bytes / avg_s / 1e9, 2) if t_n else 0.0,
+                            'frac': round(stage_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if t_n else 0.0,
+                            'what': 'SURVEY §8(d) stage boundary: rate-dematched input LLRs + decoded bits'}}
+
+
+def stage_bytes_per_frame(config, plan, prec):
+    """Algorithmic HBM bytes per frame of each timed stage (the streams a stage
+    must read and write at its boundaries; complex = 2 x esz B) for the
+    uncoded configs' roofline."""
+    esz = 8 if prec == 'f64' else 4
+    c = 2 * esz
+    L, n_sym, bits = plan.L, plan.n_sym, plan.n_bits / 8
+    if config == 3:
+        nr = plan.num_rx
+        return {'ofdm_tx': ('k_ofdm_tx (fused SIMO channel)', bits + nr * L * c),
+                'rx_data': ('k_rx_frame_simo', nr * L * c + bits)}
+    nt, nr = plan.num_tx, plan.num_rx
+    y = n_sym * nr * plan.n_dsc * c
+    h = nr * plan.n_est * nt * plan.n_dsc * c
+    return {'ofdm_tx': ('k_ofdm_tx_mimo', bits + nt * L * c),
+            'channel': ('k_channel_mimo', (nt + nr) * L * c),
+            'rx_chest': ('k_rx_fft_mimo', nr * L * c + y + h),
+            'rx_data': ('k_det_spatial', y + h + bits)}
+
+
+def hbm_roofline(config, plan, prec, tim, F):
+    """Uncoded configs: the dominant timed stage against the HBM roofline --
+    its algorithmic bytes per frame x frames / its mean launch time."""
+    sb = stage_bytes_per_frame(config, plan, prec)
+    stages = {k: v for k, v in tim.items() if k in sb and v[1]}
+    if not stages:
+        return None
+    dom = max(stages, key=lambda k: stages[k][0] / stages[k][1])
+    t_ms, n = stages[dom]
+    avg_s = t_ms / n * 1e-3
+    kern, b = sb[dom]
+    gbs = b * F / avg_s / 1e9
+    return {'bound': 'hbm', 'kernel': kern, 'stage': dom, 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+            'alg_bytes_per_frame': round(b), 'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': n,
+            'frames_per_launch': F,
+            'what': 'algorithmic stage-boundary bytes (the streams the kernel must read / write) x frames / '
+                    'mean launch time (HIP events on the plan stream)',
+            'other_stages': {k: {'kernel': sb[k][0], 'ms': round(v[0] / v[1], 3),
+                                 'GBs': round(sb[k][1] * F / (v[0] / v[1] * 1e-3) / 1e9, 1)}
+                             for k, v in stages.items() if k != dom}}
+
+
+def roofline(config, prec, tim, steps, F, el, value, world, iters=8, plan=None):
+    if config in (2, 4):
+        roof = turbo_roofline(prec, tim, F, iters)
+        t_ms = tim.get('turbo', (0.0, 0))[0]
+        roof['turbo_share_of_step'] = round(t_ms / (el * 1e3) if el > 0 else 0, 3)
+        if config == 2:
+            esz = 8 if prec == 'f64' else 4
+            roof['front_end'] = front_end(prec, tim, F)
             # SURVEY §8(d)'s whole-chain view: compulsory stage-boundary bytes per subframe
-            'pipeline_hbm': {'bytes_per_subframe': B_SF_F32 * esz // 4,
-                             'achieved_GBs': round(B_SF_F32 * esz / 4 * value / world / 1e9, 2),
-                             'frac': round(B_SF_F32 * esz / 4 * value / world / 1e9 / HBM_PEAK_GBS, 5)}}
+            roof['pipeline_hbm'] = {'bytes_per_subframe': B_SF_F32 * esz // 4,
+                                    'achieved_GBs': round(B_SF_F32 * esz / 4 * value / world / 1e9, 2),
+                                    'frac': round(B_SF_F32 * esz / 4 * value / world / 1e9 / HBM_PEAK_GBS, 5)}
+    else:
+        roof = hbm_roofline(config, plan, prec, tim, F) if plan is not None else None
+        if roof is None:
+            return None
+    roof['kernel_ms_per_step'] = {k: round(v[0] / steps, 3) for k, v in tim.items() if v[1]}
     return roof
 
 
@@ -261,17 +426,40 @@ def front_end(prec, tim, F):
     return out
 
 
-def dry_run_counts(ids, S):
+def dry_run_counts(ids, S, n_bits=TB):
     """--dry-run: a deterministic per-frame statistic in place of the GPU chain
     (exercises the launcher, sharding and reductions without a device)."""
     from lte_phy import dist as D
     si = D.snr_index(ids, S)
     c = np.zeros((S, 4), dtype=np.uint64)
     np.add.at(c[:, 0], si, ids % np.uint64(7))
-    np.add.at(c[:, 1], si, np.uint64(TB))
+    np.add.at(c[:, 1], si, np.uint64(n_bits))
     np.add.at(c[:, 2], si, (ids % np.uint64(3) == 0).astype(np.uint64))
     np.add.at(c[:, 3], si, np.uint64(1))
     return c
+
+
+def make_plan(config, args):
+    """The bench plan of one config (the same builders the drop-in API uses)."""
+    import lte_phy
+    from lte_phy import _capi as C
+    Cfg, Sim = lte_phy.LTEConfig, lte_phy.OFDMSimulator
+    F = args.frames
+    if config == 2:
+        sim = Sim(Cfg(bandwidth=20.0, modulation='64-QAM'), channel_type='rayleigh_mp', itu_profile='Pedestrian_A',
+                  velocity_kmh=args.velocity, precision=args.precision)
+        return sim._plan(C.CHAIN_CODED, 0, TB, max_frames=F, iters=args.iters)
+    if config == 3:
+        sim = Sim(Cfg(bandwidth=10.0, modulation='16-QAM'), channel_type='rayleigh_mp', itu_profile='Vehicular_A',
+                  velocity_kmh=args.velocity, precision=args.precision)
+        return sim._plan(C.CHAIN_SIMO, 14, WORKLOADS[3]['n_bits'], num_rx=4, max_frames=F)
+    if config == 4:
+        sim = Sim(Cfg(bandwidth=20.0, modulation='64-QAM'), channel_type='rayleigh_mp', itu_profile='Pedestrian_A',
+                  velocity_kmh=args.velocity, precision=args.precision)
+        return sim._sfbc_plan(0, TB, 2, coded=True, max_frames=F, iters=args.iters)
+    from lte_phy.ofdm_core import _spatial_plan
+    return _spatial_plan(Cfg(bandwidth=20.0, modulation='64-QAM'), args.channel or 'awgn', 'Pedestrian_A',
+                         args.velocity or 3.0, 2.0, 14, WORKLOADS[5]['n_bits'], F, precision=args.precision)[0]
 
 
 def main():
@@ -279,17 +467,24 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--frames', type=int, default=65536, help='subframes per step per GPU')
+    ap.add_argument('--config', type=int, choices=sorted(WORKLOADS), default=2,
+                    help='BASELINE.json config: 2 (the headline), 3, 4 or 5')
+    ap.add_argument('--frames', type=int, default=None, help='subframes per step per GPU (default: per config)')
     ap.add_argument('--iters', type=int, default=8)
     ap.add_argument('--precision', choices=('f64', 'f32'), default='f64')
     ap.add_argument('--velocity', type=float, default=0.0,
                     help='UE speed in km/h (fD = v fc / c at 2 GHz); 0 = the OFDMSimulator default (static taps), '
                          '3 = the GUI default (Jakes fading over the subframe): a secondary line, not the headline')
-    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--channel', choices=('awgn', 'rayleigh_mp'), default=None,
+                    help='config 5 only: flat CN(0,1) links (default, simulate_spatial_multiplexing\'s default) '
+                         'or PedA Rayleigh at --velocity (3 km/h if 0)')
+    ap.add_argument('--cpu-seconds', type=float, default=None)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--dry-run', action='store_true', help='no GPU: launcher / sharding / reductions only (gloo)')
     argv = sys.argv[1:]
     args = ap.parse_args()
+    wl = WORKLOADS[args.config]
+    args.frames = int(args.frames or wl['frames'])
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args, argv))
@@ -304,9 +499,12 @@ def main():
     # wait for it in the rendezvous), or in the self-launching parent, which
     # hands it over in LTE_BENCH_CPU_JSON
     cpu = None
-    if rank == 0 and not args.no_cpu:
-        cpu = (json.loads(os.environ['LTE_BENCH_CPU_JSON']) if os.environ.get('LTE_BENCH_CPU_JSON')
-               else cpu_baseline(args.cpu_seconds))
+    if rank == 0 and os.environ.get('LTE_BENCH_CPU_JSON'):
+        with open(os.environ['LTE_BENCH_CPU_JSON']) as f:
+            cpu = json.load(f)
+    elif rank == 0 and cpu_seconds(args) > 0:
+        cpu = cpu_baseline(args.config, args.frames, cpu_seconds(args), None, args.channel)
+        cpu['config'] = args.config
     import torch
     dist = None
     # LTE_BENCH_BACKEND=gloo: rehearse the N>1 path with several ranks sharing
@@ -330,29 +528,25 @@ def main():
 
     from lte_phy import dist as D
     S = len(SNRS)
-    F = int(args.frames)
+    F = args.frames
     counts = np.zeros((S, 4), dtype=np.uint64)
+    prec = args.precision
     if args.dry_run:
         plan = None
         dev_id = f'rank{rank}'
-        step = lambda k: dry_run_counts(D.frame_ids(k, rank, world, F), S)   # noqa: E731
-        prec = args.precision
+        step = lambda k: dry_run_counts(D.frame_ids(k, rank, world, F), S, wl['n_bits'])   # noqa: E731
     else:
-        import lte_phy
         from lte_phy import _capi as C
         C.device_init(local)
         props = torch.cuda.get_device_properties(local)
         dev_id = f"{getattr(props, 'pci_bus_id', '')}:{getattr(props, 'uuid', local)}"
-        sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=20.0, modulation='64-QAM'),
-                                    channel_type='rayleigh_mp', itu_profile='Pedestrian_A',
-                                    velocity_kmh=args.velocity, precision=args.precision)
-        plan = sim._plan(C.CHAIN_CODED, 0, TB, max_frames=F, iters=args.iters)
+        plan = make_plan(args.config, args)
         prec = plan.precision
 
         def step(k):
             ids = D.frame_ids(k, rank, world, F)
             si = D.snr_index(ids, S)
-            return plan.run(SNRS[si], snr_index=si, n_snr=S, seed=0x5EED, frame_ids=ids)['counts']
+            return plan.run(SNRS[si], snr_index=si, n_snr=S, seed=SEED, frame_ids=ids)['counts']
 
     def barrier():
         if not args.dry_run:
@@ -400,23 +594,32 @@ def main():
     value = total / el
     ber = (counts[:, 0] / np.maximum(counts[:, 1], 1)).tolist()
     bler = (counts[:, 2] / np.maximum(counts[:, 3], 1)).tolist()
-    workload = ('config 2: SISO 20 MHz (N=2048) 64-QAM, Rayleigh ITU Pedestrian-A, '
-                'turbo max-log-MAP 8 it., TB 27760 (5 CBs, 14 OFDM symbols), SNR 0:2:30 dB')
+    workload = wl['desc']
     if args.velocity:
         workload += f' -- SECONDARY line: UE at {args.velocity:g} km/h (Jakes fading over the subframe)'
-    out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'subframes/s', 'n_gpus': n_dev,
+    if args.config == 5 and args.channel == 'rayleigh_mp':
+        workload += f' -- links: Rayleigh PedA at {args.velocity or 3.0:g} km/h'
+    metric = METRIC if args.config == 2 else f"LTE subframes/sec ({wl['short']}) at 1/2/4/8 GPU; BER match"
+    out = {'metric': metric, 'value': round(value, 1), 'unit': 'subframes/s', 'n_gpus': n_dev,
            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el * 1e3 / args.steps, 3),
            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': prec,
            'data': 'synthetic (Philox4x32-10 payload bits, Jakes phases and AWGN generated on the GPU)',
-           'config': {'workload': workload, 'velocity_kmh': args.velocity,
+           'config': {'workload': workload, 'bench_config': args.config, 'velocity_kmh': args.velocity,
                       'frames_per_step_per_gpu': F, 'global_batch': F * world, 'parallelism': f'dp{world}',
                       'ranks': world, 'snr_db': SNRS.tolist()},
-           'roofline': roofline(prec, tim, args.steps, F, el, value, world, args.iters) if tim else None,
+           'roofline': (roofline(args.config, prec, tim, args.steps, F, el, value, world, args.iters, plan)
+                        if tim else None),
            'ber': [float(f'{b:.4e}') for b in ber], 'bler': [float(f'{b:.4e}') for b in bler]}
     if args.dry_run:
         out['dry_run'] = True
         out['counts'] = counts.tolist()
     if rank == 0:
+        # BER match on the oracle's sample of this run's own frames (outside the timed region)
+        out['ber_match'] = ber_match(plan, cpu, wl['coded']) if plan is not None else None
+        if cpu:
+            cpu = {k: v for k, v in cpu.items() if k not in ('frames', 'config')}
+            if world > 1:
+                cpu['note'] = f'{cpu["cores"]} host cores of the node ({CPU_PER_GPU} per GPU)'
         out['cpu_baseline'] = cpu
         print(json.dumps(out), flush=True)
     if dist is not None:

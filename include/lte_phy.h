@@ -196,6 +196,16 @@ int lte_fft_host(int N, int inverse, int64_t batch, const float *in, float *out)
 int lte_fft_host64(int N, int inverse, int64_t batch, const double *in, double *out);
 /* Pilots: PilotPattern.generate_pilots core/resource_mapper.py:137-152 (MT19937 seed(cell_id) + choice([1,-1])) */
 int lte_pilots(int cell_id, int n, double *out_re_im);
+/* The Philox mode's device random streams (the draws that replace the
+ * reference's np.random.randint / rand / normal: core/rayleighchannel.py:31,
+ * core/channel.py:227-228): for each frame f and counter c < n_ctr,
+ * Philox4x32-10 of counter (c, stream, frame_id lo, hi), key (seed lo, hi).
+ * out_u32 [n_frames][n_ctr][4] the four outputs; out_gauss64 / out_gauss32
+ * [n_frames][n_ctr][4] the unit normal pairs the noise kernels form from
+ * outputs (x, y) and (z, w) (float64 / float32 Box-Muller).  Any output may
+ * be NULL. */
+int lte_philox_host(uint64_t seed, int n_frames, const uint64_t *frame_ids, uint32_t stream, int64_t n_ctr,
+                    uint32_t *out_u32, double *out_gauss64, float *out_gauss32);
 /* SC-FDM DFT / IDFT of size M (<= 1024): DFTPrecodifier.precoding /
  * IDFTDecodifier.decoding core/dft_precoding.py:66-118, 199-226 (unitary,
  * 1/sqrt(M)); in / out [batch][M] complex64.  Bluestein on the device. */

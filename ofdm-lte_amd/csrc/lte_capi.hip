@@ -489,6 +489,9 @@ template <class R> ChainBufs<R>& cbuf(lte_plan* p);
 template <> ChainBufs<float>& cbuf<float>(lte_plan* p) { return p->c32; }
 template <> ChainBufs<double>& cbuf<double>(lte_plan* p) { return p->c64; }
 
+// chunk width of the plan's decoder rows (allocated for ceil(max_frames / 64) groups)
+int turbo_plan_ch(const lte_plan* p) { return turbo_chunk((p->d.max_frames + 63) / 64); }
+
 void collect_timing(lte_plan* p) {
   for (auto& u : p->evuse) {
     float ms = 0.f;
@@ -538,6 +541,34 @@ int lte_pilots(int cell_id, int n, double* out) {
   make_pilots(cell_id, n, v);
   std::memcpy(out, v.data(), v.size() * sizeof(double));
   return LTE_OK;
+}
+
+int lte_philox_host(uint64_t seed, int n_frames, const uint64_t* frame_ids, uint32_t stream, int64_t n_ctr,
+                    uint32_t* out_u32, double* out_gauss64, float* out_gauss32) {
+  if (n_frames < 0 || n_ctr < 0 || n_ctr > 0xFFFFFFFFll || (n_frames && !frame_ids))
+    return fail(LTE_EINVAL, "bad philox arguments");
+  const int64_t n = (int64_t)n_frames * n_ctr;
+  if (n == 0) return LTE_OK;
+  DBuf<uint64_t> dfid;
+  DBuf<uint32_t> du;
+  DBuf<double> d64;
+  DBuf<float> d32;
+  auto rel = [&] { dfid.release(); du.release(); d64.release(); d32.release(); };
+  if (dfid.alloc(n_frames) || (out_u32 && du.alloc(4 * n)) || (out_gauss64 && d64.alloc(4 * n)) ||
+      (out_gauss32 && d32.alloc(4 * n))) {
+    rel();
+    return fail(LTE_ENOMEM, "philox buffers");
+  }
+  int rc = LTE_OK;
+  if (hipMemcpy(dfid.p, frame_ids, n_frames * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_philox_draws(nullptr, seed, dfid.p, n_frames, stream, n_ctr, du.p, d64.p, d32.p) ||
+      hipDeviceSynchronize() != hipSuccess ||
+      (out_u32 && hipMemcpy(out_u32, du.p, 16 * n, hipMemcpyDeviceToHost) != hipSuccess) ||
+      (out_gauss64 && hipMemcpy(out_gauss64, d64.p, 32 * n, hipMemcpyDeviceToHost) != hipSuccess) ||
+      (out_gauss32 && hipMemcpy(out_gauss32, d32.p, 16 * n, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = fail(LTE_EHIP, "philox failed");
+  rel();
+  return rc;
 }
 
 }  // extern "C"
@@ -1502,13 +1533,14 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   if (coded) {
     {
       Timer t(p, KN_DEMATCH);
-      LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p));
+      LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p,
+                                 turbo_plan_ch(p)));
     }
     const int G = (B + 63) / 64;
     std::vector<TurboJob> jobs(p->C);
     for (int r = 0; r < p->C; ++r) {
       const CbInfo& cb = p->cbs[r];
-      jobs[r] = TurboJob{c.blk[r].p, c.ckpt[r].p, p->decb[r].p, cb.K, cb.f1, cb.f2, G};
+      jobs[r] = TurboJob{c.blk[r].p, c.ckpt[r].p, p->decb[r].p, cb.K, cb.f1, cb.f2, G, turbo_plan_ch(p)};
     }
     {
       Timer t(p, KN_TURBO);
@@ -1899,15 +1931,16 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
       Timer t(p, KN_DEMATCH);
       if (zn)
         LCHK(launch_dematch_zn<R>(s, zn_z<R>(p), zn_nv<R>(p), p->n_re_bits / d.bps, p->Nd, d.bps, B, p->rx_map.p,
-                                  p->n_layers, c.blk_ptrs.p, p->rows_dev.p));
+                                  p->n_layers, c.blk_ptrs.p, p->rows_dev.p, turbo_plan_ch(p)));
       else
-        LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p));
+        LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p,
+                                 turbo_plan_ch(p)));
     }
     const int G = (B + 63) / 64;
     std::vector<TurboJob> jobs(p->C);
     for (int r = 0; r < p->C; ++r) {
       const CbInfo& cb = p->cbs[r];
-      jobs[r] = TurboJob{c.blk[r].p, c.ckpt[r].p, p->decb[r].p, cb.K, cb.f1, cb.f2, G};
+      jobs[r] = TurboJob{c.blk[r].p, c.ckpt[r].p, p->decb[r].p, cb.K, cb.f1, cb.f2, G, turbo_plan_ch(p)};
     }
     {
       Timer t(p, KN_TURBO);
@@ -2266,32 +2299,34 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const T* llr, const T* 
   if (ncb == 0) return LTE_OK;
   const int f64 = sizeof(T) == 8;
   const int G = (int)((ncb + 63) / 64);
+  const int ch = turbo_chunk(G);   // fewer than TURBO_CH groups: contiguous blocks, no padding
   const int64_t rows = turbo_rows(K);
   std::vector<T> h((size_t)turbo_galloc(G) * rows * 64, (T)0);
-  auto at = [&](int64_t c, int64_t row) -> T& { return h[turbo_elem(rows, c / 64, row) + (c % 64)]; };
+  auto at = [&](int64_t c, int64_t row) -> T& { return h[turbo_elem_ch(ch, rows, c / 64, row) + (c % 64)]; };
+  // decoder rows hold LLR/2 (exact; lte_decoder.hip gam)
+  auto put = [&](int64_t c, int64_t row, T v) { at(c, row) = (T)0.5 * v; };
   for (int64_t c = 0; c < ncb; ++c) {
     if (mode == TM_APP) {
       const T* s = ls + c * (K + 3);
       const T* q = lp + c * (K + 3);
       const T* A = la + c * (K + 3);
-      for (int k = 0; k < K + 3; ++k) { at(c, trow_ls(K, k)) = s[k]; at(c, trow_lp(K, 1, k)) = q[k]; }
-      for (int k = 0; k < K; ++k) at(c, trow_le(K, k)) = A[k];
+      for (int k = 0; k < K + 3; ++k) { put(c, trow_ls(K, k), s[k]); put(c, trow_lp(K, 1, k), q[k]); }
+      for (int k = 0; k < K; ++k) put(c, trow_le(K, k), A[k]);
     } else {
       const T* l = llr + c * (3 * K + 12);
       for (int k = 0; k < K; ++k) {
-        at(c, trow_ls(K, k)) = l[3 * k];
-        at(c, trow_lp(K, 1, k)) = l[3 * k + 1];
-        at(c, trow_lp(K, 2, k)) = l[3 * k + 2];
+        put(c, trow_ls(K, k), l[3 * k]);
+        put(c, trow_lp(K, 1, k), l[3 * k + 1]);
+        put(c, trow_lp(K, 2, k), l[3 * k + 2]);
       }
       for (int t = 0; t < 3; ++t) {
-        at(c, trow_ls(K, K + t)) = l[3 * K + t];
-        at(c, trow_lp(K, 1, K + t)) = l[3 * K + 3 + t];
-        at(c, trow_ls2t(K, t)) = l[3 * K + 6 + t];
-        at(c, trow_lp(K, 2, K + t)) = l[3 * K + 9 + t];
+        put(c, trow_ls(K, K + t), l[3 * K + t]);
+        put(c, trow_lp(K, 1, K + t), l[3 * K + 3 + t]);
+        put(c, trow_ls2t(K, t), l[3 * K + 6 + t]);
+        put(c, trow_lp(K, 2, K + t), l[3 * K + 9 + t]);
       }
     }
   }
-  for (T& v : h) v *= (T)0.5;   // decoder rows hold LLR/2 (exact; lte_decoder.hip gam)
   DBuf<T> db, dck;
   DBuf<uint32_t> dbits;
   const int KW = turbo_kw(K);
@@ -2301,7 +2336,7 @@ static int turbo_host_run(int K, int iters, int64_t ncb, const T* llr, const T* 
   int rc = LTE_OK;
   std::vector<uint32_t> hb((size_t)G * KW * 64);
   if (hipMemcpy(db.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess ||
-      launch_turbo(nullptr, db.p, dck.p, dbits.p, K, f1, f2, iters, G, mode, f64) ||
+      launch_turbo(nullptr, db.p, dck.p, dbits.p, K, f1, f2, iters, G, mode, f64, ch) ||
       hipDeviceSynchronize() != hipSuccess)
     rc = fail(LTE_EHIP, std::string("turbo failed: ") + hipGetErrorString(hipGetLastError()));
   if (rc == LTE_OK) {

@@ -43,8 +43,8 @@ enum : uint32_t {
   RNG_STREAM_BITS = 1u,
   RNG_STREAM_FADE = 0x100u,   // + rx*64 + tx
   RNG_STREAM_NOISE = 0x10000u, // + rx
-  RNG_STREAM_MIMO_FADE = 0x20000u,  // + (rx*16 + tx)*16 + path
-  RNG_STREAM_MIMO_LINK = 0x30000u,  // + rx*16 + tx : link noise (transmit_mimo) / flat link gain (spatial)
+  RNG_STREAM_MIMO_FADE = 0x20000u,  // + link * n_paths + path, link = rx * num_tx + tx
+  RNG_STREAM_MIMO_LINK = 0x30000u,  // + link : link noise (transmit_mimo) / flat link gain (spatial)
   RNG_STREAM_BF = 0x40000u,         // + rx*num_tx + tx : beamforming flat channel H
 };
 
@@ -81,7 +81,10 @@ __device__ __forceinline__ double2 box_muller64(uint32_t a, uint32_t b) {
 // within a few float64 ulps of them (scripts/rx_parts_bench.hip measures both).
 //  ln u, u = (a + 0.5) 2^-32: u = 2^e m, m in [1, 2); m = c_i (1 + r) with c_i
 //  the centre of m's 1/128 bucket, ln u = e ln 2 + ln c_i + log1p(r); for u in
-//  [1 - 2^-8, 1) log1p(-(1 - u)) directly (keeps the relative precision near 1).
+//  [1/2, 1) (e = -1) ln(c_i / 2) + log1p(r) from its own correctly rounded
+//  table (BM_LH: -ln 2 + ln c_i cancels there, which cost up to 81 ulp of the
+//  radius near u = 1 - 2^-8, tests/test_gpu_philox.py); for u in [1 - 2^-8, 1)
+//  log1p(-(1 - u)) directly (keeps the relative precision near 1).
 //  angle 2 pi (b + 0.5) 2^-32 = 2 pi (i + 0.5) / 256 + x, |x| < 2 pi 2^-9.
 __device__ __forceinline__ double log1p_small(double r) {   // |r| <= 2^-8, error < 2^-60
   return r * (1.0 + r * (-0.5 + r * (0x1.5555555555555p-2 + r * (-0.25 + r * (0.2 + r * (-0x1.5555555555555p-3 +
@@ -100,7 +103,9 @@ __device__ __forceinline__ double ln_u32(uint32_t a) {
   const double r = near1 ? -d : (m - c) * t.x;                    // m - c exact
   const double p = log1p_small(r);
   const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
-  return near1 ? p : (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
+  if (near1) return p;
+  if (e == -1) return BM_LH[i] + p;
+  return (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
 }
 __device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b) {
   const double r = sqrt(-2.0 * ln_u32(a));
@@ -108,8 +113,10 @@ __device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b) {
   const double x = ((double)((int)(b & 0xFFFFFFu) - 0x800000) + 0.5) * 0x1p-32 * 0x1.921fb54442d18p+2;
   const double x2 = x * x;
   const double sx = x + x * x2 * (-0x1.5555555555555p-3 + x2 * (0x1.1111111111111p-7 + x2 * -0x1.a01a01a01a01ap-13));
-  const double cx = 1.0 + x2 * (-0.5 + x2 * (0x1.5555555555555p-5 + x2 * -0x1.6c16c16c16c17p-10));
-  const double c = T.x * cx - T.y * sx, s = T.y * cx + T.x * sx;
+  const double cm1 = x2 * (-0.5 + x2 * (0x1.5555555555555p-5 + x2 * -0x1.6c16c16c16c17p-10));   // cos x - 1
+  // the table value plus a small correction, rounded once: |error| <= 2^-53
+  // per component (cos x formed as 1 + cm1 first doubled it)
+  const double c = T.x + (T.x * cm1 - T.y * sx), s = T.y + (T.y * cm1 + T.x * sx);
   return make_double2(r * c, r * s);
 }
 template <class R> __device__ __forceinline__ cx<R> gauss2(uint32_t a, uint32_t b);

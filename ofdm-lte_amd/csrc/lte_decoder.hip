@@ -270,16 +270,16 @@ struct RowPtr {
 // MODE TM_FINAL: the decoder-1 a-posteriori pass that ends a decode; it also
 // packs the hard decisions L < 0 MSB-first into `bo` (words [kw][64 lanes]),
 // storing each word as the backward sweep reaches its bit 0 (no re-read pass).
-template <class T, int MODE, bool LM = false>
+template <class T, int MODE, bool LM = false, int CH = TURBO_CH>
 __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__ wck, int slot, int lane, int K,
                                           int f1, int f2, bool first, uint32_t* __restrict__ bo = nullptr) {
   using TT = TurboT<T>;
-  using DRow = RowPtr<T, RS * TURBO_CH * (int)sizeof(T), LTE_TURBO_CPOL>;   // the block arrays' rows
+  using DRow = RowPtr<T, RS * CH * (int)sizeof(T), LTE_TURBO_CPOL>;   // the block arrays' rows (CH groups side by side)
   constexpr int TSUB = TT::TSUB, SW = TW * TSUB, CK = TT::CK, CK0 = 8 - CK;   // CK0: first stored state
   constexpr int TH = TW / TT::HALVES;
   // wbase / wck: the group's chunk; slot: the group's place in it (turbo_elem)
   const int vo = (slot * RS + lane) * (int)sizeof(T);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * TURBO_CH * RS * sizeof(T)));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(wbase, (uint32_t)(turbo_rows(K) * CH * RS * sizeof(T)));
   // rows of step k < K: base + k * stride (lte_internal.h trow_*); tails separately
   constexpr int IST = LTE_TURBO_ILV == 3 ? 4 : LTE_TURBO_ILV == 2 ? 3 : LTE_TURBO_ILV == 1 ? 2 : 1;
   constexpr int DEC = (MODE == TM_DEC2) ? 2 : 1;
@@ -289,7 +289,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
   const DRow LPT{rb, (int)trow_lp(K, DEC, K), vo};   // parity tail
   const DRow LS2T{rb, (int)trow_ls2t(K, 0), vo};
   const DRow LE{rb, (int)trow_le(K, 0), vo, IST};
-  const DRow ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * CK * TURBO_CH * RS * sizeof(T))), 0, vo};
+  const DRow ck{make_rsrc(wck, (uint32_t)(turbo_nwin(K) * CK * CH * RS * sizeof(T))), 0, vo};
   const int nsub = K / TW;   // every LTE K is a multiple of 8
   const int tf2 = (2 * f2) % K;
   const bool use_la = !first;
@@ -496,7 +496,7 @@ __device__ __forceinline__ void half_pass(T* __restrict__ wbase, T* __restrict__
 // One launch decodes every code-block slot of the batch: wave w -> job r
 // (CB slot, i.e. one K) and frame group g.  256-thread blocks = 4 independent
 // waves (no LDS, no barriers).
-template <class T, bool LM = false>
+template <class T, bool LM = false, int CH = TURBO_CH>
 __device__ __forceinline__ void turbo_body(const TurboJobs& jobs, int iters, int mode) {
   const int wg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -506,22 +506,22 @@ __device__ __forceinline__ void turbo_body(const TurboJobs& jobs, int iters, int
   const TurboJob jb = jobs.j[r];
   const int g = wg - jobs.prefix[r];
   const int K = jb.K;
-  // the group's chunk of the block arrays (turbo_elem: [chunk][row][TURBO_CH][64])
-  const int slot = g % TURBO_CH;
-  T* base = reinterpret_cast<T*>(jb.blk) + turbo_elem(turbo_rows(K), g - slot, 0);
-  T* ck = reinterpret_cast<T*>(jb.ck) + turbo_elem(turbo_nwin(K) * TurboT<T>::CK, g - slot, 0);
+  // the group's chunk of the block arrays (turbo_elem: [chunk][row][CH][64])
+  const int slot = g % CH;
+  T* base = reinterpret_cast<T*>(jb.blk) + turbo_elem<CH>(turbo_rows(K), g - slot, 0);
+  T* ck = reinterpret_cast<T*>(jb.ck) + turbo_elem<CH>(turbo_nwin(K) * TurboT<T>::CK, g - slot, 0);
   uint32_t* bo = jb.bits + (size_t)g * turbo_kw(K) * RS;
   if (mode == TM_APP) {
-    half_pass<T, TM_APP, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, false);
+    half_pass<T, TM_APP, LM, CH>(base, ck, slot, lane, K, jb.f1, jb.f2, false);
     return;
   }
   for (int it = 0; it < iters; ++it) {
-    half_pass<T, TM_DEC1, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, it == 0);
-    half_pass<T, TM_DEC2, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, false);
+    half_pass<T, TM_DEC1, LM, CH>(base, ck, slot, lane, K, jb.f1, jb.f2, it == 0);
+    half_pass<T, TM_DEC2, LM, CH>(base, ck, slot, lane, K, jb.f1, jb.f2, false);
   }
   // final pass = decoder 1 a-posteriori LLRs (turbo_decoder.py:440-447) and
   // the hard decisions L < 0 (:276), packed MSB-first
-  half_pass<T, TM_FINAL, LM>(base, ck, slot, lane, K, jb.f1, jb.f2, iters == 0, bo);
+  half_pass<T, TM_FINAL, LM, CH>(base, ck, slot, lane, K, jb.f1, jb.f2, iters == 0, bo);
 }
 
 // f32 fast mode: 134 VGPRs = 3 waves per SIMD; LTE_TURBO32_WAVES = 2 / 1 caps
@@ -529,13 +529,16 @@ __device__ __forceinline__ void turbo_body(const TurboJobs& jobs, int iters, int
 #ifndef LTE_TURBO32_WAVES
 #define LTE_TURBO32_WAVES 3
 #endif
+// CH: the chunk width of the jobs' block arrays (TURBO_CH, or 1 for arrays of
+// fewer groups: turbo_chunk)
+template <int CH>
 __global__ __launch_bounds__(256, LTE_TURBO32_WAVES == 3 ? 2 : 1) void k_turbo(TurboJobs jobs, int iters, int mode) {
 #if LTE_TURBO32_WAVES == 2
   asm volatile("" ::: "a47");
 #elif LTE_TURBO32_WAVES == 1
   asm volatile("" ::: "a127");
 #endif
-  turbo_body<float>(jobs, iters, mode);
+  turbo_body<float, false, CH>(jobs, iters, mode);
 }
 
 // f64: one wave per SIMD (LTE_TURBO64_ONE_WAVE, default on; 0: up to 256
@@ -545,16 +548,18 @@ __global__ __launch_bounds__(256, LTE_TURBO32_WAVES == 3 ? 2 : 1) void k_turbo(T
 #ifndef LTE_TURBO64_ONE_WAVE
 #define LTE_TURBO64_ONE_WAVE 1
 #endif
+template <int CH>
 __global__ __launch_bounds__(256, LTE_TURBO64_ONE_WAVE ? 1 : 2) void k_turbo64(TurboJobs jobs, int iters, int mode) {
 #if LTE_TURBO64_ONE_WAVE
   asm volatile("" ::: "a31");
 #endif
-  turbo_body<double>(jobs, iters, mode);
+  turbo_body<double, false, CH>(jobs, iters, mode);
 }
 
 // f64 exact log-MAP (set_decoder_mode(False)); not a hot path
+template <int CH>
 __global__ __launch_bounds__(256, 1) void k_turbo64_logmap(TurboJobs jobs, int iters, int mode) {
-  turbo_body<double, true>(jobs, iters, mode);
+  turbo_body<double, true, CH>(jobs, iters, mode);
 }
 
 // decoder arithmetic of the f64 entry points and chains: max-log-MAP (the
@@ -574,9 +579,21 @@ int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int
     }
     const int waves = J.prefix[J.n];
     if (waves == 0) continue;
-    if (f64 && g_logmap) hipLaunchKernelGGL(k_turbo64_logmap, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
-    else if (f64) hipLaunchKernelGGL(k_turbo64, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
-    else hipLaunchKernelGGL(k_turbo, dim3((waves + 3) / 4), dim3(256), 0, s, J, iters, mode);
+    const int ch = J.j[0].ch;
+    for (int i = 1; i < J.n; ++i)
+      if (J.j[i].ch != ch) return (int)hipErrorInvalidValue;   // one chunk width per launch
+    const dim3 grid((waves + 3) / 4);
+    if (ch == TURBO_CH) {
+      if (f64 && g_logmap) hipLaunchKernelGGL(k_turbo64_logmap<TURBO_CH>, grid, dim3(256), 0, s, J, iters, mode);
+      else if (f64) hipLaunchKernelGGL(k_turbo64<TURBO_CH>, grid, dim3(256), 0, s, J, iters, mode);
+      else hipLaunchKernelGGL(k_turbo<TURBO_CH>, grid, dim3(256), 0, s, J, iters, mode);
+    } else if (ch == 1) {
+      if (f64 && g_logmap) hipLaunchKernelGGL(k_turbo64_logmap<1>, grid, dim3(256), 0, s, J, iters, mode);
+      else if (f64) hipLaunchKernelGGL(k_turbo64<1>, grid, dim3(256), 0, s, J, iters, mode);
+      else hipLaunchKernelGGL(k_turbo<1>, grid, dim3(256), 0, s, J, iters, mode);
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
     const int e = (int)hipGetLastError();
     if (e) return e;
   }
@@ -584,8 +601,8 @@ int launch_turbo_jobs(hipStream_t s, const TurboJob* jobs, int n, int iters, int
 }
 
 int launch_turbo(hipStream_t s, void* blk, void* ckpt, uint32_t* bits, int K, int f1, int f2, int iters, int G,
-                 int mode, int f64) {
-  TurboJob j{blk, ckpt, bits, K, f1, f2, G};
+                 int mode, int f64, int ch) {
+  TurboJob j{blk, ckpt, bits, K, f1, f2, G, ch};
   return launch_turbo_jobs(s, &j, 1, iters, mode, f64);
 }
 

@@ -102,6 +102,10 @@ bool txch_supported(const Grid& g, int n_paths, int max_delay);
 // host payload bits (one uint8 per bit, frames `stride` bytes apart) already on
 // the device -> packed MSB-first words [nf][nwd]
 int launch_pack_bits(hipStream_t s, const uint8_t* bits, int64_t stride, int n_bits, int nwd, int nf, uint32_t* out);
+// the Philox mode's raw streams: per (frame, counter) the 4 outputs of rng4 and
+// the unit normal pairs of gauss2<double> / gauss2<float> (any pointer may be null)
+int launch_philox_draws(hipStream_t s, uint64_t seed, const uint64_t* fid, int nf, uint32_t stream, int64_t n_ctr,
+                        uint32_t* u, double* g64, float* g32);
 // per-OFDM-symbol Taylor sets of the SISO paths from k_fading's phases (the
 // fused TX channel at fD != 0): [B][n_paths][n_sym][mimo_ncf<R>()]
 template <class R>
@@ -151,24 +155,26 @@ int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const 
 // Rate dematch into the decoder rows (rows of R: float / double).  rx_map
 // [n_layers][T]: layer 0 assigns, layers 1.. add in order (E > N_cb
 // repetition, rate_matching.py:433-436).  g0: first 64-frame group.
+// ch: chunk width of the decoder rows (turbo_chunk of their capacity in groups)
 template <class R>
 int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_map, int n_layers, R* const* blk,
-                   const int64_t* rows, int g0 = 0);
+                   const int64_t* rows, int ch, int g0 = 0);
 // dematch with the soft demapper fused in: reads the equalised symbols z
 // ([B][n_re]) and their noise variances ([B][n_grp][nd] per data subcarrier,
 // from the receivers' nv_out mode) instead of LLRs; same decoder rows as
 // launch_dematch (bps 4 / 6)
 template <class R>
 int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int nd, int bps, int B,
-                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int g0 = 0);
+                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int ch, int g0 = 0);
 // f64 != 0: the float64 decoder (bit-exact with the reference), blk / ckpt hold doubles
 int launch_turbo(hipStream_t s, void* blk, void* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
-                 int G, int mode, int f64);
+                 int G, int mode, int f64, int ch);
 struct TurboJob {           // one CB slot of a batch: G groups of 64 code blocks of size K
   void* blk;                // float / double rows (lte_decoder.hip)
   void* ck;
   uint32_t* bits;
   int K, f1, f2, G;
+  int ch;                   // chunk width of blk / ck (turbo_chunk of their capacity); one per launch
 };
 constexpr int TURBO_MAX_JOBS = 16;
 struct TurboJobs {
@@ -357,17 +363,28 @@ constexpr int TURBO_CK_ROWS_F64 = 8;
 __host__ __device__ inline int turbo_ck_rows(int f64) { return f64 ? TURBO_CK_ROWS_F64 : TURBO_CK_ROWS_F32; }
 constexpr int TURBO_RS = 64;   // decoder row stride (elements): 64 code blocks per wave
 // Block arrays (decoder rows, checkpoints) are chunked over frame groups:
-// [chunk][row][TURBO_CH groups][64 lanes], so the rows of TURBO_CH waves that
-// run side by side share DRAM pages and TLB entries (TURBO_CH = 1: one group's
-// block contiguous).  Jobs allocate whole chunks (turbo_galloc).
+// [chunk][row][CH groups][64 lanes], so the rows of CH waves that run side by
+// side share DRAM pages and TLB entries.  CH = TURBO_CH for arrays of at least
+// TURBO_CH groups (which then allocate whole chunks); arrays of fewer groups
+// (small plans, the host entry points) take CH = 1, each group's block
+// contiguous, and allocate exactly their groups (turbo_chunk / turbo_galloc of
+// the array's capacity in groups).  Every launch on an array passes its CH.
 #ifndef LTE_TURBO_CH
 #define LTE_TURBO_CH 32
 #endif
 constexpr int TURBO_CH = LTE_TURBO_CH;
-__host__ __device__ inline int64_t turbo_galloc(int64_t G) { return (G + TURBO_CH - 1) / TURBO_CH * TURBO_CH; }
+__host__ __device__ inline int turbo_chunk(int64_t G) { return G < TURBO_CH ? 1 : TURBO_CH; }
+__host__ __device__ inline int64_t turbo_galloc(int64_t G) {
+  return turbo_chunk(G) == 1 ? G : (G + TURBO_CH - 1) / TURBO_CH * TURBO_CH;
+}
 // element offset of lane 0 of (group g, row) in a block array of `rows` rows per group
+template <int CH = TURBO_CH>
 __host__ __device__ inline int64_t turbo_elem(int64_t rows, int64_t g, int64_t row) {
-  return (((g / TURBO_CH) * rows + row) * TURBO_CH + g % TURBO_CH) * TURBO_RS;
+  return (((g / CH) * rows + row) * CH + g % CH) * TURBO_RS;
+}
+// the same for a runtime chunk width (1 or TURBO_CH)
+__host__ __device__ inline int64_t turbo_elem_ch(int ch, int64_t rows, int64_t g, int64_t row) {
+  return ch == 1 ? turbo_elem<1>(rows, g, row) : turbo_elem<TURBO_CH>(rows, g, row);
 }
 __host__ __device__ inline int turbo_kw(int K) { return (K + 31) / 32; }
 

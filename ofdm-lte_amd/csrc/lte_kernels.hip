@@ -669,6 +669,49 @@ int launch_pack_bits(hipStream_t s, const uint8_t* bits, int64_t stride, int n_b
   return (int)hipGetLastError();
 }
 
+// The Philox mode's raw streams (lte_philox_host): one thread per (frame,
+// counter) -- the four 32-bit outputs of rng4 and the unit normal pairs every
+// noise loader forms from them, (x, y) and (z, w): gauss2<double>
+// (box_muller64t) and gauss2<float> (box_muller).
+__global__ __launch_bounds__(WG) void k_philox_draws(uint64_t seed, const uint64_t* __restrict__ fid, int nf,
+                                                     uint32_t stream, int64_t n_ctr, uint32_t* __restrict__ u,
+                                                     double* __restrict__ g64, float* __restrict__ g32) {
+  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (i >= (int64_t)nf * n_ctr) return;
+  const int f = (int)(i / n_ctr);
+  const uint32_t c = (uint32_t)(i - (int64_t)f * n_ctr);
+  const u32x4 r = rng4(seed, fid[f], stream, c);
+  if (u) {
+    u[4 * i] = r.x;
+    u[4 * i + 1] = r.y;
+    u[4 * i + 2] = r.z;
+    u[4 * i + 3] = r.w;
+  }
+  if (g64) {
+    const double2 a = gauss2<double>(r.x, r.y), b = gauss2<double>(r.z, r.w);
+    g64[4 * i] = a.x;
+    g64[4 * i + 1] = a.y;
+    g64[4 * i + 2] = b.x;
+    g64[4 * i + 3] = b.y;
+  }
+  if (g32) {
+    const float2 a = gauss2<float>(r.x, r.y), b = gauss2<float>(r.z, r.w);
+    g32[4 * i] = a.x;
+    g32[4 * i + 1] = a.y;
+    g32[4 * i + 2] = b.x;
+    g32[4 * i + 3] = b.y;
+  }
+}
+
+int launch_philox_draws(hipStream_t s, uint64_t seed, const uint64_t* fid, int nf, uint32_t stream, int64_t n_ctr,
+                        uint32_t* u, double* g64, float* g32) {
+  const int64_t n = (int64_t)nf * n_ctr;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_philox_draws, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, seed, fid, nf, stream, n_ctr,
+                     u, g64, g32);
+  return (int)hipGetLastError();
+}
+
 // Per-symbol Taylor sets of the SISO paths (fD != 0, the fused TX channel):
 // one thread per (frame, path) from k_fading's 16 phases (jakes_symbol_sets).
 template <class R>

@@ -38,7 +38,7 @@ template <class R>
 __global__ __launch_bounds__(256) void k_dematch(const R* __restrict__ llr, int T, int B,
                                                  const int32_t* __restrict__ rx_map, int add,
                                                  R* const* __restrict__ blk, const int64_t* __restrict__ rows,
-                                                 int g0) {
+                                                 int ch, int g0) {
   __shared__ R tile[64][DM_CH + 1];   // [frame][t], +1: conflict-free column reads
   const int g = g0 + blockIdx.y;
   const int t0 = blockIdx.x * DM_CH;
@@ -64,18 +64,18 @@ __global__ __launch_bounds__(256) void k_dematch(const R* __restrict__ llr, int 
     const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
-    dm_store(&blk[r][turbo_elem(rows[r], g, row) + f], tile[f][c], add != 0);
+    dm_store(&blk[r][turbo_elem_ch(ch, rows[r], g, row) + f], tile[f][c], add != 0);
   }
 }
 
 template <class R>
 int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_map, int n_layers, R* const* blk,
-                   const int64_t* rows, int g0) {
+                   const int64_t* rows, int ch, int g0) {
   const int G = (B + 63) / 64 - g0;   // groups g0 .. ceil(B/64)-1
   if (G < 1 || G > 65535 || n_layers < 1) return (int)hipErrorInvalidValue;
   for (int k = 0; k < n_layers; ++k) {
     hipLaunchKernelGGL(k_dematch<R>, dim3((T + DM_CH - 1) / DM_CH, G), dim3(256), 0, s, llr, T, B,
-                       rx_map + (size_t)k * T, k > 0 ? 1 : 0, blk, rows, g0);
+                       rx_map + (size_t)k * T, k > 0 ? 1 : 0, blk, rows, ch, g0);
     const int e = (int)hipGetLastError();
     if (e) return e;
   }
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
                                                     int nd, int n_nv, int B, const int32_t* __restrict__ rx_map,
                                                     int add,
                                                     R* const* __restrict__ blk, const int64_t* __restrict__ rows,
-                                                    int g0) {
+                                                    int ch, int g0) {
   using V = cx<R>;
   constexpr int DZ_RE = dz_re<R>(), TC = DZ_RE * BPS, PER = 64 * DZ_RE / 256;
   __shared__ R tile[64][TC + 1];
@@ -137,13 +137,13 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
     const int m = rx_map[t0 + c];
     if (m < 0) continue;
     const int r = m >> 24, row = m & 0xFFFFFF;
-    dm_store(&blk[r][turbo_elem(rows[r], g, row) + f], tile[f][c], add != 0);
+    dm_store(&blk[r][turbo_elem_ch(ch, rows[r], g, row) + f], tile[f][c], add != 0);
   }
 }
 
 template <class R>
 int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int nd, int bps, int B,
-                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int g0) {
+                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int ch, int g0) {
   const int G = (B + 63) / 64 - g0;
   if (G < 1 || G > 65535 || (bps != 4 && bps != 6) || n_layers < 1 || nd < 1) return (int)hipErrorInvalidValue;
   const int n_nv = ((n_re / nd + 13) / 14) * nd;   // groups x data subcarriers per frame
@@ -154,10 +154,10 @@ int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int 
     const int32_t* mp = rx_map + (size_t)k * T;
     if (bps == 4)
       hipLaunchKernelGGL((k_dematch_zn<R, 4>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, B, mp, k > 0 ? 1 : 0,
-                         blk, rows, g0);
+                         blk, rows, ch, g0);
     else
       hipLaunchKernelGGL((k_dematch_zn<R, 6>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, B, mp, k > 0 ? 1 : 0,
-                         blk, rows, g0);
+                         blk, rows, ch, g0);
     const int e = (int)hipGetLastError();
     if (e) return e;
   }
@@ -165,13 +165,13 @@ int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int 
 }
 
 template int launch_dematch<float>(hipStream_t, const float*, int, int, const int32_t*, int, float* const*,
-                                   const int64_t*, int);
+                                   const int64_t*, int, int);
 template int launch_dematch<double>(hipStream_t, const double*, int, int, const int32_t*, int, double* const*,
-                                    const int64_t*, int);
+                                    const int64_t*, int, int);
 template int launch_dematch_zn<float>(hipStream_t, const float2*, const float*, int, int, int, int, const int32_t*,
-                                      int, float* const*, const int64_t*, int);
+                                      int, float* const*, const int64_t*, int, int);
 template int launch_dematch_zn<double>(hipStream_t, const double2*, const double*, int, int, int, int,
-                                       const int32_t*, int, double* const*, const int64_t*, int);
+                                       const int32_t*, int, double* const*, const int64_t*, int, int);
 
 // ---------------------------------------------------------------------------
 // Stage entry: rate_dematching_turbo (rate_matching.py:374-489) for any E,

@@ -73,6 +73,8 @@ _SIGS = {
     'lte_fft_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float)]),
     'lte_fft_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(c_f64), P(c_f64)]),
     'lte_pilots': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P(c_f64)]),
+    'lte_philox_host': (ctypes.c_int, [c_u64, ctypes.c_int, P(c_u64), ctypes.c_uint32, c_i64, P(ctypes.c_uint32),
+                                       P(c_f64), P(ctypes.c_float)]),
     'lte_dft_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float)]),
     'lte_dft_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(c_f64), P(c_f64)]),
     'lte_llr_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_float), P(ctypes.c_float)]),
@@ -212,6 +214,22 @@ def pilots(cell_id, n):
     out = np.empty(2 * n, dtype=np.float64)
     check(load().lte_pilots(cell_id, n, ptr(out, F64)))
     return out[0::2] + 1j * out[1::2]
+
+
+def philox(seed, frame_ids, stream, n_ctr):
+    """The Philox mode's device streams (lte_philox_host): per frame and
+    counter the four 32-bit outputs [nf, n_ctr, 4] uint32 and the unit normal
+    pairs the noise kernels form from them, float64 and float32 [nf, n_ctr, 4]
+    (re / im of the (x, y) pair, then of the (z, w) pair)."""
+    device_init()
+    fid = np.ascontiguousarray(np.atleast_1d(frame_ids), dtype=np.uint64)
+    nf, n_ctr = len(fid), int(n_ctr)
+    u = np.empty((nf, n_ctr, 4), dtype=np.uint32)
+    g64 = np.empty((nf, n_ctr, 4), dtype=np.float64)
+    g32 = np.empty((nf, n_ctr, 4), dtype=np.float32)
+    check(load().lte_philox_host(int(seed) & 0xFFFFFFFFFFFFFFFF, nf, ptr(fid, U64), int(stream), n_ctr, ptr(u, U32),
+                                 ptr(g64, F64), ptr(g32, F32)))
+    return u, g64, g32
 
 
 def rate_dematch_map(K, E, rv_idx=0):

@@ -108,9 +108,13 @@ def test_bench_self_launches_ranks_dry_run():
     cpu = out['cpu_baseline']
     assert cpu and cpu['value'] > 0 and cpu['cores'] >= 1 and cpu['kind'] == 'port'
     roof = out['roofline']
-    assert roof['bound'] in ('hbm', 'valu') and roof['unit'] == 'GB/s' and roof['peak'] == 8000.0
-    for k in ('achieved', 'frac', 'traffic', 'alg_bytes_per_launch', 'avg_launch_ms', 'valu', 'stage_bytes'):
+    # SURVEY §8(d)'s K7 roofline (VALU) with the HBM row-stream view beside it
+    assert roof['bound'] == 'valu' and roof['unit'] == 'Top/s' and roof['peak'] == 39.32
+    for k in ('achieved', 'frac', 'traffic', 'avg_launch_ms', 'hbm_row_stream', 'stage_bytes', 'measured_limiter'):
         assert k in roof, k
+    assert roof['hbm_row_stream']['peak_GBs'] == 8000.0 and 'store_cost' in roof['hbm_row_stream']
+    # the BER-match sample comes from the CPU baseline's oracle frames; no device here
+    assert out['ber_match'] is None and 'frames' not in cpu
     # rank 1's synthetic timer is 1 % slower: the merged timer is the max
     assert abs(roof['avg_launch_ms'] - 0.8 * out['ms_per_step'] * 1.01) < 0.05 * out['ms_per_step']
 

@@ -8,7 +8,10 @@ out exactly as it does in a small batch:
   in a 64-frame plan -- the last frames sit past 2^31 bytes in every per-frame
   buffer (the received streams alone are 32 GB), so 32-bit offset arithmetic
   anywhere on the path shows up here;
-* the SNR curve: BER falls over 0:2:30 dB and the top of the curve decodes.
+* the SNR curve: BER falls over 0:2:30 dB and the top of the curve decodes;
+* f64: those 64 frames (bench step 7's first and last 32) re-run by the oracle
+  on its restatement of the device's Philox draws (oracle/philox.py) give the
+  same bit errors and block errors frame by frame.
 """
 import numpy as np
 import pytest
@@ -54,6 +57,13 @@ def test_bench_size_batch_invariance(C, prec):
     ref = small.run(snr[sel], snr_index=np.arange(64, dtype=np.int32), n_snr=64, seed=0x5EED,
                     frame_ids=ids[sel])['counts']
     assert np.array_equal(per_frame[sel], ref)
+    if prec == 'f64':
+        # the same frames through the float64 oracle on its Philox restatement
+        # (oracle/philox.py): identical bit errors and block verdicts
+        from oracle import philox as P
+        orc = np.array([P.config2_frame(int(f)) for f in ids[sel]])
+        assert np.array_equal(per_frame[sel, 0], orc[:, 0])
+        assert np.array_equal(per_frame[sel, 2], 1 - orc[:, 1])
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])

@@ -56,9 +56,12 @@ enum { LTE_DET_MMSE = 0, LTE_DET_ZF = 1, LTE_DET_SIC = 2, LTE_DET_MRC = 3 };
 enum { LTE_CH_AWGN = 0, LTE_CH_RAYLEIGH = 1 }; /* core/channel.py:10-245 */
 
 /* Arithmetic type of a plan's signal chain and turbo decoder.  DEFAULT =
- * float64 for the SISO / SIMO chains (uncoded, coded, MRC: the reference
- * computes in float64 / complex128 throughout) and float32 for the
- * multi-antenna and beamforming chains, which have no float64 path. */
+ * float64 for every chain (the reference computes in float64 / complex128
+ * throughout); F32 is the opt-in fast mode.  ABI version 2 (lte_version):
+ * in version 1 DEFAULT meant float32 for the multi-antenna and beamforming
+ * chains -- their real / complex captures and in_signal are now float64 /
+ * complex128 unless LTE_PREC_F32 is asked for ("ABI
+ * versions"). */
 enum { LTE_PREC_DEFAULT = 0, LTE_PREC_F32 = 32, LTE_PREC_F64 = 64 };
 
 #define LTE_MAX_PATHS 16
@@ -172,7 +175,7 @@ typedef struct {
 const char *lte_strerror(int code);
 const char *lte_last_error(void);
 int lte_device_init(int device);            /* select + check gfx950 */
-int lte_version(void);
+int lte_version(void);                     /* ABI version: 2 */
 
 /* Plans. */
 int lte_plan_create(const lte_plan_desc *desc, lte_plan **out);

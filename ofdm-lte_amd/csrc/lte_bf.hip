@@ -10,6 +10,10 @@
 //   k_bf_setup  one thread per frame: H, PMI, W, H_eff, gain (float64 math)
 //   k_bf_data   one thread per (frame, OFDM symbol, data RE): QAM map,
 //               precode, channel, noise, MRC, slice, bit errors
+// Both are templated on the chain's arithmetic R: double (the default, the
+// reference's complex128, with NumPy's own forms where they are cheap:
+// |.| as hypot, complex / real as a multiply by the reciprocal, noise
+// (z_re, z_im) * sqrt(s2 / 2) with s2 = 10^(-SNR/10)) or float (fast mode).
 #include "lte_common.h"
 #include "lte_internal.h"
 #include "lte_dev.h"
@@ -18,27 +22,42 @@ namespace lte {
 
 constexpr int BWG = 256;
 
+// |z|^2 as the reference forms it: np.abs (hypot) squared
+__device__ __forceinline__ double abs2_np(double2 z) {
+  const double a = hypot(z.x, z.y);
+  return a * a;
+}
+
+template <class R>
 __global__ __launch_bounds__(BWG) void k_bf_setup(int B, int num_tx, int num_rx, int adaptive, int ncb,
                                                   const double* __restrict__ cb, const uint64_t* __restrict__ fid,
-                                                  uint64_t seed, const float* __restrict__ inj_h, int64_t inj_stride,
-                                                  BfFrame* __restrict__ fr) {
+                                                  uint64_t seed, const R* __restrict__ inj_h, int64_t inj_stride,
+                                                  BfFrameT<R>* __restrict__ fr) {
+  constexpr bool F64 = sizeof(R) == 8;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  BfFrame* f = fr + b;
+  BfFrameT<R>* f = fr + b;
   // H = (randn + j randn) / sqrt(2) (core/ofdm_core.py:2345-2346): injected or Philox
+  double2 H[LTE_BF_MAX_RX][LTE_BF_MAX_TX];
   for (int r = 0; r < num_rx; ++r)
     for (int t = 0; t < num_tx; ++t) {
       const int link = r * num_tx + t;
-      float2 h;
+      double2 h;
       if (inj_h) {
-        const float* p = inj_h + (size_t)b * inj_stride + (size_t)link * 2;
-        h = make_float2(p[0], p[1]);
+        const R* p = inj_h + (size_t)b * inj_stride + (size_t)link * 2;
+        h = make_double2((double)p[0], (double)p[1]);
       } else {
         const u32x4 v = rng4(seed, fid[b], RNG_STREAM_BF + (uint32_t)link, 0u);
-        const float2 z = box_muller(v.x, v.y);
-        h = make_float2(z.x * 0.70710678118654752f, z.y * 0.70710678118654752f);
+        if constexpr (F64) {   // complex / np.sqrt(2): NumPy multiplies by the reciprocal
+          const double2 z = gauss2<double>(v.x, v.y);
+          h = make_double2(z.x * 0.7071067811865475, z.y * 0.7071067811865475);
+        } else {
+          const float2 z = box_muller(v.x, v.y);
+          h = make_double2(z.x * 0.70710678118654752f, z.y * 0.70710678118654752f);
+        }
       }
-      f->H[r][t] = h;
+      H[r][t] = h;
+      f->H[r][t] = mkc((R)h.x, (R)h.y);
     }
   // PMI: first codebook vector with the largest ||H w||^2 (LTECodebook.select_best_pmi)
   int pmi = 0;
@@ -48,24 +67,25 @@ __global__ __launch_bounds__(BWG) void k_bf_setup(int B, int num_tx, int num_rx,
     for (int r = 0; r < num_rx; ++r) {
       double er = 0.0, ei = 0.0;
       for (int t = 0; t < num_tx; ++t) {
-        const double hr = f->H[r][t].x, hi = f->H[r][t].y;
+        const double hr = H[r][t].x, hi = H[r][t].y;
         const double wr = cb[((size_t)i * num_tx + t) * 2], wi = cb[((size_t)i * num_tx + t) * 2 + 1];
         er += hr * wr - hi * wi;
         ei += hr * wi + hi * wr;
       }
-      m += er * er + ei * ei;
+      m += F64 ? abs2_np(make_double2(er, ei)) : er * er + ei * ei;
     }
     if (m > best) { best = m; pmi = i; }
   }
   double wr[LTE_BF_MAX_TX], wi[LTE_BF_MAX_TX];
-  if (adaptive) {   // MRT: conj(mean over RX of H) / ||.||
+  if (adaptive) {   // MRT: conj(np.mean(H, axis=0)) / sqrt(sum |.|^2)
+    const double inv_rx = 1.0 / (double)num_rx;   // complex / count: the reciprocal (exact for 1, 2, 4, 8)
     double nrm = 0.0;
     for (int t = 0; t < num_tx; ++t) {
       double ar = 0.0, ai = 0.0;
-      for (int r = 0; r < num_rx; ++r) { ar += f->H[r][t].x; ai += f->H[r][t].y; }
-      wr[t] = ar / num_rx;
-      wi[t] = -ai / num_rx;
-      nrm += wr[t] * wr[t] + wi[t] * wi[t];
+      for (int r = 0; r < num_rx; ++r) { ar += H[r][t].x; ai += H[r][t].y; }
+      wr[t] = F64 ? ar * inv_rx : ar / num_rx;
+      wi[t] = F64 ? -(ai * inv_rx) : -ai / num_rx;
+      nrm += F64 ? abs2_np(make_double2(wr[t], wi[t])) : wr[t] * wr[t] + wi[t] * wi[t];
     }
     const double s = 1.0 / sqrt(nrm);
     for (int t = 0; t < num_tx; ++t) { wr[t] *= s; wi[t] *= s; }
@@ -79,60 +99,62 @@ __global__ __launch_bounds__(BWG) void k_bf_setup(int B, int num_tx, int num_rx,
   for (int r = 0; r < num_rx; ++r) {
     double er = 0.0, ei = 0.0;
     for (int t = 0; t < num_tx; ++t) {
-      const double hr = f->H[r][t].x, hi = f->H[r][t].y;
+      const double hr = H[r][t].x, hi = H[r][t].y;
       er += hr * wr[t] - hi * wi[t];
       ei += hr * wi[t] + hi * wr[t];
-      ph += hr * hr + hi * hi;
+      ph += F64 ? abs2_np(H[r][t]) : hr * hr + hi * hi;
     }
-    f->He[r] = make_float2((float)er, (float)ei);
-    pe += er * er + ei * ei;
+    f->He[r] = mkc((R)er, (R)ei);
+    pe += F64 ? abs2_np(make_double2(er, ei)) : er * er + ei * ei;
   }
-  for (int t = 0; t < num_tx; ++t) f->W[t] = make_float2((float)wr[t], (float)wi[t]);
-  f->inv_p = (float)(1.0 / pe);
+  for (int t = 0; t < num_tx; ++t) f->W[t] = mkc((R)wr[t], (R)wi[t]);
+  f->inv_p = (R)(1.0 / pe);   // comb / np.sum(|He|^2): NumPy multiplies by the reciprocal
   f->pmi = pmi;
   // BeamformingPrecoder.calculate_beamforming_gain: only the adaptive precoder holds W
   f->gain_db = adaptive ? (float)(10.0 * log10(pe / (ph / num_tx))) : 0.0f;
 }
 
-template <int BPS>
+template <class R, int BPS>
 __global__ __launch_bounds__(BWG) void k_bf_data(int B, int n_sym, int Nd, int num_tx, int num_rx,
-                                                 const BfFrame* __restrict__ fr, const float* __restrict__ snr_lin,
+                                                 const BfFrameT<R>* __restrict__ fr, const R* __restrict__ sigma,
                                                  const uint32_t* __restrict__ pw, int PW, int n_bits,
                                                  const uint64_t* __restrict__ fid, uint64_t seed,
-                                                 const float* __restrict__ inj_z, int64_t inj_stride,
-                                                 uint32_t* __restrict__ frame_err, float2* __restrict__ cap_syms,
+                                                 const R* __restrict__ inj_z, int64_t inj_stride,
+                                                 uint32_t* __restrict__ frame_err, cx<R>* __restrict__ cap_syms,
                                                  uint8_t* __restrict__ cap_bits) {
+  using V = cx<R>;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t per = (int64_t)n_sym * Nd;
   const bool act = i < (int64_t)B * per;       // tail lanes stay for the wave-level error reduction
   const int b = act ? (int)(i / per) : B - 1;
   const int n = act ? (int)(i - (int64_t)b * per) : 0;     // RE index within the frame (l * Nd + j)
-  const BfFrame* f = fr + b;
+  const BfFrameT<R>* f = fr + b;
   const uint32_t* fb = pw + (size_t)b * PW;
   int idx = 0;
 #pragma unroll
   for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, (int64_t)n * BPS + m);
-  const float2 s = qam_point<BPS>(idx);
-  const float sigma = sqrtf(0.5f / snr_lin[b]);
+  const V s = qam_point<BPS, R>(idx);
+  const R sg = sigma[b];
   const int L = n_sym * Nd;
-  float2 acc = make_float2(0.f, 0.f);
+  V acc = mkc((R)0, (R)0);
   for (int r = 0; r < num_rx; ++r) {
-    float2 y = make_float2(0.f, 0.f);
+    // y[r] += H[r, t] * x[t], x = W s (W @ d: one product per element)
+    V y = mkc((R)0, (R)0);
     for (int t = 0; t < num_tx; ++t) y = cadd(y, cmul(f->H[r][t], cmul(f->W[t], s)));
-    float2 z;
+    V z;
     if (inj_z) {
-      const float* zf = inj_z + (size_t)b * inj_stride + (size_t)r * 2 * L;
-      z = make_float2(zf[n], zf[L + n]);
+      const R* zf = inj_z + (size_t)b * inj_stride + (size_t)r * 2 * L;
+      z = mkc(zf[n], zf[L + n]);
     } else {
       const u32x4 v = rng4(seed, fid[b], RNG_STREAM_NOISE + (uint32_t)r, (uint32_t)(n >> 1));
-      z = (n & 1) ? box_muller(v.z, v.w) : box_muller(v.x, v.y);
+      z = (n & 1) ? gauss2<R>(v.z, v.w) : gauss2<R>(v.x, v.y);
     }
-    y = make_float2(y.x + sigma * z.x, y.y + sigma * z.y);
+    y = mkc(y.x + z.x * sg, y.y + z.y * sg);
     acc = cadd(acc, cmulc(y, f->He[r]));     // conj(He_r) y_r
   }
-  const float2 c = make_float2(acc.x * f->inv_p, acc.y * f->inv_p);
+  const V c = cscale(acc, f->inv_p);
   if (act && cap_syms) cap_syms[(size_t)b * per + n] = c;
-  const int hidx = hard_index(c, BPS, (float)qam_norm<BPS>());
+  const int hidx = hard_index(c, BPS, (R)qam_norm<BPS>());
   uint32_t errs = 0;
 #pragma unroll
   for (int m = 0; m < BPS; ++m) {
@@ -146,21 +168,29 @@ __global__ __launch_bounds__(BWG) void k_bf_data(int B, int n_sym, int Nd, int n
   frame_err_add(frame_err, b, errs);
 }
 
+template <class R>
 int launch_bf(hipStream_t s, int B, int n_sym, int Nd, int bps, int num_tx, int num_rx, int adaptive, int ncb,
-              const double* cb, const uint64_t* fid, uint64_t seed, const float* inj_h, int64_t inj_h_stride,
-              BfFrame* fr, const float* snr_lin, const uint32_t* pw, int PW, int n_bits, const float* inj_z,
-              int64_t inj_z_stride, uint32_t* frame_err, float2* cap_syms, uint8_t* cap_bits) {
+              const double* cb, const uint64_t* fid, uint64_t seed, const R* inj_h, int64_t inj_h_stride,
+              BfFrameT<R>* fr, const R* sigma, const uint32_t* pw, int PW, int n_bits, const R* inj_z,
+              int64_t inj_z_stride, uint32_t* frame_err, cx<R>* cap_syms, uint8_t* cap_bits) {
   if (num_tx < 1 || num_tx > LTE_BF_MAX_TX || num_rx < 1 || num_rx > LTE_BF_MAX_RX) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bf_setup, dim3((B + BWG - 1) / BWG), dim3(BWG), 0, s, B, num_tx, num_rx, adaptive, ncb, cb,
+  hipLaunchKernelGGL(k_bf_setup<R>, dim3((B + BWG - 1) / BWG), dim3(BWG), 0, s, B, num_tx, num_rx, adaptive, ncb, cb,
                      fid, seed, inj_h, inj_h_stride, fr);
   const int64_t n = (int64_t)B * n_sym * Nd;
   const dim3 grid((unsigned)((n + BWG - 1) / BWG));
 #define LTE_BFD(B_)                                                                                                \
-  hipLaunchKernelGGL(k_bf_data<B_>, grid, dim3(BWG), 0, s, B, n_sym, Nd, num_tx, num_rx, fr, snr_lin, pw, PW,     \
+  hipLaunchKernelGGL((k_bf_data<R, B_>), grid, dim3(BWG), 0, s, B, n_sym, Nd, num_tx, num_rx, fr, sigma, pw, PW,  \
                      n_bits, fid, seed, inj_z, inj_z_stride, frame_err, cap_syms, cap_bits)
   if (bps == 2) LTE_BFD(2); else if (bps == 4) LTE_BFD(4); else LTE_BFD(6);
 #undef LTE_BFD
   return (int)hipGetLastError();
 }
+
+template int launch_bf<float>(hipStream_t, int, int, int, int, int, int, int, int, const double*, const uint64_t*,
+                              uint64_t, const float*, int64_t, BfFrameT<float>*, const float*, const uint32_t*, int,
+                              int, const float*, int64_t, uint32_t*, float2*, uint8_t*);
+template int launch_bf<double>(hipStream_t, int, int, int, int, int, int, int, int, const double*, const uint64_t*,
+                               uint64_t, const double*, int64_t, BfFrameT<double>*, const double*, const uint32_t*,
+                               int, int, const double*, int64_t, uint32_t*, double2*, uint8_t*);
 
 }  // namespace lte

@@ -444,13 +444,14 @@ struct lte_plan {
   bool bf = false;
   int bf_ncb = 0;
   DBuf<double> bf_cb;
-  DBuf<BfFrame> bf_fr;
+  DBuf<BfFrameT<float>> bf_fr;
+  DBuf<BfFrameT<double>> bf_fr64;
   int res = 0;                       // QAM symbols per OFDM symbol (= Nd for SISO / SIMO)
   MimoGrid mg{};
   DBuf<int32_t> m_np, m_ppos, m_pseg;
   DBuf<float2> m_pval;
   DBuf<double2> m_pval64;
-  DBuf<float> m_pig, inj_lh;
+  DBuf<float> m_pig;
   DBuf<double> m_pig64, m_W;
   // timing
   bool timing = false;
@@ -486,6 +487,9 @@ struct Timer {  // brackets one launch with events when timing is on
 };
 
 template <class R> ChainBufs<R>& cbuf(lte_plan* p);
+template <class R> BfFrameT<R>* bf_frames(lte_plan* p);
+template <> BfFrameT<float>* bf_frames<float>(lte_plan* p) { return p->bf_fr.p; }
+template <> BfFrameT<double>* bf_frames<double>(lte_plan* p) { return p->bf_fr64.p; }
 template <> ChainBufs<float>& cbuf<float>(lte_plan* p) { return p->c32; }
 template <> ChainBufs<double>& cbuf<double>(lte_plan* p) { return p->c64; }
 
@@ -507,7 +511,7 @@ void collect_timing(lte_plan* p) {
 
 extern "C" {
 
-int lte_version(void) { return 1; }
+int lte_version(void) { return 2; }   // 2: LTE_PREC_DEFAULT is float64 for every chain
 
 const char* lte_last_error(void) { return g_err.c_str(); }
 
@@ -1161,18 +1165,19 @@ static int plan_alloc(lte_plan* p) {
   const lte_plan_desc& d = p->d;
   const size_t B = (size_t)d.max_frames;
   const int G = (int)((B + 63) / 64);
-  const int rx = d.num_rx;
   const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
   bool bad = false;
   bad |= p->pw.alloc(B * p->PW) != 0;
   if (p->mimo) {
     bad |= !(p->f64 ? alloc_mimo<double>(p, coded) : alloc_mimo<float>(p, coded));
-  } else if (p->bf) {   // float32 chain
-    ChainBufs<float>& c = p->c32;
-    bad |= p->bf_fr.alloc(B) != 0;
-    bad |= c.pow_part.alloc(B * rx * p->nblk) != 0;
-    bad |= c.npow.alloc(B * rx) != 0;
-    bad |= c.snr_lin.alloc(B) != 0;
+  } else if (p->bf) {   // per frame: the BfFrameT state and the noise scale (in snr_lin)
+    if (p->f64) {
+      bad |= p->bf_fr64.alloc(B) != 0;
+      bad |= p->c64.snr_lin.alloc(B) != 0;
+    } else {
+      bad |= p->bf_fr.alloc(B) != 0;
+      bad |= p->c32.snr_lin.alloc(B) != 0;
+    }
   } else {
     bad |= !(p->f64 ? alloc_siso<double>(p, coded) : alloc_siso<float>(p, coded));
   }
@@ -1237,15 +1242,12 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
   if (d.n_bits < 1) return fail(LTE_EINVAL, "Bits array cannot be empty");
   if (d.precision != LTE_PREC_DEFAULT && d.precision != LTE_PREC_F32 && d.precision != LTE_PREC_F64)
     return fail(LTE_EINVAL, "precision must be LTE_PREC_DEFAULT, LTE_PREC_F32 or LTE_PREC_F64");
-  // float64 (the reference's arithmetic) is the default of every chain but
-  // beamforming, which computes in float32
-  if (bf && d.precision == LTE_PREC_F64)
-    return fail(LTE_EUNSUP, "the beamforming chain computes in float32 (LTE_PREC_F32)");
+  // float64 (the reference's arithmetic) is the default of every chain
   lte_plan* p = new lte_plan();
   p->d = d;
   p->d.num_tx = num_tx;
   p->mimo = mimo;
-  p->f64 = !bf && d.precision != LTE_PREC_F32;
+  p->f64 = d.precision != LTE_PREC_F32;
   const bool coded = d.chain == LTE_CHAIN_CODED || d.chain == LTE_CHAIN_SFBC_CODED;
   if (coded && d.turbo_iters < 0) { delete p; return fail(LTE_EINVAL, "bad turbo_iters"); }
   int rc = plan_tables(p);
@@ -1359,8 +1361,9 @@ int lte_plan_destroy(lte_plan* p) {
   for (auto& b : p->decb) b.release();
   p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
   p->m_np.release(); p->m_ppos.release(); p->m_pseg.release(); p->m_pval.release(); p->m_pval64.release();
-  p->m_pig.release(); p->m_pig64.release(); p->inj_lh.release(); p->m_W.release(); p->bf_cb.release();
+  p->m_pig.release(); p->m_pig64.release(); p->m_W.release(); p->bf_cb.release();
   p->bf_fr.release();
+  p->bf_fr64.release();
   for (auto e : p->evpool) (void)hipEventDestroy(e);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -1618,34 +1621,41 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
 
 extern "C" {
 
-// Beamforming chain (frequency domain, flat H per frame).
-static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const uint32_t* inj_bits,
-                  int64_t inj_bits_stride, const float* inj_z, int64_t inj_z_stride) {
+}  // extern "C"
+
+// Beamforming chain (frequency domain, flat H per frame), R = double (the
+// default) / float.  sig: the per-frame noise scale sqrt(10^(-SNR/10) / 2).
+template <class R>
+static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const std::vector<double>& sig,
+                  const uint32_t* inj_bits, int64_t inj_bits_stride) {
   const lte_plan_desc& d = p->d;
   hipStream_t s = p->stream;
+  ChainBufs<R>& c = cbuf<R>(p);
+  BfFrameT<R>* frd = bf_frames<R>(p);
   const size_t links = (size_t)d.num_rx * d.num_tx;
-  const float* inj_h = nullptr;
-  int64_t inj_h_stride = 0;
+  std::vector<R> sg(B);
+  for (int b = 0; b < B; ++b) sg[b] = (R)sig[b];
+  HIPCHK(hipMemcpyAsync(c.snr_lin.p, sg.data(), B * sizeof(R), hipMemcpyHostToDevice, s));
+  const R *inj_h = nullptr, *inj_z = nullptr;
+  int64_t inj_h_stride = 0, inj_z_stride = 0;
   if (a->link_h) {
-    const int nf = a->link_h_stride ? B : 1;
-    std::vector<float> hh((size_t)nf * links * 2);
-    for (int f = 0; f < nf; ++f)
-      for (size_t i = 0; i < links * 2; ++i) hh[f * links * 2 + i] = (float)a->link_h[(size_t)f * a->link_h_stride + i];
-    if (p->inj_lh.alloc(hh.size())) return fail(LTE_ENOMEM, "inj channel");
-    HIPCHK(hipMemcpyAsync(p->inj_lh.p, hh.data(), hh.size() * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
-    inj_h = p->inj_lh.p;
-    inj_h_stride = a->link_h_stride ? (int64_t)links * 2 : 0;
+    const int e = upload_inj<R>(c.inj_lh, a->link_h, a->link_h_stride, B, links * 2, s, &inj_h, &inj_h_stride);
+    if (e != LTE_OK) return e;
+  }
+  if (a->noise) {
+    const int e = upload_inj<R>(c.inj_z, a->noise, a->noise_stride, B, (size_t)d.num_rx * 2 * p->L, s, &inj_z,
+                                &inj_z_stride);
+    if (e != LTE_OK) return e;
   }
   {
     Timer t(p, KN_PAYLOAD);
     LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
   }
-  float2* cap_syms_dev = nullptr;
+  cx<R>* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
   if (a->cap_data_syms) {
-    if (p->c32.capbuf.alloc((size_t)B * p->L)) return fail(LTE_ENOMEM, "capture");
-    cap_syms_dev = p->c32.capbuf.p;
+    if (c.capbuf.alloc((size_t)B * p->L)) return fail(LTE_ENOMEM, "capture");
+    cap_syms_dev = c.capbuf.p;
   }
   if (a->cap_bits_rx) {
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
@@ -1653,9 +1663,9 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   }
   {
     Timer t(p, KN_RX_DATA);
-    LCHK(launch_bf(s, B, p->n_sym, p->Nd, d.bps, d.num_tx, d.num_rx, d.bf_adaptive, p->bf_ncb, p->bf_cb.p, p->fid.p,
-                   a->seed, inj_h, inj_h_stride, p->bf_fr.p, p->c32.snr_lin.p, p->pw.p, p->PW, d.n_bits, inj_z,
-                   inj_z_stride, p->frame_err.p, cap_syms_dev, cap_bits_dev));
+    LCHK(launch_bf<R>(s, B, p->n_sym, p->Nd, d.bps, d.num_tx, d.num_rx, d.bf_adaptive, p->bf_ncb, p->bf_cb.p,
+                      p->fid.p, a->seed, inj_h, inj_h_stride, frd, c.snr_lin.p, p->pw.p, p->PW, d.n_bits, inj_z,
+                      inj_z_stride, p->frame_err.p, cap_syms_dev, cap_bits_dev));
   }
   {
     Timer t(p, KN_ACC);
@@ -1666,21 +1676,21 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   if (a->frame_errors)
     HIPCHK(hipMemcpyAsync(a->frame_errors, p->frame_err.p, B * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (a->cap_data_syms)
-    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->L * sizeof(float2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(a->cap_data_syms, cap_syms_dev, (size_t)B * p->L * sizeof(cx<R>), hipMemcpyDeviceToHost, s));
   if (a->cap_bits_rx)
     HIPCHK(hipMemcpyAsync(a->cap_bits_rx, cap_bits_dev, (size_t)B * d.n_bits, hipMemcpyDeviceToHost, s));
-  std::vector<BfFrame> fr;
+  std::vector<BfFrameT<R>> fr;
   if (a->cap_H || a->cap_pmi || a->cap_bf_gain) {
     fr.resize(B);
-    HIPCHK(hipMemcpyAsync(fr.data(), p->bf_fr.p, B * sizeof(BfFrame), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(fr.data(), frd, B * sizeof(BfFrameT<R>), hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
   if (p->timing) collect_timing(p);
   for (int b = 0; b < (int)fr.size(); ++b) {
-    if (a->cap_H)
+    if (a->cap_H)   // [n_frames][num_rx][num_tx] complex in the plan's type
       for (int r = 0; r < d.num_rx; ++r)
         for (int t = 0; t < d.num_tx; ++t) {
-          float* o = static_cast<float*>(a->cap_H) + (((size_t)b * d.num_rx + r) * d.num_tx + t) * 2;
+          R* o = static_cast<R*>(a->cap_H) + (((size_t)b * d.num_rx + r) * d.num_tx + t) * 2;
           o[0] = fr[b].H[r][t].x;
           o[1] = fr[b].H[r][t].y;
         }
@@ -1692,7 +1702,7 @@ static int run_bf(lte_plan* p, const lte_run_args* a, int B, int n_snr, const ui
   return LTE_OK;
 }
 
-}  // extern "C"
+
 
 // TX with the channel fused in (TxChannelT): SISO / SIMO Rayleigh (SC-FDM
 // precoding included), delays within the CP, no TX / RX stream capture; static
@@ -2018,7 +2028,6 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (B < 1 || B > d.max_frames) return fail(LTE_EINVAL, "n_frames out of range (1..max_frames)");
   if (!a->snr_db) return fail(LTE_EINVAL, "snr_db required");
   const int n_snr = std::max(1, a->n_snr);
-  const int rx = d.num_rx;
   hipStream_t s = p->stream;
   if (p->counts.alloc((size_t)4 * n_snr)) return fail(LTE_ENOMEM, "counts");
   // per-frame parameters
@@ -2065,19 +2074,12 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   if (p->mimo)
     return p->f64 ? run_mimo<double>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride)
                   : run_mimo<float>(p, a, B, n_snr, sl, inj_bits, inj_bits_stride);
-  // beamforming chain: float32
-  ChainBufs<float>& c = p->c32;
-  std::vector<float> slf(B);
-  for (int b = 0; b < B; ++b) slf[b] = (float)sl[b];
-  HIPCHK(hipMemcpyAsync(c.snr_lin.p, slf.data(), B * sizeof(float), hipMemcpyHostToDevice, s));
-  const float* inj_z = nullptr;
-  int64_t inj_z_stride = 0;
-  if (a->noise) {
-    const int e = upload_inj<float>(c.inj_z, a->noise, a->noise_stride, B, (size_t)rx * 2 * p->L, s, &inj_z,
-                                    &inj_z_stride);
-    if (e != LTE_OK) return e;
-  }
-  return run_bf(p, a, B, n_snr, inj_bits, inj_bits_stride, inj_z, inj_z_stride);
+  // beamforming chain: noise scale sqrt(noise_variance / 2), noise_variance =
+  // 10 ** (-snr_db / 10) (core/ofdm_core.py:2397-2399)
+  std::vector<double> sig(B);
+  for (int b = 0; b < B; ++b) sig[b] = std::sqrt(std::pow(10.0, -(double)a->snr_db[b] / 10.0) / 2.0);
+  return p->f64 ? run_bf<double>(p, a, B, n_snr, sig, inj_bits, inj_bits_stride)
+                : run_bf<float>(p, a, B, n_snr, sig, inj_bits, inj_bits_stride);
 }
 
 // ------------------------------------------------------------------ stage entry points

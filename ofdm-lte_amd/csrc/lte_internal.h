@@ -305,19 +305,23 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
 
 // ---------------------------------------------------------------- beamforming (lte_bf.hip)
 constexpr int LTE_BF_MAX_TX = 8, LTE_BF_MAX_RX = 8;
-struct BfFrame {              // per frame: channel, precoder, effective channel, 1/||H_eff||^2, PMI, gain
-  float2 H[LTE_BF_MAX_RX][LTE_BF_MAX_TX];
-  float2 W[LTE_BF_MAX_TX];
-  float2 He[LTE_BF_MAX_RX];
-  float inv_p;
+// per frame: channel, precoder, effective channel, 1/||H_eff||^2, PMI, gain;
+// R = double (the default) / float (fast mode)
+template <class R>
+struct BfFrameT {
+  cx<R> H[LTE_BF_MAX_RX][LTE_BF_MAX_TX];
+  cx<R> W[LTE_BF_MAX_TX];
+  cx<R> He[LTE_BF_MAX_RX];
+  R inv_p;
   int pmi;
   float gain_db;
-  int pad;
 };
+// sigma: per frame noise scale sqrt(10^(-SNR/10) / 2) (core/ofdm_core.py:2397-2399)
+template <class R>
 int launch_bf(hipStream_t s, int B, int n_sym, int Nd, int bps, int num_tx, int num_rx, int adaptive, int ncb,
-              const double* cb, const uint64_t* fid, uint64_t seed, const float* inj_h, int64_t inj_h_stride,
-              BfFrame* fr, const float* snr_lin, const uint32_t* pw, int PW, int n_bits, const float* inj_z,
-              int64_t inj_z_stride, uint32_t* frame_err, float2* cap_syms, uint8_t* cap_bits);
+              const double* cb, const uint64_t* fid, uint64_t seed, const R* inj_h, int64_t inj_h_stride,
+              BfFrameT<R>* fr, const R* sigma, const uint32_t* pw, int PW, int n_bits, const R* inj_z,
+              int64_t inj_z_stride, uint32_t* frame_err, cx<R>* cap_syms, uint8_t* cap_bits);
 
 // turbo modes
 enum { TM_DEC1 = 0, TM_DEC2 = 1, TM_DECODE = 2, TM_APP = 3, TM_FINAL = 4 };  // TM_DECODE: full decode (iterations + decisions)

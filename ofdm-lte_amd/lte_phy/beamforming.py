@@ -149,11 +149,11 @@ class CSIFeedback:
                 'pmi_distribution': np.bincount(self.pmi_history, minlength=self.codebook.codebook_size)}
 
 
-def bf_plan(config, n_sym, n_bits, num_tx, num_rx, adaptive, max_frames=1):
+def bf_plan(config, n_sym, n_bits, num_tx, num_rx, adaptive, max_frames=1, precision=None):
     from .engine import get_plan
     return get_plan(N=config.N, Nc=config.Nc, cp_len=config.cp_length, bps=config.bits_per_symbol, n_sym=n_sym,
                     chain=C.CHAIN_BEAMFORMING, channel=C.CH_AWGN, num_rx=num_rx, num_tx=num_tx, n_bits=n_bits,
-                    max_frames=max_frames, bf_adaptive=int(adaptive))
+                    max_frames=max_frames, bf_adaptive=int(adaptive), precision=precision)
 
 
 def simulate_beamforming(sim, bits, snr_db=10.0, num_tx=2, num_rx=1, codebook_type='TM6', velocity_kmh=3.0,
@@ -174,7 +174,7 @@ def simulate_beamforming(sim, bits, snr_db=10.0, num_tx=2, num_rx=1, codebook_ty
     Nd = sim.Nd
     n_sym = int(np.ceil(n0 / (Nd * cfg.bits_per_symbol)))
     adaptive = update_mode == 'adaptive'
-    plan = bf_plan(cfg, n_sym, n0, num_tx, num_rx, adaptive)
+    plan = bf_plan(cfg, n_sym, n0, num_tx, num_rx, adaptive, precision=sim.precision)
     H = (np.random.randn(num_rx, num_tx) + 1j * np.random.randn(num_rx, num_tx)) / np.sqrt(2)
     L = n_sym * Nd
     z = np.zeros((num_rx, 2, L))

@@ -34,10 +34,8 @@ class Plan:
         d.num_tx = int(num_tx)
         d.rank, d.detector, d.sc_fdm, d.bf_adaptive = int(rank), int(detector), int(sc_fdm), int(bf_adaptive)
         d.no_equalization = int(no_equalization)
-        # float64 (the reference's arithmetic) unless 'f32' is asked for; the
-        # beamforming chain runs float32
-        bf = chain == C.CHAIN_BEAMFORMING
-        d.precision = C.PREC_DEFAULT if bf else (C.PREC_F64 if C.precision_of(precision) == 'f64' else C.PREC_F32)
+        # float64 (the reference's arithmetic) unless 'f32' is asked for
+        d.precision = C.PREC_F64 if C.precision_of(precision) == 'f64' else C.PREC_F32
         if rank and num_tx <= 4 and rank <= 4:   # W [num_tx][rank] -> the [4][4] table of lte_plan_desc.precoder
             #                                    (larger arrays: lte_plan_create rejects them, LTE_EUNSUP)
             W = np.asarray(precoder, dtype=np.complex128).reshape(int(num_tx), int(rank))

@@ -839,7 +839,7 @@ class OFDMSimulator:
             bfo.update(beamforming or {})
             nb = int(n_bits or SLOT_SIZE * self.Nd * cfg.bits_per_symbol)
             plan = bf_plan(cfg, int(np.ceil(nb / (self.Nd * cfg.bits_per_symbol))), nb, bfo['num_tx'],
-                           bfo['num_rx'], bfo['update_mode'] == 'adaptive', frames_per_call)
+                           bfo['num_rx'], bfo['update_mode'] == 'adaptive', frames_per_call, precision=self.precision)
         elif mimo is not None:
             raise ValueError(f"unknown mimo mode {mimo!r}")
         elif coded:

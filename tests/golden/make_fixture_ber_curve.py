@@ -116,9 +116,15 @@ def main():
                         **extra)
     ber = err.sum(1) / (FRAMES * TB)
     with open(out.replace('.npz', '_manifest.json'), 'w') as f:
-        json.dump({'generated_by': 'tests/golden/make_fixture_ber_curve.py' + (' --config 4' if c4 else '') +
-                   ' (float64 oracle)', 'numpy': np.__version__, 'ber': ber.tolist(),
-                   'bler': (1 - crc.mean(1)).tolist()}, f, indent=1)
+        man = {'generated_by': 'tests/golden/make_fixture_ber_curve.py' + (' --config 4' if c4 else '') +
+               ' (float64 oracle)', 'numpy': np.__version__, 'ber': ber.tolist(),
+               'bler': (1 - crc.mean(1)).tolist()}
+        if c4:
+            man['parity'] = ('unpinned by the reference: the reference has no function that composes SFBC with '
+                             'the coding chain; this fixture is the float64 oracle\'s composition '
+                             '(oracle/mimo_oracle.py simulate_sfbc_coded, DESIGN.md 3a), each of whose components '
+                             'is pinned to the reference\'s goldens')
+        json.dump(man, f, indent=1)
     print('BER', np.array2string(ber, precision=4), f'({time.time() - t0:.0f}s)')
 
 

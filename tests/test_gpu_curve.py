@@ -197,7 +197,9 @@ def curve_runs_c4(C, fixture_curve_c4):
 def test_sfbc_coded_ber_curve_fixture_f64_exact(curve_runs_c4, fixture_curve_c4):
     """Config 4 (SFBC 2x2 + turbo, 20 MHz 64-QAM PedA), 512 injected frames over
     0:2:30 dB: the float64 GPU chain == the float64 oracle composition frame by
-    frame (bit errors and CRC verdicts)."""
+    frame (bit errors and CRC verdicts).  Parity unpinned by the reference: it
+    has no coded SFBC function, so this pins the GPU to the oracle's
+    composition of reference-pinned components (fixture manifest "parity")."""
     err, crc = curve_runs_c4['f64']
     assert np.array_equal(err, fixture_curve_c4['bit_errors'])
     assert np.array_equal(crc, fixture_curve_c4['crc_ok'])

@@ -168,7 +168,7 @@ typedef struct {
   /* beamforming capture: per frame PMI (CSIFeedback) and beamforming gain (dB);
    * cap_H holds H [n_frames][num_rx][num_tx] for this chain */
   int32_t *cap_pmi;
-  float *cap_bf_gain;
+  double *cap_bf_gain;         /* [n_frames] beamforming gain (dB), float64 (ABI 2; float in ABI 1) */
 } lte_run_args;
 
 /* Library / device. */

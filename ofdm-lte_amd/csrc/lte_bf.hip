@@ -111,7 +111,7 @@ __global__ __launch_bounds__(BWG) void k_bf_setup(int B, int num_tx, int num_rx,
   f->inv_p = (R)(1.0 / pe);   // comb / np.sum(|He|^2): NumPy multiplies by the reciprocal
   f->pmi = pmi;
   // BeamformingPrecoder.calculate_beamforming_gain: only the adaptive precoder holds W
-  f->gain_db = adaptive ? (float)(10.0 * log10(pe / (ph / num_tx))) : 0.0f;
+  f->gain_db = adaptive ? 10.0 * log10(pe / (ph / num_tx)) : 0.0;
 }
 
 template <class R, int BPS>

@@ -493,6 +493,12 @@ template <> BfFrameT<double>* bf_frames<double>(lte_plan* p) { return p->bf_fr64
 template <> ChainBufs<float>& cbuf<float>(lte_plan* p) { return p->c32; }
 template <> ChainBufs<double>& cbuf<double>(lte_plan* p) { return p->c64; }
 
+// an on/off switch from the environment (A/B knobs): unset -> def
+bool env_on(const char* name, bool def) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) != 0 : def;
+}
+
 // chunk width of the plan's decoder rows (allocated for ceil(max_frames / 64) groups)
 int turbo_plan_ch(const lte_plan* p) { return turbo_chunk((p->d.max_frames + 63) / 64); }
 
@@ -690,7 +696,7 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
   m.n_cs = (ray && fD != 0.0 && !m.exact_jakes) ? (int)((L + chunk - 1) / chunk) : 1;
   const int np = ray ? n_paths : 1;
   // partial-sum slots: 256-sample blocks (link stats) or OFDM-symbol blocks (channel), whichever is more
-  const int nblk = std::max((int)((L + 255) / 256), mimo_channel_nblk((int)L, g.N + g.cp));
+  const int nblk = std::max((int)((L + 255) / 256), mimo_channel_pblk<R>(g, m));
   const size_t links = (size_t)num_rx * num_tx;
   const bool link_noise_on = mode == 0 && ray;
   DBuf<V> dx, dy, dcoef, dout;
@@ -731,8 +737,9 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
                                    (!ray && mode == 1 && link_h) ? dlh.p : nullptr, 0, dcoef.p, dphs.p) == 0;
   const R* lz = (link_noise_on && link_noise) ? dlz.p : nullptr;
   ok = ok && launch_channel_mimo<R>(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dphs.p, dgain.p, fs, dx.p,
-                                    dy.p, link_noise_on ? 1 : 0, dfid.p, seed, lz, 0, dlp.p, dls.p, dpp.p, nblk) == 0;
-  ok = ok && launch_npow_mimo<R>(nullptr, 1, num_rx, dpp.p, mimo_channel_nblk((int)L, g.N + g.cp), (int)L, dsl.p,
+                                    dy.p, link_noise_on ? 1 : 0, dfid.p, seed, lz, 0, dlp.p, dls.p, dpp.p, nblk, 0,
+                                    ray ? *std::max_element(delays, delays + n_paths) : 0) == 0;
+  ok = ok && launch_npow_mimo<R>(nullptr, 1, num_rx, dpp.p, mimo_channel_pblk<R>(g, m), (int)L, dsl.p,
                                  mode == 0 ? (double)num_tx : 1.0, dnp.p) == 0;
   if (ok) {
     hipLaunchKernelGGL(k_cap_rx<R>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
@@ -1125,7 +1132,8 @@ static bool alloc_mimo(lte_plan* p, bool coded) {
   const MimoGrid& m = p->mg;
   const size_t links = (size_t)m.num_rx * m.num_tx;
   bool bad = false;
-  bad |= c.x.alloc(B * m.num_tx * p->L) != 0;
+  // c.x (the TX streams) is allocated by run_mimo when a path writes it (the
+  // fused flat-link TX never does)
   bad |= c.y.alloc(B * m.num_rx * p->L) != 0;
   bad |= c.coef.alloc(B * links * (ray ? d.n_paths : 1) * m.n_cs * (p->f64 ? mimo_ncf<double>() : mimo_ncf<float>())) != 0;
   if (ray && m.exact_jakes) bad |= c.phases.alloc(B * links * d.n_paths * 16) != 0;
@@ -1490,10 +1498,6 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     Timer t(p, KN_ENCODE);
     LCHK(launch_encode(s, p->pw.p, p->PW, p->KWmax, p->enc.p, p->EW, p->cbi.p, p->C, B, p->enc_qmask.p, p->qstride));
   }
-  {
-    Timer t(p, KN_OFDM_TX);
-    LCHK(launch_ofdm_tx_mimo<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, c.x.p, B));
-  }
   const int np = ray ? d.n_paths : 1;
   R* phases = (ray && m.exact_jakes) ? c.phases.p : nullptr;
   {
@@ -1501,14 +1505,43 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     LCHK(launch_fading_mimo<R>(s, g, m, B, ray ? 1 : 0, d.n_paths, c.gains.p, d.fD, d.fs, p->fid.p, a->seed, inj_ph,
                                inj_ph_stride, inj_lh, inj_lh_stride, c.coef.p, phases));
   }
-  {
+  // transmit_mimo's link power on the TX symbols in LDS (static taps, N >= 512,
+  // delays within the CP): the channel pass then reads x once
+  TxLinkPower<R> lp{};
+  const int maxd = ray ? *std::max_element(d.delays, d.delays + d.n_paths) : 0;
+  const bool lp_fuse = link_noise && m.n_cs == 1 && !m.exact_jakes && (g.N >> 3) >= 64 && maxd <= g.cp &&
+                       d.n_paths <= TXCH_MAXP &&
+                       env_on("LTE_MIMO_LP_FUSE", true);
+  // (partials [link][symbol]: the layout k_link_power writes, nch = n_sym blocks per link)
+  if (lp_fuse) lp = TxLinkPower<R>{p->delays.p, c.coef.p, c.link_part.p, d.n_paths, maxd,
+                                   mimo_channel_nblk(p->L, g.N + g.cp)};
+  // flat links (AWGN: spatial CN(0,1), SFBC exp(j t pi/2)): TX and channel in
+  // one pass per (frame, symbol, RX) -- y_r = IFFT(sum_t h_rt G_t) -- when no
+  // TX-stream capture needs x
+  const int nch = mimo_channel_nblk(p->L, g.N + g.cp);
+  const bool flat_fuse = !ray && !a->cap_signal_tx && !a->cap_link_stats && (g.N >> 3) >= 64 && m.num_tx <= 4 &&
+                         env_on("LTE_MIMO_FLAT_FUSE", true);
+  if (flat_fuse) {
+    Timer t(p, KN_OFDM_TX);
+    LCHK(launch_ofdm_txch_flat<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p,
+                                  c.coef.p, c.y.p, c.pow_part.p, nch, B));
+  } else {
+    if (c.x.alloc((size_t)d.max_frames * m.num_tx * p->L)) return fail(LTE_ENOMEM, "TX signal buffer");
+    {
+      Timer t(p, KN_OFDM_TX);
+      LCHK(launch_ofdm_tx_mimo<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, c.x.p,
+                                  B, lp));
+    }
     Timer t(p, KN_CHANNEL);
     LCHK(launch_channel_mimo<R>(s, g, m, B, np, ray ? p->delays.p : nullptr, c.coef.p, phases, c.gains.p, d.fs, c.x.p,
                                 c.y.p, link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, c.link_part.p,
-                                c.link_sigma.p, c.pow_part.p, p->nblk));
+                                c.link_sigma.p, c.pow_part.p, p->nblk, lp_fuse ? 1 : 0, maxd));
+  }
+  {
+    Timer t(p, KN_CHANNEL);
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
-    LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, mimo_channel_nblk(p->L, g.N + g.cp), p->L, c.snr_lin.p,
-                             sfbc ? (double)m.num_tx : 1.0, c.npow.p));
+    LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, flat_fuse ? nch : mimo_channel_pblk<R>(g, m), p->L,
+                             c.snr_lin.p, sfbc ? (double)m.num_tx : 1.0, c.npow.p));
   }
   {
     Timer t(p, KN_RX_CHEST);

@@ -261,9 +261,19 @@ template <> struct MGT<double> {
 };
 // Multi-antenna launchers, R = double (the reference's complex128, default)
 // or float (fast mode); explicit instances in lte_mimo.hip.
+// transmit_mimo's link power made by the TX kernel (part = null: not asked for):
+// per link and OFDM symbol the power of the link's faded signal (static taps)
+template <class R>
+struct TxLinkPower {
+  const int32_t* delays;   // [n_paths] (device)
+  const cx<R>* coef;       // [B][num_rx][num_tx][n_paths][mimo_ncf<R>()] (n_cs = 1)
+  R* part;                 // [B][num_rx][num_tx][nblk]
+  int n_paths, max_delay, nblk;
+};
 template <class R>
 int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
-                        const uint32_t* enc, int enc_words, const int32_t* tx_map, cx<R>* x, int B);
+                        const uint32_t* enc, int enc_words, const int32_t* tx_map, cx<R>* x, int B,
+                        const TxLinkPower<R>& lp);
 // per link path: f32 h(n) = A + B d + C d^2 around the centre of n's OFDM
 // symbol (fD != 0), or A (fD == 0); f64 A (fD == 0) or the phases (exact Jakes)
 template <class R>
@@ -271,13 +281,24 @@ int launch_fading_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, i
                        const R* gains, double fD, double fs, const uint64_t* fid, uint64_t seed,
                        const R* inj_ph, int64_t inj_ph_stride, const R* inj_h, int64_t inj_h_stride,
                        cx<R>* coef, R* phases);
+// TX + flat (AWGN) channel in one pass per (frame, symbol, RX): y [B][num_rx][L]
+// and pow_part [B][num_rx][nblk] (per OFDM symbol); coef from launch_fading_mimo
+template <class R>
+int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
+                          const uint32_t* enc, int enc_words, const int32_t* tx_map, const cx<R>* coef, cx<R>* y,
+                          R* pow_part, int nblk, int B);
 // phases / gains: exact-Jakes mode (m.exact_jakes) only
 template <class R>
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
                         const cx<R>* coef, const R* phases, const R* gains, double fs, const cx<R>* x, cx<R>* y,
                         int link_noise, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
-                        R* link_part, R* link_sigma, R* pow_part, int nblk);
-int mimo_channel_nblk(int L, int sym_len);   // power partials per (frame, rx) written by launch_channel_mimo
+                        R* link_part, R* link_sigma, R* pow_part, int nblk, int link_part_done = 0,
+                        int max_delay = 0);   // max_delay: largest of delays (host value; staged chunks)
+int mimo_channel_nblk(int L, int sym_len);   // OFDM symbols (blocks of N + cp samples) of a stream
+// power partials per (frame, rx) written by launch_channel_mimo (symbols x
+// chunks of the staged kernel)
+template <class R>
+int mimo_channel_pblk(const Grid& g, const MimoGrid& m);
 // per link [mean|x|^2, mean|y|^2, Re, Im mean(y conj x)] of the link's output
 // y (with its 100 dB link noise when link_sigma is set)
 template <class R>
@@ -314,7 +335,7 @@ struct BfFrameT {
   cx<R> He[LTE_BF_MAX_RX];
   R inv_p;
   int pmi;
-  float gain_db;
+  double gain_db;
 };
 // sigma: per frame noise scale sqrt(10^(-SNR/10) / 2) (core/ofdm_core.py:2397-2399)
 template <class R>

@@ -60,11 +60,20 @@ __device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ 
   return zero ? mkc((R)0, (R)0) : qam_point<BPS, R>(idx);
 }
 
+// transmit_mimo's per-link power pass (core/ofdm_core.py:490-503: each
+// Rayleigh link's 100 dB ChannelSimulator measures mean |y0|^2 of its own faded
+// signal) done on the symbol while it is in LDS: for every RX r, the power of
+// y0[m] = sum_p c_{r,t,p} x[m - d_p] over the CP-extended symbol's samples m in
+// [max_delay, S) -- every delayed sample inside the symbol (sample j of the
+// extended symbol is buf[(j - cp) mod N] * sc, the values x holds).  The first
+// max_delay samples, whose taps reach into the previous symbol, are added by
+// k_link_power_fix from x.  Static taps only (n_cs = 1); part[link][l].
+
 template <class R, int MODE, int CODED, int BPS, int NC = 0>
 __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                       const uint32_t* __restrict__ enc, int enc_words,
                                                       const int32_t* __restrict__ tx_map, cx<R>* __restrict__ x,
-                                                      int B, int stage_enc) {
+                                                      int B, int stage_enc, TxLinkPower<R> lp) {
   using V = cx<R>;
   V* sm = mimo_lds<V>();
   const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
@@ -114,20 +123,226 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
   }
   __syncthreads();
   fft_lds<true, NC>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
+  const R sc = tx_scale<R>(N);
   if (active) {
-    const R sc = tx_scale<R>(N);
     V* xo = x + ((size_t)b * m.num_tx + t) * g.L + (size_t)l * (N + g.cp);
     for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
     for (int k = tid; k < g.cp; k += T) xo[k] = cscale(buf[N - g.cp + k], sc);
   }
+  if (lp.part) {   // whole waves per slot (T >= 64): launch_ofdm_tx_mimo checks
+    __shared__ R red[MWG / 64];
+    constexpr int NCF = mimo_ncf<R>();
+    const int S = N + g.cp, D = lp.max_delay, np = lp.n_paths;
+    int dl[TXCH_MAXP];
+#pragma unroll
+    for (int p = 0; p < TXCH_MAXP; ++p) dl[p] = p < np ? g.cp + lp.delays[p] : 0;
+    for (int r = 0; r < m.num_rx; ++r) {
+      R pwr = (R)0;
+      if (active) {
+        const V* cf = lp.coef + (((size_t)b * m.num_rx + r) * m.num_tx + t) * np * NCF;
+        V c[TXCH_MAXP];
+#pragma unroll
+        for (int p = 0; p < TXCH_MAXP; ++p) c[p] = p < np ? cf[p * NCF] : mkc((R)0, (R)0);
+        for (int j = D + tid; j < S; j += T) {
+          V acc = mkc((R)0, (R)0);
+#pragma unroll
+          for (int p = 0; p < TXCH_MAXP; ++p)
+            if (p < np) acc = cadd(acc, cmul(c[p], cscale(buf[(j - dl[p]) & (N - 1)], sc)));
+          pwr += acc.x * acc.x + acc.y * acc.y;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) pwr += __shfl_xor(pwr, o);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pwr;
+      __syncthreads();
+      if (active && tid == 0) {
+        R tot = (R)0;
+        for (int w = 0; w < T / 64; ++w) tot += red[slot * (T / 64) + w];
+        lp.part[(((size_t)b * m.num_rx + r) * m.num_tx + t) * lp.nblk + l] = tot;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// TX + flat channel in one pass (AWGN links: spatial h ~ CN(0,1), SFBC h =
+// exp(j t pi/2)): one slot per (frame, OFDM symbol, RX).  A flat link is a
+// scalar, so y_r = sum_t h_rt x_t = IFFT(sum_t h_rt G_t) sqrt(N): the slot
+// builds Y = sum_t h_rt G_t (each TX's data REs and its own pilot subset, t in
+// order from zero) in LDS, runs ONE IFFT per RX instead of one per TX, and
+// writes the received stream y (CP included) and its power partial per symbol
+// -- the TX streams x never go through HBM and the channel pass disappears.
+// The same sums as ys[r] += hh * xs[t] (core/channel.py:473-491) taken in the
+// frequency domain, and for spatial layers through the effective channel h_r W
+// (x_t = sum_c W[t][c] s_c): equal up to float64 rounding (the reference adds
+// the time-domain products), tests/test_gpu_mimo.py::test_flat_channel_fused_tx.
+template <class R, int MODE, int CODED, int BPS, int NC = 0>
+__global__ __launch_bounds__(MWG) void k_ofdm_txch_flat(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
+                                                        const uint32_t* __restrict__ enc, int enc_words,
+                                                        const int32_t* __restrict__ tx_map,
+                                                        const cx<R>* __restrict__ coef, cx<R>* __restrict__ y,
+                                                        R* __restrict__ pow_part, int nblk, int B, int stage_enc) {
+  using V = cx<R>;
+  constexpr int NCF = mimo_ncf<R>();
+  __shared__ R red[MWG / 64];
+  V* sm = mimo_lds<V>();
+  const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
+  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int per = g.n_sym * m.num_rx;
+  const int gs = blockIdx.x * spw + slot;
+  const int b = gs / per, rr = gs - b * per, l = rr / m.num_rx, r = rr - l * m.num_rx;
+  const bool active = slot < spw && b < B;
+  V* buf = sm + slot * N;
+  const uint32_t* fe = enc + (size_t)b * enc_words;
+  if (CODED && stage_enc) {
+    uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
+    if (active)
+      for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
+    fe = es;
+  }
+  if (active)
+    for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
+  __syncthreads();
+  if (active) {
+    const uint32_t* fb = pw + (size_t)b * PW;
+    const int64_t q0 = (int64_t)l * m.res;
+    const V* hr = coef + ((size_t)b * m.num_rx + r) * m.num_tx * NCF;   // h_rt at hr[t * NCF]
+    V E[4];   // spatial: the effective channel of RX r, E_c = sum_t h_rt W[t][c]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      E[c] = mkc((R)0, (R)0);
+      if (MODE == MIMO_SPATIAL && c < m.rank)
+        for (int t = 0; t < m.num_tx; ++t)
+          E[c] = cadd(E[c], cmul(hr[t * NCF], mkc((R)m.W[(t * 4 + c) * 2], (R)m.W[(t * 4 + c) * 2 + 1])));
+    }
+    for (int j = tid; j < m.n_dsc; j += T) {
+      V acc = mkc((R)0, (R)0);
+      if constexpr (MODE == MIMO_SFBC) {
+        const int64_t qp = q0 + (j & ~1);
+        const V s0 = qam_at<R, CODED, BPS>(qp, fb, fe, tx_map), s1 = qam_at<R, CODED, BPS>(qp + 1, fb, fe, tx_map);
+        const V v0 = (j & 1) == 0 ? s0 : mkc(-s1.x, s1.y);   // TX0 [s0, -conj(s1)]
+        const V v1 = (j & 1) == 0 ? s1 : mkc(s0.x, -s0.y);   // TX1 [s1, conj(s0)]
+        acc = cadd(cmul(hr[0], v0), cmul(hr[NCF], v1));
+      } else {   // sum_t h_rt (W s)_t = sum_c E_c s_c, E = (h_r W) formed once per thread
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int qi = m.rank * j + c;
+          if (c < m.rank && qi < m.res) acc = cadd(acc, cmul(E[c], qam_at<R, CODED, BPS>(q0 + qi, fb, fe, tx_map)));
+        }
+      }
+      buf[g.data_idx[j]] = acc;
+    }
+    for (int t = 0; t < m.num_tx; ++t) {   // each TX's CRS pilots on its own subset
+      const V* pv = MGT<R>::pval(m) + t * m.maxP;
+      const V h = hr[t * NCF];
+      for (int p = tid; p < m.np_tx[t]; p += T) {
+        V& e = buf[m.ppos[t * m.maxP + p]];
+        e = cadd(e, cmul(h, pv[p]));
+      }
+    }
+  }
+  __syncthreads();
+  fft_lds<true, NC>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
+  const R sc = tx_scale<R>(N);
+  R pwr = (R)0;
+  if (active) {
+    V* yo = y + ((size_t)b * m.num_rx + r) * g.L + (size_t)l * (N + g.cp);
+    for (int k = tid; k < N; k += T) {
+      const V v = cscale(buf[k], sc);
+      yo[g.cp + k] = v;
+      pwr += v.x * v.x + v.y * v.y;
+    }
+    for (int k = tid; k < g.cp; k += T) {
+      const V v = cscale(buf[N - g.cp + k], sc);
+      yo[k] = v;
+      pwr += v.x * v.x + v.y * v.y;
+    }
+  }
+  if (T >= 64) {   // whole waves per slot
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pwr += __shfl_xor(pwr, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pwr;
+    __syncthreads();
+    if (active && tid == 0) {
+      R tot = (R)0;
+      for (int w = 0; w < T / 64; ++w) tot += red[slot * (T / 64) + w];
+      pow_part[((size_t)b * m.num_rx + r) * nblk + l] = tot;
+    }
+  }
+}
+
+template <class R>
+int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
+                          const uint32_t* enc, int enc_words, const int32_t* tx_map, const cx<R>* coef, cx<R>* y,
+                          R* pow_part, int nblk, int B) {
+  const int spw = MWG / (g.N >> 3);
+  const int64_t total = (int64_t)B * g.n_sym * m.num_rx;
+  if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6) || (g.N >> 3) < 64 || nblk < g.n_sym ||
+      m.num_tx > 4)
+    return (int)hipErrorInvalidValue;
+  const int blocks = (int)((total + spw - 1) / spw);
+  const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
+  const int stage_enc = coded && enc_shm <= 32768;
+  const size_t shm = spw * g.N * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
+#define LTE_TXF(M_, C_, B_)                                                                                          \
+  do {                                                                                                               \
+    if (g.N == 2048)                                                                                                 \
+      hipLaunchKernelGGL((k_ofdm_txch_flat<R, M_, C_, B_, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc, \
+                         enc_words, tx_map, coef, y, pow_part, nblk, B, stage_enc);                                  \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_ofdm_txch_flat<R, M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc,      \
+                         enc_words, tx_map, coef, y, pow_part, nblk, B, stage_enc);                                  \
+  } while (0)
+#define LTE_TXF_BPS(M_, C_) \
+  do { if (g.bps == 2) LTE_TXF(M_, C_, 2); else if (g.bps == 4) LTE_TXF(M_, C_, 4); else LTE_TXF(M_, C_, 6); } while (0)
+  if (m.mode == MIMO_SFBC) {
+    if (coded) LTE_TXF_BPS(MIMO_SFBC, 1); else LTE_TXF_BPS(MIMO_SFBC, 0);
+  } else {
+    if (coded) LTE_TXF_BPS(MIMO_SPATIAL, 1); else LTE_TXF_BPS(MIMO_SPATIAL, 0);
+  }
+#undef LTE_TXF_BPS
+#undef LTE_TXF
+  return (int)hipGetLastError();
+}
+
+// The link power of the first max_delay samples of every symbol (their taps
+// reach into the previous symbol; stream-level delay with a zero prefix), from
+// x, added to k_ofdm_tx_mimo's partial: one lane per (frame, link, symbol).
+template <class R>
+__global__ __launch_bounds__(MWG) void k_link_power_fix(int B, int num_rx, int num_tx, int n_sym, int sym_len, int L,
+                                                        const cx<R>* __restrict__ x, TxLinkPower<R> lp) {
+  using V = cx<R>;
+  constexpr int NCF = mimo_ncf<R>();
+  const int64_t i = (int64_t)blockIdx.x * MWG + threadIdx.x;
+  const int64_t nl = (int64_t)num_rx * num_tx;
+  if (i >= (int64_t)B * nl * n_sym) return;
+  const int l = (int)(i % n_sym);
+  const int64_t bl = i / n_sym;              // b * nl + link
+  const int b = (int)(bl / nl), link = (int)(bl % nl), t = link % num_tx;
+  const V* xf = x + ((size_t)b * num_tx + t) * L;
+  const V* cf = lp.coef + (size_t)bl * lp.n_paths * NCF;
+  const int n0 = l * sym_len;
+  R pwr = (R)0;
+  for (int mm = 0; mm < lp.max_delay; ++mm) {
+    V acc = mkc((R)0, (R)0);
+    for (int p = 0; p < lp.n_paths; ++p) {
+      const int src = n0 + mm - lp.delays[p];
+      if (src >= 0) acc = cadd(acc, cmul(cf[p * NCF], xf[src]));
+    }
+    pwr += acc.x * acc.x + acc.y * acc.y;
+  }
+  lp.part[(size_t)bl * lp.nblk + l] += pwr;
 }
 
 template <class R>
 int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
-                        const uint32_t* enc, int enc_words, const int32_t* tx_map, cx<R>* x, int B) {
+                        const uint32_t* enc, int enc_words, const int32_t* tx_map, cx<R>* x, int B,
+                        const TxLinkPower<R>& lp) {
   const int spw = MWG / (g.N >> 3);
   const int64_t total = (int64_t)B * g.n_sym * m.num_tx;
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
+  if (lp.part && ((g.N >> 3) < 64 || lp.max_delay > g.cp || lp.nblk < g.n_sym || lp.n_paths > TXCH_MAXP))
+    return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
   const int stage_enc = coded && enc_shm <= 32768;
@@ -136,10 +351,10 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
   do {                                                                                                               \
     if (g.N == 2048)   /* 20 MHz: compile-time N (unrolled passes, twiddle recurrence) */                            \
       hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc,  \
-                         enc_words, tx_map, x, B, stage_enc);                                                        \
+                         enc_words, tx_map, x, B, stage_enc, lp);                                                    \
     else                                                                                                             \
       hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc,        \
-                         enc_words, tx_map, x, B, stage_enc);                                                        \
+                         enc_words, tx_map, x, B, stage_enc, lp);                                                    \
   } while (0)
 #define LTE_TXM_BPS(M_, C_) \
   do { if (g.bps == 2) LTE_TXM(M_, C_, 2); else if (g.bps == 4) LTE_TXM(M_, C_, 4); else LTE_TXM(M_, C_, 6); } while (0)
@@ -150,6 +365,13 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
   }
 #undef LTE_TXM_BPS
 #undef LTE_TXM
+  if (lp.part && lp.max_delay > 0) {
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+    const int64_t n = total * m.num_rx;   // (frame, link, symbol)
+    hipLaunchKernelGGL(k_link_power_fix<R>, dim3((unsigned)((n + MWG - 1) / MWG)), dim3(MWG), 0, s, B, m.num_rx,
+                       m.num_tx, g.n_sym, g.N + g.cp, g.L, x, lp);
+  }
   return (int)hipGetLastError();
 }
 
@@ -363,6 +585,13 @@ constexpr int MC_RXG = 4;     // receive antennas accumulated per pass over the 
 #define LTE_CHM_G2_WAVES 5
 #endif
 
+// acc[q][j] += sum_p h_{rx q, tx, p}(n_j) x_tx[n_j - delay_p] for the nq <=
+// MC_RXG receive antennas of a group and one transmit stream: each delayed TX
+// sample is loaded once for all of them (the group's links share the TX
+// stream).  cs: the first link's coefficients at this symbol (stride n_cs *
+// mimo_ncf per path, cs_q per receive antenna); EX: f64 exact Jakes from the
+// phases ph (ph_q per receive antenna) -- a separate instance, so that its
+// sincos calls do not set the register budget of the coefficient path.
 // acc[q][j] += sum_p h_{rx q, tx, p}(n_j) x_tx[n_j - delay_p] for the nq <=
 // MC_RXG receive antennas of a group and one transmit stream: each delayed TX
 // sample is loaded once for all of them (the group's links share the TX
@@ -624,14 +853,21 @@ __global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8 && !EX) ? LTE_CHM_G2
 
 int mimo_channel_nblk(int L, int sym_len) { return (L + sym_len - 1) / sym_len; }
 
+// power partials per (frame, RX) the channel pass writes: one per OFDM symbol
+template <class R>
+int mimo_channel_pblk(const Grid& g, const MimoGrid&) {
+  return mimo_channel_nblk(g.L, g.N + g.cp);
+}
+
 template <class R>
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
                         const cx<R>* coef, const R* phases, const R* gains, double fs, const cx<R>* x, cx<R>* y,
                         int link_noise, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
-                        R* link_part, R* link_sigma, R* pow_part, int nblk) {
+                        R* link_part, R* link_sigma, R* pow_part, int nblk, int link_part_done, int max_delay) {
   const int sym_len = g.N + g.cp;
   if (m.num_rx > MC_MAXRX) return (int)hipErrorInvalidValue;
   const int nch = mimo_channel_nblk(g.L, sym_len);
+  (void)max_delay;
   if (nch > nblk) return (int)hipErrorInvalidValue;   // partial buffers are sized for nblk blocks
   const R* ph = m.exact_jakes ? phases : nullptr;
   if (m.exact_jakes && (!phases || !gains)) return (int)hipErrorInvalidValue;
@@ -652,9 +888,10 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
 #define LTE_CHM_EXG(J_, EX_, G_)                                                                                    \
   do {                                                                                                             \
     if (link_noise) {                                                                                              \
-      hipLaunchKernelGGL((k_link_power<R, J_, EX_, G_>), dim3(nch * B, m.num_tx), dim3(MWG), 0, s, g.L,           \
-                         m.num_rx, m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x,          \
-                         link_part, nch);                                                                          \
+      if (!link_part_done)   /* else k_ofdm_tx_mimo + k_link_power_fix wrote the partials */                      \
+        hipLaunchKernelGGL((k_link_power<R, J_, EX_, G_>), dim3(nch * B, m.num_tx), dim3(MWG), 0, s, g.L,         \
+                           m.num_rx, m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x,        \
+                           link_part, nch);                                                                        \
       const int nl = B * m.num_rx * m.num_tx;                                                                      \
       hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L,        \
                          link_sigma);                                                                              \
@@ -1283,13 +1520,16 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
 // explicit instances: float (fast mode) and double (the reference's precision)
 #define LTE_MIMO_INST(R)                                                                                           \
   template int launch_ofdm_tx_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,       \
-                                      const uint32_t*, int, const int32_t*, cx<R>*, int);                          \
+                                      const uint32_t*, int, const int32_t*, cx<R>*, int, const TxLinkPower<R>&);   \
+  template int mimo_channel_pblk<R>(const Grid&, const MimoGrid&);                                              \
+  template int launch_ofdm_txch_flat<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,     \
+                                        const uint32_t*, int, const int32_t*, const cx<R>*, cx<R>*, R*, int, int); \
   template int launch_fading_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const R*, double,   \
                                      double, const uint64_t*, uint64_t, const R*, int64_t, const R*, int64_t,      \
                                      cx<R>*, R*);                                                                  \
   template int launch_channel_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const int32_t*,         \
                                       const cx<R>*, const R*, const R*, double, const cx<R>*, cx<R>*, int,         \
-                                      const uint64_t*, uint64_t, const R*, int64_t, R*, R*, R*, int);              \
+                                      const uint64_t*, uint64_t, const R*, int64_t, R*, R*, R*, int, int, int);    \
   template int launch_link_stats<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const int32_t*,           \
                                     const cx<R>*, const R*, const R*, double, const cx<R>*, const R*,              \
                                     const uint64_t*, uint64_t, const R*, int64_t, R*, int, R*);                    \

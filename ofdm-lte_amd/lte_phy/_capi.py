@@ -52,7 +52,7 @@ class RunArgs(ctypes.Structure):
                 ('link_noise', P(c_f64)), ('link_noise_stride', c_i64),
                 ('link_h', P(c_f64)), ('link_h_stride', c_i64),
                 ('cap_link_stats', ctypes.c_void_p),
-                ('cap_pmi', P(c_i32)), ('cap_bf_gain', P(ctypes.c_float))]
+                ('cap_pmi', P(c_i32)), ('cap_bf_gain', P(c_f64))]
 
 
 # every symbol include/lte_phy.h declares, with its ctypes signature

@@ -162,7 +162,7 @@ class Plan:
         if self.bf:
             shapes.update({'H': ((B, self.num_rx, self.num_tx), cdt, 'cap_H', None),
                            'pmi': ((B,), np.int32, 'cap_pmi', C.I32),
-                           'bf_gain': ((B,), np.float32, 'cap_bf_gain', C.F32)})
+                           'bf_gain': ((B,), np.float64, 'cap_bf_gain', C.F64)})
             for k in ('pilot_stats', 'tx_syms', 'signal_tx', 'signal_rx', 'llr', 'noise_power'):
                 shapes.pop(k)
         for name in capture:

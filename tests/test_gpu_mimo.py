@@ -169,6 +169,54 @@ def test_sfbc_coded_llrs_and_decoding(C, oracle, chan, prec):
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('mode', ['spatial', 'sfbc'])
+def test_flat_channel_fused_tx(C, prec, mode, monkeypatch):
+    """Flat (AWGN) links: TX and channel in one pass per (frame, symbol, RX),
+    y_r = IFFT(sum_t h_rt G_t) (k_ofdm_txch_flat, default) against the TX
+    streams through HBM and the channel pass (LTE_MIMO_FLAT_FUSE=0): received
+    streams equal to float64 rounding (the sums are taken in the frequency
+    domain), identical per-frame bit errors."""
+    from lte_phy.ofdm_core import _spatial_plan
+    cfg_sim = _sim(20.0, '64-QAM', 'awgn', prec)
+    if mode == 'spatial':
+        plan = _spatial_plan(cfg_sim.config, 'awgn', 'Pedestrian_A', 3.0, 2.0, 14, 14 * 999 * 6, 6, precision=prec)[0]
+    else:
+        plan = cfg_sim._sfbc_plan(14, 14 * 998 * 6, 2, max_frames=6)
+    snrs = np.array([5.0, 10.0, 15.0, 20.0, 25.0, 30.0])
+    outs = []
+    for fuse in ('1', '0'):
+        monkeypatch.setenv('LTE_MIMO_FLAT_FUSE', fuse)
+        outs.append(plan.run(snrs, seed=33, capture=('signal_rx', 'data_syms')))
+    a, b = outs
+    y0, y1 = a['signal_rx'].astype(np.complex128), b['signal_rx'].astype(np.complex128)
+    assert np.linalg.norm(y0 - y1) / np.linalg.norm(y1) < (1e-14 if prec == 'f64' else 2e-6)
+    z0, z1 = a['data_syms'].astype(np.complex128), b['data_syms'].astype(np.complex128)
+    assert np.linalg.norm(z0 - z1) / np.linalg.norm(z1) < (1e-13 if prec == 'f64' else 1e-5)
+    assert np.array_equal(a['frame_errors'], b['frame_errors'])
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+def test_link_power_in_tx_matches_separate_pass(C, prec, monkeypatch):
+    """Config 4 (SFBC 2x2, Rayleigh links, transmit_mimo's 100 dB link noise):
+    the link powers formed on the TX symbols in LDS (k_ofdm_tx_mimo +
+    k_link_power_fix, default) against the separate k_link_power pass over x
+    (LTE_MIMO_LP_FUSE=0): received streams equal to 1e-15 relative (the power
+    sums differ only in their order, which moves the 1e-5 link noise by ulps),
+    identical per-frame errors and CRC."""
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
+    plan = sim._sfbc_plan(0, 27760, 2, coded=True, max_frames=6)
+    snrs = np.array([6.0, 12.0, 16.0, 18.0, 22.0, 30.0])
+    outs = []
+    for fuse in ('1', '0'):
+        monkeypatch.setenv('LTE_MIMO_LP_FUSE', fuse)
+        outs.append(plan.run(snrs, seed=21, capture=('signal_rx',)))
+    a, b = outs
+    y0, y1 = a['signal_rx'].astype(np.complex128), b['signal_rx'].astype(np.complex128)
+    assert np.linalg.norm(y0 - y1) / np.linalg.norm(y1) < (1e-15 if prec == 'f64' else 1e-6)
+    assert np.array_equal(a['frame_errors'], b['frame_errors']) and np.array_equal(a['crc_ok'], b['crc_ok'])
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mimo,coded,chan', [('sfbc', True, 'rayleigh_mp'), ('spatial', False, 'rayleigh_mp'),
                                             ('spatial', False, 'awgn')])
 def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan, prec):

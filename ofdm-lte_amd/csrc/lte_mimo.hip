@@ -24,6 +24,8 @@
 #include "lte_internal.h"
 #include "lte_dev.h"
 
+#include <cstdlib>
+
 namespace lte {
 
 constexpr int MWG = 256;
@@ -69,7 +71,10 @@ __device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ 
 // max_delay samples, whose taps reach into the previous symbol, are added by
 // k_link_power_fix from x.  Static taps only (n_cs = 1); part[link][l].
 
-template <class R, int MODE, int CODED, int BPS, int NC = 0>
+// PF (coded): one slot per frame walking its (OFDM symbol, TX) pairs, the
+// frame's coded streams staged in LDS once instead of once per pair (as
+// k_ofdm_txf does for SISO); otherwise one slot per (frame, symbol, TX).
+template <class R, int MODE, int CODED, int BPS, int NC = 0, bool PF = false>
 __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                       const uint32_t* __restrict__ enc, int enc_words,
                                                       const int32_t* __restrict__ tx_map, cx<R>* __restrict__ x,
@@ -80,7 +85,8 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
   const int slot = threadIdx.x / T, tid = threadIdx.x % T;
   const int per = g.n_sym * m.num_tx;
   const int gs = blockIdx.x * spw + slot;
-  const int b = gs / per, r = gs - b * per, l = r / m.num_tx, t = r - l * m.num_tx;
+  const int b = PF ? gs : gs / per;
+  const int lt0 = PF ? 0 : gs - b * per, lt1 = PF ? per : lt0 + 1;
   const bool active = slot < spw && b < B;
   V* buf = sm + slot * N;
   // coded: the frame's coded streams are staged in LDS (coalesced), so the
@@ -92,9 +98,11 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
       for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
     fe = es;
   }
+  for (int lt = lt0; lt < lt1; ++lt) {
+  const int l = lt / m.num_tx, t = lt - l * m.num_tx;
   if (active)
     for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
-  __syncthreads();
+  __syncthreads();   // (first pair: also the staged streams)
   if (active) {
     const uint32_t* fb = pw + (size_t)b * PW;
     const int64_t q0 = (int64_t)l * m.res;
@@ -162,6 +170,8 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
       }
       __syncthreads();
     }
+  }
+  if (PF) __syncthreads();   // the next pair zeroes buf
   }
 }
 
@@ -343,13 +353,19 @@ int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int cod
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
   if (lp.part && ((g.N >> 3) < 64 || lp.max_delay > g.cp || lp.nblk < g.n_sym || lp.n_paths > TXCH_MAXP))
     return (int)hipErrorInvalidValue;
-  const int blocks = (int)((total + spw - 1) / spw);
   const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
   const int stage_enc = coded && enc_shm <= 32768;
   const size_t shm = spw * g.N * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
+  // coded frames: one slot per frame over its (symbol, TX) pairs (LTE_TXM_FRAME=0: one per pair)
+  const char* pfe = std::getenv("LTE_TXM_FRAME");
+  const bool pf = stage_enc && g.N == 2048 && !(pfe && std::atoi(pfe) == 0);
+  const int blocks = pf ? (B + spw - 1) / spw : (int)((total + spw - 1) / spw);
 #define LTE_TXM(M_, C_, B_)                                                                                          \
   do {                                                                                                               \
-    if (g.N == 2048)   /* 20 MHz: compile-time N (unrolled passes, twiddle recurrence) */                            \
+    if (g.N == 2048 && pf)                                                                                           \
+      hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_, 2048, true>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, \
+                         enc, enc_words, tx_map, x, B, stage_enc, lp);                                               \
+    else if (g.N == 2048)   /* 20 MHz: compile-time N (unrolled passes, twiddle recurrence) */                       \
       hipLaunchKernelGGL((k_ofdm_tx_mimo<R, M_, C_, B_, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc,  \
                          enc_words, tx_map, x, B, stage_enc, lp);                                                    \
     else                                                                                                             \
@@ -851,12 +867,196 @@ __global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8 && !EX) ? LTE_CHM_G2
   }
 }
 
+// The coefficient-path channel (per-symbol Taylor sets, TAY, or one static
+// tap set per link path): the same sums as k_channel_mimo without the exact
+// Jakes instance, laid out for the f64 FMA pipe.
+//  * The block's (link, path) coefficient sets of its OFDM symbol are staged
+//    in LDS once (nl np K complex values) and read back as wave-uniform
+//    broadcasts: scalar registers cannot hold them for four receive
+//    antennas without spilling inside the FMA loop.
+//  * Each delayed TX sample is loaded once for the G receive antennas of a
+//    group (G divides num_rx: no runtime antenna guard in the unrolled loops,
+//    which made the compiler hold every antenna's coefficients at once);
+//    every receive stream accumulates h x with two FMAs per component.
+//  * Link noise (LN: its own instance) and the power partials as in
+//    k_channel_mimo; the f64 streams
+//    add each (link, path) product straight into the RX sum (the reference
+//    sums each link first -- a different rounding order only, within the
+//    1e-12 stream bars).
+#ifndef LTE_CHT_WAVES   // k_channel_tay: minimum waves per SIMD asked of the register allocator
+#define LTE_CHT_WAVES 4
+#endif
+template <class R, int J, int G, bool TAY, bool LN>
+__global__ __launch_bounds__(MWG, LTE_CHT_WAVES) void k_channel_tay(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
+                                                     const int32_t* __restrict__ delays,
+                                                     const cx<R>* __restrict__ coef, const cx<R>* __restrict__ x,
+                                                     cx<R>* __restrict__ y, const R* __restrict__ link_sigma,
+                                                     const uint64_t* __restrict__ fid, uint64_t seed,
+                                                     const R* __restrict__ inj_lz, int64_t inj_lz_stride,
+                                                     R* __restrict__ pow_part, int nblk) {
+  using V = cx<R>;
+  constexpr int NCF = mimo_ncf<R>();   // stored terms per (path, symbol)
+  constexpr int K = TAY ? NCF : 1;     // terms evaluated
+  __shared__ R red[MWG / 64];
+  V* cl = mimo_lds<V>();               // [num_rx][num_tx][np][K]
+  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
+  const int sidx = TAY ? blk : 0;
+  const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
+  const float dc = 0.5f * (float)(sym_len - 1);
+  const int nl = num_rx * num_tx;
+  {
+    const size_t ps = (size_t)n_cs * NCF;
+    const V* cb = coef + (size_t)b * nl * np * ps + (size_t)sidx * NCF;
+    for (int i = threadIdx.x; i < nl * np * K; i += MWG) {
+      const int lp = i / K, k = i - lp * K;
+      cl[i] = cb[(size_t)lp * ps + k];
+    }
+  }
+  __syncthreads();
+  for (int rg = 0; rg < num_rx; rg += G) {
+    R pw[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) pw[q] = (R)0;
+    for (int base = nbeg; base < nend; base += J * MWG) {
+      const SymSpan<J> sp(base, nbeg, nend, dc, TAY);
+      V v[G][J];
+#pragma unroll
+      for (int q = 0; q < G; ++q)
+#pragma unroll
+        for (int j = 0; j < J; ++j) v[q][j] = mkc((R)0, (R)0);
+#pragma unroll 1
+      for (int tx = 0; tx < num_tx; ++tx) {
+        const V* xf = x + ((size_t)b * num_tx + tx) * L;
+#pragma unroll 1
+        for (int p = 0; p < np; ++p) {
+          const int dl = delays ? delays[p] : 0;
+          V xs[J];
+#pragma unroll
+          for (int j = 0; j < J; ++j) {
+            const int src = sp.n[j] - dl;
+            xs[j] = (sp.ok[j] && src >= 0) ? xf[src] : mkc((R)0, (R)0);
+          }
+#pragma unroll
+          for (int q = 0; q < G; ++q) {
+            const V* c = cl + (((rg + q) * num_tx + tx) * np + p) * K;
+            // Horner over the J samples together, one coefficient live at a time
+            V h[J];
+            const V ct = c[K - 1];
+#pragma unroll
+            for (int j = 0; j < J; ++j) h[j] = ct;
+#pragma unroll
+            for (int k = K - 2; k >= 0; --k) {
+              const V ck = c[k];
+#pragma unroll
+              for (int j = 0; j < J; ++j) {
+                const R dj = (R)sp.d[j];
+                h[j] = mkc(h[j].x * dj + ck.x, h[j].y * dj + ck.y);
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+              v[q][j].x = fma(h[j].x, xs[j].x, fma(-h[j].y, xs[j].y, v[q][j].x));
+              v[q][j].y = fma(h[j].x, xs[j].y, fma(h[j].y, xs[j].x, v[q][j].y));
+            }
+            __builtin_amdgcn_sched_barrier(0);   // keep the next antenna's coefficient reads from piling up
+          }
+        }
+        if (LN) {
+#pragma unroll
+          for (int q = 0; q < G; ++q) {
+            const int link = (rg + q) * num_tx + tx;
+            const R sg = link_sigma[(size_t)b * nl + link];
+            if (inj_lz) {
+              const R* zf = inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L;
+#pragma unroll
+              for (int j = 0; j < J; ++j)
+                if (sp.ok[j]) v[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, v[q][j]);
+            } else {
+              link_noise_span<R, J>(v[q], sp, sg, seed, fid[b], link, (nbeg & 1) == 0);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        const int r = rg + q;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (sp.ok[j]) {
+            y[((size_t)b * num_rx + r) * L + sp.n[j]] = v[q][j];
+            pw[q] += v[q][j].x * v[q][j].x + v[q][j].y * v[q][j].y;
+          }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const R t = block_sum(pw[q], red);
+      if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + rg + q) * nblk + blk] = t;
+      __syncthreads();
+    }
+  }
+}
+
+// LDS bytes of k_channel_tay's coefficient stage
+template <class R>
+size_t channel_tay_lds(const MimoGrid& m, int np) {
+  return (size_t)m.num_rx * m.num_tx * np * (m.n_cs > 1 ? mimo_ncf<R>() : 1) * sizeof(cx<R>);
+}
+
 int mimo_channel_nblk(int L, int sym_len) { return (L + sym_len - 1) / sym_len; }
 
 // power partials per (frame, RX) the channel pass writes: one per OFDM symbol
 template <class R>
 int mimo_channel_pblk(const Grid& g, const MimoGrid&) {
   return mimo_channel_nblk(g.L, g.N + g.cp);
+}
+
+// k_channel_tay's launch: G receive antennas per group (a divisor of num_rx);
+// J (samples per thread per pass, 1..3) the one covering a symbol with the
+// fewest idle lanes (20 MHz: 3 -> 2304 lanes for 2192 samples)
+template <class R>
+static void launch_channel_tay(hipStream_t s, int B, int nch, int L, const MimoGrid& m, int np, int sym_len,
+                               const int32_t* delays, const cx<R>* coef, const cx<R>* x, cx<R>* y,
+                               const R* link_sigma, const uint64_t* fid, uint64_t seed, const R* inj_lz,
+                               int64_t inj_lz_stride, R* pow_part) {
+  int J = 1;
+  long best = -1;
+  for (int j = 1; j <= 3; ++j) {
+    const long cover = (long)((sym_len + j * MWG - 1) / (j * MWG)) * j * MWG;
+    if (best < 0 || cover <= best) { best = cover; J = j; }
+  }
+  const bool tay = m.n_cs > 1;
+  const size_t shm = channel_tay_lds<R>(m, np);
+  // receive antennas per group: a divisor of num_rx, at most 4
+  const int G = m.num_rx <= 4 ? m.num_rx : m.num_rx % 4 == 0 ? 4 : m.num_rx % 3 == 0 ? 3 : m.num_rx % 2 == 0 ? 2 : 1;
+#define LTE_CHT(J_, G_, T_)                                                                                          \
+  do {                                                                                                               \
+    if (link_sigma)                                                                                                  \
+      hipLaunchKernelGGL((k_channel_tay<R, J_, G_, T_, true>), dim3(nch * B), dim3(MWG), shm, s, L, m.num_rx,       \
+                         m.num_tx, np, m.n_cs, sym_len, delays, coef, x, y, link_sigma, fid, seed, inj_lz,          \
+                         inj_lz_stride, pow_part, nch);                                                              \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_channel_tay<R, J_, G_, T_, false>), dim3(nch * B), dim3(MWG), shm, s, L, m.num_rx,      \
+                         m.num_tx, np, m.n_cs, sym_len, delays, coef, x, y, nullptr, fid, seed, nullptr, 0,         \
+                         pow_part, nch);                                                                             \
+  } while (0)
+#define LTE_CHT_G(J_, T_)                                                                                            \
+  do {                                                                                                               \
+    switch (G) {                                                                                                     \
+      case 4: LTE_CHT(J_, 4, T_); break;                                                                             \
+      case 3: LTE_CHT(J_, 3, T_); break;                                                                             \
+      case 2: LTE_CHT(J_, 2, T_); break;                                                                             \
+      default: LTE_CHT(J_, 1, T_); break;                                                                            \
+    }                                                                                                                \
+  } while (0)
+#define LTE_CHT_J(T_)                                                                                                \
+  do {                                                                                                               \
+    if (J == 1) LTE_CHT_G(1, T_); else if (J == 2) LTE_CHT_G(2, T_); else LTE_CHT_G(3, T_);                          \
+  } while (0)
+  if (tay) LTE_CHT_J(true); else LTE_CHT_J(false);
+#undef LTE_CHT_J
+#undef LTE_CHT_G
+#undef LTE_CHT
 }
 
 template <class R>
@@ -877,6 +1077,9 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
   // per-link vl); measured J = 1 / 2 / 3 / 5 at 20 MHz, f64 config 5 channel
   // 6.0 / 6.0 / 6.8 / 11.2 ms and 3 km/h 26.9 / 19.3 / 27.1 / 41.9 ms per 8192
   // frames; f32 4.2 / 3.1 / 3.0 / 3.2 and 15.9 / 11.0 / 9.6 / 11.3 ms
+  // the coefficient path runs k_channel_tay (LTE_CHM_TAY=0: k_channel_mimo, for A/B)
+  const char* tye = std::getenv("LTE_CHM_TAY");
+  const bool tay_on = !(tye && std::atoi(tye) == 0);
   const int jn = (sym_len + MWG - 1) / MWG;
   const int jmax = sizeof(R) == 8 ? 2 : 3;
   const int J = jn <= 1 ? 1 : jn <= 2 || jmax == 2 ? 2 : 3;
@@ -896,10 +1099,13 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
       hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, nch, g.L,        \
                          link_sigma);                                                                              \
     }                                                                                                              \
-    hipLaunchKernelGGL((k_channel_mimo<R, J_, EX_, G_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, \
-                       n_paths,                                                                                    \
-                       m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x, y, link_noise ? link_sigma : nullptr,   \
-                       fid, seed, inj_lz, inj_lz_stride, pow_part, nch);                                           \
+    if (!(EX_) && tay_on && channel_tay_lds<R>(m, n_paths) <= 32768)                                               \
+      launch_channel_tay<R>(s, B, nch, g.L, m, n_paths, sym_len, delays, coef, x, y,                               \
+                            link_noise ? link_sigma : nullptr, fid, seed, inj_lz, inj_lz_stride, pow_part);        \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_channel_mimo<R, J_, EX_, G_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx,         \
+                         m.num_tx, n_paths, m.n_cs, sym_len, delays, coef, ph, gains, fs, m, x, y,                 \
+                         link_noise ? link_sigma : nullptr, fid, seed, inj_lz, inj_lz_stride, pow_part, nch);      \
   } while (0)
 #define LTE_CHM(J_)                                                                                                 \
   do {                                                                                                             \

@@ -386,6 +386,25 @@ def roofline(config, prec, tim, steps, F, el, value, world, iters=8, plan=None):
     return roof
 
 
+def same_box_shape_ceiling(hrs, F):
+    """The decoder's access-shape ceiling measured on this box after the timed
+    region (scripts/turbo_shape_bench, built with -DLTE_SHAPE_AUX=3, run as a
+    child process): replaces the stored round-3 ceiling from another box."""
+    exe = os.path.join(ROOT, 'scripts', 'turbo_shape_bench')
+    if not os.path.exists(exe) or F % 64:
+        return
+    try:
+        r = subprocess.run([exe, str(F), 'decoder'], capture_output=True, text=True, timeout=180)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return
+    ceil = d['decoder_layout']['GBs_best']
+    tr = hrs.get('traffic_GBs')
+    hrs['shape_ceiling'] = {'GBs': ceil, 'traffic_frac_of_ceiling': round(tr / ceil, 4) if tr else None,
+                            'shape_ms': {k: d['decoder_layout'][k] for k in ('ms_1wps', 'ms_2wps', 'ms_free')},
+                            'source': 'same box, same call: scripts/turbo_shape_bench F decoder after the timed region'}
+
+
 def merge_timers(all_tim):
     """Per stage, the rank whose mean launch time is the largest (the roofline
     prices the slowest rank's kernels, like the step time)."""
@@ -480,6 +499,9 @@ def main():
                          'or PedA Rayleigh at --velocity (3 km/h if 0)')
     ap.add_argument('--cpu-seconds', type=float, default=None)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--shape-ceiling', action='store_true',
+                    help="after the timed region, measure the decoder's access-shape ceiling on this box "
+                         '(scripts/turbo_shape_bench F decoder, a child process) for roofline.hbm_row_stream')
     ap.add_argument('--dry-run', action='store_true', help='no GPU: launcher / sharding / reductions only (gloo)')
     argv = sys.argv[1:]
     args = ap.parse_args()
@@ -616,6 +638,8 @@ def main():
     if rank == 0:
         # BER match on the oracle's sample of this run's own frames (outside the timed region)
         out['ber_match'] = ber_match(plan, cpu, wl['coded']) if plan is not None else None
+        if args.shape_ceiling and plan is not None and out['roofline'] and 'hbm_row_stream' in out['roofline']:
+            same_box_shape_ceiling(out['roofline']['hbm_row_stream'], F)
         if cpu:
             cpu = {k: v for k, v in cpu.items() if k not in ('frames', 'config')}
             if world > 1:

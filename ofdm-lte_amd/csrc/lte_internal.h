@@ -1,5 +1,6 @@
 // Internal (non-ABI) declarations shared by the kernel TUs and the C-ABI TU.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/lte_phy.h"
@@ -118,10 +119,22 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
 template <class R>
 int launch_chan_fix(hipStream_t s, const Grid& g, int B, const TxChannelT<R>& ch);
 // coded TX + channel with one slot per frame (the frame's coded streams staged
-// in LDS once); same outputs as launch_ofdm_tx_ch(coded = 1)
+// in LDS once); same outputs as launch_ofdm_tx_ch(coded = 1).  txf_map / txf_re
+// (both or neither): the bank-aware lane order of plan_txf_lane_order --
+// [n_sym][N/2][bps] sources and [n_sym][N/2] RE of each slot.
 template <class R>
-int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map, int B,
-                    cx<R>* cap_syms, const TxChannelT<R>& ch);
+int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map,
+                    const int32_t* txf_map, const int32_t* txf_re, int B, cx<R>* cap_syms,
+                    const TxChannelT<R>& ch);
+// the lane order: for each OFDM symbol a permutation of its Nd data REs over
+// the N/2 TX slots, greedy per 32-slot group (one ds_read_b32 lane group) so
+// that each of the bps coded-bit gathers sees as few distinct words per LDS
+// bank (word mod 32) as it can, and each 8-slot group (one ds_write_b128 lane
+// group) distinct RE positions mod 8.  tx_map [n_sym][Nd][bps]; returns the
+// modelled extra LDS cycles per 32-lane gather before / after in model[2].
+void plan_txf_lane_order(const std::vector<int32_t>& tx_map, const std::vector<int32_t>& data_idx, int n_sym,
+                         int Nd, int bps, int slots, std::vector<int32_t>& txf_map, std::vector<int32_t>& txf_re,
+                         double model[2]);
 template <class R>
 int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>* y, int64_t y_rx_stride,
                     int64_t y_frame_stride, const R* npow, const uint64_t* fid, uint64_t seed, const R* inj_z,

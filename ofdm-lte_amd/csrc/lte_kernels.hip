@@ -438,9 +438,15 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
 #ifndef TXF_STAGE   // 1: the frame's coded streams staged in LDS; 0: bit gathers through L1 / L2
 #define TXF_STAGE 1
 #endif
+// Lane order (txf_re, plan_txf_lane_order): slot s = tid + q T of symbol l
+// carries RE txf_re[l][s] and reads its coded-bit sources from the slot-ordered
+// copy of tx_map (txf_map[l][s][m]), chosen on the host so that the 32 lanes of
+// each ds_read_b32 gather hit distinct LDS banks; null: slot s = RE s.
 template <class R, int BPS, int NC = 0, bool TV = false>
 __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32_t* __restrict__ enc, int enc_words,
-                                                          const int32_t* __restrict__ tx_map, int B,
+                                                          const int32_t* __restrict__ tx_map,
+                                                          const int32_t* __restrict__ txf_map,
+                                                          const int32_t* __restrict__ txf_re, int B,
                                                           cx<R>* __restrict__ cap_syms, TxChannelT<R> ch) {
   using V = cx<R>;
   using G = GridT<R>;
@@ -465,15 +471,18 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
     int tid = tid0;   // opaque per symbol: address arithmetic is not hoisted out of the loop
     asm volatile("" : "+v"(tid));
     int srcs[QM][BPS];
-    int kpos[QM];
+    int kpos[QM], jre[QM];
 #pragma unroll
     for (int q = 0; q < QM; ++q) {
-      const int j = tid + q * T;
-      const bool ok = active && j < g.Nd;
-      const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
+      const int sl = tid + q * T;
+      const bool ok = active && sl < g.Nd;
+      const int j = txf_re ? (ok ? txf_re[(size_t)l * QM * T + sl] : 0) : sl;
+      const int64_t t0 = txf_re ? ((int64_t)l * QM * T + sl) * BPS : ((int64_t)l * g.Nd + j) * BPS;
+      const int32_t* map = txf_re ? txf_map : tx_map;
 #pragma unroll
-      for (int m = 0; m < BPS; ++m) srcs[q][m] = ok ? tx_map[t0 + m] : -1;
+      for (int m = 0; m < BPS; ++m) srcs[q][m] = ok ? map[t0 + m] : -1;
       kpos[q] = ok ? g.data_idx[j] : 0;
+      jre[q] = j;
 #if LTE_LDS_PROBE & 1   // timing probe only (wrong outputs): conflict-free RE positions
       kpos[q] = ok ? N / 2 - 512 + j : 0;
 #endif
@@ -488,8 +497,7 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
     if (active) {
 #pragma unroll
       for (int q = 0; q < QM; ++q) {
-        const int j = tid + q * T;
-        if (j >= g.Nd) break;
+        if (tid + q * T >= g.Nd) break;
         int idx = 0;
         bool zero = false;
 #pragma unroll
@@ -500,7 +508,7 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
         }
         const V sym = zero ? mkc((R)0, (R)0) : qam_point<BPS, R>(idx);
         buf[kpos[q]] = sym;
-        if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + j] = sym;
+        if (cap_syms) cap_syms[(size_t)b * g.n_sym * g.Nd + (size_t)l * g.Nd + jre[q]] = sym;
       }
       for (int p = tid; p < g.Np; p += T) buf[g.pilot_idx[p]] = G::pilots(g)[p];
     }
@@ -513,8 +521,9 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
 }
 
 template <class R>
-int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map, int B,
-                    cx<R>* cap_syms, const TxChannelT<R>& ch) {
+int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map,
+                    const int32_t* txf_map, const int32_t* txf_re, int B, cx<R>* cap_syms,
+                    const TxChannelT<R>& ch) {
   const int spw = WG / (g.N >> 3);
   if (!txch_supported(g, ch.n_paths, ch.max_delay) || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
   const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + (TXF_STAGE ? (size_t)spw * enc_words * sizeof(uint32_t) : 0);
@@ -524,10 +533,10 @@ int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_w
   do {                                                                                                          \
     if (ch.tcoef)                                                                                               \
       hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_, true>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words,   \
-                         tx_map, B, cap_syms, ch);                                                              \
+                         tx_map, txf_map, txf_re, B, cap_syms, ch);                                             \
     else                                                                                                        \
       hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, tx_map, \
-                         B, cap_syms, ch);                                                                      \
+                         txf_map, txf_re, B, cap_syms, ch);                                                     \
   } while (0)
   if (g.N == 2048) {
     if (g.bps == 2) LTE_TXF(2, 2048); else if (g.bps == 4) LTE_TXF(4, 2048); else LTE_TXF(6, 2048);
@@ -1695,8 +1704,8 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
   template int launch_ofdm_tx_ch<R>(hipStream_t, const Grid&, int, const uint32_t*, int, const uint32_t*, int,       \
                                     const int32_t*, int, cx<R>*, const TxChannelT<R>&, int);                        \
   template int launch_chan_fix<R>(hipStream_t, const Grid&, int, const TxChannelT<R>&);                             \
-  template int launch_ofdm_txf<R>(hipStream_t, const Grid&, const uint32_t*, int, const int32_t*, int, cx<R>*,      \
-                                  const TxChannelT<R>&);                                                             \
+  template int launch_ofdm_txf<R>(hipStream_t, const Grid&, const uint32_t*, int, const int32_t*, const int32_t*,   \
+                                  const int32_t*, int, cx<R>*, const TxChannelT<R>&);                                \
   template int launch_fading<R>(hipStream_t, int, int, int, const R*, const uint64_t*, uint64_t, const R*, int64_t, \
                                 R*, cx<R>*);                                                                         \
   template int launch_jakes_sets<R>(hipStream_t, int, int, int, int, const R*, const R*, double, double, cx<R>*);     \

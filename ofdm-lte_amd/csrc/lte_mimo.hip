@@ -681,6 +681,23 @@ __device__ __forceinline__ cx<R> link_noise_at(int n, R sg, const R* __restrict_
   return mkc(v.x + sg * z.x, v.y + sg * z.y);
 }
 
+// transmit_mimo's 100 dB link noise on the Philox path, per receive antenna:
+// the num_tx links' independent complex Gaussians (standard deviations s_rt,
+// k_link_sigma) sum to one complex Gaussian of standard deviation
+// sqrt(sum_t s_rt^2), drawn once per RX sample on link (r, 0)'s stream -- the
+// same distribution as one draw per link at 1 / num_tx of the draws.  (Injected
+// link noise, the reference's own draws, is still added per link.)
+template <class R>
+__device__ __forceinline__ R rx_link_sigma(const R* __restrict__ link_sigma, size_t lk0, int num_tx) {
+#pragma clang fp contract(off)
+  R s2 = (R)0;
+  for (int t = 0; t < num_tx; ++t) {
+    const R s = link_sigma[lk0 + t];
+    s2 = s2 + s * s;
+  }
+  return sqrt(s2);
+}
+
 // The link noise of a SymSpan's J samples (Philox path; the same values as
 // link_noise_at per sample).  With an even base, lane pair (2k, 2k+1) holds
 // sample pairs (n, n + 1) that share one Philox draw (counter n >> 1): the
@@ -828,21 +845,26 @@ __global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8 && !EX) ? LTE_CHM_G2
         for (int q = 0; q < G; ++q) {
           if (q >= nq) break;
           const int link = (rg + q) * num_tx + tx;
-          if (link_sigma) {
+          if (link_sigma && inj_lz) {
             const R sg = link_sigma[(size_t)b * nl + link];
-            if (inj_lz) {
-              const R* zf = inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L;
+            const R* zf = inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L;
 #pragma unroll
-              for (int j = 0; j < J; ++j)
-                if (sp.ok[j]) acc[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, acc[q][j]);
-            } else {
-              link_noise_span<R, J>(acc[q], sp, sg, seed, fid[b], link, (nbeg & 1) == 0);
-            }
+            for (int j = 0; j < J; ++j)
+              if (sp.ok[j]) acc[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, acc[q][j]);
           }
           if constexpr (F64) {
 #pragma unroll
             for (int j = 0; j < J; ++j) v[q][j] = cadd(v[q][j], vl[q][j]);
           }
+        }
+      }
+      if (link_sigma && !inj_lz) {   // Philox: one draw per RX sample (rx_link_sigma)
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          if (q >= nq) break;
+          const int r = rg + q;
+          const R sr = rx_link_sigma(link_sigma, (size_t)b * nl + (size_t)r * num_tx, num_tx);
+          link_noise_span<R, J>(v[q], sp, sr, seed, fid[b], r * num_tx, (nbeg & 1) == 0);
         }
       }
 #pragma unroll
@@ -961,20 +983,24 @@ __global__ __launch_bounds__(MWG, LTE_CHT_WAVES) void k_channel_tay(int L, int n
             __builtin_amdgcn_sched_barrier(0);   // keep the next antenna's coefficient reads from piling up
           }
         }
-        if (LN) {
+        if (LN && inj_lz) {   // the reference's own draws: per link
 #pragma unroll
           for (int q = 0; q < G; ++q) {
             const int link = (rg + q) * num_tx + tx;
             const R sg = link_sigma[(size_t)b * nl + link];
-            if (inj_lz) {
-              const R* zf = inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L;
+            const R* zf = inj_lz + (size_t)b * inj_lz_stride + (size_t)link * 2 * L;
 #pragma unroll
-              for (int j = 0; j < J; ++j)
-                if (sp.ok[j]) v[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, v[q][j]);
-            } else {
-              link_noise_span<R, J>(v[q], sp, sg, seed, fid[b], link, (nbeg & 1) == 0);
-            }
+            for (int j = 0; j < J; ++j)
+              if (sp.ok[j]) v[q][j] = link_noise_at<R>(sp.n[j], sg, zf, L, seed, fid[b], link, v[q][j]);
           }
+        }
+      }
+      if (LN && !inj_lz) {   // Philox: one draw per RX sample (rx_link_sigma)
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          const int r = rg + q;
+          const R sr = rx_link_sigma(link_sigma, (size_t)b * nl + (size_t)r * num_tx, num_tx);
+          link_noise_span<R, J>(v[q], sp, sr, seed, fid[b], r * num_tx, (nbeg & 1) == 0);
         }
       }
 #pragma unroll
@@ -1125,7 +1151,9 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
 
 // Per-link statistics for the reported channel matrix (transmit_mimo,
 // core/ofdm_core.py:505-516): mean|x|^2, mean|y_link|^2, mean(y_link conj(x)),
-// y_link with its link noise when link_sigma is set (the reference's y).
+// y_link with its link noise when link_sigma is set (the reference's y; on the
+// Philox path each link its own draw, while the RX streams take one combined
+// draw per RX, rx_link_sigma).
 template <class R, bool EX>
 __global__ __launch_bounds__(MWG) void k_link_stats_part(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                          const int32_t* __restrict__ delays,

@@ -136,6 +136,12 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
     Hm = np.zeros((num_rx, num_tx), dtype=complex)
     for r in range(num_rx):
         acc = np.zeros(L, dtype=complex)
+        # the device's Philox mode (draws[r]['combined_link_noise']): the links'
+        # 100 dB noises enter the RX sum as one draw of standard deviation
+        # sqrt(sum_t s_rt^2) on link (r, 0)'s numbers (lte_mimo.hip
+        # rx_link_sigma); each link's own draw still forms its Hm entry
+        comb = channel != 'awgn' and bool(draws[r].get('combined_link_noise'))
+        s2 = 0.0
         for t in range(num_tx):
             x = xs[t]
             if channel == 'awgn':
@@ -147,6 +153,7 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
                 y0 = multipath(x, dl, g, d['phases'], 0.0, num.fs)
                 p = np.mean(np.abs(y0) ** 2)
                 s = np.sqrt((p / 10 ** (100.0 / 10)) / 2)
+                s2 = s2 + s * s
                 y = y0 + (s * d['z_re'] + 1j * (s * d['z_im']))
                 tp = np.mean(np.abs(x) ** 2)
                 rp = np.mean(np.abs(y) ** 2)
@@ -154,8 +161,14 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
                     h = np.sqrt(rp / tp) * np.exp(1j * np.angle(np.mean(y * np.conj(x))))
                 else:
                     h = 1.0 + 0j
+                if comb:
+                    y = y0
             Hm[r, t] = h
             acc += y
+        if comb:
+            s = np.sqrt(s2)
+            z0 = draws[r]['links'][0]
+            acc = acc + (s * z0['z_re'] + 1j * (s * z0['z_im']))
         sp = np.mean(np.abs(acc) ** 2)
         npow = (sp / num_tx) / 10 ** (snr_db / 10)
         s = np.sqrt(npow / 2)

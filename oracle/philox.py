@@ -144,7 +144,9 @@ def siso_draws(seed: int, frame: int, L: int, n_paths: int, n_rx: int = 1):
 # Multi-antenna links (lte_mimo.hip k_fading_mimo / link_noise_at): link = rx *
 # num_tx + tx; path p of a Rayleigh link on STREAM_MIMO_FADE + link * n_paths + p
 # (phase m = output m % 4 of counter m // 4, as k_fading); the 100 dB link noise
-# of transmit_mimo on STREAM_MIMO_LINK + link (samples as the RX noise); a flat
+# of transmit_mimo on STREAM_MIMO_LINK + link (samples as the RX noise; the RX
+# streams take one draw per RX on link (r, 0)'s stream, of standard deviation
+# sqrt(sum_t s_rt^2): mimo_oracle.transmit_mimo 'combined_link_noise'); a flat
 # spatial link h ~ CN(0, 1) = normal(0, 1/sqrt 2) re, im from outputs (x, y) of
 # counter 0x7FFFFFFF on STREAM_MIMO_LINK + link; RX noise on STREAM_NOISE + rx.
 def mimo_phases(seed: int, frame: int, link: int, n_paths: int) -> np.ndarray:
@@ -173,7 +175,7 @@ def sfbc_draws(seed: int, frame: int, L: int, num_rx: int, n_paths: int, num_tx:
             zr, zi = normals(seed, frame, STREAM_MIMO_LINK + link, L)
             links.append({'phases': [ph[p] for p in range(n_paths)], 'z_re': zr, 'z_im': zi})
         zr, zi = normals(seed, frame, STREAM_NOISE + r, L)
-        out.append({'links': links, 'z_re': zr, 'z_im': zi})
+        out.append({'links': links, 'z_re': zr, 'z_im': zi, 'combined_link_noise': True})
     return out
 
 

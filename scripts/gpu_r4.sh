@@ -39,7 +39,7 @@ for s in "$@"; do
       extra=${arg#*:}
       [ "$extra" = "$arg" ] && extra=""
       tag=c${cfg}${extra//[^a-zA-Z0-9]/_}
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$tag" -o run -- \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o run -- \
         python3 bench.py --config "$cfg" --gpus 1 --steps 20 --warmup 5 ${extra//,/ } > "$OUT/prof_$tag.json" \
         2> "$OUT/prof_$tag.err" || { tail -20 "$OUT/prof_$tag.err"; exit 1; }
       cut -c1-300 "$OUT/prof_$tag.json"

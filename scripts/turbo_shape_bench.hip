@@ -17,6 +17,7 @@
 // with and without the checkpoint rows, and with two waves per SIMD; _seq:
 // decoder 2 addressed in natural order (what a QPP-free layout would reach).
 // Build: hipcc -O3 --offload-arch=gfx950 -o scripts/turbo_shape_bench scripts/turbo_shape_bench.hip
+// Usage: turbo_shape_bench [frames] [decoder]   (decoder: the decoder's layout only, one JSON line)
 // (-DLTE_SHAPE_AUX=3: the decoder's sc0|nt policy, LTE_TURBO_CPOL).  The
 // CH lines place the rows of CH consecutive waves side by side, as the decoder
 // does since round 3 (TURBO_CH = 32, lte_internal.h); "decoder_layout" is that
@@ -24,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
@@ -244,6 +246,19 @@ int main(int argc, char** argv) {
     (void)hipEventElapsedTime(&ms, a, b);
     return ms / 3.0;
   };
+  if (argc > 2 && std::string(argv[2]) == "decoder") {   // the decoder's layout only (bench.py --shape-ceiling)
+    const double a1 = run(true, 96 * 1024, false, 32), a2 = run(true, 64 * 1024, false, 32), a3 = run(true, 0, false, 32);
+    const double best = a1 < a2 ? (a1 < a3 ? a1 : a3) : (a2 < a3 ? a2 : a3);
+    if (hipDeviceSynchronize() != hipSuccess) {
+      printf("kernel failed\n");
+      return 1;
+    }
+    printf("{\"frames\": %d, \"waves\": %d, \"bytes_per_launch_ckpt\": %.0f, \"decoder_layout\": {\"CH\": 32, "
+           "\"aux\": %d, \"ms_1wps\": %.3f, \"ms_2wps\": %.3f, \"ms_free\": %.3f, \"GBs_best\": %.1f}}\n",
+           F, waves, bytes_ck, LTE_SHAPE_AUXL, a1, a2, a3, bytes_ck / (best * 1e-3) / 1e9);
+    for (void* p : bufs) (void)hipFree(p);
+    return 0;
+  }
   const double m1 = run(true, 96 * 1024), m0 = run(false, 96 * 1024), m2 = run(true, 64 * 1024),
                m3 = run(true, 0), m4 = run(true, 96 * 1024, true), m5 = run(true, 0, true);
   if (hipDeviceSynchronize() != hipSuccess) {

@@ -338,31 +338,33 @@ def stage_bytes_per_frame(config, plan, prec):
     y = n_sym * nr * plan.n_dsc * c
     h = nr * plan.n_est * nt * plan.n_dsc * c
     return {'ofdm_tx': ('k_ofdm_tx_mimo', bits + nt * L * c),
-            'channel': ('k_channel_mimo', (nt + nr) * L * c),
+            'channel': ('k_fading_mimo + k_channel_tay (k_channel_mimo: exact Jakes)', (nt + nr) * L * c),
             'rx_chest': ('k_rx_fft_mimo', nr * L * c + y + h),
             'rx_data': ('k_det_spatial', y + h + bits)}
 
 
-def hbm_roofline(config, plan, prec, tim, F):
+def hbm_roofline(config, plan, prec, tim, F, steps):
     """Uncoded configs: the dominant timed stage against the HBM roofline --
-    its algorithmic bytes per frame x frames / its mean launch time."""
+    its algorithmic bytes per frame x frames / its time per step (a stage's
+    timer may cover several launches per step: config 5's channel stage is
+    k_fading_mimo + the channel kernel)."""
     sb = stage_bytes_per_frame(config, plan, prec)
     stages = {k: v for k, v in tim.items() if k in sb and v[1]}
     if not stages:
         return None
-    dom = max(stages, key=lambda k: stages[k][0] / stages[k][1])
+    dom = max(stages, key=lambda k: stages[k][0])
     t_ms, n = stages[dom]
-    avg_s = t_ms / n * 1e-3
+    st_s = t_ms / steps * 1e-3
     kern, b = sb[dom]
-    gbs = b * F / avg_s / 1e9
+    gbs = b * F / st_s / 1e9
     return {'bound': 'hbm', 'kernel': kern, 'stage': dom, 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
-            'alg_bytes_per_frame': round(b), 'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': n,
-            'frames_per_launch': F,
-            'what': 'algorithmic stage-boundary bytes (the streams the kernel must read / write) x frames / '
-                    'mean launch time (HIP events on the plan stream)',
-            'other_stages': {k: {'kernel': sb[k][0], 'ms': round(v[0] / v[1], 3),
-                                 'GBs': round(sb[k][1] * F / (v[0] / v[1] * 1e-3) / 1e9, 1)}
+            'alg_bytes_per_frame': round(b), 'stage_ms_per_step': round(st_s * 1e3, 3), 'launches': n,
+            'steps': steps, 'frames_per_step': F,
+            'what': 'algorithmic stage-boundary bytes (the streams the stage must read / write) x frames / '
+                    'the stage time per step (HIP events on the plan stream)',
+            'other_stages': {k: {'kernel': sb[k][0], 'ms_per_step': round(v[0] / steps, 3),
+                                 'GBs': round(sb[k][1] * F / (v[0] / steps * 1e-3) / 1e9, 1)}
                              for k, v in stages.items() if k != dom}}
 
 
@@ -379,7 +381,7 @@ def roofline(config, prec, tim, steps, F, el, value, world, iters=8, plan=None):
                                     'achieved_GBs': round(B_SF_F32 * esz / 4 * value / world / 1e9, 2),
                                     'frac': round(B_SF_F32 * esz / 4 * value / world / 1e9 / HBM_PEAK_GBS, 5)}
     else:
-        roof = hbm_roofline(config, plan, prec, tim, F) if plan is not None else None
+        roof = hbm_roofline(config, plan, prec, tim, F, steps) if plan is not None else None
         if roof is None:
             return None
     roof['kernel_ms_per_step'] = {k: round(v[0] / steps, 3) for k, v in tim.items() if v[1]}

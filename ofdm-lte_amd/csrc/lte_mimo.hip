@@ -24,6 +24,7 @@
 #include "lte_internal.h"
 #include "lte_dev.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace lte {
@@ -43,8 +44,10 @@ __device__ __forceinline__ V* mimo_lds() {
 // Spatial (core/ofdm_core.py:2596-2655): layer c = q[R j + c] on data SC j <
 // ceil(Nd/R) (Q20), x_t = sum_c W[t][c] layer_c.  Pilots: TX t at its subset
 // (cell t % 4).  x = ifft(grid) sqrt(N) (tx_scale), CP prepended.
-template <class R, int CODED, int BPS>
-__device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fe,
+// QAM code of coded symbol q: the constellation index, or -1 for a padding
+// symbol (zero)
+template <int CODED, int BPS>
+__device__ __forceinline__ int qam_code(int64_t q, const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fe,
                                         const int32_t* __restrict__ tx_map) {
   int idx = 0;
   bool zero = false;
@@ -59,7 +62,16 @@ __device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ 
 #pragma unroll
     for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, q * BPS + m);
   }
-  return zero ? mkc((R)0, (R)0) : qam_point<BPS, R>(idx);
+  return zero ? -1 : idx;
+}
+template <class R, int BPS>
+__device__ __forceinline__ cx<R> qam_of(int code) {
+  return code < 0 ? mkc((R)0, (R)0) : qam_point<BPS, R>(code);
+}
+template <class R, int CODED, int BPS>
+__device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fe,
+                                        const int32_t* __restrict__ tx_map) {
+  return qam_of<R, BPS>(qam_code<CODED, BPS>(q, fb, fe, tx_map));
 }
 
 // transmit_mimo's per-link power pass (core/ofdm_core.py:490-503: each
@@ -75,7 +87,7 @@ __device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ 
 // frame's coded streams staged in LDS once instead of once per pair (as
 // k_ofdm_txf does for SISO); otherwise one slot per (frame, symbol, TX).
 template <class R, int MODE, int CODED, int BPS, int NC = 0, bool PF = false>
-__global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
+__global__ __launch_bounds__(MWG, PF ? 3 : 1) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                       const uint32_t* __restrict__ enc, int enc_words,
                                                       const int32_t* __restrict__ tx_map, cx<R>* __restrict__ x,
                                                       int B, int stage_enc, TxLinkPower<R> lp) {
@@ -98,12 +110,34 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
       for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
     fe = es;
   }
+  // PF SFBC: each thread's Alamouti pairs (at most SFP per symbol) keep their
+  // QAM codes from TX 0 to TX 1 of the same symbol (the bit gathers once)
+  constexpr int SFP = 4;
+  int qc[SFP][2];
   for (int lt = lt0; lt < lt1; ++lt) {
   const int l = lt / m.num_tx, t = lt - l * m.num_tx;
   if (active)
     for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
   __syncthreads();   // (first pair: also the staged streams)
-  if (active) {
+  if (active && MODE == MIMO_SFBC && PF) {   // one thread per pair, both REs
+    const uint32_t* fb = pw + (size_t)b * PW;
+    const int64_t q0 = (int64_t)l * m.res;
+#pragma unroll
+    for (int k = 0; k < SFP; ++k) {
+      const int j = 2 * (tid + k * T);
+      if (j >= m.n_dsc) break;
+      if (t == 0) {
+        qc[k][0] = qam_code<CODED, BPS>(q0 + j, fb, fe, tx_map);
+        qc[k][1] = qam_code<CODED, BPS>(q0 + j + 1, fb, fe, tx_map);
+      }
+      const V s0 = qam_of<R, BPS>(qc[k][0]), s1 = qam_of<R, BPS>(qc[k][1]);
+      buf[g.data_idx[j]] = t == 0 ? s0 : s1;
+      if (j + 1 < m.n_dsc) buf[g.data_idx[j + 1]] = t == 0 ? mkc(-s1.x, s1.y) : mkc(s0.x, -s0.y);
+    }
+    const int npt = m.np_tx[t];
+    const V* pv = MGT<R>::pval(m) + t * m.maxP;
+    for (int p = tid; p < npt; p += T) buf[m.ppos[t * m.maxP + p]] = pv[p];
+  } else if (active) {
     const uint32_t* fb = pw + (size_t)b * PW;
     const int64_t q0 = (int64_t)l * m.res;
     for (int j = tid; j < m.n_dsc; j += T) {
@@ -144,31 +178,52 @@ __global__ __launch_bounds__(MWG) void k_ofdm_tx_mimo(Grid g, MimoGrid m, const 
     int dl[TXCH_MAXP];
 #pragma unroll
     for (int p = 0; p < TXCH_MAXP; ++p) dl[p] = p < np ? g.cp + lp.delays[p] : 0;
-    for (int r = 0; r < m.num_rx; ++r) {
-      R pwr = (R)0;
-      if (active) {
-        const V* cf = lp.coef + (((size_t)b * m.num_rx + r) * m.num_tx + t) * np * NCF;
-        V c[TXCH_MAXP];
+    // receive antennas in groups of LPG: each delayed sample x(j - d_p) is
+    // read from LDS (and scaled) once for the group's links
+    constexpr int LPG = 1;
+    for (int r0 = 0; r0 < m.num_rx; r0 += LPG) {
+      R pwr[LPG];
 #pragma unroll
-        for (int p = 0; p < TXCH_MAXP; ++p) c[p] = p < np ? cf[p * NCF] : mkc((R)0, (R)0);
+      for (int q = 0; q < LPG; ++q) pwr[q] = (R)0;
+      if (active) {
+        V c[LPG][TXCH_MAXP];
+#pragma unroll
+        for (int q = 0; q < LPG; ++q) {
+          const int r = min(r0 + q, m.num_rx - 1);
+          const V* cf = lp.coef + (((size_t)b * m.num_rx + r) * m.num_tx + t) * np * NCF;
+#pragma unroll
+          for (int p = 0; p < TXCH_MAXP; ++p) c[q][p] = p < np ? cf[p * NCF] : mkc((R)0, (R)0);
+        }
         for (int j = D + tid; j < S; j += T) {
-          V acc = mkc((R)0, (R)0);
+          V acc[LPG];
+#pragma unroll
+          for (int q = 0; q < LPG; ++q) acc[q] = mkc((R)0, (R)0);
 #pragma unroll
           for (int p = 0; p < TXCH_MAXP; ++p)
-            if (p < np) acc = cadd(acc, cmul(c[p], cscale(buf[(j - dl[p]) & (N - 1)], sc)));
-          pwr += acc.x * acc.x + acc.y * acc.y;
+            if (p < np) {
+              const V xv = cscale(buf[(j - dl[p]) & (N - 1)], sc);
+#pragma unroll
+              for (int q = 0; q < LPG; ++q) acc[q] = cadd(acc[q], cmul(c[q][p], xv));
+            }
+#pragma unroll
+          for (int q = 0; q < LPG; ++q) pwr[q] += acc[q].x * acc[q].x + acc[q].y * acc[q].y;
         }
       }
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) pwr += __shfl_xor(pwr, o);
-      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pwr;
-      __syncthreads();
-      if (active && tid == 0) {
-        R tot = (R)0;
-        for (int w = 0; w < T / 64; ++w) tot += red[slot * (T / 64) + w];
-        lp.part[(((size_t)b * m.num_rx + r) * m.num_tx + t) * lp.nblk + l] = tot;
+      for (int q = 0; q < LPG; ++q) {
+        if (r0 + q >= m.num_rx) break;
+        R pv = pwr[q];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) pv += __shfl_xor(pv, o);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pv;
+        __syncthreads();
+        if (active && tid == 0) {
+          R tot = (R)0;
+          for (int w = 0; w < T / 64; ++w) tot += red[slot * (T / 64) + w];
+          lp.part[(((size_t)b * m.num_rx + r0 + q) * m.num_tx + t) * lp.nblk + l] = tot;
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
   if (PF) __syncthreads();   // the next pair zeroes buf
@@ -905,6 +960,14 @@ __global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8 && !EX) ? LTE_CHM_G2
 //    add each (link, path) product straight into the RX sum (the reference
 //    sums each link first -- a different rounding order only, within the
 //    1e-12 stream bars).
+#ifndef LTE_CHT_SB   // 1: a scheduling barrier after each antenna (its coefficient reads not hoisted)
+#define LTE_CHT_SB 0
+#endif
+#if LTE_CHT_SB
+#define LTE_CHT_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define LTE_CHT_SCHED_BARRIER() ((void)0)
+#endif
 #ifndef LTE_CHT_WAVES   // k_channel_tay: minimum waves per SIMD asked of the register allocator
 #define LTE_CHT_WAVES 4
 #endif
@@ -980,7 +1043,7 @@ __global__ __launch_bounds__(MWG, LTE_CHT_WAVES) void k_channel_tay(int L, int n
               v[q][j].x = fma(h[j].x, xs[j].x, fma(-h[j].y, xs[j].y, v[q][j].x));
               v[q][j].y = fma(h[j].x, xs[j].y, fma(h[j].y, xs[j].x, v[q][j].y));
             }
-            __builtin_amdgcn_sched_barrier(0);   // keep the next antenna's coefficient reads from piling up
+            LTE_CHT_SCHED_BARRIER();
           }
         }
         if (LN && inj_lz) {   // the reference's own draws: per link
@@ -1054,7 +1117,13 @@ static void launch_channel_tay(hipStream_t s, int B, int nch, int L, const MimoG
   const bool tay = m.n_cs > 1;
   const size_t shm = channel_tay_lds<R>(m, np);
   // receive antennas per group: a divisor of num_rx, at most 4
-  const int G = m.num_rx <= 4 ? m.num_rx : m.num_rx % 4 == 0 ? 4 : m.num_rx % 3 == 0 ? 3 : m.num_rx % 2 == 0 ? 2 : 1;
+  int G = m.num_rx <= 4 ? m.num_rx : m.num_rx % 4 == 0 ? 4 : m.num_rx % 3 == 0 ? 3 : m.num_rx % 2 == 0 ? 2 : 1;
+  // A/B overrides (LTE_CHT_J in 1..3; LTE_CHT_G a divisor of num_rx up to 4)
+  if (const char* e = std::getenv("LTE_CHT_J")) J = std::min(3, std::max(1, std::atoi(e)));
+  if (const char* e = std::getenv("LTE_CHT_G")) {
+    const int g = std::atoi(e);
+    if (g >= 1 && g <= 4 && m.num_rx % g == 0) G = g;
+  }
 #define LTE_CHT(J_, G_, T_)                                                                                          \
   do {                                                                                                               \
     if (link_sigma)                                                                                                  \

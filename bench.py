@@ -501,9 +501,9 @@ def main():
                          'or PedA Rayleigh at --velocity (3 km/h if 0)')
     ap.add_argument('--cpu-seconds', type=float, default=None)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--shape-ceiling', action='store_true',
-                    help="after the timed region, measure the decoder's access-shape ceiling on this box "
-                         '(scripts/turbo_shape_bench F decoder, a child process) for roofline.hbm_row_stream')
+    ap.add_argument('--no-shape-ceiling', action='store_true',
+                    help="skip measuring the decoder's access-shape ceiling on this box after the timed region "
+                         '(scripts/turbo_shape_bench F decoder, a child process; N = 1, coded configs)')
     ap.add_argument('--dry-run', action='store_true', help='no GPU: launcher / sharding / reductions only (gloo)')
     argv = sys.argv[1:]
     args = ap.parse_args()
@@ -640,7 +640,8 @@ def main():
     if rank == 0:
         # BER match on the oracle's sample of this run's own frames (outside the timed region)
         out['ber_match'] = ber_match(plan, cpu, wl['coded']) if plan is not None else None
-        if args.shape_ceiling and plan is not None and out['roofline'] and 'hbm_row_stream' in out['roofline']:
+        if (not args.no_shape_ceiling and world == 1 and prec == 'f64' and plan is not None and out['roofline']
+                and 'hbm_row_stream' in out['roofline']):
             same_box_shape_ceiling(out['roofline']['hbm_row_stream'], F)
         if cpu:
             cpu = {k: v for k, v in cpu.items() if k not in ('frames', 'config')}

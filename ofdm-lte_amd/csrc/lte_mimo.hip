@@ -25,6 +25,7 @@
 #include "lte_dev.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 namespace lte {
@@ -971,7 +972,7 @@ __global__ __launch_bounds__(MWG, (G == 2 && sizeof(R) == 8 && !EX) ? LTE_CHM_G2
 #ifndef LTE_CHT_WAVES   // k_channel_tay: minimum waves per SIMD asked of the register allocator
 #define LTE_CHT_WAVES 4
 #endif
-template <class R, int J, int G, bool TAY, bool LN>
+template <class R, int J, int G, bool TAY, bool LN, bool EC = false>
 __global__ __launch_bounds__(MWG, LTE_CHT_WAVES) void k_channel_tay(int L, int num_rx, int num_tx, int np, int n_cs, int sym_len,
                                                      const int32_t* __restrict__ delays,
                                                      const cx<R>* __restrict__ coef, const cx<R>* __restrict__ x,
@@ -981,7 +982,7 @@ __global__ __launch_bounds__(MWG, LTE_CHT_WAVES) void k_channel_tay(int L, int n
                                                      R* __restrict__ pow_part, int nblk) {
   using V = cx<R>;
   constexpr int NCF = mimo_ncf<R>();   // stored terms per (path, symbol)
-  constexpr int K = TAY ? NCF : 1;     // terms evaluated
+  constexpr int K = TAY ? (EC ? NCF - 1 : NCF) : 1;   // terms evaluated
   __shared__ R red[MWG / 64];
   V* cl = mimo_lds<V>();               // [num_rx][num_tx][np][K]
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
@@ -992,9 +993,22 @@ __global__ __launch_bounds__(MWG, LTE_CHT_WAVES) void k_channel_tay(int L, int n
   {
     const size_t ps = (size_t)n_cs * NCF;
     const V* cb = coef + (size_t)b * nl * np * ps + (size_t)sidx * NCF;
+    // EC: the degree-5 set economised to degree 4 over the symbol, d in
+    // [-D, D]: c5 d^5 = c5 D^5 (T5(u) + 20 u^3 - 5 u) / 16, u = d / D, keeps
+    // c3 + (5/4) D^2 c5 and c1 - (5/16) D^4 c5 and drops c5 D^5 T5(u) / 16
+    // (|T5| <= 1; the host enables it while that is below 1e-17 of the gain)
+    const R D = (R)0.5 * (R)(sym_len - 1);
     for (int i = threadIdx.x; i < nl * np * K; i += MWG) {
       const int lp = i / K, k = i - lp * K;
-      cl[i] = cb[(size_t)lp * ps + k];
+      V c = cb[(size_t)lp * ps + k];
+      if constexpr (EC) {
+        if (k == 1 || k == 3) {
+          const V c5 = cb[(size_t)lp * ps + 5];
+          const R f = k == 1 ? -(R)0.3125 * (D * D) * (D * D) : (R)1.25 * (D * D);
+          c = mkc(c.x + f * c5.x, c.y + f * c5.y);
+        }
+      }
+      cl[i] = c;
     }
   }
   __syncthreads();
@@ -1092,6 +1106,19 @@ size_t channel_tay_lds(const MimoGrid& m, int np) {
   return (size_t)m.num_rx * m.num_tx * np * (m.n_cs > 1 ? mimo_ncf<R>() : 1) * sizeof(cx<R>);
 }
 
+// k_channel_tay's degree-4 economisation holds the per-sample error under
+// 1e-17 of the path gain: |c5| <= sqrt(2/16) 16 W^5 / 5! for the fastest
+// sinusoid W = max |w_m| / fs, so |c5| D^5 / 16 <= 5.657 (W D)^5 / 1920 with D
+// the half symbol (3 km/h at 20 MHz: W D = 1.245e-3, 2.5 % inside the bound)
+static bool channel_tay_econ(const MimoGrid& m, int sym_len, double fs) {
+  if (const char* e = std::getenv("LTE_CHT_ECON"))
+    if (std::atoi(e) == 0) return false;
+  double w = 0.0;
+  for (int k = 0; k < 16; ++k) w = std::max(w, std::fabs(m.jw[k]));
+  const double x = w / fs * 0.5 * (sym_len - 1);
+  return 5.657 * x * x * x * x * x / 1920.0 <= 1e-17;
+}
+
 int mimo_channel_nblk(int L, int sym_len) { return (L + sym_len - 1) / sym_len; }
 
 // power partials per (frame, RX) the channel pass writes: one per OFDM symbol
@@ -1105,7 +1132,7 @@ int mimo_channel_pblk(const Grid& g, const MimoGrid&) {
 // fewest idle lanes (20 MHz: 3 -> 2304 lanes for 2192 samples)
 template <class R>
 static void launch_channel_tay(hipStream_t s, int B, int nch, int L, const MimoGrid& m, int np, int sym_len,
-                               const int32_t* delays, const cx<R>* coef, const cx<R>* x, cx<R>* y,
+                               double fs, const int32_t* delays, const cx<R>* coef, const cx<R>* x, cx<R>* y,
                                const R* link_sigma, const uint64_t* fid, uint64_t seed, const R* inj_lz,
                                int64_t inj_lz_stride, R* pow_part) {
   int J = 1;
@@ -1124,30 +1151,36 @@ static void launch_channel_tay(hipStream_t s, int B, int nch, int L, const MimoG
     const int g = std::atoi(e);
     if (g >= 1 && g <= 4 && m.num_rx % g == 0) G = g;
   }
-#define LTE_CHT(J_, G_, T_)                                                                                          \
+#define LTE_CHT(J_, G_, T_, E_)                                                                                      \
   do {                                                                                                               \
     if (link_sigma)                                                                                                  \
-      hipLaunchKernelGGL((k_channel_tay<R, J_, G_, T_, true>), dim3(nch * B), dim3(MWG), shm, s, L, m.num_rx,       \
+      hipLaunchKernelGGL((k_channel_tay<R, J_, G_, T_, true, E_>), dim3(nch * B), dim3(MWG), shm, s, L, m.num_rx,   \
                          m.num_tx, np, m.n_cs, sym_len, delays, coef, x, y, link_sigma, fid, seed, inj_lz,          \
                          inj_lz_stride, pow_part, nch);                                                              \
     else                                                                                                             \
-      hipLaunchKernelGGL((k_channel_tay<R, J_, G_, T_, false>), dim3(nch * B), dim3(MWG), shm, s, L, m.num_rx,      \
+      hipLaunchKernelGGL((k_channel_tay<R, J_, G_, T_, false, E_>), dim3(nch * B), dim3(MWG), shm, s, L, m.num_rx,  \
                          m.num_tx, np, m.n_cs, sym_len, delays, coef, x, y, nullptr, fid, seed, nullptr, 0,         \
                          pow_part, nch);                                                                             \
   } while (0)
-#define LTE_CHT_G(J_, T_)                                                                                            \
+#define LTE_CHT_G(J_, T_, E_)                                                                                        \
   do {                                                                                                               \
     switch (G) {                                                                                                     \
-      case 4: LTE_CHT(J_, 4, T_); break;                                                                             \
-      case 3: LTE_CHT(J_, 3, T_); break;                                                                             \
-      case 2: LTE_CHT(J_, 2, T_); break;                                                                             \
-      default: LTE_CHT(J_, 1, T_); break;                                                                            \
+      case 4: LTE_CHT(J_, 4, T_, E_); break;                                                                         \
+      case 3: LTE_CHT(J_, 3, T_, E_); break;                                                                         \
+      case 2: LTE_CHT(J_, 2, T_, E_); break;                                                                         \
+      default: LTE_CHT(J_, 1, T_, E_); break;                                                                        \
     }                                                                                                                \
   } while (0)
 #define LTE_CHT_J(T_)                                                                                                \
   do {                                                                                                               \
-    if (J == 1) LTE_CHT_G(1, T_); else if (J == 2) LTE_CHT_G(2, T_); else LTE_CHT_G(3, T_);                          \
+    if (J == 1) LTE_CHT_G(1, T_, false); else if (J == 2) LTE_CHT_G(2, T_, false); else LTE_CHT_G(3, T_, false);     \
   } while (0)
+  if constexpr (sizeof(R) == 8) {   // the economised degree-4 sets (f64 Taylor path, J = 3)
+    if (tay && J == 3 && channel_tay_econ(m, sym_len, fs)) {
+      LTE_CHT_G(3, true, true);
+      return;
+    }
+  }
   if (tay) LTE_CHT_J(true); else LTE_CHT_J(false);
 #undef LTE_CHT_J
 #undef LTE_CHT_G
@@ -1195,7 +1228,7 @@ int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, 
                          link_sigma);                                                                              \
     }                                                                                                              \
     if (!(EX_) && tay_on && channel_tay_lds<R>(m, n_paths) <= 32768)                                               \
-      launch_channel_tay<R>(s, B, nch, g.L, m, n_paths, sym_len, delays, coef, x, y,                               \
+      launch_channel_tay<R>(s, B, nch, g.L, m, n_paths, sym_len, fs, delays, coef, x, y,                           \
                             link_noise ? link_sigma : nullptr, fid, seed, inj_lz, inj_lz_stride, pow_part);        \
     else                                                                                                           \
       hipLaunchKernelGGL((k_channel_mimo<R, J_, EX_, G_>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx,         \

@@ -149,7 +149,11 @@ def test_ofdm_channel_transmit_moving_vs_oracle(C, oracle, kmh, prec, tol):
     assert np.linalg.norm(y - ref) / np.linalg.norm(ref) < tol
 
 
-@pytest.mark.parametrize('prec,tol,kmh', [('f64', 1e-12, 30.0), ('f64', 1e-12, 120.0), ('f64', 1e-12, 500.0),
+# (3 and 6 km/h: the per-symbol sets evaluated at degree 4 after Chebyshev
+# economisation, k_channel_tay EC -- inside its 1e-17 bound for this stage's
+# 1024-sample symbols up to ~6.5 km/h)
+@pytest.mark.parametrize('prec,tol,kmh', [('f64', 1e-12, 3.0), ('f64', 1e-12, 6.0), ('f64', 1e-12, 30.0),
+                                          ('f64', 1e-12, 120.0), ('f64', 1e-12, 500.0),
                                           ('f32', 1e-5, 30.0), ('f32', 1e-5, 120.0), ('f32', 1e-5, 500.0)])
 def test_spatial_multiplexing_channel_moving_vs_oracle(C, mimo_oracle, oracle, kmh, prec, tol):
     import lte_phy
@@ -168,3 +172,23 @@ def test_spatial_multiplexing_channel_moving_vs_oracle(C, mimo_oracle, oracle, k
     for r in range(4):
         assert np.linalg.norm(ys[r] - ref[r]) / np.linalg.norm(ref[r]) < tol, r
     assert np.allclose(Hm, Href, rtol=1e-9 if prec == 'f64' else 1e-5, atol=1e-12 if prec == 'f64' else 1e-6)
+
+
+def test_channel_economised_sets_match_degree5(C, monkeypatch):
+    """k_channel_tay's degree-4 economised sets (LTE_CHT_ECON, on by default
+    where the bound holds) against the degree-5 sets: the 4x4 PedA links at
+    3 km/h, the same draws, streams equal to 1e-14."""
+    import lte_phy
+    rs = np.random.RandomState(7)
+    xs = [(rs.randn(8 * 2192) + 1j * rs.randn(8 * 2192)) / np.sqrt(2) for _ in range(4)]
+    out = []
+    for econ in ('1', '0'):
+        monkeypatch.setenv('LTE_CHT_ECON', econ)
+        cs = lte_phy.ChannelSimulator(channel_type='rayleigh_mp', snr_db=18.0, fs=30.72e6,
+                                      itu_profile='Pedestrian_A', frequency_ghz=2.0, velocity_kmh=3.0,
+                                      verbose=False, precision='f64')
+        np.random.seed(99)
+        ys, _ = cs.transmit_spatial_multiplexing(list(xs), num_rx=4)
+        out.append(ys)
+    for a, b in zip(*out):
+        assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-14

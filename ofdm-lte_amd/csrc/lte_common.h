@@ -94,6 +94,9 @@ __device__ __forceinline__ double log1p_small(double r) {   // |r| <= 2^-8, erro
   return r * (1.0 + r * (-0.5 + r * (0x1.5555555555555p-2 + r * (-0.25 + r * (0.2 + r * (-0x1.5555555555555p-3 +
                                                                                           r * 0x1.2492492492492p-3))))));
 }
+#ifndef LTE_BM_SELECT   // 0: the three ln u cases as branches (A/B)
+#define LTE_BM_SELECT 1
+#endif
 __device__ __forceinline__ double ln_u32(uint32_t a) {
   const double x = (double)a + 0.5;   // exact
   const uint64_t bx = (uint64_t)__double_as_longlong(x);
@@ -107,9 +110,17 @@ __device__ __forceinline__ double ln_u32(uint32_t a) {
   const double r = near1 ? -d : (m - c) * t.x;                    // m - c exact
   const double p = log1p_small(r);
   const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
+  // the three cases as selects, not branches: a wave's lanes split about
+  // evenly between u < 1/2 and u >= 1/2, so branches ran both paths anyway
+#if LTE_BM_SELECT
+  const double lh = BM_LH[i] + p;
+  const double gen = (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
+  return near1 ? p : (e == -1 ? lh : gen);
+#else
   if (near1) return p;
   if (e == -1) return BM_LH[i] + p;
   return (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
+#endif
 }
 __device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b) {
   const double r = sqrt(-2.0 * ln_u32(a));

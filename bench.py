@@ -71,7 +71,7 @@ WORKLOADS = {
         'n_bits': 14 * 499 * 4,
         'desc': 'config 3: SIMO 1x4 MRC, 10 MHz (N=1024) 16-QAM, Rayleigh ITU Vehicular-A per RX antenna, '
                 '14 OFDM symbols (27944 bits) uncoded, SNR 0:2:30 dB'},
-    4: {'short': 'config 4: SFBC 2x2 + turbo, 20 MHz, 64-QAM, Rayleigh', 'frames': 49152, 'coded': True,
+    4: {'short': 'config 4: SFBC 2x2 + turbo, 20 MHz, 64-QAM, Rayleigh', 'frames': 65536, 'coded': True,
         'n_bits': TB,
         'desc': 'config 4: Tx diversity 2x2 Alamouti SFBC + turbo max-log-MAP 8 it., 20 MHz 64-QAM, Rayleigh ITU '
                 'Pedestrian-A per link (transmit_mimo), TB 27760, SNR 0:2:30 dB'},

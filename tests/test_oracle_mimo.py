@@ -136,3 +136,41 @@ def test_sfbc_coded_fixture_frames(oracle, mimo_oracle, fixture_curve_c4):
     for s, f in [(8, 3), (12, 0)]:
         _, _, err, crc = mk.one_c4((s, f))
         assert err == int(fixture_curve_c4['bit_errors'][s, f]) and crc == int(fixture_curve_c4['crc_ok'][s, f])
+
+
+def test_transmit_mimo_combined_link_noise(golden_mimo, oracle, mimo_oracle):
+    """The device's Philox mode for transmit_mimo (draws[r]['combined_link_noise']):
+    the RX stream takes the faded links' sum plus ONE draw of standard deviation
+    sqrt(sum_t s_rt^2) on link (r, 0)'s numbers, while the reported channel
+    matrix keeps each link's own draw -- against the per-link form on the same
+    draws: Hm identical, the noise-free parts equal, and the difference of the
+    streams exactly the two noise terms (before the RX noise, which the
+    measured power then scales)."""
+    num = _num(oracle, 20.0, '64-QAM')
+    xs = [golden_mimo['txmimo_x0'], golden_mimo['txmimo_x1']]
+    L = len(xs[0])
+    np.random.seed(5)
+    draws = mimo_oracle.transmit_mimo_draws(2, 2, 'rayleigh_mp', L)
+    comb = [dict(d, combined_link_noise=True) for d in draws]
+    # RX noise off (huge SNR) so the streams show the link noise alone
+    ys_a, H_a = mimo_oracle.transmit_mimo(num, xs, 2, 'rayleigh_mp', 400.0, draws=draws)
+    ys_b, H_b = mimo_oracle.transmit_mimo(num, xs, 2, 'rayleigh_mp', 400.0, draws=comb)
+    assert np.array_equal(H_a, H_b)
+    dl, g = mimo_oracle.itu_paths(num, 'Pedestrian_A')
+    for r in range(2):
+        s2, y0 = 0.0, np.zeros(L, dtype=complex)
+        per_link = np.zeros(L, dtype=complex)
+        for t in range(2):
+            d = draws[r]['links'][t]
+            y = mimo_oracle.multipath(xs[t], dl, g, d['phases'], 0.0, num.fs)
+            s = np.sqrt((np.mean(np.abs(y) ** 2) / 1e10) / 2)
+            s2 = s2 + s * s
+            y0 += y
+            per_link += s * d['z_re'] + 1j * (s * d['z_im'])
+        z0 = draws[r]['links'][0]
+        sr = np.sqrt(s2)
+        comb_noise = sr * z0['z_re'] + 1j * (sr * z0['z_im'])
+        assert np.allclose(ys_a[r], y0 + per_link, rtol=0, atol=1e-12)
+        assert np.allclose(ys_b[r], y0 + comb_noise, rtol=0, atol=1e-12)
+        # same distribution: both noise terms carry the summed variance
+        assert abs(np.var(comb_noise) / np.var(per_link) - 1) < 0.05

@@ -1539,6 +1539,15 @@ static int upload_inj(DBuf<R>& dst, const double* src, int64_t stride, int B, si
   return LTE_OK;
 }
 
+// (z, nv) of the fused demap path in the LLR buffer: [max_frames][n_re] z,
+// then the noise variances (see demap_in_dematch; k_det_sfbc's per RE pair)
+template <class R>
+static cx<R>* zn_z(lte_plan* p) { return reinterpret_cast<cx<R>*>(cbuf<R>(p).llr.p); }
+template <class R>
+static R* zn_nv(lte_plan* p) {
+  return cbuf<R>(p).llr.p + 2 * (size_t)p->d.max_frames * (p->n_re_bits / p->d.bps);
+}
+
 // Multi-antenna chains (SFBC 2xN, uncoded / coded; TM4 spatial multiplexing)
 // in precision R.
 template <class R>
@@ -1647,11 +1656,17 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     if (p->cap_bits.alloc((size_t)B * d.n_bits)) return fail(LTE_ENOMEM, "capture");
     cap_bits_dev = p->cap_bits.p;
   }
+  // coded SFBC 16/64-QAM without an LLR capture: the detector hands over the
+  // combined symbols and each RE pair's sigma^2_eff, k_dematch_zn demaps (as
+  // the SISO chain does; LTE_DEMAP_IN_DEMATCH=0 keeps the LLR round trip)
+  const bool zn = coded && sfbc && (d.bps == 4 || d.bps == 6) && !a->cap_llr && (m.res & 1) == 0 &&
+                  m.n_dsc <= m.res && env_on("LTE_DEMAP_IN_DEMATCH", true);
   {
     Timer t(p, KN_RX_DATA);
     if (sfbc)
       LCHK(launch_det_sfbc<R>(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, c.Ym.p, c.H.p, c.snr_lin.p, p->pw.p, p->PW,
-                              d.n_bits, p->frame_err.p, c.llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev));
+                              d.n_bits, p->frame_err.p, c.llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev,
+                              zn ? zn_z<R>(p) : nullptr, zn ? zn_nv<R>(p) : nullptr));
     else
       LCHK(launch_det_spatial<R>(s, g, m, B, c.Ym.p, c.H.p, c.snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
                                  cap_syms_dev, cap_bits_dev));
@@ -1659,7 +1674,11 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   if (coded) {
     {
       Timer t(p, KN_DEMATCH);
-      LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p,
+      if (zn)
+        LCHK(launch_dematch_zn<R>(s, zn_z<R>(p), zn_nv<R>(p), p->n_re_bits / d.bps, m.res, d.bps, B, p->rx_map.p,
+                                  p->n_layers, c.blk_ptrs.p, p->rows_dev.p, turbo_plan_ch(p), 0, 1));
+      else
+        LCHK(launch_dematch<R>(s, c.llr.p, p->n_re_bits, B, p->rx_map.p, p->n_layers, c.blk_ptrs.p, p->rows_dev.p,
                                  turbo_plan_ch(p)));
     }
     const int G = (B + 63) / 64;
@@ -1914,12 +1933,6 @@ static bool demap_in_dematch(const lte_plan* p, const lte_run_args* a) {
   if (const char* e = std::getenv("LTE_DEMAP_IN_DEMATCH"))
     if (std::atoi(e) == 0) return false;
   return true;
-}
-template <class R>
-static cx<R>* zn_z(lte_plan* p) { return reinterpret_cast<cx<R>*>(cbuf<R>(p).llr.p); }
-template <class R>
-static R* zn_nv(lte_plan* p) {
-  return cbuf<R>(p).llr.p + 2 * (size_t)p->d.max_frames * (p->n_re_bits / p->d.bps);
 }
 
 // Fused SISO receiver (k_rx_frame): one RX, coded or uncoded, no SC-FDM.

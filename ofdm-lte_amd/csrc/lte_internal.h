@@ -174,11 +174,13 @@ int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_
                    const int64_t* rows, int ch, int g0 = 0);
 // dematch with the soft demapper fused in: reads the equalised symbols z
 // ([B][n_re]) and their noise variances ([B][n_grp][nd] per data subcarrier,
-// from the receivers' nv_out mode) instead of LLRs; same decoder rows as
+// from the receivers' nv_out mode; nv_pairs: [B][n_sym][nd / 2] per Alamouti
+// RE pair, k_det_sfbc's) instead of LLRs; same decoder rows as
 // launch_dematch (bps 4 / 6)
 template <class R>
 int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int nd, int bps, int B,
-                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int ch, int g0 = 0);
+                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int ch, int g0 = 0,
+                      int nv_pairs = 0);
 // f64 != 0: the float64 decoder (bit-exact with the reference), blk / ckpt hold doubles
 int launch_turbo(hipStream_t s, void* blk, void* ckpt, uint32_t* bits, int K, int f1, int f2, int iters,
                  int G, int mode, int f64, int ch);
@@ -327,9 +329,11 @@ template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
                        const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H);
 template <class R>
+// coded: LLRs to llr, or (zo != null) the combined symbols to zo [B][n_sym][res]
+// and sigma^2_eff per RE pair to nvo [B][n_sym][res / 2] for launch_dematch_zn
 int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const cx<R>* Y,
                     const cx<R>* H, const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits);
+                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* zo = nullptr, R* nvo = nullptr);
 template <class R>
 int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* Y, const cx<R>* H,
                        const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,

@@ -1446,7 +1446,8 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
                                                   const cx<R>* __restrict__ H, const R* __restrict__ snr_lin,
                                                   const uint32_t* __restrict__ pw, int PW, int n_bits,
                                                   uint32_t* __restrict__ frame_err, R* __restrict__ llr,
-                                                  cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+                                                  cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits,
+                                                  cx<R>* __restrict__ zo, R* __restrict__ nvo) {
   using V = cx<R>;
   constexpr bool F64 = sizeof(R) == 8;
   const int npair = m.n_dsc >> 1;
@@ -1496,6 +1497,13 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
   if constexpr (CODED) {
     const R s2 = (R)1 / snr_lin[b];
     const R nv = F64 ? fmax((s2 / (R)(m.num_rx * m.num_rx)) * inv_g, s2 / (R)4) : fmax(s2 * ir * ir * inv_g, s2 * (R)0.25);
+    if (zo) {   // k_dematch_zn demaps: (z0, z1) and the pair's sigma^2_eff (24 B per RE instead of 8 bps)
+      if (!act) return;
+      zo[(size_t)b * g.n_sym * m.res + re] = z0;
+      zo[(size_t)b * g.n_sym * m.res + re + 1] = z1;
+      nvo[(size_t)b * g.n_sym * (m.res >> 1) + (size_t)l * (m.res >> 1) + pr] = nv;
+      return;
+    }
     R o[BPS];
     R* lo = llr + ((size_t)b * g.n_sym * m.res + re) * BPS;
     if (!act) return;
@@ -1527,13 +1535,14 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
 template <class R>
 int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int rayleigh, int B, const cx<R>* Y,
                     const cx<R>* H, const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits) {
+                    R* llr, cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* zo, R* nvo) {
   (void)rayleigh;
+  if (zo && (!coded || !nvo || (m.res & 1) || m.n_dsc > m.res)) return (int)hipErrorInvalidValue;
   const int64_t n = (int64_t)B * g.n_sym * (m.n_dsc >> 1);
   const dim3 grid((unsigned)((n + MWG - 1) / MWG));
 #define LTE_DS(C_, B_) \
   hipLaunchKernelGGL((k_det_sfbc<R, C_, B_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits, \
-                     frame_err, llr, cap_syms, cap_bits)
+                     frame_err, llr, cap_syms, cap_bits, zo, nvo)
   if (coded) {
     if (g.bps == 2) LTE_DS(1, 2); else if (g.bps == 4) LTE_DS(1, 4); else LTE_DS(1, 6);
   } else {
@@ -1874,7 +1883,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
                                      const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*);                \
   template int launch_det_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const cx<R>*,          \
                                   const cx<R>*, const R*, const uint32_t*, int, int, uint32_t*, R*, cx<R>*,        \
-                                  uint8_t*);                                                                       \
+                                  uint8_t*, cx<R>*, R*);                                                           \
   template int launch_det_spatial<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const cx<R>*,   \
                                      const R*, const uint32_t*, int, int, uint32_t*, cx<R>*, uint8_t*);
 LTE_MIMO_INST(float)

@@ -95,8 +95,8 @@ int launch_dematch(hipStream_t s, const R* llr, int T, int B, const int32_t* rx_
 template <class R> constexpr int dz_re() { return sizeof(R) == 8 ? LTE_DZ_RE64 : 16; }
 template <class R, int BPS>
 __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z, const R* __restrict__ nv, int n_re,
-                                                    int nd, int n_nv, int B, const int32_t* __restrict__ rx_map,
-                                                    int add,
+                                                    int nd, int n_nv, int nv_grp, int nv_sh, int B,
+                                                    const int32_t* __restrict__ rx_map, int add,
                                                     R* const* __restrict__ blk, const int64_t* __restrict__ rows,
                                                     int ch, int g0) {
   using V = cx<R>;
@@ -116,10 +116,11 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
     const int l = (re0 + r) / nd, j = re0 + r - l * nd;
     if (LTE_DM_NT & 2) {
       zv[k] = ok ? mkc(__builtin_nontemporal_load(&z[i].x), __builtin_nontemporal_load(&z[i].y)) : mkc((R)0, (R)0);
-      nvv[k] = ok ? __builtin_nontemporal_load(&nv[(size_t)b * n_nv + (l / 14) * nd + j]) : (R)1;
+      nvv[k] = ok ? __builtin_nontemporal_load(&nv[(size_t)b * n_nv + (l / nv_grp) * (nd >> nv_sh) + (j >> nv_sh)])
+                  : (R)1;
     } else {
       zv[k] = ok ? z[i] : mkc((R)0, (R)0);
-      nvv[k] = ok ? nv[(size_t)b * n_nv + (l / 14) * nd + j] : (R)1;
+      nvv[k] = ok ? nv[(size_t)b * n_nv + (l / nv_grp) * (nd >> nv_sh) + (j >> nv_sh)] : (R)1;
     }
   }
 #pragma unroll
@@ -143,21 +144,25 @@ __global__ __launch_bounds__(256) void k_dematch_zn(const cx<R>* __restrict__ z,
 
 template <class R>
 int launch_dematch_zn(hipStream_t s, const cx<R>* z, const R* nv, int n_re, int nd, int bps, int B,
-                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int ch, int g0) {
+                      const int32_t* rx_map, int n_layers, R* const* blk, const int64_t* rows, int ch, int g0,
+                      int nv_pairs) {
   const int G = (B + 63) / 64 - g0;
   if (G < 1 || G > 65535 || (bps != 4 && bps != 6) || n_layers < 1 || nd < 1) return (int)hipErrorInvalidValue;
-  const int n_nv = ((n_re / nd + 13) / 14) * nd;   // groups x data subcarriers per frame
+  if (nv_pairs && (nd & 1)) return (int)hipErrorInvalidValue;
+  // nv per (14-symbol group, data subcarrier) (SISO), or per (symbol, RE pair) (SFBC)
+  const int nv_grp = nv_pairs ? 1 : 14, nv_sh = nv_pairs ? 1 : 0;
+  const int n_nv = ((n_re / nd + nv_grp - 1) / nv_grp) * (nd >> nv_sh);
   constexpr int DZ = dz_re<R>();
   const dim3 grid((n_re + DZ - 1) / DZ, G);
   const int T = n_re * bps;
   for (int k = 0; k < n_layers; ++k) {
     const int32_t* mp = rx_map + (size_t)k * T;
     if (bps == 4)
-      hipLaunchKernelGGL((k_dematch_zn<R, 4>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, B, mp, k > 0 ? 1 : 0,
-                         blk, rows, ch, g0);
+      hipLaunchKernelGGL((k_dematch_zn<R, 4>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, nv_grp, nv_sh, B, mp,
+                         k > 0 ? 1 : 0, blk, rows, ch, g0);
     else
-      hipLaunchKernelGGL((k_dematch_zn<R, 6>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, B, mp, k > 0 ? 1 : 0,
-                         blk, rows, ch, g0);
+      hipLaunchKernelGGL((k_dematch_zn<R, 6>), grid, dim3(256), 0, s, z, nv, n_re, nd, n_nv, nv_grp, nv_sh, B, mp,
+                         k > 0 ? 1 : 0, blk, rows, ch, g0);
     const int e = (int)hipGetLastError();
     if (e) return e;
   }
@@ -169,9 +174,9 @@ template int launch_dematch<float>(hipStream_t, const float*, int, int, const in
 template int launch_dematch<double>(hipStream_t, const double*, int, int, const int32_t*, int, double* const*,
                                     const int64_t*, int, int);
 template int launch_dematch_zn<float>(hipStream_t, const float2*, const float*, int, int, int, int, const int32_t*,
-                                      int, float* const*, const int64_t*, int, int);
+                                      int, float* const*, const int64_t*, int, int, int);
 template int launch_dematch_zn<double>(hipStream_t, const double2*, const double*, int, int, int, int,
-                                       const int32_t*, int, double* const*, const int64_t*, int, int);
+                                       const int32_t*, int, double* const*, const int64_t*, int, int, int);
 
 // ---------------------------------------------------------------------------
 // Stage entry: rate_dematching_turbo (rate_matching.py:374-489) for any E,

@@ -276,3 +276,23 @@ def test_mimo_argument_errors(C):
         lte_phy.OFDMChannel().transmit_mimo([])
     with pytest.raises(ValueError):
         lte_phy.OFDMChannel().transmit_mimo([np.ones(10), np.ones(11)])
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('mod', ['16-QAM', '64-QAM'])
+def test_sfbc_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
+    """Coded SFBC: k_det_sfbc handing the combined symbols and each RE pair's
+    sigma^2_eff to k_dematch_zn (which runs the same max-log demapper while it
+    builds the decoder rows) decodes exactly like the LLR round trip
+    (k_det_sfbc LLRs -> k_dematch): identical per-frame bit errors, CRC flags
+    and counts on the same Philox frames, over more than one decoder group."""
+    sim = _sim(20.0, mod, 'rayleigh_mp', prec)
+    B = 64 + 7
+    plan = sim._sfbc_plan(0, 27760 if mod == '64-QAM' else 18000, 2, coded=True, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    monkeypatch.setenv('LTE_DEMAP_IN_DEMATCH', '0')
+    a = plan.run(snr, seed=0x5EED, frame_id0=5)
+    monkeypatch.setenv('LTE_DEMAP_IN_DEMATCH', '1')
+    b = plan.run(snr, seed=0x5EED, frame_id0=5)
+    assert np.array_equal(a['crc_ok'], b['crc_ok']) and np.array_equal(a['counts'], b['counts'])
+    assert np.array_equal(a['frame_errors'], b['frame_errors'])

@@ -84,6 +84,9 @@ __device__ __forceinline__ cx<R> qam_at(int64_t q, const uint32_t* __restrict__ 
 // max_delay samples, whose taps reach into the previous symbol, are added by
 // k_link_power_fix from x.  Static taps only (n_cs = 1); part[link][l].
 
+#ifndef LTE_TXM_LPG   // receive antennas per group of the TX link-power sums (each delayed sample read once per group)
+#define LTE_TXM_LPG 2
+#endif
 // PF (coded): one slot per frame walking its (OFDM symbol, TX) pairs, the
 // frame's coded streams staged in LDS once instead of once per pair (as
 // k_ofdm_txf does for SISO); otherwise one slot per (frame, symbol, TX).
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(MWG, PF ? 3 : 1) void k_ofdm_tx_mimo(Grid g, MimoGr
   using V = cx<R>;
   V* sm = mimo_lds<V>();
   const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
-  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
+  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
   const int per = g.n_sym * m.num_tx;
   const int gs = blockIdx.x * spw + slot;
   const int b = PF ? gs : gs / per;
@@ -108,7 +111,7 @@ __global__ __launch_bounds__(MWG, PF ? 3 : 1) void k_ofdm_tx_mimo(Grid g, MimoGr
   if (CODED && stage_enc) {
     uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
     if (active)
-      for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
+      for (int i = tid0; i < enc_words; i += T) es[i] = fe[i];
     fe = es;
   }
   // PF SFBC: each thread's Alamouti pairs (at most SFP per symbol) keep their
@@ -117,6 +120,10 @@ __global__ __launch_bounds__(MWG, PF ? 3 : 1) void k_ofdm_tx_mimo(Grid g, MimoGr
   int qc[SFP][2];
   for (int lt = lt0; lt < lt1; ++lt) {
   const int l = lt / m.num_tx, t = lt - l * m.num_tx;
+  // opaque per pair (PF): the FFT's twiddle addressing is not hoisted out of
+  // the loop into registers
+  int tid = tid0;
+  if (PF) asm volatile("" : "+v"(tid));
   if (active)
     for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
   __syncthreads();   // (first pair: also the staged streams)
@@ -153,8 +160,11 @@ __global__ __launch_bounds__(MWG, PF ? 3 : 1) void k_ofdm_tx_mimo(Grid g, MimoGr
         for (int c = 0; c < m.rank; ++c) {
           const int qi = m.rank * j + c;
           if (qi >= m.res) break;
-          const V sq = qam_at<R, CODED, BPS>(q0 + qi, fb, fe, tx_map);
           const V w = mkc((R)m.W[(t * 4 + c) * 2], (R)m.W[(t * 4 + c) * 2 + 1]);
+          // a zero precoder entry adds a signed zero to a nonzero sum (every
+          // constellation point is nonzero): skip its bit gathers (W = I: 3 of 4)
+          if (w.x == (R)0 && w.y == (R)0) continue;
+          const V sq = qam_at<R, CODED, BPS>(q0 + qi, fb, fe, tx_map);
           v = cadd(v, cmul(w, sq));
         }
       }
@@ -181,7 +191,7 @@ __global__ __launch_bounds__(MWG, PF ? 3 : 1) void k_ofdm_tx_mimo(Grid g, MimoGr
     for (int p = 0; p < TXCH_MAXP; ++p) dl[p] = p < np ? g.cp + lp.delays[p] : 0;
     // receive antennas in groups of LPG: each delayed sample x(j - d_p) is
     // read from LDS (and scaled) once for the group's links
-    constexpr int LPG = 1;
+    constexpr int LPG = LTE_TXM_LPG;
     for (int r0 = 0; r0 < m.num_rx; r0 += LPG) {
       R pwr[LPG];
 #pragma unroll
@@ -242,7 +252,10 @@ __global__ __launch_bounds__(MWG, PF ? 3 : 1) void k_ofdm_tx_mimo(Grid g, MimoGr
 // frequency domain, and for spatial layers through the effective channel h_r W
 // (x_t = sum_c W[t][c] s_c): equal up to float64 rounding (the reference adds
 // the time-domain products), tests/test_gpu_mimo.py::test_flat_channel_fused_tx.
-template <class R, int MODE, int CODED, int BPS, int NC = 0>
+// PR (spatial): one slot per (frame, OFDM symbol) walking the receive
+// antennas, each thread's layer QAM codes formed at the first RX and reused
+// for the others (the bit gathers once per symbol instead of once per RX).
+template <class R, int MODE, int CODED, int BPS, int NC = 0, bool PR = false>
 __global__ __launch_bounds__(MWG) void k_ofdm_txch_flat(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                         const uint32_t* __restrict__ enc, int enc_words,
                                                         const int32_t* __restrict__ tx_map,
@@ -253,19 +266,29 @@ __global__ __launch_bounds__(MWG) void k_ofdm_txch_flat(Grid g, MimoGrid m, cons
   __shared__ R red[MWG / 64];
   V* sm = mimo_lds<V>();
   const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
-  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
-  const int per = g.n_sym * m.num_rx;
+  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
+  const int per = PR ? g.n_sym : g.n_sym * m.num_rx;
   const int gs = blockIdx.x * spw + slot;
-  const int b = gs / per, rr = gs - b * per, l = rr / m.num_rx, r = rr - l * m.num_rx;
+  const int b = gs / per, rr = gs - b * per;
+  const int l = PR ? rr : rr / m.num_rx;
+  const int r0 = PR ? 0 : rr - l * m.num_rx, r1 = PR ? m.num_rx : r0 + 1;
   const bool active = slot < spw && b < B;
   V* buf = sm + slot * N;
   const uint32_t* fe = enc + (size_t)b * enc_words;
   if (CODED && stage_enc) {
     uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
     if (active)
-      for (int i = tid; i < enc_words; i += T) es[i] = fe[i];
+      for (int i = tid0; i < enc_words; i += T) es[i] = fe[i];
     fe = es;
   }
+  constexpr int QC = 4;   // data subcarriers per thread: n_dsc < N / 2 = QC T
+  int codes[QC][4];
+#pragma unroll 1
+  for (int r = r0; r < r1; ++r) {
+  // opaque per RX (PR): the FFT's twiddle addressing is not hoisted out of
+  // the loop into registers (as k_ofdm_txf does per symbol)
+  int tid = tid0;
+  if (PR) asm volatile("" : "+v"(tid));
   if (active)
     for (int k = tid; k < N; k += T) buf[k] = mkc((R)0, (R)0);
   __syncthreads();
@@ -281,6 +304,23 @@ __global__ __launch_bounds__(MWG) void k_ofdm_txch_flat(Grid g, MimoGrid m, cons
         for (int t = 0; t < m.num_tx; ++t)
           E[c] = cadd(E[c], cmul(hr[t * NCF], mkc((R)m.W[(t * 4 + c) * 2], (R)m.W[(t * 4 + c) * 2 + 1])));
     }
+    if constexpr (PR && MODE == MIMO_SPATIAL) {
+#pragma unroll
+      for (int k = 0; k < QC; ++k) {
+        const int j = tid + k * T;
+        if (j >= m.n_dsc) break;
+        V acc = mkc((R)0, (R)0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int qi = m.rank * j + c;
+          if (c < m.rank && qi < m.res) {
+            if (r == r0) codes[k][c] = qam_code<CODED, BPS>(q0 + qi, fb, fe, tx_map);
+            acc = cadd(acc, cmul(E[c], qam_of<R, BPS>(codes[k][c])));
+          }
+        }
+        buf[g.data_idx[j]] = acc;
+      }
+    } else {
     for (int j = tid; j < m.n_dsc; j += T) {
       V acc = mkc((R)0, (R)0);
       if constexpr (MODE == MIMO_SFBC) {
@@ -297,6 +337,7 @@ __global__ __launch_bounds__(MWG) void k_ofdm_txch_flat(Grid g, MimoGrid m, cons
         }
       }
       buf[g.data_idx[j]] = acc;
+    }
     }
     for (int t = 0; t < m.num_tx; ++t) {   // each TX's CRS pilots on its own subset
       const V* pv = MGT<R>::pval(m) + t * m.maxP;
@@ -335,6 +376,8 @@ __global__ __launch_bounds__(MWG) void k_ofdm_txch_flat(Grid g, MimoGrid m, cons
       pow_part[((size_t)b * m.num_rx + r) * nblk + l] = tot;
     }
   }
+  if (PR) __syncthreads();   // the next RX zeroes buf and reuses red
+  }
 }
 
 template <class R>
@@ -342,7 +385,10 @@ int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int c
                           const uint32_t* enc, int enc_words, const int32_t* tx_map, const cx<R>* coef, cx<R>* y,
                           R* pow_part, int nblk, int B) {
   const int spw = MWG / (g.N >> 3);
-  const int64_t total = (int64_t)B * g.n_sym * m.num_rx;
+  // spatial: one slot per (frame, symbol) over the receive antennas (LTE_TXCH_PR=0: one per RX)
+  const char* pre = std::getenv("LTE_TXCH_PR");
+  const bool pr = m.mode == MIMO_SPATIAL && g.N == 2048 && m.n_dsc <= 4 * (g.N >> 3) && !(pre && std::atoi(pre) == 0);
+  const int64_t total = (int64_t)B * g.n_sym * (pr ? 1 : m.num_rx);
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6) || (g.N >> 3) < 64 || nblk < g.n_sym ||
       m.num_tx > 4)
     return (int)hipErrorInvalidValue;
@@ -352,7 +398,10 @@ int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int c
   const size_t shm = spw * g.N * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
 #define LTE_TXF(M_, C_, B_)                                                                                          \
   do {                                                                                                               \
-    if (g.N == 2048)                                                                                                 \
+    if (g.N == 2048 && pr)                                                                                           \
+      hipLaunchKernelGGL((k_ofdm_txch_flat<R, M_, C_, B_, 2048, true>), dim3(blocks), dim3(MWG), shm, s, g, m, pw,   \
+                         PW, enc, enc_words, tx_map, coef, y, pow_part, nblk, B, stage_enc);                         \
+    else if (g.N == 2048)                                                                                            \
       hipLaunchKernelGGL((k_ofdm_txch_flat<R, M_, C_, B_, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, pw, PW, enc, \
                          enc_words, tx_map, coef, y, pow_part, nblk, B, stage_enc);                                  \
     else                                                                                                             \

@@ -64,6 +64,14 @@ enum { LTE_CH_AWGN = 0, LTE_CH_RAYLEIGH = 1 }; /* core/channel.py:10-245 */
  * versions"). */
 enum { LTE_PREC_DEFAULT = 0, LTE_PREC_F32 = 32, LTE_PREC_F64 = 64 };
 
+/* ABI version this header describes; lte_version() returns the library's.
+ * A client checks lte_version() == LTE_ABI_VERSION once before any other call
+ * (lte_abi_check(LTE_ABI_VERSION) does exactly that).  History (INTEGRATION.md "ABI versions"):
+ *   1  LTE_PREC_DEFAULT = float32 for the multi-antenna / beamforming chains
+ *   2  LTE_PREC_DEFAULT = float64 for every chain; cap_bf_gain double
+ *   3  lte_run_args.snr_db is double (the reference's float64 SNR in dB) */
+#define LTE_ABI_VERSION 3
+
 #define LTE_MAX_PATHS 16
 enum { LTE_STAGE_TX = 1, LTE_STAGE_CHANNEL = 2, LTE_STAGE_RX = 4, LTE_STAGE_ALL = 7 };
 
@@ -121,7 +129,11 @@ typedef struct lte_plan lte_plan;
  * consecutive frames (0 = the same data broadcast to every frame). */
 typedef struct {
   int32_t n_frames;
-  const float *snr_db;         /* host [n_frames]                                  */
+  /* host [n_frames] SNR in dB, float64 as the reference holds it; the library
+   * forms 10 ** (snr_db / 10) (core/channel.py:32,191) and the detectors'
+   * noise variances 1 / 10 ** (snr_db / 10) (core/ofdm_core.py:1224) or
+   * 10 ** (-snr_db / 10) (:2397, :2737) from it in float64.  (ABI <= 2: float) */
+  const double *snr_db;
   const int32_t *snr_index;    /* host [n_frames] row in counts (NULL -> 0)        */
   int32_t n_snr;               /* rows of counts                                   */
   uint64_t seed;
@@ -175,7 +187,11 @@ typedef struct {
 const char *lte_strerror(int code);
 const char *lte_last_error(void);
 int lte_device_init(int device);            /* select + check gfx950 */
-int lte_version(void);                     /* ABI version: 2 */
+int lte_version(void);                     /* ABI version: LTE_ABI_VERSION (3) */
+/* Call once as lte_abi_check(LTE_ABI_VERSION): LTE_OK when the loaded library
+ * implements the ABI of the header the caller was compiled against, LTE_EUNSUP
+ * (with lte_last_error() naming both versions) otherwise. */
+int lte_abi_check(int abi_version);
 
 /* Plans. */
 int lte_plan_create(const lte_plan_desc *desc, lte_plan **out);
@@ -280,6 +296,16 @@ int lte_channel_mimo_host64(int64_t L, int num_tx, int num_rx, int mode, int cha
  * MMSE, :225-228) -> out [rank][n_sc] complex128.  num_rx, num_tx <= 4. */
 int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps, int64_t n_sc, const double *y,
                          const double *H, const double *W, double sigma2, double *out);
+/* SFBC Alamouti on host arrays, float64 [n] complex128 (interleaved re, im),
+ * n even (LTE_EINVAL with the reference's ValueError text otherwise; n = 0
+ * writes nothing).  encode: SFBCAlamouti.encode (core/sfbc_alamouti.py:45-78),
+ * per pair TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)].  decode:
+ * SFBCAlamouti.decode (:80-163) with per-subcarrier estimates H0 / H1 and the
+ * caller's regularization (the reference's default 1e-10) -- the combiner the
+ * chains' SFBC detector runs. */
+int lte_sfbc_encode_host64(int64_t n, const double *syms, double *tx0, double *tx1);
+int lte_sfbc_decode_host64(int64_t n, const double *rx, const double *H0, const double *H1, double regularization,
+                           double *out);
 /* Rate dematching map: rate_dematching_turbo core/channel_coding/rate_matching.py:374-489
  * src[j] = index into the E rate-matched LLRs feeding output j of [3K+12], -1 = zero. */
 int lte_rate_dematch_map(int K, int E, int rv_idx, int32_t *src);

@@ -433,6 +433,7 @@ struct lte_plan {
   ChainBufs<double> c64;             // f64 plans
   DBuf<uint32_t> frame_err, frame_crc;
   DBuf<int32_t> snr_idx;
+  DBuf<double> nvar;                 // spatial detectors' noise variance 10 ** (-snr_db / 10), float64
   DBuf<uint64_t> fid;
   DBuf<unsigned long long> counts;
   DBuf<uint8_t> cap_bits;
@@ -519,7 +520,13 @@ void collect_timing(lte_plan* p) {
 
 extern "C" {
 
-int lte_version(void) { return 2; }   // 2: LTE_PREC_DEFAULT is float64 for every chain
+int lte_version(void) { return LTE_ABI_VERSION; }   // 3: snr_db is double (include/lte_phy.h history)
+
+int lte_abi_check(int abi_version) {
+  if (abi_version == LTE_ABI_VERSION) return LTE_OK;
+  return fail(LTE_EUNSUP, "ABI mismatch: caller built against version " + std::to_string(abi_version) +
+                              ", library implements " + std::to_string(LTE_ABI_VERSION));
+}
 
 const char* lte_last_error(void) { return g_err.c_str(); }
 
@@ -811,6 +818,41 @@ int lte_mimo_detect_host(int detector, int num_rx, int num_tx, int rank, int bps
   if (!ok) rc = fail(LTE_EHIP, std::string("mimo detect failed: ") + hipGetErrorString(hipGetLastError()));
   dy.release(); dH.release(); dW.release(); dout.release();
   return rc;
+}
+
+// SFBCAlamouti.encode / .decode on host arrays (core/sfbc_alamouti.py:45-163).
+static int sfbc_stage(int decode, int64_t n, const double* a, const double* h0, const double* h1, double reg,
+                      double* o0, double* o1) {
+  if (n % 2 != 0)
+    return fail(LTE_EINVAL, decode ? "Number of RX symbols must be even, got " + std::to_string(n)
+                                   : "Number of symbols must be even for Alamouti coding, got " + std::to_string(n));
+  if (n < 0 || n > (1LL << 28) || !a || !o0 || (decode ? (!h0 || !h1) : !o1))
+    return fail(LTE_EINVAL, "bad SFBC arguments");
+  if (n == 0) return LTE_OK;
+  const size_t nr = (size_t)n * 2;
+  DBuf<double> da, dh0, dh1, d0, d1;
+  bool ok = da.alloc(nr) == 0 && d0.alloc(nr) == 0 && (decode ? dh0.alloc(nr) == 0 && dh1.alloc(nr) == 0
+                                                                : d1.alloc(nr) == 0) &&
+            hipMemcpy(da.p, a, nr * 8, hipMemcpyHostToDevice) == hipSuccess;
+  if (ok && decode)
+    ok = hipMemcpy(dh0.p, h0, nr * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(dh1.p, h1, nr * 8, hipMemcpyHostToDevice) == hipSuccess;
+  ok = ok && launch_sfbc_stage(nullptr, decode, n, da.p, dh0.p, dh1.p, reg, d0.p, d1.p) == 0;
+  ok = ok && hipDeviceSynchronize() == hipSuccess && hipMemcpy(o0, d0.p, nr * 8, hipMemcpyDeviceToHost) == hipSuccess;
+  if (ok && !decode) ok = hipMemcpy(o1, d1.p, nr * 8, hipMemcpyDeviceToHost) == hipSuccess;
+  int rc = LTE_OK;
+  if (!ok) rc = fail(LTE_EHIP, std::string("SFBC stage failed: ") + hipGetErrorString(hipGetLastError()));
+  da.release(); dh0.release(); dh1.release(); d0.release(); d1.release();
+  return rc;
+}
+
+int lte_sfbc_encode_host64(int64_t n, const double* syms, double* tx0, double* tx1) {
+  return sfbc_stage(0, n, syms, nullptr, nullptr, 0.0, tx0, tx1);
+}
+
+int lte_sfbc_decode_host64(int64_t n, const double* rx, const double* H0, const double* H1, double regularization,
+                           double* out) {
+  return sfbc_stage(1, n, rx, H0, H1, regularization, out, nullptr);
 }
 
 // Output position j of [3K+12] (turbo_encode order) fed by rate-matched index
@@ -1279,6 +1321,7 @@ static int plan_alloc(lte_plan* p) {
     bad |= !(p->f64 ? alloc_siso<double>(p, coded) : alloc_siso<float>(p, coded));
   }
   bad |= p->snr_idx.alloc(B) != 0;
+  if (p->mimo) bad |= p->nvar.alloc(B) != 0;
   bad |= p->fid.alloc(B) != 0;
   bad |= p->frame_err.alloc(B) != 0;
   bad |= p->frame_crc.alloc(B) != 0;
@@ -1454,7 +1497,7 @@ int lte_plan_destroy(lte_plan* p) {
   p->txf_map.release(); p->txf_re.release();
   p->pw.release(); p->enc.release(); p->inj_bits.release(); p->inj_bytes.release(); p->enc_qmask.release();
   p->c32.release(); p->c64.release();
-  p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->fid.release(); p->counts.release();
+  p->frame_err.release(); p->frame_crc.release(); p->snr_idx.release(); p->nvar.release(); p->fid.release(); p->counts.release();
   p->cap_bits.release();
   for (auto& b : p->decb) b.release();
   p->rows_dev.release(); p->dec_ptrs.release(); p->kw_dev.release();
@@ -1567,6 +1610,12 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   std::vector<R> sl(B);
   for (int b = 0; b < B; ++b) sl[b] = (R)snr_lin[b];
   HIPCHK(hipMemcpyAsync(c.snr_lin.p, sl.data(), B * sizeof(R), hipMemcpyHostToDevice, s));
+  std::vector<double> nv;
+  if (!sfbc) {   // MIMODetector's noise_variance = 10 ** (-snr_db / 10) (core/ofdm_core.py:2737), float64
+    nv.resize(B);
+    for (int b = 0; b < B; ++b) nv[b] = std::pow(10.0, -a->snr_db[b] / 10.0);
+    HIPCHK(hipMemcpyAsync(p->nvar.p, nv.data(), B * sizeof(double), hipMemcpyHostToDevice, s));
+  }
   // injections (the reference's own draws, ref-compat mode)
   const R *inj_ph = nullptr, *inj_z = nullptr, *inj_lz = nullptr, *inj_lh = nullptr;
   int64_t inj_ph_stride = 0, inj_z_stride = 0, inj_lz_stride = 0, inj_lh_stride = 0;
@@ -1668,7 +1717,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                               d.n_bits, p->frame_err.p, c.llr.p, cap_syms_dev, coded ? nullptr : cap_bits_dev,
                               zn ? zn_z<R>(p) : nullptr, zn ? zn_nv<R>(p) : nullptr));
     else
-      LCHK(launch_det_spatial<R>(s, g, m, B, c.Ym.p, c.H.p, c.snr_lin.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
+      LCHK(launch_det_spatial<R>(s, g, m, B, c.Ym.p, c.H.p, p->nvar.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
                                  cap_syms_dev, cap_bits_dev));
   }
   if (coded) {
@@ -2172,7 +2221,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   std::vector<int32_t> si(B, 0);
   std::vector<uint64_t> fid(B);
   for (int b = 0; b < B; ++b) {
-    sl[b] = std::pow(10.0, (double)a->snr_db[b] / 10.0);   // snr_linear = 10 ** (snr_db / 10) (channel.py:32)
+    sl[b] = std::pow(10.0, a->snr_db[b] / 10.0);   // snr_linear = 10 ** (snr_db / 10) (channel.py:32), float64
     if (a->snr_index) {
       si[b] = a->snr_index[b];
       if (si[b] < 0 || si[b] >= n_snr) return fail(LTE_EINVAL, "snr_index out of range");
@@ -2214,7 +2263,7 @@ int lte_run(lte_plan* p, const lte_run_args* a) {
   // beamforming chain: noise scale sqrt(noise_variance / 2), noise_variance =
   // 10 ** (-snr_db / 10) (core/ofdm_core.py:2397-2399)
   std::vector<double> sig(B);
-  for (int b = 0; b < B; ++b) sig[b] = std::sqrt(std::pow(10.0, -(double)a->snr_db[b] / 10.0) / 2.0);
+  for (int b = 0; b < B; ++b) sig[b] = std::sqrt(std::pow(10.0, -a->snr_db[b] / 10.0) / 2.0);
   return p->f64 ? run_bf<double>(p, a, B, n_snr, sig, inj_bits, inj_bits_stride)
                 : run_bf<float>(p, a, B, n_snr, sig, inj_bits, inj_bits_stride);
 }

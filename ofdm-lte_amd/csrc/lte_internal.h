@@ -336,8 +336,12 @@ int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, 
                     R* llr, cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* zo = nullptr, R* nvo = nullptr);
 template <class R>
 int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* Y, const cx<R>* H,
-                       const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                       const double* nvar, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
                        cx<R>* cap_syms, uint8_t* cap_bits);
+// SFBCAlamouti.encode (decode = 0: a = symbols -> o0 = TX0, o1 = TX1) / .decode
+// (decode = 1: a = rx, h0 / h1 the per-SC estimates -> o0), float64 [n] complex, n even
+int launch_sfbc_stage(hipStream_t s, int decode, int64_t n, const double* a, const double* h0, const double* h1,
+                      double reg, double* o0, double* o1);
 int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int64_t n, const double* y,
                      const double* H, const double* W, double s2, double* out);
 

@@ -1480,13 +1480,43 @@ int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, c
 }
 
 // ---------------------------------------------------------------------------
+// SFBCAlamouti.decode's combiner for one subcarrier pair (core/sfbc_alamouti.py:
+// 139-161), shared by the chain's detector (k_det_sfbc) and the stage entry
+// (lte_sfbc_decode_host64): s0 = conj(h0k) rk + h1k1 conj(rk1), s1 = conj(h1k)
+// rk - h0k1 conj(rk1), norm = |avg(h0)|**2 + |avg(h1)|**2 + reg.  f64 in the
+// reference's NumPy complex128 scalar semantics: |z| = hypot, s / norm = s *
+// (1 / norm) (NumPy's complex / real division multiplies by the reciprocal of
+// its real denominator).  d0 = s0 / norm, d1 = s1 / norm; returns norm.
+template <class R>
+__device__ __forceinline__ R sfbc_combine(cx<R> rk, cx<R> rk1, cx<R> h0k, cx<R> h1k, cx<R> h0k1, cx<R> h1k1, R reg,
+                                          cx<R>& d0, cx<R>& d1) {
+  using V = cx<R>;
+  const V rc = mkc(rk1.x, -rk1.y);
+  const V s0 = cadd(cmulc(rk, h0k), cmul(h1k1, rc));      // conj(h0k) rk + h1k1 conj(rk1)
+  const V s1 = csub(cmulc(rk, h1k), cmul(h0k1, rc));      // conj(h1k) rk - h0k1 conj(rk1)
+  const V a0 = mkc((R)0.5 * (h0k.x + h0k1.x), (R)0.5 * (h0k.y + h0k1.y));
+  const V a1 = mkc((R)0.5 * (h1k.x + h1k1.x), (R)0.5 * (h1k.y + h1k1.y));
+  if constexpr (sizeof(R) == 8) {
+    const double n0 = hypot(a0.x, a0.y), n1 = hypot(a1.x, a1.y);
+    const double nrm = (n0 * n0 + n1 * n1) + reg;
+    const double rn = 1.0 / nrm;
+    d0 = make_double2(s0.x * rn, s0.y * rn);
+    d1 = make_double2(s1.x * rn, s1.y * rn);
+    return nrm;
+  } else {
+    const float nrm = (a0.x * a0.x + a0.y * a0.y) + (a1.x * a1.x + a1.y * a1.y) + reg;
+    d0 = make_float2(s0.x / nrm, s0.y / nrm);
+    d1 = make_float2(s1.x / nrm, s1.y / nrm);
+    return nrm;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // SFBC detection.  One thread per (frame, OFDM symbol, SC pair).
 // SFBCAlamouti.decode (core/sfbc_alamouti.py:80-163) per RX with that RX's
 // slot estimate, averaged over RX (core/ofdm_core.py:2204, Q17).  f64 in the
-// reference's NumPy complex128 scalar semantics: s0 = conj(h0k) rk + h1k1
-// conj(rk1), norm = |avg(h0)|**2 + |avg(h1)|**2 + 1e-10 with |z| = hypot,
-// s / norm = s * (1 / norm) (complex / real divides by Smith's rule with a
-// zero imaginary part), the RX mean (sum_r d_r) * (1 / num_rx).  Uncoded:
+// reference's NumPy complex128 scalar semantics (sfbc_combine, reg = 1e-10),
+// the RX mean (sum_r d_r) * (1 / num_rx).  Uncoded:
 // nearest-point hard bits vs the payload (bit errors).  Coded (config 4):
 // max-log LLRs (core/ofdm_core.py:791-923) with the per-RE noise variance of
 // the combined estimate, sigma^2 / R^2 * sum_r 1 / clip(norm_r, 1e-6, 1e6),
@@ -1516,26 +1546,12 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
     const V* Yr = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
     const V* H0 = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + 0) * m.n_dsc;
     const V* H1 = H0 + m.n_dsc;
-    const V rk = Yr[j], rk1 = Yr[j + 1];
-    const V h0k = H0[j], h1k = H1[j], h0k1 = H0[j + 1], h1k1 = H1[j + 1];
-    const V rc = mkc(rk1.x, -rk1.y);
-    const V s0 = cadd(cmulc(rk, h0k), cmul(h1k1, rc));      // conj(h0k) rk + h1k1 conj(rk1)
-    const V s1 = csub(cmulc(rk, h1k), cmul(h0k1, rc));      // conj(h1k) rk - h0k1 conj(rk1)
-    const V a0 = mkc((R)0.5 * (h0k.x + h0k1.x), (R)0.5 * (h0k.y + h0k1.y));
-    const V a1 = mkc((R)0.5 * (h1k.x + h1k1.x), (R)0.5 * (h1k.y + h1k1.y));
-    if constexpr (F64) {
-      const double n0 = hypot(a0.x, a0.y), n1 = hypot(a1.x, a1.y);
-      const double nrm = (n0 * n0 + n1 * n1) + 1e-10;
-      const double rn = 1.0 / nrm;
-      z0 = cadd(z0, make_double2(s0.x * rn, s0.y * rn));
-      z1 = cadd(z1, make_double2(s1.x * rn, s1.y * rn));
-      inv_g += 1.0 / fmin(fmax(nrm, 1e-6), 1e6);
-    } else {
-      const float nrm = (a0.x * a0.x + a0.y * a0.y) + (a1.x * a1.x + a1.y * a1.y) + 1e-10f;
-      z0 = make_float2(z0.x + s0.x / nrm, z0.y + s0.y / nrm);
-      z1 = make_float2(z1.x + s1.x / nrm, z1.y + s1.y / nrm);
-      inv_g += 1.0f / fminf(fmaxf(nrm, 1e-6f), 1e6f);
-    }
+    V d0, d1;
+    const R nrm = sfbc_combine<R>(Yr[j], Yr[j + 1], H0[j], H1[j], H0[j + 1], H1[j + 1], (R)1e-10, d0, d1);
+    z0 = cadd(z0, d0);
+    z1 = cadd(z1, d1);
+    if constexpr (F64) inv_g += 1.0 / fmin(fmax(nrm, 1e-6), 1e6);
+    else inv_g += 1.0f / fminf(fmaxf(nrm, 1e-6f), 1e6f);
   }
   const R ir = (R)1 / (R)m.num_rx;
   z0 = mkc(z0.x * ir, z0.y * ir);
@@ -1796,7 +1812,7 @@ __device__ __forceinline__ void detect_sc(const dc (&He)[DMAX][DMAX], const dc (
 
 template <class R, int BPS, bool SIC_ON>
 __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
-                                                     const cx<R>* __restrict__ H, const R* __restrict__ snr_lin,
+                                                     const cx<R>* __restrict__ H, const double* __restrict__ nvar,
                                                      const uint32_t* __restrict__ pw, int PW, int n_bits,
                                                      uint32_t* __restrict__ frame_err, cx<R>* __restrict__ cap_syms,
                                                      uint8_t* __restrict__ cap_bits) {
@@ -1829,7 +1845,7 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
     }
   }
   dc sv[DMAX];
-  detect_sc<SIC_ON>(He, yv, R_, m.det, 1.0 / (double)snr_lin[b], BPS, sv);
+  detect_sc<SIC_ON>(He, yv, R_, m.det, nvar[b], BPS, sv);
   const uint32_t* fb = pw + (size_t)b * PW;
   uint32_t errs = 0;
 #pragma unroll
@@ -1855,7 +1871,7 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
 
 template <class R>
 int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* Y, const cx<R>* H,
-                       const R* snr_lin, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
+                       const double* nvar, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
                        cx<R>* cap_syms, uint8_t* cap_bits) {
   if (m.num_tx < 1 || m.num_tx > DMAX || m.num_rx < 1 || m.num_rx > DMAX || m.rank < 1 || m.rank > m.num_rx ||
       m.rank > m.num_tx || !m.W)
@@ -1863,13 +1879,55 @@ int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, c
   const int64_t n = (int64_t)B * g.n_sym * m.n_dsc;
   const dim3 grid((unsigned)((n + MWG - 1) / MWG));
 #define LTE_DSP(B_, S_)                                                                                            \
-  hipLaunchKernelGGL((k_det_spatial<R, B_, S_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, snr_lin, pw, PW, n_bits,     \
+  hipLaunchKernelGGL((k_det_spatial<R, B_, S_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, nvar, pw, PW, n_bits,        \
                      frame_err, cap_syms, cap_bits)
   const bool sic = m.det == LTE_DET_SIC;
   if (g.bps == 2) { if (sic) LTE_DSP(2, true); else LTE_DSP(2, false); }
   else if (g.bps == 4) { if (sic) LTE_DSP(4, true); else LTE_DSP(4, false); }
   else { if (sic) LTE_DSP(6, true); else LTE_DSP(6, false); }
 #undef LTE_DSP
+  return (int)hipGetLastError();
+}
+
+// Stage entries (SFBCAlamouti.encode / .decode on host arrays, float64): one
+// thread per subcarrier pair.  encode: TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)]
+// (core/sfbc_alamouti.py:45-78) -- the same pair rule the chain's TX kernels
+// apply; decode: sfbc_combine with the caller's regularization (:80-163).
+__global__ __launch_bounds__(MWG) void k_sfbc_encode_stage(int64_t npair, const double2* __restrict__ s,
+                                                           double2* __restrict__ tx0, double2* __restrict__ tx1) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npair) return;
+  const double2 s0 = s[2 * i], s1 = s[2 * i + 1];
+  tx0[2 * i] = s0;
+  tx1[2 * i] = s1;
+  tx0[2 * i + 1] = make_double2(-s1.x, s1.y);   // -conj(s1)
+  tx1[2 * i + 1] = make_double2(s0.x, -s0.y);   // conj(s0)
+}
+
+__global__ __launch_bounds__(MWG) void k_sfbc_decode_stage(int64_t npair, const double2* __restrict__ rx,
+                                                           const double2* __restrict__ H0,
+                                                           const double2* __restrict__ H1, double reg,
+                                                           double2* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npair) return;
+  const int64_t k = 2 * i;
+  double2 d0, d1;
+  sfbc_combine<double>(rx[k], rx[k + 1], H0[k], H1[k], H0[k + 1], H1[k + 1], reg, d0, d1);
+  out[k] = d0;
+  out[k + 1] = d1;
+}
+
+int launch_sfbc_stage(hipStream_t s, int decode, int64_t n, const double* a, const double* h0, const double* h1,
+                      double reg, double* o0, double* o1) {
+  if (n < 2 || (n & 1)) return (int)hipErrorInvalidValue;
+  const int64_t np = n >> 1;
+  const dim3 grid((unsigned)((np + MWG - 1) / MWG));
+  if (decode)
+    hipLaunchKernelGGL(k_sfbc_decode_stage, grid, dim3(MWG), 0, s, np, (const double2*)a, (const double2*)h0,
+                       (const double2*)h1, reg, (double2*)o0);
+  else
+    hipLaunchKernelGGL(k_sfbc_encode_stage, grid, dim3(MWG), 0, s, np, (const double2*)a, (double2*)o0,
+                       (double2*)o1);
   return (int)hipGetLastError();
 }
 
@@ -1936,7 +1994,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
                                   const cx<R>*, const R*, const uint32_t*, int, int, uint32_t*, R*, cx<R>*,        \
                                   uint8_t*, cx<R>*, R*);                                                           \
   template int launch_det_spatial<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const cx<R>*,   \
-                                     const R*, const uint32_t*, int, int, uint32_t*, cx<R>*, uint8_t*);
+                                     const double*, const uint32_t*, int, int, uint32_t*, cx<R>*, uint8_t*);
 LTE_MIMO_INST(float)
 LTE_MIMO_INST(double)
 #undef LTE_MIMO_INST

@@ -14,10 +14,11 @@ from . import channel_coding
 from .tm4 import LTECodebook, LayerMapper, MIMODetector, RankAdaptation
 from .beamforming import AdaptiveBeamforming, BeamformingPrecoder, CSIFeedback
 from .image_processing import ImageProcessor
+from .sfbc_alamouti import SFBCAlamouti, SFBCResourceMapper
 
 __version__ = '0.1.0'
 __all__ = ['LTEConfig', 'OFDMModule', 'OFDMSimulator', 'OFDMTransmitter', 'OFDMReceiver', 'OFDMChannel',
            'ChannelSimulator', 'simulate_spatial_multiplexing', 'channel_coding', 'LTECodebook', 'LayerMapper',
            'MIMODetector', 'RankAdaptation', 'BeamformingPrecoder', 'AdaptiveBeamforming', 'CSIFeedback',
-           'ImageProcessor', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
+           'ImageProcessor', 'SFBCAlamouti', 'SFBCResourceMapper', 'MODULATION_SCHEMES', 'ITU_CHANNEL_MODELS',
            'LTE_PROFILES', 'CP_VALUES', 'SUBCARRIER_SPACING']

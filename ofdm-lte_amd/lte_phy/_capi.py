@@ -22,6 +22,7 @@ DET_MMSE, DET_ZF, DET_SIC, DET_MRC = 0, 1, 2, 3
 STAGE_TX, STAGE_CHANNEL, STAGE_RX, STAGE_ALL = 1, 2, 4, 7
 MAX_PATHS = 16
 PREC_DEFAULT, PREC_F32, PREC_F64 = 0, 32, 64
+ABI_VERSION = 3   # LTE_ABI_VERSION of include/lte_phy.h that these ctypes layouts describe
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 P = ctypes.POINTER
@@ -37,7 +38,7 @@ class PlanDesc(ctypes.Structure):
 
 
 class RunArgs(ctypes.Structure):
-    _fields_ = [('n_frames', c_i32), ('snr_db', P(ctypes.c_float)), ('snr_index', P(c_i32)), ('n_snr', c_i32),
+    _fields_ = [('n_frames', c_i32), ('snr_db', P(c_f64)), ('snr_index', P(c_i32)), ('n_snr', c_i32),
                 ('seed', c_u64), ('frame_ids', P(c_u64)), ('frame_id0', c_u64),
                 ('bits', P(ctypes.c_uint8)), ('bits_stride', c_i64),
                 ('phases', P(c_f64)), ('phases_stride', c_i64),
@@ -61,6 +62,7 @@ _SIGS = {
     'lte_last_error': (ctypes.c_char_p, []),
     'lte_device_init': (ctypes.c_int, [ctypes.c_int]),
     'lte_version': (ctypes.c_int, []),
+    'lte_abi_check': (ctypes.c_int, [ctypes.c_int]),
     'lte_plan_create': (ctypes.c_int, [P(PlanDesc), P(ctypes.c_void_p)]),
     'lte_plan_destroy': (ctypes.c_int, [ctypes.c_void_p]),
     'lte_plan_info': (ctypes.c_int, [ctypes.c_void_p, P(c_i64)]),
@@ -92,6 +94,8 @@ _SIGS = {
                                     P(ctypes.c_uint32)]),
     'lte_mimo_detect_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             c_i64, P(c_f64), P(c_f64), P(c_f64), c_f64, P(c_f64)]),
+    'lte_sfbc_encode_host64': (ctypes.c_int, [c_i64, P(c_f64), P(c_f64), P(c_f64)]),
+    'lte_sfbc_decode_host64': (ctypes.c_int, [c_i64, P(c_f64), P(c_f64), P(c_f64), c_f64, P(c_f64)]),
     'lte_rate_dematch_map': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_i32)]),
     'lte_rate_dematch_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, P(c_f64), P(c_f64)]),
     'lte_qpp_perm': (ctypes.c_int, [ctypes.c_int, P(c_i32)]),
@@ -131,6 +135,8 @@ def load():
                 f = getattr(lib, name)
                 f.restype = res
                 f.argtypes = args
+            if lib.lte_abi_check(ABI_VERSION) != LTE_OK:   # the RunArgs layout above is ABI 3's
+                raise RuntimeError(f"{LIB_PATH}: {lib.lte_last_error().decode(errors='replace')}; rebuild it")
             _lib = lib
     return _lib
 
@@ -253,6 +259,29 @@ def mimo_detect(det, y, H, sigma2, W, bps=0):
     check(load().lte_mimo_detect_host(int(det), nr, nt, rank, int(bps), n, ptr(y.view(np.float64), F64),
                                       ptr(H.view(np.float64), F64), ptr(W.view(np.float64), F64), float(sigma2),
                                       ptr(out.view(np.float64), F64)))
+    return out
+
+
+def sfbc_encode(symbols):
+    """SFBCAlamouti.encode on the GPU (lte_sfbc_encode_host64): [n] complex -> (tx0, tx1)."""
+    device_init()
+    s = np.ascontiguousarray(symbols, dtype=np.complex128)
+    tx0, tx1 = np.empty_like(s), np.empty_like(s)
+    check(load().lte_sfbc_encode_host64(len(s), ptr(s.view(np.float64), F64), ptr(tx0.view(np.float64), F64),
+                                        ptr(tx1.view(np.float64), F64)))
+    return tx0, tx1
+
+
+def sfbc_decode(rx, H0, H1, regularization=1e-10):
+    """SFBCAlamouti.decode on the GPU (lte_sfbc_decode_host64)."""
+    device_init()
+    r = np.ascontiguousarray(rx, dtype=np.complex128)
+    h0 = np.ascontiguousarray(H0, dtype=np.complex128)
+    h1 = np.ascontiguousarray(H1, dtype=np.complex128)
+    out = np.empty_like(r)
+    check(load().lte_sfbc_decode_host64(len(r), ptr(r.view(np.float64), F64), ptr(h0.view(np.float64), F64),
+                                        ptr(h1.view(np.float64), F64), float(regularization),
+                                        ptr(out.view(np.float64), F64)))
     return out
 
 

@@ -81,11 +81,11 @@ class Plan:
     def run(self, snr_db, *, snr_index=None, n_snr=1, seed=0, frame_ids=None, frame_id0=0, bits=None,
             bits_broadcast=False, phases=None, phases_broadcast=False, noise=None, noise_broadcast=False,
             stages=C.STAGE_ALL, in_signal=None, capture=(), link_noise=None, link_h=None, link_broadcast=False):
-        snr = np.ascontiguousarray(np.atleast_1d(snr_db), dtype=np.float32)
+        snr = np.ascontiguousarray(np.atleast_1d(snr_db), dtype=np.float64)   # float64 as the reference (ABI 3)
         B = len(snr)
         a = C.RunArgs()
         a.n_frames = B
-        a.snr_db = C.ptr(snr, C.F32)
+        a.snr_db = C.ptr(snr, C.F64)
         keep = [snr]
         if snr_index is not None:
             si = np.ascontiguousarray(snr_index, dtype=np.int32)

@@ -182,7 +182,7 @@ def transmit_payload(bits, simulator: OFDMSimulator, snr_db: float, coded: bool 
     crc = np.ones(nf, dtype=np.uint8)
     for i in range(0, nf, frames_per_call):
         f = frames[i:i + frames_per_call]
-        r = plan.run(np.full(len(f), snr_db, dtype=np.float32), seed=seed, frame_id0=i, bits=f,
+        r = plan.run(np.full(len(f), snr_db, dtype=np.float64), seed=seed, frame_id0=i, bits=f,
                      capture=('bits_rx',))
         rx[i:i + len(f)] = r['bits_rx']
         if coded:

@@ -129,3 +129,11 @@ def oracle():
 def unpack(a, n=None):
     b = np.unpackbits(np.asarray(a, dtype=np.uint8))
     return b if n is None else b[:n]
+
+
+GOLDEN_R5 = os.path.join(ROOT, 'tests', 'golden', 'golden_r5.npz')
+
+
+@pytest.fixture(scope='session')
+def golden_r5():
+    return np.load(GOLDEN_R5, allow_pickle=False)

@@ -40,6 +40,24 @@ def test_struct_layouts_match_header():
     assert flat == cnames
 
 
+def test_abi_version_and_float64_snr():
+    """ABI 3: the header's LTE_ABI_VERSION, the library's lte_version() and the
+    ctypes layout agree, and lte_run_args.snr_db is float64 as the reference's
+    SNR is (core/channel.py:32); a caller built against another version is
+    refused (no device needed)."""
+    import ctypes
+    from lte_phy import _capi
+    h = open(os.path.join(ROOT, 'include', 'lte_phy.h')).read()
+    assert int(re.search(r'#define LTE_ABI_VERSION (\d+)', h).group(1)) == _capi.ABI_VERSION == 3
+    lib = _capi.load()
+    assert lib.lte_version() == 3
+    assert lib.lte_abi_check(3) == _capi.LTE_OK
+    assert lib.lte_abi_check(2) == _capi.LTE_EUNSUP
+    assert b'version 2' in lib.lte_last_error()
+    assert re.search(r'const double \*snr_db;', h)
+    assert dict(_capi.RunArgs._fields_)['snr_db'] == ctypes.POINTER(ctypes.c_double)
+
+
 def test_pilots_native_mt19937_matches_reference(golden):
     from lte_phy import _capi
     for cell in range(4):

@@ -135,12 +135,21 @@ def cpu_baseline(config=2, F=65536, seconds=15.0, procs=None, channel=None):
     for v in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
         os.environ[v] = '1'
     jobs = [(config, seconds, ids, channel) for ids in sample_ids(F, procs)]
-    with mp.get_context('spawn').Pool(procs) as pool:
+    # close() + join(), not the context manager's terminate(): the workers exit
+    # on their own (under rocprofv3 a terminate() leaves SIGTERM stack dumps)
+    pool = mp.get_context('spawn').Pool(procs)
+    try:
         res = pool.map(_cpu_worker, jobs)
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     n = sum(len(r[0]) for r in res)
     value = sum(len(r[0]) / r[1] for r in res)
     frames = sorted(x for r in res for x in r[0])
-    return {'value': value, 'unit': 'subframes/s', 'cores': procs, 'kind': 'port',
+    return {'value': value, 'unit': 'subframes/s', 'cores': procs, 'kind': 'port', 'host_cores': os.cpu_count(),
             'per_core': value / procs, 'cpu_model': _cpu_model(),
             'sample': f'{n} of the bench\'s own config-{config} frames (ids from both ends of rank 0\'s first '
                       f'timed step, the oracle\'s restatement of the device Philox draws) over SNR 0:2:30 dB, '
@@ -311,12 +320,15 @@ def turbo_roofline(prec, tim, F, iters=8):
                 'shape_ceiling': ({'GBs': ceil, 'traffic_frac_of_ceiling': round(tr_gbs / ceil, 4) if tr_gbs else None,
                                    'source': 'profiles/r3_turbo_shape_microbench.json (another box: +-5 %)'}
                                   if ceil else None),
-                # same box, same layout: the decoder's access shape with and
-                # without its stores (extrinsic + checkpoint rows, 17 % of the bytes)
+                # the decoder's access shape with and without its stores (extrinsic +
+                # checkpoint rows, 17 % of the bytes): a STORED reference value from
+                # round 3, replaced by this box's own measurement when the shape bench
+                # runs after the timed region (same_box_shape_ceiling)
                 'store_cost': {'shape_ms_full': 319.5, 'shape_ms_reads_only': 237.4,
                                'store_share_of_time': round(1 - 237.4 / 319.5, 3), 'store_share_of_bytes': 0.17,
-                               'source': 'profiles/r3_turbo_shape_layouts.jsonl run shape4, variants aux3 / a3nost, '
-                                         'CH 32 (65 536 frames)'}},
+                               'measured_in_this_run': False,
+                               'source': 'stored: profiles/r3_turbo_shape_layouts.jsonl run shape4, variants aux3 / '
+                                         'a3nost, CH 32 (65 536 frames), another box'}},
             'stage_bytes': {'bytes_per_launch': int(stage_bytes),
                             'achieved_GBs': round(stage_bytes / avg_s / 1e9, 2) if t_n else 0.0,
                             'frac': round(stage_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if t_n else 0.0,
@@ -400,11 +412,19 @@ def same_box_shape_ceiling(hrs, F):
         d = json.loads(r.stdout.strip().splitlines()[-1])
     except (subprocess.SubprocessError, ValueError, IndexError, OSError):
         return
-    ceil = d['decoder_layout']['GBs_best']
+    dl = d['decoder_layout']
+    ceil = dl['GBs_best']
     tr = hrs.get('traffic_GBs')
     hrs['shape_ceiling'] = {'GBs': ceil, 'traffic_frac_of_ceiling': round(tr / ceil, 4) if tr else None,
-                            'shape_ms': {k: d['decoder_layout'][k] for k in ('ms_1wps', 'ms_2wps', 'ms_free')},
+                            'shape_ms': {k: dl[k] for k in ('ms_1wps', 'ms_2wps', 'ms_free')},
                             'source': 'same box, same call: scripts/turbo_shape_bench F decoder after the timed region'}
+    if 'ms_1wps_reads_only' in dl:
+        full, ro = dl['ms_1wps'], dl['ms_1wps_reads_only']
+        hrs['store_cost'] = {'shape_ms_full': full, 'shape_ms_reads_only': ro,
+                             'store_share_of_time': round(1 - ro / full, 3), 'store_share_of_bytes': 0.17,
+                             'measured_in_this_run': True,
+                             'source': 'same box, same call: the shape at one wave per SIMD with and without its '
+                                       'extrinsic / checkpoint stores (scripts/turbo_shape_bench F decoder)'}
 
 
 def merge_timers(all_tim):
@@ -458,6 +478,28 @@ def dry_run_counts(ids, S, n_bits=TB):
     np.add.at(c[:, 2], si, (ids % np.uint64(3) == 0).astype(np.uint64))
     np.add.at(c[:, 3], si, np.uint64(1))
     return c
+
+
+# --dry-run: each config's plan geometry (what lte_plan_info reports for the
+# bench plan) and synthetic per-stage timers, so the N > 1 rehearsal prices
+# the same roofline as a GPU run (the line is marked dry_run)
+DRY_GEOM = {
+    2: dict(L=14 * 2192, n_sym=14, n_bits=TB, num_rx=1, num_tx=1),
+    3: dict(L=14 * 1096, n_sym=14, n_bits=14 * 499 * 4, num_rx=4, num_tx=1),
+    4: dict(L=14 * 2192, n_sym=14, n_bits=TB, num_rx=2, num_tx=2, n_dsc=998, n_est=1),
+    5: dict(L=14 * 2192, n_sym=14, n_bits=14 * 999 * 6, num_rx=4, num_tx=4, n_dsc=250, n_est=14),
+}
+DRY_STAGE_SHARE = {2: {'turbo': 0.87, 'ofdm_tx': 0.04, 'rx_data': 0.045, 'dematch': 0.03},
+                   3: {'ofdm_tx': 0.3, 'rx_data': 0.65},
+                   4: {'turbo': 0.69, 'ofdm_tx': 0.08, 'channel': 0.1, 'rx_chest': 0.07, 'dematch': 0.03},
+                   5: {'ofdm_tx': 0.25, 'channel': 0.05, 'rx_chest': 0.45, 'rx_data': 0.2}}
+
+
+def dry_run_timers(config, el, steps, rank):
+    """Synthetic kernel timers (ms, launches) of one rank: each stage's share
+    of the elapsed time, rank r 1 % slower per rank (exercises the slowest-rank
+    gather)."""
+    return {k: (f * el * 1e3 * (1 + 0.01 * rank), steps) for k, f in DRY_STAGE_SHARE[config].items()}
 
 
 def make_plan(config, args):
@@ -555,8 +597,11 @@ def main():
     F = args.frames
     counts = np.zeros((S, 4), dtype=np.uint64)
     prec = args.precision
+    geom = None   # the plan's geometry for the uncoded configs' stage bytes
     if args.dry_run:
+        import types
         plan = None
+        geom = types.SimpleNamespace(**DRY_GEOM[args.config])
         dev_id = f'rank{rank}'
         step = lambda k: dry_run_counts(D.frame_ids(k, rank, world, F), S, wl['n_bits'])   # noqa: E731
     else:
@@ -565,6 +610,7 @@ def main():
         props = torch.cuda.get_device_properties(local)
         dev_id = f"{getattr(props, 'pci_bus_id', '')}:{getattr(props, 'uuid', local)}"
         plan = make_plan(args.config, args)
+        geom = plan
         prec = plan.precision
 
         def step(k):
@@ -598,7 +644,7 @@ def main():
     elif args.dry_run:
         # --dry-run: synthetic per-rank kernel timers (exercise the roofline
         # gather; the line is marked dry_run)
-        tim = {'turbo': (0.8 * el * 1e3 * (1 + 0.01 * rank), args.steps)}
+        tim = dry_run_timers(args.config, el, args.steps, rank)
 
     el = D.allreduce_max(el, dist)
     counts = D.allreduce_counts(counts, dist)
@@ -631,7 +677,7 @@ def main():
            'config': {'workload': workload, 'bench_config': args.config, 'velocity_kmh': args.velocity,
                       'frames_per_step_per_gpu': F, 'global_batch': F * world, 'parallelism': f'dp{world}',
                       'ranks': world, 'snr_db': SNRS.tolist()},
-           'roofline': (roofline(args.config, prec, tim, args.steps, F, el, value, world, args.iters, plan)
+           'roofline': (roofline(args.config, prec, tim, args.steps, F, el, value, world, args.iters, geom)
                         if tim else None),
            'ber': [float(f'{b:.4e}') for b in ber], 'bler': [float(f'{b:.4e}') for b in bler]}
     if args.dry_run:
@@ -646,7 +692,9 @@ def main():
         if cpu:
             cpu = {k: v for k, v in cpu.items() if k not in ('frames', 'config')}
             if world > 1:
-                cpu['note'] = f'{cpu["cores"]} host cores of the node ({CPU_PER_GPU} per GPU)'
+                cpu['note'] = (f'{cpu["cores"]} single-threaded worker processes, one per core '
+                               f'({cpu.get("host_cores", "?")} CPUs visible to the launcher; the CPU share is up to '
+                               f'{CPU_PER_GPU} per GPU, {CPU_PER_GPU * world} for {world} GPUs)')
         out['cpu_baseline'] = cpu
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -1,0 +1,2 @@
+"""Alias of core/channel_coding/turbo_encoder.py -> lte_phy.channel_coding."""
+from lte_phy.channel_coding import qpp_deinterleave, qpp_interleave, turbo_encode  # noqa: F401

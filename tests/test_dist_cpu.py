@@ -116,7 +116,50 @@ def test_bench_self_launches_ranks_dry_run():
     # the BER-match sample comes from the CPU baseline's oracle frames; no device here
     assert out['ber_match'] is None and 'frames' not in cpu
     # rank 1's synthetic timer is 1 % slower: the merged timer is the max
-    assert abs(roof['avg_launch_ms'] - 0.8 * out['ms_per_step'] * 1.01) < 0.05 * out['ms_per_step']
+    assert abs(roof['avg_launch_ms'] - 0.87 * out['ms_per_step'] * 1.01) < 0.05 * out['ms_per_step']
+
+
+@pytest.mark.parametrize('config', [4, 5])
+def test_bench_other_configs_dry_run_world2(config):
+    """`bench.py --config 4|5 --gpus 2 --dry-run`: config 5 is the config
+    BASELINE names for the 8-GPU sharded grid.  The line sums both ranks'
+    counters (each config's own payload size), carries a roofline priced on
+    the slowest rank (config 4: the decoder's K7 view; config 5: the dominant
+    stage against HBM with the plan's stage bytes) and a cpu_baseline whose
+    note states the cores actually used."""
+    import json
+    from lte_phy import dist as D
+    F, steps = 64, 2
+    r = _bench(['--config', str(config), '--gpus', '2', '--dry-run', '--steps', str(steps), '--warmup', '0',
+                '--frames', str(F), '--cpu-seconds', '0.3'])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(line) == 1, r.stdout
+    out = json.loads(line[0])
+    nb = {4: 27760, 5: 14 * 999 * 6}[config]
+    ids = np.concatenate([D.frame_ids(k, rk, 2, F) for k in range(steps) for rk in range(2)])
+    si = D.snr_index(ids, 16)
+    ref = np.zeros((16, 4), dtype=np.uint64)
+    np.add.at(ref[:, 0], si, ids % np.uint64(7))
+    np.add.at(ref[:, 1], si, np.uint64(nb))
+    np.add.at(ref[:, 2], si, (ids % np.uint64(3) == 0).astype(np.uint64))
+    np.add.at(ref[:, 3], si, np.uint64(1))
+    assert np.array_equal(np.array(out['counts'], dtype=np.uint64), ref)
+    assert out['config']['bench_config'] == config and out['n_gpus'] == 2
+    roof = out['roofline']
+    assert roof is not None
+    if config == 4:
+        assert roof['kernel'] == 'k_turbo64' and roof['frac'] > 0 and 'hbm_row_stream' in roof
+    else:
+        # rx_chest (k_rx_fft_mimo) is the largest synthetic stage: y in + Y + H out per frame
+        assert roof['bound'] == 'hbm' and roof['stage'] == 'rx_chest' and roof['unit'] == 'GB/s'
+        c = 16
+        assert roof['alg_bytes_per_frame'] == round(4 * 14 * 2192 * c + 14 * 4 * 250 * c + 4 * 14 * 4 * 250 * c)
+        assert set(roof['other_stages']) == {'ofdm_tx', 'channel', 'rx_data'}
+    cpu = out['cpu_baseline']
+    assert cpu['cores'] == min(32, os.cpu_count())
+    assert cpu['note'].startswith(f"{cpu['cores']} single-threaded worker processes")
+    assert f"{os.cpu_count()} CPUs visible" in cpu['note']
 
 
 def test_merge_timers_takes_slowest_rank():

@@ -143,7 +143,7 @@ def test_other_config_bench_frames_match_oracle(C, config):
     configs' default batches) through the float64 GPU chains and the oracle's
     compositions on the oracle's Philox draws (SIMO MRC, SFBC 2x2 + turbo, 4x4
     MMSE on flat CN(0,1) links): identical per-frame bit errors (and CRC)."""
-    F_c = {3: 65536, 4: 49152, 5: 32768}[config]
+    F_c = {3: 65536, 4: 65536, 5: 32768}[config]
     ids = np.concatenate([np.arange(12), F_c - 16 + np.array([8, 10, 12, 15])]).astype(np.uint64)
     S = len(P.BENCH_SNRS)
     si = (ids % np.uint64(S)).astype(np.int32)

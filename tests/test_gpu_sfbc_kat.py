@@ -67,3 +67,34 @@ def test_stage_errors(al):
         al.encode(np.ones(3, complex))
     t0, t1 = al.encode(np.zeros(0, complex))
     assert t0.shape == (0,) and t1.shape == (0,)
+
+
+def test_reference_callers_through_compat_paths():
+    """The reference's own import lines with only PYTHONPATH changed
+    (ofdm-lte_amd/compat): test/test_alamouti_unit.py:11's `from
+    core.sfbc_alamouti import SFBCAlamouti` runs its KAT on the HIP path, and
+    examples/example_basic.py:17's `from module import OFDMModule, LTEConfig`
+    transmits through the GPU chain (a child process, one GPU call each)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    code = r'''
+import numpy as np
+from core.sfbc_alamouti import SFBCAlamouti
+from module import OFDMModule, LTEConfig
+al = SFBCAlamouti(num_tx=2, enabled=True)
+s0, s1 = 1.0 + 1.0j, -1.0 + 1.0j
+tx0, tx1 = al.encode(np.array([s0, s1]))
+rx = np.array([tx0[0] + 1j * tx1[0], tx0[1] + 1j * tx1[1]])
+dec = al.decode(rx, np.array([1.0 + 0j, 1.0 + 0j]), np.array([1j, 1j]), regularization=1e-10)
+assert abs(dec[0] - s0) < 1e-10 and abs(dec[1] - s1) < 1e-10
+m = OFDMModule()
+r = m.transmit(np.random.RandomState(0).randint(0, 2, 10000), snr_db=20)
+assert r['ber'] < 1e-2, r['ber']
+print('ok', m.config.bandwidth, r['ber'])
+'''
+    env = dict(os.environ)
+    env['PYTHONPATH'] = os.path.join(ROOT, 'ofdm-lte_amd', 'compat')
+    r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=240, cwd='/tmp')
+    assert r.returncode == 0 and 'ok' in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])

@@ -14,6 +14,7 @@
 
 #include "lte_common.h"
 #include "lte_internal.h"
+#include "lte_dev.h"
 
 using namespace lte;
 
@@ -389,7 +390,8 @@ namespace lte {
 template <class R>
 __global__ void k_cap_rx(int L, int num_rx, int B, const cx<R>* __restrict__ y, int64_t y_rx_stride,
                          int64_t y_frame_stride, const R* __restrict__ npow, const uint64_t* __restrict__ fid,
-                         uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride, cx<R>* __restrict__ out) {
+                         uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride, cx<R>* __restrict__ out,
+                         const R* __restrict__ link_sigma, int num_tx) {
   const int nb = (L + 255) / 256;
   const int n = (blockIdx.x % nb) * blockDim.x + threadIdx.x;
   const int rx = blockIdx.y, b = blockIdx.x / nb;
@@ -403,7 +405,10 @@ __global__ void k_cap_rx(int L, int num_rx, int B, const cx<R>* __restrict__ y, 
     const u32x4 r = rng4(seed, fid[b], RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)(n >> 1));
     z = (n & 1) ? gauss2<R>(r.z, r.w) : gauss2<R>(r.x, r.y);
   }
-  const cx<R> v = y[b * y_frame_stride + rx * y_rx_stride + n];
+  cx<R> v = y[b * y_frame_stride + rx * y_rx_stride + n];
+  if (link_sigma)   // config 4's fused path: y holds the faded signal; its link noise first (k_rx_fft_mimo LN)
+    v = link_noise_at<R>(n, rx_link_sigma(link_sigma, ((size_t)b * num_rx + rx) * num_tx, num_tx), nullptr, 0, seed,
+                         fid[b], rx * num_tx, v);
   out[((size_t)b * num_rx + rx) * L + n] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
 }
 }  // namespace lte
@@ -647,7 +652,7 @@ static int channel_host(int64_t L, int num_rx, int channel, int n_paths, const i
     const V* ys = ray ? dy.p : dx.p;
     hipLaunchKernelGGL(k_cap_rx<R>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
                        1, ys, ray ? L : 0, ray ? (int64_t)num_rx * L : L, dnp.p, dfid.p, seed,
-                       noise ? dz.p : nullptr, 0, dout.p);
+                       noise ? dz.p : nullptr, 0, dout.p, nullptr, 0);
     ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
          hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(V), hipMemcpyDeviceToHost) == hipSuccess &&
          (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(R), hipMemcpyDeviceToHost) == hipSuccess);
@@ -705,7 +710,7 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
   m.n_cs = (ray && fD != 0.0 && !m.exact_jakes) ? (int)((L + chunk - 1) / chunk) : 1;
   const int np = ray ? n_paths : 1;
   // partial-sum slots: 256-sample blocks (link stats) or OFDM-symbol blocks (channel), whichever is more
-  const int nblk = std::max((int)((L + 255) / 256), mimo_channel_pblk<R>(g, m));
+  const int nblk = std::max((int)((L + 255) / 256), mimo_channel_nblk(g.L, g.N + g.cp));
   const size_t links = (size_t)num_rx * num_tx;
   const bool link_noise_on = mode == 0 && ray;
   DBuf<V> dx, dy, dcoef, dout;
@@ -746,14 +751,13 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
                                    (!ray && mode == 1 && link_h) ? dlh.p : nullptr, 0, dcoef.p, dphs.p) == 0;
   const R* lz = (link_noise_on && link_noise) ? dlz.p : nullptr;
   ok = ok && launch_channel_mimo<R>(nullptr, g, m, 1, np, ray ? ddel.p : nullptr, dcoef.p, dphs.p, dgain.p, fs, dx.p,
-                                    dy.p, link_noise_on ? 1 : 0, dfid.p, seed, lz, 0, dlp.p, dls.p, dpp.p, nblk, 0,
-                                    ray ? *std::max_element(delays, delays + n_paths) : 0) == 0;
-  ok = ok && launch_npow_mimo<R>(nullptr, 1, num_rx, dpp.p, mimo_channel_pblk<R>(g, m), (int)L, dsl.p,
+                                    dy.p, link_noise_on ? 1 : 0, dfid.p, seed, lz, 0, dlp.p, dls.p, dpp.p, nblk, 0) == 0;
+  ok = ok && launch_npow_mimo<R>(nullptr, 1, num_rx, dpp.p, mimo_channel_nblk(g.L, g.N + g.cp), (int)L, dsl.p,
                                  mode == 0 ? (double)num_tx : 1.0, dnp.p) == 0;
   if (ok) {
     hipLaunchKernelGGL(k_cap_rx<R>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
                        dy.p, (int64_t)L, (int64_t)num_rx * L, dnp.p, dfid.p, seed, noise ? dz.p : nullptr, 0,
-                       dout.p);
+                       dout.p, nullptr, 0);
     ok = hipGetLastError() == hipSuccess;
   }
   if (ok && link_stats) {
@@ -1669,7 +1673,25 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   const int nch = mimo_channel_nblk(p->L, g.N + g.cp);
   const bool flat_fuse = !ray && !a->cap_signal_tx && !a->cap_link_stats && (g.N >> 3) >= 64 && m.num_tx <= 4 &&
                          env_on("LTE_MIMO_FLAT_FUSE", true);
-  if (flat_fuse) {
+  // config 4 (SFBC, static-tap Rayleigh links with the 100 dB link noise, Philox
+  // draws): TX and the links' fading in one pass per frame writing the faded RX
+  // signals (k_ofdm_txch_sfbc), then the RX power with the link noise
+  // (k_link_noise_power), which the receiver draws again and adds (k_rx_fft_mimo
+  // LN) -- x never goes through HBM, the link noise never does.  Captures of x / the link statistics and the
+  // reference's own (injected) link noise keep the separate kernels.
+  const bool sfbc_fuse = link_noise && !inj_lz && !inj_z && !a->cap_signal_tx && !a->cap_link_stats &&
+                         sfbc_txch_supported<R>(g, m, d.n_paths, maxd) && env_on("LTE_SFBC_TXCH_FUSE", true);
+  if (sfbc_fuse) {
+    const TxLinkPower<R> lf{p->delays.p, c.coef.p, c.link_part.p, d.n_paths, maxd, 1};
+    {
+      Timer t(p, KN_OFDM_TX);
+      LCHK(launch_ofdm_txch_sfbc<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, lf,
+                                    c.y.p, B));
+    }
+    Timer t(p, KN_CHANNEL);
+    LCHK(launch_link_noise_power<R>(s, g, m, B, c.link_part.p, c.link_sigma.p, c.y.p, p->fid.p, a->seed,
+                                    c.pow_part.p));
+  } else if (flat_fuse) {
     Timer t(p, KN_OFDM_TX);
     LCHK(launch_ofdm_txch_flat<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p,
                                   c.coef.p, c.y.p, c.pow_part.p, nch, B));
@@ -1683,17 +1705,18 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     Timer t(p, KN_CHANNEL);
     LCHK(launch_channel_mimo<R>(s, g, m, B, np, ray ? p->delays.p : nullptr, c.coef.p, phases, c.gains.p, d.fs, c.x.p,
                                 c.y.p, link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, c.link_part.p,
-                                c.link_sigma.p, c.pow_part.p, p->nblk, lp_fuse ? 1 : 0, maxd));
+                                c.link_sigma.p, c.pow_part.p, p->nblk, lp_fuse ? 1 : 0));
   }
   {
     Timer t(p, KN_CHANNEL);
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
-    LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, flat_fuse ? nch : mimo_channel_pblk<R>(g, m), p->L,
-                             c.snr_lin.p, sfbc ? (double)m.num_tx : 1.0, c.npow.p));
+    LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, nch, p->L, c.snr_lin.p, sfbc ? (double)m.num_tx : 1.0,
+                             c.npow.p));
   }
   {
     Timer t(p, KN_RX_CHEST);
-    LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p));
+    LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p,
+                               sfbc_fuse ? c.link_sigma.p : nullptr));
   }
   V* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
@@ -1769,7 +1792,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
       Timer t(p, KN_CAP);
       hipLaunchKernelGGL(k_cap_rx<R>, dim3(((p->L + 255) / 256) * B, m.num_rx), dim3(256), 0, s, p->L, m.num_rx, B,
                          c.y.p, (int64_t)p->L, (int64_t)m.num_rx * p->L, c.npow.p, p->fid.p, a->seed, inj_z,
-                         inj_z_stride, tmp.p);
+                         inj_z_stride, tmp.p, sfbc_fuse ? c.link_sigma.p : nullptr, m.num_tx);
       LCHK((int)hipGetLastError());
     }
     HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * m.num_rx * p->L * sizeof(V), hipMemcpyDeviceToHost, s));
@@ -2172,7 +2195,7 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     {
       Timer t(p, KN_CAP);
       hipLaunchKernelGGL(k_cap_rx<R>, dim3(((p->L + 255) / 256) * B, rx), dim3(256), 0, s, p->L, rx, B, ysrc, yrs, yfs,
-                         c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p);
+                         c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p, nullptr, 0);
       LCHK((int)hipGetLastError());
     }
     HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * rx * p->L * sizeof(V), hipMemcpyDeviceToHost, s));

@@ -409,6 +409,127 @@ __device__ __forceinline__ void fft_lds(V* buf, int N_, int log2N_, const V* __r
   }
 }
 
+// Two transforms of the same compile-time size NC in one sweep (buffers a and
+// b, e.g. the two TX grids of an Alamouti symbol): the passes of fft_lds<INV,
+// NC, SC, TWR = true> on both, sharing each butterfly's twiddles and the
+// barriers (half of them, and twice the independent work between them).
+// Outputs identical to two fft_lds calls (the same operations per element).
+template <bool INV, int NC, bool SC = false, class V>
+__device__ __forceinline__ void fft2_lds(V* a, V* b, const V* __restrict__ tw, int tid, bool active,
+                                         re_t<V> osc = (re_t<V>)1) {
+  static_assert(NC >= 128, "compile-time N only");
+  constexpr int N = NC, log2N = __builtin_ctz(NC), T = N >> 3;
+  constexpr int n8 = log2N / 3, rem = log2N - 3 * n8;
+  V* bufs[2] = {a, b};
+  int Ns = 1, lNs = 0;
+#pragma unroll
+  for (int s = 0; s < n8; ++s) {
+    const bool rsw = s > 0, wsw = !(s == n8 - 1 && rem == 0);
+    V v[2][8];
+    const int j = tid;
+    if (active) {
+      V w[8];
+      if (s > 0) {
+        const int ks = (j & (Ns - 1)) * (N >> (lNs + 3));
+        w[1] = twid<INV>(tw, ks);
+        w[2] = cmul(w[1], w[1]);
+        w[3] = cmul(w[2], w[1]);
+        w[4] = cmul(w[2], w[2]);
+        w[5] = cmul(w[4], w[1]);
+        w[6] = cmul(w[3], w[3]);
+        w[7] = cmul(w[4], w[3]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int i = j + r * T;
+          v[u][r] = bufs[u][rsw ? fft_sw<V>(i) : i];
+        }
+        if (s > 0) {
+#pragma unroll
+          for (int r = 1; r < 8; ++r) v[u][r] = cmul(v[u][r], w[r]);
+        }
+        dft8_inplace<INV>(v[u]);
+      }
+    }
+    __syncthreads();
+    if (active) {
+      const int idx = ((j >> lNs) << (lNs + 3)) + (j & (Ns - 1));
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int i = idx + r * Ns;
+          bufs[u][wsw ? fft_sw<V>(i) : i] = (SC && !wsw) ? cscale(v[u][r], osc) : v[u][r];
+        }
+    }
+    __syncthreads();
+    Ns <<= 3;
+    lNs += 3;
+  }
+  if constexpr (rem == 2) {   // final radix-4 pass: two butterflies per thread and buffer
+    constexpr int q4 = N >> 2;
+    V v[2][2][4];
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = tid + q * T;
+        const V w1 = twid<INV>(tw, j), w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[u][q][r] = bufs[u][fft_sw<V>(j + r * q4)];
+          v[u][q][1] = cmul(v[u][q][1], w1);
+          v[u][q][2] = cmul(v[u][q][2], w2);
+          v[u][q][3] = cmul(v[u][q][3], w3);
+          dft4_inplace<INV>(v[u][q][0], v[u][q][1], v[u][q][2], v[u][q][3]);
+        }
+      }
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int j = tid + q * T;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bufs[u][j + r * q4] = SC ? cscale(v[u][q][r], osc) : v[u][q][r];
+        }
+    }
+    __syncthreads();
+  } else if constexpr (rem == 1) {   // final radix-2 pass
+    constexpr int h = N >> 1;
+    V v[2][4][2];
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = tid + q * T;
+        const V w = twid<INV>(tw, j);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const V x0 = bufs[u][fft_sw<V>(j)], x1 = cmul(bufs[u][fft_sw<V>(j + h)], w);
+          v[u][q][0] = cadd(x0, x1);
+          v[u][q][1] = csub(x0, x1);
+        }
+      }
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = tid + q * T;
+          bufs[u][j] = SC ? cscale(v[u][q][0], osc) : v[u][q][0];
+          bufs[u][j + h] = SC ? cscale(v[u][q][1], osc) : v[u][q][1];
+        }
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- CRC-24 algebra
 // The LTE CRCs (crc.py:89-184: zero initial register, no reflection, no final
 // XOR) are linear over GF(2): crc(M) = M(x) x^24 mod P.  A message split into

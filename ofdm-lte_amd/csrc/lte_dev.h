@@ -169,18 +169,55 @@ __device__ __forceinline__ float2 zf_div(float2 y, float2 h) {
 __device__ __forceinline__ float2 zf_eq(float2 y, float2 h) { return zf_div(y, make_float2(h.x + 1e-6f, h.y)); }
 __device__ __forceinline__ double2 zf_eq(double2 y, double2 h) { return cdiv(y, make_double2(h.x + 1e-6, h.y)); }
 
+// the link's 100 dB noise: y + (s z_re + j s z_im) (injected [2][L] or Philox)
+template <class R>
+__device__ __forceinline__ cx<R> link_noise_at(int n, R sg, const R* __restrict__ zf, int L, uint64_t seed,
+                                               uint64_t frame, int link, cx<R> v) {
+  cx<R> z;
+  if (zf) {
+    z = mkc(zf[n], zf[L + n]);
+  } else {
+    const u32x4 rr = rng4(seed, frame, RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
+    z = (n & 1) ? gauss2<R>(rr.z, rr.w) : gauss2<R>(rr.x, rr.y);
+  }
+  return mkc(v.x + sg * z.x, v.y + sg * z.y);
+}
+
+// transmit_mimo's 100 dB link noise on the Philox path, per receive antenna:
+// the num_tx links' independent complex Gaussians (standard deviations s_rt,
+// k_link_sigma) sum to one complex Gaussian of standard deviation
+// sqrt(sum_t s_rt^2), drawn once per RX sample on link (r, 0)'s stream -- the
+// same distribution as one draw per link at 1 / num_tx of the draws.  (Injected
+// link noise, the reference's own draws, is still added per link.)
+template <class R>
+__device__ __forceinline__ R rx_link_sigma(const R* __restrict__ link_sigma, size_t lk0, int num_tx) {
+#pragma clang fp contract(off)
+  R s2 = (R)0;
+  for (int t = 0; t < num_tx; ++t) {
+    const R s = link_sigma[lk0 + t];
+    s2 = s2 + s * s;
+  }
+  return sqrt(s2);
+}
+
 // Noise-add for one OFDM symbol into LDS, one Philox call per pair of
 // samples (sample n uses half (n&1) of counter n>>1 -- same draws as
 // load_symbol_noisy, at half the generator cost).  Lane t stores samples 2t
 // and 2t + 1 (a stride-2 ds_write pattern, 2-way on 16-B and 8-B elements);
 // SW = true stores them swizzled (conflict-free) for fft_lds<.., ISW = true>.
-template <bool SW = false, class V>
+// LN: a second Gaussian per sample added first, v = (y + sig_l z_l) + sigma z --
+// transmit_mimo's 100 dB link noise of the RX (the combined draw of
+// rx_link_sigma, Philox stream lstream with the same pair mapping, counter n >> 1,
+// half n & 1) before its receiver noise, as the reference sums them (the
+// multi-antenna receiver of config 4; Philox draws only, zf must be null).
+template <bool SW = false, bool LN = false, class V>
 __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__ yf, int N, int cp, int l,
                                                    re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
-                                                   const re_t<V>* __restrict__ zf, int L, int tid, int T) {
+                                                   const re_t<V>* __restrict__ zf, int L, int tid, int T,
+                                                   re_t<V> sig_l = 0, uint32_t lstream = 0) {
   using R = re_t<V>;
   const int off = l * (N + cp) + cp;
-  if (zf) {
+  if (!LN && zf) {
     load_symbol_noisy<SW>(buf, yf, N, cp, l, sigma, seed, frame, rx, zf, L, tid, T);
     return;
   }
@@ -201,6 +238,12 @@ __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__
     const int p = p0 + tid + i * T, n0 = 2 * p;
     if (p > p1) break;
     const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
+    if constexpr (LN) {
+      const u32x4 q = rng4(seed, frame, lstream, (uint32_t)p);
+      const V za = gauss2<R>(q.x, q.y), zb = gauss2<R>(q.z, q.w);
+      va[i] = mkc(va[i].x + sig_l * za.x, va[i].y + sig_l * za.y);
+      vb[i] = mkc(vb[i].x + sig_l * zb.x, vb[i].y + sig_l * zb.y);
+    }
     if (n0 >= off) {
       const V z = gauss2<R>(r.x, r.y);
       buf[SW ? fft_sw<V>(n0 - off) : n0 - off] = mkc(va[i].x + sigma * z.x, va[i].y + sigma * z.y);

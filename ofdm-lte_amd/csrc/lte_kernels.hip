@@ -1311,7 +1311,10 @@ __device__ __forceinline__ cx<R> chest_interp(const Grid& g, const cx<R>* hp, in
 #ifndef RXF_WAVES
 #define RXF_WAVES 3
 #endif
-template <class R, int CHAIN, int BPS, int NC = 0>
+// ZN (coded, the default): the equalised symbols go to k_dematch_zn and the
+// per-subcarrier sigma^2_eff to nvo at each estimate, so no per-RE noise
+// variance stays live across the symbol loop (8 VGPRs of the f64 instance)
+template <class R, int CHAIN, int BPS, int NC = 0, bool ZN = false>
 __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh, int B, const cx<R>* __restrict__ y,
                                                  int64_t y_frame_stride, const R* __restrict__ npow,
                                                  const R* __restrict__ snr_lin, const uint64_t* __restrict__ fid,
@@ -1381,8 +1384,9 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh
             const V h = chest_interp<R>(g, hp, kpos[q]);
             zc[q].set(mkc(h.x + (R)1e-6, h.y));
             const R den = abs2_ref(h);
-            nvq[q] = rayleigh ? fmax(s2 / fmin(fmax(den, (R)1e-6), (R)1e6), s2 / (R)4) : s2;
-            if (nvo) nvo[((size_t)b * g.n_grp + grp) * g.Nd + j] = nvq[q];
+            const R nv = rayleigh ? fmax(s2 / fmin(fmax(den, (R)1e-6), (R)1e6), s2 / (R)4) : s2;
+            if constexpr (ZN) nvo[((size_t)b * g.n_grp + grp) * g.Nd + j] = nv;
+            else nvq[q] = nv;
           }
         }
         if (RXF_EXP != 1 && pstats && tid == 0) {
@@ -1408,11 +1412,10 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh
         const V Y = cscale(buf[kpos[q]], sc);
         const V z = (CHAIN == LTE_CHAIN_UNCODED && g.no_eq) ? Y : zc[q].apply(Y);
         if (cap_syms) cap_syms[fre + re] = z;
-        if constexpr (CHAIN == LTE_CHAIN_CODED) {
-          if (nvo) {   // demap in k_dematch_zn: the equalised symbol (sigma^2_eff per subcarrier in nvo)
-            reinterpret_cast<V*>(llr)[fre + re] = z;
-            continue;
-          }
+        if constexpr (CHAIN == LTE_CHAIN_CODED && ZN) {
+          // demap in k_dematch_zn: the equalised symbol (sigma^2_eff per subcarrier in nvo)
+          reinterpret_cast<V*>(llr)[fre + re] = z;
+        } else if constexpr (CHAIN == LTE_CHAIN_CODED) {
           R o[BPS];
           soft_demap<BPS>(z, nvq[q], o);
           R* lo = llr + (fre + re) * BPS;
@@ -1457,9 +1460,16 @@ int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B
   const int blocks = (B + spw - 1) / spw;
   const size_t shm = (size_t)spw * (g.N + g.Np) * sizeof(cx<R>);
 #define LTE_RXF(CH_, BPS_, NC_)                                                                                      \
-  hipLaunchKernelGGL((k_rx_frame<R, CH_, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, y,             \
-                     y_frame_stride, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, llr,    \
-                     cap_syms, cap_bits, nv_out, H, pstats)
+  do {                                                                                                               \
+    if (CH_ == LTE_CHAIN_CODED && nv_out)                                                                            \
+      hipLaunchKernelGGL((k_rx_frame<R, CH_, BPS_, NC_, CH_ == LTE_CHAIN_CODED>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, y,   \
+                         y_frame_stride, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err,    \
+                         llr, cap_syms, cap_bits, nv_out, H, pstats);                                                \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_rx_frame<R, CH_, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, rayleigh, B, y,         \
+                         y_frame_stride, npow, snr_lin, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err,    \
+                         llr, cap_syms, cap_bits, nv_out, H, pstats);                                                \
+  } while (0)
 #define LTE_RXF_BPS(CH_, NC_)                                                                                        \
   do {                                                                                                               \
     if (g.bps == 2) LTE_RXF(CH_, 2, NC_);                                                                            \

@@ -774,37 +774,6 @@ __device__ __forceinline__ void links_accumulate(cx<R> (&acc)[G][J], int nq, con
   }
 }
 
-// the link's 100 dB noise: y + (s z_re + j s z_im) (injected [2][L] or Philox)
-template <class R>
-__device__ __forceinline__ cx<R> link_noise_at(int n, R sg, const R* __restrict__ zf, int L, uint64_t seed,
-                                               uint64_t frame, int link, cx<R> v) {
-  cx<R> z;
-  if (zf) {
-    z = mkc(zf[n], zf[L + n]);
-  } else {
-    const u32x4 rr = rng4(seed, frame, RNG_STREAM_MIMO_LINK + (uint32_t)link, (uint32_t)(n >> 1));
-    z = (n & 1) ? gauss2<R>(rr.z, rr.w) : gauss2<R>(rr.x, rr.y);
-  }
-  return mkc(v.x + sg * z.x, v.y + sg * z.y);
-}
-
-// transmit_mimo's 100 dB link noise on the Philox path, per receive antenna:
-// the num_tx links' independent complex Gaussians (standard deviations s_rt,
-// k_link_sigma) sum to one complex Gaussian of standard deviation
-// sqrt(sum_t s_rt^2), drawn once per RX sample on link (r, 0)'s stream -- the
-// same distribution as one draw per link at 1 / num_tx of the draws.  (Injected
-// link noise, the reference's own draws, is still added per link.)
-template <class R>
-__device__ __forceinline__ R rx_link_sigma(const R* __restrict__ link_sigma, size_t lk0, int num_tx) {
-#pragma clang fp contract(off)
-  R s2 = (R)0;
-  for (int t = 0; t < num_tx; ++t) {
-    const R s = link_sigma[lk0 + t];
-    s2 = s2 + s * s;
-  }
-  return sqrt(s2);
-}
-
 // The link noise of a SymSpan's J samples (Philox path; the same values as
 // link_noise_at per sample).  With an even base, lane pair (2k, 2k+1) holds
 // sample pairs (n, n + 1) that share one Philox draw (counter n >> 1): the
@@ -893,6 +862,230 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
   double acc = 0.0;
   for (int k = 0; k < nblk; ++k) acc += part[(size_t)i * nblk + k];
   sigma[i] = (R)sqrt(((acc / L) / 1e10) / 2.0);
+}
+
+// ---------------------------------------------------------------------------
+// Config 4's TX and its static-tap Rayleigh links in one pass (SFBC 2 x NRX,
+// transmit_mimo core/ofdm_core.py:434-543 with every link a 100 dB
+// ChannelSimulator, :490-503).  One slot (the block's 256 threads) per frame
+// walks the frame's OFDM symbols.  Per symbol both TX grids (the Alamouti pairs
+// of SFBCAlamouti.encode + SFBCResourceMapper, core/sfbc_alamouti.py:45-78,
+// 213-256, each thread's pairs for both TX at once; each TX's CRS subset) are
+// built and IFFT'd in two LDS buffers, the last pass applying NumPy's sqrt(N)/N
+// output scale, so the buffers hold x_t.  Then for every sample n of the
+// CP-extended symbol and every RX r: y0_rt = sum_p c_rtp x_t[n - d_p] (each
+// link from zero, in path order) and y0_r = y0_r0 + y0_r1 (the links summed in
+// TX order, as mimo_oracle.transmit_mimo sums them); the delayed samples that
+// reach into the previous symbol come from its last TL samples of each TX,
+// kept in LDS -- the frame walks its symbols in order, so no fix-up pass is
+// needed.  Each link's power sum_n |y0_rt|^2 accumulates over the frame (the
+// link noise's standard deviation, k_link_sigma).  y0 goes to HBM once; the
+// TX streams x never do.  k_link_noise_power then forms the RX power with the
+// link noise, which the receiver (k_rx_fft_mimo<.., LN>) draws again and adds
+// before its own noise.  Static taps only (n_cs = 1), N = 2048 (two 32 KB
+// grids: two slots per CU).
+constexpr int SFX_TL = 32;   // largest max_delay (samples) the kept tails cover
+template <class R, int CODED, int BPS, int NRX, int NC = 2048>
+__global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
+                                                          const uint32_t* __restrict__ enc, int enc_words,
+                                                          const int32_t* __restrict__ tx_map, TxLinkPower<R> lp,
+                                                          cx<R>* __restrict__ y, int B, int stage_enc) {
+  using V = cx<R>;
+  constexpr int N = NC, T = N >> 3, NTX = 2, NCF = mimo_ncf<R>();
+  static_assert(T == MWG, "one slot per block");
+  __shared__ R red[MWG / 64];
+  // LDS: grids / x_t at [t * N, (t + 1) * N), then [NTX][SFX_TL] the previous
+  // symbol's last TL samples of each x_t (one array, so that a delayed sample's
+  // address is one index expression), then the staged coded streams
+  V* sm = mimo_lds<V>();
+  constexpr int TB0 = 2 * N;
+  const int tid0 = threadIdx.x, b = blockIdx.x;
+  const bool active = b < B;   // (grid = B blocks: always; kept for the shared FFT helper)
+  const int S = N + g.cp, TL = lp.max_delay, np = lp.n_paths;
+  const uint32_t* fb = pw + (size_t)b * PW;
+  const uint32_t* fe = enc + (size_t)b * enc_words;
+  if (CODED && stage_enc) {
+    uint32_t* es = reinterpret_cast<uint32_t*>(sm + TB0 + NTX * SFX_TL);
+    for (int i = tid0; i < enc_words; i += T) es[i] = fe[i];
+    fe = es;
+  }
+  for (int i = tid0; i < NTX * SFX_TL; i += T) sm[TB0 + i] = mkc((R)0, (R)0);   // zero prefix of the stream
+  int dl[TXCH_MAXP];
+#pragma unroll
+  for (int p = 0; p < TXCH_MAXP; ++p) dl[p] = p < np ? lp.delays[p] : 0;
+  R pwr[NRX][NTX];
+#pragma unroll
+  for (int r = 0; r < NRX; ++r)
+#pragma unroll
+    for (int t = 0; t < NTX; ++t) pwr[r][t] = (R)0;
+  const R sc = tx_scale<R>(N);
+  constexpr int SFP = 4;   // Alamouti pairs per thread per symbol (n_dsc / 2 <= SFP T)
+  for (int l = 0; l < g.n_sym; ++l) {
+    int tid = tid0;   // opaque per symbol: the FFT's addressing is not hoisted into registers
+    asm volatile("" : "+v"(tid));
+    for (int k = tid; k < 2 * N; k += T) sm[k] = mkc((R)0, (R)0);
+    __syncthreads();   // (first symbol: also the staged streams and the zeroed tails)
+    {
+      const int64_t q0 = (int64_t)l * m.res;
+#pragma unroll
+      for (int k = 0; k < SFP; ++k) {   // TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)]
+        const int j = 2 * (tid + k * T);
+        if (j >= m.n_dsc) break;
+        const V s0 = qam_of<R, BPS>(qam_code<CODED, BPS>(q0 + j, fb, fe, tx_map));
+        const V s1 = qam_of<R, BPS>(qam_code<CODED, BPS>(q0 + j + 1, fb, fe, tx_map));
+        const int k0 = g.data_idx[j];
+        sm[k0] = s0;
+        sm[N + k0] = s1;
+        if (j + 1 < m.n_dsc) {
+          const int k1 = g.data_idx[j + 1];
+          sm[k1] = mkc(-s1.x, s1.y);
+          sm[N + k1] = mkc(s0.x, -s0.y);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NTX; ++t) {
+        const V* pv = MGT<R>::pval(m) + t * m.maxP;
+        for (int p = tid; p < m.np_tx[t]; p += T) sm[t * N + m.ppos[t * m.maxP + p]] = pv[p];
+      }
+    }
+    __syncthreads();
+    // x_t = ifft(G_t) sqrt(N), both grids in one sweep (ends with a barrier)
+    fft2_lds<true, NC, true>(sm, sm + N, GridT<R>::tw(g), tid, active, sc);
+    // the frame's static taps c_rtp (coef [B][num_rx][num_tx][np][NCF], n_cs =
+    // 1), loaded per symbol into VGPRs for the sample loop only: as
+    // wave-uniform values the compiler would keep them in SGPRs and spill them
+    // to VGPR lanes inside the loop; held across the FFTs they would crowd them
+    V c[NRX][NTX][TXCH_MAXP];
+#pragma unroll
+    for (int r = 0; r < NRX; ++r)
+#pragma unroll
+      for (int t = 0; t < NTX; ++t) {
+        const V* cf = lp.coef + (((size_t)b * NRX + r) * NTX + t) * np * NCF;
+#pragma unroll
+        for (int p = 0; p < TXCH_MAXP; ++p) {
+          c[r][t][p] = p < np ? cf[p * NCF] : mkc((R)0, (R)0);
+          asm volatile("" : "+v"(c[r][t][p].x), "+v"(c[r][t][p].y));
+        }
+      }
+    V* yl = y + (size_t)b * NRX * g.L + (size_t)l * S;
+    for (int n = tid; n < S; n += T) {
+      V xs[NTX][TXCH_MAXP];   // x_t at CP-extended position n - d_p (negative: the previous symbol's tail)
+#pragma unroll
+      for (int p = 0; p < TXCH_MAXP; ++p)
+        if (p < np) {
+          const int i = n - dl[p];
+#pragma unroll
+          for (int t = 0; t < NTX; ++t) xs[t][p] = sm[i >= 0 ? t * N + ((i - g.cp) & (N - 1)) : TB0 + t * SFX_TL + TL + i];
+        }
+#pragma unroll
+      for (int r = 0; r < NRX; ++r) {
+        V a[NTX];
+#pragma unroll
+        for (int t = 0; t < NTX; ++t) {
+          a[t] = mkc((R)0, (R)0);
+#pragma unroll
+          for (int p = 0; p < TXCH_MAXP; ++p)
+            if (p < np) a[t] = cadd(a[t], cmul(c[r][t][p], xs[t][p]));
+          pwr[r][t] += a[t].x * a[t].x + a[t].y * a[t].y;
+        }
+        yl[(size_t)r * g.L + n] = cadd(a[0], a[1]);
+      }
+    }
+    __syncthreads();   // every read of the old tails and of the grids done
+    for (int i = tid; i < NTX * TL; i += T) {
+      const int t = i / TL, k = i - t * TL;
+      sm[TB0 + t * SFX_TL + k] = sm[t * N + ((S - TL + k - g.cp) & (N - 1))];
+    }
+    __syncthreads();   // the tails are in place before the next symbol zeroes the grids
+  }
+#pragma unroll
+  for (int r = 0; r < NRX; ++r)
+#pragma unroll
+    for (int t = 0; t < NTX; ++t) {
+      const R v = block_sum(pwr[r][t], red);
+      if (threadIdx.x == 0) lp.part[((size_t)b * NRX + r) * NTX + t] = v;   // one partial per link (nblk 1)
+      __syncthreads();
+    }
+}
+
+// transmit_mimo's RX power on the Philox path after k_ofdm_txch_sfbc: the
+// partials per OFDM symbol of sum_n |y0_r[n] + s_r z_r[n]|^2, y0_r the faded
+// signal and s_r z_r the RX's combined 100 dB link noise (rx_link_sigma, one
+// draw per sample on link (r, 0)'s stream, the values k_channel_tay adds and
+// in its order), for the (P / num_tx) / SNR rule (core/ofdm_core.py:524-534).
+// y is not written: the receiver (k_rx_fft_mimo<.., LN>) draws the same link
+// noise again and adds it before its own noise, so the faded signal crosses
+// HBM once and the link noise never does.  One block per (frame, OFDM symbol).
+template <class R, int J>
+__global__ __launch_bounds__(MWG) void k_link_noise_power(int L, int num_rx, int num_tx, int sym_len,
+                                                          const cx<R>* __restrict__ y, const R* __restrict__ link_sigma,
+                                                          const uint64_t* __restrict__ fid, uint64_t seed,
+                                                          R* __restrict__ pow_part, int nblk) {
+  using V = cx<R>;
+  __shared__ R red[MWG / 64];
+  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
+  const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
+  for (int r = 0; r < num_rx; ++r) {
+    const R sr = rx_link_sigma(link_sigma, ((size_t)b * num_rx + r) * num_tx, num_tx);
+    const V* yr = y + ((size_t)b * num_rx + r) * L;
+    R pw = (R)0;
+    for (int base = nbeg; base < nend; base += J * MWG) {
+      const SymSpan<J> sp(base, nbeg, nend, 0.f, false);
+      V v[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) v[j] = sp.ok[j] ? yr[sp.n[j]] : mkc((R)0, (R)0);
+      link_noise_span<R, J>(v, sp, sr, seed, fid[b], r * num_tx, (nbeg & 1) == 0);
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+        if (sp.ok[j]) pw += v[j].x * v[j].x + v[j].y * v[j].y;
+    }
+    const R t = block_sum(pw, red);
+    if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
+    __syncthreads();
+  }
+}
+
+template <class R>
+bool sfbc_txch_supported(const Grid& g, const MimoGrid& m, int n_paths, int max_delay) {
+  return m.mode == MIMO_SFBC && m.num_tx == 2 && (m.num_rx == 1 || m.num_rx == 2) && g.N == 2048 && m.n_cs == 1 &&
+         !m.exact_jakes && n_paths >= 1 && n_paths <= TXCH_MAXP && max_delay >= 0 && max_delay <= SFX_TL &&
+         max_delay <= g.cp && m.n_dsc <= 2 * 4 * (g.N >> 3) && (g.bps == 2 || g.bps == 4 || g.bps == 6);
+}
+
+template <class R>
+int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
+                          const uint32_t* enc, int enc_words, const int32_t* tx_map, const TxLinkPower<R>& lp,
+                          cx<R>* y, int B) {
+  if (!sfbc_txch_supported<R>(g, m, lp.n_paths, lp.max_delay) || !lp.part) return (int)hipErrorInvalidValue;
+  const size_t enc_shm = (size_t)enc_words * sizeof(uint32_t);
+  const int stage_enc = coded && enc_shm <= 32768;
+  const size_t shm = (2 * (size_t)g.N + 2 * SFX_TL) * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
+#define LTE_SFX(C_, B_, NR_)                                                                                          \
+  do {                                                                                                                \
+    auto k = k_ofdm_txch_sfbc<R, C_, B_, NR_>;                                                                        \
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                  \
+    hipLaunchKernelGGL(k, dim3(B), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words, tx_map, lp, y, B, stage_enc);     \
+  } while (0)
+#define LTE_SFX_NR(C_, B_) do { if (m.num_rx == 1) LTE_SFX(C_, B_, 1); else LTE_SFX(C_, B_, 2); } while (0)
+#define LTE_SFX_B(C_) \
+  do { if (g.bps == 2) LTE_SFX_NR(C_, 2); else if (g.bps == 4) LTE_SFX_NR(C_, 4); else LTE_SFX_NR(C_, 6); } while (0)
+  if (coded) LTE_SFX_B(1); else LTE_SFX_B(0);
+#undef LTE_SFX_B
+#undef LTE_SFX_NR
+#undef LTE_SFX
+  return (int)hipGetLastError();
+}
+
+template <class R>
+int launch_link_noise_power(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
+                            const cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part) {
+  const int sym_len = g.N + g.cp;
+  const int nch = mimo_channel_nblk(g.L, sym_len);
+  const int nl = B * m.num_rx * m.num_tx;   // one partial per link (k_ofdm_txch_sfbc)
+  hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, 1, g.L, link_sigma);
+  hipLaunchKernelGGL((k_link_noise_power<R, 3>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, sym_len,
+                     y, link_sigma, fid, seed, pow_part, nch);
+  return (int)hipGetLastError();
 }
 
 // One block per (frame, OFDM symbol): the symbol index -- hence every link
@@ -1172,12 +1365,6 @@ static bool channel_tay_econ(const MimoGrid& m, int sym_len, double fs) {
 
 int mimo_channel_nblk(int L, int sym_len) { return (L + sym_len - 1) / sym_len; }
 
-// power partials per (frame, RX) the channel pass writes: one per OFDM symbol
-template <class R>
-int mimo_channel_pblk(const Grid& g, const MimoGrid&) {
-  return mimo_channel_nblk(g.L, g.N + g.cp);
-}
-
 // k_channel_tay's launch: G receive antennas per group (a divisor of num_rx);
 // J (samples per thread per pass, 1..3) the one covering a symbol with the
 // fewest idle lanes (20 MHz: 3 -> 2304 lanes for 2192 samples)
@@ -1242,11 +1429,10 @@ template <class R>
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
                         const cx<R>* coef, const R* phases, const R* gains, double fs, const cx<R>* x, cx<R>* y,
                         int link_noise, const uint64_t* fid, uint64_t seed, const R* inj_lz, int64_t inj_lz_stride,
-                        R* link_part, R* link_sigma, R* pow_part, int nblk, int link_part_done, int max_delay) {
+                        R* link_part, R* link_sigma, R* pow_part, int nblk, int link_part_done) {
   const int sym_len = g.N + g.cp;
   if (m.num_rx > MC_MAXRX) return (int)hipErrorInvalidValue;
   const int nch = mimo_channel_nblk(g.L, sym_len);
-  (void)max_delay;
   if (nch > nblk) return (int)hipErrorInvalidValue;   // partial buffers are sized for nblk blocks
   const R* ph = m.exact_jakes ? phases : nullptr;
   if (m.exact_jakes && (!phases || !gains)) return (int)hipErrorInvalidValue;
@@ -1402,11 +1588,16 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
 // TX's pilot subset + linear interpolation with edge hold (:108-185 +
 // lte_receiver.py:98-133: np.linspace, k (delta / gap) + start) at the data
 // SCs -> H[b][rx][e][tx][n_dsc].
-template <class R, int NC = 0>
+// LN: y holds the RX's faded signal without transmit_mimo's 100 dB link
+// noise (k_ofdm_txch_sfbc); the combined link noise (rx_link_sigma of
+// link_sigma, stream of link (rx, 0)) is drawn here and added before the
+// receiver noise -- the values k_link_noise_power summed into the RX power.
+template <class R, int NC = 0, bool LN = false>
 __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
                                                      const R* __restrict__ npow, const uint64_t* __restrict__ fid,
                                                      uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride,
-                                                     cx<R>* __restrict__ Y, cx<R>* __restrict__ H) {
+                                                     cx<R>* __restrict__ Y, cx<R>* __restrict__ H,
+                                                     const R* __restrict__ link_sigma) {
   using V = cx<R>;
   V* sm = mimo_lds<V>();
   const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
@@ -1420,8 +1611,14 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
   if (active) {
     const R sigma = sqrt(npow[(size_t)b * m.num_rx + rx] * (R)0.5);
     const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-    load_symbol_noisy2<true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf,
-                             g.L, tid, T);
+    if constexpr (LN) {
+      const R sl = rx_link_sigma(link_sigma, ((size_t)b * m.num_rx + rx) * m.num_tx, m.num_tx);
+      load_symbol_noisy2<true, true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b],
+                                     rx, nullptr, g.L, tid, T, sl, RNG_STREAM_MIMO_LINK + (uint32_t)(rx * m.num_tx));
+    } else {
+      load_symbol_noisy2<true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf,
+                               g.L, tid, T);
+    }
   }
   __syncthreads();
   fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
@@ -1464,18 +1661,25 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
 
 template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
-                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H) {
+                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H,
+                       const R* link_sigma) {
   const int spw = MWG / (g.N >> 3);
+  if (link_sigma && inj_z) return (int)hipErrorInvalidValue;   // the link noise is drawn (Philox) only
   const int64_t total = (int64_t)B * m.num_rx * g.n_sym;
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(cx<R>);
-  if (g.N == 2048)   // 20 MHz: compile-time N (unrolled passes, twiddle recurrence)
+  if (g.N == 2048 && link_sigma)   // config 4 after k_ofdm_txch_sfbc (N = 2048 only)
+    hipLaunchKernelGGL((k_rx_fft_mimo<R, 2048, true>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed,
+                       inj_z, inj_stride, Y, H, link_sigma);
+  else if (link_sigma)
+    return (int)hipErrorInvalidValue;
+  else if (g.N == 2048)   // 20 MHz: compile-time N (unrolled passes, twiddle recurrence)
     hipLaunchKernelGGL((k_rx_fft_mimo<R, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
-                       inj_stride, Y, H);
+                       inj_stride, Y, H, nullptr);
   else
     hipLaunchKernelGGL((k_rx_fft_mimo<R>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
-                       inj_stride, Y, H);
+                       inj_stride, Y, H, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -1973,9 +2177,13 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
 
 // explicit instances: float (fast mode) and double (the reference's precision)
 #define LTE_MIMO_INST(R)                                                                                           \
+  template int launch_ofdm_txch_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,     \
+                                        const uint32_t*, int, const int32_t*, const TxLinkPower<R>&, cx<R>*, int); \
+  template int launch_link_noise_power<R>(hipStream_t, const Grid&, const MimoGrid&, int, const R*, R*,            \
+                                          const cx<R>*, const uint64_t*, uint64_t, R*);                            \
+  template bool sfbc_txch_supported<R>(const Grid&, const MimoGrid&, int, int);                                   \
   template int launch_ofdm_tx_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,       \
                                       const uint32_t*, int, const int32_t*, cx<R>*, int, const TxLinkPower<R>&);   \
-  template int mimo_channel_pblk<R>(const Grid&, const MimoGrid&);                                              \
   template int launch_ofdm_txch_flat<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,     \
                                         const uint32_t*, int, const int32_t*, const cx<R>*, cx<R>*, R*, int, int); \
   template int launch_fading_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const R*, double,   \
@@ -1983,13 +2191,13 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
                                      cx<R>*, R*);                                                                  \
   template int launch_channel_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const int32_t*,         \
                                       const cx<R>*, const R*, const R*, double, const cx<R>*, cx<R>*, int,         \
-                                      const uint64_t*, uint64_t, const R*, int64_t, R*, R*, R*, int, int, int);    \
+                                      const uint64_t*, uint64_t, const R*, int64_t, R*, R*, R*, int, int);    \
   template int launch_link_stats<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const int32_t*,           \
                                     const cx<R>*, const R*, const R*, double, const cx<R>*, const R*,              \
                                     const uint64_t*, uint64_t, const R*, int64_t, R*, int, R*);                    \
   template int launch_npow_mimo<R>(hipStream_t, int, int, const R*, int, int, const R*, double, R*);               \
   template int launch_rx_fft_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const R*,       \
-                                     const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*);                \
+                                     const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*, const R*);                \
   template int launch_det_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const cx<R>*,          \
                                   const cx<R>*, const R*, const uint32_t*, int, int, uint32_t*, R*, cx<R>*,        \
                                   uint8_t*, cx<R>*, R*);                                                           \

@@ -489,8 +489,8 @@ class OFDMSimulator:
                  itu_profile: str = 'Pedestrian_A', frequency_ghz: float = 2.0, velocity_kmh: float = 0.0,
                  *, precision: Optional[str] = None):
         """precision (not in the reference): arithmetic type of the GPU chains
-        (SISO, SIMO, SFBC, spatial multiplexing; beamforming is float32) and of
-        this simulator's channels, 'f64' (default; the reference's float64) or
+        (SISO, SIMO, SFBC, spatial multiplexing, beamforming) and of this
+        simulator's channels, 'f64' (default; the reference's float64) or
         'f32' (fast mode)."""
         if config is None:
             config = LTEConfig()

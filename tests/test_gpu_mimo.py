@@ -207,6 +207,7 @@ def test_link_power_in_tx_matches_separate_pass(C, prec, monkeypatch):
     plan = sim._sfbc_plan(0, 27760, 2, coded=True, max_frames=6)
     snrs = np.array([6.0, 12.0, 16.0, 18.0, 22.0, 30.0])
     outs = []
+    monkeypatch.setenv('LTE_SFBC_TXCH_FUSE', '0')   # the separate TX / channel kernels this test compares
     for fuse in ('1', '0'):
         monkeypatch.setenv('LTE_MIMO_LP_FUSE', fuse)
         outs.append(plan.run(snrs, seed=21, capture=('signal_rx',)))
@@ -214,6 +215,46 @@ def test_link_power_in_tx_matches_separate_pass(C, prec, monkeypatch):
     y0, y1 = a['signal_rx'].astype(np.complex128), b['signal_rx'].astype(np.complex128)
     assert np.linalg.norm(y0 - y1) / np.linalg.norm(y1) < (1e-15 if prec == 'f64' else 1e-6)
     assert np.array_equal(a['frame_errors'], b['frame_errors']) and np.array_equal(a['crc_ok'], b['crc_ok'])
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('coded,nrx', [(True, 2), (False, 2), (False, 1)])
+def test_sfbc_txch_fused_matches_separate_kernels(C, prec, coded, nrx, monkeypatch):
+    """Config 4's TX + static-tap Rayleigh links in one pass per frame
+    (k_ofdm_txch_sfbc + k_link_noise_add, default on the Philox path) against
+    the TX streams through HBM and the channel pass (LTE_SFBC_TXCH_FUSE=0):
+    received streams (signal_rx: the faded links, the combined 100 dB link
+    noise, the RX noise) equal to float64 rounding -- the link paths are summed
+    per link here and straight into the RX sum there, and the power sums in
+    another order move the 1e-5 link noise by ulps -- and identical per-frame
+    errors and CRC verdicts, over the delayed samples that cross every symbol
+    boundary (the kept tails), 1 and 2 RX, coded and uncoded (float32: the
+    north_star 1e-3 on the blocks past the cliff, identical CRC verdicts)."""
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
+    plan = (sim._sfbc_plan(0, 27760, nrx, coded=True, max_frames=6) if coded else
+            sim._sfbc_plan(14, 14 * 998 * 6, nrx, max_frames=6))
+    snrs = np.array([6.0, 12.0, 16.0, 18.0, 22.0, 30.0])
+    outs = []
+    for fuse in ('1', '0'):
+        monkeypatch.setenv('LTE_SFBC_TXCH_FUSE', fuse)
+        outs.append(plan.run(snrs, seed=27, frame_id0=1000, capture=('signal_rx',)))
+    a, b = outs
+    y0, y1 = a['signal_rx'].astype(np.complex128), b['signal_rx'].astype(np.complex128)
+    assert y0.shape == (6, nrx, plan.L)
+    assert np.linalg.norm(y0 - y1) / np.linalg.norm(y1) < (1e-14 if prec == 'f64' else 1e-6)
+    # the first samples of every symbol after the first (their taps reach into the previous symbol)
+    S = 2192
+    for l in range(1, 14):
+        seg0, seg1 = y0[..., l * S:l * S + 16], y1[..., l * S:l * S + 16]
+        assert np.max(np.abs(seg0 - seg1)) <= (1e-13 if prec == 'f64' else 1e-5) * np.max(np.abs(seg1))
+    if coded:
+        assert np.array_equal(a['crc_ok'], b['crc_ok'])
+    if prec == 'f64':
+        assert np.array_equal(a['frame_errors'], b['frame_errors'])
+    else:   # float32: rounding-level LLR changes move a few decisions of the blocks that fail anyway
+        nb = 27760 if coded else 14 * 998 * 6
+        assert np.max(np.abs(a['frame_errors'].astype(np.int64) - b['frame_errors'])) / nb < 1e-3
+        assert np.array_equal(a['frame_errors'] == 0, b['frame_errors'] == 0)
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])

@@ -296,7 +296,13 @@ def turbo_roofline(prec, tim, F, iters=8):
     busy = (sq['valu_wave_instr_per_frame'] * Fp * sq['issue_cycles_per_instr'] / (avg_s * 2.4e9 * 1024)
             if sq and t_n else None)
     ceil = shape.get(f'ceiling_GBs_{prec}') if shape else None
+    limiter = 'hbm' if busy is None or (tr_gbs or gbs) / HBM_PEAK_GBS >= busy else 'valu'
     return {'bound': 'valu', 'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo',
+            'bound_basis': 'SURVEY §8(d) names VALU as K7\'s roofline (the round-3 review asked for this `frac`); the '
+                           'reference recursion has 103 add/max per trellis step and pass (gamma 6, alpha 24, beta '
+                           '24, a-posteriori 47, extrinsic 2), which §8(d) rounds to 100.  What limits the kernel as '
+                           'measured is `measured_limiter` (' + limiter + '): see hbm_row_stream, traffic and '
+                           'issued_valu_busy_frac',
             'achieved': round(achieved_T, 3), 'peak': round(peak / 1e12, 2), 'unit': 'Top/s',
             'frac': round(achieved_T * 1e12 / peak, 4) if t_n else 0.0,
             'traffic': round(tr) if tr else None,
@@ -307,7 +313,7 @@ def turbo_roofline(prec, tim, F, iters=8):
             'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': t_n, 'frames_per_launch': F,
             'issued_valu_busy_frac': round(busy, 4) if busy is not None else None,
             'valu_wave_instr_per_frame': sq['valu_wave_instr_per_frame'] if sq else None,
-            'measured_limiter': 'hbm' if busy is None or (tr_gbs or gbs) / HBM_PEAK_GBS >= busy else 'valu',
+            'measured_limiter': limiter,
             'hbm_row_stream': {
                 'achieved_GBs': round(gbs, 1), 'peak_GBs': HBM_PEAK_GBS,
                 'frac_row_stream': round(gbs / HBM_PEAK_GBS, 4),

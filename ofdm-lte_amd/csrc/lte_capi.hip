@@ -14,7 +14,6 @@
 
 #include "lte_common.h"
 #include "lte_internal.h"
-#include "lte_dev.h"
 
 using namespace lte;
 
@@ -390,8 +389,7 @@ namespace lte {
 template <class R>
 __global__ void k_cap_rx(int L, int num_rx, int B, const cx<R>* __restrict__ y, int64_t y_rx_stride,
                          int64_t y_frame_stride, const R* __restrict__ npow, const uint64_t* __restrict__ fid,
-                         uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride, cx<R>* __restrict__ out,
-                         const R* __restrict__ link_sigma, int num_tx) {
+                         uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride, cx<R>* __restrict__ out) {
   const int nb = (L + 255) / 256;
   const int n = (blockIdx.x % nb) * blockDim.x + threadIdx.x;
   const int rx = blockIdx.y, b = blockIdx.x / nb;
@@ -405,10 +403,7 @@ __global__ void k_cap_rx(int L, int num_rx, int B, const cx<R>* __restrict__ y, 
     const u32x4 r = rng4(seed, fid[b], RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)(n >> 1));
     z = (n & 1) ? gauss2<R>(r.z, r.w) : gauss2<R>(r.x, r.y);
   }
-  cx<R> v = y[b * y_frame_stride + rx * y_rx_stride + n];
-  if (link_sigma)   // config 4's fused path: y holds the faded signal; its link noise first (k_rx_fft_mimo LN)
-    v = link_noise_at<R>(n, rx_link_sigma(link_sigma, ((size_t)b * num_rx + rx) * num_tx, num_tx), nullptr, 0, seed,
-                         fid[b], rx * num_tx, v);
+  const cx<R> v = y[b * y_frame_stride + rx * y_rx_stride + n];
   out[((size_t)b * num_rx + rx) * L + n] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
 }
 }  // namespace lte
@@ -652,7 +647,7 @@ static int channel_host(int64_t L, int num_rx, int channel, int n_paths, const i
     const V* ys = ray ? dy.p : dx.p;
     hipLaunchKernelGGL(k_cap_rx<R>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx,
                        1, ys, ray ? L : 0, ray ? (int64_t)num_rx * L : L, dnp.p, dfid.p, seed,
-                       noise ? dz.p : nullptr, 0, dout.p, nullptr, 0);
+                       noise ? dz.p : nullptr, 0, dout.p);
     ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
          hipMemcpy(y, dout.p, (size_t)num_rx * L * sizeof(V), hipMemcpyDeviceToHost) == hipSuccess &&
          (!noise_power || hipMemcpy(noise_power, dnp.p, num_rx * sizeof(R), hipMemcpyDeviceToHost) == hipSuccess);
@@ -757,7 +752,7 @@ static int channel_mimo_host(int64_t L, int num_tx, int num_rx, int mode, int ch
   if (ok) {
     hipLaunchKernelGGL(k_cap_rx<R>, dim3((unsigned)((L + 255) / 256), num_rx), dim3(256), 0, nullptr, (int)L, num_rx, 1,
                        dy.p, (int64_t)L, (int64_t)num_rx * L, dnp.p, dfid.p, seed, noise ? dz.p : nullptr, 0,
-                       dout.p, nullptr, 0);
+                       dout.p);
     ok = hipGetLastError() == hipSuccess;
   }
   if (ok && link_stats) {
@@ -991,19 +986,35 @@ void lte::plan_txf_lane_order(const std::vector<int32_t>& tx_map, const std::vec
     const int32_t v = tx_map[((size_t)l * Nd + j) * bps + m];
     return v >= 0 ? (int)(v >> 5) : -1;
   };
+  // Per (gather m, bank), the distinct words a lane group touches: fixed-size
+  // sets (a group has at most GL lanes, so at most GL words per bank) -- no heap
+  // allocation inside the search (the round-4 version built 32 std::vectors per
+  // gather of every group).
+  struct BankSets {
+    int n[8][GL];
+    int w[8][GL][GL];
+    void clear(int bps_) { for (int m = 0; m < bps_; ++m) for (int b = 0; b < GL; ++b) n[m][b] = 0; }
+    bool has(int m, int x) const {
+      const int b = x % GL;
+      for (int i = 0; i < n[m][b]; ++i) if (w[m][b][i] == x) return true;
+      return false;
+    }
+    void add(int m, int x) { if (!has(m, x)) { const int b = x % GL; w[m][b][n[m][b]++] = x; } }
+    int size(int m, int x) const { return n[m][x % GL]; }
+  };
+  BankSets bs;
   // extra cycles of the bps gathers of one lane group: per gather, the most
   // distinct words on one bank, minus one
   auto group_extra = [&](int l, const int* re, int n) {
+    bs.clear(bps);
     int ex = 0;
     for (int m = 0; m < bps; ++m) {
-      std::vector<int> w[GL];
       int mx = 1;
       for (int k = 0; k < n; ++k) {
         const int x = word(l, re[k], m);
         if (x < 0) continue;
-        std::vector<int>& v = w[x % GL];
-        if (std::find(v.begin(), v.end(), x) == v.end()) v.push_back(x);
-        mx = std::max(mx, (int)v.size());
+        bs.add(m, x);
+        mx = std::max(mx, bs.size(m, x));
       }
       ex += mx - 1;
     }
@@ -1012,13 +1023,14 @@ void lte::plan_txf_lane_order(const std::vector<int32_t>& tx_map, const std::vec
   double ex0 = 0, ex1 = 0, ng = 0;
   std::vector<char> used(Nd);
   std::vector<int> grp(GL), ident(GL);
+  BankSets wb;
   for (int l = 0; l < n_sym; ++l) {
     std::fill(used.begin(), used.end(), 0);
     for (int g = 0; g * GL < Nd; ++g) {
       const int n = std::min(GL, Nd - g * GL);
       for (int k = 0; k < n; ++k) ident[k] = g * GL + k;
       ex0 += group_extra(l, ident.data(), n);
-      std::vector<int> wb[8][GL];   // bps <= 8: per gather and bank, the group's words
+      wb.clear(bps);   // bps <= 8: per gather and bank, the group's words
       int cnt8[GL / 8][8] = {};
       for (int k = 0; k < n; ++k) {
         int best = -1, bc = 1 << 30;
@@ -1028,8 +1040,8 @@ void lte::plan_txf_lane_order(const std::vector<int32_t>& tx_map, const std::vec
           for (int m = 0; m < bps && c < bc; ++m) {
             const int x = word(l, j, m);
             if (x < 0) continue;
-            const std::vector<int>& v = wb[m][x % GL];
-            if (!v.empty() && std::find(v.begin(), v.end(), x) == v.end()) c += (int)v.size();
+            const int sz = wb.size(m, x);
+            if (sz && !wb.has(m, x)) c += sz;
           }
           if (c < bc) { bc = c; best = j; if (c == 0) break; }
         }
@@ -1038,9 +1050,7 @@ void lte::plan_txf_lane_order(const std::vector<int32_t>& tx_map, const std::vec
         ++cnt8[k / 8][data_idx[best] & 7];
         for (int m = 0; m < bps; ++m) {
           const int x = word(l, best, m);
-          if (x < 0) continue;
-          std::vector<int>& v = wb[m][x % GL];
-          if (std::find(v.begin(), v.end(), x) == v.end()) v.push_back(x);
+          if (x >= 0) wb.add(m, x);
         }
         const size_t sl = (size_t)l * slots + g * GL + k;
         txf_re[sl] = best;
@@ -1142,9 +1152,13 @@ static int plan_coded_maps(lte_plan* p) {
   encode_qmask(p->cbs.data(), p->C, p->qstride, qm.data());
   if (upload(p->tx_map, txm) || upload(p->rx_map, rxm) || upload(p->cbi, p->cbs) || upload(p->enc_qmask, qm))
     return fail(LTE_ENOMEM, "map upload failed");
-  // k_ofdm_txf's lane order (SISO grids with whole 32-lane groups per transform;
-  // LTE_TXF_LANE_ORDER=0: RE order, for A/B)
-  if (p->res == p->Nd && d.N >= 512 && p->Nd <= d.N / 2 && env_on("LTE_TXF_LANE_ORDER", true)) {
+  // k_ofdm_txf's bank-aware lane order (SISO grids with whole 32-lane groups per
+  // transform): off by default since round 5 -- it cut the modelled gather
+  // conflicts 2.07 -> 0.19 cycles and the measured ones 0.91 -> 0.18 per LDS
+  // instruction but not the kernel time (15.34 ms with it, 15.17 without,
+  // DESIGN.md §5 round 4), and its greedy search costs plan-create time on every
+  // plan-cache miss.  LTE_TXF_LANE_ORDER=1 turns it on.
+  if (p->res == p->Nd && d.N >= 512 && p->Nd <= d.N / 2 && env_on("LTE_TXF_LANE_ORDER", false)) {
     std::vector<int32_t> tfm, tfr;
     plan_txf_lane_order(txm, p->gh.data, p->n_sym, Nd, bps, d.N / 2, tfm, tfr, p->txf_model);
     if (env_on("LTE_TXF_LANE_ORDER_REPORT", false))
@@ -1675,9 +1689,8 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                          env_on("LTE_MIMO_FLAT_FUSE", true);
   // config 4 (SFBC, static-tap Rayleigh links with the 100 dB link noise, Philox
   // draws): TX and the links' fading in one pass per frame writing the faded RX
-  // signals (k_ofdm_txch_sfbc), then the RX power with the link noise
-  // (k_link_noise_power), which the receiver draws again and adds (k_rx_fft_mimo
-  // LN) -- x never goes through HBM, the link noise never does.  Captures of x / the link statistics and the
+  // signals (k_ofdm_txch_sfbc), then the link noise + RX power (k_link_noise_add)
+  // -- x never goes through HBM.  Captures of x / the link statistics and the
   // reference's own (injected) link noise keep the separate kernels.
   const bool sfbc_fuse = link_noise && !inj_lz && !inj_z && !a->cap_signal_tx && !a->cap_link_stats &&
                          sfbc_txch_supported<R>(g, m, d.n_paths, maxd) && env_on("LTE_SFBC_TXCH_FUSE", true);
@@ -1689,8 +1702,8 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                                     c.y.p, B));
     }
     Timer t(p, KN_CHANNEL);
-    LCHK(launch_link_noise_power<R>(s, g, m, B, c.link_part.p, c.link_sigma.p, c.y.p, p->fid.p, a->seed,
-                                    c.pow_part.p));
+    LCHK(launch_link_noise_add<R>(s, g, m, B, c.link_part.p, c.link_sigma.p, c.y.p, p->fid.p, a->seed,
+                                  c.pow_part.p));
   } else if (flat_fuse) {
     Timer t(p, KN_OFDM_TX);
     LCHK(launch_ofdm_txch_flat<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p,
@@ -1715,8 +1728,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   {
     Timer t(p, KN_RX_CHEST);
-    LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p,
-                               sfbc_fuse ? c.link_sigma.p : nullptr));
+    LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p));
   }
   V* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
@@ -1792,7 +1804,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
       Timer t(p, KN_CAP);
       hipLaunchKernelGGL(k_cap_rx<R>, dim3(((p->L + 255) / 256) * B, m.num_rx), dim3(256), 0, s, p->L, m.num_rx, B,
                          c.y.p, (int64_t)p->L, (int64_t)m.num_rx * p->L, c.npow.p, p->fid.p, a->seed, inj_z,
-                         inj_z_stride, tmp.p, sfbc_fuse ? c.link_sigma.p : nullptr, m.num_tx);
+                         inj_z_stride, tmp.p);
       LCHK((int)hipGetLastError());
     }
     HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * m.num_rx * p->L * sizeof(V), hipMemcpyDeviceToHost, s));
@@ -2195,7 +2207,7 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     {
       Timer t(p, KN_CAP);
       hipLaunchKernelGGL(k_cap_rx<R>, dim3(((p->L + 255) / 256) * B, rx), dim3(256), 0, s, p->L, rx, B, ysrc, yrs, yfs,
-                         c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p, nullptr, 0);
+                         c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, tmp.p);
       LCHK((int)hipGetLastError());
     }
     HIPCHK(hipMemcpyAsync(a->cap_signal_rx, tmp.p, (size_t)B * rx * p->L * sizeof(V), hipMemcpyDeviceToHost, s));

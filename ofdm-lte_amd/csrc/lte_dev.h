@@ -205,19 +205,13 @@ __device__ __forceinline__ R rx_link_sigma(const R* __restrict__ link_sigma, siz
 // load_symbol_noisy, at half the generator cost).  Lane t stores samples 2t
 // and 2t + 1 (a stride-2 ds_write pattern, 2-way on 16-B and 8-B elements);
 // SW = true stores them swizzled (conflict-free) for fft_lds<.., ISW = true>.
-// LN: a second Gaussian per sample added first, v = (y + sig_l z_l) + sigma z --
-// transmit_mimo's 100 dB link noise of the RX (the combined draw of
-// rx_link_sigma, Philox stream lstream with the same pair mapping, counter n >> 1,
-// half n & 1) before its receiver noise, as the reference sums them (the
-// multi-antenna receiver of config 4; Philox draws only, zf must be null).
-template <bool SW = false, bool LN = false, class V>
+template <bool SW = false, class V>
 __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__ yf, int N, int cp, int l,
                                                    re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
-                                                   const re_t<V>* __restrict__ zf, int L, int tid, int T,
-                                                   re_t<V> sig_l = 0, uint32_t lstream = 0) {
+                                                   const re_t<V>* __restrict__ zf, int L, int tid, int T) {
   using R = re_t<V>;
   const int off = l * (N + cp) + cp;
-  if (!LN && zf) {
+  if (zf) {
     load_symbol_noisy<SW>(buf, yf, N, cp, l, sigma, seed, frame, rx, zf, L, tid, T);
     return;
   }
@@ -238,12 +232,6 @@ __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__
     const int p = p0 + tid + i * T, n0 = 2 * p;
     if (p > p1) break;
     const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
-    if constexpr (LN) {
-      const u32x4 q = rng4(seed, frame, lstream, (uint32_t)p);
-      const V za = gauss2<R>(q.x, q.y), zb = gauss2<R>(q.z, q.w);
-      va[i] = mkc(va[i].x + sig_l * za.x, va[i].y + sig_l * za.y);
-      vb[i] = mkc(vb[i].x + sig_l * zb.x, vb[i].y + sig_l * zb.y);
-    }
     if (n0 >= off) {
       const V z = gauss2<R>(r.x, r.y);
       buf[SW ? fft_sw<V>(n0 - off) : n0 - off] = mkc(va[i].x + sigma * z.x, va[i].y + sigma * z.y);

@@ -303,9 +303,9 @@ int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int c
                           const uint32_t* enc, int enc_words, const int32_t* tx_map, const cx<R>* coef, cx<R>* y,
                           R* pow_part, int nblk, int B);
 // config 4: SFBC TX + static-tap Rayleigh links in one pass per frame (y gets
-// the faded RX signals without link noise, lp.part one power per link); then
-// the link sigmas and the RX power partials pow_part [B][num_rx][n_sym] of y +
-// the combined link noise, which launch_rx_fft_mimo(.., link_sigma) adds
+// the faded RX signals, lp.part one power per link); then the link sigmas, the
+// combined link noise added to y and the RX power partials pow_part
+// [B][num_rx][n_sym]
 template <class R>
 bool sfbc_txch_supported(const Grid& g, const MimoGrid& m, int n_paths, int max_delay);
 template <class R>
@@ -313,8 +313,8 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
                           const uint32_t* enc, int enc_words, const int32_t* tx_map, const TxLinkPower<R>& lp,
                           cx<R>* y, int B);
 template <class R>
-int launch_link_noise_power(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
-                            const cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part);
+int launch_link_noise_add(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
+                          cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part);
 // phases / gains: exact-Jakes mode (m.exact_jakes) only
 template <class R>
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,
@@ -337,8 +337,7 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
                      double div, R* npow);
 template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
-                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H,
-                       const R* link_sigma = nullptr);   // config 4 fused path: the link noise drawn here
+                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H);
 template <class R>
 // coded: LLRs to llr, or (zo != null) the combined symbols to zo [B][n_sym][res]
 // and sigma^2_eff per RE pair to nvo [B][n_sym][res / 2] for launch_dematch_zn

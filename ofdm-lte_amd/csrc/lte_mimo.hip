@@ -880,9 +880,8 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
 // kept in LDS -- the frame walks its symbols in order, so no fix-up pass is
 // needed.  Each link's power sum_n |y0_rt|^2 accumulates over the frame (the
 // link noise's standard deviation, k_link_sigma).  y0 goes to HBM once; the
-// TX streams x never do.  k_link_noise_power then forms the RX power with the
-// link noise, which the receiver (k_rx_fft_mimo<.., LN>) draws again and adds
-// before its own noise.  Static taps only (n_cs = 1), N = 2048 (two 32 KB
+// TX streams x never do.  k_link_noise_add then adds the link noise and forms
+// the RX power partials.  Static taps only (n_cs = 1), N = 2048 (two 32 KB
 // grids: two slots per CU).
 constexpr int SFX_TL = 32;   // largest max_delay (samples) the kept tails cover
 template <class R, int CODED, int BPS, int NRX, int NC = 2048>
@@ -1008,40 +1007,61 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
     }
 }
 
-// transmit_mimo's RX power on the Philox path after k_ofdm_txch_sfbc: the
-// partials per OFDM symbol of sum_n |y0_r[n] + s_r z_r[n]|^2, y0_r the faded
-// signal and s_r z_r the RX's combined 100 dB link noise (rx_link_sigma, one
-// draw per sample on link (r, 0)'s stream, the values k_channel_tay adds and
-// in its order), for the (P / num_tx) / SNR rule (core/ofdm_core.py:524-534).
-// y is not written: the receiver (k_rx_fft_mimo<.., LN>) draws the same link
-// noise again and adds it before its own noise, so the faded signal crosses
-// HBM once and the link noise never does.  One block per (frame, OFDM symbol).
-template <class R, int J>
-__global__ __launch_bounds__(MWG) void k_link_noise_power(int L, int num_rx, int num_tx, int sym_len,
-                                                          const cx<R>* __restrict__ y, const R* __restrict__ link_sigma,
-                                                          const uint64_t* __restrict__ fid, uint64_t seed,
-                                                          R* __restrict__ pow_part, int nblk) {
+// transmit_mimo's link noise on the Philox path after k_ofdm_txch_sfbc: y0_r +
+// the RX's combined 100 dB link noise (rx_link_sigma, one draw per sample on
+// link (r, 0)'s stream, the values and the order k_channel_tay adds them in),
+// written back, and the RX power partials per OFDM symbol of the result for
+// the (P / num_tx) / SNR rule (core/ofdm_core.py:524-534).  One block per
+// (frame, OFDM symbol); every receive antenna's J samples of a pass are loaded
+// before their noise is drawn (NRX x J loads in flight), one reduction for all
+// antennas at the end.  (Measured against drawing the link noise a second time
+// in the receiver instead of writing it here: the receiver is VALU-bound and
+// lost more, 12.5 ms, than the write saved, 9.3 ms per 65 536 frames.)
+template <class R, int J, int NRX>
+__global__ __launch_bounds__(MWG) void k_link_noise_add(int L, int num_tx, int sym_len, cx<R>* __restrict__ y,
+                                                        const R* __restrict__ link_sigma,
+                                                        const uint64_t* __restrict__ fid, uint64_t seed,
+                                                        R* __restrict__ pow_part, int nblk) {
   using V = cx<R>;
-  __shared__ R red[MWG / 64];
+  __shared__ R red[NRX][MWG / 64];
   const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
   const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
-  for (int r = 0; r < num_rx; ++r) {
-    const R sr = rx_link_sigma(link_sigma, ((size_t)b * num_rx + r) * num_tx, num_tx);
-    const V* yr = y + ((size_t)b * num_rx + r) * L;
-    R pw = (R)0;
-    for (int base = nbeg; base < nend; base += J * MWG) {
-      const SymSpan<J> sp(base, nbeg, nend, 0.f, false);
-      V v[J];
+  R sr[NRX], pw[NRX];
 #pragma unroll
-      for (int j = 0; j < J; ++j) v[j] = sp.ok[j] ? yr[sp.n[j]] : mkc((R)0, (R)0);
-      link_noise_span<R, J>(v, sp, sr, seed, fid[b], r * num_tx, (nbeg & 1) == 0);
+  for (int r = 0; r < NRX; ++r) {
+    sr[r] = rx_link_sigma(link_sigma, ((size_t)b * NRX + r) * num_tx, num_tx);
+    pw[r] = (R)0;
+  }
+  V* yb = y + (size_t)b * NRX * L;
+  for (int base = nbeg; base < nend; base += J * MWG) {
+    const SymSpan<J> sp(base, nbeg, nend, 0.f, false);
+    V v[NRX][J];
+#pragma unroll
+    for (int r = 0; r < NRX; ++r)
+#pragma unroll
+      for (int j = 0; j < J; ++j) v[r][j] = sp.ok[j] ? yb[(size_t)r * L + sp.n[j]] : mkc((R)0, (R)0);
+#pragma unroll
+    for (int r = 0; r < NRX; ++r) {
+      link_noise_span<R, J>(v[r], sp, sr[r], seed, fid[b], r * num_tx, (nbeg & 1) == 0);
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        if (sp.ok[j]) pw += v[j].x * v[j].x + v[j].y * v[j].y;
+        if (sp.ok[j]) {
+          yb[(size_t)r * L + sp.n[j]] = v[r][j];
+          pw[r] += v[r][j].x * v[r][j].x + v[r][j].y * v[r][j].y;
+        }
     }
-    const R t = block_sum(pw, red);
-    if (threadIdx.x == 0) pow_part[((size_t)b * num_rx + r) * nblk + blk] = t;
-    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < NRX; ++r) {
+    R t = pw[r];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if ((threadIdx.x & 63) == 0) red[r][threadIdx.x >> 6] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < NRX) {
+    R t = (R)0;
+    for (int i = 0; i < MWG / 64; ++i) t += red[threadIdx.x][i];
+    pow_part[((size_t)b * NRX + threadIdx.x) * nblk + blk] = t;
   }
 }
 
@@ -1077,14 +1097,19 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
 }
 
 template <class R>
-int launch_link_noise_power(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
-                            const cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part) {
+int launch_link_noise_add(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
+                          cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part) {
+  if (m.num_rx < 1 || m.num_rx > 2) return (int)hipErrorInvalidValue;
   const int sym_len = g.N + g.cp;
   const int nch = mimo_channel_nblk(g.L, sym_len);
   const int nl = B * m.num_rx * m.num_tx;   // one partial per link (k_ofdm_txch_sfbc)
   hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, 1, g.L, link_sigma);
-  hipLaunchKernelGGL((k_link_noise_power<R, 3>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_rx, m.num_tx, sym_len,
-                     y, link_sigma, fid, seed, pow_part, nch);
+  if (m.num_rx == 1)
+    hipLaunchKernelGGL((k_link_noise_add<R, 3, 1>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_tx, sym_len, y,
+                       link_sigma, fid, seed, pow_part, nch);
+  else
+    hipLaunchKernelGGL((k_link_noise_add<R, 3, 2>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_tx, sym_len, y,
+                       link_sigma, fid, seed, pow_part, nch);
   return (int)hipGetLastError();
 }
 
@@ -1588,16 +1613,11 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
 // TX's pilot subset + linear interpolation with edge hold (:108-185 +
 // lte_receiver.py:98-133: np.linspace, k (delta / gap) + start) at the data
 // SCs -> H[b][rx][e][tx][n_dsc].
-// LN: y holds the RX's faded signal without transmit_mimo's 100 dB link
-// noise (k_ofdm_txch_sfbc); the combined link noise (rx_link_sigma of
-// link_sigma, stream of link (rx, 0)) is drawn here and added before the
-// receiver noise -- the values k_link_noise_power summed into the RX power.
-template <class R, int NC = 0, bool LN = false>
+template <class R, int NC = 0>
 __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
                                                      const R* __restrict__ npow, const uint64_t* __restrict__ fid,
                                                      uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride,
-                                                     cx<R>* __restrict__ Y, cx<R>* __restrict__ H,
-                                                     const R* __restrict__ link_sigma) {
+                                                     cx<R>* __restrict__ Y, cx<R>* __restrict__ H) {
   using V = cx<R>;
   V* sm = mimo_lds<V>();
   const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
@@ -1611,14 +1631,8 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
   if (active) {
     const R sigma = sqrt(npow[(size_t)b * m.num_rx + rx] * (R)0.5);
     const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-    if constexpr (LN) {
-      const R sl = rx_link_sigma(link_sigma, ((size_t)b * m.num_rx + rx) * m.num_tx, m.num_tx);
-      load_symbol_noisy2<true, true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b],
-                                     rx, nullptr, g.L, tid, T, sl, RNG_STREAM_MIMO_LINK + (uint32_t)(rx * m.num_tx));
-    } else {
-      load_symbol_noisy2<true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf,
-                               g.L, tid, T);
-    }
+    load_symbol_noisy2<true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf,
+                             g.L, tid, T);
   }
   __syncthreads();
   fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
@@ -1661,25 +1675,18 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
 
 template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
-                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H,
-                       const R* link_sigma) {
+                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H) {
   const int spw = MWG / (g.N >> 3);
-  if (link_sigma && inj_z) return (int)hipErrorInvalidValue;   // the link noise is drawn (Philox) only
   const int64_t total = (int64_t)B * m.num_rx * g.n_sym;
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(cx<R>);
-  if (g.N == 2048 && link_sigma)   // config 4 after k_ofdm_txch_sfbc (N = 2048 only)
-    hipLaunchKernelGGL((k_rx_fft_mimo<R, 2048, true>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed,
-                       inj_z, inj_stride, Y, H, link_sigma);
-  else if (link_sigma)
-    return (int)hipErrorInvalidValue;
-  else if (g.N == 2048)   // 20 MHz: compile-time N (unrolled passes, twiddle recurrence)
+  if (g.N == 2048)   // 20 MHz: compile-time N (unrolled passes, twiddle recurrence)
     hipLaunchKernelGGL((k_rx_fft_mimo<R, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
-                       inj_stride, Y, H, nullptr);
+                       inj_stride, Y, H);
   else
     hipLaunchKernelGGL((k_rx_fft_mimo<R>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
-                       inj_stride, Y, H, nullptr);
+                       inj_stride, Y, H);
   return (int)hipGetLastError();
 }
 
@@ -2179,8 +2186,8 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
 #define LTE_MIMO_INST(R)                                                                                           \
   template int launch_ofdm_txch_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,     \
                                         const uint32_t*, int, const int32_t*, const TxLinkPower<R>&, cx<R>*, int); \
-  template int launch_link_noise_power<R>(hipStream_t, const Grid&, const MimoGrid&, int, const R*, R*,            \
-                                          const cx<R>*, const uint64_t*, uint64_t, R*);                            \
+  template int launch_link_noise_add<R>(hipStream_t, const Grid&, const MimoGrid&, int, const R*, R*, cx<R>*,      \
+                                        const uint64_t*, uint64_t, R*);                                            \
   template bool sfbc_txch_supported<R>(const Grid&, const MimoGrid&, int, int);                                   \
   template int launch_ofdm_tx_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,       \
                                       const uint32_t*, int, const int32_t*, cx<R>*, int, const TxLinkPower<R>&);   \
@@ -2197,7 +2204,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
                                     const uint64_t*, uint64_t, const R*, int64_t, R*, int, R*);                    \
   template int launch_npow_mimo<R>(hipStream_t, int, int, const R*, int, int, const R*, double, R*);               \
   template int launch_rx_fft_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const R*,       \
-                                     const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*, const R*);                \
+                                     const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*);                \
   template int launch_det_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const cx<R>*,          \
                                   const cx<R>*, const R*, const uint32_t*, int, int, uint32_t*, R*, cx<R>*,        \
                                   uint8_t*, cx<R>*, R*);                                                           \

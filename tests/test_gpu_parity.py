@@ -520,6 +520,35 @@ def test_frame_tx_matches_symbol_tx(C, monkeypatch, bw, mod, prec):
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+def test_txf_lane_order_matches_re_order(C, monkeypatch, prec):
+    """k_ofdm_txf with the plan-time bank-aware lane order (LTE_TXF_LANE_ORDER=1,
+    off by default since round 5) and in RE order: the lane order only changes
+    which lane forms which RE, so the transmitted symbols, noise powers, LLRs
+    and counts are identical; plan creation with the order times its greedy
+    search (printed for the record)."""
+    import time
+    from lte_phy import engine
+    sim = _sim(20.0, '64-QAM', 'rayleigh_mp', prec)
+    B = 64 + 5
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('noise_power', 'tx_syms', 'llr')
+    outs, secs = [], []
+    for lo in ('1', '0'):
+        monkeypatch.setenv('LTE_TXF_LANE_ORDER', lo)
+        engine.clear_cache()
+        t = time.perf_counter()
+        plan = sim._plan(C.CHAIN_CODED, 0, 27760, max_frames=B)
+        secs.append(time.perf_counter() - t)
+        outs.append(plan.run(snr, seed=0x5EED, frame_id0=77, capture=cap))
+    engine.clear_cache()
+    a, b = outs
+    for k in cap:
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a['crc_ok'], b['crc_ok']) and np.array_equal(a['counts'], b['counts'])
+    print(f'plan create: lane order {secs[0] * 1e3:.1f} ms, RE order {secs[1] * 1e3:.1f} ms')
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mod', ['16-QAM', '64-QAM'])
 def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
     """k_rx_data handing (z, sigma^2_eff) per RE to k_dematch_zn, which runs the

@@ -1692,6 +1692,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   // signals (k_ofdm_txch_sfbc), then the link noise + RX power (k_link_noise_add)
   // -- x never goes through HBM.  Captures of x / the link statistics and the
   // reference's own (injected) link noise keep the separate kernels.
+  int npow_nblk = nch;   // RX power partials per (frame, RX) that k_npow_mimo sums
   const bool sfbc_fuse = link_noise && !inj_lz && !inj_z && !a->cap_signal_tx && !a->cap_link_stats &&
                          sfbc_txch_supported<R>(g, m, d.n_paths, maxd) && env_on("LTE_SFBC_TXCH_FUSE", true);
   if (sfbc_fuse) {
@@ -1701,9 +1702,12 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
       LCHK(launch_ofdm_txch_sfbc<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, lf,
                                     c.y.p, B));
     }
+    // (chunks of frames with each chunk's noise pass on a second stream beside
+    // the next chunk's TX measured no overlap: TX + noise 67.3-68.0 ms per
+    // 65 536 frames with 1, 2, 4 or 8 chunks)
     Timer t(p, KN_CHANNEL);
     LCHK(launch_link_noise_add<R>(s, g, m, B, c.link_part.p, c.link_sigma.p, c.y.p, p->fid.p, a->seed,
-                                  c.pow_part.p));
+                                  c.pow_part.p, &npow_nblk));
   } else if (flat_fuse) {
     Timer t(p, KN_OFDM_TX);
     LCHK(launch_ofdm_txch_flat<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p,
@@ -1723,7 +1727,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   {
     Timer t(p, KN_CHANNEL);
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
-    LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, nch, p->L, c.snr_lin.p, sfbc ? (double)m.num_tx : 1.0,
+    LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, npow_nblk, p->L, c.snr_lin.p, sfbc ? (double)m.num_tx : 1.0,
                              c.npow.p));
   }
   {

@@ -97,14 +97,44 @@ __device__ __forceinline__ double log1p_small(double r) {   // |r| <= 2^-8, erro
 #ifndef LTE_BM_SELECT   // 0: the three ln u cases as branches (A/B)
 #define LTE_BM_SELECT 1
 #endif
-__device__ __forceinline__ double ln_u32(uint32_t a) {
+// Where box_muller64t reads its tables: BmTabC the __constant__ arrays (vector
+// gathers through the L1 / L2), BmTabL copies of them in LDS (bm_tables_lds).
+struct BmTabC {
+  __device__ __forceinline__ double2 sc(int i) const { return BM_SC[i]; }
+  __device__ __forceinline__ double2 lg(int i) const { return BM_LG[i]; }
+  __device__ __forceinline__ double lh(int i) const { return BM_LH[i]; }
+};
+struct BmTabL {
+  const double2* s;
+  const double2* g;
+  const double* h;
+  __device__ __forceinline__ double2 sc(int i) const { return s[i]; }
+  __device__ __forceinline__ double2 lg(int i) const { return g[i]; }
+  __device__ __forceinline__ double lh(int i) const { return h[i]; }
+};
+constexpr int BM_LDS_BYTES = 256 * 16 + 128 * 16 + 128 * 8;   // 7 KB
+// copy the tables into lds (BM_LDS_BYTES, 16-B aligned) by nt threads; the
+// caller's barrier must follow before the first draw
+__device__ __forceinline__ BmTabL bm_tables_lds(void* lds, int tid, int nt) {
+  double2* s = reinterpret_cast<double2*>(lds);
+  double2* g = s + 256;
+  double* h = reinterpret_cast<double*>(g + 128);
+  for (int i = tid; i < 256; i += nt) s[i] = BM_SC[i];
+  for (int i = tid; i < 128; i += nt) {
+    g[i] = BM_LG[i];
+    h[i] = BM_LH[i];
+  }
+  return BmTabL{s, g, h};
+}
+template <class TB = BmTabC>
+__device__ __forceinline__ double ln_u32(uint32_t a, const TB& tb = TB{}) {
   const double x = (double)a + 0.5;   // exact
   const uint64_t bx = (uint64_t)__double_as_longlong(x);
   const int e = (int)(bx >> 52) - 1023 - 32;
   const int i = (int)(bx >> 45) & 127;
   const double m = __longlong_as_double((long long)((bx & 0xFFFFFFFFFFFFFull) | 0x3FF0000000000000ull));
   const double c = 1.0 + ((double)i + 0.5) * 0.0078125;   // exact
-  const double2 t = BM_LG[i];
+  const double2 t = tb.lg(i);
   const bool near1 = a >= 0xFF000000u;
   const double d = ((double)(0xFFFFFFFFu - a) + 0.5) * 0x1p-32;   // 1 - u, exact
   const double r = near1 ? -d : (m - c) * t.x;                    // m - c exact
@@ -113,18 +143,19 @@ __device__ __forceinline__ double ln_u32(uint32_t a) {
   // the three cases as selects, not branches: a wave's lanes split about
   // evenly between u < 1/2 and u >= 1/2, so branches ran both paths anyway
 #if LTE_BM_SELECT
-  const double lh = BM_LH[i] + p;
+  const double lh = tb.lh(i) + p;
   const double gen = (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
   return near1 ? p : (e == -1 ? lh : gen);
 #else
   if (near1) return p;
-  if (e == -1) return BM_LH[i] + p;
+  if (e == -1) return tb.lh(i) + p;
   return (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
 #endif
 }
-__device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b) {
-  const double r = sqrt(-2.0 * ln_u32(a));
-  const double2 T = BM_SC[b >> 24];
+template <class TB = BmTabC>
+__device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b, const TB& tb = TB{}) {
+  const double r = sqrt(-2.0 * ln_u32(a, tb));
+  const double2 T = tb.sc(b >> 24);
   const double x = ((double)((int)(b & 0xFFFFFFu) - 0x800000) + 0.5) * 0x1p-32 * 0x1.921fb54442d18p+2;
   const double x2 = x * x;
   const double sx = x + x * x2 * (-0x1.5555555555555p-3 + x2 * (0x1.1111111111111p-7 + x2 * -0x1.a01a01a01a01ap-13));
@@ -137,6 +168,11 @@ __device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b) {
 template <class R> __device__ __forceinline__ cx<R> gauss2(uint32_t a, uint32_t b);
 template <> __device__ __forceinline__ float2 gauss2<float>(uint32_t a, uint32_t b) { return box_muller(a, b); }
 template <> __device__ __forceinline__ double2 gauss2<double>(uint32_t a, uint32_t b) { return box_muller64t(a, b); }
+// the same draws with the float64 tables read through tb (float32: no tables)
+template <class R, class TB> __device__ __forceinline__ cx<R> gauss2t(uint32_t a, uint32_t b, const TB& tb) {
+  if constexpr (sizeof(R) == 8) return box_muller64t(a, b, tb);
+  else return box_muller(a, b);
+}
 
 // ---------------------------------------------------------------- complex
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }

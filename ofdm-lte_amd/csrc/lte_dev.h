@@ -200,15 +200,32 @@ __device__ __forceinline__ R rx_link_sigma(const R* __restrict__ link_sigma, siz
   return sqrt(s2);
 }
 
+// The float64 Box-Muller tables of a block's noise draws: staged into its
+// static LDS array bmt (BM_LDS_BYTES; the 4-8 table gathers per draw then hit
+// LDS instead of the L1 / L2: the config-4 link-noise pass 32.0 -> 27.1 ms per
+// 65 536 frames); float32 draws use no tables.  A barrier must follow before
+// the first draw.
+#ifndef LTE_BM_LDS   // 0: the __constant__ tables (A/B builds)
+#define LTE_BM_LDS 1
+#endif
+template <class R>
+__device__ __forceinline__ auto bm_stage(double2* bmt) {
+  if constexpr (sizeof(R) == 8 && LTE_BM_LDS) return bm_tables_lds(bmt, threadIdx.x, blockDim.x);
+  else return BmTabC{};
+}
+#define LTE_BM_LDS_DECL(R) __shared__ double2 lte_bmt[sizeof(R) == 8 && LTE_BM_LDS ? BM_LDS_BYTES / 16 : 1]
+
 // Noise-add for one OFDM symbol into LDS, one Philox call per pair of
 // samples (sample n uses half (n&1) of counter n>>1 -- same draws as
 // load_symbol_noisy, at half the generator cost).  Lane t stores samples 2t
 // and 2t + 1 (a stride-2 ds_write pattern, 2-way on 16-B and 8-B elements);
 // SW = true stores them swizzled (conflict-free) for fft_lds<.., ISW = true>.
-template <bool SW = false, class V>
+// tb: where the float64 Box-Muller tables are read (bm_stage).
+template <bool SW = false, class V, class TB = BmTabC>
 __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__ yf, int N, int cp, int l,
                                                    re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
-                                                   const re_t<V>* __restrict__ zf, int L, int tid, int T) {
+                                                   const re_t<V>* __restrict__ zf, int L, int tid, int T,
+                                                   const TB& tb = TB{}) {
   using R = re_t<V>;
   const int off = l * (N + cp) + cp;
   if (zf) {
@@ -233,11 +250,11 @@ __device__ __forceinline__ void load_symbol_noisy2(V* buf, const V* __restrict__
     if (p > p1) break;
     const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
     if (n0 >= off) {
-      const V z = gauss2<R>(r.x, r.y);
+      const V z = gauss2t<R>(r.x, r.y, tb);
       buf[SW ? fft_sw<V>(n0 - off) : n0 - off] = mkc(va[i].x + sigma * z.x, va[i].y + sigma * z.y);
     }
     if (n0 + 1 < off + N) {
-      const V z = gauss2<R>(r.z, r.w);
+      const V z = gauss2t<R>(r.z, r.w, tb);
       buf[SW ? fft_sw<V>(n0 + 1 - off) : n0 + 1 - off] = mkc(vb[i].x + sigma * z.x, vb[i].y + sigma * z.y);
     }
   }

@@ -305,7 +305,7 @@ int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int c
 // config 4: SFBC TX + static-tap Rayleigh links in one pass per frame (y gets
 // the faded RX signals, lp.part one power per link); then the link sigmas, the
 // combined link noise added to y and the RX power partials pow_part
-// [B][num_rx][n_sym]
+// [B][num_rx][*pow_nblk] (*pow_nblk = 1: one per frame and RX)
 template <class R>
 bool sfbc_txch_supported(const Grid& g, const MimoGrid& m, int n_paths, int max_delay);
 template <class R>
@@ -314,7 +314,7 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
                           cx<R>* y, int B);
 template <class R>
 int launch_link_noise_add(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
-                          cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part);
+                          cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part, int* pow_nblk);
 // phases / gains: exact-Jakes mode (m.exact_jakes) only
 template <class R>
 int launch_channel_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, int n_paths, const int32_t* delays,

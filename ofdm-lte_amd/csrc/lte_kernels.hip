@@ -147,7 +147,12 @@ __device__ __forceinline__ V* dyn_lds() {
 // one slot (T >= 64), so the set's address is wave-uniform (scalar loads);
 // paths outer, the thread's samples (at most TXCH_MAXS) inner.
 constexpr int TXCH_MAXS = 10;   // samples per thread per symbol: S <= 1.25 N (cp <= N / 4), T = N / 8
-template <class R, bool TV>
+// NP > 0: the path count as a compile-time constant (static taps), so only NP
+// taps are formed (with a runtime count the unrolled TXCH_MAXP taps were all
+// computed and masked by selects).  float64 only: in float32 the compiler
+// contracts the tap sums into FMAs differently once the selects are gone, and
+// k_ofdm_txf must equal the per-symbol k_ofdm_tx<.., CH> bit for bit.
+template <class R, bool TV, int NP = 0>
 __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxChannelT<R>& ch, int b, int l, int slot,
                                            int tid, int T, bool active, R sc) {
   using V = cx<R>;
@@ -204,11 +209,13 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
       }
     } else if (!TV && active) {
       // sample j of the CP-extended symbol is buf[(j - cp) mod N] (N a power of 2)
-      V cf[TXCH_MAXP];
-      int off[TXCH_MAXP];
+      constexpr int PM = NP ? NP : TXCH_MAXP;
+      const int np = NP ? NP : ch.n_paths;
+      V cf[PM];
+      int off[PM];
 #pragma unroll
-      for (int p = 0; p < TXCH_MAXP; ++p) {
-        const V c = p < ch.n_paths ? ch.coef[br * ch.n_paths + p] : mkc((R)0, (R)0);
+      for (int p = 0; p < PM; ++p) {
+        const V c = p < np ? ch.coef[br * np + p] : mkc((R)0, (R)0);
         cf[p] = F64 ? c : cscale(c, sc);
         off[p] = ch.delays[p] + cp;
       }
@@ -216,8 +223,8 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
       for (int m = D + tid; m < S; m += T) {
         V v = mkc((R)0, (R)0);
 #pragma unroll
-        for (int p = 0; p < TXCH_MAXP; ++p)
-          if (p < ch.n_paths) v = cadd(v, cmul(cf[p], buf[(m - off[p]) & (N - 1)]));
+        for (int p = 0; p < PM; ++p)
+          if (p < np) v = cadd(v, cmul(cf[p], buf[(m - off[p]) & (N - 1)]));
         if (m >= cp) yo[m] = v;
         pw += v.x * v.x + v.y * v.y;
       }
@@ -245,7 +252,7 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
 // DFT-precoded (M = Nd, core/modulator.py:232-236) in a second LDS buffer first.
 // CH: the channel applied in place (tx_channel: 1 static taps, 2 time-varying);
 // NC: compile-time N (fft_lds).
-template <class R, int CODED, int BPS, bool SCF = false, int CH = 0, int NC = 0>
+template <class R, int CODED, int BPS, bool SCF = false, int CH = 0, int NC = 0, int NP = 0>
 __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restrict__ pw, int PW,
                                                 const uint32_t* __restrict__ enc, int enc_words,
                                                 const int32_t* __restrict__ tx_map, cx<R>* __restrict__ x, int B,
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
   // f64 + channel: the IFFT's last pass applies the output scale
   fft_lds<true, NC, CH != 0 && sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
   if constexpr (CH != 0) {
-    tx_channel<R, CH == 2>(buf, g, ch, b, l, slot, tid, T, active, sc);
+    tx_channel<R, CH == 2, NP>(buf, g, ch, b, l, slot, tid, T, active, sc);
   } else if (active) {
     V* xo = x + (size_t)b * g.L + (size_t)l * (N + g.cp);
     for (int k = tid; k < N; k += T) xo[g.cp + k] = cscale(buf[k], sc);
@@ -385,6 +392,47 @@ bool txch_supported(const Grid& g, int n_paths, int max_delay) {
          2 * max_delay < g.N + g.cp;
 }
 
+// one k_ofdm_tx<.., CH> launch; float64 static taps (CH 1) of the ITU path
+// counts 4 and 6 with the count at compile time (tx_channel NP)
+template <class R, int C_, int B_, bool S_, int CH_, int NC_>
+static void ofdm_tx_ch_np(hipStream_t s, int blocks, size_t shm, const Grid& g, const uint32_t* pw, int PW,
+                          const uint32_t* enc, int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms,
+                          int stage_enc, const TxChannelT<R>& ch) {
+  if constexpr (CH_ == 1 && !S_ && sizeof(R) == 8) {
+    if (ch.n_paths == 4) {
+      hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, S_, CH_, NC_, 4>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,
+                         enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch);
+      return;
+    }
+    if (ch.n_paths == 6) {
+      hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, S_, CH_, NC_, 6>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,
+                         enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, S_, CH_, NC_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc, enc_words,
+                     tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch);
+}
+// compile-time N: 2048 (20 MHz), and 1024 (10 MHz, config 3) for the uncoded
+// OFDM transmitters with static taps
+template <class R, int C_, int B_, bool S_, int CH_>
+static void ofdm_tx_ch_go(hipStream_t s, int blocks, size_t shm, const Grid& g, const uint32_t* pw, int PW,
+                          const uint32_t* enc, int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms,
+                          int stage_enc, const TxChannelT<R>& ch) {
+  if (g.N == 2048) {
+    ofdm_tx_ch_np<R, C_, B_, S_, CH_, 2048>(s, blocks, shm, g, pw, PW, enc, enc_words, tx_map, B, cap_syms, stage_enc, ch);
+    return;
+  }
+  if constexpr (CH_ == 1 && !S_ && !C_) {
+    if (g.N == 1024) {
+      ofdm_tx_ch_np<R, C_, B_, S_, CH_, 1024>(s, blocks, shm, g, pw, PW, enc, enc_words, tx_map, B, cap_syms, stage_enc,
+                                              ch);
+      return;
+    }
+  }
+  ofdm_tx_ch_np<R, C_, B_, S_, CH_, 0>(s, blocks, shm, g, pw, PW, enc, enc_words, tx_map, B, cap_syms, stage_enc, ch);
+}
+
 template <class R>
 int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* pw, int PW, const uint32_t* enc,
                       int enc_words, const int32_t* tx_map, int B, cx<R>* cap_syms, const TxChannelT<R>& ch,
@@ -400,13 +448,8 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
   const size_t enc_shm = tx_enc_shm(coded, spw, enc_words);
   const int stage_enc = enc_shm > 0;
   const size_t shm = (sc_fdm ? 2 : 1) * (size_t)spw * g.N * sizeof(cx<R>) + enc_shm;
-#define LTE_TXC2(C_, B_, S_, CH_)                                                                                 \
-  if (g.N == 2048)                                                                                                 \
-    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, S_, CH_, 2048>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,      \
-                       enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch);                             \
-  else                                                                                                             \
-    hipLaunchKernelGGL((k_ofdm_tx<R, C_, B_, S_, CH_>), dim3(blocks), dim3(WG), shm, s, g, pw, PW, enc,             \
-                       enc_words, tx_map, (cx<R>*)nullptr, B, cap_syms, stage_enc, ch)
+#define LTE_TXC2(C_, B_, S_, CH_) \
+  ofdm_tx_ch_go<R, C_, B_, S_, CH_>(s, blocks, shm, g, pw, PW, enc, enc_words, tx_map, B, cap_syms, stage_enc, ch)
 #define LTE_TXC(C_, B_, S_)                                                                                      \
   do {                                                                                                             \
     if (ch.tcoef) { LTE_TXC2(C_, B_, S_, 2); } else { LTE_TXC2(C_, B_, S_, 1); }                                   \
@@ -442,7 +485,7 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
 // carries RE txf_re[l][s] and reads its coded-bit sources from the slot-ordered
 // copy of tx_map (txf_map[l][s][m]), chosen on the host so that the 32 lanes of
 // each ds_read_b32 gather hit distinct LDS banks; null: slot s = RE s.
-template <class R, int BPS, int NC = 0, bool TV = false>
+template <class R, int BPS, int NC = 0, bool TV = false, int NP = 0>
 __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32_t* __restrict__ enc, int enc_words,
                                                           const int32_t* __restrict__ tx_map,
                                                           const int32_t* __restrict__ txf_map,
@@ -516,7 +559,7 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
     fft_lds<true, NC, sizeof(R) == 8>(buf, N, g.log2N, G::tw(g), tid, active, sc);
     // every read of buf in tx_channel precedes its reduction barrier, so the
     // next symbol may overwrite buf after it
-    tx_channel<R, TV>(buf, g, ch, b, l, slot, tid, T, active, sc);
+    tx_channel<R, TV, NP>(buf, g, ch, b, l, slot, tid, T, active, sc);
   }
 }
 
@@ -533,10 +576,13 @@ int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_w
   do {                                                                                                          \
     if (ch.tcoef)                                                                                               \
       hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_, true>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words,   \
-                         tx_map, txf_map, txf_re, B, cap_syms, ch);                                             \
+                         tx_map, txf_map, txf_re, B, cap_syms, ch);                              \
+    else if (NC_ == 2048 && ch.n_paths == 4 && sizeof(R) == 8)                                                  \
+      hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_, false, 4>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, \
+                         tx_map, txf_map, txf_re, B, cap_syms, ch);                              \
     else                                                                                                        \
       hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, tx_map, \
-                         txf_map, txf_re, B, cap_syms, ch);                                                     \
+                         txf_map, txf_re, B, cap_syms, ch);                                      \
   } while (0)
   if (g.N == 2048) {
     if (g.bps == 2) LTE_TXF(2, 2048); else if (g.bps == 4) LTE_TXF(4, 2048); else LTE_TXF(6, 2048);
@@ -1354,13 +1400,16 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh
   ZfCoef<R> zc[QM];
   R nvq[QM];
   uint32_t errs = 0;
+  LTE_BM_LDS_DECL(R);
+  const auto bmt = bm_stage<R>(lte_bmt);
+  __syncthreads();
   for (int l = 0; l < g.n_sym; ++l) {
     // tid made opaque per symbol: the FFT / loader address arithmetic derived
     // from it is recomputed each symbol instead of hoisted and held live
     // across the loop (which took the kernel to 255 VGPRs)
     int tid = tid0;
     asm volatile("" : "+v"(tid));
-    if (active) load_symbol_noisy2<true>(buf, yf, N, g.cp, l, sigma, seed, fr, 0, zf, g.L, tid, T);
+    if (active) load_symbol_noisy2<true>(buf, yf, N, g.cp, l, sigma, seed, fr, 0, zf, g.L, tid, T, bmt);
     __syncthreads();
     fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, G::tw(g), tid, active);
     if (l % 14 == 0) {   // group estimate from its first symbol (lte_receiver.py:360-411)
@@ -1543,6 +1592,9 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo(
 #pragma unroll
   for (int q = 0; q < QM; ++q) den[q] = (R)0;
   uint32_t errs = 0;
+  LTE_BM_LDS_DECL(R);
+  const auto bmt = bm_stage<R>(lte_bmt);
+  __syncthreads();
   for (int l = 0; l < g.n_sym; ++l) {
     const bool est = l % 14 == 0;
     const int grp = l / 14;
@@ -1559,7 +1611,7 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo(
       if (active) {
         const R sigma = sqrt(npow[(size_t)b * num_rx + rx] / (R)2);
         const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-        load_symbol_noisy2<true>(buf, yf + rx * y_rx_stride, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T);
+        load_symbol_noisy2<true>(buf, yf + rx * y_rx_stride, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T, bmt);
       }
       __syncthreads();
       fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, G::tw(g), tid, active);

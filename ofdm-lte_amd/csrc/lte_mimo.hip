@@ -880,11 +880,16 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
 // kept in LDS -- the frame walks its symbols in order, so no fix-up pass is
 // needed.  Each link's power sum_n |y0_rt|^2 accumulates over the frame (the
 // link noise's standard deviation, k_link_sigma).  y0 goes to HBM once; the
-// TX streams x never do.  k_link_noise_add then adds the link noise and forms
+// TX streams x never do.  k_link_noise_pairs then adds the link noise and forms
 // the RX power partials.  Static taps only (n_cs = 1), N = 2048 (two 32 KB
 // grids: two slots per CU).
 constexpr int SFX_TL = 32;   // largest max_delay (samples) the kept tails cover
-template <class R, int CODED, int BPS, int NRX, int NC = 2048>
+// timing probes for A/B builds only (wrong results): bit 0 skips the Alamouti
+// mapping, bit 1 the IFFTs, bit 2 the link taps (y = x_0 + x_1 at n)
+#ifndef LTE_SFX_PROBE
+#define LTE_SFX_PROBE 0
+#endif
+template <class R, int CODED, int BPS, int NRX, int NP = 0, int NC = 2048>
 __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                           const uint32_t* __restrict__ enc, int enc_words,
                                                           const int32_t* __restrict__ tx_map, TxLinkPower<R> lp,
@@ -900,7 +905,10 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
   constexpr int TB0 = 2 * N;
   const int tid0 = threadIdx.x, b = blockIdx.x;
   const bool active = b < B;   // (grid = B blocks: always; kept for the shared FFT helper)
-  const int S = N + g.cp, TL = lp.max_delay, np = lp.n_paths;
+  // NP > 0: the path count at compile time (only NP taps formed; a runtime
+  // count computed all TXCH_MAXP unrolled taps under selects)
+  constexpr int PM = NP ? NP : TXCH_MAXP;
+  const int S = N + g.cp, TL = lp.max_delay, np = NP ? NP : lp.n_paths;
   const uint32_t* fb = pw + (size_t)b * PW;
   const uint32_t* fe = enc + (size_t)b * enc_words;
   if (CODED && stage_enc) {
@@ -909,9 +917,9 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
     fe = es;
   }
   for (int i = tid0; i < NTX * SFX_TL; i += T) sm[TB0 + i] = mkc((R)0, (R)0);   // zero prefix of the stream
-  int dl[TXCH_MAXP];
+  int dl[PM];
 #pragma unroll
-  for (int p = 0; p < TXCH_MAXP; ++p) dl[p] = p < np ? lp.delays[p] : 0;
+  for (int p = 0; p < PM; ++p) dl[p] = p < np ? lp.delays[p] : 0;
   R pwr[NRX][NTX];
 #pragma unroll
   for (int r = 0; r < NRX; ++r)
@@ -924,7 +932,7 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
     asm volatile("" : "+v"(tid));
     for (int k = tid; k < 2 * N; k += T) sm[k] = mkc((R)0, (R)0);
     __syncthreads();   // (first symbol: also the staged streams and the zeroed tails)
-    {
+    if (!(LTE_SFX_PROBE & 1)) {
       const int64_t q0 = (int64_t)l * m.res;
 #pragma unroll
       for (int k = 0; k < SFP; ++k) {   // TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)]
@@ -949,33 +957,53 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
     }
     __syncthreads();
     // x_t = ifft(G_t) sqrt(N), both grids in one sweep (ends with a barrier)
-    fft2_lds<true, NC, true>(sm, sm + N, GridT<R>::tw(g), tid, active, sc);
+    if (!(LTE_SFX_PROBE & 2)) fft2_lds<true, NC, true>(sm, sm + N, GridT<R>::tw(g), tid, active, sc);
     // the frame's static taps c_rtp (coef [B][num_rx][num_tx][np][NCF], n_cs =
     // 1), loaded per symbol into VGPRs for the sample loop only: as
     // wave-uniform values the compiler would keep them in SGPRs and spill them
     // to VGPR lanes inside the loop; held across the FFTs they would crowd them
-    V c[NRX][NTX][TXCH_MAXP];
+    V c[NRX][NTX][PM];
 #pragma unroll
     for (int r = 0; r < NRX; ++r)
 #pragma unroll
       for (int t = 0; t < NTX; ++t) {
         const V* cf = lp.coef + (((size_t)b * NRX + r) * NTX + t) * np * NCF;
 #pragma unroll
-        for (int p = 0; p < TXCH_MAXP; ++p) {
+        for (int p = 0; p < PM; ++p) {
           c[r][t][p] = p < np ? cf[p * NCF] : mkc((R)0, (R)0);
           asm volatile("" : "+v"(c[r][t][p].x), "+v"(c[r][t][p].y));
         }
       }
     V* yl = y + (size_t)b * NRX * g.L + (size_t)l * S;
     for (int n = tid; n < S; n += T) {
-      V xs[NTX][TXCH_MAXP];   // x_t at CP-extended position n - d_p (negative: the previous symbol's tail)
+      if (LTE_SFX_PROBE & 4) {
+        const V a = cadd(sm[(n - g.cp) & (N - 1)], sm[N + ((n - g.cp) & (N - 1))]);
 #pragma unroll
-      for (int p = 0; p < TXCH_MAXP; ++p)
-        if (p < np) {
-          const int i = n - dl[p];
-#pragma unroll
-          for (int t = 0; t < NTX; ++t) xs[t][p] = sm[i >= 0 ? t * N + ((i - g.cp) & (N - 1)) : TB0 + t * SFX_TL + TL + i];
+        for (int r = 0; r < NRX; ++r) {
+          yl[(size_t)r * g.L + n] = a;
+          pwr[r][0] += a.x * a.x;
         }
+        continue;
+      }
+      V xs[NTX][PM];   // x_t at CP-extended position n - d_p (negative: the previous symbol's tail)
+      if (n >= g.cp + TL) {   // every tap inside the symbol's own samples, past the CP: grid index n - cp - d_p
+        const int i0 = n - g.cp;
+#pragma unroll
+        for (int p = 0; p < PM; ++p)
+          if (p < np) {
+#pragma unroll
+            for (int t = 0; t < NTX; ++t) xs[t][p] = sm[t * N + i0 - dl[p]];
+          }
+      } else {
+#pragma unroll
+        for (int p = 0; p < PM; ++p)
+          if (p < np) {
+            const int i = n - dl[p];
+#pragma unroll
+            for (int t = 0; t < NTX; ++t)
+              xs[t][p] = sm[i >= 0 ? t * N + ((i - g.cp) & (N - 1)) : TB0 + t * SFX_TL + TL + i];
+          }
+      }
 #pragma unroll
       for (int r = 0; r < NRX; ++r) {
         V a[NTX];
@@ -983,7 +1011,7 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
         for (int t = 0; t < NTX; ++t) {
           a[t] = mkc((R)0, (R)0);
 #pragma unroll
-          for (int p = 0; p < TXCH_MAXP; ++p)
+          for (int p = 0; p < PM; ++p)
             if (p < np) a[t] = cadd(a[t], cmul(c[r][t][p], xs[t][p]));
           pwr[r][t] += a[t].x * a[t].x + a[t].y * a[t].y;
         }
@@ -1010,59 +1038,68 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
 // transmit_mimo's link noise on the Philox path after k_ofdm_txch_sfbc: y0_r +
 // the RX's combined 100 dB link noise (rx_link_sigma, one draw per sample on
 // link (r, 0)'s stream, the values and the order k_channel_tay adds them in),
-// written back, and the RX power partials per OFDM symbol of the result for
-// the (P / num_tx) / SNR rule (core/ofdm_core.py:524-534).  One block per
-// (frame, OFDM symbol); every receive antenna's J samples of a pass are loaded
-// before their noise is drawn (NRX x J loads in flight), one reduction for all
-// antennas at the end.  (Measured against drawing the link noise a second time
-// in the receiver instead of writing it here: the receiver is VALU-bound and
-// lost more, 12.5 ms, than the write saved, 9.3 ms per 65 536 frames.)
-template <class R, int J, int NRX>
-__global__ __launch_bounds__(MWG) void k_link_noise_add(int L, int num_tx, int sym_len, cx<R>* __restrict__ y,
-                                                        const R* __restrict__ link_sigma,
-                                                        const uint64_t* __restrict__ fid, uint64_t seed,
-                                                        R* __restrict__ pow_part, int nblk) {
+// written back, and the RX power of the result for the (P / num_tx) / SNR rule
+// (core/ofdm_core.py:524-534).  One block per (frame, RX antenna) walking the
+// whole frame in sample pairs: lane k of a round takes pair p = (2p, 2p+1), the
+// two halves of one Philox draw (counter p, as link_noise_at), so there is one
+// draw per two samples with no lane exchange.  Loads for U pairs are issued
+// before the first draw.  One RX power partial per (frame, RX): nblk = 1 for
+// k_npow_mimo.  (Measured against drawing the link noise a second time in the
+// receiver instead of writing it here: the receiver is VALU-bound and lost
+// more, 12.5 ms, than the write saved, 9.3 ms per 65 536 frames; against the
+// per-(frame, symbol) form with J-sample spans and lane-pair shuffles: 32.1 vs
+// 32.9 ms.)
+// LT: the float64 Box-Muller tables read from an LDS copy (bm_tables_lds)
+// instead of the __constant__ arrays.
+template <class R, int U, bool LT>
+__global__ __launch_bounds__(MWG) void k_link_noise_pairs(int L, int num_rx, int num_tx, cx<R>* __restrict__ y,
+                                                          const R* __restrict__ link_sigma,
+                                                          const uint64_t* __restrict__ fid, uint64_t seed,
+                                                          R* __restrict__ pow_part) {
   using V = cx<R>;
-  __shared__ R red[NRX][MWG / 64];
-  const int blk = blockIdx.x % nblk, b = blockIdx.x / nblk;
-  const int nbeg = blk * sym_len, nend = min(nbeg + sym_len, L);
-  R sr[NRX], pw[NRX];
-#pragma unroll
-  for (int r = 0; r < NRX; ++r) {
-    sr[r] = rx_link_sigma(link_sigma, ((size_t)b * NRX + r) * num_tx, num_tx);
-    pw[r] = (R)0;
+  __shared__ R red[MWG / 64];
+  constexpr bool TL = LT && sizeof(R) == 8;
+  __shared__ double2 bmt[TL ? BM_LDS_BYTES / 16 : 1];
+  BmTabL tbl{};
+  if constexpr (TL) {
+    tbl = bm_tables_lds(bmt, threadIdx.x, MWG);
+    __syncthreads();
   }
-  V* yb = y + (size_t)b * NRX * L;
-  for (int base = nbeg; base < nend; base += J * MWG) {
-    const SymSpan<J> sp(base, nbeg, nend, 0.f, false);
-    V v[NRX][J];
+  const int br = blockIdx.x, r = br % num_rx;
+  const size_t b = (size_t)(br / num_rx);
+  const R sg = rx_link_sigma(link_sigma, (size_t)br * num_tx, num_tx);
+  const uint64_t frame = fid[b];
+  const uint32_t stream = RNG_STREAM_MIMO_LINK + (uint32_t)(r * num_tx);
+  V* yb = y + (size_t)br * L;
+  const int npair = (L + 1) >> 1;
+  R pw = (R)0;
+  for (int p0 = threadIdx.x; p0 < npair; p0 += U * MWG) {
+    V va[U], vb[U];
 #pragma unroll
-    for (int r = 0; r < NRX; ++r)
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * MWG, n = 2 * p;
+      va[u] = p < npair ? yb[n] : mkc((R)0, (R)0);
+      vb[u] = n + 1 < L ? yb[n + 1] : mkc((R)0, (R)0);
+    }
 #pragma unroll
-      for (int j = 0; j < J; ++j) v[r][j] = sp.ok[j] ? yb[(size_t)r * L + sp.n[j]] : mkc((R)0, (R)0);
-#pragma unroll
-    for (int r = 0; r < NRX; ++r) {
-      link_noise_span<R, J>(v[r], sp, sr[r], seed, fid[b], r * num_tx, (nbeg & 1) == 0);
-#pragma unroll
-      for (int j = 0; j < J; ++j)
-        if (sp.ok[j]) {
-          yb[(size_t)r * L + sp.n[j]] = v[r][j];
-          pw[r] += v[r][j].x * v[r][j].x + v[r][j].y * v[r][j].y;
-        }
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * MWG, n = 2 * p;
+      if (p >= npair) break;
+      const u32x4 q = rng4(seed, frame, stream, (uint32_t)p);
+      const V z0 = TL ? gauss2t<R>(q.x, q.y, tbl) : gauss2<R>(q.x, q.y);
+      const V a = mkc(va[u].x + sg * z0.x, va[u].y + sg * z0.y);
+      yb[n] = a;
+      pw += a.x * a.x + a.y * a.y;
+      if (n + 1 < L) {
+        const V z1 = TL ? gauss2t<R>(q.z, q.w, tbl) : gauss2<R>(q.z, q.w);
+        const V c = mkc(vb[u].x + sg * z1.x, vb[u].y + sg * z1.y);
+        yb[n + 1] = c;
+        pw += c.x * c.x + c.y * c.y;
+      }
     }
   }
-#pragma unroll
-  for (int r = 0; r < NRX; ++r) {
-    R t = pw[r];
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-    if ((threadIdx.x & 63) == 0) red[r][threadIdx.x >> 6] = t;
-  }
-  __syncthreads();
-  if (threadIdx.x < NRX) {
-    R t = (R)0;
-    for (int i = 0; i < MWG / 64; ++i) t += red[threadIdx.x][i];
-    pow_part[((size_t)b * NRX + threadIdx.x) * nblk + blk] = t;
-  }
+  const R t = block_sum(pw, red);
+  if (threadIdx.x == 0) pow_part[br] = t;
 }
 
 template <class R>
@@ -1082,7 +1119,7 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
   const size_t shm = (2 * (size_t)g.N + 2 * SFX_TL) * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
 #define LTE_SFX(C_, B_, NR_)                                                                                          \
   do {                                                                                                                \
-    auto k = k_ofdm_txch_sfbc<R, C_, B_, NR_>;                                                                        \
+    auto k = lp.n_paths == 4 ? k_ofdm_txch_sfbc<R, C_, B_, NR_, 4> : k_ofdm_txch_sfbc<R, C_, B_, NR_, 0>;           \
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                  \
     hipLaunchKernelGGL(k, dim3(B), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words, tx_map, lp, y, B, stage_enc);     \
   } while (0)
@@ -1098,18 +1135,13 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
 
 template <class R>
 int launch_link_noise_add(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
-                          cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part) {
+                          cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part, int* pow_nblk) {
   if (m.num_rx < 1 || m.num_rx > 2) return (int)hipErrorInvalidValue;
-  const int sym_len = g.N + g.cp;
-  const int nch = mimo_channel_nblk(g.L, sym_len);
   const int nl = B * m.num_rx * m.num_tx;   // one partial per link (k_ofdm_txch_sfbc)
   hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, 1, g.L, link_sigma);
-  if (m.num_rx == 1)
-    hipLaunchKernelGGL((k_link_noise_add<R, 3, 1>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_tx, sym_len, y,
-                       link_sigma, fid, seed, pow_part, nch);
-  else
-    hipLaunchKernelGGL((k_link_noise_add<R, 3, 2>), dim3(nch * B), dim3(MWG), 0, s, g.L, m.num_tx, sym_len, y,
-                       link_sigma, fid, seed, pow_part, nch);
+  *pow_nblk = 1;
+  hipLaunchKernelGGL((k_link_noise_pairs<R, 4, LTE_BM_LDS != 0>), dim3(B * m.num_rx), dim3(MWG), 0, s, g.L, m.num_rx,
+                     m.num_tx, y, link_sigma, fid, seed, pow_part);
   return (int)hipGetLastError();
 }
 
@@ -1628,11 +1660,14 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
   const bool active = slot < spw && b < B;
   V* buf = sm + slot * N;
   V* hp = sm + spw * N + slot * (m.num_tx * m.maxP);
+  LTE_BM_LDS_DECL(R);
+  const auto bmt = bm_stage<R>(lte_bmt);
+  __syncthreads();
   if (active) {
     const R sigma = sqrt(npow[(size_t)b * m.num_rx + rx] * (R)0.5);
     const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
     load_symbol_noisy2<true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf,
-                             g.L, tid, T);
+                             g.L, tid, T, bmt);
   }
   __syncthreads();
   fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
@@ -2187,7 +2222,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
   template int launch_ofdm_txch_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,     \
                                         const uint32_t*, int, const int32_t*, const TxLinkPower<R>&, cx<R>*, int); \
   template int launch_link_noise_add<R>(hipStream_t, const Grid&, const MimoGrid&, int, const R*, R*, cx<R>*,      \
-                                        const uint64_t*, uint64_t, R*);                                            \
+                                        const uint64_t*, uint64_t, R*, int*);                                      \
   template bool sfbc_txch_supported<R>(const Grid&, const MimoGrid&, int, int);                                   \
   template int launch_ofdm_tx_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,       \
                                       const uint32_t*, int, const int32_t*, cx<R>*, int, const TxLinkPower<R>&);   \

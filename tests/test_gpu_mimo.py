@@ -221,7 +221,7 @@ def test_link_power_in_tx_matches_separate_pass(C, prec, monkeypatch):
 @pytest.mark.parametrize('coded,nrx', [(True, 2), (False, 2), (False, 1)])
 def test_sfbc_txch_fused_matches_separate_kernels(C, prec, coded, nrx, monkeypatch):
     """Config 4's TX + static-tap Rayleigh links in one pass per frame
-    (k_ofdm_txch_sfbc + k_link_noise_add, default on the Philox path) against
+    (k_ofdm_txch_sfbc + k_link_noise_pairs, default on the Philox path) against
     the TX streams through HBM and the channel pass (LTE_SFBC_TXCH_FUSE=0):
     received streams (signal_rx: the faded links, the combined 100 dB link
     noise, the RX noise) equal to float64 rounding -- the link paths are summed

@@ -152,9 +152,25 @@ __device__ __forceinline__ double ln_u32(uint32_t a, const TB& tb = TB{}) {
   return (double)e * ln2_hi + (t.y + ((double)e * ln2_lo + p));
 #endif
 }
+// sqrt for x in [2^-767, 2^1023): the steps of LLVM's correctly rounded
+// float64 sqrt expansion for gfx950 (v_rsq_f64 + two Newton-Raphson /
+// Goldschmidt corrections), without its range scaling (two ldexp) and its
+// zero / inf / nan selects, so the same bits on that range.  The radius
+// argument -2 ln u of box_muller64t lies in [2.3e-10, 46].
+__device__ __forceinline__ double sqrt_pos(double x) {
+  double g = x * __builtin_amdgcn_rsq(x);
+  double h = __builtin_amdgcn_rsq(x) * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
 template <class TB = BmTabC>
 __device__ __forceinline__ double2 box_muller64t(uint32_t a, uint32_t b, const TB& tb = TB{}) {
-  const double r = sqrt(-2.0 * ln_u32(a, tb));
+  const double r = sqrt_pos(-2.0 * ln_u32(a, tb));
   const double2 T = tb.sc(b >> 24);
   const double x = ((double)((int)(b & 0xFFFFFFu) - 0x800000) + 0.5) * 0x1p-32 * 0x1.921fb54442d18p+2;
   const double x2 = x * x;

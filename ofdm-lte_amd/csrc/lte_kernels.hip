@@ -522,8 +522,23 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
       const int j = txf_re ? (ok ? txf_re[(size_t)l * QM * T + sl] : 0) : sl;
       const int64_t t0 = txf_re ? ((int64_t)l * QM * T + sl) * BPS : ((int64_t)l * g.Nd + j) * BPS;
       const int32_t* map = txf_re ? txf_map : tx_map;
+      // the RE's BPS entries as 8-B loads (t0 even; BPS 4: 16 B)
+      if (ok) {
+        if constexpr (BPS == 4) {
+          const int4 v = *reinterpret_cast<const int4*>(map + t0);
+          srcs[q][0] = v.x; srcs[q][1] = v.y; srcs[q][2] = v.z; srcs[q][3] = v.w;
+        } else {
 #pragma unroll
-      for (int m = 0; m < BPS; ++m) srcs[q][m] = ok ? map[t0 + m] : -1;
+          for (int m = 0; m < BPS; m += 2) {
+            const int2 v = *reinterpret_cast<const int2*>(map + t0 + m);
+            srcs[q][m] = v.x;
+            srcs[q][m + 1] = v.y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < BPS; ++m) srcs[q][m] = -1;
+      }
       kpos[q] = ok ? g.data_idx[j] : 0;
       jre[q] = j;
 #if LTE_LDS_PROBE & 1   // timing probe only (wrong outputs): conflict-free RE positions

@@ -65,6 +65,37 @@ __device__ __forceinline__ int qam_code(int64_t q, const uint32_t* __restrict__ 
   }
   return zero ? -1 : idx;
 }
+// the QAM codes of coded symbols q and q + 1 (q even, tx_map 16-B aligned):
+// their 2 BPS tx_map entries as BPS / 2 16-B loads instead of 2 BPS 4-B loads
+template <int BPS>
+__device__ __forceinline__ void qam_code_pair(int64_t q, const uint32_t* __restrict__ fe,
+                                              const int32_t* __restrict__ tx_map, int& c0, int& c1) {
+  int src[2 * BPS];
+  const int4* m4 = reinterpret_cast<const int4*>(tx_map + q * BPS);
+#pragma unroll
+  for (int i = 0; i < BPS / 2; ++i) {
+    const int4 v = m4[i];
+    src[4 * i] = v.x;
+    src[4 * i + 1] = v.y;
+    src[4 * i + 2] = v.z;
+    src[4 * i + 3] = v.w;
+  }
+  int c[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    int idx = 0;
+    bool zero = false;
+#pragma unroll
+    for (int m = 0; m < BPS; ++m) {
+      const int sv = src[u * BPS + m];
+      zero |= sv == -2;
+      idx = (idx << 1) | (int)(sv >= 0 ? getbit(fe, sv) : 0u);
+    }
+    c[u] = zero ? -1 : idx;
+  }
+  c0 = c[0];
+  c1 = c[1];
+}
 template <class R, int BPS>
 __device__ __forceinline__ cx<R> qam_of(int code) {
   return code < 0 ? mkc((R)0, (R)0) : qam_point<BPS, R>(code);
@@ -889,15 +920,18 @@ constexpr int SFX_TL = 32;   // largest max_delay (samples) the kept tails cover
 #ifndef LTE_SFX_PROBE
 #define LTE_SFX_PROBE 0
 #endif
-template <class R, int CODED, int BPS, int NRX, int NP = 0, int NC = 2048>
-__global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
+// TPB = 256: one thread per radix-8 butterfly of each grid, both grids in one
+// dual-buffer sweep; TPB = 512: each half of the block transforms one grid
+// (the same operations per element), twice the waves per slot.
+template <class R, int CODED, int BPS, int NRX, int NP = 0, int TPB = MWG, int NC = 2048>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, TPB / 128))) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                           const uint32_t* __restrict__ enc, int enc_words,
                                                           const int32_t* __restrict__ tx_map, TxLinkPower<R> lp,
                                                           cx<R>* __restrict__ y, int B, int stage_enc) {
   using V = cx<R>;
   constexpr int N = NC, T = N >> 3, NTX = 2, NCF = mimo_ncf<R>();
-  static_assert(T == MWG, "one slot per block");
-  __shared__ R red[MWG / 64];
+  static_assert(TPB == T || TPB == 2 * T, "one slot per block");
+  __shared__ R red[TPB / 64];
   // LDS: grids / x_t at [t * N, (t + 1) * N), then [NTX][SFX_TL] the previous
   // symbol's last TL samples of each x_t (one array, so that a delayed sample's
   // address is one index expression), then the staged coded streams
@@ -913,10 +947,10 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
   const uint32_t* fe = enc + (size_t)b * enc_words;
   if (CODED && stage_enc) {
     uint32_t* es = reinterpret_cast<uint32_t*>(sm + TB0 + NTX * SFX_TL);
-    for (int i = tid0; i < enc_words; i += T) es[i] = fe[i];
+    for (int i = tid0; i < enc_words; i += TPB) es[i] = fe[i];
     fe = es;
   }
-  for (int i = tid0; i < NTX * SFX_TL; i += T) sm[TB0 + i] = mkc((R)0, (R)0);   // zero prefix of the stream
+  for (int i = tid0; i < NTX * SFX_TL; i += TPB) sm[TB0 + i] = mkc((R)0, (R)0);   // zero prefix of the stream
   int dl[PM];
 #pragma unroll
   for (int p = 0; p < PM; ++p) dl[p] = p < np ? lp.delays[p] : 0;
@@ -926,20 +960,27 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
 #pragma unroll
     for (int t = 0; t < NTX; ++t) pwr[r][t] = (R)0;
   const R sc = tx_scale<R>(N);
-  constexpr int SFP = 4;   // Alamouti pairs per thread per symbol (n_dsc / 2 <= SFP T)
+  constexpr int SFP = 4 * T / TPB;   // Alamouti pairs per thread per symbol (n_dsc / 2 <= SFP TPB)
   for (int l = 0; l < g.n_sym; ++l) {
     int tid = tid0;   // opaque per symbol: the FFT's addressing is not hoisted into registers
     asm volatile("" : "+v"(tid));
-    for (int k = tid; k < 2 * N; k += T) sm[k] = mkc((R)0, (R)0);
+    for (int k = tid; k < 2 * N; k += TPB) sm[k] = mkc((R)0, (R)0);
     __syncthreads();   // (first symbol: also the staged streams and the zeroed tails)
     if (!(LTE_SFX_PROBE & 1)) {
       const int64_t q0 = (int64_t)l * m.res;
 #pragma unroll
       for (int k = 0; k < SFP; ++k) {   // TX0 [s0, -conj(s1)], TX1 [s1, conj(s0)]
-        const int j = 2 * (tid + k * T);
+        const int j = 2 * (tid + k * TPB);
         if (j >= m.n_dsc) break;
-        const V s0 = qam_of<R, BPS>(qam_code<CODED, BPS>(q0 + j, fb, fe, tx_map));
-        const V s1 = qam_of<R, BPS>(qam_code<CODED, BPS>(q0 + j + 1, fb, fe, tx_map));
+        int c0, c1;
+        if constexpr (CODED) {   // (m.res even: q0 + j even)
+          qam_code_pair<BPS>(q0 + j, fe, tx_map, c0, c1);
+        } else {
+          c0 = qam_code<CODED, BPS>(q0 + j, fb, fe, tx_map);
+          c1 = qam_code<CODED, BPS>(q0 + j + 1, fb, fe, tx_map);
+        }
+        const V s0 = qam_of<R, BPS>(c0);
+        const V s1 = qam_of<R, BPS>(c1);
         const int k0 = g.data_idx[j];
         sm[k0] = s0;
         sm[N + k0] = s1;
@@ -952,12 +993,15 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
 #pragma unroll
       for (int t = 0; t < NTX; ++t) {
         const V* pv = MGT<R>::pval(m) + t * m.maxP;
-        for (int p = tid; p < m.np_tx[t]; p += T) sm[t * N + m.ppos[t * m.maxP + p]] = pv[p];
+        for (int p = tid; p < m.np_tx[t]; p += TPB) sm[t * N + m.ppos[t * m.maxP + p]] = pv[p];
       }
     }
     __syncthreads();
     // x_t = ifft(G_t) sqrt(N), both grids in one sweep (ends with a barrier)
-    if (!(LTE_SFX_PROBE & 2)) fft2_lds<true, NC, true>(sm, sm + N, GridT<R>::tw(g), tid, active, sc);
+    if (!(LTE_SFX_PROBE & 2)) {
+      if constexpr (TPB == T) fft2_lds<true, NC, true>(sm, sm + N, GridT<R>::tw(g), tid, active, sc);
+      else fft_lds<true, NC, true, true>(sm + (tid >= T ? N : 0), N, 0, GridT<R>::tw(g), tid & (T - 1), active, sc);
+    }
     // the frame's static taps c_rtp (coef [B][num_rx][num_tx][np][NCF], n_cs =
     // 1), loaded per symbol into VGPRs for the sample loop only: as
     // wave-uniform values the compiler would keep them in SGPRs and spill them
@@ -975,7 +1019,7 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
         }
       }
     V* yl = y + (size_t)b * NRX * g.L + (size_t)l * S;
-    for (int n = tid; n < S; n += T) {
+    for (int n = tid; n < S; n += TPB) {
       if (LTE_SFX_PROBE & 4) {
         const V a = cadd(sm[(n - g.cp) & (N - 1)], sm[N + ((n - g.cp) & (N - 1))]);
 #pragma unroll
@@ -1019,7 +1063,7 @@ __global__ __launch_bounds__(MWG, 2) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, c
       }
     }
     __syncthreads();   // every read of the old tails and of the grids done
-    for (int i = tid; i < NTX * TL; i += T) {
+    for (int i = tid; i < NTX * TL; i += TPB) {
       const int t = i / TL, k = i - t * TL;
       sm[TB0 + t * SFX_TL + k] = sm[t * N + ((S - TL + k - g.cp) & (N - 1))];
     }
@@ -1105,10 +1149,14 @@ __global__ __launch_bounds__(MWG) void k_link_noise_pairs(int L, int num_rx, int
 template <class R>
 bool sfbc_txch_supported(const Grid& g, const MimoGrid& m, int n_paths, int max_delay) {
   return m.mode == MIMO_SFBC && m.num_tx == 2 && (m.num_rx == 1 || m.num_rx == 2) && g.N == 2048 && m.n_cs == 1 &&
+         (m.res & 1) == 0 &&
          !m.exact_jakes && n_paths >= 1 && n_paths <= TXCH_MAXP && max_delay >= 0 && max_delay <= SFX_TL &&
          max_delay <= g.cp && m.n_dsc <= 2 * 4 * (g.N >> 3) && (g.bps == 2 || g.bps == 4 || g.bps == 6);
 }
 
+#ifndef LTE_SFX_TPB   // threads per frame slot of k_ofdm_txch_sfbc (256 or 512)
+#define LTE_SFX_TPB 512
+#endif
 template <class R>
 int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
                           const uint32_t* enc, int enc_words, const int32_t* tx_map, const TxLinkPower<R>& lp,
@@ -1119,9 +1167,10 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
   const size_t shm = (2 * (size_t)g.N + 2 * SFX_TL) * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
 #define LTE_SFX(C_, B_, NR_)                                                                                          \
   do {                                                                                                                \
-    auto k = lp.n_paths == 4 ? k_ofdm_txch_sfbc<R, C_, B_, NR_, 4> : k_ofdm_txch_sfbc<R, C_, B_, NR_, 0>;           \
+    const int tpb = lp.n_paths == 4 ? LTE_SFX_TPB : MWG;                                                              \
+    auto k = lp.n_paths == 4 ? k_ofdm_txch_sfbc<R, C_, B_, NR_, 4, LTE_SFX_TPB> : k_ofdm_txch_sfbc<R, C_, B_, NR_, 0>; \
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                  \
-    hipLaunchKernelGGL(k, dim3(B), dim3(MWG), shm, s, g, m, pw, PW, enc, enc_words, tx_map, lp, y, B, stage_enc);     \
+    hipLaunchKernelGGL(k, dim3(B), dim3(tpb), shm, s, g, m, pw, PW, enc, enc_words, tx_map, lp, y, B, stage_enc);     \
   } while (0)
 #define LTE_SFX_NR(C_, B_) do { if (m.num_rx == 1) LTE_SFX(C_, B_, 1); else LTE_SFX(C_, B_, 2); } while (0)
 #define LTE_SFX_B(C_) \
@@ -1637,14 +1686,17 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
 }
 
 // ---------------------------------------------------------------------------
-// RX FFT + MIMO CRS estimation.  One slot per (frame, rx, OFDM symbol):
-// noise + CP removal + FFT/sqrt(N) (demodulate_and_estimate_mimo, core/
-// mimo_channel_estimator_periodic.py:236-273); the n_dsc data SCs go to
-// Y[b][l][rx][n_dsc].  On estimation symbols (SFBC: first of each 14-symbol
-// group, :195-234; spatial: every symbol, core/ofdm_core.py:2752) LS at each
-// TX's pilot subset + linear interpolation with edge hold (:108-185 +
-// lte_receiver.py:98-133: np.linspace, k (delta / gap) + start) at the data
-// SCs -> H[b][rx][e][tx][n_dsc].
+// RX FFT + MIMO CRS estimation.  One slot per (frame, rx) walking the frame's
+// OFDM symbols (per symbol the same work as one slot per (frame, rx, symbol)
+// did; the walk amortises the slot's setup and the LDS copy of the Box-Muller
+// tables over 14 symbols): noise + CP removal + FFT/sqrt(N)
+// (demodulate_and_estimate_mimo, core/mimo_channel_estimator_periodic.py:
+// 236-273); the n_dsc data SCs go to Y[b][l][rx][n_dsc].  On estimation
+// symbols (SFBC: first of each 14-symbol group, :195-234; spatial: every
+// symbol, core/ofdm_core.py:2752) LS at each TX's pilot subset + linear
+// interpolation with edge hold (:108-185 + lte_receiver.py:98-133:
+// np.linspace, k (delta / gap) + start) at the data SCs ->
+// H[b][rx][e][tx][n_dsc].
 template <class R, int NC = 0>
 __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
                                                      const R* __restrict__ npow, const uint64_t* __restrict__ fid,
@@ -1653,58 +1705,62 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
   using V = cx<R>;
   V* sm = mimo_lds<V>();
   const int N = NC ? NC : g.N, T = N >> 3, spw = MWG / T;
-  const int slot = threadIdx.x / T, tid = threadIdx.x % T;
-  const int per = m.num_rx * g.n_sym;
+  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
   const int gs = blockIdx.x * spw + slot;
-  const int b = gs / per, r = gs - b * per, rx = r / g.n_sym, l = r - rx * g.n_sym;
+  const int b = gs / m.num_rx, rx = gs - b * m.num_rx;
   const bool active = slot < spw && b < B;
   V* buf = sm + slot * N;
   V* hp = sm + spw * N + slot * (m.num_tx * m.maxP);
   LTE_BM_LDS_DECL(R);
   const auto bmt = bm_stage<R>(lte_bmt);
-  __syncthreads();
-  if (active) {
-    const R sigma = sqrt(npow[(size_t)b * m.num_rx + rx] * (R)0.5);
-    const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-    load_symbol_noisy2<true>(buf, y + ((size_t)b * m.num_rx + rx) * g.L, N, g.cp, l, sigma, seed, fid[b], rx, zf,
-                             g.L, tid, T, bmt);
-  }
-  __syncthreads();
-  fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
-  const int e = m.mode == MIMO_SFBC ? l / 14 : l;
-  const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
   const R sc = rx_scale<R>(N);
   const V* pv = MGT<R>::pval(m);
-  if (active && est) {
-    for (int t = 0; t < m.num_tx; ++t)
-      for (int p = tid; p < m.np_tx[t]; p += T)
-        hp[t * m.maxP + p] = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), pv[t * m.maxP + p]);
-  }
+  const size_t br = (size_t)(active ? b : 0) * m.num_rx + rx;
+  const R sigma = active ? sqrt(npow[br] * (R)0.5) : (R)0;
+  const uint64_t fr = active ? fid[b] : 0ull;
+  const R* zf = (inj_z && active) ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+  const V* yf = y + br * g.L;
   __syncthreads();
-  if (active) {
-    V* Yo = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
-    for (int j = tid; j < m.n_dsc; j += T) Yo[j] = cscale(buf[g.data_idx[j]], sc);
-    if (est) {
-      const R* pig = MGT<R>::pig(m);
-      for (int t = 0; t < m.num_tx; ++t) {
-        const V* hpt = hp + t * m.maxP;
-        const int npt = m.np_tx[t];
-        V* Ho = H + ((((size_t)b * m.num_rx + rx) * m.n_est + e) * m.num_tx + t) * m.n_dsc;
-        for (int j = tid; j < m.n_dsc; j += T) {
-          const int sidx = m.pseg[t * m.n_dsc + j];
-          V h;
-          if (sidx < 0) h = hpt[0];
-          else if (sidx >= npt - 1) h = hpt[npt - 1];
-          else {
-            const V v0 = hpt[sidx], v1 = hpt[sidx + 1];
-            const R fk = (R)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
-            const R ig = pig[t * m.maxP + sidx];
-            h = mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+  for (int l = 0; l < g.n_sym; ++l) {
+    int tid = tid0;   // opaque per symbol (see k_rx_frame)
+    asm volatile("" : "+v"(tid));
+    if (active) load_symbol_noisy2<true>(buf, yf, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T, bmt);
+    __syncthreads();
+    fft_lds<false, NC, false, (NC > 0), true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
+    const int e = m.mode == MIMO_SFBC ? l / 14 : l;
+    const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
+    if (active && est) {
+      for (int t = 0; t < m.num_tx; ++t)
+        for (int p = tid; p < m.np_tx[t]; p += T)
+          hp[t * m.maxP + p] = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), pv[t * m.maxP + p]);
+    }
+    __syncthreads();
+    if (active) {
+      V* Yo = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
+      for (int j = tid; j < m.n_dsc; j += T) Yo[j] = cscale(buf[g.data_idx[j]], sc);
+      if (est) {
+        const R* pig = MGT<R>::pig(m);
+        for (int t = 0; t < m.num_tx; ++t) {
+          const V* hpt = hp + t * m.maxP;
+          const int npt = m.np_tx[t];
+          V* Ho = H + (((br * m.n_est + e) * m.num_tx + t)) * m.n_dsc;
+          for (int j = tid; j < m.n_dsc; j += T) {
+            const int sidx = m.pseg[t * m.n_dsc + j];
+            V h;
+            if (sidx < 0) h = hpt[0];
+            else if (sidx >= npt - 1) h = hpt[npt - 1];
+            else {
+              const V v0 = hpt[sidx], v1 = hpt[sidx + 1];
+              const R fk = (R)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
+              const R ig = pig[t * m.maxP + sidx];
+              h = mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+            }
+            Ho[j] = h;
           }
-          Ho[j] = h;
         }
       }
     }
+    __syncthreads();   // buf and hp are rewritten by the next symbol
   }
 }
 
@@ -1712,7 +1768,7 @@ template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
                        const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H) {
   const int spw = MWG / (g.N >> 3);
-  const int64_t total = (int64_t)B * m.num_rx * g.n_sym;
+  const int64_t total = (int64_t)B * m.num_rx;
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(cx<R>);

@@ -934,7 +934,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
   __shared__ R red[TPB / 64];
   // LDS: grids / x_t at [t * N, (t + 1) * N), then [NTX][SFX_TL] the previous
   // symbol's last TL samples of each x_t (one array, so that a delayed sample's
-  // address is one index expression), then the staged coded streams
+  // address is one index expression), the frame's taps [NRX][NTX][PM], then
+  // the staged coded streams
   V* sm = mimo_lds<V>();
   constexpr int TB0 = 2 * N;
   const int tid0 = threadIdx.x, b = blockIdx.x;
@@ -945,8 +946,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
   const int S = N + g.cp, TL = lp.max_delay, np = NP ? NP : lp.n_paths;
   const uint32_t* fb = pw + (size_t)b * PW;
   const uint32_t* fe = enc + (size_t)b * enc_words;
+  // the frame's static taps c_rtp (coef [B][num_rx][num_tx][np][NCF], n_cs = 1)
+  // copied to LDS once; each symbol's sample loop reads them from there
+  V* ct = sm + TB0 + NTX * SFX_TL;
+  for (int i = tid0; i < NRX * NTX * PM; i += TPB) {
+    const int p = i % PM, rt = i / PM;
+    ct[i] = p < np ? lp.coef[(((size_t)b * NRX * NTX + rt) * np + p) * NCF] : mkc((R)0, (R)0);
+  }
   if (CODED && stage_enc) {
-    uint32_t* es = reinterpret_cast<uint32_t*>(sm + TB0 + NTX * SFX_TL);
+    uint32_t* es = reinterpret_cast<uint32_t*>(ct + NRX * NTX * PM);
     for (int i = tid0; i < enc_words; i += TPB) es[i] = fe[i];
     fe = es;
   }
@@ -961,6 +969,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
     for (int t = 0; t < NTX; ++t) pwr[r][t] = (R)0;
   const R sc = tx_scale<R>(N);
   constexpr int SFP = 4 * T / TPB;   // Alamouti pairs per thread per symbol (n_dsc / 2 <= SFP TPB)
+  // (each pair's grid positions held in registers across the symbols instead of
+  // re-read per symbol: 28.06 / 27.77 vs 27.53 / 27.52 ms, the 4 registers spill)
   for (int l = 0; l < g.n_sym; ++l) {
     int tid = tid0;   // opaque per symbol: the FFT's addressing is not hoisted into registers
     asm volatile("" : "+v"(tid));
@@ -1002,22 +1012,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
       if constexpr (TPB == T) fft2_lds<true, NC, true>(sm, sm + N, GridT<R>::tw(g), tid, active, sc);
       else fft_lds<true, NC, true, true>(sm + (tid >= T ? N : 0), N, 0, GridT<R>::tw(g), tid & (T - 1), active, sc);
     }
-    // the frame's static taps c_rtp (coef [B][num_rx][num_tx][np][NCF], n_cs =
-    // 1), loaded per symbol into VGPRs for the sample loop only: as
-    // wave-uniform values the compiler would keep them in SGPRs and spill them
-    // to VGPR lanes inside the loop; held across the FFTs they would crowd them
+    // the taps into VGPRs from LDS for the sample loop only: as wave-uniform
+    // values the compiler would keep them in SGPRs and spill them to VGPR
+    // lanes inside the loop; held across the FFTs they would crowd them
     V c[NRX][NTX][PM];
 #pragma unroll
     for (int r = 0; r < NRX; ++r)
 #pragma unroll
-      for (int t = 0; t < NTX; ++t) {
-        const V* cf = lp.coef + (((size_t)b * NRX + r) * NTX + t) * np * NCF;
+      for (int t = 0; t < NTX; ++t)
 #pragma unroll
         for (int p = 0; p < PM; ++p) {
-          c[r][t][p] = p < np ? cf[p * NCF] : mkc((R)0, (R)0);
+          c[r][t][p] = ct[(r * NTX + t) * PM + p];
           asm volatile("" : "+v"(c[r][t][p].x), "+v"(c[r][t][p].y));
         }
-      }
     V* yl = y + (size_t)b * NRX * g.L + (size_t)l * S;
     for (int n = tid; n < S; n += TPB) {
       if (LTE_SFX_PROBE & 4) {
@@ -1164,7 +1171,8 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
   if (!sfbc_txch_supported<R>(g, m, lp.n_paths, lp.max_delay) || !lp.part) return (int)hipErrorInvalidValue;
   const size_t enc_shm = (size_t)enc_words * sizeof(uint32_t);
   const int stage_enc = coded && enc_shm <= 32768;
-  const size_t shm = (2 * (size_t)g.N + 2 * SFX_TL) * sizeof(cx<R>) + (stage_enc ? enc_shm : 0);
+  const size_t shm = (2 * (size_t)g.N + 2 * SFX_TL + (size_t)m.num_rx * 2 * TXCH_MAXP) * sizeof(cx<R>) +
+                     (stage_enc ? enc_shm : 0);
 #define LTE_SFX(C_, B_, NR_)                                                                                          \
   do {                                                                                                                \
     const int tpb = lp.n_paths == 4 ? LTE_SFX_TPB : MWG;                                                              \

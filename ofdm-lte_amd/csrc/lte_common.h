@@ -644,3 +644,27 @@ __device__ __forceinline__ uint32_t crc24_slice4(const uint32_t* T, uint32_t c, 
 __device__ __forceinline__ uint32_t getbit(const uint32_t* __restrict__ w, int64_t i) {
   return (w[i >> 5] >> (31 - (i & 31))) & 1u;
 }
+// bits [i, i + NB) of an MSB-first stream (NB <= 32), bit i in the result's
+// bit NB - 1: one or two word loads instead of NB single-bit loads.  Word
+// (i >> 5) + 1 is read only when the bits reach into it and it starts before
+// lim (the stream's bit count); bits at or past lim read as 0.
+template <int NB>
+__device__ __forceinline__ uint32_t getbits(const uint32_t* __restrict__ w, int64_t i, int64_t lim) {
+  const int64_t wi = i >> 5;
+  const int sh = (int)(i & 31);
+  uint64_t v = (uint64_t)w[wi] << 32;
+  if (sh + NB > 32 && ((wi + 1) << 5) < lim) v |= w[wi + 1];
+  uint32_t r = (uint32_t)(v >> (64 - sh - NB)) & (uint32_t)((1ull << NB) - 1);
+  if (i + NB > lim) {
+    const int valid = lim > i ? (int)(lim - i) : 0;
+    r &= ~(uint32_t)((1ull << (NB - valid)) - 1);
+  }
+  return r;
+}
+// mask of the first min(max(lim - i, 0), NB) of NB bits (MSB-first, as getbits)
+template <int NB>
+__device__ __forceinline__ uint32_t bits_valid(int64_t i, int64_t lim) {
+  if (i + NB <= lim) return (uint32_t)((1ull << NB) - 1);
+  const int valid = lim > i ? (int)(lim - i) : 0;
+  return (uint32_t)((1ull << NB) - 1) & ~(uint32_t)((1ull << (NB - valid)) - 1);
+}

@@ -322,9 +322,7 @@ __global__ __launch_bounds__(WG) void k_ofdm_tx(Grid g, const uint32_t* __restri
     const uint32_t* fb = pw + (size_t)b * PW;
     for (int j = tid; j < (CODED ? 0 : g.Nd); j += T) {   // uncoded: payload bits in order
       const int64_t t0 = ((int64_t)l * g.Nd + j) * BPS;
-      int idx = 0;
-#pragma unroll
-      for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, t0 + m);
+      const int idx = (int)getbits<BPS>(fb, t0, INT64_MAX);
       const V sym = qam_point<BPS, R>(idx);
       if constexpr (SCF) pre[j] = sym;
       else buf[g.data_idx[j]] = sym;
@@ -1294,14 +1292,11 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
     } else {
       const int idx = hard_index(z, BPS, QS);
       const int64_t pb0 = (int64_t)re * BPS;
+      errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+      if (cap_bits) {
 #pragma unroll
-      for (int m = 0; m < BPS; ++m) {
-        const int64_t pbit = pb0 + m;
-        if (pbit < n_bits) {
-          const uint32_t bit = (idx >> (BPS - 1 - m)) & 1;
-          errs += bit ^ getbit(fb, pbit);
-          if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
-        }
+        for (int m = 0; m < BPS; ++m)
+          if (pb0 + m < n_bits) cap_bits[(size_t)b * n_bits + pb0 + m] = (uint8_t)((idx >> (BPS - 1 - m)) & 1);
       }
     }
   }
@@ -1492,14 +1487,11 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame(Grid g, int rayleigh
         } else {
           const int idx = hard_index(z, BPS, QS);
           const int64_t pb0 = (int64_t)re * BPS;
+          errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+          if (cap_bits) {
 #pragma unroll
-          for (int m = 0; m < BPS; ++m) {
-            const int64_t pbit = pb0 + m;
-            if (pbit < n_bits) {
-              const uint32_t bit = (idx >> (BPS - 1 - m)) & 1;
-              errs += bit ^ getbit(fb, pbit);
-              if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
-            }
+            for (int m = 0; m < BPS; ++m)
+              if (pb0 + m < n_bits) cap_bits[(size_t)b * n_bits + pb0 + m] = (uint8_t)((idx >> (BPS - 1 - m)) & 1);
           }
         }
       }
@@ -1684,14 +1676,11 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo(
         if (cap_syms) cap_syms[fre + re] = z;
         const int idx = hard_index(z, BPS, QS);
         const int64_t pb0 = (int64_t)re * BPS;
+        errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+        if (cap_bits) {
 #pragma unroll
-        for (int m = 0; m < BPS; ++m) {
-          const int64_t pbit = pb0 + m;
-          if (pbit < n_bits) {
-            const uint32_t bit = (idx >> (BPS - 1 - m)) & 1;
-            errs += bit ^ getbit(fb, pbit);
-            if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
-          }
+          for (int m = 0; m < BPS; ++m)
+            if (pb0 + m < n_bits) cap_bits[(size_t)b * n_bits + pb0 + m] = (uint8_t)((idx >> (BPS - 1 - m)) & 1);
         }
       }
     }

@@ -60,8 +60,7 @@ __device__ __forceinline__ int qam_code(int64_t q, const uint32_t* __restrict__ 
       idx = (idx << 1) | (int)(src >= 0 ? getbit(fe, src) : 0u);
     }
   } else {
-#pragma unroll
-    for (int m = 0; m < BPS; ++m) idx = (idx << 1) | (int)getbit(fb, q * BPS + m);
+    idx = (int)getbits<BPS>(fb, q * BPS, INT64_MAX);
   }
   return zero ? -1 : idx;
 }
@@ -1197,7 +1196,10 @@ int launch_link_noise_add(hipStream_t s, const Grid& g, const MimoGrid& m, int B
   const int nl = B * m.num_rx * m.num_tx;   // one partial per link (k_ofdm_txch_sfbc)
   hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, 1, g.L, link_sigma);
   *pow_nblk = 1;
-  hipLaunchKernelGGL((k_link_noise_pairs<R, 4, LTE_BM_LDS != 0>), dim3(B * m.num_rx), dim3(MWG), 0, s, g.L, m.num_rx,
+#ifndef LTE_LN_U   // sample pairs per lane in flight in k_link_noise_pairs (A/B)
+#define LTE_LN_U 8
+#endif
+  hipLaunchKernelGGL((k_link_noise_pairs<R, LTE_LN_U, LTE_BM_LDS != 0>), dim3(B * m.num_rx), dim3(MWG), 0, s, g.L, m.num_rx,
                      m.num_tx, y, link_sigma, fid, seed, pow_part);
   return (int)hipGetLastError();
 }
@@ -1895,13 +1897,13 @@ __global__ __launch_bounds__(MWG) void k_det_sfbc(Grid g, MimoGrid m, int B, con
     uint32_t errs = 0;
     for (int h = 0; h < 2; ++h) {
       const int idx = hard_index(h ? z1 : z0, BPS, (R)qam_norm<BPS>());
+      const int64_t pb0 = (re + h) * BPS;
+      if (act) {
+        errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+        if (cap_bits) {
 #pragma unroll
-      for (int q = 0; q < BPS; ++q) {
-        const int64_t pbit = (re + h) * BPS + q;
-        if (act && pbit < n_bits) {
-          const uint32_t bit = (idx >> (BPS - 1 - q)) & 1;
-          errs += bit ^ getbit(fb, pbit);
-          if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
+          for (int q = 0; q < BPS; ++q)
+            if (pb0 + q < n_bits) cap_bits[(size_t)b * n_bits + pb0 + q] = (uint8_t)((idx >> (BPS - 1 - q)) & 1);
         }
       }
     }
@@ -2166,13 +2168,13 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
     const int64_t re = (int64_t)l * m.res + qi;
     if (cap_syms && act) cap_syms[(size_t)b * g.n_sym * m.res + re] = z;
     const int idx = hard_index(z, BPS, (R)qam_norm<BPS>());
+    const int64_t pb0 = re * BPS;
+    if (act) {
+      errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+      if (cap_bits) {
 #pragma unroll
-    for (int q = 0; q < BPS; ++q) {
-      const int64_t pbit = re * BPS + q;
-      if (act && pbit < n_bits) {
-        const uint32_t bit = (idx >> (BPS - 1 - q)) & 1;
-        errs += bit ^ getbit(fb, pbit);
-        if (cap_bits) cap_bits[(size_t)b * n_bits + pbit] = (uint8_t)bit;
+        for (int q = 0; q < BPS; ++q)
+          if (pb0 + q < n_bits) cap_bits[(size_t)b * n_bits + pb0 + q] = (uint8_t)((idx >> (BPS - 1 - q)) & 1);
       }
     }
   }

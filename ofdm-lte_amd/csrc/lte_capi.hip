@@ -1124,7 +1124,6 @@ static int plan_coded_maps(lte_plan* p) {
       txm[(size_t)re * bps + m] = v;
     }
     // RX: de-interleave (ofdm_core.py:1176-1197) then rate dematch rows
-    int32_t base = -1;
     int qr = -1;
     if (re < rows_rx * Nd) {
       const int c2 = re / rows_rx, r2 = re % rows_rx;
@@ -1145,7 +1144,6 @@ static int plan_coded_maps(lte_plan* p) {
       else if (s.stream == 2) row = (int)trow_lp(K, 2, s.idx);
       if (row >= 0) rxm[(size_t)(i / (3 * (K + 6))) * p->n_re_bits + (size_t)re * bps + m] = (r << 24) | row;
     }
-    (void)base;
   }
   p->qstride = Kmax + 32;
   std::vector<uint16_t> qm((size_t)p->C * p->qstride, 0);
@@ -1730,7 +1728,18 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, npow_nblk, p->L, c.snr_lin.p, sfbc ? (double)m.num_tx : 1.0,
                              c.npow.p));
   }
-  {
+  // config 4 (SFBC on Philox draws, zn handoff or uncoded, no capture of the
+  // received grids / estimates / symbols): receiver + detector in one pass
+  const bool zn0 = coded && sfbc && (d.bps == 4 || d.bps == 6) && !a->cap_llr && (m.res & 1) == 0 &&
+                   m.n_dsc <= m.res && env_on("LTE_DEMAP_IN_DEMATCH", true);
+  const bool rx_fuse = sfbc && !inj_z && !a->cap_H && !a->cap_data_syms && !a->cap_bits_rx && (zn0 || !coded) &&
+                       rx_sfbc_supported<R>(g, m) && env_on("LTE_SFBC_RX_FUSE", true);
+  if (rx_fuse) {
+    Timer t(p, KN_RX_CHEST);
+    LCHK(launch_rx_sfbc<R>(s, g, m, coded ? 1 : 0, B, c.y.p, c.npow.p, p->fid.p, a->seed, c.snr_lin.p, p->pw.p,
+                           p->PW, d.n_bits, p->frame_err.p, coded ? zn_z<R>(p) : nullptr,
+                           coded ? zn_nv<R>(p) : nullptr));
+  } else {
     Timer t(p, KN_RX_CHEST);
     LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p));
   }
@@ -1747,9 +1756,8 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   // coded SFBC 16/64-QAM without an LLR capture: the detector hands over the
   // combined symbols and each RE pair's sigma^2_eff, k_dematch_zn demaps (as
   // the SISO chain does; LTE_DEMAP_IN_DEMATCH=0 keeps the LLR round trip)
-  const bool zn = coded && sfbc && (d.bps == 4 || d.bps == 6) && !a->cap_llr && (m.res & 1) == 0 &&
-                  m.n_dsc <= m.res && env_on("LTE_DEMAP_IN_DEMATCH", true);
-  {
+  const bool zn = zn0;
+  if (!rx_fuse) {
     Timer t(p, KN_RX_DATA);
     if (sfbc)
       LCHK(launch_det_sfbc<R>(s, g, m, coded ? 1 : 0, ray ? 1 : 0, B, c.Ym.p, c.H.p, c.snr_lin.p, p->pw.p, p->PW,

@@ -338,6 +338,15 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
 template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
                        const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H);
+// config 4's receiver + SFBC detector in one pass per frame (k_rx_sfbc): the
+// outputs of launch_rx_fft_mimo + launch_det_sfbc (zn handoff or bit errors)
+// without Y / H in HBM
+template <class R>
+bool rx_sfbc_supported(const Grid& g, const MimoGrid& m);
+template <class R>
+int launch_rx_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int B, const cx<R>* y, const R* npow,
+                   const uint64_t* fid, uint64_t seed, const R* snr_lin, const uint32_t* pw, int PW, int n_bits,
+                   uint32_t* frame_err, cx<R>* zo, R* nvo);
 template <class R>
 // coded: LLRs to llr, or (zo != null) the combined symbols to zo [B][n_sym][res]
 // and sigma^2_eff per RE pair to nvo [B][n_sym][res / 2] for launch_dematch_zn

@@ -1707,6 +1707,21 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
 // interpolation with edge hold (:108-185 + lte_receiver.py:98-133:
 // np.linspace, k (delta / gap) + start) at the data SCs ->
 // H[b][rx][e][tx][n_dsc].
+// TX t's estimate at data SC j from its LS pilot estimates hpt (np_t of them):
+// linear interpolation with edge hold (mimo_channel_estimator_periodic.py:
+// 108-185), the one expression k_rx_fft_mimo and k_rx_sfbc share
+template <class R>
+__device__ __forceinline__ cx<R> mimo_interp(const Grid& g, const MimoGrid& m, const cx<R>* hpt, int npt,
+                                             const R* __restrict__ pig, int t, int j) {
+  const int sidx = m.pseg[t * m.n_dsc + j];
+  if (sidx < 0) return hpt[0];
+  if (sidx >= npt - 1) return hpt[npt - 1];
+  const cx<R> v0 = hpt[sidx], v1 = hpt[sidx + 1];
+  const R fk = (R)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
+  const R ig = pig[t * m.maxP + sidx];
+  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+}
+
 template <class R, int NC = 0>
 __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
                                                      const R* __restrict__ npow, const uint64_t* __restrict__ fid,
@@ -1754,19 +1769,7 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
           const V* hpt = hp + t * m.maxP;
           const int npt = m.np_tx[t];
           V* Ho = H + (((br * m.n_est + e) * m.num_tx + t)) * m.n_dsc;
-          for (int j = tid; j < m.n_dsc; j += T) {
-            const int sidx = m.pseg[t * m.n_dsc + j];
-            V h;
-            if (sidx < 0) h = hpt[0];
-            else if (sidx >= npt - 1) h = hpt[npt - 1];
-            else {
-              const V v0 = hpt[sidx], v1 = hpt[sidx + 1];
-              const R fk = (R)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
-              const R ig = pig[t * m.maxP + sidx];
-              h = mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
-            }
-            Ho[j] = h;
-          }
+          for (int j = tid; j < m.n_dsc; j += T) Ho[j] = mimo_interp<R>(g, m, hpt, npt, pig, t, j);
         }
       }
     }
@@ -1928,6 +1931,139 @@ int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, 
     if (g.bps == 2) LTE_DS(0, 2); else if (g.bps == 4) LTE_DS(0, 4); else LTE_DS(0, 6);
   }
 #undef LTE_DS
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Config 4's receiver and SFBC detector in one pass: one slot per frame walks
+// its OFDM symbols; per symbol each RX in order is loaded with its noise and
+// FFT'd (k_rx_fft_mimo's per-symbol work), on the group's first symbol its LS
+// pilot estimates per TX stay in LDS, and each thread's Alamouti pairs are
+// combined (sfbc_combine with the estimates interpolated at the pair's
+// subcarriers, mimo_interp) and summed over RX in RX order -- k_det_sfbc's
+// arithmetic.  Y and H never go through HBM.  Outputs: the combined symbols and
+// each pair's sigma^2_eff for k_dematch_zn (coded), or the bit errors
+// (uncoded).  N = 2048, one slot per block.
+template <class R, int CODED, int BPS, int NC = 2048>
+__global__ __launch_bounds__(MWG) void k_rx_sfbc(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
+                                                 const R* __restrict__ npow, const uint64_t* __restrict__ fid,
+                                                 uint64_t seed, const R* __restrict__ snr_lin,
+                                                 const uint32_t* __restrict__ pw, int PW, int n_bits,
+                                                 uint32_t* __restrict__ frame_err, cx<R>* __restrict__ zo,
+                                                 R* __restrict__ nvo) {
+  using V = cx<R>;
+  constexpr bool F64 = sizeof(R) == 8;
+  constexpr int N = NC, T = N >> 3, PP = 3;   // Alamouti pairs per thread: n_dsc / 2 <= PP T
+  static_assert(T == MWG, "one slot per block");
+  V* sm = mimo_lds<V>();
+  V* buf = sm;
+  V* hpa = sm + N;   // [num_rx][num_tx][maxP] LS pilot estimates of the current group
+  LTE_BM_LDS_DECL(R);
+  const auto bmt = bm_stage<R>(lte_bmt);
+  const int b = blockIdx.x, tid0 = threadIdx.x;
+  const bool active = b < B;   // (grid = B blocks)
+  const int npair = m.n_dsc >> 1;
+  const R sc = rx_scale<R>(N);
+  const V* pv = MGT<R>::pval(m);
+  const R* pig = MGT<R>::pig(m);
+  const uint64_t fr = fid[b];
+  const R s2 = (R)1 / snr_lin[b];
+  const R ir = (R)1 / (R)m.num_rx;
+  uint32_t errs = 0;
+  __syncthreads();
+  for (int l = 0; l < g.n_sym; ++l) {
+    const bool est = (l % 14) == 0;
+    V z[PP][2];
+    R inv_g[PP];
+#pragma unroll
+    for (int k = 0; k < PP; ++k) {
+      z[k][0] = z[k][1] = mkc((R)0, (R)0);
+      inv_g[k] = (R)0;
+    }
+    for (int rx = 0; rx < m.num_rx; ++rx) {
+      int tid = tid0;   // opaque per pass (see k_rx_frame)
+      asm volatile("" : "+v"(tid));
+      const size_t br = (size_t)b * m.num_rx + rx;
+      const R sigma = sqrt(npow[br] * (R)0.5);
+      load_symbol_noisy2<true>(buf, y + br * g.L, N, g.cp, l, sigma, seed, fr, rx, (const R*)nullptr, g.L, tid, T,
+                               bmt);
+      __syncthreads();
+      fft_lds<false, NC, false, true, true>(buf, N, g.log2N, GridT<R>::tw(g), tid, active);
+      V* hp = hpa + rx * (m.num_tx * m.maxP);
+      if (est) {
+        for (int t = 0; t < m.num_tx; ++t)
+          for (int p = tid; p < m.np_tx[t]; p += T)
+            hp[t * m.maxP + p] = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), pv[t * m.maxP + p]);
+        __syncthreads();
+      }
+#pragma unroll
+      for (int k = 0; k < PP; ++k) {
+        const int pr = tid + k * T;
+        if (pr >= npair) break;
+        const int j = 2 * pr;
+        const V Y0 = cscale(buf[g.data_idx[j]], sc), Y1 = cscale(buf[g.data_idx[j + 1]], sc);
+        const V h0k = mimo_interp<R>(g, m, hp, m.np_tx[0], pig, 0, j);
+        const V h1k = mimo_interp<R>(g, m, hp + m.maxP, m.np_tx[1], pig, 1, j);
+        const V h0k1 = mimo_interp<R>(g, m, hp, m.np_tx[0], pig, 0, j + 1);
+        const V h1k1 = mimo_interp<R>(g, m, hp + m.maxP, m.np_tx[1], pig, 1, j + 1);
+        V d0, d1;
+        const R nrm = sfbc_combine<R>(Y0, Y1, h0k, h1k, h0k1, h1k1, (R)1e-10, d0, d1);
+        z[k][0] = cadd(z[k][0], d0);
+        z[k][1] = cadd(z[k][1], d1);
+        if constexpr (F64) inv_g[k] += 1.0 / fmin(fmax(nrm, 1e-6), 1e6);
+        else inv_g[k] += 1.0f / fminf(fmaxf(nrm, 1e-6f), 1e6f);
+      }
+      __syncthreads();   // buf (and on estimate symbols hp) rewritten by the next pass
+    }
+#pragma unroll
+    for (int k = 0; k < PP; ++k) {
+      const int pr = tid0 + k * T;
+      if (pr >= npair) break;
+      const int j = 2 * pr;
+      const V z0 = mkc(z[k][0].x * ir, z[k][0].y * ir), z1 = mkc(z[k][1].x * ir, z[k][1].y * ir);
+      const int64_t re = (int64_t)l * m.res + j;
+      if constexpr (CODED) {
+        const R nv = F64 ? fmax((s2 / (R)(m.num_rx * m.num_rx)) * inv_g[k], s2 / (R)4)
+                         : fmax(s2 * ir * ir * inv_g[k], s2 * (R)0.25);
+        zo[(size_t)b * g.n_sym * m.res + re] = z0;
+        zo[(size_t)b * g.n_sym * m.res + re + 1] = z1;
+        nvo[(size_t)b * g.n_sym * (m.res >> 1) + (size_t)l * (m.res >> 1) + pr] = nv;
+      } else {
+        const uint32_t* fb = pw + (size_t)b * PW;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int idx = hard_index(h ? z1 : z0, BPS, (R)qam_norm<BPS>());
+          const int64_t pb0 = (re + h) * BPS;
+          errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+        }
+      }
+    }
+  }
+  if constexpr (!CODED) frame_err_add(frame_err, b, errs);
+}
+
+template <class R>
+bool rx_sfbc_supported(const Grid& g, const MimoGrid& m) {
+  return m.mode == MIMO_SFBC && m.num_tx == 2 && m.num_rx >= 1 && m.num_rx <= 4 && g.N == 2048 &&
+         (m.n_dsc >> 1) <= 3 * (g.N >> 3) && (m.res & 1) == 0 && m.n_dsc <= m.res && m.n_est == (g.n_sym + 13) / 14 &&
+         (g.bps == 2 || g.bps == 4 || g.bps == 6);
+}
+
+template <class R>
+int launch_rx_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, int B, const cx<R>* y, const R* npow,
+                   const uint64_t* fid, uint64_t seed, const R* snr_lin, const uint32_t* pw, int PW, int n_bits,
+                   uint32_t* frame_err, cx<R>* zo, R* nvo) {
+  if (!rx_sfbc_supported<R>(g, m) || (coded && (!zo || !nvo))) return (int)hipErrorInvalidValue;
+  const size_t shm = ((size_t)g.N + (size_t)m.num_rx * m.num_tx * m.maxP) * sizeof(cx<R>);
+#define LTE_RS(C_, B_)                                                                                        \
+  hipLaunchKernelGGL((k_rx_sfbc<R, C_, B_>), dim3(B), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, snr_lin, pw, \
+                     PW, n_bits, frame_err, zo, nvo)
+  if (coded) {
+    if (g.bps == 2) LTE_RS(1, 2); else if (g.bps == 4) LTE_RS(1, 4); else LTE_RS(1, 6);
+  } else {
+    if (g.bps == 2) LTE_RS(0, 2); else if (g.bps == 4) LTE_RS(0, 4); else LTE_RS(0, 6);
+  }
+#undef LTE_RS
   return (int)hipGetLastError();
 }
 
@@ -2306,6 +2442,10 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
   template int launch_npow_mimo<R>(hipStream_t, int, int, const R*, int, int, const R*, double, R*);               \
   template int launch_rx_fft_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const R*,       \
                                      const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*);                \
+  template bool rx_sfbc_supported<R>(const Grid&, const MimoGrid&);                                                \
+  template int launch_rx_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const cx<R>*, const R*,      \
+                                 const uint64_t*, uint64_t, const R*, const uint32_t*, int, int, uint32_t*, cx<R>*,  \
+                                 R*);                                                                              \
   template int launch_det_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, int, const cx<R>*,          \
                                   const cx<R>*, const R*, const uint32_t*, int, int, uint32_t*, R*, cx<R>*,        \
                                   uint8_t*, cx<R>*, R*);                                                           \

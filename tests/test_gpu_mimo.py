@@ -258,6 +258,38 @@ def test_sfbc_txch_fused_matches_separate_kernels(C, prec, coded, nrx, monkeypat
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('coded,nrx,chan', [(True, 2, 'rayleigh_mp'), (False, 2, 'rayleigh_mp'),
+                                            (False, 1, 'rayleigh_mp'), (True, 2, 'awgn'), (False, 2, 'awgn')])
+def test_sfbc_rx_fused_matches_separate_kernels(C, prec, coded, nrx, chan, monkeypatch):
+    """Config 4's receiver and SFBC detector in one pass per frame (k_rx_sfbc,
+    default when nothing captures Y / H / the symbols) against k_rx_fft_mimo +
+    k_det_sfbc through HBM (LTE_SFBC_RX_FUSE=0): the same operations per
+    subcarrier pair (mimo_interp, sfbc_combine, the RX sum in RX order), so
+    identical per-frame bit errors and CRC verdicts, coded (the demapper's
+    inputs) and uncoded, 1 and 2 RX, Rayleigh and flat links (float32: the
+    north_star 1e-3 and identical CRC verdicts)."""
+    sim = _sim(20.0, '64-QAM', chan, prec)
+    plan = (sim._sfbc_plan(0, 27760, nrx, coded=True, max_frames=7) if coded else
+            sim._sfbc_plan(14, 14 * 998 * 6, nrx, max_frames=7))
+    snrs = np.array([6.0, 10.0, 14.0, 16.0, 18.0, 22.0, 30.0])
+    outs = []
+    for fuse in ('1', '0'):
+        monkeypatch.setenv('LTE_SFBC_RX_FUSE', fuse)
+        outs.append(plan.run(snrs, seed=31, frame_id0=4242))
+    a, b = outs
+    if coded:
+        assert np.array_equal(a['crc_ok'], b['crc_ok'])
+    assert 0 < int(a['counts'][:, 0].sum())
+    if prec == 'f64':
+        assert np.array_equal(a['frame_errors'], b['frame_errors'])
+        assert np.array_equal(a['counts'], b['counts'])
+    else:   # float32: the compiler contracts other products into FMAs in the fused kernel
+        nb = 27760 if coded else 14 * 998 * 6
+        assert np.max(np.abs(a['frame_errors'].astype(np.int64) - b['frame_errors'])) / nb < 1e-3
+        assert np.array_equal(a['frame_errors'] == 0, b['frame_errors'] == 0)
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mimo,coded,chan', [('sfbc', True, 'rayleigh_mp'), ('spatial', False, 'rayleigh_mp'),
                                             ('spatial', False, 'awgn')])
 def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan, prec):
@@ -326,7 +358,10 @@ def test_sfbc_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
     sigma^2_eff to k_dematch_zn (which runs the same max-log demapper while it
     builds the decoder rows) decodes exactly like the LLR round trip
     (k_det_sfbc LLRs -> k_dematch): identical per-frame bit errors, CRC flags
-    and counts on the same Philox frames, over more than one decoder group."""
+    and counts on the same Philox frames, over more than one decoder group
+    (both through k_det_sfbc: LTE_SFBC_RX_FUSE=0; the fused receiver has its
+    own test)."""
+    monkeypatch.setenv('LTE_SFBC_RX_FUSE', '0')
     sim = _sim(20.0, mod, 'rayleigh_mp', prec)
     B = 64 + 7
     plan = sim._sfbc_plan(0, 27760 if mod == '64-QAM' else 18000, 2, coded=True, max_frames=B)

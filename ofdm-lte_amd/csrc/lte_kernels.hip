@@ -1688,6 +1688,115 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo(
   frame_err_add(frame_err, b, errs);
 }
 
+// k_rx_frame_simo with the receive antennas in pairs (N = 1024, an even
+// number of RX, no capture of H / pilot statistics): one frame per 256-thread
+// block; each half loads and transforms one RX of the pair (RX 2p + h) into
+// its own buffer, then every thread folds both into its REs' MRC sums in RX
+// order -- the same operations per RE as k_rx_frame_simo, with half the
+// passes (and barriers) per symbol.
+template <class R, int BPS, int NC>
+__global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo2(
+    Grid g, int B, int num_rx, const cx<R>* __restrict__ y, int64_t y_rx_stride, int64_t y_frame_stride,
+    const R* __restrict__ npow, const uint64_t* __restrict__ fid, uint64_t seed, const R* __restrict__ inj_z,
+    int64_t inj_stride, const uint32_t* __restrict__ pw, int PW, int n_bits, uint32_t* __restrict__ frame_err,
+    cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+  using V = cx<R>;
+  using G = GridT<R>;
+  constexpr int N = NC, T = N >> 3;
+  static_assert(2 * T == WG, "one frame per block, one RX per half");
+  V* sm = dyn_lds<V>();
+  const int half = threadIdx.x / T, th = threadIdx.x % T, tid0 = threadIdx.x;
+  const int b = blockIdx.x;
+  V* bufs = sm;                  // [2][N]
+  V* hpa = sm + 2 * N;           // [RXS_MAXRX][Np] pilot LS estimates of the current group
+  const R sc = rx_scale<R>(N);
+  constexpr R QS = (R)qam_norm<BPS>();
+  constexpr int QM = 2;   // data REs per thread (Nd < N/2 = QM WG)
+  const uint64_t fr = fid[b];
+  const V* yf = y + (size_t)b * y_frame_stride;
+  const uint32_t* fb = pw + (size_t)b * PW;
+  const size_t fre = (size_t)b * g.n_sym * g.Nd;
+  int kpos[QM], sg[QM];
+  R fk[QM], ig[QM];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {   // chest_interp's per-subcarrier terms
+    const int j = tid0 + q * WG;
+    kpos[q] = j < g.Nd ? g.data_idx[j] : 0;
+    sg[q] = g.seg[kpos[q]];
+    const int sc_ = sg[q] < 0 ? 0 : (sg[q] >= g.Np - 1 ? g.Np - 1 : sg[q]);
+    fk[q] = (R)(kpos[q] - g.pilot_idx[sc_]);
+    ig[q] = GridT<R>::inv_gap(g)[sc_];
+  }
+  R den[QM];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) den[q] = (R)0;
+  uint32_t errs = 0;
+  LTE_BM_LDS_DECL(R);
+  const auto bmt = bm_stage<R>(lte_bmt);
+  __syncthreads();
+  for (int l = 0; l < g.n_sym; ++l) {
+    const bool est = l % 14 == 0;
+    V num[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) num[q] = mkc((R)0, (R)0);
+    if (est) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) den[q] = (R)0;
+    }
+    for (int r0 = 0; r0 < num_rx; r0 += 2) {
+      int tid = th;   // opaque per pass (see k_rx_frame)
+      asm volatile("" : "+v"(tid));
+      const int rx = r0 + half;
+      V* buf = bufs + half * N;
+      {
+        const R sigma = sqrt(npow[(size_t)b * num_rx + rx] / (R)2);
+        const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+        load_symbol_noisy2<true>(buf, yf + rx * y_rx_stride, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T, bmt);
+      }
+      __syncthreads();
+      fft_lds<false, NC, false, true, true>(buf, N, g.log2N, G::tw(g), tid, true);
+      if (est) {   // this RX's group estimate from the group's first symbol (lte_receiver.py:360-411)
+        V* hp = hpa + rx * g.Np;
+        for (int p = tid; p < g.Np; p += T) hp[p] = cdiv(cscale(buf[g.pilot_idx[p]], sc), G::pilots(g)[p]);
+        __syncthreads();
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {   // the pair's RX in order
+        const V* bu = bufs + u * N;
+        const V* hp = hpa + (r0 + u) * g.Np;
+#pragma unroll
+        for (int q = 0; q < QM; ++q) {
+          const int j = tid0 + q * WG;
+          if (j < g.Nd) {
+            const V h = interp_seg<R>(hp, g.Np, sg[q], fk[q], ig[q]);
+            if (est) den[q] += abs2_ref(h);
+            num[q] = cadd(num[q], cmulc(cscale(bu[kpos[q]], sc), h));
+          }
+        }
+      }
+      __syncthreads();   // every read of both buffers done before the next pair / symbol lands in them
+    }
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = tid0 + q * WG;
+      if (j >= g.Nd) continue;
+      const int re = l * g.Nd + j;
+      const R rr = (R)1 / (den[q] + (R)1e-10);
+      const V z = mkc(num[q].x * rr, num[q].y * rr);
+      if (cap_syms) cap_syms[fre + re] = z;
+      const int idx = hard_index(z, BPS, QS);
+      const int64_t pb0 = (int64_t)re * BPS;
+      errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+      if (cap_bits) {
+#pragma unroll
+        for (int m = 0; m < BPS; ++m)
+          if (pb0 + m < n_bits) cap_bits[(size_t)b * n_bits + pb0 + m] = (uint8_t)((idx >> (BPS - 1 - m)) & 1);
+      }
+    }
+  }
+  frame_err_add(frame_err, b, errs);
+}
+
 bool rx_frame_simo_supported(const Grid& g, int num_rx) {
   return num_rx >= 2 && num_rx <= RXS_MAXRX && (g.bps == 2 || g.bps == 4 || g.bps == 6) && 2 * g.Nd < g.N;
 }
@@ -1698,6 +1807,16 @@ int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const 
                          int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
                          cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats) {
   if (!rx_frame_simo_supported(g, num_rx)) return (int)hipErrorInvalidValue;
+  const char* pe = std::getenv("LTE_RXS_PAIRS");   // 0: one slot per frame with T threads, the RX in sequence (A/B)
+  if (g.N == 1024 && (num_rx & 1) == 0 && !H && !pstats && g.Nd <= 2 * WG && (!pe || std::atoi(pe) != 0)) {
+    const size_t shm2 = (2 * (size_t)g.N + RXS_MAXRX * g.Np) * sizeof(cx<R>);
+#define LTE_RXS2(BPS_)                                                                                               \
+  hipLaunchKernelGGL((k_rx_frame_simo2<R, BPS_, 1024>), dim3(B), dim3(WG), shm2, s, g, B, num_rx, y, y_rx_stride,    \
+                     y_frame_stride, npow, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, cap_syms, cap_bits)
+    if (g.bps == 2) LTE_RXS2(2); else if (g.bps == 4) LTE_RXS2(4); else LTE_RXS2(6);
+#undef LTE_RXS2
+    return (int)hipGetLastError();
+  }
   const int spw = WG / (g.N >> 3);
   const int blocks = (B + spw - 1) / spw;
   const size_t shm = (size_t)spw * (g.N + RXS_MAXRX * g.Np) * sizeof(cx<R>);

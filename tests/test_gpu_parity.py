@@ -499,6 +499,37 @@ def test_fused_simo_receiver_matches_separate_kernels(C, monkeypatch, bw, mod, n
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('nrx,mod', [(4, '16-QAM'), (2, '64-QAM'), (4, 'QPSK')])
+def test_simo_receiver_rx_pairs_match_sequential(C, monkeypatch, nrx, mod, prec):
+    """10 MHz SIMO MRC: k_rx_frame_simo2 (one frame per block, the RX in pairs,
+    each half of the block transforming one RX of the pair, the MRC sums in
+    RX order) against k_rx_frame_simo (the RX in sequence, LTE_RXS_PAIRS=0):
+    the same operations per RE, so identical combined symbols, received bits
+    and counts on the same Philox frames (float64; float32 to round-off)."""
+    import lte_phy
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=10.0, modulation=mod), channel_type='rayleigh_mp',
+                                itu_profile='Vehicular_A', precision=prec)
+    B = 64 + 3
+    bps = sim.config.bits_per_symbol
+    plan = sim._plan(C.CHAIN_SIMO, 14, 14 * sim.Nd * bps - 5, num_rx=nrx, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('data_syms', 'bits_rx')
+    runs = {}
+    for pairs in ('0', '1'):
+        monkeypatch.setenv('LTE_RXS_PAIRS', pairs)
+        runs[pairs] = plan.run(snr, seed=0x5EED, frame_id0=77, capture=cap)
+    a, b = runs['0'], runs['1']
+    if prec == 'f64':
+        assert np.array_equal(a['data_syms'], b['data_syms'])
+        assert np.array_equal(a['bits_rx'], b['bits_rx'])
+        assert np.array_equal(a['counts'], b['counts'])
+    else:
+        assert np.max(np.abs(b['data_syms'] - a['data_syms'])) <= 1e-5 * np.max(np.abs(a['data_syms']))
+        assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 2
+    assert 0 < int(b['counts'][:, 0].sum())
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('bw,mod', [(20.0, '64-QAM'), (5.0, '16-QAM'), (10.0, 'QPSK')])
 def test_frame_tx_matches_symbol_tx(C, monkeypatch, bw, mod, prec):
     """Coded TX + channel with one slot per frame (k_ofdm_txf, coded streams

@@ -1288,8 +1288,12 @@ static bool alloc_mimo(lte_plan* p, bool coded) {
     bad |= c.link_part.alloc(B * links * p->nblk) != 0;
     bad |= c.link_sigma.alloc(B * links) != 0;
   }
-  bad |= c.Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
-  bad |= c.H.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
+  // received grids and estimates: SFBC allocates them on the first run that
+  // takes the separate receiver + detector (k_rx_sfbc never uses them)
+  if (m.mode != MIMO_SFBC) {
+    bad |= c.Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
+    bad |= c.H.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
+  }
   if (ray) {
     std::vector<R> gh(d.gains, d.gains + d.n_paths);
     bad |= upload(c.gains, gh) != 0;
@@ -1740,6 +1744,9 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                            p->PW, d.n_bits, p->frame_err.p, coded ? zn_z<R>(p) : nullptr,
                            coded ? zn_nv<R>(p) : nullptr));
   } else {
+    if (c.Ym.alloc((size_t)d.max_frames * p->n_sym * m.num_rx * m.n_dsc) ||
+        c.H.alloc((size_t)d.max_frames * m.num_rx * m.n_est * m.num_tx * m.n_dsc))
+      return fail(LTE_ENOMEM, "received grids / estimates");
     Timer t(p, KN_RX_CHEST);
     LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p));
   }

@@ -156,7 +156,7 @@ template <class R, bool TV, int NP = 0>
 __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxChannelT<R>& ch, int b, int l, int slot,
                                            int tid, int T, bool active, R sc) {
   using V = cx<R>;
-  __shared__ R red[WG / 64];
+  __shared__ R red[2 * WG / 64];   // (k_ofdm_txf<.., SP = 2>: 512 threads)
   constexpr bool F64 = sizeof(R) == 8;
   const int N = g.N, cp = g.cp, S = N + cp, D = ch.max_delay;
   if (active && D > 0) {   // the TX samples x at both ends of the symbol (every RX's taps read them)
@@ -483,8 +483,12 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
 // carries RE txf_re[l][s] and reads its coded-bit sources from the slot-ordered
 // copy of tx_map (txf_map[l][s][m]), chosen on the host so that the 32 lanes of
 // each ds_read_b32 gather hit distinct LDS banks; null: slot s = RE s.
-template <class R, int BPS, int NC = 0, bool TV = false, int NP = 0>
-__global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32_t* __restrict__ enc, int enc_words,
+// SP = 2 (N = 2048): a 512-thread block per frame whose halves transform
+// symbols 2s and 2s + 1 side by side, sharing one LDS copy of the coded
+// streams (the symbols of a frame are independent here: the taps' reach into
+// the previous symbol is k_chan_fix's).
+template <class R, int BPS, int NC = 0, bool TV = false, int NP = 0, int SP = 1>
+__global__ __launch_bounds__(WG * SP, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32_t* __restrict__ enc, int enc_words,
                                                           const int32_t* __restrict__ tx_map,
                                                           const int32_t* __restrict__ txf_map,
                                                           const int32_t* __restrict__ txf_re, int B,
@@ -492,23 +496,26 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
   using V = cx<R>;
   using G = GridT<R>;
   V* sm = dyn_lds<V>();
-  const int N = NC ? NC : g.N, T = N >> 3, spw = WG / T;
-  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;
-  const int b = blockIdx.x * spw + slot;
-  const bool active = slot < spw && b < B;
+  static_assert(SP == 1 || NC == 2048, "symbol pairs: one frame per block");
+  const int N = NC ? NC : g.N, T = N >> 3, spw = SP == 1 ? WG / T : 1;
+  const int slot = threadIdx.x / T, tid0 = threadIdx.x % T;   // SP = 2: slot = the half
+  const int b = SP == 1 ? blockIdx.x * spw + slot : blockIdx.x;
+  const bool fa = SP == 1 ? slot < spw && b < B : b < B;
   V* buf = sm + slot * N;
 #if TXF_STAGE
-  uint32_t* es = reinterpret_cast<uint32_t*>(sm + spw * N) + slot * enc_words;
-  if (active) {
+  uint32_t* es = reinterpret_cast<uint32_t*>(sm + (SP == 1 ? spw : 2) * N) + (SP == 1 ? slot * enc_words : 0);
+  if (fa) {
     const uint32_t* fe = enc + (size_t)b * enc_words;
-    for (int i = tid0; i < enc_words; i += T) es[i] = fe[i];
+    for (int i = SP == 1 ? tid0 : (int)threadIdx.x; i < enc_words; i += SP == 1 ? T : 2 * T) es[i] = fe[i];
   }
 #else
-  const uint32_t* es = enc + (size_t)(active ? b : 0) * enc_words;
+  const uint32_t* es = enc + (size_t)(fa ? b : 0) * enc_words;
 #endif
   const R sc = tx_scale<R>(N);
   constexpr int QM = 4;   // Nd < N/2 = QM * T for every LTE profile
-  for (int l = 0; l < g.n_sym; ++l) {
+  for (int l0 = 0; l0 < g.n_sym; l0 += SP) {
+    const int l = l0 + (SP == 1 ? 0 : slot);
+    const bool active = fa && l < g.n_sym;
     int tid = tid0;   // opaque per symbol: address arithmetic is not hoisted out of the loop
     asm volatile("" : "+v"(tid));
     int srcs[QM][BPS];
@@ -576,6 +583,20 @@ __global__ __launch_bounds__(WG, TXF_WAVES) void k_ofdm_txf(Grid g, const uint32
   }
 }
 
+#ifndef LTE_TXF_SP   // symbols per pass of k_ofdm_txf's float64 PedA instance (1 or 2)
+#define LTE_TXF_SP 2
+#endif
+// k_ofdm_txf's compile-time-path-count instance (N = 2048): SP = 2 takes one
+// 512-thread block per frame and 64 KB + the staged streams of LDS
+template <class R, int BPS, int SP>
+static void txf_peda_launch(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map,
+                            const int32_t* txf_map, const int32_t* txf_re, int B, cx<R>* cap_syms,
+                            const TxChannelT<R>& ch, int blocks, size_t shm, size_t shm2) {
+  auto k = k_ofdm_txf<R, BPS, 2048, false, 4, SP>;
+  if (SP == 2) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm2);
+  hipLaunchKernelGGL(k, dim3(SP == 2 ? B : blocks), dim3(WG * SP), SP == 2 ? shm2 : shm, s, g, enc, enc_words, tx_map,
+                     txf_map, txf_re, B, cap_syms, ch);
+}
 template <class R>
 int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map,
                     const int32_t* txf_map, const int32_t* txf_re, int B, cx<R>* cap_syms,
@@ -584,6 +605,8 @@ int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_w
   if (!txch_supported(g, ch.n_paths, ch.max_delay) || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
   const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + (TXF_STAGE ? (size_t)spw * enc_words * sizeof(uint32_t) : 0);
   if (shm > 65536) return (int)hipErrorInvalidValue;
+  // symbol pairs (LTE_TXF_SP = 2): two grids and one staged copy per frame
+  const size_t shm2 = 2 * (size_t)g.N * sizeof(cx<R>) + (TXF_STAGE ? (size_t)enc_words * sizeof(uint32_t) : 0);
   const int blocks = (B + spw - 1) / spw;
 #define LTE_TXF(BPS_, NC_)                                                                                      \
   do {                                                                                                          \
@@ -591,8 +614,8 @@ int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_w
       hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_, true>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words,   \
                          tx_map, txf_map, txf_re, B, cap_syms, ch);                              \
     else if (NC_ == 2048 && ch.n_paths == 4 && sizeof(R) == 8)                                                  \
-      hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_, false, 4>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, \
-                         tx_map, txf_map, txf_re, B, cap_syms, ch);                              \
+      txf_peda_launch<R, BPS_, NC_ == 2048 ? LTE_TXF_SP : 1>(s, g, enc, enc_words, tx_map, txf_map, txf_re, B,     \
+                                                            cap_syms, ch, blocks, shm, shm2);                   \
     else                                                                                                        \
       hipLaunchKernelGGL((k_ofdm_txf<R, BPS_, NC_>), dim3(blocks), dim3(WG), shm, s, g, enc, enc_words, tx_map, \
                          txf_map, txf_re, B, cap_syms, ch);                                      \

@@ -1691,7 +1691,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                          env_on("LTE_MIMO_FLAT_FUSE", true);
   // config 4 (SFBC, static-tap Rayleigh links with the 100 dB link noise, Philox
   // draws): TX and the links' fading in one pass per frame writing the faded RX
-  // signals (k_ofdm_txch_sfbc), then the link noise + RX power (k_link_noise_add)
+  // signals (k_ofdm_txch_sfbc), then the link noise + RX power (k_link_noise_pairs)
   // -- x never goes through HBM.  Captures of x / the link statistics and the
   // reference's own (injected) link noise keep the separate kernels.
   int npow_nblk = nch;   // RX power partials per (frame, RX) that k_npow_mimo sums

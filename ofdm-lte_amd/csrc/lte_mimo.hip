@@ -912,7 +912,7 @@ __global__ void k_link_sigma(int n_links_total, const R* __restrict__ part, int 
 // link noise's standard deviation, k_link_sigma).  y0 goes to HBM once; the
 // TX streams x never do.  k_link_noise_pairs then adds the link noise and forms
 // the RX power partials.  Static taps only (n_cs = 1), N = 2048 (two 32 KB
-// grids: two slots per CU).
+// grids and the staged streams: two slots per CU, each of TPB threads).
 constexpr int SFX_TL = 32;   // largest max_delay (samples) the kept tails cover
 // timing probes for A/B builds only (wrong results): bit 0 skips the Alamouti
 // mapping, bit 1 the IFFTs, bit 2 the link taps (y = x_0 + x_1 at n)

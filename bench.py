@@ -391,6 +391,8 @@ def roofline(config, prec, tim, steps, F, el, value, world, iters=8, plan=None):
         roof = turbo_roofline(prec, tim, F, iters)
         t_ms = tim.get('turbo', (0.0, 0))[0]
         roof['turbo_share_of_step'] = round(t_ms / (el * 1e3) if el > 0 else 0, 3)
+        if config == 4:
+            roof['front_end'] = front_end(prec, tim, F, 4)
         if config == 2:
             esz = 8 if prec == 'f64' else 4
             roof['front_end'] = front_end(prec, tim, F)
@@ -447,29 +449,51 @@ def merge_timers(all_tim):
 # front-end stages (bench timers) -> their kernels in the committed PMC summary
 FE_KERNELS = {'payload': ['k_payload'], 'encode': ['k_encode'], 'ofdm_tx': ['k_ofdm_txf'],
               'rx_data': ['k_rx_frame'], 'dematch': ['k_dematch_zn'], 'crc_count': ['k_crc_count']}
+FE_KERNELS_C4 = {'payload': ['k_payload'], 'encode': ['k_encode'], 'ofdm_tx': ['k_ofdm_txch_sfbc'],
+                 'channel': ['k_link_noise_pairs'], 'rx_chest': ['k_rx_sfbc'], 'dematch': ['k_dematch_zn'],
+                 'crc_count': ['k_crc_count']}
 
 
-def front_end(prec, tim, F):
+def front_end(prec, tim, F, config=2):
     """Per front-end stage: its HIP-event time per launch, the HBM bytes per
     frame its kernels move (profiles/r3_pmc_<prec>.json, rocprofv3 FETCH_SIZE /
     WRITE_SIZE, gfx950-corrected) and the resulting rate against the 8 TB/s
     peak, plus the VALU / LDS shares of active issue from the same PMC passes
     (what bounds the FFT / noise kernels, which are not HBM-bound)."""
-    pmc = load_profile(f'r3_pmc_{prec}.json') or load_profile(f'r2_pmc_{prec}.json')
+    # the newest committed summary of the config-2 chain in this precision
+    # (kernel keys carry their template arguments since round 4)
+    pmc, used = None, None
+    names = [f'r5_pmc_c{config}_final.json'] if prec == 'f64' else []
+    if config == 2:
+        names += [f'r3_pmc_{prec}.json', f'r2_pmc_{prec}.json']
+    for name in names:
+        pmc = load_profile(name)
+        if pmc:
+            used = name
+            break
     if not pmc:
         return None
     ks = pmc['kernels']
+
+    def find(name):   # exact key, or the instance '<name><template args>' that ran
+        if name in ks:
+            return ks[name]
+        hits = [v for k, v in ks.items() if k.startswith(name + '<')]
+        return max(hits, key=lambda v: v.get('ms', 0)) if hits else None
+
     out = {}
-    for stage, names in FE_KERNELS.items():
+    for stage, names in (FE_KERNELS_C4 if config == 4 else FE_KERNELS).items():
         t_ms, n = tim.get(stage, (0.0, 0))
-        if not n or not all(k in ks for k in names):
+        rows = [find(k) for k in names]
+        if not n or not all(rows):
             continue
-        b = sum(ks[k]['hbm_bytes_per_frame'] for k in names)
+        b = sum(r['hbm_bytes_per_frame'] for r in rows)
         gbs = b * F / (t_ms / n * 1e-3) / 1e9
-        share = ks[names[0]].get('share_of_active_issue', {})
+        share = rows[0].get('share_of_active_issue', {})
         out[stage] = {'kernels': names, 'ms': round(t_ms / n, 3), 'hbm_bytes_per_frame': round(b),
                       'achieved_GBs': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 3),
-                      'valu_share': share.get('valu'), 'lds_share': share.get('lds')}
+                      'valu_share': share.get('valu'), 'lds_share': share.get('lds'),
+                      'pmc_source': 'profiles/' + used}
     return out
 
 

@@ -1289,10 +1289,11 @@ static bool alloc_mimo(lte_plan* p, bool coded) {
     bad |= c.link_sigma.alloc(B * links) != 0;
   }
   // received grids and estimates: SFBC allocates them on the first run that
-  // takes the separate receiver + detector (k_rx_sfbc never uses them)
+  // takes the separate receiver + detector (k_rx_sfbc never uses them);
+  // spatial holds the pilot estimates (maxP per TX) until a run captures H
   if (m.mode != MIMO_SFBC) {
     bad |= c.Ym.alloc(B * p->n_sym * m.num_rx * m.n_dsc) != 0;
-    bad |= c.H.alloc(B * m.num_rx * m.n_est * m.num_tx * m.n_dsc) != 0;
+    bad |= c.H.alloc(B * m.num_rx * m.n_est * m.num_tx * std::min(m.maxP, m.n_dsc)) != 0;
   }
   if (ray) {
     std::vector<R> gh(d.gains, d.gains + d.n_paths);
@@ -1738,6 +1739,11 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                    m.n_dsc <= m.res && env_on("LTE_DEMAP_IN_DEMATCH", true);
   const bool rx_fuse = sfbc && !inj_z && !a->cap_H && !a->cap_data_syms && !a->cap_bits_rx && (zn0 || !coded) &&
                        rx_sfbc_supported<R>(g, m) && env_on("LTE_SFBC_RX_FUSE", true);
+  // spatial multiplexing without a capture of H: the receiver hands over each
+  // estimation symbol's LS pilot estimates and the detector interpolates them
+  // per RE (the same mimo_interp), instead of a round trip of the interpolated
+  // H (num_tx x n_dsc per RX and symbol) through HBM
+  const bool h_pilots = !sfbc && !a->cap_H && env_on("LTE_SPATIAL_HP", true);
   if (rx_fuse) {
     Timer t(p, KN_RX_CHEST);
     LCHK(launch_rx_sfbc<R>(s, g, m, coded ? 1 : 0, B, c.y.p, c.npow.p, p->fid.p, a->seed, c.snr_lin.p, p->pw.p,
@@ -1745,10 +1751,11 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                            coded ? zn_nv<R>(p) : nullptr));
   } else {
     if (c.Ym.alloc((size_t)d.max_frames * p->n_sym * m.num_rx * m.n_dsc) ||
-        c.H.alloc((size_t)d.max_frames * m.num_rx * m.n_est * m.num_tx * m.n_dsc))
+        c.H.alloc((size_t)d.max_frames * m.num_rx * m.n_est * m.num_tx * (h_pilots ? m.maxP : m.n_dsc)))
       return fail(LTE_ENOMEM, "received grids / estimates");
     Timer t(p, KN_RX_CHEST);
-    LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p));
+    LCHK(launch_rx_fft_mimo<R>(s, g, m, B, c.y.p, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride, c.Ym.p, c.H.p,
+                               h_pilots ? 1 : 0));
   }
   V* cap_syms_dev = nullptr;
   uint8_t* cap_bits_dev = nullptr;
@@ -1772,7 +1779,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                               zn ? zn_z<R>(p) : nullptr, zn ? zn_nv<R>(p) : nullptr));
     else
       LCHK(launch_det_spatial<R>(s, g, m, B, c.Ym.p, c.H.p, p->nvar.p, p->pw.p, p->PW, d.n_bits, p->frame_err.p,
-                                 cap_syms_dev, cap_bits_dev));
+                                 cap_syms_dev, cap_bits_dev, h_pilots ? 1 : 0));
   }
   if (coded) {
     {

@@ -336,8 +336,12 @@ template <class R>
 int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nblk, int L, const R* snr_lin,
                      double div, R* npow);
 template <class R>
+// h_pilots: H receives the LS pilot estimates [b][rx][e][tx][maxP] instead of
+// the interpolated [b][rx][e][tx][n_dsc] (launch_det_spatial's h_pilots
+// interpolates them per RE with the same mimo_interp)
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
-                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H);
+                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H,
+                       int h_pilots = 0);
 // config 4's receiver + SFBC detector in one pass per frame (k_rx_sfbc): the
 // outputs of launch_rx_fft_mimo + launch_det_sfbc (zn handoff or bit errors)
 // without Y / H in HBM
@@ -356,7 +360,7 @@ int launch_det_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, 
 template <class R>
 int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* Y, const cx<R>* H,
                        const double* nvar, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                       cx<R>* cap_syms, uint8_t* cap_bits);
+                       cx<R>* cap_syms, uint8_t* cap_bits, int h_pilots = 0);
 // SFBCAlamouti.encode (decode = 0: a = symbols -> o0 = TX0, o1 = TX1) / .decode
 // (decode = 1: a = rx, h0 / h1 the per-SC estimates -> o0), float64 [n] complex, n even
 int launch_sfbc_stage(hipStream_t s, int decode, int64_t n, const double* a, const double* h0, const double* h1,

@@ -1722,7 +1722,17 @@ __device__ __forceinline__ cx<R> mimo_interp(const Grid& g, const MimoGrid& m, c
   return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
 }
 
-template <class R, int NC = 0>
+// mimo_interp at a looked-up point (segment sidx, offset fk, 1 / gap ig):
+// the same expression
+template <class R>
+__device__ __forceinline__ cx<R> mimo_interp_at(const cx<R>* hpt, int npt, int sidx, R fk, R ig) {
+  if (sidx < 0) return hpt[0];
+  if (sidx >= npt - 1) return hpt[npt - 1];
+  const cx<R> v0 = hpt[sidx], v1 = hpt[sidx + 1];
+  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+}
+
+template <class R, int NC = 0, bool HPO = false>
 __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ y,
                                                      const R* __restrict__ npow, const uint64_t* __restrict__ fid,
                                                      uint64_t seed, const R* __restrict__ inj_z, int64_t inj_stride,
@@ -1756,14 +1766,17 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
     const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
     if (active && est) {
       for (int t = 0; t < m.num_tx; ++t)
-        for (int p = tid; p < m.np_tx[t]; p += T)
-          hp[t * m.maxP + p] = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), pv[t * m.maxP + p]);
+        for (int p = tid; p < m.np_tx[t]; p += T) {
+          const V h = cdiv(cscale(buf[m.ppos[t * m.maxP + p]], sc), pv[t * m.maxP + p]);
+          if constexpr (HPO) H[((br * m.n_est + e) * m.num_tx + t) * m.maxP + p] = h;
+          else hp[t * m.maxP + p] = h;
+        }
     }
-    __syncthreads();
+    if constexpr (!HPO) __syncthreads();
     if (active) {
       V* Yo = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
       for (int j = tid; j < m.n_dsc; j += T) Yo[j] = cscale(buf[g.data_idx[j]], sc);
-      if (est) {
+      if (!HPO && est) {
         const R* pig = MGT<R>::pig(m);
         for (int t = 0; t < m.num_tx; ++t) {
           const V* hpt = hp + t * m.maxP;
@@ -1779,13 +1792,20 @@ __global__ __launch_bounds__(MWG) void k_rx_fft_mimo(Grid g, MimoGrid m, int B, 
 
 template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
-                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H) {
+                       const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H,
+                       int h_pilots) {
   const int spw = MWG / (g.N >> 3);
   const int64_t total = (int64_t)B * m.num_rx;
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t shm = spw * (g.N + m.num_tx * m.maxP) * sizeof(cx<R>);
-  if (g.N == 2048)   // 20 MHz: compile-time N (unrolled passes, twiddle recurrence)
+  if (g.N == 2048 && h_pilots)
+    hipLaunchKernelGGL((k_rx_fft_mimo<R, 2048, true>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed,
+                       inj_z, inj_stride, Y, H);
+  else if (h_pilots)
+    hipLaunchKernelGGL((k_rx_fft_mimo<R, 0, true>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
+                       inj_stride, Y, H);
+  else if (g.N == 2048)   // 20 MHz: compile-time N (unrolled passes, twiddle recurrence)
     hipLaunchKernelGGL((k_rx_fft_mimo<R, 2048>), dim3(blocks), dim3(MWG), shm, s, g, m, B, y, npow, fid, seed, inj_z,
                        inj_stride, Y, H);
   else
@@ -2258,7 +2278,7 @@ __device__ __forceinline__ void detect_sc(const dc (&He)[DMAX][DMAX], const dc (
     if (l >= R) sv[l] = {0.0, 0.0};
 }
 
-template <class R, int BPS, bool SIC_ON>
+template <class R, int BPS, bool SIC_ON, bool HPI = false>
 __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
                                                      const cx<R>* __restrict__ H, const double* __restrict__ nvar,
                                                      const uint32_t* __restrict__ pw, int PW, int n_bits,
@@ -2282,14 +2302,33 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
     if (r < NR) {
       const V v = Y[(((size_t)b * g.n_sym + l) * NR + r) * m.n_dsc + j];
       yv[r] = {(double)v.x, (double)v.y};
-      const V* Hr = H + (((size_t)b * NR + r) * m.n_est + l) * NT * m.n_dsc + j;
-      for (int t = 0; t < NT; ++t) {                 // He[r][c] = sum_t H[r][t] W[t][c]
-        const V hv = Hr[(size_t)t * m.n_dsc];
-        const dc h = {(double)hv.x, (double)hv.y};
-#pragma unroll
-        for (int c = 0; c < DMAX; ++c)
-          if (c < R_) He[r][c] = dadd(He[r][c], dmul(h, dc{m.W[(t * DMAX + c) * 2], m.W[(t * DMAX + c) * 2 + 1]}));
+    }
+  }
+  // He[r][c] = sum_t H[r][t] W[t][c], each (r, c) summed in t order; with the
+  // pilot estimates (HPI) TX t's interpolation point (segment, offset, 1 / gap)
+  // is looked up once for every RX
+  const size_t hrs = (size_t)m.n_est * NT * (HPI ? m.maxP : m.n_dsc);
+  const V* H0 = H + ((size_t)b * NR * m.n_est + l) * NT * (HPI ? m.maxP : m.n_dsc) + (HPI ? 0 : j);
+  for (int t = 0; t < NT; ++t) {
+    int sidx = 0, npt = 0;
+    R fk = (R)0, ig = (R)0;
+    if constexpr (HPI) {
+      npt = m.np_tx[t];
+      sidx = m.pseg[t * m.n_dsc + j];
+      if (sidx >= 0 && sidx < npt - 1) {
+        fk = (R)(g.data_idx[j] - m.ppos[t * m.maxP + sidx]);
+        ig = MGT<R>::pig(m)[t * m.maxP + sidx];
       }
+    }
+#pragma unroll
+    for (int r = 0; r < DMAX; ++r) {
+      if (r >= NR) break;
+      const V* Hr = H0 + r * hrs;
+      const V hv = HPI ? mimo_interp_at<R>(Hr + (size_t)t * m.maxP, npt, sidx, fk, ig) : Hr[(size_t)t * m.n_dsc];
+      const dc h = {(double)hv.x, (double)hv.y};
+#pragma unroll
+      for (int c = 0; c < DMAX; ++c)
+        if (c < R_) He[r][c] = dadd(He[r][c], dmul(h, dc{m.W[(t * DMAX + c) * 2], m.W[(t * DMAX + c) * 2 + 1]}));
     }
   }
   dc sv[DMAX];
@@ -2320,15 +2359,21 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
 template <class R>
 int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* Y, const cx<R>* H,
                        const double* nvar, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                       cx<R>* cap_syms, uint8_t* cap_bits) {
+                       cx<R>* cap_syms, uint8_t* cap_bits, int h_pilots) {
   if (m.num_tx < 1 || m.num_tx > DMAX || m.num_rx < 1 || m.num_rx > DMAX || m.rank < 1 || m.rank > m.num_rx ||
       m.rank > m.num_tx || !m.W)
     return (int)hipErrorInvalidValue;
   const int64_t n = (int64_t)B * g.n_sym * m.n_dsc;
   const dim3 grid((unsigned)((n + MWG - 1) / MWG));
 #define LTE_DSP(B_, S_)                                                                                            \
-  hipLaunchKernelGGL((k_det_spatial<R, B_, S_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, nvar, pw, PW, n_bits,        \
-                     frame_err, cap_syms, cap_bits)
+  do {                                                                                                             \
+    if (h_pilots)                                                                                                  \
+      hipLaunchKernelGGL((k_det_spatial<R, B_, S_, true>), grid, dim3(MWG), 0, s, g, m, B, Y, H, nvar, pw, PW,      \
+                         n_bits, frame_err, cap_syms, cap_bits);                                                   \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_det_spatial<R, B_, S_>), grid, dim3(MWG), 0, s, g, m, B, Y, H, nvar, pw, PW, n_bits,    \
+                         frame_err, cap_syms, cap_bits);                                                           \
+  } while (0)
   const bool sic = m.det == LTE_DET_SIC;
   if (g.bps == 2) { if (sic) LTE_DSP(2, true); else LTE_DSP(2, false); }
   else if (g.bps == 4) { if (sic) LTE_DSP(4, true); else LTE_DSP(4, false); }
@@ -2441,7 +2486,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
                                     const uint64_t*, uint64_t, const R*, int64_t, R*, int, R*);                    \
   template int launch_npow_mimo<R>(hipStream_t, int, int, const R*, int, int, const R*, double, R*);               \
   template int launch_rx_fft_mimo<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const R*,       \
-                                     const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*);                \
+                                     const uint64_t*, uint64_t, const R*, int64_t, cx<R>*, cx<R>*, int);                \
   template bool rx_sfbc_supported<R>(const Grid&, const MimoGrid&);                                                \
   template int launch_rx_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, int, const cx<R>*, const R*,      \
                                  const uint64_t*, uint64_t, const R*, const uint32_t*, int, int, uint32_t*, cx<R>*,  \
@@ -2450,7 +2495,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
                                   const cx<R>*, const R*, const uint32_t*, int, int, uint32_t*, R*, cx<R>*,        \
                                   uint8_t*, cx<R>*, R*);                                                           \
   template int launch_det_spatial<R>(hipStream_t, const Grid&, const MimoGrid&, int, const cx<R>*, const cx<R>*,   \
-                                     const double*, const uint32_t*, int, int, uint32_t*, cx<R>*, uint8_t*);
+                                     const double*, const uint32_t*, int, int, uint32_t*, cx<R>*, uint8_t*, int);
 LTE_MIMO_INST(float)
 LTE_MIMO_INST(double)
 #undef LTE_MIMO_INST

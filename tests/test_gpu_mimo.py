@@ -290,6 +290,34 @@ def test_sfbc_rx_fused_matches_separate_kernels(C, prec, coded, nrx, chan, monke
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
+@pytest.mark.parametrize('chan,det', [('rayleigh_mp', 'DET_MMSE'), ('awgn', 'DET_MMSE'), ('rayleigh_mp', 'DET_ZF'),
+                                      ('rayleigh_mp', 'DET_SIC')])
+def test_spatial_pilot_handoff_matches_interpolated_h(C, prec, chan, det, monkeypatch):
+    """Config 5's receiver hands the detector each symbol's LS pilot estimates
+    and k_det_spatial interpolates them per RE (default without an H capture)
+    against the interpolated H through HBM (LTE_SPATIAL_HP=0): the same
+    mimo_interp per (RX, TX, RE), so identical per-frame bit errors in float64
+    (float32: the north_star 1e-3)."""
+    from lte_phy.ofdm_core import _spatial_plan
+    sim = _sim(20.0, '64-QAM', chan, prec)
+    nb = 14 * 999 * 6
+    plan = _spatial_plan(sim.config, chan, 'Pedestrian_A', 3.0, 2.0, 14, nb, 7, detector=getattr(C, det),
+                         precision=prec)[0]
+    snrs = np.array([6.0, 10.0, 14.0, 18.0, 22.0, 26.0, 30.0])
+    outs = []
+    for hp in ('1', '0'):
+        monkeypatch.setenv('LTE_SPATIAL_HP', hp)
+        outs.append(plan.run(snrs, seed=17, frame_id0=777))
+    a, b = outs
+    assert 0 < int(a['counts'][:, 0].sum())
+    if prec == 'f64':
+        assert np.array_equal(a['frame_errors'], b['frame_errors'])
+        assert np.array_equal(a['counts'], b['counts'])
+    else:
+        assert np.max(np.abs(a['frame_errors'].astype(np.int64) - b['frame_errors'])) / nb < 1e-3
+
+
+@pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mimo,coded,chan', [('sfbc', True, 'rayleigh_mp'), ('spatial', False, 'rayleigh_mp'),
                                             ('spatial', False, 'awgn')])
 def test_run_grid_mimo_sharding_invariant(C, mimo, coded, chan, prec):

@@ -2278,8 +2278,14 @@ __device__ __forceinline__ void detect_sc(const dc (&He)[DMAX][DMAX], const dc (
     if (l >= R) sv[l] = {0.0, 0.0};
 }
 
+#ifndef LTE_DSP_WAVES
+#define LTE_DSP_WAVES 4
+#endif
+// linear detectors: 4 waves per SIMD (<= 128 VGPRs; the kernel waits on its
+// loads at 3, 131 VGPRs)
 template <class R, int BPS, bool SIC_ON, bool HPI = false>
-__global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
+__global__ __launch_bounds__(MWG) __attribute__((amdgpu_waves_per_eu(SIC_ON ? 1 : LTE_DSP_WAVES)))
+void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
                                                      const cx<R>* __restrict__ H, const double* __restrict__ nvar,
                                                      const uint32_t* __restrict__ pw, int PW, int n_bits,
                                                      uint32_t* __restrict__ frame_err, cx<R>* __restrict__ cap_syms,
@@ -2309,7 +2315,9 @@ __global__ __launch_bounds__(MWG) void k_det_spatial(Grid g, MimoGrid m, int B, 
   // is looked up once for every RX
   const size_t hrs = (size_t)m.n_est * NT * (HPI ? m.maxP : m.n_dsc);
   const V* H0 = H + ((size_t)b * NR * m.n_est + l) * NT * (HPI ? m.maxP : m.n_dsc) + (HPI ? 0 : j);
-  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+  for (int t = 0; t < DMAX; ++t) {   // unrolled: the four TX's table and estimate loads in flight together
+    if (t >= NT) break;
     int sidx = 0, npt = 0;
     R fk = (R)0, ig = (R)0;
     if constexpr (HPI) {

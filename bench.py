@@ -123,17 +123,10 @@ def sample_ids(F, procs):
     return [order[i::procs].tolist() for i in range(procs)]
 
 
-def cpu_baseline(config=2, F=65536, seconds=15.0, procs=None, channel=None):
-    """Time the oracle (float64 CPU restatement: NumPy front end + C turbo
-    decoder, bit-exact with the reference) on this host's cores on a bounded
-    sample of the bench's own frames: one single-threaded worker process per
-    core (frames are independent), the box's CPU share at most (16 cores per
-    GPU).  Runs before the GPU is initialised (spawned processes).  The
-    per-frame results feed `ber_match`."""
+def _cpu_pool(config, F, seconds, procs, channel):
+    """`procs` single-threaded oracle worker processes on the bench's frames for
+    `seconds`: (frames/s summed over workers, [(id, errors, crc)], wall s)."""
     import multiprocessing as mp
-    procs = procs or max(1, min(CPU_PER_GPU, os.cpu_count() or 1))
-    for v in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
-        os.environ[v] = '1'
     jobs = [(config, seconds, ids, channel) for ids in sample_ids(F, procs)]
     # close() + join(), not the context manager's terminate(): the workers exit
     # on their own (under rocprofv3 a terminate() leaves SIGTERM stack dumps)
@@ -146,15 +139,49 @@ def cpu_baseline(config=2, F=65536, seconds=15.0, procs=None, channel=None):
         raise
     finally:
         pool.join()
-    n = sum(len(r[0]) for r in res)
     value = sum(len(r[0]) / r[1] for r in res)
     frames = sorted(x for r in res for x in r[0])
-    return {'value': value, 'unit': 'subframes/s', 'cores': procs, 'kind': 'port', 'host_cores': os.cpu_count(),
-            'per_core': value / procs, 'cpu_model': _cpu_model(),
+    return value, frames, max(r[1] for r in res)
+
+
+def cpu_baseline(config=2, F=65536, seconds=15.0, procs=None, channel=None, single_seconds=None):
+    """Time the oracle (float64 CPU restatement: NumPy front end + C turbo
+    decoder, bit-exact with the reference) on this host's cores on a bounded
+    sample of the bench's own frames, as BASELINE.md's CPU timing asks: one
+    single-threaded worker process per core (frames are independent) over the
+    box's CPU share (16 cores per GPU: `value`, `gpu_share`), and one process
+    alone (`single_process`, `single_seconds`, default 8 s; 0 skips it).
+    `all_cores` is the per-core rate x the host's CPUs, an extrapolation: the
+    pool's rules size worker pools to the CPU share, not the whole machine
+    (scripts/cpu_baseline_scaling.py measures 1 .. all cores where that is
+    allowed; profiles/r6_cpu_baseline_scaling.json).  Runs before the GPU is
+    initialised (spawned processes).  The per-frame results feed `ber_match`."""
+    procs = procs or max(1, min(CPU_PER_GPU, os.cpu_count() or 1))
+    for v in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
+        os.environ[v] = '1'
+    value, frames, wall = _cpu_pool(config, F, seconds, procs, channel)
+    n = len(frames)
+    single_seconds = min(8.0, seconds) if single_seconds is None else single_seconds
+    single = None
+    if single_seconds > 0:
+        v1, f1, w1 = _cpu_pool(config, F, single_seconds, 1, channel)
+        single = {'value': v1, 'cores': 1, 'frames': len(f1), 'seconds': round(w1, 1)}
+    host = os.cpu_count() or procs
+    per_core = value / procs
+    return {'value': value, 'unit': 'subframes/s', 'cores': procs, 'kind': 'port', 'host_cores': host,
+            'per_core': per_core, 'cpu_model': _cpu_model(),
+            'gpu_share': {'value': value, 'cores': procs, 'frames': n, 'seconds': round(wall, 1)},
+            'single_process': single,
+            'all_cores': {'value': per_core * host, 'cores': host, 'measured': False,
+                          'what': 'per-core rate of the gpu_share pool x the host CPUs (linear: the frames are '
+                                  'independent); not run here -- worker pools on the box are sized to its CPU '
+                                  'share. Measured 1 .. all cores of another host: '
+                                  'profiles/r6_cpu_baseline_scaling.json'},
             'sample': f'{n} of the bench\'s own config-{config} frames (ids from both ends of rank 0\'s first '
                       f'timed step, the oracle\'s restatement of the device Philox draws) over SNR 0:2:30 dB, '
-                      f'{max(r[1] for r in res):.1f} s on {procs} host cores, one single-threaded process each '
-                      f'(oracle: NumPy + C, float64)',
+                      f'{wall:.1f} s on {procs} host cores, one single-threaded process each '
+                      f'(oracle: NumPy + C, float64)' +
+                      (f'; single process: {single["frames"]} frames in {single["seconds"]} s' if single else ''),
             'frames': frames}
 
 
@@ -268,14 +295,39 @@ def decoder_row_bytes(K, esz, iters):
     return K * rows * esz + 3 * 2 * passes * esz + K / 8
 
 
+def shape_bytes(K, iters=8):
+    """(all bytes, store bytes) one 64-frame wave of the decoder's access-shape
+    microbenchmark moves for a code block of K (scripts/turbo_shape_bench.hip
+    wave_bytes: 512-B rows; forward + backward row loads, tails, extrinsic
+    stores, checkpoint stores and loads)."""
+    nsub = K // 8
+    nsw = (nsub + 2) // 3
+    rows = stores = 0
+    for p in range(2 * iters + 1):
+        per = 2 if p == 0 else 3
+        rows += per * K * 2 + 6 + K + ((nsub + 2) // 3) * 8 + nsw * 8
+        stores += K + ((nsub + 2) // 3) * 8
+    return rows * 512, stores * 512
+
+
+def shape_store_share(iters=8):
+    """Share of the decoder shape's bytes that are stores (extrinsic +
+    checkpoint rows), from the shape bench's own byte counts."""
+    from lte_phy.channel_coding import segmentation_sizes
+    tot = [shape_bytes(K, iters) for K in segmentation_sizes(TB + 24)]
+    return sum(t[1] for t in tot) / sum(t[0] for t in tot)
+
+
 def turbo_roofline(prec, tim, F, iters=8):
-    """Turbo decoder (the dominant kernel of configs 2 and 4) against SURVEY
-    §8(d)'s roofline for it, K7: VALU, sum(K+3) x 17 passes x ~100 add/max ops
-    per subframe against the non-packed f64 (f32) vector peak -> `frac`.
-    Beside it the measured limiter: the exact recursion's HBM row stream
-    (`hbm_row_stream`: compulsory row bytes per launch / the mean launch time,
-    PMC traffic, the access-shape ceiling and what the stores cost), and the
-    SQ-counted VALU issue occupancy."""
+    """Turbo decoder (the dominant kernel of configs 2 and 4).  `bound` is the
+    measured limiter: the exact lane-per-code-block recursion streams its rows
+    through HBM (a code block's working set cannot stay on chip), so
+    achieved / peak / frac price the compulsory row stream of that algorithm
+    (decoder_row_bytes per launch / the mean launch time) against 8 TB/s, and
+    `traffic` is the PMC-measured HBM bytes per launch (hbm_frac = its rate /
+    8 TB/s).  Beside it SURVEY §8(d)'s K7 figure, `valu_frac`: sum(K+3) x 17
+    passes x ~100 add/max ops per subframe against the non-packed f64 (f32)
+    vector peak, and the SQ-counted VALU issue occupancy."""
     from lte_phy.channel_coding import segmentation_sizes
     t_ms, t_n = tim.get('turbo', (0.0, 0))
     avg_s = t_ms / max(t_n, 1) * 1e-3
@@ -297,93 +349,213 @@ def turbo_roofline(prec, tim, F, iters=8):
             if sq and t_n else None)
     ceil = shape.get(f'ceiling_GBs_{prec}') if shape else None
     limiter = 'hbm' if busy is None or (tr_gbs or gbs) / HBM_PEAK_GBS >= busy else 'valu'
-    return {'bound': 'valu', 'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo',
-            'bound_basis': 'SURVEY §8(d) names VALU as K7\'s roofline (the round-3 review asked for this `frac`); the '
-                           'reference recursion has 103 add/max per trellis step and pass (gamma 6, alpha 24, beta '
-                           '24, a-posteriori 47, extrinsic 2), which §8(d) rounds to 100.  What limits the kernel as '
-                           'measured is `measured_limiter` (' + limiter + '): see hbm_row_stream, traffic and '
-                           'issued_valu_busy_frac',
-            'achieved': round(achieved_T, 3), 'peak': round(peak / 1e12, 2), 'unit': 'Top/s',
-            'frac': round(achieved_T * 1e12 / peak, 4) if t_n else 0.0,
-            'traffic': round(tr) if tr else None,
-            'what': 'SURVEY §8(d) K7: sum(K+3) x (2 it. + 1) passes x 100 add/max ops per subframe '
-                    f'({ops_sf} op) x frames / mean launch time, against the non-packed {prec} vector peak; '
-                    'traffic = PMC-measured HBM bytes per launch (gfx950-corrected)',
-            'ops_per_subframe': ops_sf,
-            'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': t_n, 'frames_per_launch': F,
-            'issued_valu_busy_frac': round(busy, 4) if busy is not None else None,
-            'valu_wave_instr_per_frame': sq['valu_wave_instr_per_frame'] if sq else None,
-            'measured_limiter': limiter,
-            'hbm_row_stream': {
-                'achieved_GBs': round(gbs, 1), 'peak_GBs': HBM_PEAK_GBS,
-                'frac_row_stream': round(gbs / HBM_PEAK_GBS, 4),
-                'alg_bytes_per_launch': int(row_bytes),
-                'alg_bytes': 'exact-recursion row stream: per code-block step 7 rows (Ls, Lp, La forward and '
-                             'backward + extrinsic store) x esz B x 17 passes (first pass 5, final 6 + K/8 B decisions)',
-                'traffic_over_alg': round(tr / row_bytes, 3) if tr else None,
-                'traffic_GBs': round(tr_gbs, 1) if tr_gbs else None,
-                'traffic_frac': round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs else None,
-                'shape_ceiling': ({'GBs': ceil, 'traffic_frac_of_ceiling': round(tr_gbs / ceil, 4) if tr_gbs else None,
-                                   'source': 'profiles/r3_turbo_shape_microbench.json (another box: +-5 %)'}
-                                  if ceil else None),
-                # the decoder's access shape with and without its stores (extrinsic +
-                # checkpoint rows, 17 % of the bytes): a STORED reference value from
-                # round 3, replaced by this box's own measurement when the shape bench
-                # runs after the timed region (same_box_shape_ceiling)
-                'store_cost': {'shape_ms_full': 319.5, 'shape_ms_reads_only': 237.4,
-                               'store_share_of_time': round(1 - 237.4 / 319.5, 3), 'store_share_of_bytes': 0.17,
-                               'measured_in_this_run': False,
-                               'source': 'stored: profiles/r3_turbo_shape_layouts.jsonl run shape4, variants aux3 / '
-                                         'a3nost, CH 32 (65 536 frames), another box'}},
-            'stage_bytes': {'bytes_per_launch': int(stage_bytes),
-                            'achieved_GBs': round(stage_bytes / avg_s / 1e9, 2) if t_n else 0.0,
-                            'frac': round(stage_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if t_n else 0.0,
-                            'what': 'SURVEY §8(d) stage boundary: rate-dematched input LLRs + decoded bits'}}
+    valu_frac = round(achieved_T * 1e12 / peak, 4) if t_n else 0.0
+    if limiter == 'hbm':
+        head = {'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(gbs / HBM_PEAK_GBS, 4) if t_n else 0.0}
+        what = ('compulsory row stream of the exact recursion (decoder_row_bytes: per code-block step 7 rows of '
+                f'{esz} B -- Ls, Lp, La forward and backward + the extrinsic store -- over 2 it. + 1 passes) x '
+                'frames / mean launch time, against 8 TB/s; traffic = PMC-measured HBM bytes per launch '
+                '(gfx950-corrected)')
+    else:
+        head = {'achieved': round(achieved_T, 3), 'peak': round(peak / 1e12, 2), 'unit': 'Top/s', 'frac': valu_frac}
+        what = (f'SURVEY §8(d) K7: sum(K+3) x (2 it. + 1) passes x 100 add/max ops per subframe ({ops_sf} op) x '
+                f'frames / mean launch time, against the non-packed {prec} vector peak')
+    out = {'bound': limiter, 'kernel': 'k_turbo64' if prec == 'f64' else 'k_turbo'}
+    out.update(head)
+    out.update({
+        'traffic': round(tr) if tr else None,
+        'hbm_frac': round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs else None,
+        'valu_frac': valu_frac,
+        'what': what,
+        'bound_basis': 'bound = the measured limiter: the PMC traffic rate as a share of 8 TB/s (hbm_frac) against '
+                       'the SQ-counted VALU issue occupancy (issued_valu_busy_frac), whichever is higher.  SURVEY '
+                       "§8(d) names VALU as K7's roofline; that figure is valu_frac (the reference recursion has "
+                       '103 add/max per trellis step and pass -- gamma 6, alpha 24, beta 24, a-posteriori 47, '
+                       'extrinsic 2 -- which §8(d) rounds to 100)',
+        'valu': {'achieved': round(achieved_T, 3), 'peak': round(peak / 1e12, 2), 'unit': 'Top/s',
+                 'frac': valu_frac, 'ops_per_subframe': ops_sf,
+                 'what': f'SURVEY §8(d) K7: sum(K+3) x (2 it. + 1) passes x 100 add/max ops per subframe x frames / '
+                         f'mean launch time, against the non-packed {prec} vector peak'},
+        'ops_per_subframe': ops_sf,
+        'avg_launch_ms': round(avg_s * 1e3, 3), 'launches': t_n, 'frames_per_launch': F,
+        'issued_valu_busy_frac': round(busy, 4) if busy is not None else None,
+        'valu_wave_instr_per_frame': sq['valu_wave_instr_per_frame'] if sq else None,
+        'measured_limiter': limiter,
+        'hbm_row_stream': {
+            'achieved_GBs': round(gbs, 1), 'peak_GBs': HBM_PEAK_GBS,
+            'frac_row_stream': round(gbs / HBM_PEAK_GBS, 4),
+            'alg_bytes_per_launch': int(row_bytes),
+            'alg_bytes': 'exact-recursion row stream: per code-block step 7 rows (Ls, Lp, La forward and '
+                         'backward + extrinsic store) x esz B x 17 passes (first pass 5, final 6 + K/8 B decisions)',
+            'traffic_over_alg': round(tr / row_bytes, 3) if tr else None,
+            'traffic_GBs': round(tr_gbs, 1) if tr_gbs else None,
+            'traffic_frac': round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs else None,
+            'shape_ceiling': ({'GBs': ceil, 'traffic_frac_of_ceiling': round(tr_gbs / ceil, 4) if tr_gbs else None,
+                               'source': 'profiles/r3_turbo_shape_microbench.json (another box: +-5 %)'}
+                              if ceil else None),
+            # the decoder's access shape with and without its stores (extrinsic +
+            # checkpoint rows): a STORED reference time from round 3, replaced by
+            # this box's own measurement when the shape bench runs after the timed
+            # region (same_box_shape_ceiling); the byte share is the shape's own count
+            'store_cost': {'shape_ms_full': 319.5, 'shape_ms_reads_only': 237.4,
+                           'store_share_of_time': round(1 - 237.4 / 319.5, 3),
+                           'store_share_of_bytes': round(shape_store_share(iters), 4),
+                           'measured_in_this_run': False,
+                           'source': 'stored: profiles/r3_turbo_shape_layouts.jsonl run shape4, variants aux3 / '
+                                     'a3nost, CH 32 (65 536 frames), another box; byte share: shape_bytes'}},
+        'stage_bytes': {'bytes_per_launch': int(stage_bytes),
+                        'achieved_GBs': round(stage_bytes / avg_s / 1e9, 2) if t_n else 0.0,
+                        'frac': round(stage_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if t_n else 0.0,
+                        'what': 'SURVEY §8(d) stage boundary: rate-dematched input LLRs + decoded bits'}})
+    return out
 
 
 def stage_bytes_per_frame(config, plan, prec):
-    """Algorithmic HBM bytes per frame of each timed stage (the streams a stage
-    must read and write at its boundaries; complex = 2 x esz B) for the
-    uncoded configs' roofline."""
+    """Algorithmic HBM bytes per frame of each timed stage of the bench's
+    default path (the kernels lte_run launches for it with every LTE_* knob at
+    its default), from the streams those kernels must read and write
+    (complex = 2 x esz B, packed bits).  Stage -> (kernels, bytes, what); the
+    kernel names are the keys of the committed PMC summaries (PMC_FILES), so
+    each stage's measured traffic sits beside its algorithmic bytes.
+    * The fused transmitters (configs 2/3: static taps; configs 4/5) write the
+      received streams without their CP samples where the receiver never reads
+      them (SISO / SIMO: k_chan_fix rebuilds the stream's first samples);
+      configs 4/5 keep the CP (the link power is measured over it).
+    * The receivers read n_sym x N samples per RX (the CP is stripped).
+    * Config 5 (spatial, no H capture): k_rx_fft_mimo hands the detector the
+      LS pilot estimates, nr x n_est x nt x pilots-per-TX (LTE_SPATIAL_HP),
+      not the interpolated H.
+    * Flat links (config 5 'awgn'): TX and links are one pass
+      (k_ofdm_txch_flat); the 'channel' timer then covers only k_npow_mimo's
+      per-RX power (partials in, one noise power out)."""
     esz = 8 if prec == 'f64' else 4
     c = 2 * esz
     L, n_sym, bits = plan.L, plan.n_sym, plan.n_bits / 8
-    if config == 3:
-        nr = plan.num_rx
-        return {'ofdm_tx': ('k_ofdm_tx (fused SIMO channel)', bits + nr * L * c),
-                'rx_data': ('k_rx_frame_simo', nr * L * c + bits)}
-    nt, nr = plan.num_tx, plan.num_rx
-    y = n_sym * nr * plan.n_dsc * c
-    h = nr * plan.n_est * nt * plan.n_dsc * c
-    return {'ofdm_tx': ('k_ofdm_tx_mimo', bits + nt * L * c),
-            'channel': ('k_fading_mimo + k_channel_tay (k_channel_mimo: exact Jakes)', (nt + nr) * L * c),
-            'rx_chest': ('k_rx_fft_mimo', nr * L * c + y + h),
-            'rx_data': ('k_det_spatial', y + h + bits)}
+    N, nr = plan.N, plan.num_rx
+    sym = n_sym * N * c                       # one antenna's symbols without CP
+    rows = 0
+    if config in (2, 4):                      # decoder rows: 3K + 12 per code block
+        from lte_phy.channel_coding import segmentation_sizes
+        rows = sum(3 * K + 12 for K in segmentation_sizes(plan.n_bits + 24))
+    if config in (2, 3):
+        ctx = {2: 'k_ofdm_txf', 3: 'k_ofdm_tx'}[config]
+        crx = {2: 'k_rx_frame', 3: 'k_rx_frame_simo2'}[config]
+        tx_in = plan.coded_bits / 8 if config == 2 else bits
+        out = {'ofdm_tx': ([ctx], tx_in + nr * sym, 'payload / coded bits in, each RX stream (no CP) out'),
+               'rx_data': ([crx], nr * sym + (0 if config == 2 else bits),
+                           'each RX stream (no CP) in' + (', payload bits in for the error count' if config == 3
+                                                           else ''))}
+        if plan.channel == 1:   # static taps: coefficients, then the first-samples power fix-up + noise power
+            D, P = plan.max_delay, plan.n_paths
+            out['fading'] = (['k_fading'], nr * P * c, 'one tap coefficient per (RX, path) out')
+            out['channel'] = (['k_chan_fix', 'k_npow'], n_sym * 2 * D * c + nr * P * c + 3 * nr * n_sym * esz,
+                              "each symbol's head / previous tail (2 x max delay) and the taps in, the power "
+                              'partials updated, the noise power out')
+        if config == 2:   # equalised symbols + sigma^2_eff per (group, data SC) to k_dematch_zn
+            out['rx_data'] = ([crx], nr * sym + n_sym * plan.Nd * c + plan.n_grp * plan.Nd * esz,
+                              'the RX stream (no CP) in; equalised symbols + sigma^2_eff per data SC out')
+            out['dematch'] = (['k_dematch_zn'], n_sym * plan.Nd * c + plan.n_grp * plan.Nd * esz + rows * esz,
+                              'symbols + sigma^2_eff in, the decoder rows (3K + 12 per CB) out')
+        return out
+    nt = plan.num_tx
+    stream = L * c                            # one antenna's stream with CP
+    if config == 4:
+        res = plan.res
+        return {'ofdm_tx': (['k_ofdm_txch_sfbc'], plan.coded_bits / 8 + nr * stream,
+                            'coded bits in, each RX antenna\'s faded stream (with CP) out'),
+                'channel': (['k_link_noise_pairs'], 2 * nr * stream, 'each RX stream in and out (+ link noise)'),
+                'rx_chest': (['k_rx_sfbc'], nr * sym + n_sym * res * c + n_sym * (res // 2) * esz,
+                             'each RX stream (no CP) in; combined symbols + sigma^2_eff per RE pair out'),
+                'dematch': (['k_dematch_zn'], n_sym * res * c + n_sym * (res // 2) * esz + rows * esz,
+                            'symbols + sigma^2_eff in, the decoder rows out')}
+    y = n_sym * nr * plan.n_dsc * c           # data-SC values per RX and symbol
+    hp = nr * plan.n_est * nt * plan.pilots_per_tx * c   # LS pilot estimates
+    flat = plan.channel == 0
+    out = {'rx_chest': (['k_rx_fft_mimo'], nr * sym + y + hp,
+                        'each RX stream (no CP) in; data-SC values + LS pilot estimates out'),
+           'rx_data': (['k_det_spatial'], y + hp + bits, 'data-SC values + pilot estimates + payload bits in')}
+    if flat:
+        out['ofdm_tx'] = (['k_ofdm_txch_flat'], bits + nr * stream, 'payload bits in, each RX stream (with CP) out')
+        out['fading'] = (['k_fading_mimo'], nr * nt * c, 'the flat link gains out')
+        out['channel'] = (['k_npow_mimo'], nr * (n_sym + 1) * esz, 'per-symbol power partials in, noise power out')
+    else:
+        out['ofdm_tx'] = (['k_ofdm_tx_mimo'], bits + nt * stream, 'payload bits in, each TX stream (with CP) out')
+        out['channel'] = (['k_channel_tay', 'k_npow_mimo'], (nt + nr) * stream,
+                          'each TX stream in, each RX stream out')
+    return out
+
+
+# the committed rocprofv3 --pmc summary of each config's bench step (the
+# traffic beside each stage's algorithmic bytes; tests/test_roofline_pmc.py)
+PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r5_pmc_c3_final.json', 4: 'r5_pmc_c4_final.json',
+             5: 'r5_pmc_c5_hp.json'}
+
+
+def pmc_stage_bytes(pmc, kernels):
+    """HBM bytes per frame of a stage's kernels in a PMC summary (the instance
+    '<name><template args>' that ran, the longest if several): None when the
+    first (main) kernel is absent; a later helper kernel the summary does not
+    list (k_npow: a few hundred bytes) counts 0."""
+    if not pmc:
+        return None
+    ks = pmc['kernels']
+    tot = 0.0
+    for i, name in enumerate(kernels):
+        hits = [v for k, v in ks.items() if k == name or k.startswith(name + '<')]
+        if not hits:
+            if i == 0:
+                return None
+            continue
+        tot += max(hits, key=lambda v: v.get('ms', 0))['hbm_bytes_per_frame']
+    return tot
+
+
+def stage_table(config, plan, prec, tim, F, steps):
+    """Every timed stage that has an algorithmic byte count: its kernels, its
+    algorithmic bytes per frame, the committed PMC bytes per frame of the same
+    kernels (PMC_FILES) and both rates against the 8 TB/s peak."""
+    sb = stage_bytes_per_frame(config, plan, prec)
+    pmc = load_profile(PMC_FILES[config]) if prec == 'f64' else None
+    out = {}
+    for k, (ms, n) in tim.items():
+        if k not in sb or not n:
+            continue
+        kern, b, what = sb[k]
+        st_s = ms / steps * 1e-3
+        gbs = b * F / st_s / 1e9
+        tb = pmc_stage_bytes(pmc, kern)
+        out[k] = {'kernels': kern, 'ms_per_step': round(st_s * 1e3, 3), 'alg_bytes_per_frame': round(b),
+                  'alg_GBs': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 4), 'what': what,
+                  'pmc_bytes_per_frame': round(tb) if tb else None,
+                  'traffic_GBs': round(tb * F / st_s / 1e9, 1) if tb else None,
+                  'traffic_frac': round(tb * F / st_s / 1e9 / HBM_PEAK_GBS, 4) if tb else None}
+    return out
 
 
 def hbm_roofline(config, plan, prec, tim, F, steps):
     """Uncoded configs: the dominant timed stage against the HBM roofline --
-    its algorithmic bytes per frame x frames / its time per step (a stage's
-    timer may cover several launches per step: config 5's channel stage is
-    k_fading_mimo + the channel kernel)."""
-    sb = stage_bytes_per_frame(config, plan, prec)
-    stages = {k: v for k, v in tim.items() if k in sb and v[1]}
-    if not stages:
+    its algorithmic bytes per frame x frames / its time per step (HIP events
+    on the plan stream), the committed PMC bytes of the same kernels as
+    `traffic`, every other stage beside it (stage_table)."""
+    st = stage_table(config, plan, prec, tim, F, steps)
+    if not st:
         return None
-    dom = max(stages, key=lambda k: stages[k][0])
-    t_ms, n = stages[dom]
-    st_s = t_ms / steps * 1e-3
-    kern, b = sb[dom]
-    gbs = b * F / st_s / 1e9
-    return {'bound': 'hbm', 'kernel': kern, 'stage': dom, 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
-            'alg_bytes_per_frame': round(b), 'stage_ms_per_step': round(st_s * 1e3, 3), 'launches': n,
-            'steps': steps, 'frames_per_step': F,
-            'what': 'algorithmic stage-boundary bytes (the streams the stage must read / write) x frames / '
-                    'the stage time per step (HIP events on the plan stream)',
-            'other_stages': {k: {'kernel': sb[k][0], 'ms_per_step': round(v[0] / steps, 3),
-                                 'GBs': round(sb[k][1] * F / (v[0] / steps * 1e-3) / 1e9, 1)}
-                             for k, v in stages.items() if k != dom}}
+    dom = max(st, key=lambda k: st[k]['ms_per_step'])
+    d = st[dom]
+    tb = d['pmc_bytes_per_frame']
+    return {'bound': 'hbm', 'kernel': ' + '.join(d['kernels']), 'stage': dom, 'achieved': d['alg_GBs'],
+            'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': d['frac'],
+            'traffic': round(tb * F) if tb else None,
+            'hbm_frac': d['traffic_frac'],
+            'alg_bytes_per_frame': d['alg_bytes_per_frame'], 'stage_ms_per_step': d['ms_per_step'],
+            'launches': tim[dom][1], 'steps': steps, 'frames_per_step': F,
+            'what': 'algorithmic bytes of the kernels the default path launches (stage_bytes_per_frame: the streams '
+                    'they must read / write) x frames / the stage time per step (HIP events on the plan stream); '
+                    'traffic = the same kernels\' HBM bytes per frame in the committed PMC summary ('
+                    + PMC_FILES[config] + ') x frames per launch; hbm_frac = that traffic\'s rate / 8 TB/s',
+            'pmc_source': 'profiles/' + PMC_FILES[config],
+            'other_stages': {k: v for k, v in st.items() if k != dom}}
 
 
 def roofline(config, prec, tim, steps, F, el, value, world, iters=8, plan=None):
@@ -391,11 +563,10 @@ def roofline(config, prec, tim, steps, F, el, value, world, iters=8, plan=None):
         roof = turbo_roofline(prec, tim, F, iters)
         t_ms = tim.get('turbo', (0.0, 0))[0]
         roof['turbo_share_of_step'] = round(t_ms / (el * 1e3) if el > 0 else 0, 3)
-        if config == 4:
-            roof['front_end'] = front_end(prec, tim, F, 4)
+        if plan is not None:
+            roof['front_end'] = front_end(prec, tim, F, config, plan, steps)
         if config == 2:
             esz = 8 if prec == 'f64' else 4
-            roof['front_end'] = front_end(prec, tim, F)
             # SURVEY §8(d)'s whole-chain view: compulsory stage-boundary bytes per subframe
             roof['pipeline_hbm'] = {'bytes_per_subframe': B_SF_F32 * esz // 4,
                                     'achieved_GBs': round(B_SF_F32 * esz / 4 * value / world / 1e9, 2),
@@ -428,8 +599,10 @@ def same_box_shape_ceiling(hrs, F):
                             'source': 'same box, same call: scripts/turbo_shape_bench F decoder after the timed region'}
     if 'ms_1wps_reads_only' in dl:
         full, ro = dl['ms_1wps'], dl['ms_1wps_reads_only']
+        share = (d['bytes_per_launch_stores'] / d['bytes_per_launch_ckpt'] if d.get('bytes_per_launch_stores')
+                 else shape_store_share())
         hrs['store_cost'] = {'shape_ms_full': full, 'shape_ms_reads_only': ro,
-                             'store_share_of_time': round(1 - ro / full, 3), 'store_share_of_bytes': 0.17,
+                             'store_share_of_time': round(1 - ro / full, 3), 'store_share_of_bytes': round(share, 4),
                              'measured_in_this_run': True,
                              'source': 'same box, same call: the shape at one wave per SIMD with and without its '
                                        'extrinsic / checkpoint stores (scripts/turbo_shape_bench F decoder)'}
@@ -446,55 +619,22 @@ def merge_timers(all_tim):
     return out
 
 
-# front-end stages (bench timers) -> their kernels in the committed PMC summary
-FE_KERNELS = {'payload': ['k_payload'], 'encode': ['k_encode'], 'ofdm_tx': ['k_ofdm_txf'],
-              'rx_data': ['k_rx_frame'], 'dematch': ['k_dematch_zn'], 'crc_count': ['k_crc_count']}
-FE_KERNELS_C4 = {'payload': ['k_payload'], 'encode': ['k_encode'], 'ofdm_tx': ['k_ofdm_txch_sfbc'],
-                 'channel': ['k_link_noise_pairs'], 'rx_chest': ['k_rx_sfbc'], 'dematch': ['k_dematch_zn'],
-                 'crc_count': ['k_crc_count']}
-
-
-def front_end(prec, tim, F, config=2):
-    """Per front-end stage: its HIP-event time per launch, the HBM bytes per
-    frame its kernels move (profiles/r3_pmc_<prec>.json, rocprofv3 FETCH_SIZE /
-    WRITE_SIZE, gfx950-corrected) and the resulting rate against the 8 TB/s
-    peak, plus the VALU / LDS shares of active issue from the same PMC passes
-    (what bounds the FFT / noise kernels, which are not HBM-bound)."""
-    # the newest committed summary of the config-2 chain in this precision
-    # (kernel keys carry their template arguments since round 4)
-    pmc, used = None, None
-    names = [f'r5_pmc_c{config}_final.json'] if prec == 'f64' else []
-    if config == 2:
-        names += [f'r3_pmc_{prec}.json', f'r2_pmc_{prec}.json']
-    for name in names:
-        pmc = load_profile(name)
+def front_end(prec, tim, F, config, plan, steps):
+    """Coded configs (2, 4): every front-end stage's algorithmic bytes
+    (stage_bytes_per_frame) and committed PMC traffic beside its HIP-event
+    time (stage_table), plus the VALU / LDS shares of active issue of its first
+    kernel from the same PMC passes (what bounds the FFT / noise kernels, which
+    are not HBM-bound)."""
+    st = stage_table(config, plan, prec, tim, F, steps)
+    pmc = load_profile(PMC_FILES[config]) if prec == 'f64' else None
+    for k, v in st.items():
         if pmc:
-            used = name
-            break
-    if not pmc:
-        return None
-    ks = pmc['kernels']
-
-    def find(name):   # exact key, or the instance '<name><template args>' that ran
-        if name in ks:
-            return ks[name]
-        hits = [v for k, v in ks.items() if k.startswith(name + '<')]
-        return max(hits, key=lambda v: v.get('ms', 0)) if hits else None
-
-    out = {}
-    for stage, names in (FE_KERNELS_C4 if config == 4 else FE_KERNELS).items():
-        t_ms, n = tim.get(stage, (0.0, 0))
-        rows = [find(k) for k in names]
-        if not n or not all(rows):
-            continue
-        b = sum(r['hbm_bytes_per_frame'] for r in rows)
-        gbs = b * F / (t_ms / n * 1e-3) / 1e9
-        share = rows[0].get('share_of_active_issue', {})
-        out[stage] = {'kernels': names, 'ms': round(t_ms / n, 3), 'hbm_bytes_per_frame': round(b),
-                      'achieved_GBs': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 3),
-                      'valu_share': share.get('valu'), 'lds_share': share.get('lds'),
-                      'pmc_source': 'profiles/' + used}
-    return out
+            hits = [r for n, r in pmc['kernels'].items() if n == v['kernels'][0] or n.startswith(v['kernels'][0] + '<')]
+            if hits:
+                share = max(hits, key=lambda r: r.get('ms', 0)).get('share_of_active_issue', {})
+                v['valu_share'], v['lds_share'] = share.get('valu'), share.get('lds')
+        v['pmc_source'] = 'profiles/' + PMC_FILES[config] if pmc else None
+    return st
 
 
 def dry_run_counts(ids, S, n_bits=TB):
@@ -514,15 +654,19 @@ def dry_run_counts(ids, S, n_bits=TB):
 # bench plan) and synthetic per-stage timers, so the N > 1 rehearsal prices
 # the same roofline as a GPU run (the line is marked dry_run)
 DRY_GEOM = {
-    2: dict(L=14 * 2192, n_sym=14, n_bits=TB, num_rx=1, num_tx=1),
-    3: dict(L=14 * 1096, n_sym=14, n_bits=14 * 499 * 4, num_rx=4, num_tx=1),
-    4: dict(L=14 * 2192, n_sym=14, n_bits=TB, num_rx=2, num_tx=2, n_dsc=998, n_est=1),
-    5: dict(L=14 * 2192, n_sym=14, n_bits=14 * 999 * 6, num_rx=4, num_tx=4, n_dsc=250, n_est=14),
+    2: dict(L=14 * 2192, n_sym=14, n_bits=TB, num_rx=1, num_tx=1, N=2048, Nd=999, n_grp=1, n_cb=5,
+            coded_bits=83772, channel=1, n_paths=4, max_delay=13),
+    3: dict(L=14 * 1096, n_sym=14, n_bits=14 * 499 * 4, num_rx=4, num_tx=1, N=1024, Nd=499, n_grp=1, channel=1,
+            n_paths=6, max_delay=39),
+    4: dict(L=14 * 2192, n_sym=14, n_bits=TB, num_rx=2, num_tx=2, N=2048, Nd=999, n_grp=1, n_cb=5,
+            coded_bits=83772, res=998, n_dsc=998, n_est=1, pilots_per_tx=100, channel=1),
+    5: dict(L=14 * 2192, n_sym=14, n_bits=14 * 999 * 6, num_rx=4, num_tx=4, N=2048, Nd=999, n_grp=1, n_dsc=250,
+            n_est=14, pilots_per_tx=50, channel=0),
 }
 DRY_STAGE_SHARE = {2: {'turbo': 0.87, 'ofdm_tx': 0.04, 'rx_data': 0.045, 'dematch': 0.03},
-                   3: {'ofdm_tx': 0.3, 'rx_data': 0.65},
+                   3: {'ofdm_tx': 0.3, 'channel': 0.02, 'rx_data': 0.65},
                    4: {'turbo': 0.69, 'ofdm_tx': 0.08, 'channel': 0.1, 'rx_chest': 0.07, 'dematch': 0.03},
-                   5: {'ofdm_tx': 0.25, 'channel': 0.05, 'rx_chest': 0.45, 'rx_data': 0.2}}
+                   5: {'ofdm_tx': 0.25, 'fading': 0.001, 'channel': 0.001, 'rx_chest': 0.45, 'rx_data': 0.2}}
 
 
 def dry_run_timers(config, el, steps, rank):

@@ -1737,7 +1737,10 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   // received grids / estimates / symbols): receiver + detector in one pass
   const bool zn0 = coded && sfbc && (d.bps == 4 || d.bps == 6) && !a->cap_llr && (m.res & 1) == 0 &&
                    m.n_dsc <= m.res && env_on("LTE_DEMAP_IN_DEMATCH", true);
-  const bool rx_fuse = sfbc && !inj_z && !a->cap_H && !a->cap_data_syms && !a->cap_bits_rx && (zn0 || !coded) &&
+  // (a capture of the received bits needs the detector's decisions only
+  // uncoded: coded, they come from k_crc_count)
+  const bool rx_fuse = sfbc && !inj_z && !a->cap_H && !a->cap_data_syms && !(a->cap_bits_rx && !coded) &&
+                       (zn0 || !coded) &&
                        rx_sfbc_supported<R>(g, m) && env_on("LTE_SFBC_RX_FUSE", true);
   // spatial multiplexing without a capture of H: the receiver hands over each
   // estimation symbol's LS pilot estimates and the detector interpolates them

@@ -264,8 +264,10 @@ def mimo_detect(det, y, H, sigma2, W, bps=0):
 
 def sfbc_encode(symbols):
     """SFBCAlamouti.encode on the GPU (lte_sfbc_encode_host64): [n] complex -> (tx0, tx1)."""
-    device_init()
     s = np.ascontiguousarray(symbols, dtype=np.complex128)
+    if s.ndim != 1:
+        raise ValueError(f"symbols must be 1-D, got shape {s.shape}")
+    device_init()
     tx0, tx1 = np.empty_like(s), np.empty_like(s)
     check(load().lte_sfbc_encode_host64(len(s), ptr(s.view(np.float64), F64), ptr(tx0.view(np.float64), F64),
                                         ptr(tx1.view(np.float64), F64)))
@@ -273,11 +275,16 @@ def sfbc_encode(symbols):
 
 
 def sfbc_decode(rx, H0, H1, regularization=1e-10):
-    """SFBCAlamouti.decode on the GPU (lte_sfbc_decode_host64)."""
-    device_init()
+    """SFBCAlamouti.decode on the GPU (lte_sfbc_decode_host64).  The C entry
+    reads len(rx) values from each of H0 / H1: lengths are checked here."""
     r = np.ascontiguousarray(rx, dtype=np.complex128)
     h0 = np.ascontiguousarray(H0, dtype=np.complex128)
     h1 = np.ascontiguousarray(H1, dtype=np.complex128)
+    if r.ndim != 1 or h0.ndim != 1 or h1.ndim != 1:
+        raise ValueError(f"rx, H0, H1 must be 1-D, got shapes {r.shape}, {h0.shape}, {h1.shape}")
+    if not (len(h0) == len(h1) == len(r)):
+        raise ValueError(f"Channel estimates must have length {len(r)}")
+    device_init()
     out = np.empty_like(r)
     check(load().lte_sfbc_decode_host64(len(r), ptr(r.view(np.float64), F64), ptr(h0.view(np.float64), F64),
                                         ptr(h1.view(np.float64), F64), float(regularization),

@@ -68,6 +68,13 @@ class Plan:
         self.rank = int(rank) if rank else self.num_tx
         self.n_dsc = self.res if sfbc else -(-self.Nd // max(1, self.rank))
         self.n_est = self.n_grp if sfbc else self.n_sym
+        # per-TX CRS subsets pilots[t::step], step = min(num_tx, 4) (lte_capi.hip
+        # plan_mimo_tables, core/mimo_channel_estimator_periodic.py:75-107): the
+        # largest subset is what the spatial receiver hands the detector per
+        # (RX, estimate, TX) on the pilot-estimate path (LTE_SPATIAL_HP)
+        self.cp_len, self.channel = int(cp_len), int(channel)
+        self.n_paths, self.max_delay = len(delays), int(max(delays)) if len(delays) else 0
+        self.pilots_per_tx = -(-self.Np // min(max(1, self.num_tx), 4))
 
     def __del__(self):
         try:

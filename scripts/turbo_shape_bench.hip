@@ -196,15 +196,18 @@ __global__ __launch_bounds__(256) void k_shape(Jobs J, int iters, int CH) {
   if (acc == 0x123456789abcdefull) lds_pad[0] = acc;   // never true; keeps the LDS request
 }
 
-// bytes one wave moves (the loop structure above, counted on the host)
-static double wave_bytes(int K, int iters, bool ckpt) {
+// bytes one wave moves (the loop structure above, counted on the host);
+// stores_only: just the extrinsic and checkpoint rows it writes
+// (bench.py shape_bytes mirrors this count)
+static double wave_bytes(int K, int iters, bool ckpt, bool stores_only = false) {
   const int nsub = K / 8, nsw = (nsub + 2) / 3;
   double rows = 0;
   for (int p = 0; p < 2 * iters + 1; ++p) {
     const bool first = p == 0;
     const double per = first ? 2 : 3;
-    rows += per * K * 2 + 6 + K;   // fwd + bwd loads, tails, extrinsic stores
-    if (ckpt) rows += (double)((nsub + 2) / 3) * 8 + nsw * 8;
+    if (!stores_only) rows += per * K * 2 + 6;   // fwd + bwd loads, tails
+    rows += K;                                   // extrinsic stores
+    if (ckpt) rows += (double)((nsub + 2) / 3) * 8 + (stores_only ? 0 : nsw * 8);   // checkpoint stores + loads
   }
   return rows * 512;
 }
@@ -215,7 +218,7 @@ int main(int argc, char** argv) {
   Jobs J{};
   J.n = 5;
   std::vector<void*> bufs;
-  double bytes_ck = 0, bytes_nock = 0;
+  double bytes_ck = 0, bytes_nock = 0, bytes_st = 0;
   for (int r = 0; r < 5; ++r) {
     const size_t rows = 4 * (size_t)Ks[r] + 12, ckrows = (size_t)(Ks[r] / 8 + 1) * 8;
     void *b, *c;
@@ -231,6 +234,7 @@ int main(int argc, char** argv) {
     J.prefix[r + 1] = J.prefix[r] + G;
     bytes_ck += wave_bytes(Ks[r], iters, true) * G;
     bytes_nock += wave_bytes(Ks[r], iters, false) * G;
+    bytes_st += wave_bytes(Ks[r], iters, true, true) * G;
   }
   const int waves = J.prefix[5];
   hipEvent_t a, b;
@@ -258,10 +262,11 @@ int main(int argc, char** argv) {
       printf("kernel failed\n");
       return 1;
     }
-    printf("{\"frames\": %d, \"waves\": %d, \"bytes_per_launch_ckpt\": %.0f, \"decoder_layout\": {\"CH\": 32, "
+    printf("{\"frames\": %d, \"waves\": %d, \"bytes_per_launch_ckpt\": %.0f, \"bytes_per_launch_stores\": %.0f, "
+           "\"decoder_layout\": {\"CH\": 32, "
            "\"aux\": %d, \"ms_1wps\": %.3f, \"ms_2wps\": %.3f, \"ms_free\": %.3f, \"GBs_best\": %.1f, "
            "\"ms_1wps_reads_only\": %.3f}}\n",
-           F, waves, bytes_ck, LTE_SHAPE_AUXL, a1, a2, a3, bytes_ck / (best * 1e-3) / 1e9, an);
+           F, waves, bytes_ck, bytes_st, LTE_SHAPE_AUXL, a1, a2, a3, bytes_ck / (best * 1e-3) / 1e9, an);
     for (void* p : bufs) (void)hipFree(p);
     return 0;
   }

@@ -107,11 +107,19 @@ def test_bench_self_launches_ranks_dry_run():
     # before any rank starts) and a roofline priced on the slowest rank's timers
     cpu = out['cpu_baseline']
     assert cpu and cpu['value'] > 0 and cpu['cores'] >= 1 and cpu['kind'] == 'port'
+    # BASELINE.md's CPU timing: 1 process, the GPU's share, all cores (extrapolated)
+    assert cpu['single_process']['cores'] == 1 and cpu['single_process']['value'] > 0
+    assert cpu['gpu_share']['value'] == cpu['value'] and cpu['all_cores']['cores'] == os.cpu_count()
     roof = out['roofline']
-    # SURVEY §8(d)'s K7 roofline (VALU) with the HBM row-stream view beside it
-    assert roof['bound'] == 'valu' and roof['unit'] == 'Top/s' and roof['peak'] == 39.32
-    for k in ('achieved', 'frac', 'traffic', 'avg_launch_ms', 'hbm_row_stream', 'stage_bytes', 'measured_limiter'):
+    # bound = the measured limiter (the exact recursion's HBM row stream), with
+    # SURVEY §8(d)'s K7 VALU figure beside it
+    assert roof['bound'] == roof['measured_limiter']
+    assert (roof['unit'], roof['peak']) == (('GB/s', 8000.0) if roof['bound'] == 'hbm' else ('Top/s', 39.32))
+    assert roof['valu']['unit'] == 'Top/s' and roof['valu']['peak'] == 39.32 and roof['valu_frac'] > 0
+    for k in ('achieved', 'frac', 'traffic', 'hbm_frac', 'avg_launch_ms', 'hbm_row_stream', 'stage_bytes',
+              'measured_limiter', 'front_end'):
         assert k in roof, k
+    assert set(roof['front_end']) >= {'ofdm_tx', 'rx_data', 'dematch'}
     assert roof['hbm_row_stream']['peak_GBs'] == 8000.0 and 'store_cost' in roof['hbm_row_stream']
     # the BER-match sample comes from the CPU baseline's oracle frames; no device here
     assert out['ber_match'] is None and 'frames' not in cpu
@@ -151,11 +159,13 @@ def test_bench_other_configs_dry_run_world2(config):
     if config == 4:
         assert roof['kernel'] == 'k_turbo64' and roof['frac'] > 0 and 'hbm_row_stream' in roof
     else:
-        # rx_chest (k_rx_fft_mimo) is the largest synthetic stage: y in + Y + H out per frame
+        # rx_chest (k_rx_fft_mimo) is the largest synthetic stage: the RX streams
+        # (no CP) in, the data-SC values + LS pilot estimates out per frame
         assert roof['bound'] == 'hbm' and roof['stage'] == 'rx_chest' and roof['unit'] == 'GB/s'
         c = 16
-        assert roof['alg_bytes_per_frame'] == round(4 * 14 * 2192 * c + 14 * 4 * 250 * c + 4 * 14 * 4 * 250 * c)
-        assert set(roof['other_stages']) == {'ofdm_tx', 'channel', 'rx_data'}
+        assert roof['alg_bytes_per_frame'] == 4 * 14 * 2048 * c + 14 * 4 * 250 * c + 4 * 14 * 4 * 50 * c
+        assert roof['traffic'] and roof['hbm_frac'] is not None
+        assert set(roof['other_stages']) == {'ofdm_tx', 'fading', 'channel', 'rx_data'}
     cpu = out['cpu_baseline']
     assert cpu['cores'] == min(32, os.cpu_count())
     assert cpu['note'].startswith(f"{cpu['cores']} single-threaded worker processes")

@@ -273,12 +273,15 @@ def test_sfbc_rx_fused_matches_separate_kernels(C, prec, coded, nrx, chan, monke
             sim._sfbc_plan(14, 14 * 998 * 6, nrx, max_frames=7))
     snrs = np.array([6.0, 10.0, 14.0, 16.0, 18.0, 22.0, 30.0])
     outs = []
+    cap = ('bits_rx',) if coded else ()   # coded: the decoder's bits (k_crc_count), fused path kept
     for fuse in ('1', '0'):
         monkeypatch.setenv('LTE_SFBC_RX_FUSE', fuse)
-        outs.append(plan.run(snrs, seed=31, frame_id0=4242))
+        outs.append(plan.run(snrs, seed=31, frame_id0=4242, capture=cap))
     a, b = outs
     if coded:
         assert np.array_equal(a['crc_ok'], b['crc_ok'])
+        if prec == 'f64':
+            assert np.array_equal(a['bits_rx'], b['bits_rx'])
     assert 0 < int(a['counts'][:, 0].sum())
     if prec == 'f64':
         assert np.array_equal(a['frame_errors'], b['frame_errors'])

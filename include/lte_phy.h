@@ -233,9 +233,35 @@ int lte_dft_host64(int M, int inverse, int64_t batch, const double *in, double *
 /* Soft demap: _calculate_llrs_* core/ofdm_core.py:791-923 (bps 2/4/6) */
 int lte_llr_host(int bps, int64_t n, const float *syms, const float *noise_var, float *llr);
 int lte_llr_host64(int bps, int64_t n, const double *syms, const double *noise_var, double *llr);
-/* Hard decision: QAMModulator.symbols_to_bits core/modulator.py:90-112 */
+/* QAM map: QAMModulator.bits_to_symbols core/modulator.py:61-88 -- bits [n][bps]
+ * (0 / 1 bytes, MSB first per symbol) -> n complex128 points of the
+ * natural-binary index (level * (1 / sqrt(2 | 10 | 42)), NumPy's divide) */
+int lte_qam_map_host64(int bps, int64_t n, const uint8_t *bits, double *out);
+/* Channel estimation: LTEChannelEstimator.estimate_channel + _interpolate_channel
+ * core/lte_receiver.py:40-133 -- for each of batch received grids Y [batch][N]
+ * (complex128): LS Y[p] / X[p] at the n_pilots ascending pilot_idx (known X
+ * complex128), np.linspace between consecutive pilots, edges held -> H
+ * [batch][N]; pilot_ls [batch][n_pilots] the LS values (or NULL); stats
+ * [batch][2] = mean |Y_p|^2, mean |Y_p - X_p|^2 (pairwise sums, or NULL) */
+int lte_chest_host64(int N, int n_pilots, const int32_t *pilot_idx, const double *known, int64_t batch,
+                     const double *Y, double *H, double *pilot_ls, double *stats);
+/* ZF equalizer: LTEEqualizerZF.equalize core/lte_receiver.py:154-180 --
+ * out = Y / (H + regularization), n complex128 (NumPy's complex divide) */
+int lte_zf_host64(int64_t n, const double *Y, const double *H, double regularization, double *out);
+/* Nearest point as the reference decides it: QAMModulator.symbols_to_bits
+ * core/modulator.py:90-112 -- np.abs(c - y) over the constellation (NumPy's
+ * complex absolute) and np.argmin (first minimum), also on exact decision
+ * boundaries; n complex128 in, n * bps MSB-first bits out */
+int lte_nearest_host64(int bps, int64_t n, const double *syms, uint8_t *bits);
+/* Hard decision (the chains' per-axis slicer, ties -> lower level; equal to
+ * lte_nearest_host64 off the decision boundaries):
+ * QAMModulator.symbols_to_bits core/modulator.py:90-112 */
 int lte_hard_host(int bps, int64_t n, const float *syms, uint8_t *bits);
 int lte_hard_host64(int bps, int64_t n, const double *syms, uint8_t *bits);
+/* RSC constituent encoder: rsc_encode core/channel_coding/turbo_encoder.py:137-211
+ * -- n bits in; systematic (the feedback bit a_k) and parity out, n (+ 3
+ * termination steps when termination != 0) bytes each */
+int lte_rsc_encode_host(int64_t n, const uint8_t *bits, int termination, uint8_t *systematic, uint8_t *parity);
 /* Turbo encode: turbo_encode core/channel_coding/turbo_encoder.py:214-313 */
 int lte_turbo_encode_host(int K, int64_t ncb, const uint8_t *bits, uint8_t *out /*[ncb][3K+12]*/);
 /* Turbo decode: turbo_decode core/channel_coding/turbo_decoder.py:338-450 */
@@ -251,7 +277,8 @@ int lte_turbo_decode_host64(int K, int iters, int64_t ncb, const double *llr /*[
 int lte_bcjr_host64(int n, int64_t ncb, const double *ls, const double *lp, const double *la, double *app);
 /* CRC: _calculate_crc core/channel_coding/crc.py:89-134 (MSB-first, zero init);
  * poly 0x1864CFB (CRC-24A, calculate_crc24a :137-159) or 0x1800063 (CRC-24B,
- * calculate_crc24b :162-184), len 24 */
+ * calculate_crc24b :162-184), len 24; any other poly with its x^len term and
+ * len 1..31 (CRC-16 0x11021, calculate_crc16 :187-209) by a serial kernel */
 int lte_crc_host(int64_t n, const uint8_t *bits, uint32_t poly, int len, uint32_t *crc);
 /* Channel on an arbitrary-length stream: ChannelSimulator.transmit (core/channel.py:
  * 334-345) = RayleighChannel.filter (rayleighchannel.py:44-58) + measured-power

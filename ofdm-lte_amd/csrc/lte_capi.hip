@@ -2439,7 +2439,110 @@ static int hard_host(int bps, int64_t n, const R* syms, uint8_t* bits) {
   return rc;
 }
 
+// QAMModulator.bits_to_symbols (core/modulator.py:61-88) on n whole symbols
+static int qam_map_host(int bps, int64_t n, const uint8_t* bits, double* out) {
+  if ((bps != 2 && bps != 4 && bps != 6) || n < 0 || (n && (!bits || !out)))
+    return fail(LTE_EINVAL, "bad qam map arguments");
+  if (n == 0) return LTE_OK;
+  DBuf<uint8_t> db;
+  DBuf<double2> dout;
+  if (db.alloc((size_t)n * bps) || dout.alloc(n)) return fail(LTE_ENOMEM, "qam map buffers");
+  int rc = LTE_OK;
+  if (hipMemcpy(db.p, bits, (size_t)n * bps, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_qam_map(nullptr, bps, n, db.p, dout.p) || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, dout.p, (size_t)n * 16, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(LTE_EHIP, "qam map failed");
+  db.release(); dout.release();
+  return rc;
+}
+
+// QAMModulator.symbols_to_bits (core/modulator.py:90-112), the reference's
+// own distance and argmin
+static int hard_argmin_host(int bps, int64_t n, const double* syms, uint8_t* bits) {
+  if ((bps != 2 && bps != 4 && bps != 6) || n < 0 || (n && (!syms || !bits)))
+    return fail(LTE_EINVAL, "bad decision arguments");
+  if (n == 0) return LTE_OK;
+  DBuf<double2> ds;
+  DBuf<uint8_t> db;
+  if (ds.alloc(n) || db.alloc((size_t)n * bps)) return fail(LTE_ENOMEM, "decision buffers");
+  const bool ok = hipMemcpy(ds.p, syms, (size_t)n * 16, hipMemcpyHostToDevice) == hipSuccess &&
+                  launch_hard_argmin(nullptr, bps, n, ds.p, db.p) == 0 && hipDeviceSynchronize() == hipSuccess &&
+                  hipMemcpy(bits, db.p, (size_t)n * bps, hipMemcpyDeviceToHost) == hipSuccess;
+  ds.release(); db.release();
+  return ok ? LTE_OK : fail(LTE_EHIP, "decisions failed");
+}
+
+// LTEChannelEstimator.estimate_channel + _interpolate_channel
+// (core/lte_receiver.py:40-133) on batch received grids of N subcarriers
+static int chest_host(int N, int P, const int32_t* pidx, const double* known, int64_t batch, const double* Y,
+                      double* H, double* hp, double* stats) {
+  if (N < 1 || P < 1 || P > 4096 || batch < 0 || !pidx || !known || (batch && (!Y || !H)))
+    return fail(LTE_EINVAL, "bad channel estimation arguments");
+  for (int p = 0; p < P; ++p)
+    if (pidx[p] < 0 || pidx[p] >= N || (p && pidx[p] <= pidx[p - 1]))
+      return fail(LTE_EINVAL, "pilot indices must be ascending and inside [0, N)");
+  if (batch == 0) return LTE_OK;
+  DBuf<int32_t> dp;
+  DBuf<double2> dk, dy, dh, dhp;
+  DBuf<double> dst;
+  const size_t ny = (size_t)batch * N;
+  if (dp.alloc(P) || dk.alloc(P) || dy.alloc(ny) || dh.alloc(ny) || (hp && dhp.alloc((size_t)batch * P)) ||
+      (stats && dst.alloc((size_t)batch * 2)))
+    return fail(LTE_ENOMEM, "channel estimation buffers");
+  bool ok = hipMemcpy(dp.p, pidx, (size_t)P * 4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dk.p, known, (size_t)P * 16, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dy.p, Y, ny * 16, hipMemcpyHostToDevice) == hipSuccess &&
+            launch_chest(nullptr, N, P, dp.p, dk.p, batch, dy.p, dh.p, hp ? dhp.p : nullptr,
+                         stats ? dst.p : nullptr) == 0 &&
+            hipDeviceSynchronize() == hipSuccess && hipMemcpy(H, dh.p, ny * 16, hipMemcpyDeviceToHost) == hipSuccess;
+  if (ok && hp) ok = hipMemcpy(hp, dhp.p, (size_t)batch * P * 16, hipMemcpyDeviceToHost) == hipSuccess;
+  if (ok && stats) ok = hipMemcpy(stats, dst.p, (size_t)batch * 2 * 8, hipMemcpyDeviceToHost) == hipSuccess;
+  dp.release(); dk.release(); dy.release(); dh.release(); dhp.release(); dst.release();
+  return ok ? LTE_OK : fail(LTE_EHIP, "channel estimation failed");
+}
+
+// LTEEqualizerZF.equalize (core/lte_receiver.py:154-180): Y / (H + reg)
+static int zf_host(int64_t n, const double* Y, const double* H, double reg, double* out) {
+  if (n < 0 || (n && (!Y || !H || !out))) return fail(LTE_EINVAL, "bad equalizer arguments");
+  if (n == 0) return LTE_OK;
+  DBuf<double2> dy, dh, dout;
+  if (dy.alloc(n) || dh.alloc(n) || dout.alloc(n)) return fail(LTE_ENOMEM, "equalizer buffers");
+  const bool ok = hipMemcpy(dy.p, Y, (size_t)n * 16, hipMemcpyHostToDevice) == hipSuccess &&
+                  hipMemcpy(dh.p, H, (size_t)n * 16, hipMemcpyHostToDevice) == hipSuccess &&
+                  launch_zf(nullptr, n, dy.p, dh.p, reg, dout.p) == 0 && hipDeviceSynchronize() == hipSuccess &&
+                  hipMemcpy(out, dout.p, (size_t)n * 16, hipMemcpyDeviceToHost) == hipSuccess;
+  dy.release(); dh.release(); dout.release();
+  return ok ? LTE_OK : fail(LTE_EHIP, "equalizer failed");
+}
+
 extern "C" {
+
+int lte_qam_map_host64(int bps, int64_t n, const uint8_t* bits, double* out) {
+  return qam_map_host(bps, n, bits, out);
+}
+int lte_nearest_host64(int bps, int64_t n, const double* syms, uint8_t* bits) {
+  return hard_argmin_host(bps, n, syms, bits);
+}
+int lte_chest_host64(int N, int n_pilots, const int32_t* pilot_idx, const double* known, int64_t batch,
+                     const double* Y, double* H, double* pilot_ls, double* stats) {
+  return chest_host(N, n_pilots, pilot_idx, known, batch, Y, H, pilot_ls, stats);
+}
+int lte_zf_host64(int64_t n, const double* Y, const double* H, double regularization, double* out) {
+  return zf_host(n, Y, H, regularization, out);
+}
+int lte_rsc_encode_host(int64_t n, const uint8_t* bits, int termination, uint8_t* systematic, uint8_t* parity) {
+  if (n < 0 || (n && !bits) || !systematic || !parity) return fail(LTE_EINVAL, "bad rsc arguments");
+  const int64_t m = n + (termination ? 3 : 0);
+  if (m == 0) return LTE_OK;
+  DBuf<uint8_t> du, ds, dp;
+  if (du.alloc(n ? n : 1) || ds.alloc(m) || dp.alloc(m)) return fail(LTE_ENOMEM, "rsc buffers");
+  const bool ok = (n == 0 || hipMemcpy(du.p, bits, n, hipMemcpyHostToDevice) == hipSuccess) &&
+                  launch_rsc(nullptr, n, du.p, termination ? 1 : 0, ds.p, dp.p) == 0 &&
+                  hipMemcpy(systematic, ds.p, m, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemcpy(parity, dp.p, m, hipMemcpyDeviceToHost) == hipSuccess;
+  du.release(); ds.release(); dp.release();
+  return ok ? LTE_OK : fail(LTE_EHIP, "rsc failed");
+}
 
 int lte_fft_host(int N, int inverse, int64_t batch, const float* in, float* out) {
   return fft_host<float>(N, inverse, batch, in, out);
@@ -2466,8 +2569,19 @@ int lte_hard_host64(int bps, int64_t n, const double* syms, uint8_t* bits) {
 
 int lte_crc_host(int64_t n, const uint8_t* bits, uint32_t poly, int len, uint32_t* crc) {
   if (n < 0 || !crc || (n && !bits)) return fail(LTE_EINVAL, "bad crc arguments");
-  if ((poly != 0x1864CFBu && poly != 0x1800063u) || len != 24)
-    return fail(LTE_EUNSUP, "the device CRC path computes CRC-24A / CRC-24B");
+  if ((poly != 0x1864CFBu && poly != 0x1800063u) || len != 24) {
+    // any other CRC (CRC-16 0x11021, crc.py:187-209): the serial device kernel
+    if (len < 1 || len > 31 || (poly >> len) != 1u)
+      return fail(LTE_EUNSUP, "CRC length 1..31 with the x^len term in poly");
+    DBuf<uint8_t> db;
+    DBuf<uint32_t> dout;
+    if (db.alloc(n ? n : 1) || dout.alloc(1)) return fail(LTE_ENOMEM, "buffers");
+    const bool ok = (n == 0 || hipMemcpy(db.p, bits, n, hipMemcpyHostToDevice) == hipSuccess) &&
+                    launch_crc_serial(nullptr, n, db.p, poly & ((1u << len) - 1u), len, dout.p) == 0 &&
+                    hipMemcpy(crc, dout.p, 4, hipMemcpyDeviceToHost) == hipSuccess;
+    db.release(); dout.release();
+    return ok ? LTE_OK : fail(LTE_EHIP, "crc failed");
+  }
   const int nw = (int)((n + 24 + 31) / 32) + 1;
   std::vector<uint32_t> w(nw, 0);
   pack_bits(bits, (int)n, w.data(), nw);

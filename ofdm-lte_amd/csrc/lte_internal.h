@@ -222,6 +222,14 @@ template <class R>
 int launch_llr(hipStream_t s, int bps, int64_t n, const cx<R>* syms, const R* nv, R* llr);
 template <class R>
 int launch_hard(hipStream_t s, int bps, int64_t n, const cx<R>* syms, uint8_t* bits);
+// building-block stage kernels (lte_blocks.hip, float64, NumPy's operation order)
+int launch_qam_map(hipStream_t s, int bps, int64_t n, const uint8_t* bits, double2* out);
+int launch_hard_argmin(hipStream_t s, int bps, int64_t n, const double2* y, uint8_t* bits);
+int launch_chest(hipStream_t s, int N, int P, const int32_t* pidx, const double2* known, int64_t batch,
+                 const double2* Y, double2* H, double2* hp, double* stats);
+int launch_zf(hipStream_t s, int64_t n, const double2* Y, const double2* H, double reg, double2* out);
+int launch_crc_serial(hipStream_t s, int64_t n, const uint8_t* bits, uint32_t poly_low, int len, uint32_t* out);
+int launch_rsc(hipStream_t s, int64_t n, const uint8_t* u, int term, uint8_t* sys, uint8_t* par);
 
 // ---------------------------------------------------------------- multi-antenna chains
 // SFBC 2xN (configs 4 / simulate_miso / simulate_mimo) and TM4 spatial

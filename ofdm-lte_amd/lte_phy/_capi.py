@@ -83,6 +83,13 @@ _SIGS = {
     'lte_llr_host64': (ctypes.c_int, [ctypes.c_int, c_i64, P(c_f64), P(c_f64), P(c_f64)]),
     'lte_hard_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_float), P(ctypes.c_uint8)]),
     'lte_hard_host64': (ctypes.c_int, [ctypes.c_int, c_i64, P(c_f64), P(ctypes.c_uint8)]),
+    'lte_qam_map_host64': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_uint8), P(c_f64)]),
+    'lte_nearest_host64': (ctypes.c_int, [ctypes.c_int, c_i64, P(c_f64), P(ctypes.c_uint8)]),
+    'lte_chest_host64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P(c_i32), P(c_f64), c_i64, P(c_f64), P(c_f64),
+                                        P(c_f64), P(c_f64)]),
+    'lte_zf_host64': (ctypes.c_int, [c_i64, P(c_f64), P(c_f64), c_f64, P(c_f64)]),
+    'lte_rsc_encode_host': (ctypes.c_int, [c_i64, P(ctypes.c_uint8), ctypes.c_int, P(ctypes.c_uint8),
+                                           P(ctypes.c_uint8)]),
     'lte_turbo_encode_host': (ctypes.c_int, [ctypes.c_int, c_i64, P(ctypes.c_uint8), P(ctypes.c_uint8)]),
     'lte_turbo_decode_host': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, P(ctypes.c_float),
                                              P(ctypes.c_uint8)]),

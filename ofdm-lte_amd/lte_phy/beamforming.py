@@ -148,6 +148,24 @@ class CSIFeedback:
                 'most_common_pmi': max(set(self.pmi_history), key=self.pmi_history.count),
                 'pmi_distribution': np.bincount(self.pmi_history, minlength=self.codebook.codebook_size)}
 
+    def print_statistics(self):
+        """core/csi_feedback.py:208-228 (printout of get_statistics)."""
+        stats = self.get_statistics()
+        if stats is None:
+            print("[CSIFeedback] No hay estadísticas disponibles")
+            return
+        print(f"\n{'=' * 60}")
+        print("Estadísticas CSI Feedback")
+        print(f"{'=' * 60}")
+        print(f"  Total feedbacks: {stats['total_feedbacks']}")
+        print(f"  PMIs únicos usados: {stats['unique_pmis']} / {self.codebook.codebook_size}")
+        print(f"  PMI más común: {stats['most_common_pmi']}")
+        print("\n  Distribución PMI:")
+        for pmi, count in enumerate(stats['pmi_distribution']):
+            if count > 0:
+                print(f"    PMI {pmi}: {count} ({100 * count / stats['total_feedbacks']:.1f}%)")
+        print(f"{'=' * 60}\n")
+
 
 def bf_plan(config, n_sym, n_bits, num_tx, num_rx, adaptive, max_frames=1, precision=None):
     from .engine import get_plan

@@ -19,6 +19,7 @@ from . import _capi as C
 
 CRC24A_POLYNOMIAL = 0x1864CFB
 CRC24B_POLYNOMIAL = 0x1800063
+CRC16_POLYNOMIAL = 0x11021
 USE_MAX_LOG_MAP = True
 
 __all__ = ['calculate_crc24a', 'calculate_crc24b', 'attach_crc24a', 'attach_crc24b', 'check_crc24a', 'check_crc24b',
@@ -41,13 +42,13 @@ def find_interleaver_size(min_size: int) -> int:
 
 
 # ---------------------------------------------------------------- CRC (GPU)
-def _crc(data_bits, poly):
+def _crc(data_bits, poly, length=24):
     C.device_init()
     b = np.ascontiguousarray(np.asarray(data_bits), dtype=np.uint8) & 1
     out = np.zeros(1, dtype=np.uint32)
-    C.check(C.load().lte_crc_host(len(b), C.ptr(b, C.U8), poly, 24, C.ptr(out, C.U32)))
+    C.check(C.load().lte_crc_host(len(b), C.ptr(b, C.U8), poly, length, C.ptr(out, C.U32)))
     v = int(out[0])
-    return np.array([(v >> (23 - i)) & 1 for i in range(24)], dtype=np.uint8)
+    return np.array([(v >> (length - 1 - i)) & 1 for i in range(length)], dtype=np.uint8)
 
 
 def calculate_crc24a(data_bits: np.ndarray) -> np.ndarray:
@@ -84,6 +85,31 @@ def check_crc24b(data_with_crc: np.ndarray) -> bool:
     if len(d) < 24:
         return False
     return bool(np.array_equal(d[-24:], calculate_crc24b(d[:-24])))
+
+
+def calculate_crc16(data_bits: np.ndarray) -> np.ndarray:
+    """crc.py:187-209 on the GPU (the serial CRC kernel, poly 0x11021)."""
+    return _crc(data_bits, CRC16_POLYNOMIAL, 16)
+
+
+def attach_crc16(data_bits: np.ndarray) -> np.ndarray:
+    """crc.py:260-274."""
+    return np.concatenate([data_bits, calculate_crc16(data_bits)])
+
+
+def check_crc16(data_with_crc: np.ndarray) -> bool:
+    """crc.py:343-367."""
+    d = np.asarray(data_with_crc)
+    if len(d) < 16:
+        return False
+    return bool(np.array_equal(d[-16:], calculate_crc16(d[:-16])))
+
+
+def get_test_vectors_crc24a():
+    """crc.py:370-394: (data, CRC-24A) for 40 zeros, 40 ones, alternating 0/1."""
+    vecs = [np.zeros(40, dtype=np.uint8), np.ones(40, dtype=np.uint8),
+            np.array([i % 2 for i in range(40)], dtype=np.uint8)]
+    return [(v, calculate_crc24a(v)) for v in vecs]
 
 
 # ---------------------------------------------------------------- segmentation
@@ -191,6 +217,23 @@ def qpp_deinterleave(data: np.ndarray, K: int) -> np.ndarray:
     return np.asarray(data)[inv]
 
 
+def rsc_encode(input_bits: np.ndarray, trellis_termination: bool = True) -> Tuple[np.ndarray, np.ndarray]:
+    """turbo_encoder.py:137-211 on the GPU (lte_rsc_encode_host): the
+    'systematic' output is the feedback bit, the termination feeds s1 ^ s2."""
+    C.device_init()
+    b = np.ascontiguousarray(np.asarray(input_bits), dtype=np.uint8) & 1
+    m = len(b) + (3 if trellis_termination else 0)
+    sys_, par = np.zeros(m, dtype=np.uint8), np.zeros(m, dtype=np.uint8)
+    C.check(C.load().lte_rsc_encode_host(len(b), C.ptr(b, C.U8), 1 if trellis_termination else 0,
+                                         C.ptr(sys_, C.U8), C.ptr(par, C.U8)))
+    return sys_, par
+
+
+def turbo_encode_block_list(code_blocks: list) -> list:
+    """turbo_encoder.py:316-329."""
+    return [turbo_encode(block) for block in code_blocks]
+
+
 def turbo_encode(input_bits):
     """turbo_encoder.py:214-313 on the GPU: [d0 d1 d2]*K + 12 tail bits."""
     C.device_init()
@@ -212,7 +255,26 @@ def set_decoder_mode(use_max_log_map: bool = True):
     print(f"Turbo Decoder mode set to: {mode}")
 
 
-def turbo_decode(llr_encoded, K, num_iterations=5, debug=False, precision=None):
+def log_sum_exp(a: float, b: float) -> float:
+    """turbo_decoder.py:64-88 (the scalar max* of exact log-MAP; the GPU
+    decoders evaluate the same expression per trellis branch)."""
+    if np.isinf(a) and a < 0:
+        return b
+    if np.isinf(b) and b < 0:
+        return a
+    if a > b:
+        return a + np.log1p(np.exp(b - a))
+    return b + np.log1p(np.exp(a - b))
+
+
+def max_star(a: float, b: float) -> float:
+    """turbo_decoder.py:91-115: max(a, b) in max-log-MAP mode, else log_sum_exp."""
+    if USE_MAX_LOG_MAP:
+        return max(a, b)
+    return log_sum_exp(a, b)
+
+
+def turbo_decode(llr_encoded, K, num_iterations=5, debug=False, *, precision=None):
     """turbo_decoder.py:338-450 on the GPU.  precision 'f64' (default,
     bit-exact with the reference) or 'f32' (fast mode, max-log only)."""
     return turbo_decode_batch(np.asarray(llr_encoded)[None], K, num_iterations, precision)[0]
@@ -306,6 +368,31 @@ def sub_block_deinterleaver(input_bits: np.ndarray, original_length: int, D: int
     out = np.full(n, -1, dtype=np.int64)
     out[perm[:m]] = np.asarray(x[:m]).astype(np.int64)
     return out[out != -1].astype(np.uint8)
+
+
+def sub_block_deinterleaver_llr(interleaved_data: np.ndarray, K_original: int) -> np.ndarray:
+    """rate_matching.py:300-371, an index permutation: NULL cells are the
+    last of R x 32 in column-major order of the original matrix, moved by the
+    column permutation; the values fill the permuted matrix row-major around
+    them, the inverse column permutation is applied and the matrix is read
+    column-major without the NULLs (NaN inputs are dropped like NULLs, as
+    the reference does), truncated to K_original."""
+    x = np.asarray(interleaved_data, dtype=np.float64).ravel()
+    D, Kpi = 32, len(x)
+    R = int(np.ceil(Kpi / D))
+    P = np.array([0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+                  1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31])
+    P_inv = np.argsort(P)
+    rows, cols = np.meshgrid(np.arange(R), np.arange(D), indexing='ij')
+    null_orig = cols * R + rows >= Kpi
+    null_perm = np.zeros((R, D), dtype=bool)
+    null_perm[:, P] = null_orig
+    perm = np.full((R, D), np.nan)
+    slots = np.flatnonzero(~null_perm.ravel())
+    n = min(len(slots), Kpi)
+    perm.ravel()[slots[:n]] = x[:n]
+    out = perm[:, P_inv].T.ravel()
+    return np.array(out[~np.isnan(out)][:K_original], dtype=np.float64)
 
 
 def rate_match_turbo(encoded_bits, E, K, rv_idx=0):

@@ -25,56 +25,13 @@ from .engine import get_plan
 SLOT_SIZE = 14
 
 
-# ------------------------------------------------------------------ host-side grid mirror
-class ResourceGrid:
-    """LTEResourceGrid (core/resource_mapper.py:17-111): guard bands, DC null,
-    pilot on every 6th useful SC (offset 3), data elsewhere."""
-
-    def __init__(self, N, Nc):
-        self.N, self.Nc = N, Nc
-        self.num_guard_left = (N - Nc) // 2
-        self.num_guard_right = N - Nc - self.num_guard_left
-        self.dc_index = N // 2
-        self.pilot_spacing = 6
-        k = np.arange(N)
-        guard = (k < self.num_guard_left) | (k >= N - self.num_guard_right)
-        dc = (k == self.dc_index) & ~guard
-        pilot = ~guard & ~dc & (((k - self.num_guard_left) % 6) == 3)
-        self._data = k[~guard & ~dc & ~pilot]
-        self._pilot = k[pilot]
-        self._guard = k[guard]
-
-    def get_data_indices(self):
-        return self._data.copy()
-
-    def get_pilot_indices(self):
-        return self._pilot.copy()
-
-    def get_guard_indices(self):
-        return self._guard.copy()
-
-    def get_statistics(self):
-        return {'total_subcarriers': self.N, 'useful_subcarriers': self.Nc,
-                'data_subcarriers': len(self._data), 'pilot_subcarriers': len(self._pilot),
-                'guard_subcarriers': len(self._guard), 'dc_subcarriers': 1,
-                'guard_left': self.num_guard_left, 'guard_right': self.num_guard_right,
-                'pilot_spacing': self.pilot_spacing}
-
-
-def constellation(mod):
-    """QAMModulator._generate_constellation (core/modulator.py:28-59) (host table)."""
-    if mod == 'QPSK':
-        return np.array([1 + 1j, 1 - 1j, -1 + 1j, -1 - 1j]) / np.sqrt(2)
-    lv = [-3, -1, 1, 3] if mod == '16-QAM' else [-7, -5, -3, -1, 1, 3, 5, 7]
-    sc = np.sqrt(10) if mod == '16-QAM' else np.sqrt(42)
-    return np.array([r + 1j * i for r in lv for i in lv]) / sc
-
-
-def _reseed_pilots(cell_id, n):
-    """PilotPattern.generate_pilots side effect (core/resource_mapper.py:148):
-    the reference reseeds the GLOBAL NumPy RNG every time pilots are made."""
-    np.random.seed(cell_id)
-    np.random.choice([1, -1], size=n)
+# ------------------------------------------------------------------ building blocks
+# the reference's core/resource_mapper.py, core/modulator.py and
+# core/demodulator.py classes (lte_phy.resource_mapper / .modulator / .demodulator)
+from .resource_mapper import LTEResourceGrid as ResourceGrid, _reseed_pilots  # noqa: E402,F401
+from .modulator import OFDMModulator, constellation  # noqa: E402,F401
+from .demodulator import OFDMDemodulator  # noqa: E402
+from .channel import AWGNChannel, FadingChannel, RayleighMultiPathChannel  # noqa: E402
 
 
 def _check_mode(mode, enable_sc_fdm):
@@ -124,31 +81,13 @@ def papr(signal):
 
 
 # ------------------------------------------------------------------ TX
-class _ModulatorView:
-    """Read-only stand-in for OFDMModulator's inspectable state."""
-
-    def __init__(self, config):
-        from types import SimpleNamespace
-        self.config = config
-        self.mode = 'lte'
-        self.enable_sc_fdm = False
-        self.qam_modulator = SimpleNamespace(modulation_type=config.modulation,
-                                             constellation=constellation(config.modulation),
-                                             get_constellation=lambda: constellation(config.modulation))
-        self.resource_mapper = SimpleNamespace(grid=ResourceGrid(config.N, config.Nc))
-        self.resource_mapper.get_data_indices = self.resource_mapper.grid.get_data_indices
-
-
 class OFDMTransmitter:
     """OFDMTransmitter (core/ofdm_core.py:42-155)."""
 
     def __init__(self, config: LTEConfig, mode: str = 'lte', enable_sc_fdm: bool = False):
-        sc = _check_mode(mode, enable_sc_fdm)
         self.config, self.mode, self.enable_sc_fdm = config, mode, enable_sc_fdm
-        self.modulator = _ModulatorView(config)
-        self.modulator.enable_sc_fdm = sc
-        self.modulator.mode = 'sc-fdm' if sc else mode
-        self.grid = self.modulator.resource_mapper.grid
+        self.modulator = OFDMModulator(config, mode=mode, enable_sc_fdm=enable_sc_fdm)
+        self.grid = ResourceGrid(config.N, config.Nc)
         self.last_signal_tx = self.last_symbols_tx = self.last_mapping_infos = None
 
     def _mapping_info(self, n_data):
@@ -159,11 +98,17 @@ class OFDMTransmitter:
                 'dc_index': g.dc_index, 'grid_statistics': g.get_statistics()}
 
     def modulate(self, bits) -> Tuple[np.ndarray, List[np.ndarray], List[Dict]]:
-        """OFDMModulator.modulate_stream (core/modulator.py:252-302) on the GPU."""
+        """OFDMModulator.modulate_stream (core/modulator.py:252-302) on the GPU:
+        an LTE / SC-FDM stream is one plan call (TX stage); mode 'simple'
+        goes through the modulator's per-symbol GPU stages."""
         if not isinstance(bits, np.ndarray):
             bits = np.array(bits, dtype=int)
         if bits.size == 0:
             raise ValueError("Bits array cannot be empty")
+        if self.modulator.mode not in ('lte', 'sc-fdm'):
+            sig, syms, infos = self.modulator.modulate_stream(bits)
+            self.last_signal_tx, self.last_symbols_tx, self.last_mapping_infos = sig, syms, infos
+            return sig, syms, infos
         cfg = self.config
         Nd = len(self.grid._data)
         n_sym = int(np.ceil(len(bits) / (Nd * cfg.bits_per_symbol)))
@@ -191,24 +136,16 @@ class OFDMTransmitter:
 
 
 # ------------------------------------------------------------------ RX
-class _DemodulatorView:
-    def __init__(self, config):
-        from types import SimpleNamespace
-        self.config = config
-        c = constellation(config.modulation)
-        self.qam_demodulator = SimpleNamespace(modulation_type=config.modulation, constellation=c,
-                                               get_constellation=lambda: c)
-
-
 class OFDMReceiver:
     """OFDMReceiver (core/ofdm_core.py:158-276)."""
 
     def __init__(self, config: LTEConfig, mode: str = 'lte', enable_equalization: bool = True,
                  enable_sc_fdm: bool = False):
-        self._sc = _check_mode(mode, enable_sc_fdm)
+        self._sc = bool(enable_sc_fdm) or mode == 'sc-fdm'
         self.config, self.mode = config, mode
         self.enable_equalization, self.enable_sc_fdm = enable_equalization, enable_sc_fdm
-        self.demodulator = _DemodulatorView(config)
+        self.demodulator = OFDMDemodulator(config, mode=mode, enable_equalization=enable_equalization,
+                                           enable_sc_fdm=enable_sc_fdm)
         self.grid = ResourceGrid(config.N, config.Nc)
         self.last_symbols_rx = self.last_bits_rx = self.channel_estimate = None
 
@@ -217,6 +154,10 @@ class OFDMReceiver:
         CP removal + FFT, slot-0 CRS estimation, ZF, nearest-point bits."""
         if signal_rx.size == 0:
             raise ValueError("Received signal cannot be empty")
+        if self.mode != 'lte':   # 'simple' (and the reference's other modes): the demodulator's GPU stages
+            syms, bits = self.demodulator.demodulate_stream(signal_rx)
+            self.last_symbols_rx, self.last_bits_rx = syms, bits
+            return syms, bits
         cfg = self.config
         sl = cfg.N + cfg.cp_length
         n_sym = max(1, len(signal_rx) // sl)
@@ -401,30 +342,71 @@ class OFDMChannel:
 
 
 class ChannelSimulator:
-    """ChannelSimulator (core/channel.py:297-493): 'awgn' and 'rayleigh_mp'
-    ('fading', FadingChannel, is outside the GPU path: NotImplementedError).
-    The fD rule and gain conversions are the reference's (doppler(), Q2)."""
+    """ChannelSimulator (core/channel.py:294-493) holding an AWGNChannel,
+    FadingChannel or RayleighMultiPathChannel (lte_phy.channel) as
+    `channel`.  The fD rule and gain conversions are the reference's
+    (doppler(), Q2)."""
 
     def __init__(self, channel_type='awgn', snr_db=10.0, fs=None, itu_profile='Vehicular_A', frequency_ghz=None,
                  velocity_kmh=None, verbose=True, *, precision: Optional[str] = None):
-        if channel_type == 'fading':
-            raise NotImplementedError("FadingChannel is outside the GPU path (SURVEY §8)")
-        if channel_type not in ('awgn', 'rayleigh_mp'):
-            raise ValueError(f"Tipo de canal desconocido: {channel_type}")
         self.channel_type, self.fs, self.itu_profile = channel_type, fs, itu_profile
         self.frequency_ghz, self.velocity_kmh = frequency_ghz, velocity_kmh
-        self._ch = OFDMChannel(channel_type, snr_db, fs, itu_profile, frequency_ghz, velocity_kmh, precision=precision)
+        self.precision = C.precision_of(precision)
+        if channel_type == 'awgn':
+            self.channel = AWGNChannel(snr_db, precision=self.precision)
+        elif channel_type == 'fading':
+            self.channel = FadingChannel(snr_db, precision=self.precision)
+        elif channel_type == 'rayleigh_mp':
+            if fs is None:
+                raise ValueError("Se requiere fs (frecuencia de muestreo) para canal Rayleigh")
+            self.channel = RayleighMultiPathChannel(snr_db, fs, itu_profile, frequency_ghz=frequency_ghz,
+                                                    velocity_kmh=velocity_kmh, verbose=verbose,
+                                                    precision=self.precision)
+        else:
+            raise ValueError(f"Tipo de canal desconocido: {channel_type}")
 
     @property
     def snr_db(self):
-        return self._ch.snr_db
+        return self.channel.snr_db
 
     def set_snr(self, snr_db):
-        self._ch.set_snr(snr_db)
+        self.channel.set_snr(snr_db)
 
     def transmit(self, signal):
         """core/channel.py:334-345."""
-        return self._ch.transmit(signal)
+        received, _ = self.channel.transmit(signal)
+        return received
+
+    def set_channel_type(self, channel_type, **kwargs):
+        """core/channel.py:351-373."""
+        self.channel_type = channel_type
+        snr = self.channel.snr_db if hasattr(self.channel, 'snr_db') else 10.0
+        if channel_type == 'awgn':
+            self.channel = AWGNChannel(snr, precision=self.precision)
+        elif channel_type == 'fading':
+            self.channel = FadingChannel(snr, precision=self.precision)
+        elif channel_type == 'rayleigh_mp':
+            if self.fs is None:
+                raise ValueError("Se requiere fs para cambiar a canal Rayleigh")
+            self.itu_profile = kwargs.get('itu_profile', self.itu_profile)
+            self.channel = RayleighMultiPathChannel(snr, self.fs, self.itu_profile, precision=self.precision)
+        else:
+            raise ValueError(f"Tipo de canal desconocido: {channel_type}")
+
+    def set_itu_profile(self, itu_profile):
+        if isinstance(self.channel, RayleighMultiPathChannel):
+            self.channel.set_profile(itu_profile)
+            self.itu_profile = itu_profile
+        else:
+            raise ValueError("Solo se puede cambiar perfil ITU en canal Rayleigh")
+
+    def get_channel(self):
+        return self.channel
+
+    def get_channel_info(self):
+        if hasattr(self.channel, 'get_channel_info'):
+            return self.channel.get_channel_info()
+        return {'type': self.channel_type, 'SNR_dB': self.channel.snr_db if hasattr(self.channel, 'snr_db') else None}
 
     def transmit_spatial_multiplexing(self, tx_signals, num_rx=2):
         """core/channel.py:397-493 on the device (lte_channel_mimo_host mode 1).
@@ -436,10 +418,14 @@ class ChannelSimulator:
         reference's order."""
         num_tx = len(tx_signals)
         L = min(len(sg) for sg in tx_signals)
-        ch = self._ch
-        ray = ch.rayleigh
+        if self.channel_type == 'fading':
+            raise NotImplementedError("transmit_spatial_multiplexing on 'fading' links is outside the GPU path")
+        ray = self.channel_type == 'rayleigh_mp'
+        snr_db = self.channel.snr_db
+        fD = self.channel.rayleigh.fD if ray else 0.0
+        kind = C.CH_RAYLEIGH if ray else C.CH_AWGN
         C.device_init()
-        f64 = ch.precision == 'f64'
+        f64 = self.precision == 'f64'
         cdt, rdt, ct = (np.complex128, np.float64, C.F64) if f64 else (np.complex64, np.float32, C.F32)
         x = np.ascontiguousarray(np.stack([np.asarray(sg)[:L] for sg in tx_signals]), dtype=cdt)
         if ray:
@@ -472,8 +458,8 @@ class ChannelSimulator:
         g = np.array(gains, dtype=np.float64)
         fn = C.load().lte_channel_mimo_host64 if f64 else C.load().lte_channel_mimo_host
         C.check(fn(
-            L, num_tx, num_rx, 1, ch.kind, P, C.ptr(dl, C.I32) if P else None, C.ptr(g, C.F64) if P else None,
-            float(ch.fD), float(self.fs or 0.0), float(ch.snr_db), 0, C.ptr(x.view(rdt), ct),
+            L, num_tx, num_rx, 1, kind, P, C.ptr(dl, C.I32) if P else None, C.ptr(g, C.F64) if P else None,
+            float(fD), float(self.fs or 0.0), float(snr_db), 0, C.ptr(x.view(rdt), ct),
             C.ptr(ph, C.F64) if ray else None, None, None if ray else C.ptr(lh, C.F64), C.ptr(z, C.F64),
             C.ptr(y.view(rdt), ct), None, None))
         return list(y.astype(np.complex128)), Hm
@@ -494,6 +480,7 @@ class OFDMSimulator:
         'f32' (fast mode)."""
         if config is None:
             config = LTEConfig()
+        _check_mode(mode, enable_sc_fdm)   # the simulator chains map REs the LTE way
         self.precision = C.precision_of(precision)
         self.config, self.channel_type, self.mode = config, channel_type, mode
         self.enable_sc_fdm, self.enable_equalization = enable_sc_fdm, enable_equalization
@@ -746,6 +733,14 @@ class OFDMSimulator:
         return self._simulate_sfbc(bits, snr_db, num_rx, 'MIMO-SFBC')
 
     # -------------------------------------------------------------- sweeps
+    def get_config(self) -> LTEConfig:
+        """OFDMSimulator.get_config (core/ofdm_core.py:2479-2481)."""
+        return self.config
+
+    def __repr__(self) -> str:
+        return (f"OFDMSimulator({self.config.modulation}, {'SC-FDM' if self.enable_sc_fdm else 'OFDM'}, "
+                f"{self.channel_type}, {len(self.channels)}ch)")
+
     def run_ber_sweep(self, num_bits: int, snr_range, num_trials: int = 1,
                       progress_callback: Optional[callable] = None) -> Dict:
         """core/ofdm_core.py:1795-1846.  Bits are drawn once from the global RNG;

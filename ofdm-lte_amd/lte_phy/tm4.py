@@ -145,6 +145,24 @@ class LTECodebook:
         w_opt = (np.conj(h) / np.linalg.norm(h)).reshape(-1, 1)
         return 1 - np.abs(np.vdot(w_opt.flatten(), self.get_precoder(pmi).flatten())) ** 2
 
+    def print_codebook(self):
+        """core/codebook_lte.py:413-433 (debug printout)."""
+        print(f"\n{'=' * 60}")
+        print(f"Codebook LTE - {self.transmission_mode} - {self.num_tx} TX")
+        print(f"{'=' * 60}")
+        for pmi, W in enumerate(self.codebook):
+            print(f"\nPMI = {pmi}:")
+            print(f"  W shape: {W.shape}")
+            print("  W = ")
+            for row in W:
+                real = row.real if np.abs(row.real) > 1e-10 else 0
+                imag = row.imag if np.abs(row.imag) > 1e-10 else 0
+                if imag >= 0:
+                    print(f"    {real:.3f} + {imag:.3f}j")
+                else:
+                    print(f"    {real:.3f} - {abs(imag):.3f}j")
+        print(f"\n{'=' * 60}")
+
     def get_codebook_info(self):
         return {'num_tx': self.num_tx, 'transmission_mode': self.transmission_mode,
                 'codebook_size': self.codebook_size, 'num_layers': self.codebook[0].shape[1],
@@ -254,6 +272,16 @@ class LayerMapper:
     def get_padded_length(self, total_symbols):
         return total_symbols if self.num_layers == 1 else \
             int(np.ceil(total_symbols / self.num_layers)) * self.num_layers
+
+
+class LayerDemapper:
+    """LayerDemapper (core/layer_mapper.py:153-161): LayerMapper.demap_from_layers."""
+
+    def __init__(self, num_layers):
+        self.mapper = LayerMapper(num_layers)
+
+    def demap(self, layers, original_length=None):
+        return self.mapper.demap_from_layers(layers, original_length)
 
 
 class MIMODetector:

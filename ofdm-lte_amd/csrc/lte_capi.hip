@@ -239,6 +239,14 @@ GridHost make_grid(int N, int Nc, int cp) {
   return g;
 }
 
+// Grid::kinfo: data ordinal, -(pilot ordinal + 2) or -1 per subcarrier
+std::vector<int32_t> make_kinfo(const GridHost& g) {
+  std::vector<int32_t> k(g.N, -1);
+  for (int j = 0; j < g.Nd; ++j) k[g.data[j]] = j;
+  for (int i = 0; i < g.Np; ++i) k[g.pilot[i]] = -(i + 2);
+  return k;
+}
+
 std::vector<float2> make_constellation(int bps) {  // modulator.py:28-59
   std::vector<float2> c;
   if (bps == 2) {
@@ -333,14 +341,14 @@ void make_pilots(int cell, int n, std::vector<double>& re_im) {
 }
 
 struct TableSet {  // device copies of the static grid tables for one N (f64 copies in f64 plans)
-  DBuf<int32_t> data, pilot, seg;
+  DBuf<int32_t> data, pilot, seg, kinfo;
   DBuf<float> inv_gap;
   DBuf<float2> pilots, tw, constel, chirp, bhat;
   DBuf<double> inv_gap64;
   DBuf<double2> pilots64, tw64, chirp64, bhat64;
   void release() {
-    data.release(); pilot.release(); seg.release(); inv_gap.release(); pilots.release(); tw.release();
-    constel.release(); chirp.release(); bhat.release();
+    data.release(); pilot.release(); seg.release(); kinfo.release(); inv_gap.release(); pilots.release();
+    tw.release(); constel.release(); chirp.release(); bhat.release();
     inv_gap64.release(); pilots64.release(); tw64.release(); chirp64.release(); bhat64.release();
   }
 };
@@ -949,7 +957,7 @@ static int plan_tables(lte_plan* p) {
   std::vector<float2> pil(p->Np);
   for (int i = 0; i < p->Np; ++i) pil[i] = make_float2((float)pr[2 * i], (float)pr[2 * i + 1]);
   if (upload(p->tabs.data, p->gh.data) || upload(p->tabs.pilot, p->gh.pilot) || upload(p->tabs.seg, p->gh.seg) ||
-      upload(p->tabs.inv_gap, p->gh.inv_gap) || upload(p->tabs.pilots, pil) ||
+      upload(p->tabs.inv_gap, p->gh.inv_gap) || upload(p->tabs.pilots, pil) || upload(p->tabs.kinfo, make_kinfo(p->gh)) ||
       upload(p->tabs.tw, make_twiddles(d.N)) || upload(p->tabs.constel, make_constellation(d.bps)))
     return fail(LTE_ENOMEM, "table upload failed");
   if (d.sc_fdm) {   // SC-FDM DFT of size M = Nd (DFTPrecodifier, core/dft_precoding.py:20-118)
@@ -1492,7 +1500,8 @@ int lte_plan_create(const lte_plan_desc* desc, lte_plan** out) {
                  p->tabs.tw.p, p->tabs.constel.p,
                  (float)(d.bps == 2 ? std::sqrt(2.0) : d.bps == 4 ? std::sqrt(10.0) : std::sqrt(42.0)),
                  p->tabs.chirp.p, p->tabs.bhat.p, d.no_equalization && d.chain == LTE_CHAIN_UNCODED ? 1 : 0,
-                 p->tabs.pilots64.p, p->tabs.inv_gap64.p, p->tabs.tw64.p, p->tabs.chirp64.p, p->tabs.bhat64.p};
+                 p->tabs.pilots64.p, p->tabs.inv_gap64.p, p->tabs.tw64.p, p->tabs.chirp64.p, p->tabs.bhat64.p,
+                 p->tabs.kinfo.p};
   if (d.channel == LTE_CH_RAYLEIGH) {
     std::vector<int32_t> dl(d.delays, d.delays + d.n_paths);
     for (int i = 0; i < d.n_paths; ++i)

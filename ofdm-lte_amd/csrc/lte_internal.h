@@ -35,6 +35,9 @@ struct Grid {                 // device pointers + numerology for one plan
   const double2* tw64;
   const double2* chirp64;
   const double2* bhat64;
+  // per-subcarrier role for the wave-private receivers: data ordinal j >= 0,
+  // pilot ordinal p as -(p + 2), -1 guard / DC  [N]
+  const int32_t* kinfo;
 };
 // precision-selected table accessors (R = float / double)
 template <class R> struct GridT;
@@ -150,6 +153,15 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
 // uncoded, one RX, no SC-FDM.  nv_out set: llr takes z per RE and nv_out
 // sigma^2_eff per (frame, group, data subcarrier); H / pstats: optional captures.
 bool rx_frame_supported(const Grid& g, int chain, int num_rx, int sc_fdm);
+// wave-private f64 coded receiver (lte_wave.hip): k_rx_frame's outputs (ZN demap:
+// equalised symbols zo + sigma^2_eff nv_out) for N = 2048; launch_rx_frame
+// dispatches to it unless LTE_RX_WAVE=0
+bool rx_frame_w_supported(const Grid& g, int chain, int f64);
+int rx_wave_enabled();
+int launch_rx_frame_w(hipStream_t s, const Grid& g, int rayleigh, int B, const double2* y, int64_t y_frame_stride,
+                      const double* npow, const double* snr_lin, const uint64_t* fid, uint64_t seed,
+                      const double* inj_z, int64_t inj_stride, double* zo, double* nv_out, double2* cap_syms,
+                      double2* H, double* pstats);
 template <class R>
 int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, const cx<R>* y,
                     int64_t y_frame_stride, const R* npow, const R* snr_lin, const uint64_t* fid, uint64_t seed,

@@ -423,7 +423,7 @@ def stage_bytes_per_frame(config, plan, prec):
       them (SISO / SIMO: k_chan_fix rebuilds the stream's first samples);
       configs 4/5 keep the CP (the link power is measured over it).
     * The receivers read n_sym x N samples per RX (the CP is stripped).
-    * Config 5 (spatial, no H capture): k_rx_fft_mimo hands the detector the
+    * Config 5 (spatial, no H capture): k_rx_fft_mimo(_w) hands the detector the
       LS pilot estimates, nr x n_est x nt x pilots-per-TX (LTE_SPATIAL_HP),
       not the interpolated H.
     * Flat links (config 5 'awgn'): TX and links are one pass
@@ -462,9 +462,15 @@ def stage_bytes_per_frame(config, plan, prec):
     stream = L * c                            # one antenna's stream with CP
     if config == 4:
         res = plan.res
+        # the merged link noise (default: LTE_SFBC_LINK_MERGE) folds the link noise into the receiver's draw:
+        # the 'channel' stage is then the per-RX noise powers from the TX's power partials
+        merged = os.environ.get('LTE_SFBC_LINK_MERGE', '1') != '0'
+        chan = ((['k_npow_sfbc_merged', 'k_link_sigma'], 2 * nr * nt * esz + 3 * nr * esz,
+                 'link and RX power partials in, the link sigmas and noise powers out') if merged else
+                (['k_link_noise_pairs'], 2 * nr * stream, 'each RX stream in and out (+ link noise)'))
         return {'ofdm_tx': (['k_ofdm_txch_sfbc'], plan.coded_bits / 8 + nr * stream,
                             'coded bits in, each RX antenna\'s faded stream (with CP) out'),
-                'channel': (['k_link_noise_pairs'], 2 * nr * stream, 'each RX stream in and out (+ link noise)'),
+                'channel': chan,
                 'rx_chest': (['k_rx_sfbc'], nr * sym + n_sym * res * c + n_sym * (res // 2) * esz,
                              'each RX stream (no CP) in; combined symbols + sigma^2_eff per RE pair out'),
                 'dematch': (['k_dematch_zn'], n_sym * res * c + n_sym * (res // 2) * esz + rows * esz,
@@ -472,7 +478,9 @@ def stage_bytes_per_frame(config, plan, prec):
     y = n_sym * nr * plan.n_dsc * c           # data-SC values per RX and symbol
     hp = nr * plan.n_est * nt * plan.pilots_per_tx * c   # LS pilot estimates
     flat = plan.channel == 0
-    out = {'rx_chest': (['k_rx_fft_mimo'], nr * sym + y + hp,
+    # float64: the wave-private receiver (k_rx_fft_mimo_w, the default; LTE_MIMO_RX_WAVE=0 the block kernel)
+    wave = prec == 'f64' and plan.N == 2048 and os.environ.get('LTE_MIMO_RX_WAVE', '1') != '0'
+    out = {'rx_chest': (['k_rx_fft_mimo_w' if wave else 'k_rx_fft_mimo'], nr * sym + y + hp,
                         'each RX stream (no CP) in; data-SC values + LS pilot estimates out'),
            'rx_data': (['k_det_spatial'], y + hp + bits, 'data-SC values + pilot estimates + payload bits in')}
     if flat:
@@ -488,8 +496,8 @@ def stage_bytes_per_frame(config, plan, prec):
 
 # the committed rocprofv3 --pmc summary of each config's bench step (the
 # traffic beside each stage's algorithmic bytes; tests/test_roofline_pmc.py)
-PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r5_pmc_c3_final.json', 4: 'r5_pmc_c4_final.json',
-             5: 'r5_pmc_c5_hp.json'}
+PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r5_pmc_c3_final.json', 4: 'r6_pmc_c4_merged.json',
+             5: 'r6_pmc_c5.json'}
 
 
 def pmc_stage_bytes(pmc, kernels):
@@ -665,7 +673,7 @@ DRY_GEOM = {
 }
 DRY_STAGE_SHARE = {2: {'turbo': 0.87, 'ofdm_tx': 0.04, 'rx_data': 0.045, 'dematch': 0.03},
                    3: {'ofdm_tx': 0.3, 'channel': 0.02, 'rx_data': 0.65},
-                   4: {'turbo': 0.69, 'ofdm_tx': 0.08, 'channel': 0.1, 'rx_chest': 0.07, 'dematch': 0.03},
+                   4: {'turbo': 0.75, 'ofdm_tx': 0.08, 'channel': 0.001, 'rx_chest': 0.08, 'dematch': 0.03},
                    5: {'ofdm_tx': 0.25, 'fading': 0.001, 'channel': 0.001, 'rx_chest': 0.45, 'rx_data': 0.2}}
 
 

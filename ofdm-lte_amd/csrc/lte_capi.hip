@@ -1707,8 +1707,17 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   int npow_nblk = nch;   // RX power partials per (frame, RX) that k_npow_mimo sums
   const bool sfbc_fuse = link_noise && !inj_lz && !inj_z && !a->cap_signal_tx && !a->cap_link_stats &&
                          sfbc_txch_supported<R>(g, m, d.n_paths, maxd) && env_on("LTE_SFBC_TXCH_FUSE", true);
+  // the merged link noise (launch_npow_sfbc_merged): the fused TX, then one
+  // noise draw per RX sample in the fused receiver -- only when nothing
+  // observes the received streams or noise powers in between
+  const bool zn0_ = coded && (d.bps == 4 || d.bps == 6) && !a->cap_llr && (m.res & 1) == 0 && m.n_dsc <= m.res &&
+                    env_on("LTE_DEMAP_IN_DEMATCH", true);
+  const bool sfbc_merge = sfbc_fuse && !a->cap_signal_rx && !a->cap_noise_power && !a->cap_H && !a->cap_data_syms &&
+                          !(a->cap_bits_rx && !coded) && (zn0_ || !coded) && rx_sfbc_supported<R>(g, m) &&
+                          env_on("LTE_SFBC_RX_FUSE", true) && env_on("LTE_SFBC_LINK_MERGE", true);
   if (sfbc_fuse) {
-    const TxLinkPower<R> lf{p->delays.p, c.coef.p, c.link_part.p, d.n_paths, maxd, 1};
+    TxLinkPower<R> lf{p->delays.p, c.coef.p, c.link_part.p, d.n_paths, maxd, 1};
+    if (sfbc_merge) lf.rx_part = c.pow_part.p;
     {
       Timer t(p, KN_OFDM_TX);
       LCHK(launch_ofdm_txch_sfbc<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, lf,
@@ -1718,8 +1727,12 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     // the next chunk's TX measured no overlap: TX + noise 67.3-68.0 ms per
     // 65 536 frames with 1, 2, 4 or 8 chunks)
     Timer t(p, KN_CHANNEL);
-    LCHK(launch_link_noise_add<R>(s, g, m, B, c.link_part.p, c.link_sigma.p, c.y.p, p->fid.p, a->seed,
-                                  c.pow_part.p, &npow_nblk));
+    if (sfbc_merge)
+      LCHK(launch_npow_sfbc_merged<R>(s, B, m.num_rx, m.num_tx, c.link_part.p, c.link_sigma.p, c.pow_part.p, p->L,
+                                      c.snr_lin.p, c.npow.p));
+    else
+      LCHK(launch_link_noise_add<R>(s, g, m, B, c.link_part.p, c.link_sigma.p, c.y.p, p->fid.p, a->seed,
+                                    c.pow_part.p, &npow_nblk));
   } else if (flat_fuse) {
     Timer t(p, KN_OFDM_TX);
     LCHK(launch_ofdm_txch_flat<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p,
@@ -1736,7 +1749,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                                 c.y.p, link_noise ? 1 : 0, p->fid.p, a->seed, inj_lz, inj_lz_stride, c.link_part.p,
                                 c.link_sigma.p, c.pow_part.p, p->nblk, lp_fuse ? 1 : 0));
   }
-  {
+  if (!sfbc_merge) {
     Timer t(p, KN_CHANNEL);
     // noise per RX: SFBC (P / num_tx) / SNR (core/ofdm_core.py:524-534); spatial P / SNR (channel.py:457-467)
     LCHK(launch_npow_mimo<R>(s, B, m.num_rx, c.pow_part.p, npow_nblk, p->L, c.snr_lin.p, sfbc ? (double)m.num_tx : 1.0,
@@ -1751,6 +1764,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   const bool rx_fuse = sfbc && !inj_z && !a->cap_H && !a->cap_data_syms && !(a->cap_bits_rx && !coded) &&
                        (zn0 || !coded) &&
                        rx_sfbc_supported<R>(g, m) && env_on("LTE_SFBC_RX_FUSE", true);
+  if (sfbc_merge && !rx_fuse) return fail(LTE_EINVAL, "merged link noise without the fused SFBC receiver");
   // spatial multiplexing without a capture of H: the receiver hands over each
   // estimation symbol's LS pilot estimates and the detector interpolates them
   // per RE (the same mimo_interp), instead of a round trip of the interpolated

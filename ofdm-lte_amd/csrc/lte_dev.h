@@ -365,68 +365,4 @@ __device__ __forceinline__ void jakes_symbol_sets(const double (&ph)[16], double
   }
 }
 
-
-// ---------------------------------------------------------------------------
-// Receiver pieces shared by k_rx_* (lte_kernels.hip) and the wave-private
-// receivers (lte_wave.hip)
-// |h|^2 as the reference forms it: f64 np.abs(h) ** 2 (hypot, then squared);
-// f32 h.x^2 + h.y^2
-template <class V>
-__device__ __forceinline__ re_t<V> abs2_ref(V h) {
-  if constexpr (sizeof(re_t<V>) == 8) {
-    const double a = hypot(h.x, h.y);
-    return a * a;
-  } else {
-    return h.x * h.x + h.y * h.y;
-  }
-}
-
-
-template <class R> struct ZfCoef;
-template <> struct ZfCoef<double> {   // cdiv(y, h) (Smith, lte_common.h) with the h-only terms precomputed
-  double rat, sre, sim;
-  bool swp;
-  __device__ __forceinline__ void set(double2 h) {
-    swp = !(fabs(h.x) >= fabs(h.y));
-    if (!swp) {
-      rat = (h.x == 0.0 && h.y == 0.0) ? 0.0 : h.y / h.x;   // h = 0: a / 0 as cdiv
-      sre = sim = (h.x == 0.0 && h.y == 0.0) ? 1.0 / h.x : 1.0 / (h.x + h.y * rat);
-    } else {
-      rat = h.x / h.y;
-      sre = 1.0 / (h.y + h.x * rat);
-      sim = -sre;
-    }
-  }
-  // !swp: ((a.x + a.y rat) s, (a.y - a.x rat) s); swp: ((a.x rat + a.y) s, (a.y rat - a.x) s)
-  __device__ __forceinline__ double2 apply(double2 a) const {
-    const double u = swp ? a.x : a.y, v = swp ? a.y : a.x;
-    return make_double2((v + u * rat) * sre, (u - v * rat) * sim);
-  }
-};
-template <> struct ZfCoef<float> {    // zf_div(y, h): y conj(h) / |h|^2
-  float2 h;
-  float r;
-  __device__ __forceinline__ void set(float2 hh) {
-    h = hh;
-    r = 1.0f / (hh.x * hh.x + hh.y * hh.y);
-  }
-  __device__ __forceinline__ float2 apply(float2 y) const {
-    return make_float2((y.x * h.x + y.y * h.y) * r, (y.y * h.x - y.x * h.y) * r);
-  }
-};
-
-// linear interpolation of the pilot LS estimates hp at subcarrier k with edge
-// hold (lte_receiver.py:114-133), as k_rx_chest forms it
-template <class R>
-__device__ __forceinline__ cx<R> chest_interp(const Grid& g, const cx<R>* hp, int k) {
-  using V = cx<R>;
-  const int sidx = g.seg[k];
-  if (sidx < 0) return hp[0];
-  if (sidx >= g.Np - 1) return hp[g.Np - 1];
-  const V v0 = hp[sidx], v1 = hp[sidx + 1];
-  const R fk = (R)(k - g.pilot_idx[sidx]);
-  const R ig = GridT<R>::inv_gap(g)[sidx];
-  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
-}
-
 }  // namespace lte

@@ -129,6 +129,13 @@ template <class R>
 int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map,
                     const int32_t* txf_map, const int32_t* txf_re, int B, cx<R>* cap_syms,
                     const TxChannelT<R>& ch);
+// wave-private f64 coded TX + static taps (lte_wave.hip), N = 2048, SISO, four
+// paths with every delay <= 64: launch_ofdm_txf's outputs; it dispatches to
+// it with LTE_TX_WAVE=1 (off by default)
+bool txf_w_supported(const Grid& g, int f64, int n_paths, int max_delay, int num_rx, int tv);
+int tx_wave_enabled();
+int launch_ofdm_txf_w(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map, int B,
+                      double2* cap_syms, const TxChannelT<double>& ch);
 // the lane order: for each OFDM symbol a permutation of its Nd data REs over
 // the N/2 TX slots, greedy per 32-slot group (one ds_read_b32 lane group) so
 // that each of the bps coded-bit gathers sees as few distinct words per LDS
@@ -155,7 +162,7 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
 bool rx_frame_supported(const Grid& g, int chain, int num_rx, int sc_fdm);
 // wave-private f64 coded receiver (lte_wave.hip): k_rx_frame's outputs (ZN demap:
 // equalised symbols zo + sigma^2_eff nv_out) for N = 2048; launch_rx_frame
-// dispatches to it unless LTE_RX_WAVE=0
+// dispatches to it with LTE_RX_WAVE=1 (off by default)
 bool rx_frame_w_supported(const Grid& g, int chain, int f64);
 int rx_wave_enabled();
 int launch_rx_frame_w(hipStream_t s, const Grid& g, int rayleigh, int B, const double2* y, int64_t y_frame_stride,
@@ -304,6 +311,9 @@ struct TxLinkPower {
   const cx<R>* coef;       // [B][num_rx][num_tx][n_paths][mimo_ncf<R>()] (n_cs = 1)
   R* part;                 // [B][num_rx][num_tx][nblk]
   int n_paths, max_delay, nblk;
+  // k_ofdm_txch_sfbc only, non-null: also each RX stream's power sum_n |y0_r|^2
+  // ([B][num_rx], one partial per frame and RX) for the merged link noise
+  R* rx_part;
 };
 template <class R>
 int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
@@ -332,6 +342,19 @@ template <class R>
 int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
                           const uint32_t* enc, int enc_words, const int32_t* tx_map, const TxLinkPower<R>& lp,
                           cx<R>* y, int B);
+// config 4's merged link noise (Philox mode, full chain, no capture of the
+// received streams or noise powers): instead of adding the RX's 100 dB link
+// noise to y0_r (k_link_noise_pairs) and measuring the noisy power, the RX's
+// one noise draw in the receiver carries both, per RX
+//   s2 = sum_t s_rt^2 (k_link_sigma's per-link standard deviations),
+//   P = sum_n |y0_r|^2 / L + 2 s2 (the link noise's power in expectation),
+//   npow_awgn = (P / num_tx) / snr,  npow_eff = 2 s2 + npow_awgn,
+// and k_rx_sfbc draws sqrt(npow_eff / 2) per component: the same distribution
+// as the two draws (independent Gaussians add) with P's link-noise term
+// (~1e-10 of P) in expectation.  oracle/philox.sfbc_draws(merged=True).
+template <class R>
+int launch_npow_sfbc_merged(hipStream_t s, int B, int num_rx, int num_tx, const R* link_part, R* link_sigma,
+                            const R* rx_part, int L, const R* snr_lin, R* npow);
 template <class R>
 int launch_link_noise_add(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
                           cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part, int* pow_nblk);
@@ -355,6 +378,14 @@ int launch_link_stats(hipStream_t s, const Grid& g, const MimoGrid& m, int B, in
 template <class R>
 int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nblk, int L, const R* snr_lin,
                      double div, R* npow);
+// wave-private f64 RX FFT + CRS pilot estimates (lte_wave.hip), N = 2048, the
+// pilot-estimate handoff: launch_rx_fft_mimo's outputs; it dispatches to it
+// unless LTE_MIMO_RX_WAVE=0
+bool rx_fft_mimo_w_supported(const Grid& g, const MimoGrid& m, int f64, int h_pilots);
+int mimo_rx_wave_enabled();
+int launch_rx_fft_mimo_w(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const double2* y, const double* npow,
+                         const uint64_t* fid, uint64_t seed, const double* inj_z, int64_t inj_stride, double2* Y,
+                         double2* H);
 template <class R>
 // h_pilots: H receives the LS pilot estimates [b][rx][e][tx][maxP] instead of
 // the interpolated [b][rx][e][tx][n_dsc] (launch_det_spatial's h_pilots

@@ -604,6 +604,10 @@ int launch_ofdm_txf(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_w
                     const TxChannelT<R>& ch) {
   const int spw = WG / (g.N >> 3);
   if (!txch_supported(g, ch.n_paths, ch.max_delay) || (g.bps != 2 && g.bps != 4 && g.bps != 6)) return (int)hipErrorInvalidValue;
+  if constexpr (sizeof(R) == 8)
+    if (!txf_map && txf_w_supported(g, 1, ch.n_paths, ch.max_delay, ch.num_rx, ch.tcoef != nullptr) &&
+        tx_wave_enabled())
+      return launch_ofdm_txf_w(s, g, enc, enc_words, tx_map, B, cap_syms, ch);
   const size_t shm = (size_t)spw * g.N * sizeof(cx<R>) + (TXF_STAGE ? (size_t)spw * enc_words * sizeof(uint32_t) : 0);
   if (shm > 65536) return (int)hipErrorInvalidValue;
   // symbol pairs (LTE_TXF_SP = 2): two grids and one staged copy per frame
@@ -1180,6 +1184,25 @@ int launch_rx_chest(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>
   return (int)hipGetLastError();
 }
 
+// float32 |h|^2 never contracted: rounded products, then their sum, in every
+// instance (left to the compiler, one receiver instance formed it as an FMA and
+// another not, and their f32 sigma^2_eff -- hence LLRs -- parted by an ulp)
+__device__ __forceinline__ float abs2_nc(float2 h) {
+#pragma clang fp contract(off)
+  return h.x * h.x + h.y * h.y;
+}
+// |h|^2 as the reference forms it: f64 np.abs(h) ** 2 (hypot, then squared);
+// f32 h.x^2 + h.y^2
+template <class V>
+__device__ __forceinline__ re_t<V> abs2_ref(V h) {
+  if constexpr (sizeof(re_t<V>) == 8) {
+    const double a = hypot(h.x, h.y);
+    return a * a;
+  } else {
+    return abs2_nc(h);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Hard decision / soft demap.  Natural-binary QAM, I-level-major index
 // (modulator.py:28-59, Q9): bits = [I-level bits | Q-level bits], MSB first.
@@ -1326,6 +1349,53 @@ __global__ __launch_bounds__(WG) void k_rx_data(Grid g, int rayleigh, int B, int
 // RE.  H is never re-read from HBM (written only for a capture).  Same
 // arithmetic per RE as k_rx_chest + k_rx_data (parity test
 // test_fused_receiver_matches_separate_kernels).
+template <class R> struct ZfCoef;
+template <> struct ZfCoef<double> {   // cdiv(y, h) (Smith, lte_common.h) with the h-only terms precomputed
+  double rat, sre, sim;
+  bool swp;
+  __device__ __forceinline__ void set(double2 h) {
+    swp = !(fabs(h.x) >= fabs(h.y));
+    if (!swp) {
+      rat = (h.x == 0.0 && h.y == 0.0) ? 0.0 : h.y / h.x;   // h = 0: a / 0 as cdiv
+      sre = sim = (h.x == 0.0 && h.y == 0.0) ? 1.0 / h.x : 1.0 / (h.x + h.y * rat);
+    } else {
+      rat = h.x / h.y;
+      sre = 1.0 / (h.y + h.x * rat);
+      sim = -sre;
+    }
+  }
+  // !swp: ((a.x + a.y rat) s, (a.y - a.x rat) s); swp: ((a.x rat + a.y) s, (a.y rat - a.x) s)
+  __device__ __forceinline__ double2 apply(double2 a) const {
+    const double u = swp ? a.x : a.y, v = swp ? a.y : a.x;
+    return make_double2((v + u * rat) * sre, (u - v * rat) * sim);
+  }
+};
+template <> struct ZfCoef<float> {    // zf_div(y, h): y conj(h) / |h|^2
+  float2 h;
+  float r;
+  __device__ __forceinline__ void set(float2 hh) {
+    h = hh;
+    r = 1.0f / (hh.x * hh.x + hh.y * hh.y);
+  }
+  __device__ __forceinline__ float2 apply(float2 y) const {
+    return make_float2((y.x * h.x + y.y * h.y) * r, (y.y * h.x - y.x * h.y) * r);
+  }
+};
+
+// linear interpolation of the pilot LS estimates hp at subcarrier k with edge
+// hold (lte_receiver.py:114-133), as k_rx_chest forms it
+template <class R>
+__device__ __forceinline__ cx<R> chest_interp(const Grid& g, const cx<R>* hp, int k) {
+  using V = cx<R>;
+  const int sidx = g.seg[k];
+  if (sidx < 0) return hp[0];
+  if (sidx >= g.Np - 1) return hp[g.Np - 1];
+  const V v0 = hp[sidx], v1 = hp[sidx + 1];
+  const R fk = (R)(k - g.pilot_idx[sidx]);
+  const R ig = GridT<R>::inv_gap(g)[sidx];
+  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+}
+
 #ifndef RXF_EXP
 #define RXF_EXP 0
 #endif
@@ -1470,7 +1540,6 @@ bool rx_frame_supported(const Grid& g, int chain, int num_rx, int sc_fdm) {
   return num_rx == 1 && !sc_fdm && (chain == LTE_CHAIN_CODED || chain == LTE_CHAIN_UNCODED) &&
          (g.bps == 2 || g.bps == 4 || g.bps == 6) && 2 * g.Nd < g.N;
 }
-
 
 template <class R>
 int launch_rx_frame(hipStream_t s, const Grid& g, int chain, int rayleigh, int B, const cx<R>* y,

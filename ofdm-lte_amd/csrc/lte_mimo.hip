@@ -961,11 +961,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
   int dl[PM];
 #pragma unroll
   for (int p = 0; p < PM; ++p) dl[p] = p < np ? lp.delays[p] : 0;
-  R pwr[NRX][NTX];
+  R pwr[NRX][NTX], prx[NRX];
 #pragma unroll
-  for (int r = 0; r < NRX; ++r)
+  for (int r = 0; r < NRX; ++r) {
+    prx[r] = (R)0;
 #pragma unroll
     for (int t = 0; t < NTX; ++t) pwr[r][t] = (R)0;
+  }
   const R sc = tx_scale<R>(N);
   constexpr int SFP = 4 * T / TPB;   // Alamouti pairs per thread per symbol (n_dsc / 2 <= SFP TPB)
   // (each pair's grid positions held in registers across the symbols instead of
@@ -1065,7 +1067,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
             if (p < np) a[t] = cadd(a[t], cmul(c[r][t][p], xs[t][p]));
           pwr[r][t] += a[t].x * a[t].x + a[t].y * a[t].y;
         }
-        yl[(size_t)r * g.L + n] = cadd(a[0], a[1]);
+        const V yr = cadd(a[0], a[1]);
+        yl[(size_t)r * g.L + n] = yr;
+        prx[r] += yr.x * yr.x + yr.y * yr.y;
       }
     }
     __syncthreads();   // every read of the old tails and of the grids done
@@ -1083,6 +1087,43 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
       if (threadIdx.x == 0) lp.part[((size_t)b * NRX + r) * NTX + t] = v;   // one partial per link (nblk 1)
       __syncthreads();
     }
+  if (lp.rx_part) {   // the merged link noise: each RX stream's power (one partial per frame and RX)
+#pragma unroll
+    for (int r = 0; r < NRX; ++r) {
+      const R v = block_sum(prx[r], red);
+      if (threadIdx.x == 0) lp.rx_part[(size_t)b * NRX + r] = v;
+      __syncthreads();
+    }
+  }
+}
+
+// launch_npow_sfbc_merged (lte_internal.h): npow_eff per (frame, RX), in the
+// order oracle/mimo_oracle.transmit_mimo (merged) forms it
+template <class R>
+__global__ void k_npow_sfbc_merged(int n, int num_rx, int num_tx, const R* __restrict__ link_sigma,
+                                   const R* __restrict__ rx_part, int L, const R* __restrict__ snr_lin,
+                                   R* __restrict__ npow) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s2 = 0.0;
+  for (int t = 0; t < num_tx; ++t) {
+    const double st = (double)link_sigma[(size_t)i * num_tx + t];
+    s2 = s2 + st * st;
+  }
+  const double P = (double)rx_part[i] / L + 2.0 * s2;
+  const double na = (P / (double)num_tx) / (double)snr_lin[i / num_rx];
+  npow[i] = (R)(2.0 * s2 + na);
+}
+
+template <class R>
+int launch_npow_sfbc_merged(hipStream_t s, int B, int num_rx, int num_tx, const R* link_part, R* link_sigma,
+                            const R* rx_part, int L, const R* snr_lin, R* npow) {
+  const int n = B * num_rx, nl = n * num_tx;   // one link partial per link (k_ofdm_txch_sfbc)
+  hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, 1, L, link_sigma);
+  hipLaunchKernelGGL(k_npow_sfbc_merged<R>, dim3((n + 255) / 256), dim3(256), 0, s, n, num_rx, num_tx, link_sigma,
+                     rx_part, L, snr_lin, npow);
+  return (int)hipGetLastError();
 }
 
 // transmit_mimo's link noise on the Philox path after k_ofdm_txch_sfbc: y0_r +
@@ -1794,6 +1835,9 @@ template <class R>
 int launch_rx_fft_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const cx<R>* y, const R* npow,
                        const uint64_t* fid, uint64_t seed, const R* inj_z, int64_t inj_stride, cx<R>* Y, cx<R>* H,
                        int h_pilots) {
+  if constexpr (sizeof(R) == 8)
+    if (rx_fft_mimo_w_supported(g, m, 1, h_pilots) && mimo_rx_wave_enabled())
+      return launch_rx_fft_mimo_w(s, g, m, B, y, npow, fid, seed, inj_z, inj_stride, Y, H);
   const int spw = MWG / (g.N >> 3);
   const int64_t total = (int64_t)B * m.num_rx;
   if (total > 0x7FFFFFFF - spw) return (int)hipErrorInvalidValue;
@@ -2476,6 +2520,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
 #define LTE_MIMO_INST(R)                                                                                           \
   template int launch_ofdm_txch_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,     \
                                         const uint32_t*, int, const int32_t*, const TxLinkPower<R>&, cx<R>*, int); \
+  template int launch_npow_sfbc_merged<R>(hipStream_t, int, int, int, const R*, R*, const R*, int, const R*, R*); \
   template int launch_link_noise_add<R>(hipStream_t, const Grid&, const MimoGrid&, int, const R*, R*, cx<R>*,      \
                                         const uint64_t*, uint64_t, R*, int*);                                      \
   template bool sfbc_txch_supported<R>(const Grid&, const MimoGrid&, int, int);                                   \

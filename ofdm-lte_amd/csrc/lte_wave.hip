@@ -16,6 +16,123 @@ __device__ __forceinline__ V* dyn_lds() {
   return reinterpret_cast<V*>(lte_dyn_lds);
 }
 
+// The fused SISO receiver's equaliser pieces (lte_kernels.hip: abs2_ref, ZfCoef,
+// chest_interp), restated here for the wave kernels: the same expressions.
+// (Kept apart from the block kernels' copies on purpose: defined in a shared
+// header they changed how the compiler contracted other expressions of those
+// kernels, by an ulp, which exact f32 path-equality tests caught.)
+namespace wrx {
+// |h|^2 as the reference forms it: f64 np.abs(h) ** 2 (hypot, then squared);
+// f32 h.x^2 + h.y^2
+template <class V>
+__device__ __forceinline__ re_t<V> abs2_ref(V h) {
+  if constexpr (sizeof(re_t<V>) == 8) {
+    const double a = hypot(h.x, h.y);
+    return a * a;
+  } else {
+    return h.x * h.x + h.y * h.y;
+  }
+}
+
+
+template <class R> struct ZfCoef;
+template <> struct ZfCoef<double> {   // cdiv(y, h) (Smith, lte_common.h) with the h-only terms precomputed
+  double rat, sre, sim;
+  bool swp;
+  __device__ __forceinline__ void set(double2 h) {
+    swp = !(fabs(h.x) >= fabs(h.y));
+    if (!swp) {
+      rat = (h.x == 0.0 && h.y == 0.0) ? 0.0 : h.y / h.x;   // h = 0: a / 0 as cdiv
+      sre = sim = (h.x == 0.0 && h.y == 0.0) ? 1.0 / h.x : 1.0 / (h.x + h.y * rat);
+    } else {
+      rat = h.x / h.y;
+      sre = 1.0 / (h.y + h.x * rat);
+      sim = -sre;
+    }
+  }
+  // !swp: ((a.x + a.y rat) s, (a.y - a.x rat) s); swp: ((a.x rat + a.y) s, (a.y rat - a.x) s)
+  __device__ __forceinline__ double2 apply(double2 a) const {
+    const double u = swp ? a.x : a.y, v = swp ? a.y : a.x;
+    return make_double2((v + u * rat) * sre, (u - v * rat) * sim);
+  }
+};
+template <> struct ZfCoef<float> {    // zf_div(y, h): y conj(h) / |h|^2
+  float2 h;
+  float r;
+  __device__ __forceinline__ void set(float2 hh) {
+    h = hh;
+    r = 1.0f / (hh.x * hh.x + hh.y * hh.y);
+  }
+  __device__ __forceinline__ float2 apply(float2 y) const {
+    return make_float2((y.x * h.x + y.y * h.y) * r, (y.y * h.x - y.x * h.y) * r);
+  }
+};
+
+// linear interpolation of the pilot LS estimates hp at subcarrier k with edge
+// hold (lte_receiver.py:114-133), as k_rx_chest forms it
+template <class R>
+__device__ __forceinline__ cx<R> chest_interp(const Grid& g, const cx<R>* hp, int k) {
+  using V = cx<R>;
+  const int sidx = g.seg[k];
+  if (sidx < 0) return hp[0];
+  if (sidx >= g.Np - 1) return hp[g.Np - 1];
+  const V v0 = hp[sidx], v1 = hp[sidx + 1];
+  const R fk = (R)(k - g.pilot_idx[sidx]);
+  const R ig = GridT<R>::inv_gap(g)[sidx];
+  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+}
+
+}  // namespace wrx
+
+// One OFDM symbol's N = 2048 received samples after its CP (stream offset
+// off) into wfft's register layout (lane l, register m = sample 64 m + l: 1 KB
+// per wave load instruction) plus sigma times the noise as load_symbol_noisy2
+// draws it: injected [2][L] draws, or one rng4 per sample pair on stream
+// RNG_STREAM_NOISE + rx, lanes 2t / 2t + 1 computing the pair counters of
+// registers m / m + 1 and trading halves with one DPP swap.  Half a symbol at
+// a time, a rolled loop draws into the wave's LDS scratch zs (16 KB) and each
+// register then adds its draw (unrolled over the registers, the 16 Philox + 32
+// Box-Muller chains took the kernel past 512 registers).
+template <class TB>
+__device__ __forceinline__ void wave_symbol_noisy(double2 (&v)[32], const double2* __restrict__ yf, int off, int lane,
+                                                  double sigma, uint64_t seed, uint64_t fr, int rx,
+                                                  const double* __restrict__ zf, int L, double* scratch,
+                                                  const TB& bmt) {
+  const bool odd = lane & 1;
+#pragma unroll
+  for (int m = 0; m < 32; ++m) v[m] = yf[off + 64 * m + lane];
+  double2* zs = reinterpret_cast<double2*>(scratch);   // [16][64]
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (zf) {
+#pragma unroll 1
+      for (int mm = 0; mm < 16; ++mm) {
+        const int n = off + 64 * (16 * h + mm) + lane;
+        zs[64 * mm + lane] = make_double2(zf[n], zf[L + n]);
+      }
+    } else {
+#pragma unroll 1
+      for (int mm = 0; mm < 16; mm += 2) {
+        // even lanes: the pair counter of register m; odd lanes: of register m + 1
+        const int m = 16 * h + mm;
+        const uint32_t ctr = (uint32_t)((off + 64 * m + (odd ? 64 : 0) + lane) >> 1);
+        const u32x4 r = rng4(seed, fr, RNG_STREAM_NOISE + (uint32_t)rx, ctr);
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? r.x : r.z), 0xB1, 0xF, 0xF, true);
+        const uint32_t t1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? r.y : r.w), 0xB1, 0xF, 0xF, true);
+        zs[64 * mm + lane] = gauss2t<double>(odd ? t0 : r.x, odd ? t1 : r.y, bmt);
+        zs[64 * (mm + 1) + lane] = gauss2t<double>(odd ? r.z : t0, odd ? r.w : t1, bmt);
+      }
+    }
+    wfft::wave_lds_fence();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const double2 z = zs[64 * i + lane];
+      v[16 * h + i] = make_double2(v[16 * h + i].x + sigma * z.x, v[16 * h + i].y + sigma * z.y);
+    }
+    wfft::wave_lds_fence();
+  }
+}
+
 // Wave-private fused SISO receiver (float64, N = 2048, coded chain with the
 // demap in k_dematch_zn): one wave64 per frame walks its 14 n_sym symbols with
 // no block barrier.  Per symbol: the 2048 samples after the CP land in
@@ -27,22 +144,29 @@ __device__ __forceinline__ V* dyn_lds() {
 // register q = X[64 q + c].  Grid::kinfo names each bin's role.  At the first
 // symbol of a 14-symbol group the pilot lanes form the LS estimates into the
 // wave's LDS scratch (the transpose buffer, free between transforms), and each
-// data RE's equaliser terms (ZfCoef: rat, sre in LDS by data ordinal, the swap
-// flag as bit q of a per-lane mask) and sigma^2_eff (nvo) are formed once per
-// group, exactly as k_rx_frame forms them (same chest_interp / ZfCoef / abs2_ref
-// code, so the same bits for the same FFT output).  The transform's rounding
-// differs from fft_lds's (both within a few 1e-14 of the exact DFT:
-// profiles/r6_wfft_microbench_wpe*.jsonl).
-// LDS per wave: the transpose buffer (16.5 KB) + Nd x 16 B coefficients (16 KB
-// at 20 MHz), so one wave per SIMD (four per CU); the full register file (512
-// VGPRs + AGPRs) is the wave's.
-#ifndef RXW_EXP   // register-pressure probes (wrong outputs): 1 no noise, 2 no FFT
-#define RXW_EXP 0
-#endif
+// data RE's equaliser terms (ZfCoef: rat and sre, the swap flag as bit q of a
+// per-lane mask) and sigma^2_eff (nvo) are formed once per group, exactly as
+// k_rx_frame forms them (same chest_interp / ZfCoef / abs2_ref code, so the
+// same bits for the same FFT output).  The (rat, sre) pairs wait in the
+// group's last symbol's slot of the output zo -- Nd x 16 B, exactly its size
+// -- read back by the same lane each symbol and overwritten by that symbol's
+// own outputs (read before write, same lane and address), so the wave's LDS
+// is the transpose buffer alone (16.5 KB): two waves per SIMD.  The
+// transform's rounding differs from fft_lds's (both within a few 1e-14 of the
+// exact DFT: profiles/r6_wfft_microbench_wpe*.jsonl).
 #ifndef RXW_WPE   // register budget: waves per SIMD the compiler schedules for (LDS allows 1)
 #define RXW_WPE 2
 #endif
 constexpr int RXW_WAVES = 4;
+#ifndef TXW_WAVES   // frames (waves) per block of k_ofdm_txf_w
+#define TXW_WAVES 4
+#endif
+#ifndef TXW_OUNROLL
+#define TXW_OUNROLL 2
+#endif
+#ifndef TXW_WPE
+#define TXW_WPE 2
+#endif
 __global__ __launch_bounds__(64 * RXW_WAVES) __attribute__((amdgpu_waves_per_eu(RXW_WPE, RXW_WPE)))
 void k_rx_frame_w(Grid g, int rayleigh, int B, const double2* __restrict__ y, int64_t y_frame_stride,
                   const double* __restrict__ npow, const double* __restrict__ snr_lin, const uint64_t* __restrict__ fid,
@@ -56,8 +180,7 @@ void k_rx_frame_w(Grid g, int rayleigh, int B, const double2* __restrict__ y, in
   const int lane0 = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x * RXW_WAVES + w;
-  double* tl = reinterpret_cast<double*>(dyn_lds<double2>()) + (size_t)w * (wfft::LDS_DOUBLES + 2 * g.Nd);
-  double2* cf = reinterpret_cast<double2*>(tl + wfft::LDS_DOUBLES);
+  double* tl = reinterpret_cast<double*>(dyn_lds<double2>()) + (size_t)w * wfft::LDS_DOUBLES;
   __syncthreads();   // the Box-Muller tables (the only block barrier)
   if (b >= B) return;
   const double sigma = sqrt(npow[b] / 2.0);
@@ -67,8 +190,8 @@ void k_rx_frame_w(Grid g, int rayleigh, int B, const double2* __restrict__ y, in
   const double2* yf = y + (size_t)b * y_frame_stride;
   const size_t fre = (size_t)b * g.n_sym * g.Nd;
   const double sc = rx_scale<double>(N);
-  const bool odd = lane0 & 1;
   uint32_t swpm = 0;
+  double2* cf = zo + fre;   // the current group's (rat, sre) by data ordinal
   for (int l = 0; l < g.n_sym; ++l) {
     // lane made opaque per symbol: the twiddle / address arithmetic derived
     // from it is recomputed each symbol instead of hoisted and held live (spills)
@@ -76,52 +199,13 @@ void k_rx_frame_w(Grid g, int rayleigh, int B, const double2* __restrict__ y, in
     asm volatile("" : "+v"(lane));
     const int off = l * (N + g.cp) + g.cp;
     double2 v[32];
-#pragma unroll
-    for (int m = 0; m < 32; ++m) v[m] = yf[off + 64 * m + lane];
-    // The noise, half a symbol at a time (registers 16 h .. 16 h + 15): a
-    // rolled loop draws it into the wave's LDS scratch, then each register adds
-    // its draw.  (Unrolled over the registers, the 16 Philox + 32 Box-Muller
-    // chains took the kernel past 512 registers.)
-    double2* zs = reinterpret_cast<double2*>(tl);   // [16][64]
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (zf) {
-#pragma unroll 1
-        for (int mm = 0; mm < 16; ++mm) {
-          const int n = off + 64 * (16 * h + mm) + lane;
-          zs[64 * mm + lane] = make_double2(zf[n], zf[g.L + n]);
-        }
-      } else {
-#pragma unroll 1
-        for (int mm = 0; mm < 16; mm += 2) {
-          // even lanes: the pair counter of register m; odd lanes: of register m + 1
-          const int m = 16 * h + mm;
-          const uint32_t ctr = (uint32_t)((off + 64 * m + (odd ? 64 : 0) + lane) >> 1);
-          const u32x4 r = rng4(seed, fr, RNG_STREAM_NOISE, ctr);
-          const uint32_t t0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? r.x : r.z), 0xB1, 0xF, 0xF, true);
-          const uint32_t t1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? r.y : r.w), 0xB1, 0xF, 0xF, true);
-          zs[64 * mm + lane] = gauss2t<double>(odd ? t0 : r.x, odd ? t1 : r.y, bmt);
-          zs[64 * (mm + 1) + lane] = gauss2t<double>(odd ? r.z : t0, odd ? r.w : t1, bmt);
-        }
-      }
-      wfft::wave_lds_fence();
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const double2 z = zs[64 * i + lane];
-        v[16 * h + i] = make_double2(v[16 * h + i].x + sigma * z.x, v[16 * h + i].y + sigma * z.y);
-      }
-      wfft::wave_lds_fence();
-    }
-#if RXW_EXP & 32
-    for (int m = 0; m < 32; ++m) zo[fre + (size_t)l * 2048 + 64 * m + lane] = v[m];
-    continue;
-#endif
+    wave_symbol_noisy(v, yf, off, lane, sigma, seed, fr, 0, zf, g.L, tl, bmt);
     // and again before the transform, so its twiddle loads are not hoisted
     // above the noise (48 more registers live across it)
     int lane_f = lane;
     asm volatile("" : "+v"(lane_f));
-    if (!(RXW_EXP & 2)) wfft::fft2048<false>(v, tl, G::tw(g), lane_f);
-    if (!(RXW_EXP & 16) && l % 14 == 0) {   // group estimate from its first symbol (lte_receiver.py:360-411)
+    wfft::fft2048<false>(v, tl, G::tw(g), lane_f);
+    if (l % 14 == 0) {   // group estimate from its first symbol (lte_receiver.py:360-411)
       const int grp = l / 14;
       double2* hp = reinterpret_cast<double2*>(tl);   // [Np] LS estimates, then [Np] scaled pilots
       double2* yp = hp + g.Np;
@@ -135,21 +219,22 @@ void k_rx_frame_w(Grid g, int rayleigh, int B, const double2* __restrict__ y, in
       wfft::wave_lds_fence();
       if (H) {
         double2* Hf = H + ((size_t)b * g.n_grp + grp) * N;
-        for (int k = lane; k < N; k += 64) Hf[k] = chest_interp<double>(g, hp, k);
+        for (int k = lane; k < N; k += 64) Hf[k] = wrx::chest_interp<double>(g, hp, k);
       }
       // rolled (kinfo re-read): the interpolation and ZfCoef code once, not per register
       swpm = 0;
+      cf = zo + fre + (size_t)min(l + 13, g.n_sym - 1) * g.Nd;   // the group's last symbol's slot
       const size_t nvg = ((size_t)b * g.n_grp + grp) * g.Nd;
 #pragma unroll 1
       for (int q = 0; q < 32; ++q) {
         const int k = 64 * q + lane, j = g.kinfo[k];
         if (j < 0) continue;
-        const double2 h = chest_interp<double>(g, hp, k);
-        ZfCoef<double> zc;
+        const double2 h = wrx::chest_interp<double>(g, hp, k);
+        wrx::ZfCoef<double> zc;
         zc.set(make_double2(h.x + 1e-6, h.y));
         cf[j] = make_double2(zc.rat, zc.sre);
         swpm |= (uint32_t)zc.swp << q;
-        const double den = abs2_ref(h);
+        const double den = wrx::abs2_ref(h);
         nvo[nvg + j] = rayleigh ? fmax(s2 / fmin(fmax(den, 1e-6), 1e6), s2 / 4.0) : s2;
       }
       if (pstats && lane == 0) {
@@ -164,17 +249,17 @@ void k_rx_frame_w(Grid g, int rayleigh, int B, const double2* __restrict__ y, in
         st[0] = pp / (double)g.Np;
         st[1] = en / (double)g.Np;
       }
-      wfft::wave_lds_fence();   // coefficients visible; the scratch is the next transform's
+      wfft::wave_lds_fence();   // the scratch is the next transform's
     }
     // the bins' roles re-read per symbol (L1-resident 8 KB table; held in
     // registers they were widened to 64-bit addresses and spilled)
     const size_t fl = fre + (size_t)l * g.Nd;
 #pragma unroll
-    for (int q = 0; q < ((RXW_EXP & 8) ? 0 : 32); ++q) {
+    for (int q = 0; q < 32; ++q) {
       const int j = g.kinfo[64 * q + lane];
       if (j >= 0) {
         const double2 c = cf[j];
-        ZfCoef<double> zc;
+        wrx::ZfCoef<double> zc;
         zc.rat = c.x;
         zc.sre = c.y;
         zc.swp = (swpm >> q) & 1u;
@@ -192,25 +277,291 @@ bool rx_frame_w_supported(const Grid& g, int chain, int f64) {
          32 * g.Np <= wfft::LDS_DOUBLES * 8;
 }
 
-#ifndef LTE_RX_WAVE   // 1: k_rx_frame_w where it applies (env LTE_RX_WAVE=0 / 1 overrides)
-#define LTE_RX_WAVE 1
-#endif
-int rx_wave_enabled() {
-  const char* e = std::getenv("LTE_RX_WAVE");
-  return e ? std::atoi(e) : LTE_RX_WAVE;
+// ---------------------------------------------------------------------------
+// Wave-private coded OFDM TX + static-tap channel (float64, N = 2048): one
+// wave64 per frame walks its symbols, the k_ofdm_txf outputs without a block
+// barrier.  Per symbol: lane c, register q builds bin k = 64 q + c (Grid::kinfo:
+// the data RE's BPS coded bits through tx_map -> qam_point, a pilot, or 0),
+// wfft::fft2048<INV> and the output scale sqrt(N) / N give x[64 q + c]; the
+// taps' cyclic reach (every delay <= 64 <= CP, so output sample n of the
+// received stream is sum_p c_p x[(n - d_p) mod N] for the N samples after the
+// CP and, again, for the CP samples past max_delay) reads x through the wave's
+// LDS window, half a symbol (17 registers' samples) at a time; the symbol
+// power sums |y|^2 over those samples (k_chan_fix adds the first max_delay).
+// STAGE: the frame's coded stream staged in the wave's LDS once (else the bit
+// gathers go through L1 / L2).
+constexpr int TXW_XS = 17 * 64 * 16;   // bytes: the tap window (>= the transpose buffer)
+static_assert(TXW_XS >= wfft::LDS_DOUBLES * 8, "the tap window doubles as the transpose buffer");
+template <int BPS, int NP, bool STAGE>
+__global__ __launch_bounds__(64 * TXW_WAVES) __attribute__((amdgpu_waves_per_eu(TXW_WPE, TXW_WPE)))
+void k_ofdm_txf_w(Grid g, const uint32_t* __restrict__ enc, int enc_words, const int32_t* __restrict__ tx_map, int B,
+                  double2* __restrict__ cap_syms, TxChannelT<double> ch) {
+  constexpr int N = 2048;
+  using G = GridT<double>;
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x * TXW_WAVES + w;
+  if (b >= B) return;   // no block barrier anywhere in this kernel
+  const int ew = STAGE ? (enc_words + 3) & ~3 : 0;
+  char* wl = reinterpret_cast<char*>(dyn_lds<double2>()) + (size_t)w * (TXW_XS + 4 * (size_t)ew);
+  double2* xs = reinterpret_cast<double2*>(wl);
+  const uint32_t* es;
+  if constexpr (STAGE) {
+    uint32_t* e = reinterpret_cast<uint32_t*>(wl + TXW_XS);
+    const uint32_t* fe = enc + (size_t)b * enc_words;
+    for (int i = lane0; i < enc_words; i += 64) e[i] = fe[i];
+    wfft::wave_lds_fence();
+    es = e;
+  } else {
+    es = enc + (size_t)b * enc_words;
+  }
+  const double sc = tx_scale<double>(N);
+  const int cp = g.cp, S = N + cp, D = ch.max_delay;
+  double2 cf[NP];
+  int dl[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    cf[p] = ch.coef[(size_t)b * NP + p];   // SISO: one RX
+    dl[p] = ch.delays[p];
+  }
+  for (int l = 0; l < g.n_sym; ++l) {
+    int lane = lane0;   // opaque per symbol (see k_rx_frame_w)
+    asm volatile("" : "+v"(lane));
+    double2 v[32];
+    const size_t sym0 = ((size_t)b * g.n_sym + l) * g.Nd;
+    // the bins half a symbol at a time: a rolled loop forms them into the
+    // wave's LDS window, then the registers read them (unrolled over the
+    // registers, every bin's tx_map / coded-bit loads were hoisted together)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll 1
+      for (int i = 0; i < 16; ++i) {
+        const int r = g.kinfo[64 * (16 * h + i) + lane];
+        double2 x = make_double2(0.0, 0.0);
+        if (r >= 0) {
+          const int32_t* src = tx_map + ((int64_t)l * g.Nd + r) * BPS;
+          int idx = 0;
+          bool zero = false;
+#pragma unroll
+          for (int m = 0; m < BPS; m += 2) {
+            const int2 t = *reinterpret_cast<const int2*>(src + m);
+            zero |= t.x == -2 || t.y == -2;
+            idx = (idx << 2) | (int)((t.x >= 0 ? getbit(es, t.x) : 0u) << 1) | (int)(t.y >= 0 ? getbit(es, t.y) : 0u);
+          }
+          x = zero ? make_double2(0.0, 0.0) : qam_point<BPS, double>(idx);
+          if (cap_syms) cap_syms[sym0 + r] = x;
+        } else if (r <= -2) {
+          x = G::pilots(g)[-r - 2];
+        }
+        xs[64 * i + lane] = x;
+      }
+      wfft::wave_lds_fence();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[16 * h + i] = xs[64 * i + lane];
+      wfft::wave_lds_fence();
+    }
+    int lane_f = lane;
+    asm volatile("" : "+v"(lane_f));
+    wfft::fft2048<true>(v, reinterpret_cast<double*>(xs), G::tw(g), lane_f);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) v[q] = cscale(v[q], sc);
+    if (D > 0) {   // the TX samples at both ends of the CP-extended symbol (k_chan_fix reads them)
+      double2* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        const int n = 64 * q + lane;
+        if (n >= N - cp && n < N - cp + D) xh[n - (N - cp)] = v[q];
+        if (n >= N - D) xh[n - (N - 2 * D)] = v[q];
+      }
+    }
+    double2* yo = ch.y + (size_t)b * g.L + (size_t)l * S + cp;
+    double pw = 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // window rows i = 0..16 hold registers 16 h - 1 + i (mod 32): samples
+      // 64 (16 h - 1) ... 64 (16 h + 16) - 1 of the cyclic symbol
+      wfft::wave_lds_fence();
+#pragma unroll
+      for (int i = 0; i < 17; ++i) xs[64 * i + lane] = v[(16 * h + 31 + i) & 31];
+      wfft::wave_lds_fence();
+      // outputs from the window only (not the registers): partly rolled, so the
+      // window loads of all 16 outputs are not hoisted together
+#pragma unroll TXW_OUNROLL
+      for (int i = 0; i < 16; ++i) {
+        const int q = 16 * h + i, n = 64 * q + lane;
+        double2 y = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) y = cadd(y, cmul(cf[p], xs[64 * (i + 1) + lane - dl[p]]));
+        yo[n] = y;
+        const double e = y.x * y.x + y.y * y.y;
+        pw += e;
+        if (n >= N - cp + D) pw += e;   // the CP sample m = n - N + cp carries the same value
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) pw += __shfl_xor(pw, o);
+    if (lane == 0) ch.pow_part[(size_t)b * g.n_sym + l] = pw;
+  }
 }
+
+bool txf_w_supported(const Grid& g, int f64, int n_paths, int max_delay, int num_rx, int tv) {
+  return f64 && g.N == 2048 && g.kinfo && g.pilots64 && num_rx == 1 && !tv && n_paths == 4 && max_delay <= 64 &&
+         max_delay <= g.cp && (g.bps == 2 || g.bps == 4 || g.bps == 6);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-private multi-antenna RX FFT + CRS pilot estimates (float64, N = 2048;
+// k_rx_fft_mimo<.., HPO>'s outputs): one wave64 per (frame, RX antenna) walks
+// the frame's symbols.  Per symbol wave_symbol_noisy + wfft::fft2048; the
+// n_dsc data SCs go to Y[b][l][rx][n_dsc] from the registers (Grid::kinfo's
+// data ordinal); on estimation symbols (SFBC: first of each group, spatial:
+// every symbol) the scaled spectrum passes through the wave's LDS scratch
+// half a symbol at a time and each TX's LS pilot estimates
+// (mimo_channel_estimator_periodic.py:195-273) go to H[b][rx][e][tx][maxP].
+constexpr int RXMW_WAVES = 4;
+#ifndef RXMW_WPE   // register budget (LDS allows two waves per SIMD)
+#define RXMW_WPE 2
+#endif
+__global__ __launch_bounds__(64 * RXMW_WAVES) __attribute__((amdgpu_waves_per_eu(RXMW_WPE, RXMW_WPE)))
+void k_rx_fft_mimo_w(Grid g, MimoGrid m, int B, const double2* __restrict__ y, const double* __restrict__ npow,
+                     const uint64_t* __restrict__ fid, uint64_t seed, const double* __restrict__ inj_z,
+                     int64_t inj_stride, double2* __restrict__ Y, double2* __restrict__ H) {
+  constexpr int N = 2048;
+  using G = GridT<double>;
+  LTE_BM_LDS_DECL(double);
+  const auto bmt = bm_stage<double>(lte_bmt);
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gs = blockIdx.x * RXMW_WAVES + w;
+  const int b = gs / m.num_rx, rx = gs - b * m.num_rx;
+  double* tl = reinterpret_cast<double*>(dyn_lds<double2>()) + (size_t)w * wfft::LDS_DOUBLES;
+  __syncthreads();   // the Box-Muller tables (the only block barrier)
+  if (b >= B) return;
+  const size_t br = (size_t)b * m.num_rx + rx;
+  const double sigma = sqrt(npow[br] * 0.5);
+  const uint64_t fr = fid[b];
+  const double* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+  const double2* yf = y + br * g.L;
+  const double sc = rx_scale<double>(N);
+  const double2* pv = MGT<double>::pval(m);
+  for (int l = 0; l < g.n_sym; ++l) {
+    int lane = lane0;   // opaque per symbol (see k_rx_frame_w)
+    asm volatile("" : "+v"(lane));
+    const int off = l * (N + g.cp) + g.cp;
+    double2 v[32];
+    wave_symbol_noisy(v, yf, off, lane, sigma, seed, fr, rx, zf, g.L, tl, bmt);
+    int lane_f = lane;
+    asm volatile("" : "+v"(lane_f));
+    wfft::fft2048<false>(v, tl, G::tw(g), lane_f);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) v[q] = cscale(v[q], sc);
+    const bool est = m.mode == MIMO_SFBC ? (l % 14) == 0 : true;
+    if (est) {
+      const int e = m.mode == MIMO_SFBC ? l / 14 : l;
+      double2* xs = reinterpret_cast<double2*>(tl);   // [1024]: bins 1024 h ... 1024 h + 1023
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xs[64 * i + lane] = v[16 * h + i];
+        wfft::wave_lds_fence();
+        for (int t = 0; t < m.num_tx; ++t) {
+          double2* Ho = H + ((br * m.n_est + e) * m.num_tx + t) * m.maxP;
+          for (int p = lane; p < m.np_tx[t]; p += 64) {
+            const int pos = m.ppos[t * m.maxP + p];
+            if ((pos >> 10) == h) Ho[p] = cdiv(xs[pos & 1023], pv[t * m.maxP + p]);
+          }
+        }
+        wfft::wave_lds_fence();
+      }
+    }
+    double2* Yo = Y + (((size_t)b * g.n_sym + l) * m.num_rx + rx) * m.n_dsc;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int j = g.kinfo[64 * q + lane];
+      if (j >= 0 && j < m.n_dsc) Yo[j] = v[q];
+    }
+  }
+}
+
+bool rx_fft_mimo_w_supported(const Grid& g, const MimoGrid& m, int f64, int h_pilots) {
+  return f64 && h_pilots && g.N == 2048 && g.kinfo && m.pval64 && g.cp % 2 == 0;
+}
+
+// Which wave-private kernels run by default (same-box A/B, profiles/r6_wave_ab.md):
+// the config-5 RX (k_rx_fft_mimo_w) beats its block kernel; the config-2 RX and
+// TX do not (2 waves per SIMD at most with a symbol in registers, against 3 for
+// the block kernels; the noise, the coded-bit gathers and the taps, not the
+// FFT, set their time), so they are opt-in.  Env LTE_RX_WAVE / LTE_TX_WAVE /
+// LTE_MIMO_RX_WAVE = 0 / 1 override.
+#ifndef LTE_RX_WAVE
+#define LTE_RX_WAVE 0
+#endif
+#ifndef LTE_MIMO_RX_WAVE
+#define LTE_MIMO_RX_WAVE 1
+#endif
+static int env_or(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+int rx_wave_enabled() { return env_or("LTE_RX_WAVE", LTE_RX_WAVE); }
+int mimo_rx_wave_enabled() { return env_or("LTE_MIMO_RX_WAVE", LTE_MIMO_RX_WAVE); }
 
 int launch_rx_frame_w(hipStream_t s, const Grid& g, int rayleigh, int B, const double2* y, int64_t y_frame_stride,
                       const double* npow, const double* snr_lin, const uint64_t* fid, uint64_t seed,
                       const double* inj_z, int64_t inj_stride, double* zo, double* nv_out, double2* cap_syms,
                       double2* H, double* pstats) {
   if (!rx_frame_w_supported(g, LTE_CHAIN_CODED, 1) || !nv_out) return (int)hipErrorInvalidValue;
-  const size_t shm = (size_t)RXW_WAVES * (wfft::LDS_DOUBLES * sizeof(double) + (size_t)g.Nd * sizeof(double2));
-  if (shm + BM_LDS_BYTES > 160 * 1024) return (int)hipErrorInvalidValue;
+  const size_t shm = (size_t)RXW_WAVES * wfft::LDS_DOUBLES * sizeof(double);
   (void)hipFuncSetAttribute((const void*)k_rx_frame_w, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   hipLaunchKernelGGL(k_rx_frame_w, dim3((B + RXW_WAVES - 1) / RXW_WAVES), dim3(64 * RXW_WAVES), shm, s, g, rayleigh,
                      B, y, y_frame_stride, npow, snr_lin, fid, seed, inj_z, inj_stride,
                      reinterpret_cast<double2*>(zo), nv_out, cap_syms, H, pstats);
+  return (int)hipGetLastError();
+}
+
+#ifndef LTE_TX_WAVE
+#define LTE_TX_WAVE 0
+#endif
+#ifndef TXW_STAGE_DEFAULT   // 1: the coded streams staged in the wave's LDS (LTE_TXW_STAGE overrides)
+#define TXW_STAGE_DEFAULT 0
+#endif
+int tx_wave_enabled() { return env_or("LTE_TX_WAVE", LTE_TX_WAVE); }
+
+template <int BPS, bool STAGE>
+static int txf_w_go(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map, int B,
+                    double2* cap_syms, const TxChannelT<double>& ch) {
+  const size_t shm = (size_t)TXW_WAVES * (TXW_XS + (STAGE ? 4 * (size_t)((enc_words + 3) & ~3) : 0));
+  if (shm > 160 * 1024) return (int)hipErrorInvalidValue;
+  auto k = k_ofdm_txf_w<BPS, 4, STAGE>;
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipLaunchKernelGGL(k, dim3((B + TXW_WAVES - 1) / TXW_WAVES), dim3(64 * TXW_WAVES), shm, s, g, enc, enc_words,
+                     tx_map, B, cap_syms, ch);
+  return (int)hipGetLastError();
+}
+
+int launch_ofdm_txf_w(hipStream_t s, const Grid& g, const uint32_t* enc, int enc_words, const int32_t* tx_map, int B,
+                      double2* cap_syms, const TxChannelT<double>& ch) {
+  if (!txf_w_supported(g, 1, ch.n_paths, ch.max_delay, ch.num_rx, ch.tcoef != nullptr)) return (int)hipErrorInvalidValue;
+  const char* e = std::getenv("LTE_TXW_STAGE");
+  const bool stage = e ? std::atoi(e) != 0 : TXW_STAGE_DEFAULT;
+  if (stage) {
+    if (g.bps == 2) return txf_w_go<2, true>(s, g, enc, enc_words, tx_map, B, cap_syms, ch);
+    if (g.bps == 4) return txf_w_go<4, true>(s, g, enc, enc_words, tx_map, B, cap_syms, ch);
+    return txf_w_go<6, true>(s, g, enc, enc_words, tx_map, B, cap_syms, ch);
+  }
+  if (g.bps == 2) return txf_w_go<2, false>(s, g, enc, enc_words, tx_map, B, cap_syms, ch);
+  if (g.bps == 4) return txf_w_go<4, false>(s, g, enc, enc_words, tx_map, B, cap_syms, ch);
+  return txf_w_go<6, false>(s, g, enc, enc_words, tx_map, B, cap_syms, ch);
+}
+
+int launch_rx_fft_mimo_w(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const double2* y, const double* npow,
+                         const uint64_t* fid, uint64_t seed, const double* inj_z, int64_t inj_stride, double2* Y,
+                         double2* H) {
+  if (!rx_fft_mimo_w_supported(g, m, 1, 1)) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * m.num_rx;
+  if (total > 0x7FFFFFFF - RXMW_WAVES) return (int)hipErrorInvalidValue;
+  const size_t shm = (size_t)RXMW_WAVES * wfft::LDS_DOUBLES * sizeof(double);
+  hipLaunchKernelGGL(k_rx_fft_mimo_w, dim3((unsigned)((total + RXMW_WAVES - 1) / RXMW_WAVES)), dim3(64 * RXMW_WAVES),
+                     shm, s, g, m, B, y, npow, fid, seed, inj_z, inj_stride, Y, H);
   return (int)hipGetLastError();
 }
 

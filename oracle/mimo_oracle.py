@@ -141,6 +141,10 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
         # sqrt(sum_t s_rt^2) on link (r, 0)'s numbers (lte_mimo.hip
         # rx_link_sigma); each link's own draw still forms its Hm entry
         comb = channel != 'awgn' and bool(draws[r].get('combined_link_noise'))
+        # the device's merged mode (draws[r]['merged_link_noise'], config 4's full
+        # chain: lte_internal.h launch_npow_sfbc_merged): no link-noise draw; its
+        # power 2 s2 enters P in expectation and its variance the RX noise draw
+        merged = comb and bool(draws[r].get('merged_link_noise'))
         s2 = 0.0
         for t in range(num_tx):
             x = xs[t]
@@ -165,6 +169,12 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
                     y = y0
             Hm[r, t] = h
             acc += y
+        if merged:
+            sp = np.mean(np.abs(acc) ** 2) + 2.0 * s2
+            npow = 2.0 * s2 + (sp / num_tx) / 10 ** (snr_db / 10)
+            s = np.sqrt(npow / 2)
+            ys.append(acc + (s * draws[r]['z_re'] + 1j * (s * draws[r]['z_im'])))
+            continue
         if comb:
             s = np.sqrt(s2)
             z0 = draws[r]['links'][0]

@@ -164,8 +164,11 @@ def flat_link_h(seed: int, frame: int, link: int) -> complex:
     return complex(s * zr[0], s * zi[0])
 
 
-def sfbc_draws(seed: int, frame: int, L: int, num_rx: int, n_paths: int, num_tx: int = 2):
-    """transmit_mimo's draws (mimo_oracle.transmit_mimo format), Rayleigh links."""
+def sfbc_draws(seed: int, frame: int, L: int, num_rx: int, n_paths: int, num_tx: int = 2, merged: bool = False):
+    """transmit_mimo's draws (mimo_oracle.transmit_mimo format), Rayleigh links.
+    merged: config 4's full chain on the device (no capture of the received
+    streams / noise powers): the link noise folded into the RX noise draw
+    (lte_internal.h launch_npow_sfbc_merged; the link draws are then unused)."""
     out = []
     for r in range(num_rx):
         links = []
@@ -175,7 +178,7 @@ def sfbc_draws(seed: int, frame: int, L: int, num_rx: int, n_paths: int, num_tx:
             zr, zi = normals(seed, frame, STREAM_MIMO_LINK + link, L)
             links.append({'phases': [ph[p] for p in range(n_paths)], 'z_re': zr, 'z_im': zi})
         zr, zi = normals(seed, frame, STREAM_NOISE + r, L)
-        out.append({'links': links, 'z_re': zr, 'z_im': zi, 'combined_link_noise': True})
+        out.append({'links': links, 'z_re': zr, 'z_im': zi, 'combined_link_noise': True, 'merged_link_noise': merged})
     return out
 
 
@@ -245,7 +248,7 @@ def config4_frame(frame: int, seed: int = BENCH_SEED, snr_db=None):
     L = 14 * (num.N + num.cp)
     snr = bench_snr(frame) if snr_db is None else float(snr_db)
     r = M.simulate_sfbc_coded(num, payload_bits(seed, frame, BENCH_TB), snr, 2, 'rayleigh_mp',
-                              draws=sfbc_draws(seed, frame, L, 2, 4))
+                              draws=sfbc_draws(seed, frame, L, 2, 4, merged=True))
     return int(r['bit_errors']), bool(r['crc_pass'])
 
 

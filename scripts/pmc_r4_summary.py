@@ -44,7 +44,7 @@ def main():
         for v, _, _ in passes:
             c.update(v.get(k, {}))
         ms = passes[0][1].get(k, 0.0)
-        if ms < 0.05:
+        if ms < 0.001:   # (round 6: was 0.05; config 4's merged noise-power kernels take ~4 us)
             continue
         e = {'ms': round(ms, 3), 'dispatches': len(passes[0][2].get(k, ()))}
         waves = c.get('SQ_WAVES', 0)

@@ -274,6 +274,7 @@ def test_sfbc_rx_fused_matches_separate_kernels(C, prec, coded, nrx, chan, monke
     snrs = np.array([6.0, 10.0, 14.0, 16.0, 18.0, 22.0, 30.0])
     outs = []
     cap = ('bits_rx',) if coded else ()   # coded: the decoder's bits (k_crc_count), fused path kept
+    monkeypatch.setenv('LTE_SFBC_LINK_MERGE', '0')   # the same link-noise draws on both sides
     for fuse in ('1', '0'):
         monkeypatch.setenv('LTE_SFBC_RX_FUSE', fuse)
         outs.append(plan.run(snrs, seed=31, frame_id0=4242, capture=cap))
@@ -308,6 +309,7 @@ def test_spatial_pilot_handoff_matches_interpolated_h(C, prec, chan, det, monkey
                          precision=prec)[0]
     snrs = np.array([6.0, 10.0, 14.0, 18.0, 22.0, 26.0, 30.0])
     outs = []
+    monkeypatch.setenv('LTE_MIMO_RX_WAVE', '0')   # the block receiver on both sides: only the handoff changes
     for hp in ('1', '0'):
         monkeypatch.setenv('LTE_SPATIAL_HP', hp)
         outs.append(plan.run(snrs, seed=17, frame_id0=777))
@@ -318,6 +320,35 @@ def test_spatial_pilot_handoff_matches_interpolated_h(C, prec, chan, det, monkey
         assert np.array_equal(a['counts'], b['counts'])
     else:
         assert np.max(np.abs(a['frame_errors'].astype(np.int64) - b['frame_errors'])) / nb < 1e-3
+
+
+@pytest.mark.parametrize('chan,det,inject', [('rayleigh_mp', 'DET_MMSE', False), ('awgn', 'DET_SIC', False),
+                                             ('rayleigh_mp', 'DET_MMSE', True)])
+def test_wave_mimo_receiver_matches_block_receiver(C, chan, det, inject, monkeypatch):
+    """Config 5's receiver as one wave per (frame, RX antenna)
+    (k_rx_fft_mimo_w: wave_symbol_noisy + wfft's 2048-point FFT, the pilot
+    estimates through the wave's LDS half a symbol at a time) vs the block
+    kernel k_rx_fft_mimo<.., HPO> on the same frames (Philox or injected
+    noise): the two FFTs differ in round-off only (each within a few 1e-14 of
+    the exact DFT), so per-frame bit errors and counts are identical.  7
+    frames x 4 RX = 28 waves: a partial last block."""
+    from lte_phy.ofdm_core import _spatial_plan
+    sim = _sim(20.0, '64-QAM', chan, 'f64')
+    nb = 14 * 999 * 6
+    plan = _spatial_plan(sim.config, chan, 'Pedestrian_A', 3.0, 2.0, 14, nb, 7, detector=getattr(C, det),
+                         precision='f64')[0]
+    snrs = np.array([6.0, 10.0, 14.0, 18.0, 22.0, 26.0, 30.0])
+    kw = {}
+    if inject:
+        kw = dict(noise=np.random.default_rng(3).standard_normal((7, 4, 2, plan.L)))
+    outs = []
+    for wave in ('1', '0'):
+        monkeypatch.setenv('LTE_MIMO_RX_WAVE', wave)
+        outs.append(plan.run(snrs, seed=17, frame_id0=777, **kw))
+    a, b = outs
+    assert 0 < int(a['counts'][:, 0].sum())
+    assert np.array_equal(a['frame_errors'], b['frame_errors'])
+    assert np.array_equal(a['counts'], b['counts'])
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])

@@ -574,6 +574,7 @@ def test_frame_tx_matches_symbol_tx(C, monkeypatch, bw, mod, prec):
     plan = sim._plan(C.CHAIN_CODED, 0, 27760 if bw == 20.0 else 4000, max_frames=B)
     snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
     cap = ('noise_power', 'tx_syms', 'llr')
+    monkeypatch.setenv('LTE_TX_WAVE', '0')   # the block per-frame kernel (k_ofdm_txf_w: its own test)
     monkeypatch.setenv('LTE_TX_FRAME', '0')
     a = plan.run(snr, seed=0x5EED, frame_id0=21, capture=cap)
     monkeypatch.setenv('LTE_TX_FRAME', '1')
@@ -581,6 +582,35 @@ def test_frame_tx_matches_symbol_tx(C, monkeypatch, bw, mod, prec):
     for k in cap:
         assert np.array_equal(a[k], b[k]), k
     assert np.array_equal(a['crc_ok'], b['crc_ok']) and np.array_equal(a['counts'], b['counts'])
+
+
+@pytest.mark.parametrize('mod', ['64-QAM', '16-QAM'])
+def test_wave_tx_matches_block_tx(C, monkeypatch, mod):
+    """The wave-private coded TX + static taps (k_ofdm_txf_w: one wave per
+    frame, wfft's inverse 2048-point FFT, the taps' cyclic reach through the
+    wave's LDS window) vs the block kernel k_ofdm_txf on the same frames:
+    identical transmitted symbols; the received stream and the noise powers
+    agree to the two inverse FFTs' round-off; identical decoded outcome.  Both
+    values of LTE_TXW_STAGE (coded streams staged in LDS or gathered through
+    L1 / L2) are the same kernel otherwise and must agree exactly."""
+    sim = _sim(20.0, mod, 'rayleigh_mp', 'f64')
+    B = 2 * 20 + 1
+    plan = sim._plan(C.CHAIN_CODED, 0, 27760 if mod == '64-QAM' else 18000, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('noise_power', 'tx_syms', 'signal_rx')
+    runs = {}
+    for wave, stage in (('0', '1'), ('1', '1'), ('1', '0')):
+        monkeypatch.setenv('LTE_TX_WAVE', wave)
+        monkeypatch.setenv('LTE_TXW_STAGE', stage)
+        runs[wave + stage] = plan.run(snr, seed=0x5EED, frame_id0=5, capture=cap)
+    a, b, c = runs['01'], runs['11'], runs['10']
+    assert np.array_equal(a['tx_syms'], b['tx_syms'])
+    for k in ('signal_rx', 'noise_power'):
+        assert np.max(np.abs(b[k] - a[k])) <= 1e-12 * np.max(np.abs(a[k])), k
+    for k in cap + ('crc_ok', 'counts', 'frame_errors'):
+        assert np.array_equal(b[k], c[k]), k
+    assert np.array_equal(a['crc_ok'], b['crc_ok']) and np.array_equal(a['counts'], b['counts'])
+    assert np.array_equal(a['frame_errors'], b['frame_errors'])
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
@@ -597,6 +627,7 @@ def test_txf_lane_order_matches_re_order(C, monkeypatch, prec):
     snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
     cap = ('noise_power', 'tx_syms', 'llr')
     outs, secs = [], []
+    monkeypatch.setenv('LTE_TX_WAVE', '0')   # RE order on the block kernel too
     for lo in ('1', '0'):
         monkeypatch.setenv('LTE_TXF_LANE_ORDER', lo)
         engine.clear_cache()
@@ -619,6 +650,7 @@ def test_demap_in_dematch_matches_llr_path(C, monkeypatch, mod, prec):
     same max-log demapper while it builds the decoder rows, decodes exactly
     like the LLR round trip (k_rx_data LLRs -> k_dematch): identical per-frame
     bit errors and CRC flags on the same Philox frames."""
+    monkeypatch.setenv('LTE_RX_WAVE', '0')   # both paths on the block receiver: only the demap moves
     sim = _sim(20.0, mod, 'rayleigh_mp', prec)
     B = 2 * 64 + 9
     plan = sim._plan(C.CHAIN_CODED, 0, 27760 if mod == '64-QAM' else 18000, max_frames=B)

@@ -137,6 +137,57 @@ def _config_plan(config, n):
                          14 * 999 * 6, n)[0]
 
 
+def test_config4_unmerged_link_noise_matches_oracle(C, monkeypatch):
+    """Config 4 with the link noise drawn on its own links' streams
+    (LTE_SFBC_LINK_MERGE=0: k_link_noise_pairs, the RX power measured after it)
+    against the oracle's 'combined_link_noise' composition: identical per-frame
+    bit errors and CRC verdicts.  (The default merged form is
+    test_other_config_bench_frames_match_oracle[4].)"""
+    monkeypatch.setenv('LTE_SFBC_LINK_MERGE', '0')
+    from lte_phy import engine
+    engine.clear_cache()
+    from oracle import lte_oracle as O, mimo_oracle as M
+    ids = np.array([0, 1, 2, 5, 7, 9, 11, 13], dtype=np.uint64)
+    S = len(P.BENCH_SNRS)
+    si = (ids % np.uint64(S)).astype(np.int32)
+    plan = _config_plan(4, len(ids))
+    out = plan.run(P.BENCH_SNRS[si], snr_index=si, n_snr=S, seed=P.BENCH_SEED, frame_ids=ids)
+    num = O.Numerology(bandwidth=20.0, modulation='64-QAM')
+    L = 14 * (num.N + num.cp)
+    ref = []
+    for f in ids:
+        r = M.simulate_sfbc_coded(num, P.payload_bits(P.BENCH_SEED, int(f), P.BENCH_TB), P.bench_snr(int(f)), 2,
+                                  'rayleigh_mp', draws=P.sfbc_draws(P.BENCH_SEED, int(f), L, 2, 4, merged=False))
+        ref.append((int(r['bit_errors']), bool(r['crc_pass'])))
+    engine.clear_cache()
+    assert out['frame_errors'].tolist() == [r[0] for r in ref]
+    assert out['crc_ok'].astype(bool).tolist() == [r[1] for r in ref]
+
+
+def test_config4_merged_link_noise_same_distribution(C, monkeypatch):
+    """The merged link noise (default) and the separate draws
+    (LTE_SFBC_LINK_MERGE=0) are different realisations of the same
+    distribution: over 2 048 config-4 frames at 8 / 10 / 12 dB (the BER cliff)
+    the bit-error totals agree within 4 binomial-frame standard deviations,
+    and the noise variance per RX differs only by the link term 2 s2
+    (~1e-10 of the signal power)."""
+    from lte_phy import engine
+    snrs = np.repeat([8.0, 10.0, 12.0], 683)[:2048]
+    res = {}
+    for merge in ('1', '0'):
+        monkeypatch.setenv('LTE_SFBC_LINK_MERGE', merge)
+        engine.clear_cache()
+        plan = _config_plan(4, len(snrs))
+        out = plan.run(snrs, seed=91, frame_id0=10_000)
+        res[merge] = out['frame_errors'].astype(np.float64)
+    engine.clear_cache()
+    for k in range(3):
+        sl = slice(683 * k, min(683 * (k + 1), 2048))
+        a, b = res['1'][sl], res['0'][sl]
+        sd = np.sqrt((a.var() + b.var()) / len(a))
+        assert abs(a.mean() - b.mean()) <= 4 * sd + 1e-9, (k, a.mean(), b.mean(), sd)
+
+
 @pytest.mark.parametrize('config', [3, 4, 5])
 def test_other_config_bench_frames_match_oracle(C, config):
     """bench.py --config 3 / 4 / 5 frames (both ends of the first step at the

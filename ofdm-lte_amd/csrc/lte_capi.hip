@@ -2014,7 +2014,7 @@ static bool tx_per_frame(const lte_plan* p) {
 // Fading taps, fused TX + channel, first-samples power fix-up and noise power.
 template <class R>
 static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bool coded, const R* inj_ph,
-                    int64_t inj_ph_stride, cx<R>* cap_tx_syms) {
+                    int64_t inj_ph_stride, cx<R>* cap_tx_syms, cx<R>* x_out, TxChannelT<R>* ch_out) {
   const lte_plan_desc& d = p->d;
   ChainBufs<R>& c = cbuf<R>(p);
   const int maxd = *std::max_element(d.delays, d.delays + d.n_paths);
@@ -2041,6 +2041,8 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
   ch.y = c.y.p;
   ch.xh = c.xh.p;
   ch.pow_part = c.pow_part.p;
+  ch.x_out = x_out;
+  if (ch_out) *ch_out = ch;
   {
     Timer t(p, KN_OFDM_TX, s);
     if (coded && tx_per_frame(p))
@@ -2119,11 +2121,18 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   // TX + static-tap channel in one kernel (the received stream is written once)
   const bool fuse = do_tx && do_ch && txch_fusable(p, a, coded);
+  // SIMO into the paired receiver (config 3): the TX hands over its symbols
+  // and the receiver applies each RX's taps (TxChannelT::x_out), one stream
+  // through HBM instead of num_rx; LTE_SIMO_XHAND=0 keeps the RX streams
+  const bool xhand = fuse && do_rx && d.fD == 0.0 && d.chain == LTE_CHAIN_SIMO &&
+                     rx_simo_fusable(p, d) && rx_simo2_ok(g, rx, a->cap_H != nullptr, a->cap_pilot_stats != nullptr) &&
+                     env_on("LTE_RXS_PAIRS", true) && env_on("LTE_SIMO_XHAND", true);
+  TxChannelT<R> xch{};
   if (do_tx || a->bits) {
     Timer t(p, KN_PAYLOAD);
     LCHK(launch_payload(s, p->pw.p, p->PW, d.n_bits, coded ? CRC24A_POLY : 0, p->fid.p, a->seed, B, inj_bits, inj_bits_stride));
   }
-  if (!fuse && c.x.alloc((size_t)d.max_frames * p->L)) return fail(LTE_ENOMEM, "TX signal buffer");
+  if ((!fuse || xhand) && c.x.alloc((size_t)d.max_frames * p->L)) return fail(LTE_ENOMEM, "TX signal buffer");
   if (do_tx) {
     if (coded) {
       Timer t(p, KN_ENCODE);
@@ -2135,7 +2144,7 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
       cts = c.captx.p;
     }
     if (fuse) {
-      const int e = run_txch<R>(p, s, a, B, coded, inj_ph, inj_ph_stride, cts);
+      const int e = run_txch<R>(p, s, a, B, coded, inj_ph, inj_ph_stride, cts, xhand ? c.x.p : nullptr, &xch);
       if (e != LTE_OK) return e;
     } else {
       Timer t(p, KN_OFDM_TX);
@@ -2198,7 +2207,8 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_frame_simo<R>(s, g, B, rx, ysrc, yrs, yfs, c.npow.p, p->fid.p, a->seed, inj_z, inj_z_stride,
                                  p->pw.p, p->PW, d.n_bits, p->frame_err.p, cap_syms_dev, cap_bits_dev,
-                                 a->cap_H ? c.H.p : nullptr, a->cap_pilot_stats ? c.pstats.p : nullptr));
+                                 a->cap_H ? c.H.p : nullptr, a->cap_pilot_stats ? c.pstats.p : nullptr,
+                                 xhand ? &xch : nullptr));
   } else if (do_rx) {
     Timer t(p, KN_RX_DATA);
     LCHK(launch_rx_data<R>(s, g, d.chain, ray ? 1 : 0, B, rx, ysrc, yrs, yfs, c.H.p, c.npow.p, c.snr_lin.p, p->fid.p,

@@ -101,6 +101,11 @@ struct TxChannelT {
   // fD != 0: per-symbol Taylor sets of every path [B][num_rx][n_paths][n_sym][mimo_ncf<R>()]
   // (k_jakes_sets); null for static taps (coef)
   const cx<R>* tcoef;
+  // static taps, SIMO into the paired receiver (k_rx_frame_simo2<.., XIN>):
+  // non-null, the TX writes each symbol's N time samples here [B][n_sym][N]
+  // (f64 scaled as ifft * sqrt(N), f32 unscaled with the scale in the taps)
+  // instead of num_rx received streams; the receiver applies the taps
+  cx<R>* x_out;
 };
 bool txch_supported(const Grid& g, int n_paths, int max_delay);
 // host payload bits (one uint8 per bit, frames `stride` bytes apart) already on
@@ -183,7 +188,11 @@ template <class R>
 int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>* y, int64_t y_rx_stride,
                          int64_t y_frame_stride, const R* npow, const uint64_t* fid, uint64_t seed, const R* inj_z,
                          int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                         cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats);
+                         cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats,
+                         const TxChannelT<R>* xc = nullptr);
+// the paired SIMO receiver applies (N = 1024, an even RX count, no H / pilot
+// statistics capture); xc->x_out (the TX's symbol handoff) needs it
+bool rx_simo2_ok(const Grid& g, int num_rx, bool H, bool pstats);
 // Rate dematch into the decoder rows (rows of R: float / double).  rx_map
 // [n_layers][T]: layer 0 assigns, layers 1.. add in order (E > N_cb
 // repetition, rate_matching.py:433-436).  g0: first 64-frame group.

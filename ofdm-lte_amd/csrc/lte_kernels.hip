@@ -168,6 +168,10 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
       xh[i] = F64 ? v : cscale(v, sc);
     }
   }
+  if (active && ch.x_out) {   // the symbol for the receiver's taps (one stream instead of num_rx)
+    V* xo = ch.x_out + ((size_t)b * g.n_sym + l) * N;
+    for (int k = tid; k < N; k += T) xo[k] = buf[k];
+  }
   // SIMO: each RX its own taps, stream and power partial (transmit_simo,
   // core/ofdm_core.py:361-412); the symbol in LDS is read once per RX
   for (int r = 0; r < ch.num_rx; ++r) {
@@ -226,7 +230,7 @@ __device__ __forceinline__ void tx_channel(cx<R>* buf, const Grid& g, const TxCh
 #pragma unroll
         for (int p = 0; p < PM; ++p)
           if (p < np) v = cadd(v, cmul(cf[p], buf[(m - off[p]) & (N - 1)]));
-        if (m >= cp) yo[m] = v;
+        if (m >= cp && !ch.x_out) yo[m] = v;
         pw += v.x * v.x + v.y * v.y;
       }
     }
@@ -1727,18 +1731,70 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo(
   frame_err_add(frame_err, b, errs);
 }
 
+// k_rx_frame_simo2<.., XIN>'s loader: RX rx's N samples of symbol l formed
+// from the TX symbol xs (LDS, natural order) with tx_channel's taps in its
+// order -- y[n] = sum_p c_rp x[(n - d_p) mod N]: every delay is within the CP,
+// so the received samples past the CP are a cyclic convolution of the symbol
+// -- plus the noise exactly as load_symbol_noisy2 draws it (one Philox per
+// sample pair), stored swizzled for fft_lds<.., ISW = true>.
+template <class V, class TB>
+__device__ __forceinline__ void tap_symbol_noisy2(V* buf, const V* xs, const V (&cf)[TXCH_MAXP],
+                                                  const int (&dl)[TXCH_MAXP], int np, int N, int cp, int l,
+                                                  re_t<V> sigma, uint64_t seed, uint64_t frame, int rx,
+                                                  const re_t<V>* __restrict__ zf, int L, int tid, int T, const TB& tb) {
+  using R = re_t<V>;
+  const int off = l * (N + cp) + cp;
+  auto tap = [&](int n) {
+    V v = mkc((R)0, (R)0);
+#pragma unroll
+    for (int p = 0; p < TXCH_MAXP; ++p)
+      if (p < np) v = cadd(v, cmul(cf[p], xs[(n - dl[p]) & (N - 1)]));
+    return v;
+  };
+  if (zf) {
+    for (int k = tid; k < N; k += T) {
+      const int n = off + k;
+      const V v = tap(k);
+      buf[fft_sw<V>(k)] = mkc(v.x + sigma * zf[n], v.y + sigma * zf[L + n]);
+    }
+    return;
+  }
+  const int p0 = off >> 1, p1 = (off + N - 1) >> 1;
+  constexpr int MAXR = 5;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int p = p0 + tid + i * T, n0 = 2 * p;
+    if (p > p1) break;
+    const u32x4 r = rng4(seed, frame, RNG_STREAM_NOISE + (uint32_t)rx, (uint32_t)p);
+    if (n0 >= off) {
+      const V v = tap(n0 - off);
+      const V z = gauss2t<R>(r.x, r.y, tb);
+      buf[fft_sw<V>(n0 - off)] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
+    }
+    if (n0 + 1 < off + N) {
+      const V v = tap(n0 + 1 - off);
+      const V z = gauss2t<R>(r.z, r.w, tb);
+      buf[fft_sw<V>(n0 + 1 - off)] = mkc(v.x + sigma * z.x, v.y + sigma * z.y);
+    }
+  }
+}
+
 // k_rx_frame_simo with the receive antennas in pairs (N = 1024, an even
 // number of RX, no capture of H / pilot statistics): one frame per 256-thread
 // block; each half loads and transforms one RX of the pair (RX 2p + h) into
 // its own buffer, then every thread folds both into its REs' MRC sums in RX
 // order -- the same operations per RE as k_rx_frame_simo, with half the
 // passes (and barriers) per symbol.
-template <class R, int BPS, int NC>
+// XIN: the TX handed over its symbols instead of the received streams
+// (TxChannelT::x_out): each symbol is staged in LDS once and every RX forms its
+// samples with its own taps (tap_symbol_noisy2) -- one stream through HBM
+// instead of num_rx, both ways.
+template <class R, int BPS, int NC, bool XIN = false>
 __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo2(
     Grid g, int B, int num_rx, const cx<R>* __restrict__ y, int64_t y_rx_stride, int64_t y_frame_stride,
     const R* __restrict__ npow, const uint64_t* __restrict__ fid, uint64_t seed, const R* __restrict__ inj_z,
     int64_t inj_stride, const uint32_t* __restrict__ pw, int PW, int n_bits, uint32_t* __restrict__ frame_err,
-    cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+    cx<R>* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits, TxChannelT<R> xc) {
   using V = cx<R>;
   using G = GridT<R>;
   constexpr int N = NC, T = N >> 3;
@@ -1748,6 +1804,7 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo2(
   const int b = blockIdx.x;
   V* bufs = sm;                  // [2][N]
   V* hpa = sm + 2 * N;           // [RXS_MAXRX][Np] pilot LS estimates of the current group
+  V* xs = hpa + RXS_MAXRX * g.Np;   // XIN: [N] the TX symbol
   const R sc = rx_scale<R>(N);
   constexpr R QS = (R)qam_norm<BPS>();
   constexpr int QM = 2;   // data REs per thread (Nd < N/2 = QM WG)
@@ -1782,6 +1839,11 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo2(
 #pragma unroll
       for (int q = 0; q < QM; ++q) den[q] = (R)0;
     }
+    if constexpr (XIN) {   // (the previous symbol's last barrier precedes this)
+      const V* xo = xc.x_out + ((size_t)b * g.n_sym + l) * N;
+      for (int k = tid0; k < N; k += WG) xs[k] = xo[k];
+      __syncthreads();
+    }
     for (int r0 = 0; r0 < num_rx; r0 += 2) {
       int tid = th;   // opaque per pass (see k_rx_frame)
       asm volatile("" : "+v"(tid));
@@ -1790,7 +1852,20 @@ __global__ __launch_bounds__(WG, RXF_WAVES) void k_rx_frame_simo2(
       {
         const R sigma = sqrt(npow[(size_t)b * num_rx + rx] / (R)2);
         const R* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
-        load_symbol_noisy2<true>(buf, yf + rx * y_rx_stride, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T, bmt);
+        if constexpr (XIN) {   // tx_channel's taps for this RX (f32: the output scale folded in)
+          const int np = xc.n_paths;
+          V cf[TXCH_MAXP];
+          int dl[TXCH_MAXP];
+#pragma unroll
+          for (int p = 0; p < TXCH_MAXP; ++p) {
+            const V c = p < np ? xc.coef[((size_t)b * num_rx + rx) * np + p] : mkc((R)0, (R)0);
+            cf[p] = sizeof(R) == 8 ? c : cscale(c, tx_scale<R>(N));
+            dl[p] = xc.delays[p];
+          }
+          tap_symbol_noisy2(buf, xs, cf, dl, np, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T, bmt);
+        } else {
+          load_symbol_noisy2<true>(buf, yf + rx * y_rx_stride, N, g.cp, l, sigma, seed, fr, rx, zf, g.L, tid, T, bmt);
+        }
       }
       __syncthreads();
       fft_lds<false, NC, false, true, true>(buf, N, g.log2N, G::tw(g), tid, true);
@@ -1840,22 +1915,37 @@ bool rx_frame_simo_supported(const Grid& g, int num_rx) {
   return num_rx >= 2 && num_rx <= RXS_MAXRX && (g.bps == 2 || g.bps == 4 || g.bps == 6) && 2 * g.Nd < g.N;
 }
 
+bool rx_simo2_ok(const Grid& g, int num_rx, bool H, bool pstats) {
+  return g.N == 1024 && (num_rx & 1) == 0 && num_rx <= RXS_MAXRX && !H && !pstats && g.Nd <= 2 * WG;
+}
+
 template <class R>
 int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const cx<R>* y, int64_t y_rx_stride,
                          int64_t y_frame_stride, const R* npow, const uint64_t* fid, uint64_t seed, const R* inj_z,
                          int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
-                         cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats) {
+                         cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats, const TxChannelT<R>* xc) {
   if (!rx_frame_simo_supported(g, num_rx)) return (int)hipErrorInvalidValue;
   const char* pe = std::getenv("LTE_RXS_PAIRS");   // 0: one slot per frame with T threads, the RX in sequence (A/B)
-  if (g.N == 1024 && (num_rx & 1) == 0 && !H && !pstats && g.Nd <= 2 * WG && (!pe || std::atoi(pe) != 0)) {
-    const size_t shm2 = (2 * (size_t)g.N + RXS_MAXRX * g.Np) * sizeof(cx<R>);
+  if (rx_simo2_ok(g, num_rx, H != nullptr, pstats != nullptr) && (!pe || std::atoi(pe) != 0)) {
+    const bool xin = xc && xc->x_out;
+    const size_t shm2 = (2 * (size_t)g.N + RXS_MAXRX * g.Np + (xin ? g.N : 0)) * sizeof(cx<R>);
+    const TxChannelT<R> xcv = xin ? *xc : TxChannelT<R>{};
 #define LTE_RXS2(BPS_)                                                                                               \
-  hipLaunchKernelGGL((k_rx_frame_simo2<R, BPS_, 1024>), dim3(B), dim3(WG), shm2, s, g, B, num_rx, y, y_rx_stride,    \
-                     y_frame_stride, npow, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, cap_syms, cap_bits)
+  do {                                                                                                               \
+    if (xin)                                                                                                         \
+      hipLaunchKernelGGL((k_rx_frame_simo2<R, BPS_, 1024, true>), dim3(B), dim3(WG), shm2, s, g, B, num_rx, y,       \
+                         y_rx_stride, y_frame_stride, npow, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, \
+                         cap_syms, cap_bits, xcv);                                                                   \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_rx_frame_simo2<R, BPS_, 1024>), dim3(B), dim3(WG), shm2, s, g, B, num_rx, y, y_rx_stride, \
+                         y_frame_stride, npow, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err, cap_syms,    \
+                         cap_bits, xcv);                                                                             \
+  } while (0)
     if (g.bps == 2) LTE_RXS2(2); else if (g.bps == 4) LTE_RXS2(4); else LTE_RXS2(6);
 #undef LTE_RXS2
     return (int)hipGetLastError();
   }
+  if (xc && xc->x_out) return (int)hipErrorInvalidValue;   // the symbol handoff needs the paired receiver
   const int spw = WG / (g.N >> 3);
   const int blocks = (B + spw - 1) / spw;
   const size_t shm = (size_t)spw * (g.N + RXS_MAXRX * g.Np) * sizeof(cx<R>);
@@ -1943,7 +2033,7 @@ int launch_rx_data(hipStream_t s, const Grid& g, int chain, int rayleigh, int B,
                                  const uint32_t*, int, int, uint32_t*, R*, cx<R>*, uint8_t*, int, R*);              \
   template int launch_rx_frame_simo<R>(hipStream_t, const Grid&, int, int, const cx<R>*, int64_t, int64_t, const R*,  \
                                        const uint64_t*, uint64_t, const R*, int64_t, const uint32_t*, int, int,       \
-                                       uint32_t*, cx<R>*, uint8_t*, cx<R>*, R*);                                     \
+                                       uint32_t*, cx<R>*, uint8_t*, cx<R>*, R*, const TxChannelT<R>*);               \
   template int launch_rx_frame<R>(hipStream_t, const Grid&, int, int, int, const cx<R>*, int64_t, const R*, const R*, \
                                   const uint64_t*, uint64_t, const R*, int64_t, const uint32_t*, int, int, uint32_t*, \
                                   R*, cx<R>*, uint8_t*, R*, cx<R>*, R*);

@@ -499,6 +499,40 @@ def test_wave_receiver_matches_block_receiver(C, monkeypatch, mod, chan, inject)
     assert 0 < int(np.sum(b0['crc_ok'])) < B
 
 
+@pytest.mark.parametrize('prec,inject', [('f64', False), ('f64', True), ('f32', False)])
+def test_simo_symbol_handoff_matches_rx_streams(C, monkeypatch, prec, inject):
+    """Config 3's TX hands the paired receiver its symbols and the receiver
+    applies each RX's taps (TxChannelT::x_out, k_rx_frame_simo2<.., XIN>,
+    default) vs the TX writing every RX stream (LTE_SIMO_XHAND=0): the same
+    taps in the same order over the cyclic symbol, so combined symbols agree to
+    round-off (float64 1e-12) and decisions and counts are identical in
+    float64; Philox and injected noise; 4 RX, Vehicular-A (delays to the CP)."""
+    import lte_phy
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=10.0, modulation='16-QAM'), channel_type='rayleigh_mp',
+                                itu_profile='Vehicular_A', precision=prec)
+    B = 32 + 3
+    plan = sim._plan(C.CHAIN_SIMO, 14, 14 * sim.Nd * 4, num_rx=4, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    kw = {}
+    if inject:
+        kw = dict(noise=np.random.default_rng(5).standard_normal((B, 4, 2, plan.L)))
+    runs = {}
+    for xh in ('0', '1'):
+        monkeypatch.setenv('LTE_SIMO_XHAND', xh)
+        runs[xh] = (plan.run(snr, seed=0x5EED, frame_id0=11, capture=('data_syms', 'bits_rx', 'noise_power'), **kw),
+                    plan.run(snr, seed=0x5EED, frame_id0=11, **kw))
+    (a, a0), (b, b0) = runs['0'], runs['1']
+    tol = 1e-12 if prec == 'f64' else 1e-5
+    assert np.array_equal(a['noise_power'], b['noise_power'])   # the TX forms the powers either way
+    assert np.max(np.abs(b['data_syms'] - a['data_syms'])) <= tol * np.max(np.abs(a['data_syms']))
+    if prec == 'f64':
+        assert np.array_equal(a['bits_rx'], b['bits_rx'])
+        assert np.array_equal(a0['counts'], b0['counts']) and np.array_equal(a0['frame_errors'], b0['frame_errors'])
+    else:
+        assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 4
+    assert 0 < int(b0['counts'][:, 0].sum())
+
+
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('bw,mod,nrx,prof', [(10.0, '16-QAM', 4, 'Vehicular_A'), (20.0, '64-QAM', 2, 'Pedestrian_A'),
                                              (1.25, 'QPSK', 3, 'Pedestrian_A')])

@@ -2121,12 +2121,15 @@ static int run_siso(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
   }
   // TX + static-tap channel in one kernel (the received stream is written once)
   const bool fuse = do_tx && do_ch && txch_fusable(p, a, coded);
-  // SIMO into the paired receiver (config 3): the TX hands over its symbols
-  // and the receiver applies each RX's taps (TxChannelT::x_out), one stream
-  // through HBM instead of num_rx; LTE_SIMO_XHAND=0 keeps the RX streams
+  // SIMO into the paired receiver (config 3), opt-in (LTE_SIMO_XHAND=1): the
+  // TX hands over its symbols and the receiver applies each RX's taps
+  // (TxChannelT::x_out), one stream through HBM instead of num_rx.  Measured
+  // slower (profiles/r6_simo_xhand_ab.md: TX 16.1 -> 12.9 ms, receiver 27.7 ->
+  // 43.3 ms per 65 536 frames: the taps cost the VALU-bound receiver more than
+  // the streams cost the HBM)
   const bool xhand = fuse && do_rx && d.fD == 0.0 && d.chain == LTE_CHAIN_SIMO &&
                      rx_simo_fusable(p, d) && rx_simo2_ok(g, rx, a->cap_H != nullptr, a->cap_pilot_stats != nullptr) &&
-                     env_on("LTE_RXS_PAIRS", true) && env_on("LTE_SIMO_XHAND", true);
+                     env_on("LTE_RXS_PAIRS", true) && env_on("LTE_SIMO_XHAND", false);
   TxChannelT<R> xch{};
   if (do_tx || a->bits) {
     Timer t(p, KN_PAYLOAD);

@@ -72,6 +72,24 @@ __global__ __launch_bounds__(WG) void k_payload(uint32_t* __restrict__ pw, int P
     uint32_t h0 = 0u, h1 = 0u;
     const uint64_t f = inj ? 0ull : fid[b];
     uint32_t c = 0u;
+    if (!poly) {   // no CRC: lane l draws groups l, l + 64, ... (the same draws; each store instruction
+                   // of the wave then covers one contiguous 1 KB span instead of 64 chunks KG x 16 B apart)
+      for (int g = lane; 4 * g < nwd; g += 64) {
+        u32x4 rv{0u, 0u, 0u, 0u};
+        if (!inj) rv = rng4(seed, f, RNG_STREAM_BITS, (uint32_t)g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = 4 * g + q;
+          if (i >= nwd) break;
+          uint32_t v = inj ? inj[(size_t)b * inj_stride + i] : (q == 0 ? rv.x : q == 1 ? rv.y : q == 2 ? rv.z : rv.w);
+          const int rem = n_bits - 32 * i;
+          if (rem < 32) v &= ~(0xFFFFFFFFu >> rem);
+          w[i] = v;
+        }
+      }
+      for (int i = nwd + lane; i < PW; i += 64) w[i] = 0u;   // words past the bits (the chunked loop stored zeros)
+      continue;
+    }
     for (int k = 0; k < KG; ++k) {
       const int g = lane * KG + k;
       u32x4 rv{0u, 0u, 0u, 0u};

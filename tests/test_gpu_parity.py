@@ -503,7 +503,7 @@ def test_wave_receiver_matches_block_receiver(C, monkeypatch, mod, chan, inject)
 def test_simo_symbol_handoff_matches_rx_streams(C, monkeypatch, prec, inject):
     """Config 3's TX hands the paired receiver its symbols and the receiver
     applies each RX's taps (TxChannelT::x_out, k_rx_frame_simo2<.., XIN>,
-    default) vs the TX writing every RX stream (LTE_SIMO_XHAND=0): the same
+    opt-in LTE_SIMO_XHAND=1) vs the TX writing every RX stream (default): the same
     taps in the same order over the cyclic symbol, so combined symbols agree to
     round-off (float64 1e-12) and decisions and counts are identical in
     float64; Philox and injected noise; 4 RX, Vehicular-A (delays to the CP)."""

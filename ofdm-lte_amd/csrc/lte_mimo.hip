@@ -2327,22 +2327,45 @@ __device__ __forceinline__ void detect_sc(const dc (&He)[DMAX][DMAX], const dc (
 #endif
 // linear detectors: 4 waves per SIMD (<= 128 VGPRs; the kernel waits on its
 // loads at 3, 131 VGPRs)
-template <class R, int BPS, bool SIC_ON, bool HPI = false>
-__global__ __launch_bounds__(MWG) __attribute__((amdgpu_waves_per_eu(SIC_ON ? 1 : LTE_DSP_WAVES)))
+// STG (with HPI): one block per (frame, symbol); the symbol's pilot estimates
+// of every (RX, TX) link are staged in LDS with coalesced loads before the
+// block's REs interpolate them (each RE's 2 x NR x NT interpolation reads then
+// hit LDS instead of gathers through L1 / L2); the block's threads loop over
+// the symbol's n_dsc data SCs.
+#ifndef LTE_DSP_STG_WAVES   // the staged form's register budget (waves per SIMD)
+#define LTE_DSP_STG_WAVES 3
+#endif
+template <class R, int BPS, bool SIC_ON, bool HPI = false, bool STG = false>
+__global__ __launch_bounds__(MWG) __attribute__((amdgpu_waves_per_eu(SIC_ON ? 1 : (STG ? LTE_DSP_STG_WAVES : LTE_DSP_WAVES))))
 void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
                                                      const cx<R>* __restrict__ H, const double* __restrict__ nvar,
                                                      const uint32_t* __restrict__ pw, int PW, int n_bits,
                                                      uint32_t* __restrict__ frame_err, cx<R>* __restrict__ cap_syms,
                                                      uint8_t* __restrict__ cap_bits) {
   using V = cx<R>;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t per = (int64_t)g.n_sym * m.n_dsc;
-  // lanes past the batch stay in the wave (convergent error reduction) and
-  // work on a clamped, valid index without storing anything
-  const bool act = i < (int64_t)B * per;
-  const int b = act ? (int)(i / per) : B - 1;
-  const int rem = act ? (int)(i - (int64_t)b * per) : 0, l = rem / m.n_dsc, j = rem - l * m.n_dsc;
+  static_assert(!STG || HPI, "staging is of the pilot estimates");
   const int NR = m.num_rx, NT = m.num_tx, R_ = m.rank;
+  const int64_t per = (int64_t)g.n_sym * m.n_dsc;
+  V* hs = mimo_lds<V>();   // STG: [NR][NT][maxP] this symbol's pilot estimates
+  if constexpr (STG) {
+    const int bs = blockIdx.x / g.n_sym, ls = blockIdx.x - bs * g.n_sym;
+    const int nl = NT * m.maxP;
+    for (int k = threadIdx.x; k < NR * nl; k += blockDim.x) {
+      const int r = k / nl, q = k - r * nl;
+      hs[k] = H[(((size_t)bs * NR + r) * m.n_est + ls) * nl + q];
+    }
+    __syncthreads();
+  }
+  for (int jb = 0; jb < (STG ? m.n_dsc : 1); jb += MWG) {
+  const int64_t i = STG ? (int64_t)blockIdx.x * per / g.n_sym + jb + threadIdx.x
+                        : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // lanes past the batch (or, STG, past the symbol's data SCs) stay in the wave
+  // (convergent error reduction) and work on a clamped, valid index without
+  // storing anything
+  const bool act = STG ? jb + (int)threadIdx.x < m.n_dsc : i < (int64_t)B * per;
+  const int64_t ic = act ? i : (STG ? (int64_t)blockIdx.x * per / g.n_sym : 0);
+  const int b = act || STG ? (int)(ic / per) : B - 1;
+  const int rem = act || STG ? (int)(ic - (int64_t)b * per) : 0, l = rem / m.n_dsc, j = rem - l * m.n_dsc;
   dc He[DMAX][DMAX], yv[DMAX];
 #pragma unroll
   for (int r = 0; r < DMAX; ++r) {
@@ -2357,8 +2380,8 @@ void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
   // He[r][c] = sum_t H[r][t] W[t][c], each (r, c) summed in t order; with the
   // pilot estimates (HPI) TX t's interpolation point (segment, offset, 1 / gap)
   // is looked up once for every RX
-  const size_t hrs = (size_t)m.n_est * NT * (HPI ? m.maxP : m.n_dsc);
-  const V* H0 = H + ((size_t)b * NR * m.n_est + l) * NT * (HPI ? m.maxP : m.n_dsc) + (HPI ? 0 : j);
+  const size_t hrs = STG ? (size_t)NT * m.maxP : (size_t)m.n_est * NT * (HPI ? m.maxP : m.n_dsc);
+  const V* H0 = STG ? hs : H + ((size_t)b * NR * m.n_est + l) * NT * (HPI ? m.maxP : m.n_dsc) + (HPI ? 0 : j);
 #pragma unroll
   for (int t = 0; t < DMAX; ++t) {   // unrolled: the four TX's table and estimate loads in flight together
     if (t >= NT) break;
@@ -2406,6 +2429,12 @@ void k_det_spatial(Grid g, MimoGrid m, int B, const cx<R>* __restrict__ Y,
     }
   }
   frame_err_add(frame_err, b, errs);
+  }
+}
+
+static int env_flag(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
 }
 
 template <class R>
@@ -2417,9 +2446,16 @@ int launch_det_spatial(hipStream_t s, const Grid& g, const MimoGrid& m, int B, c
     return (int)hipErrorInvalidValue;
   const int64_t n = (int64_t)B * g.n_sym * m.n_dsc;
   const dim3 grid((unsigned)((n + MWG - 1) / MWG));
+  // the pilot estimates staged per (frame, symbol) (LTE_DSP_STAGE=0: gathered per RE)
+  const size_t hshm = (size_t)m.num_rx * m.num_tx * m.maxP * sizeof(cx<R>);
+  const bool stg = h_pilots && hshm <= 32768 && (int64_t)B * g.n_sym < 0x7FFFFFFF && env_flag("LTE_DSP_STAGE", 1);
+  const dim3 sgrid((unsigned)((int64_t)B * g.n_sym));
 #define LTE_DSP(B_, S_)                                                                                            \
   do {                                                                                                             \
-    if (h_pilots)                                                                                                  \
+    if (stg)                                                                                                       \
+      hipLaunchKernelGGL((k_det_spatial<R, B_, S_, true, true>), sgrid, dim3(MWG), hshm, s, g, m, B, Y, H, nvar,   \
+                         pw, PW, n_bits, frame_err, cap_syms, cap_bits);                                           \
+    else if (h_pilots)                                                                                             \
       hipLaunchKernelGGL((k_det_spatial<R, B_, S_, true>), grid, dim3(MWG), 0, s, g, m, B, Y, H, nvar, pw, PW,      \
                          n_bits, frame_err, cap_syms, cap_bits);                                                   \
     else                                                                                                           \

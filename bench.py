@@ -465,8 +465,8 @@ def stage_bytes_per_frame(config, plan, prec):
         # the merged link noise (default: LTE_SFBC_LINK_MERGE) folds the link noise into the receiver's draw:
         # the 'channel' stage is then the per-RX noise powers from the TX's power partials
         merged = os.environ.get('LTE_SFBC_LINK_MERGE', '1') != '0'
-        chan = ((['k_npow_sfbc_merged', 'k_link_sigma'], 2 * nr * nt * esz + 3 * nr * esz,
-                 'link and RX power partials in, the link sigmas and noise powers out') if merged else
+        chan = ((['k_npow_sfbc_merged'], 2 * nr * esz + nr * esz + esz,
+                 'per RX the links\' and the stream\'s power partials and the SNR in, the noise power out') if merged else
                 (['k_link_noise_pairs'], 2 * nr * stream, 'each RX stream in and out (+ link noise)'))
         return {'ofdm_tx': (['k_ofdm_txch_sfbc'], plan.coded_bits / 8 + nr * stream,
                             'coded bits in, each RX antenna\'s faded stream (with CP) out'),

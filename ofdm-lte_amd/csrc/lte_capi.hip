@@ -1717,7 +1717,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
                           env_on("LTE_SFBC_RX_FUSE", true) && env_on("LTE_SFBC_LINK_MERGE", true);
   if (sfbc_fuse) {
     TxLinkPower<R> lf{p->delays.p, c.coef.p, c.link_part.p, d.n_paths, maxd, 1};
-    if (sfbc_merge) lf.rx_part = c.pow_part.p;
+    lf.merged = sfbc_merge ? 1 : 0;
     {
       Timer t(p, KN_OFDM_TX);
       LCHK(launch_ofdm_txch_sfbc<R>(s, g, m, coded ? 1 : 0, p->pw.p, p->PW, p->enc.p, p->enc_words, p->tx_map.p, lf,
@@ -1728,8 +1728,7 @@ static int run_mimo(lte_plan* p, const lte_run_args* a, int B, int n_snr, const 
     // 65 536 frames with 1, 2, 4 or 8 chunks)
     Timer t(p, KN_CHANNEL);
     if (sfbc_merge)
-      LCHK(launch_npow_sfbc_merged<R>(s, B, m.num_rx, m.num_tx, c.link_part.p, c.link_sigma.p, c.pow_part.p, p->L,
-                                      c.snr_lin.p, c.npow.p));
+      LCHK(launch_npow_sfbc_merged<R>(s, B, m.num_rx, m.num_tx, c.link_part.p, p->L, c.snr_lin.p, c.npow.p));
     else
       LCHK(launch_link_noise_add<R>(s, g, m, B, c.link_part.p, c.link_sigma.p, c.y.p, p->fid.p, a->seed,
                                     c.pow_part.p, &npow_nblk));

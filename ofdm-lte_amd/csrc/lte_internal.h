@@ -320,9 +320,9 @@ struct TxLinkPower {
   const cx<R>* coef;       // [B][num_rx][num_tx][n_paths][mimo_ncf<R>()] (n_cs = 1)
   R* part;                 // [B][num_rx][num_tx][nblk]
   int n_paths, max_delay, nblk;
-  // k_ofdm_txch_sfbc only, non-null: also each RX stream's power sum_n |y0_r|^2
-  // ([B][num_rx], one partial per frame and RX) for the merged link noise
-  R* rx_part;
+  // k_ofdm_txch_sfbc only, 1: the merged link noise -- part's two entries per
+  // RX are the links' powers summed and the RX stream's power
+  int merged;
 };
 template <class R>
 int launch_ofdm_tx_mimo(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
@@ -354,16 +354,17 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
 // config 4's merged link noise (Philox mode, full chain, no capture of the
 // received streams or noise powers): instead of adding the RX's 100 dB link
 // noise to y0_r (k_link_noise_pairs) and measuring the noisy power, the RX's
-// one noise draw in the receiver carries both, per RX
-//   s2 = sum_t s_rt^2 (k_link_sigma's per-link standard deviations),
-//   P = sum_n |y0_r|^2 / L + 2 s2 (the link noise's power in expectation),
+// one noise draw in the receiver carries both, per RX (from the two partials
+// k_ofdm_txch_sfbc<.., MRG> writes: sum_t sum_n |y0_rt|^2 and sum_n |y0_r|^2)
+//   s2 = ((sum_t p_rt / L) / 1e10) / 2   (the links' sigma^2 per component),
+//   P = sum_n |y0_r|^2 / L + 2 s2        (the link noise's power in expectation),
 //   npow_awgn = (P / num_tx) / snr,  npow_eff = 2 s2 + npow_awgn,
 // and k_rx_sfbc draws sqrt(npow_eff / 2) per component: the same distribution
 // as the two draws (independent Gaussians add) with P's link-noise term
 // (~1e-10 of P) in expectation.  oracle/philox.sfbc_draws(merged=True).
 template <class R>
-int launch_npow_sfbc_merged(hipStream_t s, int B, int num_rx, int num_tx, const R* link_part, R* link_sigma,
-                            const R* rx_part, int L, const R* snr_lin, R* npow);
+int launch_npow_sfbc_merged(hipStream_t s, int B, int num_rx, int num_tx, const R* link_part, int L, const R* snr_lin,
+                            R* npow);
 template <class R>
 int launch_link_noise_add(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const R* link_part, R* link_sigma,
                           cx<R>* y, const uint64_t* fid, uint64_t seed, R* pow_part, int* pow_nblk);

@@ -922,7 +922,10 @@ constexpr int SFX_TL = 32;   // largest max_delay (samples) the kept tails cover
 // TPB = 256: one thread per radix-8 butterfly of each grid, both grids in one
 // dual-buffer sweep; TPB = 512: each half of the block transforms one grid
 // (the same operations per element), twice the waves per slot.
-template <class R, int CODED, int BPS, int NRX, int NP = 0, int TPB = MWG, int NC = 2048>
+// MRG (the merged link noise, launch_npow_sfbc_merged): the two link
+// accumulators of each RX hold instead sum_t |y0_rt|^2 (the links' powers
+// summed) and |y0_r|^2 (the RX stream's power) -- the same register count.
+template <class R, int CODED, int BPS, int NRX, int NP = 0, int TPB = MWG, int NC = 2048, bool MRG = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, TPB / 128))) void k_ofdm_txch_sfbc(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW,
                                                           const uint32_t* __restrict__ enc, int enc_words,
                                                           const int32_t* __restrict__ tx_map, TxLinkPower<R> lp,
@@ -961,13 +964,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
   int dl[PM];
 #pragma unroll
   for (int p = 0; p < PM; ++p) dl[p] = p < np ? lp.delays[p] : 0;
-  R pwr[NRX][NTX], prx[NRX];
+  R pwr[NRX][NTX];
 #pragma unroll
-  for (int r = 0; r < NRX; ++r) {
-    prx[r] = (R)0;
+  for (int r = 0; r < NRX; ++r)
 #pragma unroll
     for (int t = 0; t < NTX; ++t) pwr[r][t] = (R)0;
-  }
   const R sc = tx_scale<R>(N);
   constexpr int SFP = 4 * T / TPB;   // Alamouti pairs per thread per symbol (n_dsc / 2 <= SFP TPB)
   // (each pair's grid positions held in registers across the symbols instead of
@@ -1065,11 +1066,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
 #pragma unroll
           for (int p = 0; p < PM; ++p)
             if (p < np) a[t] = cadd(a[t], cmul(c[r][t][p], xs[t][p]));
-          pwr[r][t] += a[t].x * a[t].x + a[t].y * a[t].y;
+          if (!MRG) pwr[r][t] += a[t].x * a[t].x + a[t].y * a[t].y;
         }
         const V yr = cadd(a[0], a[1]);
         yl[(size_t)r * g.L + n] = yr;
-        prx[r] += yr.x * yr.x + yr.y * yr.y;
+        if constexpr (MRG) {
+          pwr[r][0] += (a[0].x * a[0].x + a[0].y * a[0].y) + (a[1].x * a[1].x + a[1].y * a[1].y);
+          pwr[r][1] += yr.x * yr.x + yr.y * yr.y;
+        }
       }
     }
     __syncthreads();   // every read of the old tails and of the grids done
@@ -1084,45 +1088,33 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128, 
 #pragma unroll
     for (int t = 0; t < NTX; ++t) {
       const R v = block_sum(pwr[r][t], red);
-      if (threadIdx.x == 0) lp.part[((size_t)b * NRX + r) * NTX + t] = v;   // one partial per link (nblk 1)
+      // one partial per link (nblk 1); MRG: per RX the links' sum, then the RX stream's
+      if (threadIdx.x == 0) lp.part[((size_t)b * NRX + r) * NTX + t] = v;
       __syncthreads();
     }
-  if (lp.rx_part) {   // the merged link noise: each RX stream's power (one partial per frame and RX)
-#pragma unroll
-    for (int r = 0; r < NRX; ++r) {
-      const R v = block_sum(prx[r], red);
-      if (threadIdx.x == 0) lp.rx_part[(size_t)b * NRX + r] = v;
-      __syncthreads();
-    }
-  }
 }
 
 // launch_npow_sfbc_merged (lte_internal.h): npow_eff per (frame, RX), in the
 // order oracle/mimo_oracle.transmit_mimo (merged) forms it
 template <class R>
-__global__ void k_npow_sfbc_merged(int n, int num_rx, int num_tx, const R* __restrict__ link_sigma,
-                                   const R* __restrict__ rx_part, int L, const R* __restrict__ snr_lin,
-                                   R* __restrict__ npow) {
+__global__ void k_npow_sfbc_merged(int n, int num_rx, const R* __restrict__ part, int L,
+                                   const R* __restrict__ snr_lin, double num_tx, R* __restrict__ npow) {
 #pragma clang fp contract(off)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double s2 = 0.0;
-  for (int t = 0; t < num_tx; ++t) {
-    const double st = (double)link_sigma[(size_t)i * num_tx + t];
-    s2 = s2 + st * st;
-  }
-  const double P = (double)rx_part[i] / L + 2.0 * s2;
-  const double na = (P / (double)num_tx) / (double)snr_lin[i / num_rx];
+  const double s2 = (((double)part[2 * i] / L) / 1e10) / 2.0;   // sum_t s_rt^2
+  const double P = (double)part[2 * i + 1] / L + 2.0 * s2;
+  const double na = (P / num_tx) / (double)snr_lin[i / num_rx];
   npow[i] = (R)(2.0 * s2 + na);
 }
 
 template <class R>
-int launch_npow_sfbc_merged(hipStream_t s, int B, int num_rx, int num_tx, const R* link_part, R* link_sigma,
-                            const R* rx_part, int L, const R* snr_lin, R* npow) {
-  const int n = B * num_rx, nl = n * num_tx;   // one link partial per link (k_ofdm_txch_sfbc)
-  hipLaunchKernelGGL(k_link_sigma<R>, dim3((nl + 255) / 256), dim3(256), 0, s, nl, link_part, 1, L, link_sigma);
-  hipLaunchKernelGGL(k_npow_sfbc_merged<R>, dim3((n + 255) / 256), dim3(256), 0, s, n, num_rx, num_tx, link_sigma,
-                     rx_part, L, snr_lin, npow);
+int launch_npow_sfbc_merged(hipStream_t s, int B, int num_rx, int num_tx, const R* link_part, int L, const R* snr_lin,
+                            R* npow) {
+  if (num_tx != 2) return (int)hipErrorInvalidValue;   // k_ofdm_txch_sfbc<.., MRG>'s two partials per RX
+  const int n = B * num_rx;
+  hipLaunchKernelGGL(k_npow_sfbc_merged<R>, dim3((n + 255) / 256), dim3(256), 0, s, n, num_rx, link_part, L, snr_lin,
+                     (double)num_tx, npow);
   return (int)hipGetLastError();
 }
 
@@ -1216,7 +1208,10 @@ int launch_ofdm_txch_sfbc(hipStream_t s, const Grid& g, const MimoGrid& m, int c
 #define LTE_SFX(C_, B_, NR_)                                                                                          \
   do {                                                                                                                \
     const int tpb = lp.n_paths == 4 ? LTE_SFX_TPB : MWG;                                                              \
-    auto k = lp.n_paths == 4 ? k_ofdm_txch_sfbc<R, C_, B_, NR_, 4, LTE_SFX_TPB> : k_ofdm_txch_sfbc<R, C_, B_, NR_, 0>; \
+    auto k = lp.n_paths == 4 ? (lp.merged ? k_ofdm_txch_sfbc<R, C_, B_, NR_, 4, LTE_SFX_TPB, 2048, true>          \
+                                          : k_ofdm_txch_sfbc<R, C_, B_, NR_, 4, LTE_SFX_TPB>)                         \
+                             : (lp.merged ? k_ofdm_txch_sfbc<R, C_, B_, NR_, 0, MWG, 2048, true>                     \
+                                          : k_ofdm_txch_sfbc<R, C_, B_, NR_, 0>);                                    \
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                  \
     hipLaunchKernelGGL(k, dim3(B), dim3(tpb), shm, s, g, m, pw, PW, enc, enc_words, tx_map, lp, y, B, stage_enc);     \
   } while (0)
@@ -2556,7 +2551,7 @@ int launch_det_stage(hipStream_t s, int det, int NR, int NT, int R, int bps, int
 #define LTE_MIMO_INST(R)                                                                                           \
   template int launch_ofdm_txch_sfbc<R>(hipStream_t, const Grid&, const MimoGrid&, int, const uint32_t*, int,     \
                                         const uint32_t*, int, const int32_t*, const TxLinkPower<R>&, cx<R>*, int); \
-  template int launch_npow_sfbc_merged<R>(hipStream_t, int, int, int, const R*, R*, const R*, int, const R*, R*); \
+  template int launch_npow_sfbc_merged<R>(hipStream_t, int, int, int, const R*, int, const R*, R*);             \
   template int launch_link_noise_add<R>(hipStream_t, const Grid&, const MimoGrid&, int, const R*, R*, cx<R>*,      \
                                         const uint64_t*, uint64_t, R*, int*);                                      \
   template bool sfbc_txch_supported<R>(const Grid&, const MimoGrid&, int, int);                                   \

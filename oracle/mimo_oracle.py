@@ -145,7 +145,7 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
         # chain: lte_internal.h launch_npow_sfbc_merged): no link-noise draw; its
         # power 2 s2 enters P in expectation and its variance the RX noise draw
         merged = comb and bool(draws[r].get('merged_link_noise'))
-        s2 = 0.0
+        s2, pl = 0.0, 0.0
         for t in range(num_tx):
             x = xs[t]
             if channel == 'awgn':
@@ -156,6 +156,7 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
                 d = draws[r]['links'][t]
                 y0 = multipath(x, dl, g, d['phases'], 0.0, num.fs)
                 p = np.mean(np.abs(y0) ** 2)
+                pl = pl + p
                 s = np.sqrt((p / 10 ** (100.0 / 10)) / 2)
                 s2 = s2 + s * s
                 y = y0 + (s * d['z_re'] + 1j * (s * d['z_im']))
@@ -170,6 +171,8 @@ def transmit_mimo(num: Numerology, xs, num_rx: int, channel: str, snr_db: float,
             Hm[r, t] = h
             acc += y
         if merged:
+            # the links' powers summed, then one sigma^2 (k_npow_sfbc_merged's order)
+            s2 = (pl / 10 ** (100.0 / 10)) / 2
             sp = np.mean(np.abs(acc) ** 2) + 2.0 * s2
             npow = 2.0 * s2 + (sp / num_tx) / 10 ** (snr_db / 10)
             s = np.sqrt(npow / 2)

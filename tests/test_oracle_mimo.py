@@ -180,8 +180,9 @@ def test_transmit_mimo_merged_link_noise(golden_mimo, oracle, mimo_oracle):
     """The device's merged mode (draws[r]['merged_link_noise'], config 4's full
     chain): no link-noise draw; the RX stream is the faded links' sum plus ONE
     draw of standard deviation sqrt((2 s2 + npow) / 2) on the RX noise numbers,
-    npow = ((mean |y0|^2 + 2 s2) / num_tx) / SNR -- the link noise's power in
-    expectation (k_npow_sfbc_merged's expression and order)."""
+    s2 = ((sum_t mean |y0_t|^2) / 1e10) / 2, npow = ((mean |y0|^2 + 2 s2) /
+    num_tx) / SNR -- the link noise's power in expectation (k_npow_sfbc_merged's
+    expression and order)."""
     num = _num(oracle, 20.0, '64-QAM')
     xs = [golden_mimo['txmimo_x0'], golden_mimo['txmimo_x1']]
     L = len(xs[0])
@@ -195,12 +196,12 @@ def test_transmit_mimo_merged_link_noise(golden_mimo, oracle, mimo_oracle):
     assert np.array_equal(H, H_c)   # each link's own draw still forms its Hm entry
     dl, g = mimo_oracle.itu_paths(num, 'Pedestrian_A')
     for r in range(2):
-        s2, y0 = 0.0, np.zeros(L, dtype=complex)
+        pl, y0 = 0.0, np.zeros(L, dtype=complex)
         for t in range(2):
             y = mimo_oracle.multipath(xs[t], dl, g, draws[r]['links'][t]['phases'], 0.0, num.fs)
-            s = np.sqrt((np.mean(np.abs(y) ** 2) / 1e10) / 2)
-            s2 = s2 + s * s
+            pl = pl + np.mean(np.abs(y) ** 2)
             y0 += y
+        s2 = (pl / 1e10) / 2
         npow = 2.0 * s2 + ((np.mean(np.abs(y0) ** 2) + 2.0 * s2) / 2) / 10 ** (snr / 10)
         st = np.sqrt(npow / 2)
         assert np.array_equal(ys[r], y0 + (st * draws[r]['z_re'] + 1j * (st * draws[r]['z_im'])))

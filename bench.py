@@ -440,7 +440,10 @@ def stage_bytes_per_frame(config, plan, prec):
         rows = sum(3 * K + 12 for K in segmentation_sizes(plan.n_bits + 24))
     if config in (2, 3):
         ctx = {2: 'k_ofdm_txf', 3: 'k_ofdm_tx'}[config]
-        crx = {2: 'k_rx_frame', 3: 'k_rx_frame_simo2'}[config]
+        # config 3, float64: the wave-private receiver (k_rx_frame_simo_w, the default; LTE_SIMO_RX_WAVE=0 the
+        # block kernel k_rx_frame_simo2)
+        simo_w = prec == 'f64' and N == 1024 and os.environ.get('LTE_SIMO_RX_WAVE', '1') != '0'
+        crx = {2: 'k_rx_frame', 3: 'k_rx_frame_simo_w' if simo_w else 'k_rx_frame_simo2'}[config]
         tx_in = plan.coded_bits / 8 if config == 2 else bits
         out = {'ofdm_tx': ([ctx], tx_in + nr * sym, 'payload / coded bits in, each RX stream (no CP) out'),
                'rx_data': ([crx], nr * sym + (0 if config == 2 else bits),

@@ -393,6 +393,12 @@ int launch_npow_mimo(hipStream_t s, int B, int num_rx, const R* pow_part, int nb
 // unless LTE_MIMO_RX_WAVE=0
 bool rx_fft_mimo_w_supported(const Grid& g, const MimoGrid& m, int f64, int h_pilots);
 int mimo_rx_wave_enabled();
+bool rx_simo_w_supported(const Grid& g, int num_rx, int f64, bool H, bool pstats, bool xin);
+int simo_rx_wave_enabled();
+int launch_rx_frame_simo_w(hipStream_t s, const Grid& g, int B, int num_rx, const double2* y, int64_t y_rx_stride,
+                           int64_t y_frame_stride, const double* npow, const uint64_t* fid, uint64_t seed,
+                           const double* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
+                           uint32_t* frame_err, double2* cap_syms, uint8_t* cap_bits);
 int launch_rx_fft_mimo_w(hipStream_t s, const Grid& g, const MimoGrid& m, int B, const double2* y, const double* npow,
                          const uint64_t* fid, uint64_t seed, const double* inj_z, int64_t inj_stride, double2* Y,
                          double2* H);

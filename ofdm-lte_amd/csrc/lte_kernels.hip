@@ -1943,6 +1943,12 @@ int launch_rx_frame_simo(hipStream_t s, const Grid& g, int B, int num_rx, const 
                          int64_t inj_stride, const uint32_t* pw, int PW, int n_bits, uint32_t* frame_err,
                          cx<R>* cap_syms, uint8_t* cap_bits, cx<R>* H, R* pstats, const TxChannelT<R>* xc) {
   if (!rx_frame_simo_supported(g, num_rx)) return (int)hipErrorInvalidValue;
+  if constexpr (sizeof(R) == 8) {   // config 3: the wave-private receiver (lte_wave.hip)
+    if (simo_rx_wave_enabled() &&
+        rx_simo_w_supported(g, num_rx, 1, H != nullptr, pstats != nullptr, xc && xc->x_out))
+      return launch_rx_frame_simo_w(s, g, B, num_rx, y, y_rx_stride, y_frame_stride, npow, fid, seed, inj_z, inj_stride,
+                                    pw, PW, n_bits, frame_err, cap_syms, cap_bits);
+  }
   const char* pe = std::getenv("LTE_RXS_PAIRS");   // 0: one slot per frame with T threads, the RX in sequence (A/B)
   if (rx_simo2_ok(g, num_rx, H != nullptr, pstats != nullptr) && (!pe || std::atoi(pe) != 0)) {
     const bool xin = xc && xc->x_out;

@@ -82,39 +82,49 @@ __device__ __forceinline__ cx<R> chest_interp(const Grid& g, const cx<R>* hp, in
   return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
 }
 
+// the fused SIMO receiver's per-RE interpolation (lte_kernels.hip interp_seg:
+// chest_interp with the segment, offset and 1 / gap precomputed per RE)
+template <class R>
+__device__ __forceinline__ cx<R> interp_seg(const cx<R>* hp, int np, int sidx, R fk, R ig) {
+  if (sidx < 0) return hp[0];
+  if (sidx >= np - 1) return hp[np - 1];
+  const cx<R> v0 = hp[sidx], v1 = hp[sidx + 1];
+  return mkc(fk * ((v1.x - v0.x) * ig) + v0.x, fk * ((v1.y - v0.y) * ig) + v0.y);
+}
 }  // namespace wrx
 
-// One OFDM symbol's N = 2048 received samples after its CP (stream offset
+// One OFDM symbol's N = 64 M received samples after its CP (stream offset
 // off) into wfft's register layout (lane l, register m = sample 64 m + l: 1 KB
 // per wave load instruction) plus sigma times the noise as load_symbol_noisy2
 // draws it: injected [2][L] draws, or one rng4 per sample pair on stream
 // RNG_STREAM_NOISE + rx, lanes 2t / 2t + 1 computing the pair counters of
 // registers m / m + 1 and trading halves with one DPP swap.  Half a symbol at
-// a time, a rolled loop draws into the wave's LDS scratch zs (16 KB) and each
-// register then adds its draw (unrolled over the registers, the 16 Philox + 32
-// Box-Muller chains took the kernel past 512 registers).
-template <class TB>
-__device__ __forceinline__ void wave_symbol_noisy(double2 (&v)[32], const double2* __restrict__ yf, int off, int lane,
+// a time, a rolled loop draws into the wave's LDS scratch zs (M / 2 KB) and
+// each register then adds its draw (unrolled over the registers, the 16 Philox
+// + 32 Box-Muller chains of N = 2048 took the kernel past 512 registers).
+template <int M, class TB>
+__device__ __forceinline__ void wave_symbol_noisy(double2 (&v)[M], const double2* __restrict__ yf, int off, int lane,
                                                   double sigma, uint64_t seed, uint64_t fr, int rx,
                                                   const double* __restrict__ zf, int L, double* scratch,
                                                   const TB& bmt) {
+  constexpr int MH = M / 2;
   const bool odd = lane & 1;
 #pragma unroll
-  for (int m = 0; m < 32; ++m) v[m] = yf[off + 64 * m + lane];
-  double2* zs = reinterpret_cast<double2*>(scratch);   // [16][64]
+  for (int m = 0; m < M; ++m) v[m] = yf[off + 64 * m + lane];
+  double2* zs = reinterpret_cast<double2*>(scratch);   // [M / 2][64]
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (zf) {
 #pragma unroll 1
-      for (int mm = 0; mm < 16; ++mm) {
-        const int n = off + 64 * (16 * h + mm) + lane;
+      for (int mm = 0; mm < MH; ++mm) {
+        const int n = off + 64 * (MH * h + mm) + lane;
         zs[64 * mm + lane] = make_double2(zf[n], zf[L + n]);
       }
     } else {
 #pragma unroll 1
-      for (int mm = 0; mm < 16; mm += 2) {
+      for (int mm = 0; mm < MH; mm += 2) {
         // even lanes: the pair counter of register m; odd lanes: of register m + 1
-        const int m = 16 * h + mm;
+        const int m = MH * h + mm;
         const uint32_t ctr = (uint32_t)((off + 64 * m + (odd ? 64 : 0) + lane) >> 1);
         const u32x4 r = rng4(seed, fr, RNG_STREAM_NOISE + (uint32_t)rx, ctr);
         const uint32_t t0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? r.x : r.z), 0xB1, 0xF, 0xF, true);
@@ -125,9 +135,9 @@ __device__ __forceinline__ void wave_symbol_noisy(double2 (&v)[32], const double
     }
     wfft::wave_lds_fence();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < MH; ++i) {
       const double2 z = zs[64 * i + lane];
-      v[16 * h + i] = make_double2(v[16 * h + i].x + sigma * z.x, v[16 * h + i].y + sigma * z.y);
+      v[MH * h + i] = make_double2(v[MH * h + i].x + sigma * z.x, v[MH * h + i].y + sigma * z.y);
     }
     wfft::wave_lds_fence();
   }
@@ -486,6 +496,139 @@ bool rx_fft_mimo_w_supported(const Grid& g, const MimoGrid& m, int f64, int h_pi
   return f64 && h_pilots && g.N == 2048 && g.kinfo && m.pval64 && g.cp % 2 == 0;
 }
 
+// ---------------------------------------------------------------------------
+// Wave-private fused SIMO MRC receiver (float64, N = 1024, uncoded: config 3;
+// k_rx_frame_simo2's outputs): one frame per 256-thread block, wave w owns RX
+// antenna w (num_rx <= 4).  Per symbol, two phases split by the block's only
+// two barriers:
+//   1. each RX wave loads its stream's 1024 samples after the CP plus the
+//      Philox noise (wave_symbol_noisy, the same draws) and transforms them
+//      with wfft::fft1024 (registers + one wave-local LDS transpose); the
+//      scaled data bins go to its row of yb by data ordinal (Grid::kinfo) and,
+//      on a group's first symbol, its pilot bins' LS estimates to hpa;
+//   2. every thread takes up to two data REs and folds the RX in order into
+//      the MRC sums exactly as k_rx_frame_simo2 does (interp_seg, abs2_ref,
+//      cmulc), then the hard decision and bit errors.
+// A wave's yb row doubles as its noise / transpose scratch (free once phase 2
+// has read it), so the block's LDS is 4 x 544 x 16 B + the estimates + the
+// per-RE interpolation terms + the Box-Muller tables (53 KB at 10 MHz): three
+// blocks per CU.
+#ifndef SIMOW_WPE
+#define SIMOW_WPE 3
+#endif
+constexpr int SIMOW_WAVES = 4;
+constexpr int SIMOW_ROW_MIN = (wfft::LDS_DOUBLES_1024 + 1) / 2;   // double2 slots a row needs as scratch
+static_assert(SIMOW_ROW_MIN * 16 >= 8 * 64 * 16, "a row holds the noise scratch (8 registers x 64 lanes)");
+template <int BPS>
+__global__ __launch_bounds__(64 * SIMOW_WAVES) __attribute__((amdgpu_waves_per_eu(SIMOW_WPE, SIMOW_WPE)))
+void k_rx_frame_simo_w(Grid g, int B, int num_rx, int yrow, const double2* __restrict__ y, int64_t y_rx_stride,
+                       int64_t y_frame_stride, const double* __restrict__ npow, const uint64_t* __restrict__ fid,
+                       uint64_t seed, const double* __restrict__ inj_z, int64_t inj_stride,
+                       const uint32_t* __restrict__ pw, int PW, int n_bits, uint32_t* __restrict__ frame_err,
+                       double2* __restrict__ cap_syms, uint8_t* __restrict__ cap_bits) {
+  constexpr int N = 1024, WGS = 64 * SIMOW_WAVES, QM = 2;
+  using G = GridT<double>;
+  LTE_BM_LDS_DECL(double);
+  const auto bmt = bm_stage<double>(lte_bmt);
+  const int tid0 = threadIdx.x, lane0 = tid0 & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  const int b = blockIdx.x;
+  double2* yb = dyn_lds<double2>();                 // [SIMOW_WAVES][yrow] scaled data bins
+  double2* hpa = yb + (size_t)SIMOW_WAVES * yrow;    // [num_rx][Np] LS pilot estimates of the group
+  int2* rtab = reinterpret_cast<int2*>(hpa + (size_t)num_rx * g.Np);   // [QM WGS] phase 2's per-RE terms
+  double* igl = reinterpret_cast<double*>(rtab + QM * WGS);            // [Np] 1 / pilot gap
+  double* tl = reinterpret_cast<double*>(yb + (size_t)w * yrow);
+  const double sc = rx_scale<double>(N);
+  constexpr double QS = qam_norm<BPS>();
+  const uint64_t fr = fid[b];
+  const uint32_t* fb = pw + (size_t)b * PW;
+  const size_t fre = (size_t)b * g.n_sym * g.Nd;
+  // phase 1's RX
+  const bool has_rx = w < num_rx;
+  const int rx = has_rx ? w : 0;
+  const double sigma = sqrt(npow[(size_t)b * num_rx + rx] / 2.0);
+  const double* zf = inj_z ? inj_z + (size_t)b * inj_stride + (size_t)rx * 2 * g.L : nullptr;
+  const double2* yr = y + (size_t)b * y_frame_stride + rx * y_rx_stride;
+  // phase 2's REs: chest_interp's per-subcarrier terms, staged in LDS once
+  // (held in registers across phase 1 they pushed the transform into spills;
+  // re-read from the tables per symbol they put a dependent load chain on the
+  // critical path): x = data SC | (segment + 1) << 16, y = offset from the
+  // segment's left pilot
+  double den[QM];   // the sum over RX of |h|^2, per group
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    den[q] = 0.0;
+    const int j = tid0 + q * WGS;
+    if (j < g.Nd) {
+      const int kpos = g.data_idx[j], sg = g.seg[kpos];
+      const int sc_ = sg < 0 ? 0 : (sg >= g.Np - 1 ? g.Np - 1 : sg);
+      rtab[j] = make_int2(kpos | ((sg + 1) << 16), kpos - g.pilot_idx[sc_]);
+    }
+  }
+  for (int p = tid0; p < g.Np; p += WGS) igl[p] = G::inv_gap(g)[p];
+  uint32_t errs = 0;
+  __syncthreads();   // the Box-Muller tables, rtab, igl
+  for (int l = 0; l < g.n_sym; ++l) {
+    const bool est = l % 14 == 0;
+    if (has_rx) {
+      int lane = lane0;   // opaque per symbol (see k_rx_frame_w)
+      asm volatile("" : "+v"(lane));
+      const int off = l * (N + g.cp) + g.cp;
+      double2 v[16];
+      wave_symbol_noisy(v, yr, off, lane, sigma, seed, fr, rx, zf, g.L, tl, bmt);
+      int lane_f = lane;
+      asm volatile("" : "+v"(lane_f));
+      wfft::fft1024<false>(v, tl, G::tw(g), lane_f);
+      double2* hp = hpa + rx * g.Np;
+      double2* yw = yb + (size_t)w * yrow;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = g.kinfo[64 * q + lane];
+        const double2 x = cscale(v[q], sc);
+        if (j >= 0) yw[j] = x;
+        else if (est && j <= -2) hp[-j - 2] = cdiv(x, G::pilots(g)[-j - 2]);   // lte_receiver.py:360-411
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = tid0 + q * WGS;
+      if (j >= g.Nd) continue;
+      const int2 rt = rtab[j];
+      const int sg = (rt.x >> 16) - 1;
+      const int sc_ = sg < 0 ? 0 : (sg >= g.Np - 1 ? g.Np - 1 : sg);
+      const double fk = (double)rt.y, ig = igl[sc_];
+      if (est) den[q] = 0.0;
+      double2 num = make_double2(0.0, 0.0);
+      for (int u = 0; u < num_rx; ++u) {   // the RX in order
+        const double2 h = wrx::interp_seg<double>(hpa + u * g.Np, g.Np, sg, fk, ig);
+        if (est) den[q] += wrx::abs2_ref(h);
+        num = cadd(num, cmulc(yb[(size_t)u * yrow + j], h));
+      }
+      const int re = l * g.Nd + j;
+      const double rr = 1.0 / (den[q] + 1e-10);
+      const double2 z = make_double2(num.x * rr, num.y * rr);
+      if (cap_syms) cap_syms[fre + re] = z;
+      const int idx = hard_index(z, BPS, QS);
+      const int64_t pb0 = (int64_t)re * BPS;
+      errs += __popc(((uint32_t)idx ^ getbits<BPS>(fb, pb0, n_bits)) & bits_valid<BPS>(pb0, n_bits));
+      if (cap_bits) {
+#pragma unroll
+        for (int m = 0; m < BPS; ++m)
+          if (pb0 + m < n_bits) cap_bits[(size_t)b * n_bits + pb0 + m] = (uint8_t)((idx >> (BPS - 1 - m)) & 1);
+      }
+    }
+    __syncthreads();   // every read of yb / hpa done before the next symbol's phase 1
+  }
+  frame_err_add(frame_err, b, errs);
+}
+
+bool rx_simo_w_supported(const Grid& g, int num_rx, int f64, bool H, bool pstats, bool xin) {
+  return f64 && g.N == 1024 && g.kinfo && g.pilots64 && g.cp % 2 == 0 && num_rx >= 1 && num_rx <= SIMOW_WAVES &&
+         num_rx <= RXS_MAXRX && !H && !pstats && !xin && g.Nd <= 2 * 64 * SIMOW_WAVES && g.Np >= 1 &&
+         (g.bps == 2 || g.bps == 4 || g.bps == 6);
+}
+
 // Which wave-private kernels run by default (same-box A/B, profiles/r6_wave_ab.md):
 // the config-5 RX (k_rx_fft_mimo_w) beats its block kernel; the config-2 RX and
 // TX do not (2 waves per SIMD at most with a symbol in registers, against 3 for
@@ -504,6 +647,29 @@ static int env_or(const char* name, int dflt) {
 }
 int rx_wave_enabled() { return env_or("LTE_RX_WAVE", LTE_RX_WAVE); }
 int mimo_rx_wave_enabled() { return env_or("LTE_MIMO_RX_WAVE", LTE_MIMO_RX_WAVE); }
+#ifndef LTE_SIMO_RX_WAVE
+#define LTE_SIMO_RX_WAVE 1
+#endif
+int simo_rx_wave_enabled() { return env_or("LTE_SIMO_RX_WAVE", LTE_SIMO_RX_WAVE); }
+
+int launch_rx_frame_simo_w(hipStream_t s, const Grid& g, int B, int num_rx, const double2* y, int64_t y_rx_stride,
+                           int64_t y_frame_stride, const double* npow, const uint64_t* fid, uint64_t seed,
+                           const double* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,
+                           uint32_t* frame_err, double2* cap_syms, uint8_t* cap_bits) {
+  if (!rx_simo_w_supported(g, num_rx, 1, false, false, false)) return (int)hipErrorInvalidValue;
+  const int yrow = g.Nd > SIMOW_ROW_MIN ? g.Nd : SIMOW_ROW_MIN;
+  const size_t shm = ((size_t)SIMOW_WAVES * yrow + (size_t)num_rx * g.Np) * sizeof(double2) +
+                     (size_t)2 * 64 * SIMOW_WAVES * sizeof(int2) + (size_t)g.Np * sizeof(double);
+#define LTE_SIMOW(BPS_)                                                                                             \
+  hipLaunchKernelGGL(k_rx_frame_simo_w<BPS_>, dim3(B), dim3(64 * SIMOW_WAVES), shm, s, g, B, num_rx, yrow, y,       \
+                     y_rx_stride, y_frame_stride, npow, fid, seed, inj_z, inj_stride, pw, PW, n_bits, frame_err,    \
+                     cap_syms, cap_bits)
+  if (g.bps == 2) LTE_SIMOW(2);
+  else if (g.bps == 4) LTE_SIMOW(4);
+  else LTE_SIMOW(6);
+#undef LTE_SIMOW
+  return (int)hipGetLastError();
+}
 
 int launch_rx_frame_w(hipStream_t s, const Grid& g, int rayleigh, int B, const double2* y, int64_t y_frame_stride,
                       const double* npow, const double* snr_lin, const uint64_t* fid, uint64_t seed,

@@ -1,8 +1,8 @@
-// Microbenchmark: the wave-private float64 2048-point FFT (csrc/lte_wfft.h)
-// against the workgroup LDS FFT the front-end kernels use today (fft_lds in
-// csrc/lte_common.h, 256 threads per transform, a barrier per pass).
+// Microbenchmark: the wave-private float64 2048- / 1024-point FFTs
+// (csrc/lte_wfft.h) against the workgroup LDS FFT of the block kernels (fft_lds
+// in csrc/lte_common.h, N / 8 threads per transform, a barrier per pass).
 //
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../ofdm-lte_amd/csrc wfft_bench.hip -o wfft_bench
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../ofdm-lte_amd/csrc [-DWN=1024] wfft_bench.hip -o wfft_bench
 //   ./wfft_bench [M transforms] [REP]
 //
 // Two modes per kernel: HBM (load, one transform, store) and compute (load,
@@ -25,23 +25,28 @@
     }                                                                                \
   } while (0)
 
-constexpr int N = 2048;
+#ifndef WN
+#define WN 2048
+#endif
+constexpr int N = WN, TL = N / 8, LOG2N = N == 2048 ? 11 : 10, MR = N / 64;
+constexpr int WLDS = N == 2048 ? wfft::LDS_DOUBLES : wfft::LDS_DOUBLES_1024;
+static_assert(N == 2048 || N == 1024, "wfft sizes");
 
 template <bool INV, int REP>
-__global__ __launch_bounds__(256) void k_lds(const double2* __restrict__ in, double2* __restrict__ out,
+__global__ __launch_bounds__(TL) void k_lds(const double2* __restrict__ in, double2* __restrict__ out,
                                              const double2* __restrict__ tw, int M) {
   extern __shared__ double2 buf[];
   const int t = blockIdx.x;
   if (t >= M) return;   // uniform per block
   const double2* x = in + (size_t)t * N;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) buf[threadIdx.x + 256 * r] = x[threadIdx.x + 256 * r];
+  for (int r = 0; r < 8; ++r) buf[threadIdx.x + TL * r] = x[threadIdx.x + TL * r];
   __syncthreads();
 #pragma unroll 1
-  for (int rep = 0; rep < REP; ++rep) fft_lds<INV, N, false, true, false>(buf, N, 11, tw, threadIdx.x, true);
+  for (int rep = 0; rep < REP; ++rep) fft_lds<INV, N, false, true, false>(buf, N, LOG2N, tw, threadIdx.x, true);
   double2* y = out + (size_t)t * N;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) y[threadIdx.x + 256 * r] = buf[threadIdx.x + 256 * r];
+  for (int r = 0; r < 8; ++r) y[threadIdx.x + TL * r] = buf[threadIdx.x + TL * r];
 }
 
 #ifndef WPE
@@ -54,20 +59,21 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE, WPE
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = blockIdx.x * W + w;
   if (t >= M) return;   // uniform per wave; no barrier below
-  double* lds = lds_d + w * wfft::LDS_DOUBLES;
+  double* lds = lds_d + w * WLDS;
   const double2* x = in + (size_t)t * N;
-  double2 v[32];
+  double2 v[MR];
 #pragma unroll
-  for (int m = 0; m < 32; ++m) v[m] = x[64 * m + lane];
+  for (int m = 0; m < MR; ++m) v[m] = x[64 * m + lane];
 #pragma unroll 1
   for (int rep = 0; rep < REP; ++rep) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    wfft::fft2048<INV>(v, lds, tw, ln);
+    if constexpr (N == 2048) wfft::fft2048<INV>(v, lds, tw, ln);
+    else wfft::fft1024<INV>(v, lds, tw, ln);
   }
   double2* y = out + (size_t)t * N;
 #pragma unroll
-  for (int q = 0; q < 32; ++q) y[64 * q + lane] = v[q];
+  for (int q = 0; q < MR; ++q) y[64 * q + lane] = v[q];
 }
 
 static double lcg(uint64_t& s) {
@@ -109,9 +115,9 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d_in, h.data(), n * 16, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_tw, tw.data(), N * 16, hipMemcpyHostToDevice));
 
-  auto run_lds = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(M), dim3(256), N * 16, 0, d_in, d_a, d_tw, M); };
+  auto run_lds = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(M), dim3(TL), N * 16, 0, d_in, d_a, d_tw, M); };
   auto run_wave = [&](auto kern, int W) {
-    hipLaunchKernelGGL(kern, dim3((M + W - 1) / W), dim3(64 * W), W * wfft::LDS_DOUBLES * 8, 0, d_in, d_b, d_tw, M);
+    hipLaunchKernelGGL(kern, dim3((M + W - 1) / W), dim3(64 * W), W * WLDS * 8, 0, d_in, d_b, d_tw, M);
   };
   // correctness (forward and inverse, REP = 1)
   for (int inv = 0; inv < 2; ++inv) {
@@ -152,14 +158,14 @@ int main(int argc, char** argv) {
         xmax = fmax(xmax, (double)fabsl(re));
       }
     }
-    printf("{\"check\": \"%s\", \"max_abs_lds_vs_wave\": %.3e, \"max_abs_out\": %.3e, "
+    printf("{\"N\": %d, \"check\": \"%s\", \"max_abs_lds_vs_wave\": %.3e, \"max_abs_out\": %.3e, "
            "\"err_lds_vs_ldouble\": %.3e, \"err_wave_vs_ldouble\": %.3e, \"ref_max\": %.3e}\n",
-           inv ? "inverse" : "forward", dmax, amax, ea, eb, xmax);
+           N, inv ? "inverse" : "forward", dmax, amax, ea, eb, xmax);
   }
   // timing
   const double bytes = 2.0 * n * 16;
   auto line = [&](const char* k, int rep, float ms) {
-    printf("{\"kernel\": \"%s\", \"M\": %d, \"rep\": %d, \"ms\": %.4f, \"GBps\": %.1f, \"ns_per_fft\": %.3f}\n", k, M,
+    printf("{\"kernel\": \"%s\", \"N\": %d, \"M\": %d, \"rep\": %d, \"ms\": %.4f, \"GBps\": %.1f, \"ns_per_fft\": %.3f}\n", k, N, M,
            rep, ms, bytes / ms / 1e6, ms * 1e6 / ((double)M * rep));
   };
   line("lds", 1, timeit([&] { run_lds(k_lds<false, 1>); }, 10));

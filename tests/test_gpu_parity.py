@@ -517,6 +517,7 @@ def test_simo_symbol_handoff_matches_rx_streams(C, monkeypatch, prec, inject):
     if inject:
         kw = dict(noise=np.random.default_rng(5).standard_normal((B, 4, 2, plan.L)))
     runs = {}
+    monkeypatch.setenv('LTE_SIMO_RX_WAVE', '0')   # both sides on k_rx_frame_simo2 (the wave receiver: its own test)
     for xh in ('0', '1'):
         monkeypatch.setenv('LTE_SIMO_XHAND', xh)
         runs[xh] = (plan.run(snr, seed=0x5EED, frame_id0=11, capture=('data_syms', 'bits_rx', 'noise_power'), **kw),
@@ -582,6 +583,7 @@ def test_simo_receiver_rx_pairs_match_sequential(C, monkeypatch, nrx, mod, prec)
     snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
     cap = ('data_syms', 'bits_rx')
     runs = {}
+    monkeypatch.setenv('LTE_SIMO_RX_WAVE', '0')   # k_rx_frame_simo2, not the wave receiver (its own test)
     for pairs in ('0', '1'):
         monkeypatch.setenv('LTE_RXS_PAIRS', pairs)
         runs[pairs] = plan.run(snr, seed=0x5EED, frame_id0=77, capture=cap)
@@ -594,6 +596,39 @@ def test_simo_receiver_rx_pairs_match_sequential(C, monkeypatch, nrx, mod, prec)
         assert np.max(np.abs(b['data_syms'] - a['data_syms'])) <= 1e-5 * np.max(np.abs(a['data_syms']))
         assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 2
     assert 0 < int(b['counts'][:, 0].sum())
+
+
+@pytest.mark.parametrize('nrx,mod,inject', [(4, '16-QAM', False), (4, '16-QAM', True), (2, '64-QAM', False),
+                                            (4, 'QPSK', False)])
+def test_wave_simo_receiver_matches_block_receiver(C, monkeypatch, nrx, mod, inject):
+    """10 MHz SIMO MRC, float64: the wave-private receiver (k_rx_frame_simo_w:
+    one wave per RX with wfft::fft1024, the MRC sums in RX order in LDS; the
+    default) against k_rx_frame_simo2 (LTE_SIMO_RX_WAVE=0) on the same Philox
+    (or injected) noise.  Only the transform's rounding differs (both FFTs
+    within a few 1e-14 of the exact DFT), so combined symbols agree to 1e-12 of
+    their scale and decisions and counts match (a decision flip needs a symbol
+    within ~1e-13 of a boundary: at most 2 allowed)."""
+    import lte_phy
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=10.0, modulation=mod), channel_type='rayleigh_mp',
+                                itu_profile='Vehicular_A', precision='f64')
+    B = 64 + 3
+    bps = sim.config.bits_per_symbol
+    plan = sim._plan(C.CHAIN_SIMO, 14, 14 * sim.Nd * bps - 5, num_rx=nrx, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    kw = {}
+    if inject:
+        kw = dict(noise=np.random.default_rng(7).standard_normal((B, nrx, 2, plan.L)))
+    runs = {}
+    for wave in ('0', '1'):
+        monkeypatch.setenv('LTE_SIMO_RX_WAVE', wave)
+        runs[wave] = (plan.run(snr, seed=0x5EED, frame_id0=77, capture=('data_syms', 'bits_rx'), **kw),
+                      plan.run(snr, seed=0x5EED, frame_id0=77, **kw))
+    (a, a0), (b, b0) = runs['0'], runs['1']
+    assert np.max(np.abs(b['data_syms'] - a['data_syms'])) <= 1e-12 * np.max(np.abs(a['data_syms']))
+    assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 2
+    assert abs(int(a0['counts'][:, 0].sum()) - int(b0['counts'][:, 0].sum())) <= 2
+    assert np.array_equal(a0['counts'][:, 1], b0['counts'][:, 1])
+    assert 0 < int(b0['counts'][:, 0].sum())
 
 
 @pytest.mark.parametrize('prec', ['f64', 'f32'])

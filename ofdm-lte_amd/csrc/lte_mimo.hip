@@ -23,6 +23,7 @@
 #include "lte_common.h"
 #include "lte_internal.h"
 #include "lte_dev.h"
+#include "lte_wfft.h"
 
 #include <algorithm>
 #include <cmath>
@@ -410,6 +411,128 @@ __global__ __launch_bounds__(MWG) void k_ofdm_txch_flat(Grid g, MimoGrid m, cons
   }
 }
 
+// Wave-private spatial TX + flat links (float64, N = 2048; k_ofdm_txch_flat's
+// outputs): one wave64 per (frame, RX antenna) walks the frame's symbols.  The
+// effective channel E_c = sum_t h_rt W[t][c] is formed once per wave.  Per
+// symbol, lane c, register q gets bin k = 64 q + c of Y_r = sum_t h_rt G_t
+// (formed half a symbol at a time by a rolled loop through the wave's LDS,
+// from Grid::kinfo): a data SC j < n_dsc carries
+// sum_c E_c s_c (the same terms in the same order as the block kernel), pilot
+// i of the grid is TX t = i % step's pilot i / step (plan_mimo_tables' split)
+// times h_rt, anything else 0; wfft::fft2048<INV> and the output scale give
+// y_r[64 q + c], written with its CP (1 KB per wave store) and summed into the
+// symbol's power partial by one wave reduction.  No block barrier, and the
+// only LDS is the transform's 16.5 KB per wave.  The transform's and the
+// power sum's rounding differ from the block kernel's (a few 1e-14).
+constexpr int TXMW_WAVES = 4;
+constexpr int TXMW_LDS = wfft::LDS_DOUBLES + 8;   // doubles per wave: the transform + E
+#ifndef TXMW_WPE
+#define TXMW_WPE 2
+#endif
+#ifndef TXMW_BIN_UNROLL
+#define TXMW_BIN_UNROLL 8
+#endif
+template <int CODED, int BPS>
+__global__ __launch_bounds__(64 * TXMW_WAVES) __attribute__((amdgpu_waves_per_eu(TXMW_WPE, TXMW_WPE)))
+void k_ofdm_txch_flat_w(Grid g, MimoGrid m, const uint32_t* __restrict__ pw, int PW, const uint32_t* __restrict__ enc,
+                        int enc_words, const int32_t* __restrict__ tx_map, const double2* __restrict__ coef,
+                        double2* __restrict__ y, double* __restrict__ pow_part, int nblk, int B) {
+  constexpr int N = 2048, NCF = mimo_ncf<double>();
+  using V = double2;
+  extern __shared__ double lte_txmw_lds[];
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gs = blockIdx.x * TXMW_WAVES + w;
+  const int b = gs / m.num_rx, r = gs - b * m.num_rx;
+  if (b >= B) return;   // uniform per wave; no block barrier below
+  double* tl = lte_txmw_lds + (size_t)w * TXMW_LDS;
+  V* Es = reinterpret_cast<V*>(tl + wfft::LDS_DOUBLES);   // [4] E_c (in LDS, not registers: live across
+                                                          // the transform they pushed it into spills)
+  const uint32_t* fb = pw + (size_t)b * PW;
+  const uint32_t* fe = enc + (size_t)b * enc_words;
+  const size_t br = (size_t)b * m.num_rx + r;
+  const V* hr = coef + br * m.num_tx * NCF;   // h_rt at hr[t * NCF]
+  if (lane0 < 4) {
+    const int c = lane0;
+    V e = mkc(0.0, 0.0);
+    if (c < m.rank)
+      for (int t = 0; t < m.num_tx; ++t)
+        e = cadd(e, cmul(hr[t * NCF], mkc(m.W[(t * 4 + c) * 2], m.W[(t * 4 + c) * 2 + 1])));
+    Es[c] = e;
+  }
+  wfft::wave_lds_fence();
+  const int step = m.num_tx <= 4 ? m.num_tx : 4;
+  const double sc = tx_scale<double>(N);
+  const V* pv64 = MGT<double>::pval(m);
+  for (int l = 0; l < g.n_sym; ++l) {
+    int lane = lane0;   // opaque per symbol (see k_rx_frame_w)
+    asm volatile("" : "+v"(lane));
+    const int64_t q0 = (int64_t)l * m.res;
+    V v[32];
+    V* zs = reinterpret_cast<V*>(tl);   // [16][64]: half a symbol's bins
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // partly rolled: the bin code TXMW_BIN_UNROLL times (unrolled over 32
+      // registers it spilled; fully rolled, each bin's kinfo -> payload-bit
+      // load chain waited alone)
+#pragma unroll TXMW_BIN_UNROLL
+      for (int mm = 0; mm < 16; ++mm) {
+        const int kq = g.kinfo[64 * (16 * h + mm) + lane];
+        V acc = mkc(0.0, 0.0);
+        if (kq >= 0 && kq < m.n_dsc) {   // sum_t h_rt (W s)_t = sum_c E_c s_c
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int qi = m.rank * kq + c;
+            if (c < m.rank && qi < m.res)
+              acc = cadd(acc, cmul(Es[c], qam_at<double, CODED, BPS>(q0 + qi, fb, fe, tx_map)));
+          }
+        } else if (kq <= -2) {   // grid pilot i: TX i % step's pilot i / step
+          const int i = -kq - 2, t = i % step;
+          acc = cmul(hr[t * NCF], pv64[t * m.maxP + i / step]);
+        }
+        zs[64 * mm + lane] = acc;
+      }
+      wfft::wave_lds_fence();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[16 * h + i] = zs[64 * i + lane];
+      wfft::wave_lds_fence();
+    }
+    int lane_f = lane;
+    asm volatile("" : "+v"(lane_f));
+    wfft::fft2048<true>(v, tl, GridT<double>::tw(g), lane_f);
+    V* yo = y + br * g.L + (size_t)l * (N + g.cp);
+    const int cs = N - g.cp;   // the CP repeats samples cs .. N - 1
+    double pwr = 0.0;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const V x = cscale(v[q], sc);
+      const int n = 64 * q + lane_f;
+      yo[g.cp + n] = x;
+      const double e = x.x * x.x + x.y * x.y;
+      pwr += e;
+      if (q >= 24 && n >= cs) {   // (cp <= 512: only the last 8 registers hold CP samples)
+        yo[n - cs] = x;
+        pwr += e;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pwr += __shfl_xor(pwr, o);
+    if (lane_f == 0) pow_part[br * nblk + l] = pwr;
+  }
+}
+
+bool txch_flat_w_supported(const Grid& g, const MimoGrid& m, int f64) {
+  return f64 && g.N == 2048 && g.kinfo && m.pval64 && m.mode == MIMO_SPATIAL && m.num_tx >= 1 && m.num_tx <= 4 &&
+         m.rank >= 1 && m.rank <= 4 && g.cp >= 0 && g.cp <= 512;
+}
+
+// Opt-in (profiles/r6_mimo_tx_wave/): the TX itself runs 22.5 against 23.3 ms
+// per 32 768 config-5 frames, but the receiver that follows it loses as much
+// (26.8-27.1 against 26.4-26.5 ms), so config 5 does not move.
+#ifndef LTE_MIMO_TX_WAVE
+#define LTE_MIMO_TX_WAVE 0
+#endif
+
 template <class R>
 int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int coded, const uint32_t* pw, int PW,
                           const uint32_t* enc, int enc_words, const int32_t* tx_map, const cx<R>* coef, cx<R>* y,
@@ -424,6 +547,26 @@ int launch_ofdm_txch_flat(hipStream_t s, const Grid& g, const MimoGrid& m, int c
   if (total > 0x7FFFFFFF - spw || (g.bps != 2 && g.bps != 4 && g.bps != 6) || (g.N >> 3) < 64 || nblk < g.n_sym ||
       m.num_tx > 4)
     return (int)hipErrorInvalidValue;
+  if constexpr (sizeof(R) == 8) {   // the wave-private kernel (LTE_MIMO_TX_WAVE=1)
+    const char* we = std::getenv("LTE_MIMO_TX_WAVE");
+    if ((we ? std::atoi(we) != 0 : LTE_MIMO_TX_WAVE) && !pr && txch_flat_w_supported(g, m, 1)) {
+      const int64_t waves = (int64_t)B * m.num_rx;
+      if (waves > 0x7FFFFFFF - TXMW_WAVES) return (int)hipErrorInvalidValue;
+      const unsigned wb = (unsigned)((waves + TXMW_WAVES - 1) / TXMW_WAVES);
+      const size_t wshm = (size_t)TXMW_WAVES * TXMW_LDS * sizeof(double);
+#define LTE_TXFW(C_, B_)                                                                                             \
+  hipLaunchKernelGGL((k_ofdm_txch_flat_w<C_, B_>), dim3(wb), dim3(64 * TXMW_WAVES), wshm, s, g, m, pw, PW, enc,      \
+                     enc_words, tx_map, reinterpret_cast<const double2*>(coef), reinterpret_cast<double2*>(y),       \
+                     reinterpret_cast<double*>(pow_part), nblk, B)
+      if (coded) {
+        if (g.bps == 2) LTE_TXFW(1, 2); else if (g.bps == 4) LTE_TXFW(1, 4); else LTE_TXFW(1, 6);
+      } else {
+        if (g.bps == 2) LTE_TXFW(0, 2); else if (g.bps == 4) LTE_TXFW(0, 4); else LTE_TXFW(0, 6);
+      }
+#undef LTE_TXFW
+      return (int)hipGetLastError();
+    }
+  }
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t enc_shm = (size_t)spw * enc_words * sizeof(uint32_t);
   const int stage_enc = coded && enc_shm <= 32768;

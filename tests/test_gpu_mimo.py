@@ -351,6 +351,34 @@ def test_wave_mimo_receiver_matches_block_receiver(C, chan, det, inject, monkeyp
     assert np.array_equal(a['counts'], b['counts'])
 
 
+@pytest.mark.parametrize('det,inject,rank', [('DET_MMSE', False, 4), ('DET_SIC', True, 4), ('DET_ZF', False, 2)])
+def test_wave_mimo_tx_matches_block_tx(C, det, inject, rank, monkeypatch):
+    """Config 5's TX + flat links as one wave per (frame, RX antenna)
+    (k_ofdm_txch_flat_w: the bins of Y_r = sum_t h_rt G_t formed through the
+    wave's LDS, wfft's 2048-point inverse FFT, the CP and the power partial by
+    one wave reduction) vs the block kernel k_ofdm_txch_flat on the same frames:
+    the transforms and power sums differ in round-off only, so per-frame bit
+    errors and counts are identical.  7 frames x 4 RX = 28 waves: a partial
+    last block; rank 2 too."""
+    from lte_phy.ofdm_core import _spatial_plan
+    sim = _sim(20.0, '64-QAM', 'awgn', 'f64')
+    nb = 14 * 999 * 6
+    plan = _spatial_plan(sim.config, 'awgn', 'Pedestrian_A', 3.0, 2.0, 14, nb, 7, detector=getattr(C, det),
+                         precision='f64', rank=rank)[0]
+    snrs = np.array([6.0, 10.0, 14.0, 18.0, 22.0, 26.0, 30.0])
+    kw = {}
+    if inject:
+        kw = dict(noise=np.random.default_rng(4).standard_normal((7, 4, 2, plan.L)))
+    outs = []
+    for wave in ('1', '0'):
+        monkeypatch.setenv('LTE_MIMO_TX_WAVE', wave)
+        outs.append(plan.run(snrs, seed=19, frame_id0=555, **kw))
+    a, b = outs
+    assert 0 < int(a['counts'][:, 0].sum())
+    assert np.array_equal(a['frame_errors'], b['frame_errors'])
+    assert np.array_equal(a['counts'], b['counts'])
+
+
 @pytest.mark.parametrize('prec', ['f64', 'f32'])
 @pytest.mark.parametrize('mimo,coded,chan', [('sfbc', True, 'rayleigh_mp'), ('spatial', False, 'rayleigh_mp'),
                                             ('spatial', False, 'awgn')])

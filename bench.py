@@ -439,7 +439,9 @@ def stage_bytes_per_frame(config, plan, prec):
         from lte_phy.channel_coding import segmentation_sizes
         rows = sum(3 * K + 12 for K in segmentation_sizes(plan.n_bits + 24))
     if config in (2, 3):
-        ctx = {2: 'k_ofdm_txf', 3: 'k_ofdm_tx'}[config]
+        # config 3, float64: the wave-private TX (k_ofdm_tx_simo_w, the default; LTE_SIMO_TX_WAVE=0: k_ofdm_tx)
+        simo_tw = prec == 'f64' and N == 1024 and os.environ.get('LTE_SIMO_TX_WAVE', '1') != '0'
+        ctx = {2: 'k_ofdm_txf', 3: 'k_ofdm_tx_simo_w' if simo_tw else 'k_ofdm_tx'}[config]
         # config 3, float64: the wave-private receiver (k_rx_frame_simo_w, the default; LTE_SIMO_RX_WAVE=0 the
         # block kernel k_rx_frame_simo2)
         simo_w = prec == 'f64' and N == 1024 and os.environ.get('LTE_SIMO_RX_WAVE', '1') != '0'
@@ -499,7 +501,7 @@ def stage_bytes_per_frame(config, plan, prec):
 
 # the committed rocprofv3 --pmc summary of each config's bench step (the
 # traffic beside each stage's algorithmic bytes; tests/test_roofline_pmc.py)
-PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r6_pmc_c3_wave.json', 4: 'r6_pmc_c4_merged.json',
+PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r6_pmc_c3_wave2.json', 4: 'r6_pmc_c4_merged.json',
              5: 'r6_pmc_c5.json'}
 
 

@@ -395,6 +395,10 @@ bool rx_fft_mimo_w_supported(const Grid& g, const MimoGrid& m, int f64, int h_pi
 int mimo_rx_wave_enabled();
 bool rx_simo_w_supported(const Grid& g, int num_rx, int f64, bool H, bool pstats, bool xin);
 int simo_rx_wave_enabled();
+bool tx_simo_w_supported(const Grid& g, int f64, int coded, int sc_fdm, const TxChannelT<double>& ch);
+int simo_tx_wave_enabled();
+int launch_ofdm_tx_simo_w(hipStream_t s, const Grid& g, const uint32_t* pw, int PW, int B, double2* cap_syms,
+                          const TxChannelT<double>& ch);
 int launch_rx_frame_simo_w(hipStream_t s, const Grid& g, int B, int num_rx, const double2* y, int64_t y_rx_stride,
                            int64_t y_frame_stride, const double* npow, const uint64_t* fid, uint64_t seed,
                            const double* inj_z, int64_t inj_stride, const uint32_t* pw, int PW, int n_bits,

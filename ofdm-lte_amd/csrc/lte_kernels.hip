@@ -465,6 +465,10 @@ int launch_ofdm_tx_ch(hipStream_t s, const Grid& g, int coded, const uint32_t* p
   if (!txch_supported(g, ch.n_paths, ch.max_delay) || total > 0x7FFFFFFF - spw ||
       (g.bps != 2 && g.bps != 4 && g.bps != 6))
     return (int)hipErrorInvalidValue;
+  if constexpr (sizeof(R) == 8) {   // config 3: the wave-private TX (lte_wave.hip; LTE_SIMO_TX_WAVE=0: this kernel)
+    if (simo_tx_wave_enabled() && tx_simo_w_supported(g, 1, coded, sc_fdm, ch))
+      return launch_ofdm_tx_simo_w(s, g, pw, PW, B, cap_syms, ch);
+  }
   const int blocks = (int)((total + spw - 1) / spw);
   const size_t enc_shm = tx_enc_shm(coded, spw, enc_words);
   const int stage_enc = enc_shm > 0;

@@ -629,6 +629,110 @@ bool rx_simo_w_supported(const Grid& g, int num_rx, int f64, bool H, bool pstats
          (g.bps == 2 || g.bps == 4 || g.bps == 6);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-private uncoded OFDM TX + static-tap SIMO channel (float64, N = 1024:
+// config 3; k_ofdm_tx<.., CH = 1>'s outputs): one wave64 per (frame, OFDM
+// symbol), no block barrier.  Lane c, register q builds bin k = 64 q + c from
+// Grid::kinfo (a data RE's BPS payload bits -> qam_point, a pilot, or 0);
+// wfft::fft1024<INV> and the output scale give x[64 q + c], which is staged in
+// the wave's LDS (16 KB, the transform's scratch before) so that every RX's
+// taps read their cyclic shifts: received sample n = sum_p c_rp x[(n - d_p)
+// mod N] (every delay <= CP), the same terms in the same order as tx_channel.
+// Each RX's N samples after the CP go out as 1 KB wave stores; its power
+// partial is the sum of |y|^2 over those samples plus the CP samples past
+// max_delay (cyclically the last cp - max_delay samples again), by one wave
+// reduction (tx_channel sums the same values in another order).
+constexpr int TXSW_WAVES = 2;   // (LDS: 16 KB per wave, five blocks per CU)
+#ifndef TXSW_UNROLL
+#define TXSW_UNROLL 4
+#endif
+template <int BPS, int NP>
+__global__ __launch_bounds__(64 * TXSW_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, double2* __restrict__ cap_syms,
+                      TxChannelT<double> ch) {
+  constexpr int N = 1024;
+  using G = GridT<double>;
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gs = blockIdx.x * TXSW_WAVES + w;
+  const int b = gs / g.n_sym, l = gs - b * g.n_sym;
+  if (b >= B) return;   // uniform per wave; no block barrier below
+  double2* xs = dyn_lds<double2>() + (size_t)w * N;
+  int lane = lane0;
+  asm volatile("" : "+v"(lane));
+  // 1. the bins (QAMModulator.bits_to_symbols, ResourceMapper.map_symbols)
+  const uint32_t* fb = pw + (size_t)b * PW;
+  const size_t cre = ((size_t)b * g.n_sym + l) * g.Nd;
+  double2 v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int kq = g.kinfo[64 * q + lane];
+    double2 x = make_double2(0.0, 0.0);
+    if (kq >= 0) {
+      const int idx = (int)getbits<BPS>(fb, ((int64_t)l * g.Nd + kq) * BPS, INT64_MAX);
+      x = qam_point<BPS, double>(idx);
+      if (cap_syms) cap_syms[cre + kq] = x;
+    } else if (kq <= -2) {
+      x = G::pilots(g)[-kq - 2];
+    }
+    v[q] = x;
+  }
+  // 2. ifft * sqrt(N) (modulator.py:242-248), staged for the taps
+  int lane_f = lane;
+  asm volatile("" : "+v"(lane_f));
+  wfft::fft1024<true>(v, reinterpret_cast<double*>(xs), G::tw(g), lane_f);
+  const double sc = tx_scale<double>(N);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) xs[64 * q + lane_f] = cscale(v[q], sc);
+  wfft::wave_lds_fence();
+  const int cp = g.cp, S = N + cp, D = ch.max_delay;
+  if (D > 0) {   // the TX samples at both ends of the extended symbol (k_chan_fix)
+    double2* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
+    for (int i = lane_f; i < 2 * D; i += 64) {
+      const int j = i < D ? i : S - 2 * D + i;
+      xh[i] = xs[(j - cp) & (N - 1)];
+    }
+  }
+  // 3. every RX's taps (transmit_simo, core/ofdm_core.py:361-412)
+  constexpr int PM = NP ? NP : TXCH_MAXP;
+  const int np = NP ? NP : ch.n_paths;
+  const int tail = N - cp + D;   // samples n >= tail repeat as the CP samples past max_delay
+  for (int r = 0; r < ch.num_rx; ++r) {
+    const size_t br = (size_t)b * ch.num_rx + r;
+    double2 cf[PM];
+    int dl[PM];
+#pragma unroll
+    for (int p = 0; p < PM; ++p) {
+      cf[p] = p < np ? ch.coef[br * np + p] : make_double2(0.0, 0.0);
+      dl[p] = ch.delays[p];
+    }
+    double2* yo = ch.y + br * g.L + (size_t)l * S + cp;
+    double pwr = 0.0;
+    // partly rolled: fully unrolled, the 16 x NP shifted reads were all hoisted (spills)
+#pragma unroll TXSW_UNROLL
+    for (int q = 0; q < 16; ++q) {
+      const int n = 64 * q + lane_f;
+      double2 y = make_double2(0.0, 0.0);
+#pragma unroll
+      for (int p = 0; p < PM; ++p)
+        if (p < np) y = cadd(y, cmul(cf[p], xs[(n - dl[p]) & (N - 1)]));
+      yo[n] = y;
+      const double e = y.x * y.x + y.y * y.y;
+      pwr += e;
+      if (n >= tail) pwr += e;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pwr += __shfl_xor(pwr, o);
+    if (lane_f == 0) ch.pow_part[br * g.n_sym + l] = pwr;
+  }
+}
+
+bool tx_simo_w_supported(const Grid& g, int f64, int coded, int sc_fdm, const TxChannelT<double>& ch) {
+  return f64 && !coded && !sc_fdm && g.N == 1024 && g.kinfo && g.pilots64 && !ch.tcoef && !ch.x_out &&
+         ch.n_paths >= 1 && ch.n_paths <= TXCH_MAXP && ch.max_delay >= 0 && ch.max_delay <= g.cp && g.cp < 1024 &&
+         ch.num_rx >= 1 && (g.bps == 2 || g.bps == 4 || g.bps == 6);
+}
+
 // Which wave-private kernels run by default (same-box A/B, profiles/r6_wave_ab.md):
 // the config-5 RX (k_rx_fft_mimo_w) beats its block kernel; the config-2 RX and
 // TX do not (2 waves per SIMD at most with a symbol in registers, against 3 for
@@ -651,6 +755,35 @@ int mimo_rx_wave_enabled() { return env_or("LTE_MIMO_RX_WAVE", LTE_MIMO_RX_WAVE)
 #define LTE_SIMO_RX_WAVE 1
 #endif
 int simo_rx_wave_enabled() { return env_or("LTE_SIMO_RX_WAVE", LTE_SIMO_RX_WAVE); }
+#ifndef LTE_SIMO_TX_WAVE
+#define LTE_SIMO_TX_WAVE 1
+#endif
+int simo_tx_wave_enabled() { return env_or("LTE_SIMO_TX_WAVE", LTE_SIMO_TX_WAVE); }
+
+template <int BPS, int NP>
+static void tx_simo_w_go(hipStream_t s, unsigned blocks, const Grid& g, const uint32_t* pw, int PW, int B,
+                         double2* cap_syms, const TxChannelT<double>& ch) {
+  hipLaunchKernelGGL((k_ofdm_tx_simo_w<BPS, NP>), dim3(blocks), dim3(64 * TXSW_WAVES),
+                     (size_t)TXSW_WAVES * 1024 * sizeof(double2), s, g, pw, PW, B, cap_syms, ch);
+}
+template <int BPS>
+static void tx_simo_w_np(hipStream_t s, unsigned blocks, const Grid& g, const uint32_t* pw, int PW, int B,
+                         double2* cap_syms, const TxChannelT<double>& ch) {
+  if (ch.n_paths == 6) tx_simo_w_go<BPS, 6>(s, blocks, g, pw, PW, B, cap_syms, ch);
+  else if (ch.n_paths == 4) tx_simo_w_go<BPS, 4>(s, blocks, g, pw, PW, B, cap_syms, ch);
+  else tx_simo_w_go<BPS, 0>(s, blocks, g, pw, PW, B, cap_syms, ch);
+}
+int launch_ofdm_tx_simo_w(hipStream_t s, const Grid& g, const uint32_t* pw, int PW, int B, double2* cap_syms,
+                          const TxChannelT<double>& ch) {
+  if (!tx_simo_w_supported(g, 1, 0, 0, ch)) return (int)hipErrorInvalidValue;
+  const int64_t waves = (int64_t)B * g.n_sym;
+  if (waves > 0x7FFFFFFF - TXSW_WAVES) return (int)hipErrorInvalidValue;
+  const unsigned blocks = (unsigned)((waves + TXSW_WAVES - 1) / TXSW_WAVES);
+  if (g.bps == 2) tx_simo_w_np<2>(s, blocks, g, pw, PW, B, cap_syms, ch);
+  else if (g.bps == 4) tx_simo_w_np<4>(s, blocks, g, pw, PW, B, cap_syms, ch);
+  else tx_simo_w_np<6>(s, blocks, g, pw, PW, B, cap_syms, ch);
+  return (int)hipGetLastError();
+}
 
 int launch_rx_frame_simo_w(hipStream_t s, const Grid& g, int B, int num_rx, const double2* y, int64_t y_rx_stride,
                            int64_t y_frame_stride, const double* npow, const uint64_t* fid, uint64_t seed,

@@ -518,6 +518,7 @@ def test_simo_symbol_handoff_matches_rx_streams(C, monkeypatch, prec, inject):
         kw = dict(noise=np.random.default_rng(5).standard_normal((B, 4, 2, plan.L)))
     runs = {}
     monkeypatch.setenv('LTE_SIMO_RX_WAVE', '0')   # both sides on k_rx_frame_simo2 (the wave receiver: its own test)
+    monkeypatch.setenv('LTE_SIMO_TX_WAVE', '0')   # and on k_ofdm_tx (the wave TX: its own test)
     for xh in ('0', '1'):
         monkeypatch.setenv('LTE_SIMO_XHAND', xh)
         runs[xh] = (plan.run(snr, seed=0x5EED, frame_id0=11, capture=('data_syms', 'bits_rx', 'noise_power'), **kw),
@@ -596,6 +597,39 @@ def test_simo_receiver_rx_pairs_match_sequential(C, monkeypatch, nrx, mod, prec)
         assert np.max(np.abs(b['data_syms'] - a['data_syms'])) <= 1e-5 * np.max(np.abs(a['data_syms']))
         assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 2
     assert 0 < int(b['counts'][:, 0].sum())
+
+
+@pytest.mark.parametrize('nrx,mod,prof', [(4, '16-QAM', 'Vehicular_A'), (2, '64-QAM', 'Pedestrian_A'),
+                                          (3, 'QPSK', 'Vehicular_A')])
+def test_wave_simo_tx_matches_block_tx(C, monkeypatch, nrx, mod, prof):
+    """10 MHz SIMO TX + static taps, float64: the wave-private TX
+    (k_ofdm_tx_simo_w: one wave per (frame, symbol), wfft::fft1024<INV>, the
+    symbol staged in LDS for every RX's taps; the default) against k_ofdm_tx
+    (LTE_SIMO_TX_WAVE=0) on the same frames: identical transmitted symbols;
+    noise powers and combined symbols to 1e-12 (the transform and the power
+    sums differ in round-off only); decisions and counts match (at most 2 flips
+    allowed).  4, 2 and 3 RX; 6 and 2 paths."""
+    import lte_phy
+    sim = lte_phy.OFDMSimulator(lte_phy.LTEConfig(bandwidth=10.0, modulation=mod), channel_type='rayleigh_mp',
+                                itu_profile=prof, precision='f64')
+    B = 64 + 3
+    bps = sim.config.bits_per_symbol
+    plan = sim._plan(C.CHAIN_SIMO, 14, 14 * sim.Nd * bps - 5, num_rx=nrx, max_frames=B)
+    snr = np.tile(np.arange(0.0, 31.0, 2.0), B)[:B]
+    cap = ('tx_syms', 'noise_power', 'data_syms', 'bits_rx')
+    runs = {}
+    for wave in ('0', '1'):
+        monkeypatch.setenv('LTE_SIMO_TX_WAVE', wave)
+        runs[wave] = (plan.run(snr, seed=0x5EED, frame_id0=91, capture=cap),
+                      plan.run(snr, seed=0x5EED, frame_id0=91))
+    (a, a0), (b, b0) = runs['0'], runs['1']
+    assert np.array_equal(a['tx_syms'], b['tx_syms'])
+    assert np.max(np.abs(b['noise_power'] - a['noise_power']) / np.abs(a['noise_power'])) <= 1e-12
+    assert np.max(np.abs(b['data_syms'] - a['data_syms'])) <= 1e-12 * np.max(np.abs(a['data_syms']))
+    assert int(np.sum(a['bits_rx'] != b['bits_rx'])) <= 2
+    assert abs(int(a0['counts'][:, 0].sum()) - int(b0['counts'][:, 0].sum())) <= 2
+    assert np.array_equal(a0['counts'][:, 1], b0['counts'][:, 1])
+    assert 0 < int(b0['counts'][:, 0].sum())
 
 
 @pytest.mark.parametrize('nrx,mod,inject', [(4, '16-QAM', False), (4, '16-QAM', True), (2, '64-QAM', False),

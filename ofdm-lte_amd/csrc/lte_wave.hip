@@ -635,19 +635,31 @@ bool rx_simo_w_supported(const Grid& g, int num_rx, int f64, bool H, bool pstats
 // symbol), no block barrier.  Lane c, register q builds bin k = 64 q + c from
 // Grid::kinfo (a data RE's BPS payload bits -> qam_point, a pilot, or 0);
 // wfft::fft1024<INV> and the output scale give x[64 q + c], which is staged in
-// the wave's LDS (16 KB, the transform's scratch before) so that every RX's
-// taps read their cyclic shifts: received sample n = sum_p c_rp x[(n - d_p)
-// mod N] (every delay <= CP), the same terms in the same order as tx_channel.
+// the wave's LDS (the transform's scratch before) so that every RX's taps read
+// their cyclic shifts: received sample n = sum_p c_rp x[(n - d_p) mod N]
+// (every delay <= CP), the same terms in the same order as tx_channel.
 // Each RX's N samples after the CP go out as 1 KB wave stores; its power
 // partial is the sum of |y|^2 over those samples plus the CP samples past
 // max_delay (cyclically the last cp - max_delay samples again), by one wave
 // reduction (tx_channel sums the same values in another order).
-constexpr int TXSW_WAVES = 2;   // (LDS: 16 KB per wave, five blocks per CU)
+// TXSW_HALF (max_delay <= 64, cp <= 512, <= 4 RX): the taps read x through a
+// 9-register window (9 KB) half a symbol at a time instead of the whole symbol
+// staged (16 KB), for four waves per SIMD (120 VGPRs) instead of two and a
+// half (profiles/r6_simo_tx_wave/: 14.1 against 15.5 ms per 65 536 frames).
+#ifndef TXSW_HALF
+#define TXSW_HALF 1
+#endif
+constexpr int TXSW_WAVES = 2;
+constexpr int TXSW_XS = TXSW_HALF ? 9 * 64 : 1024;   // double2 per wave
+static_assert(TXSW_XS * 2 >= wfft::LDS_DOUBLES_1024, "the window doubles as the transpose buffer");
 #ifndef TXSW_UNROLL
-#define TXSW_UNROLL 4
+#define TXSW_UNROLL (TXSW_HALF ? 1 : 4)
+#endif
+#ifndef TXSW_WPE
+#define TXSW_WPE (TXSW_HALF ? 4 : 2)
 #endif
 template <int BPS, int NP>
-__global__ __launch_bounds__(64 * TXSW_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+__global__ __launch_bounds__(64 * TXSW_WAVES) __attribute__((amdgpu_waves_per_eu(TXSW_WPE, TXSW_WPE)))
 void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, double2* __restrict__ cap_syms,
                       TxChannelT<double> ch) {
   constexpr int N = 1024;
@@ -657,7 +669,7 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
   const int gs = blockIdx.x * TXSW_WAVES + w;
   const int b = gs / g.n_sym, l = gs - b * g.n_sym;
   if (b >= B) return;   // uniform per wave; no block barrier below
-  double2* xs = dyn_lds<double2>() + (size_t)w * N;
+  double2* xs = dyn_lds<double2>() + (size_t)w * TXSW_XS;
   int lane = lane0;
   asm volatile("" : "+v"(lane));
   // 1. the bins (QAMModulator.bits_to_symbols, ResourceMapper.map_symbols)
@@ -682,10 +694,72 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
   asm volatile("" : "+v"(lane_f));
   wfft::fft1024<true>(v, reinterpret_cast<double*>(xs), G::tw(g), lane_f);
   const double sc = tx_scale<double>(N);
+  const int cp = g.cp, S = N + cp, D = ch.max_delay;
+  constexpr int PM = NP ? NP : TXCH_MAXP;
+  const int np = NP ? NP : ch.n_paths;
+  const int tail = N - cp + D;   // samples n >= tail repeat as the CP samples past max_delay
+#if TXSW_HALF
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = cscale(v[q], sc);
+  if (D > 0) {   // the TX samples at both ends of the extended symbol (k_chan_fix), from the registers
+    double2* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
+#pragma unroll
+    for (int q = 8; q < 16; ++q) {   // (cp <= 512)
+      const int n = 64 * q + lane_f;
+      if (n >= N - cp && n < N - cp + D) xh[n - (N - cp)] = v[q];
+      if (n >= N - D) xh[n - N + 2 * D] = v[q];
+    }
+  }
+  // 3. every RX's taps (transmit_simo, core/ofdm_core.py:361-412), half a
+  //    symbol at a time: window slot s holds register (8 h - 1 + s) mod 16, so
+  //    output n = 512 h + 64 q + lane reads x[n - d] at slot q + 1 - d / 64
+  double pwr[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int sl = 0; sl < 9; ++sl) xs[64 * sl + lane_f] = v[(8 * h - 1 + sl) & 15];
+    wfft::wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (r >= ch.num_rx) break;
+      const size_t br = (size_t)b * ch.num_rx + r;
+      double2 cf[PM];
+      int dl[PM];
+#pragma unroll
+      for (int p = 0; p < PM; ++p) {
+        cf[p] = p < np ? ch.coef[br * np + p] : make_double2(0.0, 0.0);
+        dl[p] = ch.delays[p];
+      }
+      double2* yo = ch.y + br * g.L + (size_t)l * S + cp;
+      double pr = 0.0;
+#pragma unroll TXSW_UNROLL
+      for (int q = 0; q < 8; ++q) {
+        const int n = 512 * h + 64 * q + lane_f;
+        double2 y = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int p = 0; p < PM; ++p)
+          if (p < np) y = cadd(y, cmul(cf[p], xs[64 * q + lane_f + 64 - dl[p]]));
+        yo[n] = y;
+        const double e = y.x * y.x + y.y * y.y;
+        pr += e;
+        if (n >= tail) pr += e;
+      }
+      pwr[r] += pr;
+    }
+    wfft::wave_lds_fence();   // the window is restaged
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (r >= ch.num_rx) break;
+    double t = pwr[r];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (lane_f == 0) ch.pow_part[((size_t)b * ch.num_rx + r) * g.n_sym + l] = t;
+  }
+#else
 #pragma unroll
   for (int q = 0; q < 16; ++q) xs[64 * q + lane_f] = cscale(v[q], sc);
   wfft::wave_lds_fence();
-  const int cp = g.cp, S = N + cp, D = ch.max_delay;
   if (D > 0) {   // the TX samples at both ends of the extended symbol (k_chan_fix)
     double2* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
     for (int i = lane_f; i < 2 * D; i += 64) {
@@ -694,9 +768,6 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
     }
   }
   // 3. every RX's taps (transmit_simo, core/ofdm_core.py:361-412)
-  constexpr int PM = NP ? NP : TXCH_MAXP;
-  const int np = NP ? NP : ch.n_paths;
-  const int tail = N - cp + D;   // samples n >= tail repeat as the CP samples past max_delay
   for (int r = 0; r < ch.num_rx; ++r) {
     const size_t br = (size_t)b * ch.num_rx + r;
     double2 cf[PM];
@@ -725,12 +796,14 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
     for (int o = 32; o > 0; o >>= 1) pwr += __shfl_xor(pwr, o);
     if (lane_f == 0) ch.pow_part[br * g.n_sym + l] = pwr;
   }
+#endif
 }
 
 bool tx_simo_w_supported(const Grid& g, int f64, int coded, int sc_fdm, const TxChannelT<double>& ch) {
   return f64 && !coded && !sc_fdm && g.N == 1024 && g.kinfo && g.pilots64 && !ch.tcoef && !ch.x_out &&
          ch.n_paths >= 1 && ch.n_paths <= TXCH_MAXP && ch.max_delay >= 0 && ch.max_delay <= g.cp && g.cp < 1024 &&
-         ch.num_rx >= 1 && (g.bps == 2 || g.bps == 4 || g.bps == 6);
+         ch.num_rx >= 1 && (g.bps == 2 || g.bps == 4 || g.bps == 6) &&
+         (!TXSW_HALF || (ch.max_delay <= 64 && g.cp <= 512 && ch.num_rx <= 4));
 }
 
 // Which wave-private kernels run by default (same-box A/B, profiles/r6_wave_ab.md):
@@ -764,7 +837,7 @@ template <int BPS, int NP>
 static void tx_simo_w_go(hipStream_t s, unsigned blocks, const Grid& g, const uint32_t* pw, int PW, int B,
                          double2* cap_syms, const TxChannelT<double>& ch) {
   hipLaunchKernelGGL((k_ofdm_tx_simo_w<BPS, NP>), dim3(blocks), dim3(64 * TXSW_WAVES),
-                     (size_t)TXSW_WAVES * 1024 * sizeof(double2), s, g, pw, PW, B, cap_syms, ch);
+                     (size_t)TXSW_WAVES * TXSW_XS * sizeof(double2), s, g, pw, PW, B, cap_syms, ch);
 }
 template <int BPS>
 static void tx_simo_w_np(hipStream_t s, unsigned blocks, const Grid& g, const uint32_t* pw, int PW, int B,

@@ -501,7 +501,7 @@ def stage_bytes_per_frame(config, plan, prec):
 
 # the committed rocprofv3 --pmc summary of each config's bench step (the
 # traffic beside each stage's algorithmic bytes; tests/test_roofline_pmc.py)
-PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r6_pmc_c3_wave2.json', 4: 'r6_pmc_c4_merged.json',
+PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r6_pmc_c3_wave3.json', 4: 'r6_pmc_c4_merged.json',
              5: 'r6_pmc_c5.json'}
 
 

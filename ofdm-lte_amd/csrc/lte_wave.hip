@@ -102,6 +102,9 @@ __device__ __forceinline__ cx<R> interp_seg(const cx<R>* hp, int np, int sidx, R
 // a time, a rolled loop draws into the wave's LDS scratch zs (M / 2 KB) and
 // each register then adds its draw (unrolled over the registers, the 16 Philox
 // + 32 Box-Muller chains of N = 2048 took the kernel past 512 registers).
+#ifndef WSN_UNROLL   // the draw loop's unroll (1: rolled)
+#define WSN_UNROLL 1
+#endif
 template <int M, class TB>
 __device__ __forceinline__ void wave_symbol_noisy(double2 (&v)[M], const double2* __restrict__ yf, int off, int lane,
                                                   double sigma, uint64_t seed, uint64_t fr, int rx,
@@ -121,7 +124,7 @@ __device__ __forceinline__ void wave_symbol_noisy(double2 (&v)[M], const double2
         zs[64 * mm + lane] = make_double2(zf[n], zf[L + n]);
       }
     } else {
-#pragma unroll 1
+#pragma unroll WSN_UNROLL
       for (int mm = 0; mm < MH; mm += 2) {
         // even lanes: the pair counter of register m; odd lanes: of register m + 1
         const int m = MH * h + mm;

@@ -557,6 +557,19 @@ def hbm_roofline(config, plan, prec, tim, F, steps):
     dom = max(st, key=lambda k: st[k]['ms_per_step'])
     d = st[dom]
     tb = d['pmc_bytes_per_frame']
+    # the dominant kernel's SQ counters from the same PMC summary: with HBM well
+    # under its peak, these say where the rest of the time goes
+    sq = None
+    pmc = load_profile(PMC_FILES[config]) if prec == 'f64' else None
+    if pmc:
+        hits = [v for k, v in pmc['kernels'].items() if k == d['kernels'][0] or k.startswith(d['kernels'][0] + '<')]
+        if hits:
+            h = max(hits, key=lambda v: v.get('ms', 0))
+            sq = {'valu_wave_instr_per_frame': h.get('valu_wave_instr_per_frame'),
+                  'wave_cycles': h.get('wave_cycles'), 'share_of_active_issue': h.get('share_of_active_issue'),
+                  'what': 'SQ counters of the dominant kernel (fractions of wave cycles: active issue, waiting); '
+                          'HBM far under 8 TB/s with VALU most of the issue and waits the rest means latency-bound '
+                          'f64 VALU work (the Box-Muller noise), DESIGN.md section 5'}
     return {'bound': 'hbm', 'kernel': ' + '.join(d['kernels']), 'stage': dom, 'achieved': d['alg_GBs'],
             'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': d['frac'],
             'traffic': round(tb * F) if tb else None,
@@ -568,6 +581,7 @@ def hbm_roofline(config, plan, prec, tim, F, steps):
                     'traffic = the same kernels\' HBM bytes per frame in the committed PMC summary ('
                     + PMC_FILES[config] + ') x frames per launch; hbm_frac = that traffic\'s rate / 8 TB/s',
             'pmc_source': 'profiles/' + PMC_FILES[config],
+            'sq_counters': sq,
             'other_stages': {k: v for k, v in st.items() if k != dom}}
 
 

@@ -454,9 +454,13 @@ def stage_bytes_per_frame(config, plan, prec):
         if plan.channel == 1:   # static taps: coefficients, then the first-samples power fix-up + noise power
             D, P = plan.max_delay, plan.n_paths
             out['fading'] = (['k_fading'], nr * P * c, 'one tap coefficient per (RX, path) out')
-            out['channel'] = (['k_chan_fix', 'k_npow'], n_sym * 2 * D * c + nr * P * c + 3 * nr * n_sym * esz,
-                              "each symbol's head / previous tail (2 x max delay) and the taps in, the power "
-                              'partials updated, the noise power out')
+            if config == 3 and simo_tw:   # the wave TX forms the head samples' power itself (k_chan_fix skipped)
+                out['channel'] = (['k_npow'], nr * n_sym * esz + nr * esz,
+                                  'the power partials in, the noise power out')
+            else:
+                out['channel'] = (['k_chan_fix', 'k_npow'], n_sym * 2 * D * c + nr * P * c + 3 * nr * n_sym * esz,
+                                  "each symbol's head / previous tail (2 x max delay) and the taps in, the power "
+                                  'partials updated, the noise power out')
         if config == 2:   # equalised symbols + sigma^2_eff per (group, data SC) to k_dematch_zn
             out['rx_data'] = ([crx], nr * sym + n_sym * plan.Nd * c + plan.n_grp * plan.Nd * esz,
                               'the RX stream (no CP) in; equalised symbols + sigma^2_eff per data SC out')
@@ -501,7 +505,7 @@ def stage_bytes_per_frame(config, plan, prec):
 
 # the committed rocprofv3 --pmc summary of each config's bench step (the
 # traffic beside each stage's algorithmic bytes; tests/test_roofline_pmc.py)
-PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r6_pmc_c3_wave3.json', 4: 'r6_pmc_c4_merged.json',
+PMC_FILES = {2: 'r5_pmc_c2_final.json', 3: 'r6_pmc_c3_wave4.json', 4: 'r6_pmc_c4_merged.json',
              5: 'r6_pmc_c5.json'}
 
 

@@ -2053,7 +2053,11 @@ static int run_txch(lte_plan* p, hipStream_t s, const lte_run_args* a, int B, bo
   }
   {
     Timer t(p, KN_CHANNEL, s);
-    LCHK(launch_chan_fix<R>(s, p->grid, B, ch));
+    bool fix_fused = false;   // config 3's wave TX formed the head samples' power itself
+    if constexpr (std::is_same_v<R, double>)
+      fix_fused = !(coded && tx_per_frame(p)) && tx_simo_w_fuses_fix(p->grid, coded ? 1 : 0,
+                                                                     (d.sc_fdm && !coded) ? 1 : 0, ch);
+    if (!fix_fused) LCHK(launch_chan_fix<R>(s, p->grid, B, ch));
     LCHK(launch_npow<R>(s, B, rx, ch.pow_part, p->n_sym, p->L, c.snr_lin.p, c.npow.p));
   }
   return LTE_OK;

@@ -397,6 +397,7 @@ bool rx_simo_w_supported(const Grid& g, int num_rx, int f64, bool H, bool pstats
 int simo_rx_wave_enabled();
 bool tx_simo_w_supported(const Grid& g, int f64, int coded, int sc_fdm, const TxChannelT<double>& ch);
 int simo_tx_wave_enabled();
+bool tx_simo_w_fuses_fix(const Grid& g, int coded, int sc_fdm, const TxChannelT<double>& ch);
 int launch_ofdm_tx_simo_w(hipStream_t s, const Grid& g, const uint32_t* pw, int PW, int B, double2* cap_syms,
                           const TxChannelT<double>& ch);
 int launch_rx_frame_simo_w(hipStream_t s, const Grid& g, int B, int num_rx, const double2* y, int64_t y_rx_stride,

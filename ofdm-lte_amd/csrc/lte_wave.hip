@@ -649,14 +649,27 @@ bool rx_simo_w_supported(const Grid& g, int num_rx, int f64, bool H, bool pstats
 // 9-register window (9 KB) half a symbol at a time instead of the whole symbol
 // staged (16 KB), for four waves per SIMD (120 VGPRs) instead of two and a
 // half (profiles/r6_simo_tx_wave/: 14.1 against 15.5 ms per 65 536 frames).
+// TXSW_FRAME (with TXSW_HALF): one wave per frame walking its symbols, which
+// keeps the previous symbol's last register and so also forms each symbol's
+// first max_delay channel-output samples' power (their taps reach into the
+// previous symbol: k_chan_fix's work, which then does not run) from a tenth
+// window slot.
 #ifndef TXSW_HALF
 #define TXSW_HALF 1
 #endif
+#ifndef TXSW_FRAME
+#define TXSW_FRAME 1
+#endif
+static_assert(!TXSW_FRAME || TXSW_HALF, "the per-frame form uses the window");
 constexpr int TXSW_WAVES = 2;
-constexpr int TXSW_XS = TXSW_HALF ? 9 * 64 : 1024;   // double2 per wave
+constexpr int TXSW_XS = TXSW_HALF ? (9 + TXSW_FRAME) * 64 : 1024;   // double2 per wave
 static_assert(TXSW_XS * 2 >= wfft::LDS_DOUBLES_1024, "the window doubles as the transpose buffer");
 #ifndef TXSW_UNROLL
-#define TXSW_UNROLL (TXSW_HALF ? 1 : 4)
+#if TXSW_HALF
+#define TXSW_UNROLL 1
+#else
+#define TXSW_UNROLL 4
+#endif
 #endif
 #ifndef TXSW_WPE
 #define TXSW_WPE (TXSW_HALF ? 4 : 2)
@@ -670,8 +683,15 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
   const int lane0 = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int gs = blockIdx.x * TXSW_WAVES + w;
+#if TXSW_FRAME
+  const int b = gs;
+  if (b >= B) return;   // uniform per wave; no block barrier below
+  double2 tailp = make_double2(0.0, 0.0);   // the previous symbol's x[960 + lane]
+  for (int l = 0; l < g.n_sym; ++l) {
+#else
   const int b = gs / g.n_sym, l = gs - b * g.n_sym;
   if (b >= B) return;   // uniform per wave; no block barrier below
+#endif
   double2* xs = dyn_lds<double2>() + (size_t)w * TXSW_XS;
   int lane = lane0;
   asm volatile("" : "+v"(lane));
@@ -704,7 +724,7 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
 #if TXSW_HALF
 #pragma unroll
   for (int q = 0; q < 16; ++q) v[q] = cscale(v[q], sc);
-  if (D > 0) {   // the TX samples at both ends of the extended symbol (k_chan_fix), from the registers
+  if (!TXSW_FRAME && D > 0) {   // the TX samples at both ends of the extended symbol (k_chan_fix), from the registers
     double2* xh = ch.xh + ((size_t)b * g.n_sym + l) * 2 * D;
 #pragma unroll
     for (int q = 8; q < 16; ++q) {   // (cp <= 512)
@@ -721,6 +741,9 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int sl = 0; sl < 9; ++sl) xs[64 * sl + lane_f] = v[(8 * h - 1 + sl) & 15];
+#if TXSW_FRAME
+    if (h == 1) xs[64 * 9 + lane_f] = tailp;
+#endif
     wfft::wave_lds_fence();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -747,6 +770,23 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
         pr += e;
         if (n >= tail) pr += e;
       }
+#if TXSW_FRAME
+      if (h == 1 && lane_f < D) {
+        // extended-symbol sample m = lane < max_delay: x_ext[m - d] is this
+        // symbol's x[N - cp + m - d] (slot index 576 - cp + m - d) or, before
+        // it, the previous symbol's x[N + m - d] (slot 9; zero for symbol 0)
+        const int m = lane_f;
+        double2 y = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int p = 0; p < PM; ++p)
+          if (p < np) {
+            const int k = m - dl[p];
+            const double2 xv = k >= 0 ? xs[576 - cp + k] : (l > 0 ? xs[64 * 10 + k] : make_double2(0.0, 0.0));
+            y = cadd(y, cmul(cf[p], xv));
+          }
+        pr += y.x * y.x + y.y * y.y;
+      }
+#endif
       pwr[r] += pr;
     }
     wfft::wave_lds_fence();   // the window is restaged
@@ -759,6 +799,10 @@ void k_ofdm_tx_simo_w(Grid g, const uint32_t* __restrict__ pw, int PW, int B, do
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
     if (lane_f == 0) ch.pow_part[((size_t)b * ch.num_rx + r) * g.n_sym + l] = t;
   }
+#if TXSW_FRAME
+  tailp = v[15];
+  }   // symbols
+#endif
 #else
 #pragma unroll
   for (int q = 0; q < 16; ++q) xs[64 * q + lane_f] = cscale(v[q], sc);
@@ -808,6 +852,10 @@ bool tx_simo_w_supported(const Grid& g, int f64, int coded, int sc_fdm, const Tx
          ch.num_rx >= 1 && (g.bps == 2 || g.bps == 4 || g.bps == 6) &&
          (!TXSW_HALF || (ch.max_delay <= 64 && g.cp <= 512 && ch.num_rx <= 4));
 }
+// the wave TX also forms the head samples' power (TXSW_FRAME): k_chan_fix must not run
+bool tx_simo_w_fuses_fix(const Grid& g, int coded, int sc_fdm, const TxChannelT<double>& ch) {
+  return TXSW_FRAME && simo_tx_wave_enabled() && tx_simo_w_supported(g, 1, coded, sc_fdm, ch);
+}
 
 // Which wave-private kernels run by default (same-box A/B, profiles/r6_wave_ab.md):
 // the config-5 RX (k_rx_fft_mimo_w) beats its block kernel; the config-2 RX and
@@ -852,7 +900,7 @@ static void tx_simo_w_np(hipStream_t s, unsigned blocks, const Grid& g, const ui
 int launch_ofdm_tx_simo_w(hipStream_t s, const Grid& g, const uint32_t* pw, int PW, int B, double2* cap_syms,
                           const TxChannelT<double>& ch) {
   if (!tx_simo_w_supported(g, 1, 0, 0, ch)) return (int)hipErrorInvalidValue;
-  const int64_t waves = (int64_t)B * g.n_sym;
+  const int64_t waves = TXSW_FRAME ? (int64_t)B : (int64_t)B * g.n_sym;
   if (waves > 0x7FFFFFFF - TXSW_WAVES) return (int)hipErrorInvalidValue;
   const unsigned blocks = (unsigned)((waves + TXSW_WAVES - 1) / TXSW_WAVES);
   if (g.bps == 2) tx_simo_w_np<2>(s, blocks, g, pw, PW, B, cap_syms, ch);

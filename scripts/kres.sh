@@ -5,7 +5,7 @@ set -e
 O=$1; PAT=$2
 B=/opt/rocm/lib/llvm/bin
 T=$(mktemp -d)
-$B/llvm-objcopy --dump-section=.hip_fatbin="$T/fat.bin" "$O"
+$B/llvm-objcopy --dump-section=.hip_fatbin="$T/fat.bin" "$O" "$T/copy.o"   # (without an output file objcopy rewrites $O)
 $B/clang-offload-bundler --unbundle --type=o --input="$T/fat.bin" --targets=hipv4-amdgcn-amd-amdhsa--gfx950 \
   --output="$T/k.co"
 $B/llvm-readelf --notes "$T/k.co" | python3 -c '
